@@ -1,0 +1,183 @@
+"""In-tree native build for alphago_amd.
+
+Two shared objects are produced next to the package sources (so they travel to
+the GPU box with the repository snapshot):
+
+* ``alphago_amd/_engine*.so`` — C++17 rules engine, featurizer and batched MCTS
+  (pybind11, built with g++).
+* ``alphago_amd/_hip_kernels.so`` — hand-written CDNA4 HIP kernels for gfx950
+  (compiled directly with hipcc; no hipify, no torch JIT cache), registered as
+  ``torch.ops.alphago_amd.*`` through TORCH_LIBRARY and loaded with
+  ``torch.ops.load_library``.
+
+Usage: ``python -m alphago_amd._build [engine|hip|all] [--force]``.
+"""
+from __future__ import annotations
+
+import glob
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(os.path.dirname(PKG), "build", "native")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def engine_path() -> str:
+    return os.path.join(PKG, "_engine" + _ext_suffix())
+
+
+def hip_path() -> str:
+    return os.path.join(PKG, "_hip_kernels.so")
+
+
+def _digest(paths, extra: str = "") -> str:
+    h = hashlib.sha1(extra.encode())
+    for p in sorted(paths):
+        with open(p, "rb") as f:
+            h.update(p.encode())
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _up_to_date(target: str, digest: str) -> bool:
+    stamp = target + ".sha1"
+    if not (os.path.exists(target) and os.path.exists(stamp)):
+        return False
+    with open(stamp) as f:
+        return f.read().strip() == digest
+
+
+def _write_stamp(target: str, digest: str) -> None:
+    with open(target + ".sha1", "w") as f:
+        f.write(digest)
+
+
+def _run(cmd, verbose=False):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("command failed (%d):\n%s\n%s" % (r.returncode, " ".join(cmd), r.stdout))
+    return r.stdout
+
+
+def build_engine(force: bool = False, verbose: bool = False) -> str:
+    import pybind11
+
+    srcs = sorted(glob.glob(os.path.join(CSRC, "engine", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "engine", "*.h")))
+    out = engine_path()
+    flags = ["-O3", "-std=c++17", "-fPIC", "-mpopcnt", "-fvisibility=hidden", "-Wall", "-Wno-sign-compare"]
+    digest = _digest(srcs + hdrs, " ".join(flags))
+    if not force and _up_to_date(out, digest):
+        return out
+    os.makedirs(BUILD, exist_ok=True)
+    incs = ["-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-I" + os.path.join(CSRC, "engine")]
+
+    def compile_one(src):
+        obj = os.path.join(BUILD, "engine_" + os.path.basename(src) + ".o")
+        _run(["g++", *flags, *incs, "-c", src, "-o", obj], verbose)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = out + ".tmp"
+    _run(["g++", "-shared", "-o", tmp, *objs, "-lpthread"], verbose)
+    os.replace(tmp, out)
+    _write_stamp(out, digest)
+    return out
+
+
+def _torch_paths():
+    import torch
+    from torch.utils import cpp_extension
+
+    incs = cpp_extension.include_paths(device_type="cuda")
+    libdir = os.path.join(os.path.dirname(torch.__file__), "lib")
+    abi = "1" if torch._C._GLIBCXX_USE_CXX11_ABI else "0"
+    return incs, libdir, abi
+
+
+def build_hip(force: bool = False, verbose: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) + glob.glob(os.path.join(CSRC, "kernels", "*.cpp")))
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    out = hip_path()
+    incs, libdir, abi = _torch_paths()
+    common = [
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        "-D_GLIBCXX_USE_CXX11_ABI=" + abi,
+        "-DUSE_ROCM=1",
+        "-D__HIP_PLATFORM_AMD__=1",
+        "-DTORCH_EXTENSION_NAME=_hip_kernels",
+        "-Wno-unused-result",
+        "-Wno-deprecated-declarations",
+    ]
+    hip_flags = ["--offload-arch=" + ARCH, "-fgpu-rdc" if False else "-fno-gpu-rdc", "-munsafe-fp-atomics"]
+    digest = _digest(srcs + hdrs, " ".join(common + hip_flags))
+    if not force and _up_to_date(out, digest):
+        return out
+    os.makedirs(BUILD, exist_ok=True)
+    inc_flags = ["-I" + p for p in incs] + ["-I" + os.path.join(CSRC, "kernels"), "-I" + sysconfig.get_paths()["include"]]
+    hipcc = os.path.join(ROCM, "bin", "hipcc")
+
+    def compile_one(src):
+        obj = os.path.join(BUILD, "hip_" + os.path.basename(src) + ".o")
+        if src.endswith(".hip"):
+            cmd = [hipcc, "-x", "hip", *common, *hip_flags, *inc_flags, "-c", src, "-o", obj]
+        else:
+            cmd = [hipcc, *common, *inc_flags, "-c", src, "-o", obj]
+        _run(cmd, verbose)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(srcs)))) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = out + ".tmp"
+    _run(
+        [
+            hipcc,
+            "-shared",
+            "--offload-arch=" + ARCH,
+            "-o",
+            tmp,
+            *objs,
+            "-L" + libdir,
+            "-Wl,-rpath," + libdir,
+            "-lc10",
+            "-lc10_hip",
+            "-ltorch",
+            "-ltorch_cpu",
+            "-ltorch_hip",
+            "-lamdhip64",
+        ],
+        verbose,
+    )
+    os.replace(tmp, out)
+    _write_stamp(out, digest)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False):
+    return build_engine(force, verbose), build_hip(force, verbose)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else "all"
+    force = "--force" in sys.argv
+    verbose = "-v" in sys.argv
+    if what in ("engine", "all"):
+        print("engine:", build_engine(force, verbose))
+    if what in ("hip", "all"):
+        print("hip:", build_hip(force, verbose))

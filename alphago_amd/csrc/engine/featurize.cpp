@@ -1,0 +1,229 @@
+#include "featurize.h"
+
+#include <cstring>
+
+namespace ag {
+
+static const char* kNames[F_NUM] = {"board", "ones", "turns_since", "liberties", "capture_size",
+                                     "self_atari_size", "liberties_after", "ladder_capture",
+                                     "ladder_escape", "sensibleness", "zeros", "color", "legal"};
+static const int kPlanes[F_NUM] = {3, 1, 8, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1};
+
+int feature_planes(int fid) { return (fid >= 0 && fid < F_NUM) ? kPlanes[fid] : 0; }
+const char* feature_name(int fid) { return (fid >= 0 && fid < F_NUM) ? kNames[fid] : ""; }
+int feature_id(const std::string& name) {
+  for (int i = 0; i < F_NUM; ++i)
+    if (name == kNames[i]) return i;
+  return -1;
+}
+
+// ---------------------------------------------------------------- ladders
+static constexpr int kLadderDepth = 96;  // plies; a corner-to-corner ladder is < 80
+
+static bool hunter_wins(const GameState& s, int prey, int depth);
+
+// prey to move, prey group in atari.  True if every prey reply loses.
+static bool prey_loses(const GameState& s, int prey, int depth) {
+  if (depth > kLadderDepth) return false;
+  const int pc = s.board[prey];
+  int16_t cand[8];
+  int nc = 0;
+  int h = s.head[prey];
+  cand[nc++] = (int16_t)s.libs[h].first();
+  // captures of adjacent hunter groups in atari
+  int st = prey;
+  do {
+    for (int i = 0; i < s.g->nnbr[st]; ++i) {
+      int q = s.g->nbr[st][i];
+      if (s.board[q] == -pc && s.libc[s.head[q]] == 1) {
+        int l = s.libs[s.head[q]].first();
+        bool dup = false;
+        for (int j = 0; j < nc; ++j) dup |= (cand[j] == l);
+        if (!dup && nc < 8) cand[nc++] = (int16_t)l;
+      }
+    }
+    st = s.next[st];
+  } while (st != prey);
+  for (int k = 0; k < nc; ++k) {
+    int mv = cand[k];
+    if (mv < 0 || !s.is_legal_for(mv, pc)) continue;
+    GameState s2 = s;
+    s2.try_move(mv, pc);
+    if (s2.board[prey] != pc) continue;
+    int lc = s2.libc[s2.head[prey]];
+    if (lc >= 3) return false;
+    if (lc == 2 && !hunter_wins(s2, prey, depth + 1)) return false;
+  }
+  return true;
+}
+
+// hunter to move against the prey group.
+static bool hunter_wins(const GameState& s, int prey, int depth) {
+  if (depth > kLadderDepth) return false;
+  const int pc = s.board[prey];
+  int h = s.head[prey];
+  int lc = s.libc[h];
+  if (lc == 1) return true;
+  if (lc >= 3) return false;
+  Bits b = s.libs[h];
+  for (int k = 0; k < 2; ++k) {
+    int l = b.first();
+    if (l < 0) break;
+    b.clear(l);
+    if (!s.is_legal_for(l, -pc)) continue;
+    GameState s2 = s;
+    s2.try_move(l, -pc);
+    if (s2.board[prey] != pc) return true;  // captured outright
+    if (s2.libc[s2.head[prey]] == 1 && prey_loses(s2, prey, depth + 1)) return true;
+  }
+  return false;
+}
+
+bool ladder_capture_at(const GameState& s, int m) {
+  if (!s.is_legal(m)) return false;
+  const int me = s.current_player;
+  for (int i = 0; i < s.g->nnbr[m]; ++i) {
+    int q = s.g->nbr[m][i];
+    if (s.board[q] != -me || s.libc[s.head[q]] != 2) continue;
+    GameState s2 = s;
+    s2.try_move(m, me);
+    if (s2.board[q] != -me) return true;  // captured
+    if (s2.libc[s2.head[q]] == 1 && prey_loses(s2, q, 0)) return true;
+  }
+  return false;
+}
+
+bool ladder_escape_at(const GameState& s, int m) {
+  if (!s.is_legal(m)) return false;
+  const int me = s.current_player;
+  for (int i = 0; i < s.g->nnbr[m]; ++i) {
+    int q = s.g->nbr[m][i];
+    if (s.board[q] != me || s.libc[s.head[q]] != 1) continue;
+    GameState s2 = s;
+    s2.try_move(m, me);
+    if (s2.board[q] != me) continue;
+    int lc = s2.libc[s2.head[q]];
+    if (lc >= 3) return true;
+    if (lc == 2 && !hunter_wins(s2, q, 0)) return true;
+  }
+  return false;
+}
+
+// ---------------------------------------------------------------- planes
+int featurize(const GameState& s, const int* fids, int nf, uint8_t* out) {
+  const int np = s.np;
+  const int me = s.current_player;
+  // legal mask computed once and shared (get_legal_moves, go.py:261-267)
+  uint8_t legal[MAXP];
+  bool need_legal = false;
+  for (int i = 0; i < nf; ++i) {
+    int f = fids[i];
+    need_legal |= (f == F_CAPTURE_SIZE || f == F_SELF_ATARI_SIZE || f == F_LIBERTIES_AFTER ||
+                   f == F_SENSIBLENESS || f == F_LADDER_CAPTURE || f == F_LADDER_ESCAPE || f == F_LEGAL);
+  }
+  if (need_legal)
+    for (int p = 0; p < np; ++p) legal[p] = s.is_legal(p) ? 1 : 0;
+
+  int off = 0;
+  for (int i = 0; i < nf; ++i) {
+    const int f = fids[i];
+    const int npl = feature_planes(f);
+    uint8_t* o = out + (size_t)off * np;
+    std::memset(o, 0, (size_t)npl * np);
+    switch (f) {
+      case F_BOARD:  // preprocessing.py:9-17
+        for (int p = 0; p < np; ++p) {
+          int b = s.board[p];
+          if (b == me) o[p] = 1;
+          else if (b == -me) o[np + p] = 1;
+          else o[2 * np + p] = 1;
+        }
+        break;
+      case F_ONES:
+        std::memset(o, 1, np);
+        break;
+      case F_ZEROS:
+        break;
+      case F_COLOR:  // value.py:16's 49th plane ("player colour"), SURVEY Q18
+        if (me == BLACK) std::memset(o, 1, np);
+        break;
+      case F_TURNS_SINCE: {  // preprocessing.py:20-43
+        int depth = 0;
+        uint8_t marked[MAXP];
+        std::memset(marked, 0, sizeof(marked));
+        for (int k = (int)s.history.size() - 1; k >= 0; --k) {
+          int mv = s.history[k];
+          if (mv != PASS && s.board[mv] != EMPTY && !marked[mv]) {
+            o[depth * np + mv] = 1;
+            marked[mv] = 1;
+          }
+          if (depth < 7) ++depth;
+        }
+        break;
+      }
+      case F_LIBERTIES:  // preprocessing.py:46-61
+        for (int p = 0; p < np; ++p) {
+          int lc = s.liberty_count(p);
+          if (lc >= 1) o[(lc >= 8 ? 7 : lc - 1) * np + p] = 1;
+        }
+        break;
+      case F_CAPTURE_SIZE:  // preprocessing.py:64-88
+        for (int p = 0; p < np; ++p) {
+          if (!legal[p]) continue;
+          int16_t roots[4];
+          int k = s.groups_around(p, roots);
+          int ncap = 0;
+          for (int j = 0; j < k; ++j)
+            if (s.libc[roots[j]] == 1 && s.board[roots[j]] != me) ncap += s.gsize[roots[j]];
+          o[(ncap > 7 ? 7 : ncap) * np + p] = 1;
+        }
+        break;
+      case F_SELF_ATARI_SIZE:  // preprocessing.py:91-115
+      case F_LIBERTIES_AFTER:  // preprocessing.py:118-144
+        for (int p = 0; p < np; ++p) {
+          if (!legal[p]) continue;
+          Bits lib = s.liberty_set(p);
+          int gsz = 1;
+          int16_t roots[4];
+          int k = s.groups_around(p, roots);
+          for (int j = 0; j < k; ++j)
+            if (s.board[roots[j]] == me) {
+              lib.orr(s.libs[roots[j]]);
+              gsz += s.gsize[roots[j]];
+            }
+          lib.clear(p);
+          int nl = lib.count();
+          if (f == F_SELF_ATARI_SIZE) {
+            if (nl == 1) o[(gsz - 1 > 7 ? 7 : gsz - 1) * np + p] = 1;
+          } else {
+            int plane = nl - 1;
+            if (plane > 7) plane = 7;
+            if (plane < 0) plane = 7;  // python index -1
+            o[plane * np + p] = 1;
+          }
+        }
+        break;
+      case F_LADDER_CAPTURE:
+        for (int p = 0; p < np; ++p)
+          if (legal[p] && ladder_capture_at(s, p)) o[p] = 1;
+        break;
+      case F_LADDER_ESCAPE:
+        for (int p = 0; p < np; ++p)
+          if (legal[p] && ladder_escape_at(s, p)) o[p] = 1;
+        break;
+      case F_SENSIBLENESS:  // preprocessing.py:155-161
+        for (int p = 0; p < np; ++p)
+          if (legal[p] && !s.is_eye(p, me)) o[p] = 1;
+        break;
+      case F_LEGAL:
+        for (int p = 0; p < np; ++p) o[p] = legal[p];
+        break;
+      default:
+        break;
+    }
+    off += npl;
+  }
+  return off;
+}
+
+}  // namespace ag

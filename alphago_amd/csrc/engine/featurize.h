@@ -1,0 +1,44 @@
+// Board featurizer (CPU/native path).  Plane semantics are those of the
+// reference preprocessing (AlphaGo/preprocessing/preprocessing.py:9-214),
+// including its quirks (liberties_after: 0 liberties -> plane 7).
+// Output is uint8 one-hot planes laid out [plane][x][y] (x = SGF column,
+// flattened move index x*size+y as util.py:6-8).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "go.h"
+
+namespace ag {
+
+enum FeatureId : int {
+  F_BOARD = 0,
+  F_ONES,
+  F_TURNS_SINCE,
+  F_LIBERTIES,
+  F_CAPTURE_SIZE,
+  F_SELF_ATARI_SIZE,
+  F_LIBERTIES_AFTER,
+  F_LADDER_CAPTURE,
+  F_LADDER_ESCAPE,
+  F_SENSIBLENESS,
+  F_ZEROS,
+  F_COLOR,
+  F_LEGAL,
+  F_NUM
+};
+
+int feature_planes(int fid);
+int feature_id(const std::string& name);  // -1 if unknown
+const char* feature_name(int fid);
+
+// Write planes for one state; returns the number of planes written.
+int featurize(const GameState& s, const int* fids, int nf, uint8_t* out);
+
+// Ladder reading (paper features; NotImplementedError in the reference
+// preprocessing.py:147-152).  Exposed for tests.
+bool ladder_capture_at(const GameState& s, int move);
+bool ladder_escape_at(const GameState& s, int move);
+
+}  // namespace ag

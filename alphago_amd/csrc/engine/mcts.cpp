@@ -1,0 +1,449 @@
+#include "mcts.h"
+
+#include <pybind11/numpy.h>
+#include <pybind11/stl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <thread>
+
+#include "featurize.h"
+
+namespace py = pybind11;
+
+namespace ag {
+
+static Node make_node(int parent, int move, float P) {
+  Node n;
+  n.parent = parent;
+  n.first_child = -1;
+  n.nchild = 0;
+  n.move = (int16_t)move;
+  n.P = P;
+  n.N = 0;
+  n.W = 0.f;
+  n.vl = 0;
+  n.status = 0;
+  return n;
+}
+
+Forest::Forest(int n_trees, double c_puct, double lmbda, int rollout_limit, int playout_depth, int virtual_loss,
+               uint64_t seed, std::vector<int> feature_ids)
+    : trees_(n_trees),
+      c_puct_(c_puct),
+      lmbda_(lmbda),
+      rollout_limit_(rollout_limit),
+      playout_depth_(playout_depth),
+      vloss_(virtual_loss),
+      rng_(seed),
+      fids_(std::move(feature_ids)) {
+  for (int f : fids_) nplanes_ += ag::feature_planes(f);
+  for (auto& t : trees_) {
+    t.nodes.clear();
+    t.nodes.push_back(make_node(-1, PASS, 1.f));
+  }
+}
+
+void Forest::set_root(int t, const GameState& s) {
+  if (!pending_.empty()) throw std::runtime_error("set_root with pending evaluations");
+  auto& tr = trees_.at(t);
+  tr.root_state = s;
+  tr.nodes.clear();
+  tr.nodes.push_back(make_node(-1, PASS, 1.f));
+  tr.sims = 0;
+}
+
+int Forest::select_child(const SearchTree& tr, int u) const {
+  const Node& nu = tr.nodes[u];
+  double nparent = (double)nu.N + (double)vloss_ * nu.vl;
+  double sq = std::sqrt(std::max(nparent, 1.0));
+  int best = -1;
+  double bestv = -1e300;
+  for (int i = 0; i < nu.nchild; ++i) {
+    const Node& c = tr.nodes[nu.first_child + i];
+    double n = (double)c.N + (double)vloss_ * c.vl;
+    double q = n > 0 ? ((double)c.W - (double)vloss_ * c.vl) / n : 0.0;
+    double v = q + c_puct_ * c.P * sq / (1.0 + n);
+    if (v > bestv) {
+      bestv = v;
+      best = nu.first_child + i;
+    }
+  }
+  return best;
+}
+
+void Forest::backup(SearchTree& tr, int leaf, double v_leaf_to_move, bool remove_vl) {
+  double val = -v_leaf_to_move;
+  int x = leaf;
+  while (x >= 0) {
+    Node& nd = tr.nodes[x];
+    nd.N += 1;
+    nd.W += (float)val;
+    if (remove_vl) nd.vl -= 1;
+    val = -val;
+    x = nd.parent;
+  }
+  tr.sims += 1;
+}
+
+int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
+  if (!pending_.empty()) throw std::runtime_error("gather called with pending evaluations; call apply first");
+  leaf_states_.clear();
+  std::vector<int> all;
+  if (!which) {
+    all.resize(trees_.size());
+    for (size_t i = 0; i < trees_.size(); ++i) all[i] = (int)i;
+    which = &all;
+  }
+  for (int t : *which) {
+    SearchTree& tr = trees_.at(t);
+    for (int k = 0; k < leaves_per_tree; ++k) {
+      GameState st = tr.root_state;
+      int u = 0;
+      tr.nodes[0].vl += 1;
+      int depth = 0;
+      bool stop_tree = false;
+      while (true) {
+        Node& nd = tr.nodes[u];
+        if (nd.status == 3) {
+          int w = st.get_winner();
+          backup(tr, u, (double)(w * st.current_player), true);
+          break;
+        }
+        if (nd.status == 1) {  // collision with a leaf already queued in this batch
+          for (int x = u; x >= 0; x = tr.nodes[x].parent) tr.nodes[x].vl -= 1;
+          stop_tree = true;
+          break;
+        }
+        if (nd.status == 0 || depth >= playout_depth_) {
+          if (st.is_end_of_game) {
+            nd.status = 3;
+            int w = st.get_winner();
+            backup(tr, u, (double)(w * st.current_player), true);
+            break;
+          }
+          if (nd.status == 0) {
+            nd.status = 1;
+            pending_.push_back({t, u});
+            leaf_states_.push_back(st);
+            break;
+          }
+        }
+        int c = select_child(tr, u);
+        if (c < 0) {  // expanded with no children cannot happen (pass is always a child)
+          for (int x = u; x >= 0; x = tr.nodes[x].parent) tr.nodes[x].vl -= 1;
+          stop_tree = true;
+          break;
+        }
+        tr.nodes[c].vl += 1;
+        st.try_move(tr.nodes[c].move, 0);
+        u = c;
+        ++depth;
+      }
+      if (stop_tree) break;
+    }
+  }
+  total_evals_ += (int64_t)pending_.size();
+  return (int)pending_.size();
+}
+
+void Forest::leaf_features(uint8_t* out, int threads) const {
+  int L = (int)pending_.size();
+  if (L == 0) return;
+  size_t stride = (size_t)nplanes_ * leaf_states_[0].np;
+  int T = std::max(1, std::min(threads, L));
+  std::vector<std::thread> pool;
+  for (int t = 0; t < T; ++t)
+    pool.emplace_back([&, t]() {
+      for (int i = t; i < L; i += T) featurize(leaf_states_[i], fids_.data(), (int)fids_.size(), out + i * stride);
+    });
+  for (auto& th : pool) th.join();
+}
+
+void Forest::leaf_masks(uint8_t* out) const {
+  for (size_t i = 0; i < pending_.size(); ++i) {
+    const GameState& s = leaf_states_[i];
+    for (int p = 0; p < s.np; ++p) out[i * s.np + p] = s.is_legal(p) && !s.is_eye(p, s.current_player);
+  }
+}
+
+double Forest::rollout(GameState& s) {
+  const int p0 = s.current_player;
+  std::vector<int> cand;
+  for (int it = 0; it < rollout_limit_ && !s.is_end_of_game; ++it) {
+    int mv = PASS;
+    for (int tries = 0; tries < 24; ++tries) {
+      int p = (int)(rng_() % (uint64_t)s.np);
+      if (s.board[p] == EMPTY && s.is_legal(p) && !s.is_eye(p, s.current_player)) {
+        mv = p;
+        break;
+      }
+    }
+    if (mv == PASS) {
+      cand.clear();
+      for (int p = 0; p < s.np; ++p)
+        if (s.is_legal(p) && !s.is_eye(p, s.current_player)) cand.push_back(p);
+      if (!cand.empty()) mv = cand[rng_() % cand.size()];
+    }
+    s.try_move(mv, 0);
+  }
+  return (double)(s.get_winner() * p0);
+}
+
+void Forest::apply(const float* priors, const float* values) {
+  const int L = (int)pending_.size();
+  for (int i = 0; i < L; ++i) {
+    SearchTree& tr = trees_[pending_[i].tree];
+    const int u = pending_[i].node;
+    const GameState& st = leaf_states_[i];
+    const float* pr = priors + (size_t)i * st.np;
+    std::vector<int> moves;
+    std::vector<float> ps;
+    double sum = 0;
+    for (int p = 0; p < st.np; ++p)
+      if (st.is_legal(p) && !st.is_eye(p, st.current_player)) {
+        moves.push_back(p);
+        float v = std::max(pr[p], 0.f);
+        ps.push_back(v);
+        sum += v;
+      }
+    if (moves.empty()) {
+      moves.push_back(PASS);
+      ps.push_back(1.f);
+      sum = 1.0;
+    } else if (sum <= 0) {
+      for (auto& v : ps) v = 1.f;
+      sum = (double)ps.size();
+    }
+    int first = (int)tr.nodes.size();
+    for (size_t j = 0; j < moves.size(); ++j) tr.nodes.push_back(make_node(u, moves[j], (float)(ps[j] / sum)));
+    Node& nd = tr.nodes[u];
+    nd.first_child = first;
+    nd.nchild = (int16_t)moves.size();
+    nd.status = 2;
+    double v = values ? (double)values[i] : 0.0;
+    if (lmbda_ > 0) {
+      GameState s2 = st;
+      double z = rollout(s2);
+      v = (1.0 - lmbda_) * v + lmbda_ * z;
+    }
+    backup(tr, u, v, true);
+  }
+  pending_.clear();
+}
+
+void Forest::add_root_noise(int t, double alpha, double eps) {
+  SearchTree& tr = trees_.at(t);
+  Node& r = tr.nodes[0];
+  if (r.status != 2 || r.nchild == 0) return;
+  std::gamma_distribution<double> gam(alpha, 1.0);
+  std::vector<double> d(r.nchild);
+  double s = 0;
+  for (auto& x : d) {
+    x = gam(rng_);
+    s += x;
+  }
+  for (int i = 0; i < r.nchild; ++i) {
+    Node& c = tr.nodes[r.first_child + i];
+    c.P = (float)((1 - eps) * c.P + eps * (s > 0 ? d[i] / s : 1.0 / r.nchild));
+  }
+}
+
+void Forest::root_stats(int t, std::vector<int>& moves, std::vector<int>& visits, std::vector<float>& q) const {
+  const SearchTree& tr = trees_.at(t);
+  const Node& r = tr.nodes[0];
+  moves.clear();
+  visits.clear();
+  q.clear();
+  for (int i = 0; i < r.nchild; ++i) {
+    const Node& c = tr.nodes[r.first_child + i];
+    moves.push_back(c.move);
+    visits.push_back(c.N);
+    q.push_back(c.N > 0 ? c.W / c.N : 0.f);
+  }
+}
+
+int Forest::best_move(int t, double temperature) {
+  const SearchTree& tr = trees_.at(t);
+  const Node& r = tr.nodes[0];
+  if (r.nchild == 0) return PASS;
+  if (temperature <= 0) {
+    int best = r.first_child;
+    for (int i = 1; i < r.nchild; ++i)
+      if (tr.nodes[r.first_child + i].N > tr.nodes[best].N) best = r.first_child + i;
+    return tr.nodes[best].move;
+  }
+  std::vector<double> w(r.nchild);
+  double s = 0;
+  for (int i = 0; i < r.nchild; ++i) {
+    w[i] = std::pow((double)tr.nodes[r.first_child + i].N, 1.0 / temperature);
+    s += w[i];
+  }
+  if (s <= 0) return tr.nodes[r.first_child].move;
+  double x = std::uniform_real_distribution<double>(0, s)(rng_);
+  for (int i = 0; i < r.nchild; ++i) {
+    x -= w[i];
+    if (x <= 0) return tr.nodes[r.first_child + i].move;
+  }
+  return tr.nodes[r.first_child + r.nchild - 1].move;
+}
+
+void Forest::advance(int t, int move) {
+  if (!pending_.empty()) throw std::runtime_error("advance with pending evaluations");
+  SearchTree& tr = trees_.at(t);
+  int found = -1;
+  const Node& r = tr.nodes[0];
+  for (int i = 0; i < r.nchild; ++i)
+    if (tr.nodes[r.first_child + i].move == move) found = r.first_child + i;
+  tr.root_state.do_move(move, 0);
+  if (found < 0 || tr.nodes[found].status == 1) {
+    tr.nodes.clear();
+    tr.nodes.push_back(make_node(-1, PASS, 1.f));
+    return;
+  }
+  // BFS copy of the reused subtree (children stay contiguous)
+  std::vector<Node> nn;
+  nn.reserve(tr.nodes.size());
+  Node root = tr.nodes[found];
+  root.parent = -1;
+  nn.push_back(root);
+  std::vector<int> old_of;  // old index of each new node
+  old_of.push_back(found);
+  for (size_t k = 0; k < nn.size(); ++k) {
+    int o = old_of[k];
+    const Node& on = tr.nodes[o];
+    if (on.nchild > 0 && on.first_child >= 0) {
+      int first = (int)nn.size();
+      for (int i = 0; i < on.nchild; ++i) {
+        Node c = tr.nodes[on.first_child + i];
+        c.parent = (int)k;
+        nn.push_back(c);
+        old_of.push_back(on.first_child + i);
+      }
+      nn[k].first_child = first;
+    }
+  }
+  tr.nodes.swap(nn);
+}
+
+// ------------------------------------------------------------------ bindings
+static int tup_to_idx(const GameState& s, const py::object& a) {
+  if (a.is_none()) return PASS;
+  auto t = a.cast<std::pair<int, int>>();
+  return s.idx(t.first, t.second);
+}
+static py::object idx_to_tup(const GameState& s, int p) {
+  if (p == PASS) return py::none();
+  return py::make_tuple(p / s.n, p % s.n);
+}
+
+void bind_mcts(py::module_& m) {
+  py::class_<Forest>(m, "Forest")
+      .def(py::init([](int n_trees, double c_puct, double lmbda, int rollout_limit, int playout_depth, int vl,
+                       uint64_t seed, std::vector<std::string> features) {
+             std::vector<int> ids;
+             for (auto& f : features) {
+               int id = feature_id(f);
+               if (id < 0) throw py::value_error("unknown feature: " + f);
+               ids.push_back(id);
+             }
+             return new Forest(n_trees, c_puct, lmbda, rollout_limit, playout_depth, vl, seed, ids);
+           }),
+           py::arg("n_trees"), py::arg("c_puct") = 5.0, py::arg("lmbda") = 0.0, py::arg("rollout_limit") = 500,
+           py::arg("playout_depth") = 1000, py::arg("virtual_loss") = 3, py::arg("seed") = 0,
+           py::arg("features") = std::vector<std::string>{})
+      .def_property_readonly("n_trees", &Forest::n_trees)
+      .def_property_readonly("feature_planes", &Forest::feature_planes)
+      .def_property_readonly("n_pending", &Forest::n_pending)
+      .def_property_readonly("total_evals", &Forest::total_evals)
+      .def("set_root", &Forest::set_root)
+      .def("root_state", [](const Forest& f, int t) { return GameState(f.root_state(t)); })
+      .def(
+          "gather",
+          [](Forest& f, int lpt, py::object which) {
+            if (which.is_none()) {
+              py::gil_scoped_release r;
+              return f.gather(lpt, nullptr);
+            }
+            std::vector<int> w = which.cast<std::vector<int>>();
+            py::gil_scoped_release r;
+            return f.gather(lpt, &w);
+          },
+          py::arg("leaves_per_tree") = 1, py::arg("which") = py::none())
+      .def("leaf_state", [](const Forest& f, int i) { return GameState(f.leaf_state(i)); })
+      .def(
+          "leaf_features",
+          [](const Forest& f, int threads) {
+            int L = f.n_pending();
+            int n = L ? f.leaf_state(0).n : 0;
+            py::array_t<uint8_t> a({(ssize_t)L, (ssize_t)f.feature_planes(), (ssize_t)n, (ssize_t)n});
+            uint8_t* d = a.mutable_data();
+            {
+              py::gil_scoped_release r;
+              f.leaf_features(d, threads);
+            }
+            return a;
+          },
+          py::arg("threads") = 8)
+      .def(
+          "leaf_features_into",
+          [](const Forest& f, uintptr_t ptr, size_t capacity, int threads) {
+            int L = f.n_pending();
+            if (L == 0) return 0;
+            size_t need = (size_t)L * f.feature_planes() * f.leaf_state(0).np;
+            if (need > capacity) throw py::value_error("leaf_features_into: buffer too small");
+            py::gil_scoped_release r;
+            f.leaf_features(reinterpret_cast<uint8_t*>(ptr), threads);
+            return L;
+          },
+          py::arg("ptr"), py::arg("capacity"), py::arg("threads") = 8)
+      .def("leaf_masks",
+           [](const Forest& f) {
+             int L = f.n_pending();
+             int np = L ? f.leaf_state(0).np : 0;
+             py::array_t<uint8_t> a({(ssize_t)L, (ssize_t)np});
+             f.leaf_masks(a.mutable_data());
+             return a;
+           })
+      .def(
+          "apply",
+          [](Forest& f, py::array_t<float, py::array::c_style | py::array::forcecast> priors,
+             py::object values) {
+            int L = f.n_pending();
+            if (L == 0) return;
+            int np = f.leaf_state(0).np;
+            if (priors.ndim() != 2 || priors.shape(0) != L || priors.shape(1) != np)
+              throw py::value_error("priors must be (n_pending, size*size)");
+            const float* pv = priors.data();
+            if (values.is_none()) {
+              py::gil_scoped_release r;
+              f.apply(pv, nullptr);
+              return;
+            }
+            auto va = values.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+            if (va.size() != L) throw py::value_error("values must have n_pending entries");
+            const float* vv = va.data();
+            py::gil_scoped_release r;
+            f.apply(pv, vv);
+          },
+          py::arg("priors"), py::arg("values") = py::none())
+      .def("add_root_noise", &Forest::add_root_noise, py::arg("tree"), py::arg("alpha") = 0.03,
+           py::arg("eps") = 0.25)
+      .def("root_stats",
+           [](const Forest& f, int t) {
+             std::vector<int> mv, vis;
+             std::vector<float> q;
+             f.root_stats(t, mv, vis, q);
+             py::list moves;
+             for (int p : mv) moves.append(idx_to_tup(f.root_state(t), p));
+             return py::make_tuple(moves, vis, q);
+           })
+      .def(
+          "best_move",
+          [](Forest& f, int t, double temp) { return idx_to_tup(f.root_state(t), f.best_move(t, temp)); },
+          py::arg("tree"), py::arg("temperature") = 0.0)
+      .def("advance", [](Forest& f, int t, py::object mv) { f.advance(t, tup_to_idx(f.root_state(t), mv)); })
+      .def("sims", &Forest::sims);
+}
+
+}  // namespace ag

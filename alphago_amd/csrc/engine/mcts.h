@@ -1,0 +1,94 @@
+// Batched PUCT Monte-Carlo tree search over many independent trees.
+//
+// Replaces the serial, batch-1 MCTS of the reference (AlphaGo/mcts.py:67-171,
+// ParallelMCTS stub :174-175).  Each call to gather() descends every tree with
+// virtual loss until it has collected up to `leaves_per_tree` unexpanded leaves;
+// the caller evaluates all leaves of all trees in ONE batched network call on the
+// GPU and returns priors+values through apply(), which expands and backs up.
+//
+// Fixes over the reference: the root's visit count is
+// maintained and u = c·P·sqrt(ΣN)/(1+N) is evaluated at selection time (Q3);
+// values are backed up negamax-style from the side-to-move perspective (Q4);
+// rollouts are optional (λ = 0 is first class) and sample uniformly among
+// sensible moves instead of printing a warning at the limit (Q5).
+#pragma once
+#include <pybind11/pybind11.h>
+
+#include <cstdint>
+#include <random>
+#include <vector>
+
+#include "go.h"
+
+namespace ag {
+
+struct Node {
+  int32_t parent;
+  int32_t first_child;
+  int16_t nchild;
+  int16_t move;  // point index, PASS = -1
+  float P;
+  int32_t N;
+  float W;      // sum of values from the perspective of the player who moved into this node
+  int32_t vl;   // pending virtual-loss count
+  int8_t status;  // 0 unexpanded, 1 pending evaluation, 2 expanded, 3 terminal
+};
+
+struct Leaf {
+  int tree;
+  int node;
+};
+
+struct SearchTree {
+  std::vector<Node> nodes;
+  GameState root_state;
+  int64_t sims = 0;
+  SearchTree() : root_state(19) {}
+};
+
+class Forest {
+ public:
+  Forest(int n_trees, double c_puct, double lmbda, int rollout_limit, int playout_depth, int virtual_loss,
+         uint64_t seed, std::vector<int> feature_ids);
+
+  int n_trees() const { return (int)trees_.size(); }
+  void set_root(int t, const GameState& s);
+  const GameState& root_state(int t) const { return trees_[t].root_state; }
+  // Descend all (or the listed) trees; returns number of leaves queued for evaluation.
+  int gather(int leaves_per_tree, const std::vector<int>* which = nullptr);
+  int n_pending() const { return (int)pending_.size(); }
+  const GameState& leaf_state(int i) const { return leaf_states_[i]; }
+  int feature_planes() const { return nplanes_; }
+  // uint8 features (L, F, n, n) and sensible-move masks (L, n*n); threaded.
+  void leaf_features(uint8_t* out, int threads) const;
+  void leaf_masks(uint8_t* out) const;
+  // priors (L, n*n) float32 (any non-negative scores; renormalised over sensible moves), values (L,)
+  void apply(const float* priors, const float* values);
+  void add_root_noise(int t, double alpha, double eps);
+  // Root statistics
+  void root_stats(int t, std::vector<int>& moves, std::vector<int>& visits, std::vector<float>& q) const;
+  int best_move(int t, double temperature);
+  void advance(int t, int move);
+  int64_t sims(int t) const { return trees_[t].sims; }
+  int64_t total_evals() const { return total_evals_; }
+
+ private:
+  int select_child(const SearchTree& tr, int u) const;
+  double rollout(GameState& s);
+  void backup(SearchTree& tr, int leaf, double v_leaf_to_move, bool remove_vl);
+
+  std::vector<SearchTree> trees_;
+  std::vector<Leaf> pending_;
+  std::vector<GameState> leaf_states_;
+  std::vector<std::vector<int>> leaf_paths_;
+  double c_puct_, lmbda_;
+  int rollout_limit_, playout_depth_, vloss_;
+  std::mt19937_64 rng_;
+  std::vector<int> fids_;
+  int nplanes_ = 0;
+  int64_t total_evals_ = 0;
+};
+
+void bind_mcts(pybind11::module_& m);
+
+}  // namespace ag
