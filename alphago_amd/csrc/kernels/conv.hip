@@ -1,0 +1,384 @@
+// Implicit-GEMM convolution for 19x19 boards on CDNA4 MFMA (gfx950).
+//
+// Activation layout: zero-bordered ("padded") NHWC bf16.  Element (b, i, j, c)
+// of a tensor with padded side HP lives at ((b*HP + i)*HP + j)*C + c, the
+// board interior is i, j in [P, P+S).  Borders are zero and never written, so
+// every tap of a 'same' convolution is a plain load — no boundary branches.
+//
+// conv_fwd_kernel   D[n][m] = sum_{t,c} W_t[n][c] * X[m + shift_t][c]
+//   M = boards*S*S output pixels, N = Cout, K = taps*Cin.  Workgroup tile
+//   128(m) x BN(n), K-step = one tap x 64 channels.  Both operands are staged
+//   global->LDS with global_load_lds_dwordx4 (the A rows are a per-lane gather:
+//   row address of pixel m + tap offset); the 16-B chunks of each 128-B LDS row
+//   are XOR-swizzled on the *source* address so the 16x16x32 bf16 MFMA fragment
+//   reads (ds_read_b128) are bank-conflict free.  Double-buffered LDS.
+//   The MFMA is issued "swapped" (A = weights, B = pixels) so each lane owns 4
+//   consecutive output channels of one pixel: the epilogue (bias + ReLU, or the
+//   ReLU-derivative mask for dgrad) stores 8 bytes per lane.
+//   The same kernel computes dgrad with flipped/transposed packed weights.
+//
+// conv_wgrad_kernel dW_t[n][c] = sum_m dZ[m][n] * X[m + shift_t][c]
+//   K = pixels (split over workgroups), tile 192(n) x 192(c) per workgroup for
+//   one tap.  Tiles are staged as [16-channel block][32 pixels][16 ch] and the
+//   pixel-contiguous MFMA operands are read with the gfx950 hardware transpose
+//   read ds_read_b64_tr_b16.  The k (pixel) order inside a K-step is permuted
+//   identically for both operands so that each 32-lane half reads 8 distinct
+//   contiguous rows (conflict free).  Partial sums go to a per-split fp32 slab
+//   that conv_wgrad_reduce_kernel sums deterministically into the OIHW fp32
+//   gradient (and the bias gradient, accumulated by the tap-0 workgroups).
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace agk {
+
+// ----------------------------------------------------------------- forward
+template <int BN, int MODE>
+__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvFwdArgs a) {
+  constexpr int BM = 128;
+  constexpr int NB = BN / 32;  // 16-wide n blocks per wave (a wave covers BN/2 channels)
+  constexpr int MB = 4;        // 16-wide m blocks per wave (a wave covers 64 pixels)
+  constexpr int A_BYTES = BM * 128;
+  constexpr int B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int B_INSTR = BN / 32;  // glds instructions per wave for the weight tile
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int SS = a.S * a.S;
+  const int CC = a.Cin >> 6;  // 64-channel chunks
+  const int nK = a.K * a.K * CC;
+
+  // --- staging addresses (element offsets)
+  int arow[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wave * 32 + i * 8 + (lane >> 3);
+    int m = m0 + r;
+    m = m < a.M ? m : a.M - 1;
+    const int b = m / SS;
+    const int rem = m - b * SS;
+    const int ii = rem / a.S;
+    const int jj = rem - ii * a.S;
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    arow[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + logical * 8;
+  }
+  int brow[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int r = wave * (BN / 4) + i * 8 + (lane >> 3);
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    brow[i] = (n0 + r) * a.Cin + logical * 8;
+  }
+  const size_t wtap = (size_t)a.Cout * a.Cin;
+
+  auto stage = [&](int ks, int buf) {
+    const int t = ks / CC;
+    const int c0 = (ks - t * CC) << 6;
+    const int kh = t / a.K;
+    const int kw = t - kh * a.K;
+    const int toff = (kh * a.HPi + kw) * a.Cin + c0;
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(a.x + arow[i] + toff, base + (wave * 32 + i * 8) * 128);
+    const __bf16* wt = a.w + (size_t)t * wtap + c0;
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i) glds16(wt + brow[i], base + A_BYTES + (wave * (BN / 4) + i * 8) * 128);
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets: row*128 + (chunk ^ swz)*16, swz = ((row>>1)&7) = (lane&15)>>1
+  const int swz = (lane & 15) >> 1;
+  const int xrow0 = (wm * 64 + (lane & 15)) * 128;
+  const int wrow0 = A_BYTES + (wn * (BN / 2) + (lane & 15)) * 128;
+
+  stage(0, 0);
+  wait_vmcnt0();
+  __syncthreads();
+  for (int ks = 0; ks < nK; ++ks) {
+    const int cur = ks & 1;
+    if (ks + 1 < nK) stage(ks + 1, cur ^ 1);
+    const char* base = smem + cur * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int choff = (((kk << 2) + (lane >> 4)) ^ swz) << 4;
+      bf16x8 xf[MB], wf[NB];
+#pragma unroll
+      for (int j = 0; j < MB; ++j) xf[j] = *(const bf16x8*)(base + xrow0 + j * 16 * 128 + choff);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wf[i] = *(const bf16x8*)(base + wrow0 + i * 16 * 128 + choff);
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  // --- epilogue: lane owns channels n..n+3 of pixel m for every (i, j) block
+  const int nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    const int m = m0 + wm * 64 + j * 16 + (lane & 15);
+    if (m >= a.M) continue;
+    const int b = m / SS;
+    const int rem = m - b * SS;
+    const int ii = rem / a.S;
+    const int jj = rem - ii * a.S;
+    const size_t ooff = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int n = nbase + i * 16;
+      f32x4 v = acc[i][j];
+      if constexpr (MODE == MODE_BIAS_RELU) {
+        const f32x4 bb = *(const f32x4*)(a.bias + n);
+        v[0] = fmaxf(v[0] + bb[0], 0.f);
+        v[1] = fmaxf(v[1] + bb[1], 0.f);
+        v[2] = fmaxf(v[2] + bb[2], 0.f);
+        v[3] = fmaxf(v[3] + bb[3], 0.f);
+      } else if constexpr (MODE == MODE_MASK) {
+        const bf16x4 mk = *(const bf16x4*)(a.mask + ooff + n);
+        v[0] = (float)mk[0] > 0.f ? v[0] : 0.f;
+        v[1] = (float)mk[1] > 0.f ? v[1] : 0.f;
+        v[2] = (float)mk[2] > 0.f ? v[2] : 0.f;
+        v[3] = (float)mk[3] > 0.f ? v[3] : 0.f;
+      }
+      bf16x4 o;
+      o[0] = (__bf16)v[0];
+      o[1] = (__bf16)v[1];
+      o[2] = (__bf16)v[2];
+      o[3] = (__bf16)v[3];
+      *(bf16x4*)(a.y + ooff + n) = o;
+    }
+  }
+}
+
+template <int BN, int MODE>
+static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int smem = 2 * (128 * 128 + BN * 128);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  dim3 grid((a.M + 127) / 128, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE>), grid, dim3(256), smem, st, a);
+}
+
+template <int MODE>
+static void launch_fwd_mode(const ConvFwdArgs& a, hipStream_t st) {
+  if (a.Cout % 192 == 0) launch_fwd_t<192, MODE>(a, st);
+  else if (a.Cout % 128 == 0) launch_fwd_t<128, MODE>(a, st);
+  else launch_fwd_t<64, MODE>(a, st);
+}
+
+void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st) {
+  if (mode == MODE_BIAS_RELU) launch_fwd_mode<MODE_BIAS_RELU>(a, st);
+  else if (mode == MODE_MASK) launch_fwd_mode<MODE_MASK>(a, st);
+  else launch_fwd_mode<MODE_NONE>(a, st);
+}
+
+// ----------------------------------------------------------------- wgrad
+// 512 threads = 8 waves as 2 (n) x 4 (c).  K-step = 32 pixels.
+template <int WN, int WC>
+__global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
+  constexpr int NBn = WN / 32;  // n blocks per wave (wave covers WN/2)
+  constexpr int NBc = WC / 64;  // c blocks per wave (wave covers WC/4)
+  constexpr int DZ_BYTES = WN * 64;  // [WN/16][32 px][16 ch] bf16
+  constexpr int X_BYTES = WC * 64;
+  constexpr int STAGE = DZ_BYTES + X_BYTES;
+  constexpr int NINSTR = (WN + WC) / 16;  // 1 KB glds pieces per stage
+  constexpr int IPW = (NINSTR + 7) / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wn = wave >> 2, wc = wave & 3;
+  const int split = blockIdx.x;
+  const int t = blockIdx.y;
+  const int ncb = a.Cin / WC;
+  const int n0 = (blockIdx.z / ncb) * WN;
+  const int c0 = (blockIdx.z % ncb) * WC;
+  const int kh = t / a.K, kw = t - (t / a.K) * a.K;
+  const int toff = (kh * a.HPi + kw) * a.Cin + c0;
+  const int SS = a.S * a.S;
+  const int ks_begin = split * a.ksteps_per_split;
+  int ks_end = ks_begin + a.ksteps_per_split;
+  const int nks_total = (a.M + 31) / 32;
+  if (ks_end > nks_total) ks_end = nks_total;
+
+  auto stage = [&](int ks, int buf) {
+    const int px = ks * 32 + (lane >> 1);
+    int dzr, xr;
+    {
+      const int pm = px < a.M ? px : a.M - 1;
+      const int b = pm / SS;
+      const int rem = pm - b * SS;
+      const int ii = rem / a.S;
+      const int jj = rem - ii * a.S;
+      dzr = px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout : 0;  // 0 = zero border
+      xr = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + toff;
+    }
+    const int half = (lane & 1) * 8;
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int j = wave * IPW + i;
+      if (j < NINSTR) {
+        if (j < WN / 16) glds16(a.dz + dzr + n0 + j * 16 + half, base + j * 1024);
+        else glds16(a.x + xr + (j - WN / 16) * 16 + half, base + j * 1024);
+      }
+    }
+  };
+
+  f32x4 acc[NBn][NBc];
+#pragma unroll
+  for (int i = 0; i < NBn; ++i)
+#pragma unroll
+    for (int j = 0; j < NBc; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbs[NBn];
+#pragma unroll
+  for (int i = 0; i < NBn; ++i) dbs[i] = 0.f;
+  const bool do_bias = (t == 0) && (c0 == 0) && (wc == 0);
+
+  // transposed-read addresses: group g = lane>>4, row q = (lane&15)>>2, col 4p, p = lane&3
+  const int g = lane >> 4;
+  const int q = (lane & 15) >> 2;
+  const int p = lane & 3;
+  const int tr0 = (4 * g + q) * 32 + p * 8;         // rows 4g..4g+3
+  const int tr1 = (16 + 4 * g + q) * 32 + p * 8;    // rows 16+4g..16+4g+3
+
+  if (ks_begin < ks_end) {
+    stage(ks_begin, 0);
+    wait_vmcnt0();
+    __syncthreads();
+  }
+  for (int ks = ks_begin; ks < ks_end; ++ks) {
+    const int cur = (ks - ks_begin) & 1;
+    if (ks + 1 < ks_end) stage(ks + 1, cur ^ 1);
+    const char* base = smem + cur * STAGE;
+    bf16x8 af[NBn], bfm[NBc];
+#pragma unroll
+    for (int i = 0; i < NBn; ++i) {
+      const char* cb = base + (wn * NBn + i) * 1024;
+      bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr0));
+      bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr1));
+      af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int j = 0; j < NBc; ++j) {
+      const char* cb = base + DZ_BYTES + (wc * NBc + j) * 1024;
+      bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr0));
+      bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr1));
+      bfm[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < NBn; ++i)
+#pragma unroll
+      for (int j = 0; j < NBc; ++j) acc[i][j] = mfma16x16x32(af[i], bfm[j], acc[i][j]);
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < NBn; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)af[i][e];
+        dbs[i] += s;
+      }
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  // --- write the split's partial tile: D[n][c], lane owns n..n+3 at column c
+  float* out = a.slab + ((size_t)split * a.T + t) * (size_t)a.Cout * a.Cin;
+  const int nb0 = n0 + wn * (WN / 2) + ((lane >> 4) << 2);
+  const int cbase = c0 + wc * (WC / 4) + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < NBn; ++i)
+#pragma unroll
+    for (int j = 0; j < NBc; ++j) {
+      const int n = nb0 + i * 16;
+      const int c = cbase + j * 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(size_t)(n + r) * a.Cin + c] = acc[i][j][r];
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < NBn; ++i) {
+      float s = dbs[i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 16) a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / 2) + i * 16 + lane] = s;
+    }
+  }
+}
+
+template <int WN, int WC>
+static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
+  constexpr int smem = 2 * (WN + WC) * 64;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
+  hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC>), grid, dim3(512), smem, st, a);
+}
+
+void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
+  const bool n192 = a.Cout % 192 == 0, c192 = a.Cin % 192 == 0;
+  const bool n128 = a.Cout % 128 == 0, c128 = a.Cin % 128 == 0;
+  if (n192 && c192) launch_wgrad_t<192, 192>(a, st);
+  else if (n192 && c128) launch_wgrad_t<192, 128>(a, st);
+  else if (n192) launch_wgrad_t<192, 64>(a, st);
+  else if (n128 && c128) launch_wgrad_t<128, 128>(a, st);
+  else if (n128 && c192) launch_wgrad_t<128, 192>(a, st);
+  else if (n128) launch_wgrad_t<128, 64>(a, st);
+  else if (c192) launch_wgrad_t<64, 192>(a, st);
+  else if (c128) launch_wgrad_t<64, 128>(a, st);
+  else launch_wgrad_t<64, 64>(a, st);
+}
+
+// Sum split partials into the fp32 OIHW gradient (real channel counts) + bias.
+__global__ void conv_wgrad_reduce_kernel(WgradReduceArgs a) {
+  const int total = a.T * a.Cout_real * a.Cin_real;
+  const size_t tile = (size_t)a.Cout * a.Cin;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    // idx enumerates OIHW order: ((n*Cin_real + c)*T + t)
+    const int t = idx % a.T;
+    const int nc = idx / a.T;
+    const int c = nc % a.Cin_real;
+    const int n = nc / a.Cin_real;
+    const float* s = a.slab + (size_t)t * tile + (size_t)n * a.Cin + c;
+    float sum = 0.f;
+    for (int sp = 0; sp < a.nsplit; ++sp) sum += s[(size_t)sp * a.T * tile];
+    a.grad_w[idx] = a.beta * a.grad_w[idx] + a.scale * sum;
+  }
+  if (blockIdx.x == 0 && a.grad_b) {
+    for (int n = threadIdx.x; n < a.Cout_real; n += blockDim.x) {
+      float sum = 0.f;
+      for (int sp = 0; sp < a.nsplit; ++sp) sum += a.dbias_slab[(size_t)sp * a.Cout + n];
+      a.grad_b[n] = a.beta * a.grad_b[n] + a.scale * sum;
+    }
+  }
+}
+
+void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st) {
+  const int total = a.T * a.Cout_real * a.Cin_real;
+  int blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
+}
+
+}  // namespace agk

@@ -1,0 +1,165 @@
+// Fused policy head: 1x1 conv (F -> 1, scalar bias) + flatten + softmax over
+// S*S + clipped categorical cross-entropy + top-1 accuracy + the whole backward
+// of the head (dlogits, the ReLU-masked gradient into the last trunk layer, and
+// per-board partials of the head weight/bias gradients).  One workgroup per
+// board: the board's 361 x F activations are read from L2 twice and nothing of
+// the head ever round-trips through HBM as a separate tensor.
+//
+// Reference ops replaced: policy.py:145-154 (Conv 1x1 / Flatten / Softmax),
+// Keras categorical_crossentropy with output clipping (supervised_policy_trainer
+// .py:200) and the 'accuracy' metric; inference renormalisation over legal
+// moves replaces CNNPolicy._select_moves_and_normalize (policy.py:44-54).
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace agk {
+
+__device__ __forceinline__ float block_reduce_max(float v, float* red) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i) r = fmaxf(r, red[i]);
+  return r;
+}
+__device__ __forceinline__ float block_reduce_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r += red[i];
+  return r;
+}
+
+template <bool TRAIN>
+__global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
+  __shared__ float w_s[256];
+  __shared__ float z_s[368];
+  __shared__ float red[8];
+  __shared__ int redi[8];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int SS = a.S * a.S;
+  const int HP = a.S + 2;
+  for (int c = tid; c < a.C; c += 256) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
+  __syncthreads();
+  const __bf16* base = a.y + (size_t)b * HP * HP * a.C;
+  const float bias = a.b[0];
+  const uint8_t* legal = a.legal ? a.legal + (size_t)b * SS : nullptr;
+
+  float lmax = -INFINITY;
+  int lidx = 0x7fffffff;
+  for (int p = tid; p < SS; p += 256) {
+    const int i = p / a.S, j = p - (p / a.S) * a.S;
+    const __bf16* row = base + (size_t)((i + 1) * HP + j + 1) * a.C;
+    float dot = 0.f;
+    for (int c8 = 0; c8 < a.C; c8 += 8) {
+      const bf16x8 v = *(const bf16x8*)(row + c8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dot += (float)v[e] * w_s[c8 + e];
+    }
+    float z = (dot + bias) * a.inv_temp;
+    if (legal && !legal[p]) z = -INFINITY;
+    z_s[p] = z;
+    if (z > lmax) {  // first max wins (p increases within a thread)
+      lmax = z;
+      lidx = p;
+    }
+  }
+  // block argmax / max (ties -> smallest index)
+  {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      float ov = __shfl_xor(lmax, o, 64);
+      int oi = __shfl_xor(lidx, o, 64);
+      if (ov > lmax || (ov == lmax && oi < lidx)) {
+        lmax = ov;
+        lidx = oi;
+      }
+    }
+    if ((tid & 63) == 0) {
+      red[tid >> 6] = lmax;
+      redi[tid >> 6] = lidx;
+    }
+    __syncthreads();
+    lmax = red[0];
+    lidx = redi[0];
+    for (int w = 1; w < 4; ++w)
+      if (red[w] > lmax || (red[w] == lmax && redi[w] < lidx)) {
+        lmax = red[w];
+        lidx = redi[w];
+      }
+  }
+  const float zmax = lmax;
+  float ls = 0.f;
+  for (int p = tid; p < SS; p += 256) ls += (z_s[p] == -INFINITY) ? 0.f : __expf(z_s[p] - zmax);
+  const float sum = block_reduce_sum(ls, red);
+  const float inv = 1.f / sum;
+  if (a.probs) {
+    for (int p = tid; p < SS; p += 256)
+      a.probs[(size_t)b * SS + p] = (z_s[p] == -INFINITY) ? 0.f : __expf(z_s[p] - zmax) * inv;
+  }
+  if constexpr (TRAIN) {
+    const int t = a.target[b];
+    if (tid == 0) {
+      if (t >= 0) {
+        float pt = __expf(z_s[t] - zmax) * inv;
+        pt = fminf(fmaxf(pt, 1e-7f), 1.f - 1e-7f);  // Keras clip
+        a.loss[b] = -__logf(pt);
+        a.correct[b] = (lidx == t) ? 1.f : 0.f;
+      } else {
+        a.loss[b] = 0.f;
+        a.correct[b] = 0.f;
+      }
+    }
+    __syncthreads();  // everyone has read z_s[t]
+    for (int p = tid; p < SS; p += 256) {
+      float g = 0.f;
+      if (t >= 0) g = (__expf(z_s[p] - zmax) * inv - (p == t ? 1.f : 0.f)) * a.grad_scale;
+      z_s[p] = g;
+    }
+    __syncthreads();
+    // gradient into the last trunk activation, masked by ReLU'
+    const int C8 = a.C >> 3;
+    __bf16* dzb = a.dz + (size_t)b * HP * HP * a.C;
+    for (int idx = tid; idx < SS * C8; idx += 256) {
+      const int p = idx / C8;
+      const int c8 = (idx - p * C8) << 3;
+      const int i = p / a.S, j = p - (p / a.S) * a.S;
+      const size_t off = (size_t)((i + 1) * HP + j + 1) * a.C + c8;
+      const bf16x8 v = *(const bf16x8*)(base + off);
+      const float g = z_s[p];
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (__bf16)((float)v[e] > 0.f ? g * w_s[c8 + e] : 0.f);
+      *(bf16x8*)(dzb + off) = o;
+    }
+    // per-board head-weight / bias gradient partials
+    float* dh = a.dhead + (size_t)b * (a.C_real + 1);
+    for (int c = tid; c < a.C_real; c += 256) {
+      float s = 0.f;
+      for (int p = 0; p < SS; ++p) {
+        const int i = p / a.S, j = p - (p / a.S) * a.S;
+        s += z_s[p] * (float)base[(size_t)((i + 1) * HP + j + 1) * a.C + c];
+      }
+      dh[c] = s;
+    }
+    float gs = 0.f;
+    for (int p = tid; p < SS; p += 256) gs += z_s[p];
+    gs = block_reduce_sum(gs, red);
+    if (tid == 0) dh[a.C_real] = gs;
+  }
+}
+
+void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st) {
+  if (train) hipLaunchKernelGGL(policy_head_kernel<true>, dim3(a.B), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(policy_head_kernel<false>, dim3(a.B), dim3(256), 0, st, a);
+}
+
+}  // namespace agk

@@ -1,0 +1,85 @@
+// Kernel argument structs and host launchers (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace agk {
+
+enum { MODE_BIAS_RELU = 0, MODE_MASK = 1, MODE_NONE = 2 };
+
+struct ConvFwdArgs {
+  const __bf16* x;     // padded NHWC input
+  const __bf16* w;     // packed [T][Cout][Cin]
+  const float* bias;   // [Cout]           (MODE_BIAS_RELU)
+  const __bf16* mask;  // layout of y      (MODE_MASK: keep where mask > 0)
+  __bf16* y;           // padded NHWC output (interior written, borders untouched)
+  int M, S, Cin, Cout, K;
+  int HPi, offi;       // input padded side, (input pad - K/2)
+  int HPo, Po;         // output padded side and pad
+};
+
+struct ConvWgradArgs {
+  const __bf16* x;     // layer input (padded NHWC, Cin)
+  const __bf16* dz;    // gradient at the layer's pre-activation output (padded NHWC, Cout, zero borders)
+  float* slab;         // [nsplit][T][Cout][Cin]
+  float* dbias_slab;   // [nsplit][Cout]
+  int M, S, Cin, Cout, K, T;
+  int HPi, offi, HPo, Po;
+  int ksteps_per_split, nsplit;
+};
+
+struct WgradReduceArgs {
+  const float* slab;
+  const float* dbias_slab;
+  float* grad_w;  // OIHW fp32 [Cout_real][Cin_real][K][K]
+  float* grad_b;  // [Cout_real] or null
+  int T, Cout, Cin, Cout_real, Cin_real, nsplit;
+  float scale, beta;  // grad = beta*grad + scale*sum
+};
+
+struct PolicyHeadArgs {
+  const __bf16* y;     // padded NHWC (HP = S+2, P = 1, C)
+  const float* w;      // [C_real]
+  const float* b;      // [1]
+  const int* target;   // [B] flat move index or -1 (no loss)
+  const uint8_t* legal;  // [B][S*S] or null (inference renormalisation)
+  __bf16* dz;          // padded NHWC grad (training) or null
+  float* loss;         // [B]
+  float* correct;      // [B]
+  float* dhead;        // [B][C_real + 1] per-board partials of dW_head, db_head
+  float* probs;        // [B][S*S] or null
+  int B, S, C, C_real;
+  float grad_scale;    // d(mean loss)/d(logit) scale = 1/global_batch
+  float inv_temp;
+};
+
+struct PackInputArgs {
+  const uint8_t* planes;  // [B][Creal][S][S]
+  const int* sym;         // [B] in 0..7 or null (identity)
+  const int* target;      // [B] or null
+  int* target_out;        // [B] or null
+  __bf16* out;            // padded NHWC [B][S+2P][S+2P][Cp]
+  int B, S, Creal, Cp, P;
+};
+
+constexpr int kMaxPackLayers = 24;
+struct PackLayer {
+  const float* w;  // OIHW fp32 [Cout_real][Cin_real][K][K]
+  __bf16* wf;      // [T][Cout_p][Cin_p]
+  __bf16* wd;      // [T][Cin_p][Cout_p] flipped (dgrad) or null
+  int Cout_real, Cin_real, Cout_p, Cin_p, K;
+};
+struct PackWeightsArgs {
+  PackLayer layers[kMaxPackLayers];
+  int nlayers;
+};
+
+void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
+void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
+void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
+void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
+void launch_pack_input(const PackInputArgs& a, hipStream_t st);
+void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st);
+void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
+
+}  // namespace agk

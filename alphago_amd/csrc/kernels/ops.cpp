@@ -1,0 +1,217 @@
+// PyTorch custom-op registration for the gfx950 kernels: torch.ops.alphago_amd.*
+// All ops write into caller-provided buffers (no allocation inside), run on the
+// current HIP stream and are therefore safe to capture in HIP graphs.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a device tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+
+const __bf16* bfp(const Tensor& t) { return reinterpret_cast<const __bf16*>(t.data_ptr()); }
+__bf16* bfp_mut(const Tensor& t) { return reinterpret_cast<__bf16*>(t.data_ptr()); }
+
+// x: (B, HPi, HPi, Cin) bf16; w: (T, Cout, Cin) bf16; y: (B, HPo, HPo, Cout) bf16
+void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const c10::optional<Tensor>& mask,
+              const Tensor& y, int64_t K, int64_t S, int64_t Pin, int64_t Po, int64_t mode) {
+  CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
+  CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
+  CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && w.dim() == 3, "bad ranks");
+  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3);
+  const int64_t HPo = y.size(1), Cout = y.size(3);
+  TORCH_CHECK(x.size(2) == HPi && y.size(2) == HPo && y.size(0) == B, "bad spatial dims");
+  TORCH_CHECK(w.size(0) == K * K && w.size(1) == Cout && w.size(2) == Cin, "w must be (K*K, Cout, Cin)");
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "channels must be multiples of 64");
+  TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin && HPo == S + 2 * Po, "padding/geometry mismatch");
+  TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31) && B * HPo * HPo * Cout < (1ll << 31), "tensor too large for int32 offsets");
+  agk::ConvFwdArgs a{};
+  a.x = bfp(x);
+  a.w = bfp(w);
+  a.y = bfp_mut(y);
+  a.M = (int)(B * S * S);
+  a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
+  if (mode == agk::MODE_BIAS_RELU) {
+    TORCH_CHECK(bias.has_value(), "bias required");
+    CHECK_F32(*bias); CHECK_DEV(*bias);
+    TORCH_CHECK(bias->numel() >= Cout, "bias too small");
+    a.bias = bias->data_ptr<float>();
+  } else if (mode == agk::MODE_MASK) {
+    TORCH_CHECK(mask.has_value(), "mask required");
+    CHECK_BF16(*mask); CHECK_CONTIG(*mask);
+    TORCH_CHECK(mask->sizes() == y.sizes(), "mask must match y");
+    a.mask = bfp(*mask);
+  }
+  if (a.M == 0) return;
+  agk::launch_conv_fwd(a, (int)mode, cur_stream());
+}
+
+// slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
+void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
+                int64_t Pin, int64_t Po) {
+  CHECK_DEV(x); CHECK_DEV(dz); CHECK_DEV(slab); CHECK_DEV(dbslab);
+  CHECK_BF16(x); CHECK_BF16(dz); CHECK_F32(slab); CHECK_F32(dbslab);
+  CHECK_CONTIG(x); CHECK_CONTIG(dz); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
+  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3);
+  const int64_t HPo = dz.size(1), Cout = dz.size(3);
+  const int64_t nsplit = slab.size(0);
+  TORCH_CHECK(slab.dim() == 4 && slab.size(1) == K * K && slab.size(2) == Cout && slab.size(3) == Cin, "bad slab");
+  TORCH_CHECK(dbslab.size(0) == nsplit && dbslab.size(1) == Cout, "bad dbias slab");
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "channels must be multiples of 64");
+  TORCH_CHECK(HPi == S + 2 * Pin && HPo == S + 2 * Po && Po >= 1 && Pin >= K / 2, "geometry mismatch");
+  agk::ConvWgradArgs a{};
+  a.x = bfp(x); a.dz = bfp(dz);
+  a.slab = slab.data_ptr<float>();
+  a.dbias_slab = dbslab.data_ptr<float>();
+  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K; a.T = (int)(K * K);
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
+  const int nks = (a.M + 31) / 32;
+  a.nsplit = (int)nsplit;
+  a.ksteps_per_split = (nks + a.nsplit - 1) / a.nsplit;
+  agk::launch_conv_wgrad(a, cur_stream());
+}
+
+void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
+                       double scale, double beta) {
+  CHECK_F32(slab); CHECK_F32(grad_w); CHECK_CONTIG(grad_w);
+  const int64_t nsplit = slab.size(0), T = slab.size(1), Cout = slab.size(2), Cin = slab.size(3);
+  TORCH_CHECK(grad_w.dim() == 4 && grad_w.size(2) * grad_w.size(3) == T, "grad_w must be OIHW");
+  agk::WgradReduceArgs a{};
+  a.slab = slab.data_ptr<float>();
+  a.dbias_slab = dbslab.data_ptr<float>();
+  a.grad_w = grad_w.data_ptr<float>();
+  a.grad_b = grad_b.has_value() ? grad_b->data_ptr<float>() : nullptr;
+  a.T = (int)T; a.Cout = (int)Cout; a.Cin = (int)Cin;
+  a.Cout_real = (int)grad_w.size(0); a.Cin_real = (int)grad_w.size(1);
+  TORCH_CHECK(a.Cout_real <= Cout && a.Cin_real <= Cin, "grad_w larger than padded slab");
+  a.nsplit = (int)nsplit;
+  a.scale = (float)scale; a.beta = (float)beta;
+  agk::launch_wgrad_reduce(a, cur_stream());
+}
+
+void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::optional<Tensor>& target,
+                 const c10::optional<Tensor>& legal, const c10::optional<Tensor>& dz, const c10::optional<Tensor>& loss,
+                 const c10::optional<Tensor>& correct, const c10::optional<Tensor>& dhead,
+                 const c10::optional<Tensor>& probs, int64_t S, double grad_scale, double temperature) {
+  CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(b);
+  const int64_t B = y.size(0), C = y.size(3);
+  TORCH_CHECK(y.size(1) == S + 2, "head input must have pad 1");
+  TORCH_CHECK(C % 8 == 0 && C <= 256, "head channels must be a multiple of 8 and <= 256");
+  TORCH_CHECK(S * S <= 368, "board too large");
+  agk::PolicyHeadArgs a{};
+  a.y = bfp(y);
+  a.w = w.data_ptr<float>();
+  a.b = b.data_ptr<float>();
+  a.B = (int)B; a.S = (int)S; a.C = (int)C; a.C_real = (int)w.numel();
+  a.grad_scale = (float)grad_scale;
+  a.inv_temp = (float)(1.0 / temperature);
+  const bool train = target.has_value();
+  if (train) {
+    TORCH_CHECK(dz && loss && correct && dhead, "training head needs dz, loss, correct, dhead");
+    TORCH_CHECK(target->scalar_type() == at::kInt, "target must be int32");
+    TORCH_CHECK(dz->sizes() == y.sizes(), "dz must match y");
+    TORCH_CHECK(dhead->numel() >= B * (a.C_real + 1), "dhead too small");
+    a.target = target->data_ptr<int>();
+    a.dz = bfp_mut(*dz);
+    a.loss = loss->data_ptr<float>();
+    a.correct = correct->data_ptr<float>();
+    a.dhead = dhead->data_ptr<float>();
+  }
+  if (legal.has_value()) {
+    TORCH_CHECK(legal->scalar_type() == at::kByte && legal->numel() == B * S * S, "legal must be uint8 (B, S*S)");
+    a.legal = legal->data_ptr<uint8_t>();
+  }
+  if (probs.has_value()) {
+    CHECK_F32(*probs);
+    TORCH_CHECK(probs->numel() == B * S * S, "probs must be (B, S*S)");
+    a.probs = probs->data_ptr<float>();
+  }
+  if (B == 0) return;
+  agk::launch_policy_head(a, train, cur_stream());
+}
+
+void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c10::optional<Tensor>& target,
+                const c10::optional<Tensor>& target_out, const Tensor& out, int64_t P) {
+  TORCH_CHECK(planes.scalar_type() == at::kByte && planes.is_contiguous() && planes.dim() == 4, "planes: uint8 (B,C,S,S)");
+  CHECK_BF16(out); CHECK_CONTIG(out);
+  const int64_t B = planes.size(0), C = planes.size(1), S = planes.size(2);
+  TORCH_CHECK(out.size(0) == B && out.size(1) == S + 2 * P && out.size(3) >= C && out.size(3) % 8 == 0, "bad out");
+  agk::PackInputArgs a{};
+  a.planes = planes.data_ptr<uint8_t>();
+  a.sym = sym.has_value() ? sym->data_ptr<int>() : nullptr;
+  a.target = target.has_value() ? target->data_ptr<int>() : nullptr;
+  a.target_out = target_out.has_value() ? target_out->data_ptr<int>() : nullptr;
+  TORCH_CHECK(!a.target_out || a.target, "target_out needs target");
+  a.out = bfp_mut(out);
+  a.B = (int)B; a.S = (int)S; a.Creal = (int)C; a.Cp = (int)out.size(3); a.P = (int)P;
+  if (B == 0) return;
+  agk::launch_pack_input(a, cur_stream());
+}
+
+// ws: list of OIHW fp32; wf: list of (T, Coutp, Cinp) bf16; wd: list (possibly empty entries skipped)
+void pack_weights(at::TensorList ws, at::TensorList wf, at::TensorList wd) {
+  TORCH_CHECK(ws.size() == wf.size() && (wd.size() == 0 || wd.size() == ws.size()), "list sizes");
+  size_t i = 0;
+  while (i < ws.size()) {
+    agk::PackWeightsArgs a{};
+    a.nlayers = 0;
+    for (; i < ws.size() && a.nlayers < agk::kMaxPackLayers; ++i) {
+      const Tensor& w = ws[i];
+      CHECK_F32(w); CHECK_CONTIG(w); CHECK_BF16(wf[i]);
+      agk::PackLayer& L = a.layers[a.nlayers++];
+      L.w = w.data_ptr<float>();
+      L.Cout_real = (int)w.size(0); L.Cin_real = (int)w.size(1); L.K = (int)w.size(2);
+      L.wf = bfp_mut(wf[i]);
+      L.Cout_p = (int)wf[i].size(1); L.Cin_p = (int)wf[i].size(2);
+      TORCH_CHECK(wf[i].size(0) == L.K * L.K && L.Cout_p >= L.Cout_real && L.Cin_p >= L.Cin_real, "bad wf");
+      L.wd = nullptr;
+      if (wd.size() && wd[i].numel() > 0) {
+        CHECK_BF16(wd[i]);
+        TORCH_CHECK(wd[i].size(1) == L.Cin_p && wd[i].size(2) == L.Cout_p, "bad wd");
+        L.wd = bfp_mut(wd[i]);
+      }
+    }
+    agk::launch_pack_weights(a, cur_stream());
+  }
+}
+
+void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
+  CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
+  TORCH_CHECK(p.numel() == g.numel(), "size mismatch");
+  agk::launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(), p.numel(), (float)lr, (float)gscale, cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(alphago_amd, m) {
+  m.def("conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode) -> ()");
+  m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po) -> ()");
+  m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
+  m.def(
+      "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor(a!)? dz, Tensor(b!)? loss, "
+      "Tensor(c!)? correct, Tensor(d!)? dhead, Tensor(e!)? probs, int S, float grad_scale, float temperature) -> ()");
+  m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P) -> ()");
+  m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
+  m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
+  m.impl("conv_fwd", &conv_fwd);
+  m.impl("conv_wgrad", &conv_wgrad);
+  m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);
+  m.impl("policy_head", &policy_head);
+  m.impl("pack_input", &pack_input);
+  m.impl("pack_weights", &pack_weights);
+  m.impl("sgd_update", &sgd_update);
+}

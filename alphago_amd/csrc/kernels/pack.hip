@@ -1,0 +1,142 @@
+// Data-movement kernels around the conv trunk:
+//  * pack_input: uint8 feature planes [B][C][S][S] -> zero-bordered NHWC bf16
+//    with a per-board D4 symmetry applied on the fly (the reference does the
+//    8-way augmentation on the CPU per sample with numpy, supervised_policy_
+//    trainer.py:27-36,71-80) and the move targets transformed consistently.
+//  * pack_weights: fp32 OIHW master weights -> bf16 [tap][Cout][Cin] (forward)
+//    and the tap-flipped, transposed [tap][Cin][Cout] copy used by dgrad, for
+//    every layer in one launch.
+//  * sgd: p -= lr * scale * g over the flat fp32 parameter buffer (Keras SGD,
+//    momentum 0; the 1/world_size all-reduce average is folded into `scale`).
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace agk {
+
+// Symmetry s maps board point (x, y) to (x', y'); numpy semantics of the
+// reference BOARD_TRANSFORMATIONS on a [x][y] array.
+__device__ __forceinline__ void sym_fwd(int s, int n, int x, int y, int& ox, int& oy) {
+  switch (s) {
+    case 1: ox = n - 1 - y; oy = x; break;          // rot90
+    case 2: ox = n - 1 - x; oy = n - 1 - y; break;  // rot180
+    case 3: ox = y; oy = n - 1 - x; break;          // rot270
+    case 4: ox = x; oy = n - 1 - y; break;          // fliplr
+    case 5: ox = n - 1 - x; oy = y; break;          // flipud
+    case 6: ox = y; oy = x; break;                  // transpose
+    case 7: ox = n - 1 - y; oy = n - 1 - x; break;  // fliplr(rot90)
+    default: ox = x; oy = y; break;
+  }
+}
+__device__ __forceinline__ void sym_inv(int s, int n, int i, int j, int& x, int& y) {
+  switch (s) {
+    case 1: x = j; y = n - 1 - i; break;
+    case 3: x = n - 1 - j; y = i; break;
+    default: sym_fwd(s, n, i, j, x, y); break;  // the others are involutions
+  }
+}
+
+__global__ void pack_input_kernel(PackInputArgs a) {
+  const int SS = a.S * a.S;
+  const int C8 = a.Cp >> 3;
+  const int HP = a.S + 2 * a.P;
+  const int total = a.B * SS * C8;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int c8 = idx % C8;
+    const int rest = idx / C8;
+    const int p = rest % SS;
+    const int b = rest / SS;
+    const int i = p / a.S, j = p - (p / a.S) * a.S;
+    const int s = a.sym ? a.sym[b] : 0;
+    int x, y;
+    sym_inv(s, a.S, i, j, x, y);
+    const uint8_t* src = a.planes + (size_t)b * a.Creal * SS + x * a.S + y;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c8 * 8 + e;
+      o[e] = (__bf16)(c < a.Creal ? (float)src[(size_t)c * SS] : 0.f);
+    }
+    *(bf16x8*)(a.out + ((size_t)(b * HP + i + a.P) * HP + j + a.P) * a.Cp + c8 * 8) = o;
+    if (a.target_out && p == 0 && c8 == 0) {
+      const int t = a.target[b];
+      int r = -1;
+      if (t >= 0) {
+        int ox, oy;
+        sym_fwd(s, a.S, t / a.S, t % a.S, ox, oy);
+        r = ox * a.S + oy;
+      }
+      a.target_out[b] = r;
+    }
+  }
+}
+
+void launch_pack_input(const PackInputArgs& a, hipStream_t st) {
+  const int total = a.B * a.S * a.S * (a.Cp / 8);
+  int blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(pack_input_kernel, dim3(blocks), dim3(256), 0, st, a);
+}
+
+__global__ void pack_weights_kernel(PackWeightsArgs a) {
+  const PackLayer L = a.layers[blockIdx.y];
+  const int T = L.K * L.K;
+  const int total = T * L.Cout_p * L.Cin_p;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    const int c = idx % L.Cin_p;
+    const int rest = idx / L.Cin_p;
+    const int n = rest % L.Cout_p;
+    const int t = rest / L.Cout_p;
+    float v = 0.f;
+    if (n < L.Cout_real && c < L.Cin_real) v = L.w[((size_t)n * L.Cin_real + c) * T + t];
+    const __bf16 bv = (__bf16)v;
+    L.wf[idx] = bv;
+    if (L.wd) {
+      const int kh = t / L.K, kw = t - (t / L.K) * L.K;
+      const int tf = (L.K - 1 - kh) * L.K + (L.K - 1 - kw);
+      L.wd[((size_t)tf * L.Cin_p + c) * L.Cout_p + n] = bv;
+    }
+  }
+}
+
+void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st) {
+  if (a.nlayers <= 0) return;
+  int maxtot = 0;
+  for (int i = 0; i < a.nlayers; ++i) {
+    const PackLayer& L = a.layers[i];
+    const int tot = L.K * L.K * L.Cout_p * L.Cin_p;
+    if (tot > maxtot) maxtot = tot;
+  }
+  int blocks = (maxtot + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(blocks, a.nlayers), dim3(256), 0, st, a);
+}
+
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, int64_t n, float step) {
+  const int64_t n4 = n >> 2;
+  float4* p4 = (float4*)p;
+  const float4* g4 = (const float4*)g;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pv = p4[i];
+    const float4 gv = g4[i];
+    pv.x -= step * gv.x;
+    pv.y -= step * gv.y;
+    pv.z -= step * gv.z;
+    pv.w -= step * gv.w;
+    p4[i] = pv;
+  }
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] -= step * g[i];
+}
+
+void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st) {
+  int64_t blocks = ((n >> 2) + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, g, n, lr * gscale);
+}
+
+}  // namespace agk

@@ -1,0 +1,130 @@
+"""HIP (gfx950) kernel library: loading + thin Python wrappers.
+
+The kernels live in ``alphago_amd/csrc/kernels`` and are compiled in-tree into
+``alphago_amd/_hip_kernels.so`` (``python -m alphago_amd._build hip``).  They
+are registered as ``torch.ops.alphago_amd.*``.  There is no silent fallback:
+``load()`` raises if the library is missing on a machine with a GPU.
+
+Tensor conventions (see csrc/kernels/conv.hip): activations are zero-bordered
+NHWC bf16 ``(B, S+2P, S+2P, C)`` with C a multiple of 64; packed conv weights
+are bf16 ``(K*K, Cout_p, Cin_p)``.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Optional
+
+import torch
+
+from .. import _build
+
+_lock = threading.Lock()
+_loaded = False
+
+MODE_BIAS_RELU, MODE_MASK, MODE_NONE = 0, 1, 2
+
+
+def library_path() -> str:
+    return _build.hip_path()
+
+
+def load(build_if_missing: bool = True) -> None:
+    """Load the HIP kernel library (building it first if it is absent)."""
+    global _loaded
+    if _loaded:
+        return
+    with _lock:
+        if _loaded:
+            return
+        path = library_path()
+        if not os.path.exists(path) or os.environ.get("ALPHAGO_AMD_REBUILD"):
+            if not build_if_missing:
+                raise RuntimeError("alphago_amd HIP kernels not built: %s" % path)
+            _build.build_hip()
+        torch.ops.load_library(path)
+        _loaded = True
+
+
+def is_loaded() -> bool:
+    return _loaded
+
+
+def _ops():
+    load()
+    return torch.ops.alphago_amd
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+# ----------------------------------------------------------------- layout helpers
+def padded_empty(B: int, S: int, P: int, C: int, device, dtype=torch.bfloat16) -> torch.Tensor:
+    """Zero-initialised padded NHWC buffer (borders must stay zero)."""
+    return torch.zeros((B, S + 2 * P, S + 2 * P, C), device=device, dtype=dtype)
+
+
+def to_padded(x: torch.Tensor, P: int, Cp: Optional[int] = None) -> torch.Tensor:
+    """NCHW (any float) -> zero-bordered NHWC bf16 with channels padded to Cp."""
+    B, C, S, _ = x.shape
+    Cp = Cp or round_up(C, 64)
+    out = padded_empty(B, S, P, Cp, x.device)
+    out[:, P:P + S, P:P + S, :C] = x.permute(0, 2, 3, 1).to(torch.bfloat16)
+    return out
+
+
+def from_padded(y: torch.Tensor, P: int, C: Optional[int] = None) -> torch.Tensor:
+    """Zero-bordered NHWC -> NCHW fp32 interior."""
+    S = y.shape[1] - 2 * P
+    C = C or y.shape[3]
+    return y[:, P:P + S, P:P + S, :C].permute(0, 3, 1, 2).float()
+
+
+# ----------------------------------------------------------------- op wrappers
+def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: int = MODE_BIAS_RELU, mask=None):
+    _ops().conv_fwd(x, w_packed, bias, mask, y, K, S, Pin, Po, mode)
+    return y
+
+
+def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1):
+    _ops().conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po)
+
+
+def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, beta: float = 0.0):
+    _ops().conv_wgrad_reduce(slab, dbslab, grad_w, grad_b, scale, beta)
+
+
+def policy_head_train(y, w, b, target, dz, loss, correct, dhead, S: int, grad_scale: float):
+    _ops().policy_head(y, w, b, target, None, dz, loss, correct, dhead, None, S, grad_scale, 1.0)
+
+
+def policy_head_probs(y, w, b, probs, S: int, legal=None, temperature: float = 1.0):
+    _ops().policy_head(y, w, b, None, legal, None, None, None, None, probs, S, 0.0, temperature)
+    return probs
+
+
+def pack_input(planes_u8, out, P: int, sym=None, target=None, target_out=None):
+    _ops().pack_input(planes_u8, sym, target, target_out, out, P)
+    return out
+
+
+def pack_weights(ws, wf, wd=()):
+    _ops().pack_weights(list(ws), list(wf), list(wd))
+
+
+def sgd_update(p, g, lr: float, gscale: float = 1.0):
+    _ops().sgd_update(p, g, lr, gscale)
+
+
+def packed_weight_like(w_oihw: torch.Tensor, cin_p: int, cout_p: int, transposed: bool = False) -> torch.Tensor:
+    K = w_oihw.shape[2]
+    shape = (K * K, cin_p, cout_p) if transposed else (K * K, cout_p, cin_p)
+    return torch.zeros(shape, device=w_oihw.device, dtype=torch.bfloat16)
+
+
+def wgrad_splits(M: int, T: int, n_tiles: int = 1, target_wgs: int = 512) -> int:
+    """Number of pixel splits so the wgrad grid has ~target_wgs workgroups."""
+    nks = (M + 31) // 32
+    s = max(1, target_wgs // max(1, T * n_tiles))
+    return max(1, min(s, nks))

@@ -1,0 +1,177 @@
+"""Numerics of the gfx950 HIP kernels vs plain PyTorch fp32 references."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops(cuda_device):
+    from alphago_amd import ops as _ops
+
+    _ops.load()
+    return _ops
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _rel_err(a, b):
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-6)
+
+
+@pytest.mark.parametrize("B,Cin,Cout,K", [(5, 64, 192, 3), (3, 64, 192, 5), (4, 192, 192, 3), (7, 128, 128, 3), (2, 64, 64, 3)])
+def test_conv_fwd_bias_relu(ops, cuda_device, B, Cin, Cout, K):
+    torch.manual_seed(0)
+    S, P = 19, K // 2
+    x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
+    w = _bf(torch.randn(Cout, Cin, K, K, device=cuda_device) * 0.05)
+    b = torch.randn(Cout, device=cuda_device) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=P))
+    xp = ops.to_padded(x, P)
+    wp = ops.packed_weight_like(w, Cin, Cout)
+    ops.pack_weights([w.contiguous()], [wp])
+    y = ops.padded_empty(B, S, 1, Cout, cuda_device)
+    ops.conv_fwd(xp, wp, b, y, K, S, P, 1)
+    torch.cuda.synchronize()
+    out = ops.from_padded(y, 1)
+    assert _rel_err(out, ref) < 1e-2
+    # borders untouched
+    assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
+
+
+def test_conv_fwd_asymmetric_identity(ops, cuda_device):
+    """Tap/axis orientation check with an asymmetric single-tap kernel."""
+    B, C, S = 1, 64, 19
+    x = torch.zeros(B, C, S, S, device=cuda_device)
+    x[0, 3, 5, 7] = 1.0
+    w = torch.zeros(64, C, 3, 3, device=cuda_device)
+    w[10, 3, 0, 2] = 2.0  # kh=0, kw=2
+    ref = F.conv2d(x, w, padding=1)
+    xp = ops.to_padded(x, 1)
+    wp = ops.packed_weight_like(w, C, 64)
+    ops.pack_weights([w], [wp])
+    y = ops.padded_empty(B, S, 1, 64, cuda_device)
+    ops.conv_fwd(xp, wp, torch.zeros(64, device=cuda_device), y, 3, S, 1, 1)
+    out = ops.from_padded(y, 1)
+    assert torch.equal(out, F.relu(ref))
+
+
+@pytest.mark.parametrize("B,C,K", [(5, 192, 3), (3, 64, 3)])
+def test_conv_dgrad_with_relu_mask(ops, cuda_device, B, C, K):
+    torch.manual_seed(1)
+    S = 19
+    dz = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w = _bf(torch.randn(C, C, K, K, device=cuda_device) * 0.05)
+    yprev = _bf(torch.randn(B, C, S, S, device=cuda_device)).clamp_min(0)  # post-ReLU activation
+    # dx = conv_transpose(dz, w); masked by relu'(yprev)
+    ref = torch.nn.grad.conv2d_input((B, C, S, S), w, dz, padding=K // 2) * (yprev > 0)
+    wf = ops.packed_weight_like(w, C, C)
+    wd = ops.packed_weight_like(w, C, C, transposed=True)
+    ops.pack_weights([w], [wf], [wd])
+    dzp = ops.to_padded(dz, 1)
+    yp = ops.to_padded(yprev, 1)
+    dx = ops.padded_empty(B, S, 1, C, cuda_device)
+    ops.conv_fwd(dzp, wd, None, dx, K, S, 1, 1, mode=ops.MODE_MASK, mask=yp)
+    out = ops.from_padded(dx, 1)
+    assert _rel_err(out, ref) < 1e-2
+
+
+@pytest.mark.parametrize("B,Cin,Cout,K,Pin", [(6, 192, 192, 3, 1), (5, 64, 192, 5, 2), (3, 64, 64, 3, 1), (9, 128, 128, 3, 1)])
+def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin):
+    torch.manual_seed(2)
+    S = 19
+    x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
+    dz = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
+    ref_w = torch.nn.grad.conv2d_weight(x, (Cout, Cin, K, K), dz, padding=K // 2)
+    ref_b = dz.sum(dim=(0, 2, 3))
+    xp = ops.to_padded(x, Pin)
+    dzp = ops.to_padded(dz, 1)
+    M = B * S * S
+    ns = ops.wgrad_splits(M, K * K)
+    slab = torch.empty(ns, K * K, Cout, Cin, device=cuda_device)
+    dbs = torch.zeros(ns, Cout, device=cuda_device)
+    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1)
+    gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
+    gb = torch.zeros(Cout, device=cuda_device)
+    ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert _rel_err(gw, ref_w) < 2e-3
+    assert _rel_err(gb, ref_b) < 2e-3
+
+
+def test_policy_head_train(ops, cuda_device):
+    torch.manual_seed(3)
+    B, C, S = 7, 192, 19
+    y = _bf(torch.randn(B, C, S, S, device=cuda_device)).clamp_min(0)
+    w = torch.randn(C, device=cuda_device) * 0.05
+    b = torch.randn(1, device=cuda_device)
+    tgt = torch.randint(0, S * S, (B,), device=cuda_device, dtype=torch.int32)
+    tgt[2] = -1  # no target
+    yr = y.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    logits = (yr * wr.view(1, C, 1, 1)).sum(1).flatten(1) + br
+    valid = tgt >= 0
+    lossv = F.cross_entropy(logits[valid], tgt[valid].long(), reduction="none")
+    (lossv.sum() / B).backward()
+    yp = ops.to_padded(y, 1)
+    dz = ops.padded_empty(B, S, 1, C, cuda_device)
+    loss = torch.empty(B, device=cuda_device)
+    corr = torch.empty(B, device=cuda_device)
+    dh = torch.empty(B, C + 1, device=cuda_device)
+    ops.policy_head_train(yp, w, b, tgt, dz, loss, corr, dh, S, 1.0 / B)
+    torch.cuda.synchronize()
+    assert torch.allclose(loss[valid], lossv.detach(), rtol=1e-3, atol=1e-4)
+    assert loss[2].item() == 0
+    acc_ref = (logits.argmax(1) == tgt.long()).float() * valid
+    assert torch.equal(corr, acc_ref)
+    dzr = yr.grad * (y > 0)
+    assert _rel_err(ops.from_padded(dz, 1), dzr) < 1e-2
+    assert _rel_err(dh[:, :C].sum(0), wr.grad) < 1e-3
+    assert abs(dh[:, C].sum().item() - br.grad.item()) < 1e-4
+
+
+def test_policy_head_probs_legal(ops, cuda_device):
+    torch.manual_seed(4)
+    B, C, S = 3, 128, 19
+    y = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w = torch.randn(C, device=cuda_device) * 0.1
+    b = torch.zeros(1, device=cuda_device)
+    legal = (torch.rand(B, S * S, device=cuda_device) > 0.3).to(torch.uint8)
+    logits = (y * w.view(1, C, 1, 1)).sum(1).flatten(1)
+    ref = torch.softmax(logits.masked_fill(legal == 0, float("-inf")), 1)
+    probs = torch.empty(B, S * S, device=cuda_device)
+    ops.policy_head_probs(ops.to_padded(y, 1), w, b, probs, S, legal=legal)
+    assert torch.allclose(probs, ref, atol=1e-5)
+
+
+def test_pack_input_symmetries(ops, cuda_device):
+    torch.manual_seed(5)
+    B, C, S = 8, 48, 19
+    planes = torch.randint(0, 2, (B, C, S, S), dtype=torch.uint8)
+    sym = torch.arange(8, dtype=torch.int32)
+    tgt = torch.randint(0, S * S, (B,), dtype=torch.int32)
+    tf = [lambda a: a, lambda a: np.rot90(a, 1), lambda a: np.rot90(a, 2), lambda a: np.rot90(a, 3),
+          lambda a: np.fliplr(a), lambda a: np.flipud(a), lambda a: np.transpose(a), lambda a: np.fliplr(np.rot90(a, 1))]
+    out = ops.padded_empty(B, S, 2, 64, cuda_device)
+    tout = torch.empty(B, dtype=torch.int32, device=cuda_device)
+    ops.pack_input(planes.to(cuda_device), out, 2, sym=sym.to(cuda_device), target=tgt.to(cuda_device), target_out=tout)
+    got = ops.from_padded(out, 2, C).cpu().numpy()
+    for b in range(B):
+        exp = np.stack([tf[b](planes[b, c].numpy()) for c in range(C)])
+        assert np.array_equal(got[b], exp), "symmetry %d" % b
+        onehot = np.zeros((S, S))
+        onehot[divmod(int(tgt[b]), S)] = 1
+        assert int(np.argmax(tf[b](onehot))) == int(tout[b])
+
+
+def test_sgd_update(ops, cuda_device):
+    p = torch.randn(1003, device=cuda_device)
+    g = torch.randn(1003, device=cuda_device)
+    ref = p - 0.01 * 0.5 * g
+    ops.sgd_update(p, g, 0.01, 0.5)
+    assert torch.allclose(p, ref)
