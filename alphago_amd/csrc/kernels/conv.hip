@@ -351,19 +351,32 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
 }
 
 // Sum split partials into the fp32 OIHW gradient (real channel counts) + bias.
+// Threads walk the slab in its natural [t][n][c] order (c fastest) so every
+// split read is coalesced; the OIHW write is strided but only touches the
+// (small) gradient once.
 __global__ void conv_wgrad_reduce_kernel(WgradReduceArgs a) {
-  const int total = a.T * a.Cout_real * a.Cin_real;
+  const int total = a.T * a.Cout_real * a.Cin;
   const size_t tile = (size_t)a.Cout * a.Cin;
+  const size_t sstride = (size_t)a.T * tile;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-    // idx enumerates OIHW order: ((n*Cin_real + c)*T + t)
-    const int t = idx % a.T;
-    const int nc = idx / a.T;
-    const int c = nc % a.Cin_real;
-    const int n = nc / a.Cin_real;
+    const int c = idx % a.Cin;
+    const int tn = idx / a.Cin;
+    const int n = tn % a.Cout_real;
+    const int t = tn / a.Cout_real;
+    if (c >= a.Cin_real) continue;
     const float* s = a.slab + (size_t)t * tile + (size_t)n * a.Cin + c;
-    float sum = 0.f;
-    for (int sp = 0; sp < a.nsplit; ++sp) sum += s[(size_t)sp * a.T * tile];
-    a.grad_w[idx] = a.beta * a.grad_w[idx] + a.scale * sum;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int sp = 0;
+    for (; sp + 4 <= a.nsplit; sp += 4) {
+      s0 += s[(size_t)sp * sstride];
+      s1 += s[(size_t)(sp + 1) * sstride];
+      s2 += s[(size_t)(sp + 2) * sstride];
+      s3 += s[(size_t)(sp + 3) * sstride];
+    }
+    for (; sp < a.nsplit; ++sp) s0 += s[(size_t)sp * sstride];
+    const float sum = (s0 + s1) + (s2 + s3);
+    float* g = a.grad_w + ((size_t)n * a.Cin_real + c) * a.T + t;
+    *g = a.beta * *g + a.scale * sum;
   }
   if (blockIdx.x == 0 && a.grad_b) {
     for (int n = threadIdx.x; n < a.Cout_real; n += blockDim.x) {
@@ -375,9 +388,9 @@ __global__ void conv_wgrad_reduce_kernel(WgradReduceArgs a) {
 }
 
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st) {
-  const int total = a.T * a.Cout_real * a.Cin_real;
+  const int total = a.T * a.Cout_real * a.Cin;
   int blocks = (total + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
 }
 

@@ -1,0 +1,158 @@
+"""Process-group setup and gradient collectives (RCCL over xGMI on MI355X).
+
+One process per GPU.  ``init_from_env`` reads RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT (torchrun convention) and initialises
+``torch.distributed`` with backend ``nccl`` (= RCCL on ROCm) when a GPU is
+present, ``gloo`` otherwise (CPU tests).
+
+The reference has no distributed machinery at all; data
+parallelism is new here.  Gradients live in one flat fp32 buffer laid out in
+*forward* layer order, so the buckets that become ready during backward
+(last layers first) are contiguous slices: each bucket is all-reduced as soon
+as its wgrad reductions are enqueued, on the RCCL stream, overlapping the
+remaining dgrad/wgrad kernels.  Bucket size defaults to ~4 MiB — a ring
+all-reduce over xGMI point-to-point links is per-link bound and 8-16 MB of
+total gradients per step gives only a few buckets, each large enough to use
+the links but small enough to start early.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistEnv:
+    rank: int = 0
+    local_rank: int = 0
+    world_size: int = 1
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_ENV: Optional[DistEnv] = None
+
+
+def init_from_env(device: str = "auto", timeout_s: float = 600.0) -> DistEnv:
+    """Initialise (once) from torchrun-style environment variables."""
+    global _ENV
+    if _ENV is not None:
+        return _ENV
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    use_gpu = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
+    if use_gpu:
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    backend = "none"
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        backend = "nccl" if use_gpu else "gloo"
+        kw = {}
+        if use_gpu:
+            kw["device_id"] = dev
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    _ENV = DistEnv(rank=rank, local_rank=local, world_size=world, backend=backend, device=dev)
+    return _ENV
+
+
+def env() -> DistEnv:
+    return _ENV or DistEnv()
+
+
+def shutdown() -> None:
+    global _ENV
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _ENV = None
+
+
+def barrier() -> None:
+    if dist.is_available() and dist.is_initialized():
+        if env().backend == "nccl":
+            dist.barrier(device_ids=[env().device.index])
+        else:
+            dist.barrier()
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if dist.is_available() and dist.is_initialized():
+        dist.broadcast(t, src)
+    return t
+
+
+def all_reduce_sum_(t: torch.Tensor) -> torch.Tensor:
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(t)
+    return t
+
+
+def all_reduce_max(value: float) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return value
+    dev = env().device if env().backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_buckets(segments: Sequence[Tuple[int, int]], bucket_bytes: int = 4 << 20,
+                 elem_bytes: int = 4) -> List[Tuple[int, int, List[int]]]:
+    """Group per-layer flat segments (offset, numel) — given in *backward*
+    order — into contiguous buckets.  Returns [(offset, numel, [segment ids])]."""
+    buckets: List[Tuple[int, int, List[int]]] = []
+    cur_lo = cur_hi = None
+    cur_ids: List[int] = []
+    for sid, (off, n) in enumerate(segments):
+        lo, hi = off, off + n
+        if cur_ids and (hi - lo + (cur_hi - cur_lo)) * elem_bytes > bucket_bytes:
+            buckets.append((cur_lo, cur_hi - cur_lo, cur_ids))
+            cur_ids, cur_lo, cur_hi = [], None, None
+        if not cur_ids:
+            cur_lo, cur_hi = lo, hi
+        else:
+            if hi != cur_lo and lo != cur_hi:
+                raise ValueError("segments are not contiguous in backward order")
+            cur_lo, cur_hi = min(cur_lo, lo), max(cur_hi, hi)
+        cur_ids.append(sid)
+    if cur_ids:
+        buckets.append((cur_lo, cur_hi - cur_lo, cur_ids))
+    return buckets
+
+
+class BucketAllReducer:
+    """Async per-bucket all-reduce of slices of a flat gradient buffer."""
+
+    def __init__(self, flat: torch.Tensor, buckets):
+        self.flat = flat
+        self.buckets = buckets
+        self.handles = []
+
+    def launch(self, bucket_idx: int) -> None:
+        if not (dist.is_available() and dist.is_initialized()):
+            return
+        off, n, _ = self.buckets[bucket_idx]
+        self.handles.append(dist.all_reduce(self.flat[off:off + n], async_op=True))
+
+    def wait(self) -> None:
+        for h in self.handles:
+            h.wait()
+        self.handles = []

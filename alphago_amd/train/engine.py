@@ -1,0 +1,347 @@
+"""Training-step engines for the policy network.
+
+``HipPolicyTrainer`` is the MI355X path.  One SL step (reference:
+supervised_policy_trainer.py:199-213, Keras ``train_on_batch`` + SGD) is a
+fixed sequence of hand-written kernels over preallocated buffers:
+
+  pack_input (uint8 planes -> padded NHWC bf16, per-board D4 symmetry, targets)
+  L x conv_fwd (implicit GEMM on MFMA, fused bias+ReLU)
+  policy_head (1x1 conv + softmax + clipped CE + top-1 + head backward)
+  for l = L..1:
+     [wgrad stream]  conv_wgrad(l) -> split slab -> reduce into the flat fp32 grad
+                     -> async RCCL all-reduce of the bucket once complete
+     [main stream]   conv_fwd in dgrad mode (flipped weights, ReLU' mask fused)
+  sgd (flat fp32 master) + pack_weights (bf16 forward and dgrad copies)
+
+dgrad and wgrad of a layer are independent and run on two HIP streams; the
+gradient all-reduce of a bucket overlaps the remaining backward.  Every
+activation and gradient has its own buffer (HBM is plentiful: ~2 GB at
+batch 512), so there are no cross-stream reuse hazards.
+
+``TorchPolicyTrainer`` is the same step with torch autograd (fp32 numerics
+oracle; CPU path for tests and the "32-filter 2-layer on CPU" config).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..models.nets import PolicyNet, ValueNet
+from ..parallel import dist as agdist
+
+# The 8 D4 symmetries as flat-index permutations (numpy semantics of the
+# reference BOARD_TRANSFORMATIONS, supervised_policy_trainer.py:71-80).
+_SYM_FWD = [
+    lambda n, x, y: (x, y),
+    lambda n, x, y: (n - 1 - y, x),
+    lambda n, x, y: (n - 1 - x, n - 1 - y),
+    lambda n, x, y: (y, n - 1 - x),
+    lambda n, x, y: (x, n - 1 - y),
+    lambda n, x, y: (n - 1 - x, y),
+    lambda n, x, y: (y, x),
+    lambda n, x, y: (n - 1 - y, n - 1 - x),
+]
+
+
+def symmetry_tables(n: int, device=None) -> torch.Tensor:
+    """(8, n*n) long: fwd[s][p] = index of point p after symmetry s."""
+    t = torch.empty(8, n * n, dtype=torch.long)
+    for s, f in enumerate(_SYM_FWD):
+        for x in range(n):
+            for y in range(n):
+                ox, oy = f(n, x, y)
+                t[s, x * n + y] = ox * n + oy
+    return t.to(device) if device is not None else t
+
+
+def apply_symmetry(planes: torch.Tensor, targets: Optional[torch.Tensor], sym: torch.Tensor, table: torch.Tensor):
+    """Torch implementation of the per-sample D4 augmentation (oracle for pack_input)."""
+    B, C, S, _ = planes.shape
+    fwd = table[sym.long()]  # (B, S*S)
+    inv = torch.argsort(fwd, dim=1)
+    flat = planes.reshape(B, C, S * S)
+    out = torch.gather(flat, 2, inv.unsqueeze(1).expand(B, C, S * S)).reshape(B, C, S, S)
+    tout = None
+    if targets is not None:
+        tl = targets.long()
+        tout = torch.where(tl >= 0, torch.gather(fwd, 1, tl.clamp_min(0).unsqueeze(1)).squeeze(1), tl)
+    return out, tout
+
+
+class FlatParams:
+    """fp32 master parameters and gradients, each in ONE flat device buffer.
+
+    Module parameters are re-bound to views of the flat buffer so the rest of
+    PyTorch (save/load, eval) sees ordinary parameters."""
+
+    def __init__(self, named: Sequence[Tuple[str, torch.nn.Parameter]], device):
+        self.names = [n for n, _ in named]
+        sizes = [p.numel() for _, p in named]
+        total = (sum(sizes) + 3) // 4 * 4
+        self.flat = torch.zeros(total, device=device, dtype=torch.float32)
+        self.grad = torch.zeros(total, device=device, dtype=torch.float32)
+        self.segments: Dict[str, Tuple[int, int]] = {}
+        self.views: Dict[str, torch.Tensor] = {}
+        self.grad_views: Dict[str, torch.Tensor] = {}
+        off = 0
+        for (name, p), n in zip(named, sizes):
+            v = self.flat[off:off + n].view(p.shape)
+            v.copy_(p.data.to(device))
+            p.data = v
+            self.segments[name] = (off, n)
+            self.views[name] = v
+            self.grad_views[name] = self.grad[off:off + n].view(p.shape)
+            off += n
+        self.numel = off
+
+
+class KerasSGDSchedule:
+    """Keras 1.0 SGD learning rate: lr / (1 + decay * iterations), momentum 0."""
+
+    def __init__(self, lr: float, decay: float = 0.0, iterations: int = 0):
+        self.lr, self.decay, self.iterations = lr, decay, iterations
+
+    def current(self) -> float:
+        return self.lr / (1.0 + self.decay * self.iterations)
+
+    def advance(self) -> None:
+        self.iterations += 1
+
+
+class HipPolicyTrainer:
+    def __init__(self, net: PolicyNet, batch: int, lr: float = 0.003, decay: float = 0.0,
+                 device=None, bucket_mb: float = 4.0, overlap: bool = True, wgrad_target_wgs: int = 512,
+                 iterations: int = 0):
+        ops.load()
+        self.env = agdist.env()
+        self.device = torch.device(device) if device is not None else self.env.device
+        if self.device.type != "cuda":
+            raise RuntimeError("HipPolicyTrainer needs a GPU device")
+        self.net = net.to(self.device)
+        self.batch = batch
+        self.sched = KerasSGDSchedule(lr, decay, iterations)
+        self.overlap = overlap
+        tr = net.trunk
+        self.S = net.board
+        self.L = tr.layers
+        self.K = list(tr.widths)
+        self.C0 = tr.in_planes
+        self.C0p = ops.round_up(self.C0, 64)
+        self.F = tr.filters
+        self.Fp = ops.round_up(self.F, 64)
+        if self.F > 256:
+            raise ValueError("policy head kernel supports up to 256 filters")
+        self.P0 = self.K[0] // 2
+        named = []
+        for l in range(self.L):
+            named.append(("w%d" % l, tr.weights[l]))
+            named.append(("b%d" % l, tr.biases[l]))
+        named += [("head_w", net.head_w), ("head_b", net.head_b)]
+        self.fp = FlatParams(named, self.device)
+        if self.env.distributed:
+            agdist.broadcast_(self.fp.flat, 0)
+        dev, B, S = self.device, batch, self.S
+        # padded biases (Fp) for the epilogue
+        self.bias_p = [torch.zeros(self.Fp, device=dev) for _ in range(self.L)]
+        self.wf, self.wd = [], []
+        for l in range(self.L):
+            cin_p = self.C0p if l == 0 else self.Fp
+            w = self.fp.views["w%d" % l]
+            self.wf.append(ops.packed_weight_like(w, cin_p, self.Fp))
+            self.wd.append(ops.packed_weight_like(w, cin_p, self.Fp, transposed=True) if l > 0
+                           else torch.empty(0, device=dev, dtype=torch.bfloat16))
+        # activations / gradients (zero borders are never written)
+        self.X0 = ops.padded_empty(B, S, self.P0, self.C0p, dev)
+        self.Y = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(self.L)]
+        self.DZ = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(self.L)]
+        self.loss = torch.zeros(B, device=dev)
+        self.correct = torch.zeros(B, device=dev)
+        self.dhead = torch.zeros(B, self.F + 1, device=dev)
+        self.tgt = torch.zeros(B, dtype=torch.int32, device=dev)
+        M = B * S * S
+        self.nsplit = []
+        slab_max, db_max = 0, 0
+        for l in range(self.L):
+            cin_p = self.C0p if l == 0 else self.Fp
+            T = self.K[l] ** 2
+            tiles = max(1, (self.Fp // (192 if self.Fp % 192 == 0 else 128 if self.Fp % 128 == 0 else 64))
+                        * (cin_p // (192 if cin_p % 192 == 0 else 128 if cin_p % 128 == 0 else 64)))
+            ns = ops.wgrad_splits(M, T, tiles, wgrad_target_wgs)
+            self.nsplit.append(ns)
+            slab_max = max(slab_max, ns * T * self.Fp * cin_p)
+            db_max = max(db_max, ns * self.Fp)
+        self._slab = torch.empty(slab_max, device=dev)
+        self._dbslab = torch.zeros(db_max, device=dev)
+        self.s_w = torch.cuda.Stream(device=dev) if overlap else None
+        # buckets over the flat grad, segments in backward order
+        segs = [(self.fp.segments["head_w"][0], self.fp.segments["head_w"][1] + self.fp.segments["head_b"][1])]
+        self._seg_layer = [None]
+        for l in reversed(range(self.L)):
+            ow, nw = self.fp.segments["w%d" % l]
+            _, nb = self.fp.segments["b%d" % l]
+            segs.append((ow, nw + nb))
+            self._seg_layer.append(l)
+        self.buckets = agdist.make_buckets(segs, int(bucket_mb * (1 << 20)))
+        self._bucket_after_layer = {}
+        for bi, (_, _, ids) in enumerate(self.buckets):
+            last = ids[-1]
+            self._bucket_after_layer[self._seg_layer[last] if self._seg_layer[last] is not None else -1] = bi
+        self.reducer = agdist.BucketAllReducer(self.fp.grad, self.buckets)
+        self.repack()
+
+    # ------------------------------------------------------------------ helpers
+    def repack(self) -> None:
+        for l in range(self.L):
+            self.bias_p[l][:self.F].copy_(self.fp.views["b%d" % l])
+        ops.pack_weights([self.fp.views["w%d" % l] for l in range(self.L)], self.wf, self.wd)
+
+    def _layer_in(self, l):
+        return (self.X0, self.P0) if l == 0 else (self.Y[l - 1], 1)
+
+    def forward_trunk(self, planes: torch.Tensor, sym=None, targets=None) -> None:
+        ops.pack_input(planes, self.X0, self.P0, sym=sym, target=targets, target_out=self.tgt if targets is not None else None)
+        for l in range(self.L):
+            x, pin = self._layer_in(l)
+            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1)
+
+    def _wgrad_layer(self, l: int) -> None:
+        x, pin = self._layer_in(l)
+        T = self.K[l] ** 2
+        cin_p = x.shape[3]
+        ns = self.nsplit[l]
+        slab = self._slab[:ns * T * self.Fp * cin_p].view(ns, T, self.Fp, cin_p)
+        dbs = self._dbslab[:ns * self.Fp].view(ns, self.Fp)
+        ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1)
+        ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)
+
+    def compute_grads(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None):
+        """Forward + backward into self.fp.grad (all-reduced when distributed)."""
+        B = planes.shape[0]
+        if B != self.batch:
+            raise ValueError("batch %d != configured %d" % (B, self.batch))
+        main = torch.cuda.current_stream(self.device)
+        self.forward_trunk(planes, sym, targets)
+        gscale = 1.0 / (B * self.env.world_size)
+        hw = self.fp.views["head_w"].view(-1)
+        hb = self.fp.views["head_b"]
+        ops.policy_head_train(self.Y[-1], hw, hb, self.tgt, self.DZ[-1], self.loss, self.correct, self.dhead,
+                              self.S, gscale)
+        ho, hn = self.fp.segments["head_w"]
+        torch.sum(self.dhead, dim=0, out=self.fp.grad[ho:ho + hn + 1])
+        if -1 in self._bucket_after_layer:
+            self._launch_bucket(self._bucket_after_layer[-1], main)
+        for l in reversed(range(self.L)):
+            if self.s_w is not None:
+                ev = main.record_event()
+                with torch.cuda.stream(self.s_w):
+                    self.s_w.wait_event(ev)
+                    self._wgrad_layer(l)
+                    if l in self._bucket_after_layer:
+                        self.reducer.launch(self._bucket_after_layer[l])
+            else:
+                self._wgrad_layer(l)
+                if l in self._bucket_after_layer:
+                    self.reducer.launch(self._bucket_after_layer[l])
+            if l > 0:
+                ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
+                             mode=ops.MODE_MASK, mask=self.Y[l - 1])
+        if self.s_w is not None:
+            main.wait_stream(self.s_w)
+        self.reducer.wait()
+
+    def _launch_bucket(self, bi, stream):
+        self.reducer.launch(bi)
+
+    def step(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None):
+        """One SGD step.  Returns (sum of per-board loss, number correct) as device scalars (local)."""
+        self.compute_grads(planes, targets, sym)
+        ops.sgd_update(self.fp.flat, self.fp.grad, self.sched.current(), 1.0)
+        self.sched.advance()
+        self.repack()
+        return self.loss.sum(), self.correct.sum()
+
+    @torch.no_grad()
+    def evaluate(self, planes: torch.Tensor, targets: torch.Tensor):
+        """Loss/accuracy without update (validation)."""
+        self.forward_trunk(planes, None, targets)
+        hw = self.fp.views["head_w"].view(-1)
+        ops.policy_head_train(self.Y[-1], hw, self.fp.views["head_b"], self.tgt, self.DZ[-1], self.loss,
+                              self.correct, self.dhead, self.S, 0.0)
+        return self.loss.sum(), self.correct.sum()
+
+
+class TorchPolicyTrainer:
+    """Autograd implementation of the same SL step (fp32 by default)."""
+
+    def __init__(self, net: PolicyNet, batch: int, lr: float = 0.003, decay: float = 0.0, device=None,
+                 dtype=torch.float32, iterations: int = 0):
+        self.env = agdist.env()
+        self.device = torch.device(device) if device is not None else self.env.device
+        self.net = net.to(self.device)
+        self.batch = batch
+        self.dtype = dtype
+        self.sched = KerasSGDSchedule(lr, decay, iterations)
+        named = []
+        tr = net.trunk
+        for l in range(tr.layers):
+            named.append(("w%d" % l, tr.weights[l]))
+            named.append(("b%d" % l, tr.biases[l]))
+        named += [("head_w", net.head_w), ("head_b", net.head_b)]
+        self.params = [p for _, p in named]
+        self.fp = FlatParams(named, self.device)
+        if self.env.distributed:
+            agdist.broadcast_(self.fp.flat, 0)
+        self.table = symmetry_tables(net.board, self.device)
+
+    def _loss(self, planes, targets, sym):
+        if sym is not None:
+            planes, targets = apply_symmetry(planes, targets, sym, self.table)
+        x = planes.to(self.dtype)
+        logits = self.net.logits_torch(x)
+        t = targets.long()
+        valid = t >= 0
+        logp = torch.log_softmax(logits, 1)
+        lt = logp.gather(1, t.clamp_min(0).unsqueeze(1)).squeeze(1)
+        per = -torch.clamp(lt, min=math.log(1e-7), max=math.log(1 - 1e-7)) * valid
+        correct = ((logits.argmax(1) == t) & valid).float()
+        # gradient of mean CE (unclipped, see kernels/head.hip)
+        obj = (-(lt * valid)).sum() / (planes.shape[0] * self.env.world_size)
+        return obj, per, correct
+
+    def compute_grads(self, planes, targets, sym=None):
+        for p in self.params:
+            p.grad = None
+        obj, per, correct = self._loss(planes, targets, sym)
+        obj.backward()
+        for (name, p) in zip(self.fp.names, self.params):
+            self.fp.grad_views[name].copy_(p.grad)
+        if self.env.distributed:
+            agdist.all_reduce_sum_(self.fp.grad)
+        self._last = (per.detach(), correct.detach())
+
+    def step(self, planes, targets, sym=None):
+        self.compute_grads(planes, targets, sym)
+        with torch.no_grad():
+            self.fp.flat.add_(self.fp.grad, alpha=-self.sched.current())
+        self.sched.advance()
+        per, correct = self._last
+        return per.sum(), correct.sum()
+
+    @torch.no_grad()
+    def evaluate(self, planes, targets):
+        obj, per, correct = self._loss(planes, targets, None)
+        return per.sum(), correct.sum()
+
+
+def make_policy_trainer(net: PolicyNet, batch: int, lr: float, decay: float = 0.0, backend: str = "auto",
+                        device=None, **kw):
+    dev = torch.device(device) if device is not None else agdist.env().device
+    if backend == "auto":
+        backend = "hip" if dev.type == "cuda" else "torch"
+    if backend == "hip":
+        return HipPolicyTrainer(net, batch, lr, decay, device=dev, **kw)
+    return TorchPolicyTrainer(net, batch, lr, decay, device=dev)

@@ -1,0 +1,125 @@
+#!/usr/bin/env python
+"""Headline benchmark: SL policy-network training throughput.
+
+Metric (BASELINE.json): SL-policy positions/sec for the whole node (+ top-1
+move accuracy) on the 19x19, 12-layer, 192-filter, 48-plane policy network
+(reference CNNPolicy architecture, policy.py:93-156; paper size), bf16 compute
+with fp32 master weights, SGD with Keras decay, per-board random D4
+augmentation, on synthetic positions and random-init weights (no datasets or
+checkpoints are reachable offline).
+
+Single GPU:   python bench.py --steps 20 --warmup 5
+N GPUs:       python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+                  --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+Weak scaling: the per-GPU batch is fixed; the global batch is N x per-GPU batch.
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from alphago_amd.models.nets import PolicyNet  # noqa: E402
+from alphago_amd.parallel import dist as agdist  # noqa: E402
+from alphago_amd.train.engine import make_policy_trainer  # noqa: E402
+
+PAPER_SL_POS_PER_S = 3000.0  # paper SL throughput, 50 GPUs aggregate (derived)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024, help="per-GPU minibatch (boards)")
+    ap.add_argument("--filters", type=int, default=192)
+    ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--planes", type=int, default=48)
+    ap.add_argument("--lr", type=float, default=0.003)
+    ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--pool", type=int, default=16384, help="synthetic positions resident on device")
+    ap.add_argument("--no-overlap", action="store_true")
+    args = ap.parse_args()
+
+    env = agdist.init_from_env()
+    dev = env.device
+    torch.manual_seed(1234 + env.rank)
+    net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
+    kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap}
+    trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
+
+    # synthetic dataset, resident in HBM (uint8 one-hot planes + move targets)
+    g = torch.Generator(device=dev)
+    g.manual_seed(99 + env.rank)
+    pool = torch.randint(0, 2, (args.pool, args.planes, 19, 19), device=dev, dtype=torch.uint8, generator=g)
+    pool_tgt = torch.randint(0, 361, (args.pool,), device=dev, dtype=torch.int32, generator=g)
+
+    def batch():
+        idx = torch.randint(0, args.pool, (args.batch,), device=dev, generator=g)
+        sym = torch.randint(0, 8, (args.batch,), device=dev, dtype=torch.int32, generator=g)
+        return pool.index_select(0, idx), pool_tgt.index_select(0, idx), sym
+
+    for _ in range(args.warmup):
+        trainer.step(*batch())
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    agdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss_sum = torch.zeros((), device=dev)
+    corr_sum = torch.zeros((), device=dev)
+    for _ in range(args.steps):
+        l, c = trainer.step(*batch())
+        loss_sum += l
+        corr_sum += c
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    agdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = agdist.all_reduce_max(dt)
+    n = env.world_size
+    stats = torch.stack([loss_sum, corr_sum]).double()
+    agdist.all_reduce_sum_(stats)
+    positions = args.batch * n * args.steps
+    value = positions / dt
+    if env.is_main:
+        out = {
+            "metric": "SL-policy positions/sec (whole node) + top-1 move acc, 19x19 12-layer net",
+            "value": round(value, 1),
+            "unit": "positions/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / PAPER_SL_POS_PER_S, 2),
+            "dtype": "bf16",
+            "data": "synthetic (random uint8 planes/targets, random-init weights)",
+            "top1_acc": round(float(stats[1]) / positions, 4),
+            "mean_loss": round(float(stats[0]) / positions, 4),
+            "tflops": round(net.flops_per_position() * 3 * value / 1e12, 1),
+            "config": {
+                "model": "SL policy net (%d-layer, %d filters, %d planes)" % (args.layers, args.filters, args.planes),
+                "global_batch": args.batch * n,
+                "per_gpu_batch": args.batch,
+                "seq_len": 361,
+                "parallelism": "dp%d" % n,
+                "backend": args.backend,
+                "baseline": "paper SL throughput ~3.0k pos/s (50 GPUs), BASELINE.md (A)",
+            },
+        }
+        print(json.dumps(out), flush=True)
+    agdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,48 @@
+"""Per-kernel microbenchmark of the SL-step kernels at a given batch (standalone, no overlap)."""
+import argparse, json
+import torch
+from alphago_amd import ops
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=1024)
+ap.add_argument("--F", type=int, default=192)
+ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--splits", default="")
+a = ap.parse_args()
+ops.load()
+dev = torch.device("cuda")
+B, F, S = a.batch, a.F, 19
+M = B * S * S
+x = ops.padded_empty(B, S, 1, F, dev); x[:, 1:20, 1:20].normal_()
+x0 = ops.padded_empty(B, S, 2, 64, dev); x0[:, 2:21, 2:21].bernoulli_(torch.full_like(x0[:, 2:21, 2:21], 0.5, dtype=torch.float32).to(torch.bfloat16))
+y = ops.padded_empty(B, S, 1, F, dev)
+w = torch.randn(F, F, 3, 3, device=dev) * 0.05
+w1 = torch.randn(F, 48, 5, 5, device=dev) * 0.05
+wf = ops.packed_weight_like(w, F, F); wd = ops.packed_weight_like(w, F, F, True)
+wf1 = ops.packed_weight_like(w1, 64, F)
+ops.pack_weights([w, w1], [wf, wf1], [wd, torch.empty(0, device=dev, dtype=torch.bfloat16)])
+bias = torch.zeros(F, device=dev)
+gw = torch.zeros(F, F, 3, 3, device=dev); gb = torch.zeros(F, device=dev)
+
+def timeit(fn):
+    for _ in range(3): fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.iters): fn()
+    e1.record(); torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / a.iters * 1e3  # us
+
+res = {}
+fl3 = 2.0 * M * F * F * 9
+fl1 = 2.0 * M * F * 64 * 25
+res["fwd3x3"] = timeit(lambda: ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1))
+res["fwd5x5"] = timeit(lambda: ops.conv_fwd(x0, wf1, bias, y, 5, S, 2, 1))
+res["dgrad3x3"] = timeit(lambda: ops.conv_fwd(x, wd, None, y, 3, S, 1, 1, mode=ops.MODE_MASK, mask=x))
+splits = [int(s) for s in a.splits.split(",")] if a.splits else [ops.wgrad_splits(M, 9)]
+for ns in splits:
+    slab = torch.empty(ns, 9, F, F, device=dev); dbs = torch.zeros(ns, F, device=dev)
+    res["wgrad3x3_s%d" % ns] = timeit(lambda: ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1))
+    res["reduce_s%d" % ns] = timeit(lambda: ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0))
+out = {k: {"us": round(v, 1), "TF": round((fl1 if "5x5" in k else fl3) / (v * 1e-6) / 1e12, 1) if "reduce" not in k else None} for k, v in res.items()}
+print(json.dumps({"batch": B, "F": F, **out}))

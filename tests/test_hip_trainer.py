@@ -1,0 +1,54 @@
+"""Full HIP SL step vs the autograd fp32 step (same init, same batch/symmetries)."""
+import copy
+
+import pytest
+import torch
+
+from alphago_amd.models.nets import PolicyNet
+from alphago_amd.train.engine import HipPolicyTrainer, TorchPolicyTrainer
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("F,L,C,B", [(64, 3, 48, 6), (192, 4, 48, 5), (128, 2, 12, 3)])
+def test_hip_grads_match_torch(cuda_device, F, L, C, B):
+    torch.manual_seed(0)
+    net = PolicyNet(C, filters_per_layer=F, layers=L)
+    net_ref = copy.deepcopy(net)
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    sym = torch.randint(0, 8, (B,), dtype=torch.int32, device=cuda_device)
+    hip = HipPolicyTrainer(net, B, lr=0.01, device=cuda_device)
+    ref = TorchPolicyTrainer(net_ref, B, lr=0.01, device=cuda_device)
+    hip.compute_grads(planes, tgt, sym)
+    ref.compute_grads(planes, tgt, sym)
+    torch.cuda.synchronize()
+    for name in hip.fp.names:
+        a, b = hip.fp.grad_views[name], ref.fp.grad_views[name]
+        if name == "head_b":  # d(mean CE)/d(scalar logit bias) == 0 exactly (softmax shift invariance)
+            assert abs(a.item()) < 1e-5 and abs(b.item()) < 1e-5
+            continue
+        # bf16 activations/weights through a chain of dgrad layers: compare
+        # direction and magnitude (per-kernel 1e-2 checks are in test_hip_kernels)
+        cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
+        ratio = a.norm().item() / max(b.norm().item(), 1e-12)
+        assert cos > 0.99 and abs(ratio - 1) < 0.05, (name, cos, ratio)
+    # loss / accuracy bookkeeping
+    assert torch.allclose(hip.loss, ref._last[0], rtol=2e-2, atol=2e-2)
+
+
+def test_hip_step_reduces_loss(cuda_device):
+    torch.manual_seed(1)
+    B = 32
+    net = PolicyNet(48, filters_per_layer=64, layers=3)
+    tr = HipPolicyTrainer(net, B, lr=0.5, device=cuda_device)
+    planes = torch.randint(0, 2, (B, 48, 19, 19), dtype=torch.uint8, device=cuda_device)
+    tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    l0, _ = tr.evaluate(planes, tgt)
+    l0 = l0.item()
+    for _ in range(20):
+        tr.step(planes, tgt)
+    l1, _ = tr.evaluate(planes, tgt)
+    assert l1.item() < l0
+    # module parameters are views of the trained flat buffer
+    assert torch.equal(net.head_w.detach().view(-1), tr.fp.views["head_w"].view(-1))
