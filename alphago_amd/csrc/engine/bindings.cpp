@@ -14,6 +14,10 @@
 namespace py = pybind11;
 using namespace ag;
 
+namespace ag {
+void bind_lzf(py::module_& m);
+}
+
 static int to_idx(const GameState& s, const py::object& a) {
   if (a.is_none()) return PASS;
   auto t = a.cast<std::pair<int, int>>();
@@ -199,4 +203,5 @@ PYBIND11_MODULE(_engine, m) {
       py::arg("states"), py::arg("features"), py::arg("threads") = 8);
 
   bind_mcts(m);
+  bind_lzf(m);
 }
