@@ -1,0 +1,214 @@
+"""Batched network evaluation for play, search and self-play.
+
+On a GPU the whole forward (uint8 planes -> padded NHWC bf16 -> L x MFMA conv
+-> fused head/softmax with legal-move renormalisation) is captured once per
+batch bucket into a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and
+replayed: a search step is one H2D copy, one graph launch and one D2H copy,
+instead of ~15 kernel launches.  Batches are padded up to the next bucket.
+
+Reference paths replaced: CNNPolicy.forward / batch_eval_state
+(policy.py:26-79) which featurised in Python and ran a Theano function per
+call; MCTS policy/value callables (mcts.py:107-118).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from .nets import PolicyNet, ValueNet
+
+DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024)
+
+
+class _Bucket:
+    pass
+
+
+class HipTrunkInference:
+    """Forward-only runner of a ConvStack (+ head) on the HIP kernels."""
+
+    def __init__(self, net, device, buckets: Sequence[int] = DEFAULT_BUCKETS, use_graphs: bool = True):
+        ops.load()
+        self.net = net
+        self.device = torch.device(device)
+        tr = net.trunk
+        self.S, self.L, self.K = net.board, tr.layers, list(tr.widths)
+        self.C0, self.F = tr.in_planes, tr.filters
+        self.C0p, self.Fp = ops.round_up(self.C0, 64), ops.round_up(self.F, 64)
+        self.P0 = self.K[0] // 2
+        self.buckets = sorted(buckets)
+        self.use_graphs = use_graphs
+        dev = self.device
+        self.wf = [ops.packed_weight_like(tr.weights[l], self.C0p if l == 0 else self.Fp, self.Fp)
+                   for l in range(self.L)]
+        self.bias_p = [torch.zeros(self.Fp, device=dev) for _ in range(self.L)]
+        self.head_w = torch.zeros(self.F, device=dev)
+        self.head_b = torch.zeros(1, device=dev)
+        self._b: Dict[int, _Bucket] = {}
+        self.sync_weights()
+
+    @torch.no_grad()
+    def sync_weights(self) -> None:
+        tr = self.net.trunk
+        ws = [w.detach().to(self.device, torch.float32).contiguous() for w in tr.weights]
+        ops.pack_weights(ws, self.wf)
+        for l in range(self.L):
+            self.bias_p[l][:self.F].copy_(tr.biases[l].detach())
+        self.head_w.copy_(self.net.head_w.detach().view(-1))
+        self.head_b.copy_(self.net.head_b.detach().view(-1))
+        self._after_sync()
+
+    def _after_sync(self):
+        pass
+
+    def bucket_for(self, n: int) -> int:
+        for b in self.buckets:
+            if b >= n:
+                return b
+        return ops.round_up(n, self.buckets[-1])
+
+    def _make_bucket(self, B: int) -> _Bucket:
+        dev, S = self.device, self.S
+        bk = _Bucket()
+        bk.B = B
+        bk.planes = torch.zeros((B, self.C0, S, S), dtype=torch.uint8, device=dev)
+        bk.legal = torch.ones((B, S * S), dtype=torch.uint8, device=dev)
+        bk.X0 = ops.padded_empty(B, S, self.P0, self.C0p, dev)
+        bk.Y = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(2)]
+        self._alloc_outputs(bk)
+        bk.graph = None
+        return bk
+
+    def _alloc_outputs(self, bk):
+        bk.probs = torch.zeros((bk.B, self.S * self.S), device=self.device)
+
+    def _trunk(self, bk) -> torch.Tensor:
+        ops.pack_input(bk.planes, bk.X0, self.P0)
+        x, pin = bk.X0, self.P0
+        for l in range(self.L):
+            y = bk.Y[l % 2]
+            ops.conv_fwd(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1)
+            x, pin = y, 1
+        return x
+
+    def _head(self, bk, y):
+        ops.policy_head_probs(y, self.head_w, self.head_b, bk.probs, self.S, legal=bk.legal)
+
+    def _run(self, bk):
+        self._head(bk, self._trunk(bk))
+
+    def _get(self, n: int) -> _Bucket:
+        B = self.bucket_for(n)
+        if B not in self._b:
+            bk = self._make_bucket(B)
+            self._b[B] = bk
+            if self.use_graphs:
+                s = torch.cuda.Stream(device=self.device)
+                s.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(s):
+                    self._run(bk)  # warm-up (also sets kernel attributes outside capture)
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._run(bk)
+                bk.graph = g
+        return self._b[B]
+
+    @torch.no_grad()
+    def evaluate(self, planes, legal=None):
+        """planes: (n, C, S, S) uint8 (numpy or tensor); legal: (n, S*S) uint8 or None.
+        Returns the bucket's output tensors (views of the first n rows)."""
+        n = planes.shape[0]
+        bk = self._get(n)
+        src = torch.as_tensor(planes)
+        bk.planes[:n].copy_(src, non_blocking=True)
+        if n < bk.B:
+            bk.planes[n:].zero_()
+        if legal is not None:
+            bk.legal[:n].copy_(torch.as_tensor(legal), non_blocking=True)
+            if n < bk.B:
+                bk.legal[n:].fill_(1)
+        else:
+            bk.legal.fill_(1)
+        if bk.graph is not None:
+            bk.graph.replay()
+        else:
+            self._run(bk)
+        return self._outputs(bk, n)
+
+    def _outputs(self, bk, n):
+        return bk.probs[:n]
+
+
+class HipValueInference(HipTrunkInference):
+    """Value net: HIP trunk, then the (tiny) 1x1 conv + Dense(256) + Dense(1)+tanh head."""
+
+    def __init__(self, net: ValueNet, device, **kw):
+        self.fc = None
+        super().__init__(net, device, **kw)
+
+    def _after_sync(self):
+        n = self.net
+        self.fc = [t.detach().to(self.device, torch.float32).clone() for t in (n.fc1_w, n.fc1_b, n.fc2_w, n.fc2_b)]
+
+    def _alloc_outputs(self, bk):
+        bk.values = torch.zeros((bk.B,), device=self.device)
+
+    def _head(self, bk, y):
+        S, F = self.S, self.F
+        inner = y[:, 1:S + 1, 1:S + 1, :F].float().reshape(bk.B, S * S, F)
+        z = inner @ self.head_w + self.head_b  # (B, 361)
+        w1, b1, w2, b2 = self.fc
+        h = z @ w1 + b1
+        torch.tanh(h @ w2 + b2, out=bk.values.view(bk.B, 1))
+
+    def _outputs(self, bk, n):
+        return bk.values[:n]
+
+
+class TorchPolicyInference:
+    """CPU / reference path with the same interface."""
+
+    def __init__(self, net: PolicyNet, device="cpu"):
+        self.net, self.device = net, torch.device(device)
+
+    def sync_weights(self):
+        pass
+
+    @torch.no_grad()
+    def evaluate(self, planes, legal=None):
+        x = torch.as_tensor(planes).to(self.device)
+        logits = self.net.logits_torch(x.float())
+        if legal is not None:
+            logits = logits.masked_fill(torch.as_tensor(legal).to(self.device) == 0, float("-inf"))
+        p = torch.softmax(logits, 1)
+        return torch.nan_to_num(p, nan=0.0)
+
+
+class TorchValueInference:
+    def __init__(self, net: ValueNet, device="cpu"):
+        self.net, self.device = net, torch.device(device)
+
+    def sync_weights(self):
+        pass
+
+    @torch.no_grad()
+    def evaluate(self, planes, legal=None):
+        return self.net.forward_torch(torch.as_tensor(planes).to(self.device).float())
+
+
+def make_policy_inference(net, device, **kw):
+    device = torch.device(device)
+    if device.type == "cuda":
+        return HipTrunkInference(net, device, **kw)
+    return TorchPolicyInference(net, device)
+
+
+def make_value_inference(net, device, **kw):
+    device = torch.device(device)
+    if device.type == "cuda":
+        return HipValueInference(net, device, **kw)
+    return TorchValueInference(net, device)

@@ -1,0 +1,83 @@
+"""Players (reference AlphaGo/ai.py) + an MCTS player.
+
+GreedyPolicyPlayer / ProbabilisticPolicyPlayer keep the reference semantics
+(ai.py:6-68): only "sensible" moves (legal and not filling an own true eye),
+pass when none; probabilistic play samples p**(1/T).  ``get_moves`` evaluates
+a list of states in ONE batched forward.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+
+from .. import go
+
+
+def sensible_moves(state) -> List:
+    return [m for m in state.get_legal_moves() if not state.is_eye(m, state.current_player)]
+
+
+class GreedyPolicyPlayer(object):
+    def __init__(self, policy_function):
+        self.policy = policy_function
+
+    def get_move(self, state):
+        moves = sensible_moves(state)
+        if moves:
+            probs = self.policy.eval_state(state, moves)
+            return max(probs, key=lambda ap: ap[1])[0]
+        return go.PASS_MOVE
+
+    def get_moves(self, states):
+        lists = [sensible_moves(st) for st in states]
+        dists = self.policy.batch_eval_state(states, lists)
+        return [max(d, key=lambda ap: ap[1])[0] if d else go.PASS_MOVE for d in dists]
+
+
+class ProbabilisticPolicyPlayer(object):
+    def __init__(self, policy_function, temperature: float = 1.0, rng: Optional[np.random.Generator] = None):
+        assert temperature > 0.0
+        self.policy = policy_function
+        self.beta = 1.0 / temperature
+        self.rng = rng or np.random.default_rng()
+
+    def _sample(self, move_probs):
+        moves, p = zip(*move_probs)
+        p = np.asarray(p, dtype=np.float64) ** self.beta
+        s = p.sum()
+        p = p / s if s > 0 else np.full(len(p), 1.0 / len(p))
+        return moves[self.rng.choice(len(moves), p=p)]
+
+    def get_move(self, state):
+        moves = sensible_moves(state)
+        if moves:
+            return self._sample(self.policy.eval_state(state, moves))
+        return go.PASS_MOVE
+
+    def get_moves(self, states):
+        lists = [sensible_moves(st) for st in states]
+        dists = self.policy.batch_eval_state(states, lists)
+        return [self._sample(d) if d else go.PASS_MOVE for d in dists]
+
+
+class MCTSPlayer(object):
+    """Plays the most visited move of a batched PUCT search (see search.mcts)."""
+
+    def __init__(self, policy, value=None, n_playout: int = 1600, c_puct: float = 5.0, lmbda: float = 0.0,
+                 leaves_per_batch: int = 16, temperature: float = 0.0, seed: int = 0):
+        from .mcts import BatchedMCTS
+
+        self.search = BatchedMCTS(policy, value, n_trees=1, c_puct=c_puct, lmbda=lmbda, seed=seed)
+        self.n_playout = n_playout
+        self.leaves_per_batch = leaves_per_batch
+        self.temperature = temperature
+
+    def get_move(self, state):
+        if not sensible_moves(state):
+            return go.PASS_MOVE
+        return self.search.search([state], self.n_playout, self.leaves_per_batch, self.temperature)[0]
+
+    def get_moves(self, states):
+        self.search.resize(len(states))
+        return self.search.search(states, self.n_playout, self.leaves_per_batch, self.temperature)

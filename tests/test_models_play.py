@@ -1,0 +1,184 @@
+"""Model API, Keras-format persistence, players, MCTS and GTP (CPU; spec: reference
+tests/test_policy.py, test_mcts.py, test_gtp_wrapper.py)."""
+import io
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from alphago_amd import go
+from alphago_amd.gtp.engine import GTPEngine, format_vertex, parse_vertex, run_gtp
+from alphago_amd.io import keras_compat
+from alphago_amd.models.policy import CNNPolicy, CNNValue
+from alphago_amd.search.mcts import MCTS, BatchedMCTS
+from alphago_amd.search.players import GreedyPolicyPlayer, MCTSPlayer, ProbabilisticPolicyPlayer
+
+CPU = torch.device("cpu")
+FEATS = ["board", "ones", "turns_since"]
+REF_MINI = "/root/reference/tests/test_data/minimodel.json"
+
+
+def small_policy(board=19):
+    return CNNPolicy(FEATS, board=board, filters_per_layer=8, layers=2, device=CPU)
+
+
+def test_forward_shapes():
+    p = small_policy()
+    gs = go.GameState()
+    out = p.batch_eval_state([gs, gs])
+    assert len(out) == 2 and len(out[0]) == 361
+    assert abs(sum(pr for _, pr in out[0]) - 1) < 1e-5
+    assert p.forward(p.preprocessor.states_to_uint8([gs])).shape == (1, 361)
+    p13 = small_policy(13)
+    assert p13.forward(p13.preprocessor.states_to_uint8([go.GameState(13)])).shape == (1, 169)
+
+
+def test_save_load_roundtrip(tmp_path):
+    p = small_policy()
+    j, w = str(tmp_path / "m.json"), str(tmp_path / "w.hdf5")
+    p.save_model(j, w)
+    q = CNNPolicy.load_model(j, device=CPU)
+    x = p.preprocessor.states_to_uint8([go.GameState()])
+    assert np.allclose(p.forward(x), q.forward(x))
+    # separate weights
+    p.save_model(str(tmp_path / "m2.json"))
+    p.save_weights(str(tmp_path / "w2.hdf5"))
+    r = CNNPolicy.load_model(str(tmp_path / "m2.json"), device=CPU)
+    r.load_weights(str(tmp_path / "w2.hdf5"))
+    assert np.allclose(p.forward(x), r.forward(x))
+    spec = json.load(open(j))
+    assert spec["feature_list"] == FEATS and "keras_model" in spec
+
+
+def test_kernel_flip_convention(tmp_path):
+    """Saved conv kernels use the Theano (flipped) orientation."""
+    p = small_policy()
+    w = str(tmp_path / "w.hdf5")
+    p.save_weights(w)
+    from alphago_amd.io.h5lite import H5File
+    with H5File(w) as f:
+        names = [n.decode() for n in f.attrs["layer_names"]]
+        assert names[-2:] == ["flatten_1", "activation_1"]
+        k = f["convolution2d_1/convolution2d_1_W"].read()
+    ours = p.model.trunk.weights[0].detach().numpy()
+    assert np.allclose(k, ours[:, :, ::-1, ::-1])
+
+
+@pytest.mark.skipif(not os.path.exists(REF_MINI), reason="reference fixture absent")
+def test_load_reference_keras_spec():
+    p = CNNPolicy.load_model(REF_MINI, device=CPU)
+    assert p.preprocessor.output_dim == 12
+    assert p.model.trunk.layers == 5 and p.model.trunk.filters == 16
+    assert p.model.trunk.widths == [5, 3, 3, 3, 3]
+
+
+def test_value_model(tmp_path):
+    v = CNNValue(["board", "ones", "turns_since", "color"], board=9, filters_per_layer=8, layers=2, dense=16, device=CPU)
+    vals = v.batch_eval_state([go.GameState(9), go.GameState(9)])
+    assert len(vals) == 2 and all(-1 <= x <= 1 for x in vals)
+    j, w = str(tmp_path / "v.json"), str(tmp_path / "v.hdf5")
+    v.save_model(j, w)
+    v2 = CNNValue.load_model(j, device=CPU)
+    assert abs(v2.eval_state(go.GameState(9)) - vals[0]) < 1e-6
+
+
+def test_players_make_legal_moves():
+    p = small_policy()
+    for player in (GreedyPolicyPlayer(p), ProbabilisticPolicyPlayer(p, temperature=0.5)):
+        gs = go.GameState()
+        for _ in range(20):
+            mv = player.get_move(gs)
+            assert mv is not go.PASS_MOVE and gs.is_legal(mv)
+            gs.do_move(mv)
+    gss = [go.GameState() for _ in range(3)]
+    mvs = ProbabilisticPolicyPlayer(p).get_moves(gss)
+    assert all(g.is_legal(m) for g, m in zip(gss, mvs))
+
+
+def test_player_passes_when_only_eye():
+    p = small_policy()
+    gs = go.GameState()
+    for x in range(19):
+        for y in range(19):
+            if (x, y) != (0, 0):
+                gs.do_move((x, y), go.BLACK)
+    gs.current_player = go.BLACK
+    assert GreedyPolicyPlayer(p).get_move(gs) is go.PASS_MOVE
+    assert ProbabilisticPolicyPlayer(p).get_move(gs) is go.PASS_MOVE
+
+
+def _fake_policy(state):
+    moves = state.get_legal_moves()
+    probs = np.arange(len(moves), dtype=float)
+    probs /= probs.sum() if probs.sum() else 1
+    return list(zip(moves, probs))
+
+
+def test_reference_mcts_api():
+    gs = go.GameState()
+    # one playout: selection follows the highest prior, giving that child one visit
+    m1 = MCTS(gs, lambda s: 0.0, _fake_policy, _fake_policy, lmbda=0.0, n_search=1)
+    assert m1.get_move(gs) == (18, 18)
+    assert m1.root_visits()[(18, 18)] == 1
+    m = MCTS(gs, lambda s: 0.0, _fake_policy, _fake_policy, lmbda=0.0, n_search=20)
+    mv = m.get_move(gs)
+    visits = m.root_visits()
+    assert sum(visits.values()) >= 20 and visits[mv] == max(visits.values())
+    m.update_with_move(mv)
+    gs.do_move(mv)
+    assert gs.is_legal(m.get_move(gs))
+
+
+def test_reference_mcts_with_rollouts():
+    gs = go.GameState(7)
+    m = MCTS(gs, lambda s: 0.0, _fake_policy, _fake_policy, lmbda=0.5, rollout_limit=60, n_search=6)
+    assert gs.is_legal(m.get_move(gs))
+
+
+def test_batched_mcts_many_trees():
+    p = small_policy(9)
+    v = CNNValue(FEATS, board=9, filters_per_layer=8, layers=2, dense=8, device=CPU)
+    s = BatchedMCTS(p, v, n_trees=3, seed=1)
+    states = [go.GameState(9) for _ in range(3)]
+    moves = s.search(states, n_playout=40, leaves_per_tree=8)
+    assert len(moves) == 3 and all(st.is_legal(mv) for st, mv in zip(states, moves))
+    d = s.visit_distribution(0, 9)
+    assert abs(d.sum() - 1) < 1e-5
+    # subtree reuse
+    for st, mv in zip(states, moves):
+        st.do_move(mv)
+    moves2 = s.search(states, n_playout=20, leaves_per_tree=4)
+    assert all(st.is_legal(mv) for st, mv in zip(states, moves2))
+    pl = MCTSPlayer(p, v, n_playout=16, leaves_per_batch=4)
+    assert go.GameState(9).is_legal(pl.get_move(go.GameState(9)))
+
+
+def test_gtp_transcript():
+    class PassPlayer:
+        def get_move(self, st):
+            return go.PASS_MOVE
+
+    eng = GTPEngine(GreedyPolicyPlayer(small_policy(9)), size=9)
+    assert eng.send("protocol_version") == "= 2\n\n"
+    assert eng.send("1 name") == "=1 alphago_amd\n\n"
+    assert eng.send("boardsize 9") == "=\n\n"
+    assert eng.send("clear_board") == "=\n\n"
+    assert eng.send("komi 6.5") == "=\n\n" and eng.state.komi == 6.5
+    assert eng.send("play b D4") == "=\n\n"
+    assert eng.state.board[3, 3] == go.BLACK
+    assert eng.send("play w D4").startswith("?")
+    r = eng.send("genmove w")
+    mv = parse_vertex(r[2:].strip(), 9)
+    assert mv is not None and eng.state.board[mv] == go.WHITE
+    assert eng.send("play w pass") == "=\n\n" and eng.state.current_player == go.BLACK
+    assert eng.send("undo") == "=\n\n"
+    assert eng.send("frobnicate").startswith("?")
+    assert eng.send("known_command genmove") == "= true\n\n"
+    out = io.StringIO()
+    lines = iter(["name", "boardsize 19", "clear_board", "genmove black", "genmove white", "quit"])
+    e2 = run_gtp(PassPlayer(), lambda: next(lines), out=out)
+    assert e2.disconnect
+    assert out.getvalue().count("= pass") == 2
+    assert format_vertex((8, 0)) == "J1"
