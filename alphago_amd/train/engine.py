@@ -344,4 +344,4 @@ def make_policy_trainer(net: PolicyNet, batch: int, lr: float, decay: float = 0.
         backend = "hip" if dev.type == "cuda" else "torch"
     if backend == "hip":
         return HipPolicyTrainer(net, batch, lr, decay, device=dev, **kw)
-    return TorchPolicyTrainer(net, batch, lr, decay, device=dev)
+    return TorchPolicyTrainer(net, batch, lr, decay, device=dev, iterations=kw.get("iterations", 0))

@@ -1,0 +1,206 @@
+"""Supervised policy training (reference AlphaGo/training/supervised_policy_trainer.py).
+
+Same CLI (positional ``model train_data out_directory``; ``-B/--minibatch``,
+``-E/--epochs``, ``-l/--epoch-length``, ``-r/--learning-rate``, ``-d/--decay``,
+``-v``, ``--weights``, ``--train-val-test``) and the same output directory
+contents: ``metadata.json`` (epochs, best_epoch, training_data, model_file),
+``shuffle.npz`` (the data permutation) and Keras-format
+``weights.{epoch:05d}.hdf5`` per epoch.
+
+Differences (all fixes from SURVEY.md §2.7):
+* targets are true one-hot moves (Q1: the reference built a 38-hot row);
+* resume continues epoch numbering and the Keras lr-decay iteration count and
+  data cursor from ``checkpoint.pt`` (Q16);
+* data parallel across GPUs (one process per GPU, RCCL all-reduce inside the
+  step); each global minibatch of B*world positions is split across ranks;
+* per-board D4 augmentation happens on the GPU inside ``pack_input``.
+
+Run: ``python -m alphago_amd.train.sl model.json data.h5 outdir -B 256``
+(multi-GPU: ``torchrun --nproc-per-node 8 -m alphago_amd.train.sl ...``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..data.dataset import PositionDataset
+from ..models.policy import CNNPolicy
+from ..parallel import dist as agdist
+from ..utils.metrics import MetricsLogger
+from .engine import make_policy_trainer
+
+
+class MetadataWriter(object):
+    """metadata.json in the reference schema (supervised_policy_trainer.py:43-68)."""
+
+    def __init__(self, path: str):
+        self.file = path
+        self.metadata = {"epochs": [], "best_epoch": 0}
+
+    def on_epoch_end(self, logs: dict) -> int:
+        epoch = len(self.metadata["epochs"])
+        self.metadata["epochs"].append(logs)
+        key = "val_loss" if "val_loss" in logs else "loss"
+        best = self.metadata["epochs"][self.metadata["best_epoch"]][key]
+        if logs.get(key) < best:
+            self.metadata["best_epoch"] = epoch
+        self.save()
+        return epoch
+
+    def save(self):
+        tmp = self.file + ".tmp"
+        with open(tmp, "w") as f:
+            json.dump(self.metadata, f)
+        os.replace(tmp, self.file)
+
+
+def _parser():
+    p = argparse.ArgumentParser(description="Perform supervised training on a policy network.")
+    p.add_argument("model", help="Path to a JSON model file (i.e. from CNNPolicy.save_model())")
+    p.add_argument("train_data", help="A .h5 file of training data")
+    p.add_argument("out_directory", help="directory where metadata and weights will be saved")
+    p.add_argument("--minibatch", "-B", type=int, default=16, help="per-GPU minibatch. Default: 16")
+    p.add_argument("--epochs", "-E", type=int, default=10)
+    p.add_argument("--epoch-length", "-l", type=int, default=None,
+                   help="Number of training examples considered 'one epoch'. Default: # training data")
+    p.add_argument("--learning-rate", "-r", type=float, default=.03)
+    p.add_argument("--decay", "-d", type=float, default=.0001)
+    p.add_argument("--verbose", "-v", default=False, action="store_true")
+    p.add_argument("--weights", default=None, help="weights file (in out_directory) to resume from")
+    p.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
+    p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no-symmetries", action="store_true", help="disable random D4 augmentation")
+    p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
+    p.add_argument("--metrics", default=None, help="JSONL per-step metrics file")
+    return p
+
+
+def run_training(cmd_line_args: Optional[List[str]] = None):
+    args = _parser().parse_args(cmd_line_args)
+    env = agdist.init_from_env()
+    dev = env.device
+    resume = args.weights is not None
+    world, rank = env.world_size, env.rank
+    if args.verbose and env.is_main:
+        print("resuming from %s" % args.weights if resume else "output directory %s" % args.out_directory)
+
+    policy = CNNPolicy.load_model(args.model, device=dev)
+    net = policy.model
+    if resume:
+        policy.load_weights(os.path.join(args.out_directory, args.weights))
+
+    dataset = PositionDataset(args.train_data, device=dev, resident=args.resident)
+    if dataset.planes != policy.preprocessor.output_dim:
+        raise ValueError("dataset has %d planes, model expects %d" % (dataset.planes, policy.preprocessor.output_dim))
+    n_total = len(dataset)
+    n_train = int(args.train_val_test[0] * n_total)
+    n_val = int(args.train_val_test[1] * n_total)
+
+    if env.is_main:
+        os.makedirs(args.out_directory, exist_ok=True)
+    agdist.barrier()
+    meta = MetadataWriter(os.path.join(args.out_directory, "metadata.json"))
+    if resume and os.path.exists(meta.file):
+        with open(meta.file) as f:
+            meta.metadata = json.load(f)
+    meta.metadata["training_data"] = args.train_data
+    meta.metadata["model_file"] = args.model
+
+    shuffle_file = os.path.join(args.out_directory, "shuffle.npz")
+    if resume and os.path.exists(shuffle_file):
+        with open(shuffle_file, "rb") as f:
+            shuffle_indices = np.load(f)
+    else:
+        shuffle_indices = np.random.default_rng(args.seed).permutation(n_total)
+        if env.is_main:
+            with open(shuffle_file, "wb") as f:
+                np.save(f, shuffle_indices)
+    train_idx = shuffle_indices[:n_train]
+    val_idx = shuffle_indices[n_train:n_train + n_val]
+
+    ckpt_path = os.path.join(args.out_directory, "checkpoint.pt")
+    iterations, cursor = 0, 0
+    if resume and os.path.exists(ckpt_path):
+        ck = torch.load(ckpt_path, map_location="cpu", weights_only=True)
+        iterations, cursor = int(ck["iterations"]), int(ck["cursor"])
+
+    B = args.minibatch
+    trainer = make_policy_trainer(net, B, args.learning_rate, args.decay, backend=args.backend, device=dev,
+                                  iterations=iterations)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(args.seed * 1000 + rank)
+    global_B = B * world
+    samples_per_epoch = args.epoch_length or n_train
+    steps_per_epoch = max(1, samples_per_epoch // global_B)
+    log = MetricsLogger(args.metrics if env.is_main else None)
+
+    def global_batch(cur):
+        idx = np.take(train_idx, np.arange(cur, cur + global_B) % max(1, n_train))
+        return idx[rank * B:(rank + 1) * B], (cur + global_B) % max(1, n_train)
+
+    start_epoch = len(meta.metadata["epochs"])
+    for epoch in range(start_epoch, start_epoch + args.epochs if resume else args.epochs):
+        t0 = time.perf_counter()
+        loss_sum = torch.zeros((), device=dev, dtype=torch.float64)
+        corr_sum = torch.zeros((), device=dev, dtype=torch.float64)
+        for step in range(steps_per_epoch):
+            idx, cursor = global_batch(cursor)
+            planes, tgt = dataset.batch(idx)
+            sym = None if args.no_symmetries else torch.randint(0, 8, (B,), device=dev, dtype=torch.int32,
+                                                                 generator=gen)
+            l, c = trainer.step(planes, tgt, sym)
+            loss_sum += l.double()
+            corr_sum += c.double()
+        stats = torch.stack([loss_sum, corr_sum]).double()
+        agdist.all_reduce_sum_(stats)
+        seen = steps_per_epoch * global_B
+        logs = {"loss": float(stats[0]) / seen, "acc": float(stats[1]) / seen}
+        if n_val > 0:
+            vl, vc, vn = _validate(trainer, dataset, val_idx, B, rank, world, dev)
+            logs.update({"val_loss": vl, "val_acc": vc})
+        dt = time.perf_counter() - t0
+        if env.is_main:
+            ep = meta.on_epoch_end(logs)
+            policy.save_weights(os.path.join(args.out_directory, "weights.%05d.hdf5" % ep))
+            tmp = ckpt_path + ".tmp"
+            torch.save({"iterations": trainer.sched.iterations, "cursor": cursor, "epoch": ep}, tmp)
+            os.replace(tmp, ckpt_path)
+            log.log(epoch=ep, positions_per_s=seen / dt, **logs)
+            if args.verbose:
+                print("epoch %d: %s (%.0f pos/s)" % (ep, logs, seen / dt), flush=True)
+        agdist.barrier()
+    dataset.close()
+    return meta.metadata
+
+
+@torch.no_grad()
+def _validate(trainer, dataset, val_idx, B, rank, world, dev):
+    mine = val_idx[rank::world]
+    loss = torch.zeros((), device=dev, dtype=torch.float64)
+    corr = torch.zeros((), device=dev, dtype=torch.float64)
+    for i in range(0, len(mine), B):
+        idx = mine[i:i + B]
+        planes, tgt = dataset.batch(idx)
+        if len(idx) < B:
+            pad = B - len(idx)
+            planes = torch.cat([planes, torch.zeros((pad,) + tuple(planes.shape[1:]), dtype=planes.dtype,
+                                                    device=planes.device)])
+            tgt = torch.cat([tgt, torch.full((pad,), -1, dtype=tgt.dtype, device=tgt.device)])
+        l, c = trainer.evaluate(planes, tgt)
+        loss += l.double()
+        corr += c.double()
+    st = torch.stack([loss, corr, torch.tensor(float(len(mine)), device=dev, dtype=torch.float64)])
+    agdist.all_reduce_sum_(st)
+    n = max(1.0, float(st[2]))
+    return float(st[0]) / n, float(st[1]) / n, n
+
+
+if __name__ == "__main__":
+    run_training()
