@@ -42,7 +42,7 @@ class PositionDataset(object):
         self.resident = (resident == "yes") or (resident == "auto" and fits)
         self._states_np = ds.read()  # memmap view for contiguous data, decoded array for chunked
         if self.resident:
-            self.states = torch.from_numpy(np.ascontiguousarray(self._states_np)).to(self.device)
+            self.states = torch.from_numpy(np.array(self._states_np, copy=True)).to(self.device)
             self.targets = torch.from_numpy(self.targets_np).to(self.device)
         else:
             self.states = None

@@ -56,7 +56,8 @@ def init_from_env(device: str = "auto", timeout_s: float = 600.0) -> DistEnv:
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     use_gpu = (device == "cuda") or (device == "auto" and torch.cuda.is_available())
     if use_gpu:
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
+        ndev = max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local % ndev)
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
@@ -64,9 +65,9 @@ def init_from_env(device: str = "auto", timeout_s: float = 600.0) -> DistEnv:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
-        backend = "nccl" if use_gpu else "gloo"
+        backend = os.environ.get("ALPHAGO_AMD_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         kw = {}
-        if use_gpu:
+        if use_gpu and backend == "nccl":
             kw["device_id"] = dev
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)

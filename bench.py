@@ -102,7 +102,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / PAPER_SL_POS_PER_S, 2),
-            "dtype": "bf16",
+            "dtype": "bf16" if args.backend == "hip" else "fp32",
             "data": "synthetic (random uint8 planes/targets, random-init weights)",
             "top1_acc": round(float(stats[1]) / positions, 4),
             "mean_loss": round(float(stats[0]) / positions, 4),

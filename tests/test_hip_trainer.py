@@ -32,7 +32,7 @@ def test_hip_grads_match_torch(cuda_device, F, L, C, B):
         # direction and magnitude (per-kernel 1e-2 checks are in test_hip_kernels)
         cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
         ratio = a.norm().item() / max(b.norm().item(), 1e-12)
-        assert cos > 0.99 and abs(ratio - 1) < 0.05, (name, cos, ratio)
+        assert cos > 0.98 and abs(ratio - 1) < 0.05, (name, cos, ratio)
     # loss / accuracy bookkeeping
     assert torch.allclose(hip.loss, ref._last[0], rtol=2e-2, atol=2e-2)
 
@@ -52,3 +52,54 @@ def test_hip_step_reduces_loss(cuda_device):
     assert l1.item() < l0
     # module parameters are views of the trained flat buffer
     assert torch.equal(net.head_w.detach().view(-1), tr.fp.views["head_w"].view(-1))
+
+
+class _RoundFwd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _RoundGrad(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).float()
+
+
+def test_hip_grads_match_bf16_emulation(cuda_device):
+    """Same comparison against an fp32 reference that rounds exactly where the
+    HIP path stores bf16 (weights, activations, pre-activation gradients): any
+    real indexing/orientation bug shows up far above this tolerance."""
+    import torch.nn.functional as F
+    torch.manual_seed(0)
+    B, C, Fn, L = 5, 48, 192, 4
+    net = PolicyNet(C, filters_per_layer=Fn, layers=L)
+    ws = [w.detach().clone().to(cuda_device) for w in net.trunk.weights]
+    bs = [b.detach().clone().to(cuda_device) for b in net.trunk.biases]
+    hw, hb = net.head_w.detach().clone().to(cuda_device), net.head_b.detach().clone().to(cuda_device)
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    hip = HipPolicyTrainer(net, B, lr=0.01, device=cuda_device)
+    hip.compute_grads(planes, tgt, None)
+    params = [p.requires_grad_(True) for p in ws + bs + [hw, hb]]
+    x = planes.float()
+    for l in range(L):
+        z = F.conv2d(x, ws[l].to(torch.bfloat16).float(), bs[l], padding=net.trunk.widths[l] // 2)
+        z = _RoundGrad.apply(z)
+        x = _RoundFwd.apply(F.relu(z))
+    logits = (x * hw.view(1, Fn, 1, 1)).sum(1).flatten(1) + hb
+    loss = F.cross_entropy(logits, tgt.long(), reduction="sum") / B
+    loss.backward()
+    for l in range(L):
+        for name, ref in (("w%d" % l, ws[l].grad), ("b%d" % l, bs[l].grad)):
+            a = hip.fp.grad_views[name]
+            cos = torch.nn.functional.cosine_similarity(a.flatten().double(), ref.flatten().double(), dim=0).item()
+            assert cos > 0.999, (name, cos)
