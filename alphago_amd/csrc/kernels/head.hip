@@ -107,6 +107,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
   }
   if constexpr (TRAIN) {
     const int t = a.target[b];
+    const float wb = a.weight ? a.weight[b] : 1.f;
     if (tid == 0) {
       if (t >= 0) {
         float pt = __expf(z_s[t] - zmax) * inv;
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
     __syncthreads();  // everyone has read z_s[t]
     for (int p = tid; p < SS; p += 256) {
       float g = 0.f;
-      if (t >= 0) g = (__expf(z_s[p] - zmax) * inv - (p == t ? 1.f : 0.f)) * a.grad_scale;
+      if (t >= 0) g = (__expf(z_s[p] - zmax) * inv - (p == t ? 1.f : 0.f)) * a.grad_scale * wb;
       z_s[p] = g;
     }
     __syncthreads();

@@ -43,6 +43,7 @@ struct PolicyHeadArgs {
   const float* b;      // [1]
   const int* target;   // [B] flat move index or -1 (no loss)
   const uint8_t* legal;  // [B][S*S] or null (inference renormalisation)
+  const float* weight;   // [B] per-board gradient weight (REINFORCE reward) or null
   __bf16* dz;          // padded NHWC grad (training) or null
   float* loss;         // [B]
   float* correct;      // [B]

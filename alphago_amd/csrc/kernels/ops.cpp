@@ -101,7 +101,7 @@ void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& g
 }
 
 void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::optional<Tensor>& target,
-                 const c10::optional<Tensor>& legal, const c10::optional<Tensor>& dz, const c10::optional<Tensor>& loss,
+                 const c10::optional<Tensor>& legal, const c10::optional<Tensor>& weight, const c10::optional<Tensor>& dz, const c10::optional<Tensor>& loss,
                  const c10::optional<Tensor>& correct, const c10::optional<Tensor>& dhead,
                  const c10::optional<Tensor>& probs, int64_t S, double grad_scale, double temperature) {
   CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(b);
@@ -127,6 +127,11 @@ void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::o
     a.loss = loss->data_ptr<float>();
     a.correct = correct->data_ptr<float>();
     a.dhead = dhead->data_ptr<float>();
+  }
+  if (weight.has_value()) {
+    CHECK_F32(*weight);
+    TORCH_CHECK(weight->numel() == B, "weight must be (B,)");
+    a.weight = weight->data_ptr<float>();
   }
   if (legal.has_value()) {
     TORCH_CHECK(legal->scalar_type() == at::kByte && legal->numel() == B * S * S, "legal must be uint8 (B, S*S)");
@@ -199,7 +204,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def(
-      "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor(a!)? dz, Tensor(b!)? loss, "
+      "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor? weight, Tensor(a!)? dz, Tensor(b!)? loss, "
       "Tensor(c!)? correct, Tensor(d!)? dhead, Tensor(e!)? probs, int S, float grad_scale, float temperature) -> ()");
   m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P) -> ()");
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");

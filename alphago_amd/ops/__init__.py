@@ -95,12 +95,12 @@ def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, bet
     _ops().conv_wgrad_reduce(slab, dbslab, grad_w, grad_b, scale, beta)
 
 
-def policy_head_train(y, w, b, target, dz, loss, correct, dhead, S: int, grad_scale: float):
-    _ops().policy_head(y, w, b, target, None, dz, loss, correct, dhead, None, S, grad_scale, 1.0)
+def policy_head_train(y, w, b, target, dz, loss, correct, dhead, S: int, grad_scale: float, weight=None):
+    _ops().policy_head(y, w, b, target, None, weight, dz, loss, correct, dhead, None, S, grad_scale, 1.0)
 
 
 def policy_head_probs(y, w, b, probs, S: int, legal=None, temperature: float = 1.0):
-    _ops().policy_head(y, w, b, None, legal, None, None, None, None, probs, S, 0.0, temperature)
+    _ops().policy_head(y, w, b, None, legal, None, None, None, None, None, probs, S, 0.0, temperature)
     return probs
 
 

@@ -1,0 +1,120 @@
+"""Vectorised self-play: many games advanced in lock-step, one batched forward per side per ply.
+
+``BatchedSampler.select(states)`` featurises all states in native threads,
+builds the sensible-move masks (legal and not filling an own eye, ai.py:15),
+runs ONE policy forward with the mask applied inside the fused head kernel,
+then samples p**(1/T) (or argmax) on the device.  This replaces the
+reference's per-state Python move lists and CPU renormalisation
+(ai.py:51-68, policy.py:44-79).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import go
+from .._native import engine as _engine
+
+
+class BatchedSampler(object):
+    def __init__(self, policy, temperature: float = 1.0, greedy: bool = False, seed: int = 0, threads: int = 8):
+        self.policy = policy
+        self.beta = 1.0 / temperature if temperature > 0 else 1.0
+        self.greedy = greedy or temperature <= 0
+        self.threads = threads
+        self._names = [f.lower() for f in policy.preprocessor.feature_list]
+        self.gen = torch.Generator(device=policy.device)
+        self.gen.manual_seed(seed)
+
+    def featurize(self, states) -> np.ndarray:
+        return _engine().featurize_batch(list(states), self._names, self.threads)
+
+    def masks(self, states) -> np.ndarray:
+        m = _engine().featurize_batch(list(states), ["sensibleness"], self.threads)
+        return m.reshape(len(states), -1)
+
+    def select(self, states: Sequence, planes: Optional[np.ndarray] = None):
+        """Returns (moves list, planes uint8 array, flat move indices (-1 = pass))."""
+        n = len(states)
+        if n == 0:
+            return [], None, np.zeros(0, np.int64)
+        size = states[0].size
+        if planes is None:
+            planes = self.featurize(states)
+        masks = self.masks(states)
+        probs = self.policy.engine.evaluate(planes, masks)
+        has = torch.from_numpy(masks.any(axis=1)).to(probs.device)
+        if self.greedy:
+            idx = probs.argmax(1)
+        else:
+            p = probs.clamp_min(0) ** self.beta if self.beta != 1.0 else probs.clamp_min(0)
+            p = torch.where(has.unsqueeze(1), p, torch.ones_like(p))
+            p = p / p.sum(1, keepdim=True).clamp_min(1e-30)
+            idx = torch.multinomial(p, 1, generator=self.gen).squeeze(1)
+        idx = torch.where(has, idx, torch.full_like(idx, -1)).cpu().numpy()
+        moves = [go.PASS_MOVE if i < 0 else (int(i) // size, int(i) % size) for i in idx]
+        return moves, planes, idx
+
+    # GreedyPolicyPlayer/ProbabilisticPolicyPlayer-compatible interface
+    def get_moves(self, states):
+        return self.select(states)[0]
+
+    def get_move(self, state):
+        return self.select([state])[0][0]
+
+
+@dataclass
+class GameRecords:
+    planes: List[np.ndarray] = field(default_factory=list)   # per game: (n_i, F, S, S) uint8
+    moves: List[np.ndarray] = field(default_factory=list)    # per game: (n_i,) flat move index
+    winners: List[int] = field(default_factory=list)
+    learner_colors: List[int] = field(default_factory=list)
+    lengths: List[int] = field(default_factory=list)
+    states: List = field(default_factory=list)               # final states
+
+
+def play_games(learner: BatchedSampler, opponent: BatchedSampler, n_games: int, size: int = 19,
+               komi: float = 7.5, max_moves: int = 500, rng: Optional[np.random.Generator] = None,
+               record: bool = True, learner_colors: Optional[Sequence[int]] = None) -> GameRecords:
+    """Play n_games learner-vs-opponent games in lock-step (reference
+    make_training_pairs, reinforcement_policy_trainer.py:16-76).  The learner's
+    colour is drawn per game and its training pairs use the state
+    *before* its own move (Q6)."""
+    rng = rng or np.random.default_rng()
+    states = [go.GameState(size, komi) for _ in range(n_games)]
+    colors = list(learner_colors) if learner_colors is not None else \
+        [int(c) for c in rng.choice([go.BLACK, go.WHITE], size=n_games)]
+    rec_p: List[List[np.ndarray]] = [[] for _ in range(n_games)]
+    rec_m: List[List[int]] = [[] for _ in range(n_games)]
+    for ply in range(max_moves):
+        active = [i for i in range(n_games) if not states[i].is_end_of_game]
+        if not active:
+            break
+        lturn = [i for i in active if states[i].current_player == colors[i]]
+        oturn = [i for i in active if states[i].current_player != colors[i]]
+        for group, sampler, is_learner in ((lturn, learner, True), (oturn, opponent, False)):
+            if not group:
+                continue
+            moves, planes, idx = sampler.select([states[i] for i in group])
+            for k, i in enumerate(group):
+                if record and is_learner and moves[k] is not go.PASS_MOVE:
+                    rec_p[i].append(planes[k])
+                    rec_m[i].append(int(idx[k]))
+                try:
+                    states[i].do_move(moves[k])
+                except go.IllegalMove:  # cannot happen for masked samples; pass defensively
+                    states[i].do_move(go.PASS_MOVE)
+    out = GameRecords()
+    for i in range(n_games):
+        out.winners.append(states[i].get_winner())
+        out.learner_colors.append(colors[i])
+        out.lengths.append(len(states[i].history))
+        out.states.append(states[i])
+        if record:
+            C = learner.policy.preprocessor.output_dim
+            out.planes.append(np.stack(rec_p[i]) if rec_p[i] else np.zeros((0, C, size, size), np.uint8))
+            out.moves.append(np.asarray(rec_m[i], dtype=np.int64))
+    return out

@@ -112,15 +112,16 @@ class KerasSGDSchedule:
         self.iterations += 1
 
 
-class HipPolicyTrainer:
-    def __init__(self, net: PolicyNet, batch: int, lr: float = 0.003, decay: float = 0.0,
-                 device=None, bucket_mb: float = 4.0, overlap: bool = True, wgrad_target_wgs: int = 512,
-                 iterations: int = 0):
+class HipConvTrainer:
+    """MFMA conv-trunk training engine; subclasses provide the head."""
+
+    def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
+                 overlap: bool = True, wgrad_target_wgs: int = 512, iterations: int = 0):
         ops.load()
         self.env = agdist.env()
         self.device = torch.device(device) if device is not None else self.env.device
         if self.device.type != "cuda":
-            raise RuntimeError("HipPolicyTrainer needs a GPU device")
+            raise RuntimeError("%s needs a GPU device" % type(self).__name__)
         self.net = net.to(self.device)
         self.batch = batch
         self.sched = KerasSGDSchedule(lr, decay, iterations)
@@ -134,18 +135,18 @@ class HipPolicyTrainer:
         self.F = tr.filters
         self.Fp = ops.round_up(self.F, 64)
         if self.F > 256:
-            raise ValueError("policy head kernel supports up to 256 filters")
+            raise ValueError("head kernels support up to 256 filters")
         self.P0 = self.K[0] // 2
         named = []
         for l in range(self.L):
             named.append(("w%d" % l, tr.weights[l]))
             named.append(("b%d" % l, tr.biases[l]))
-        named += [("head_w", net.head_w), ("head_b", net.head_b)]
-        self.fp = FlatParams(named, self.device)
+        head = self._head_named_params()
+        self.head_names = [n for n, _ in head]
+        self.fp = FlatParams(named + head, self.device)
         if self.env.distributed:
             agdist.broadcast_(self.fp.flat, 0)
         dev, B, S = self.device, batch, self.S
-        # padded biases (Fp) for the epilogue
         self.bias_p = [torch.zeros(self.Fp, device=dev) for _ in range(self.L)]
         self.wf, self.wd = [], []
         for l in range(self.L):
@@ -160,8 +161,6 @@ class HipPolicyTrainer:
         self.DZ = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(self.L)]
         self.loss = torch.zeros(B, device=dev)
         self.correct = torch.zeros(B, device=dev)
-        self.dhead = torch.zeros(B, self.F + 1, device=dev)
-        self.tgt = torch.zeros(B, dtype=torch.int32, device=dev)
         M = B * S * S
         self.nsplit = []
         slab_max, db_max = 0, 0
@@ -177,8 +176,10 @@ class HipPolicyTrainer:
         self._slab = torch.empty(slab_max, device=dev)
         self._dbslab = torch.zeros(db_max, device=dev)
         self.s_w = torch.cuda.Stream(device=dev) if overlap else None
-        # buckets over the flat grad, segments in backward order
-        segs = [(self.fp.segments["head_w"][0], self.fp.segments["head_w"][1] + self.fp.segments["head_b"][1])]
+        # buckets over the flat grad, segments in backward order (head first)
+        h0 = self.fp.segments[self.head_names[0]][0]
+        h1 = sum(self.fp.segments[n][1] for n in self.head_names)
+        segs = [(h0, h1)]
         self._seg_layer = [None]
         for l in reversed(range(self.L)):
             ow, nw = self.fp.segments["w%d" % l]
@@ -191,7 +192,18 @@ class HipPolicyTrainer:
             last = ids[-1]
             self._bucket_after_layer[self._seg_layer[last] if self._seg_layer[last] is not None else -1] = bi
         self.reducer = agdist.BucketAllReducer(self.fp.grad, self.buckets)
+        self._init_head()
         self.repack()
+
+    # ------------------------------------------------------------------ head API
+    def _head_named_params(self):
+        raise NotImplementedError
+
+    def _init_head(self):
+        pass
+
+    def _head_train(self, targets, gscale: float, weight) -> None:
+        raise NotImplementedError
 
     # ------------------------------------------------------------------ helpers
     def repack(self) -> None:
@@ -202,8 +214,8 @@ class HipPolicyTrainer:
     def _layer_in(self, l):
         return (self.X0, self.P0) if l == 0 else (self.Y[l - 1], 1)
 
-    def forward_trunk(self, planes: torch.Tensor, sym=None, targets=None) -> None:
-        ops.pack_input(planes, self.X0, self.P0, sym=sym, target=targets, target_out=self.tgt if targets is not None else None)
+    def forward_trunk(self, planes: torch.Tensor, sym=None, move_targets=None, target_out=None) -> None:
+        ops.pack_input(planes, self.X0, self.P0, sym=sym, target=move_targets, target_out=target_out)
         for l in range(self.L):
             x, pin = self._layer_in(l)
             ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1)
@@ -218,22 +230,11 @@ class HipPolicyTrainer:
         ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1)
         ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)
 
-    def compute_grads(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None):
-        """Forward + backward into self.fp.grad (all-reduced when distributed)."""
-        B = planes.shape[0]
-        if B != self.batch:
-            raise ValueError("batch %d != configured %d" % (B, self.batch))
+    def backward_trunk(self) -> None:
+        """dZ[L-1] (and head grads) must be ready on the current stream."""
         main = torch.cuda.current_stream(self.device)
-        self.forward_trunk(planes, sym, targets)
-        gscale = 1.0 / (B * self.env.world_size)
-        hw = self.fp.views["head_w"].view(-1)
-        hb = self.fp.views["head_b"]
-        ops.policy_head_train(self.Y[-1], hw, hb, self.tgt, self.DZ[-1], self.loss, self.correct, self.dhead,
-                              self.S, gscale)
-        ho, hn = self.fp.segments["head_w"]
-        torch.sum(self.dhead, dim=0, out=self.fp.grad[ho:ho + hn + 1])
         if -1 in self._bucket_after_layer:
-            self._launch_bucket(self._bucket_after_layer[-1], main)
+            self.reducer.launch(self._bucket_after_layer[-1])
         for l in reversed(range(self.L)):
             if self.s_w is not None:
                 ev = main.record_event()
@@ -253,51 +254,178 @@ class HipPolicyTrainer:
             main.wait_stream(self.s_w)
         self.reducer.wait()
 
-    def _launch_bucket(self, bi, stream):
-        self.reducer.launch(bi)
+    def compute_grads(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None,
+                      weight: Optional[torch.Tensor] = None):
+        """Forward + backward into self.fp.grad (all-reduced when distributed)."""
+        B = planes.shape[0]
+        if B != self.batch:
+            raise ValueError("batch %d != configured %d" % (B, self.batch))
+        self._forward_for_head(planes, targets, sym)
+        self._head_train(targets, 1.0 / (B * self.env.world_size), weight)
+        self.backward_trunk()
 
-    def step(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None):
-        """One SGD step.  Returns (sum of per-board loss, number correct) as device scalars (local)."""
-        self.compute_grads(planes, targets, sym)
+    def apply_update(self) -> None:
         ops.sgd_update(self.fp.flat, self.fp.grad, self.sched.current(), 1.0)
         self.sched.advance()
         self.repack()
+
+    def step(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None,
+             weight: Optional[torch.Tensor] = None):
+        """One SGD step.  Returns (sum of per-board loss, metric sum) as device scalars (local)."""
+        self.compute_grads(planes, targets, sym, weight)
+        self.apply_update()
         return self.loss.sum(), self.correct.sum()
+
+
+class HipPolicyTrainer(HipConvTrainer):
+    """Policy net: fused HIP head (softmax + clipped CE + top-1 + backward).
+    ``weight`` (per board) scales each board's gradient — REINFORCE rewards."""
+
+    def _head_named_params(self):
+        return [("head_w", self.net.head_w), ("head_b", self.net.head_b)]
+
+    def _init_head(self):
+        self.dhead = torch.zeros(self.batch, self.F + 1, device=self.device)
+        self.tgt = torch.zeros(self.batch, dtype=torch.int32, device=self.device)
+
+    def _forward_for_head(self, planes, targets, sym):
+        self.forward_trunk(planes, sym, targets, self.tgt)
+
+    def _head_train(self, targets, gscale, weight):
+        hw = self.fp.views["head_w"].view(-1)
+        hb = self.fp.views["head_b"]
+        ops.policy_head_train(self.Y[-1], hw, hb, self.tgt, self.DZ[-1], self.loss, self.correct, self.dhead,
+                              self.S, gscale, weight=weight)
+        ho, hn = self.fp.segments["head_w"]
+        torch.sum(self.dhead, dim=0, out=self.fp.grad[ho:ho + hn + 1])
 
     @torch.no_grad()
     def evaluate(self, planes: torch.Tensor, targets: torch.Tensor):
         """Loss/accuracy without update (validation)."""
-        self.forward_trunk(planes, None, targets)
+        self.forward_trunk(planes, None, targets, self.tgt)
         hw = self.fp.views["head_w"].view(-1)
         ops.policy_head_train(self.Y[-1], hw, self.fp.views["head_b"], self.tgt, self.DZ[-1], self.loss,
                               self.correct, self.dhead, self.S, 0.0)
         return self.loss.sum(), self.correct.sum()
 
 
-class TorchPolicyTrainer:
-    """Autograd implementation of the same SL step (fp32 by default)."""
+class HipValueTrainer(HipConvTrainer):
+    """Value net (reference value.py): HIP trunk + 1x1 conv -> Dense(256) ->
+    Dense(1) -> tanh head; MSE against game outcomes in [-1, 1].  The head is
+    tiny (361x256 per board), so it runs as a few fused torch ops and feeds its
+    ReLU-masked input gradient back into the MFMA trunk backward.
+    ``correct`` accumulates the squared error sign agreement (sign(v) == z)."""
 
-    def __init__(self, net: PolicyNet, batch: int, lr: float = 0.003, decay: float = 0.0, device=None,
-                 dtype=torch.float32, iterations: int = 0):
+    def _head_named_params(self):
+        n = self.net
+        return [("head_w", n.head_w), ("head_b", n.head_b), ("fc1_w", n.fc1_w), ("fc1_b", n.fc1_b),
+                ("fc2_w", n.fc2_w), ("fc2_b", n.fc2_b)]
+
+    def _forward_for_head(self, planes, targets, sym):
+        self.forward_trunk(planes, sym, None, None)
+
+    def _head_forward(self, requires_grad: bool):
+        S, F, B = self.S, self.F, self.batch
+        inner = self.Y[-1][:, 1:S + 1, 1:S + 1, :F].float().reshape(B, S * S, F)
+        if requires_grad:
+            inner.requires_grad_(True)
+        v = self.fp.views
+        hp = [v[n].detach().requires_grad_(requires_grad) for n in self.head_names]
+        hw, hb, w1, b1, w2, b2 = hp
+        z = inner @ hw.view(-1) + hb
+        h = z @ w1 + b1
+        val = torch.tanh(h @ w2 + b2).squeeze(1)
+        return inner, hp, val
+
+    def _head_train(self, targets, gscale, weight):
+        with torch.enable_grad():
+            inner, hp, val = self._head_forward(True)
+            z = targets.float()
+            err = (val - z) ** 2
+            wsum = err if weight is None else err * weight
+            (wsum.sum() * gscale).backward()
+        with torch.no_grad():
+            self.loss.copy_(err.detach())
+            self.correct.copy_((torch.sign(val.detach()) == torch.sign(z)).float())
+            for n, p in zip(self.head_names, hp):
+                self.fp.grad_views[n].copy_(p.grad.view(self.fp.grad_views[n].shape))
+            S, F = self.S, self.F
+            g = inner.grad.view(self.batch, S, S, F)
+            y = self.Y[-1][:, 1:S + 1, 1:S + 1, :F]
+            self.DZ[-1][:, 1:S + 1, 1:S + 1, :F] = torch.where(y > 0, g, torch.zeros_like(g)).to(torch.bfloat16)
+
+    @torch.no_grad()
+    def evaluate(self, planes: torch.Tensor, targets: torch.Tensor):
+        self.forward_trunk(planes, None, None, None)
+        _, _, val = self._head_forward(False)
+        z = targets.float()
+        return ((val - z) ** 2).sum(), (torch.sign(val) == torch.sign(z)).float().sum()
+
+    @torch.no_grad()
+    def predict(self, planes: torch.Tensor) -> torch.Tensor:
+        self.forward_trunk(planes, None, None, None)
+        return self._head_forward(False)[2]
+
+
+class _TorchTrainerBase:
+    def _setup(self, net, batch, lr, decay, device, dtype, iterations, named):
         self.env = agdist.env()
         self.device = torch.device(device) if device is not None else self.env.device
         self.net = net.to(self.device)
         self.batch = batch
         self.dtype = dtype
         self.sched = KerasSGDSchedule(lr, decay, iterations)
-        named = []
-        tr = net.trunk
-        for l in range(tr.layers):
-            named.append(("w%d" % l, tr.weights[l]))
-            named.append(("b%d" % l, tr.biases[l]))
-        named += [("head_w", net.head_w), ("head_b", net.head_b)]
         self.params = [p for _, p in named]
         self.fp = FlatParams(named, self.device)
         if self.env.distributed:
             agdist.broadcast_(self.fp.flat, 0)
         self.table = symmetry_tables(net.board, self.device)
 
-    def _loss(self, planes, targets, sym):
+    def compute_grads(self, planes, targets, sym=None, weight=None):
+        for p in self.params:
+            p.grad = None
+        obj, per, metric = self._loss(planes, targets, sym, weight)
+        obj.backward()
+        for (name, p) in zip(self.fp.names, self.params):
+            if p.grad is None:
+                self.fp.grad_views[name].zero_()
+            else:
+                self.fp.grad_views[name].copy_(p.grad)
+        if self.env.distributed:
+            agdist.all_reduce_sum_(self.fp.grad)
+        self._last = (per.detach(), metric.detach())
+
+    def apply_update(self):
+        with torch.no_grad():
+            self.fp.flat.add_(self.fp.grad, alpha=-self.sched.current())
+        self.sched.advance()
+
+    def step(self, planes, targets, sym=None, weight=None):
+        self.compute_grads(planes, targets, sym, weight)
+        self.apply_update()
+        per, metric = self._last
+        return per.sum(), metric.sum()
+
+    @torch.no_grad()
+    def evaluate(self, planes, targets):
+        obj, per, metric = self._loss(planes, targets, None, None)
+        return per.sum(), metric.sum()
+
+
+class TorchPolicyTrainer(_TorchTrainerBase):
+    """Autograd implementation of the same SL/RL step (fp32 by default)."""
+
+    def __init__(self, net: PolicyNet, batch: int, lr: float = 0.003, decay: float = 0.0, device=None,
+                 dtype=torch.float32, iterations: int = 0):
+        named = []
+        tr = net.trunk
+        for l in range(tr.layers):
+            named.append(("w%d" % l, tr.weights[l]))
+            named.append(("b%d" % l, tr.biases[l]))
+        named += [("head_w", net.head_w), ("head_b", net.head_b)]
+        self._setup(net, batch, lr, decay, device, dtype, iterations, named)
+
+    def _loss(self, planes, targets, sym, weight):
         if sym is not None:
             planes, targets = apply_symmetry(planes, targets, sym, self.table)
         x = planes.to(self.dtype)
@@ -308,33 +436,43 @@ class TorchPolicyTrainer:
         lt = logp.gather(1, t.clamp_min(0).unsqueeze(1)).squeeze(1)
         per = -torch.clamp(lt, min=math.log(1e-7), max=math.log(1 - 1e-7)) * valid
         correct = ((logits.argmax(1) == t) & valid).float()
-        # gradient of mean CE (unclipped, see kernels/head.hip)
-        obj = (-(lt * valid)).sum() / (planes.shape[0] * self.env.world_size)
+        # gradient of mean CE (unclipped, see kernels/head.hip); optional per-board weights (REINFORCE)
+        w = valid.float() if weight is None else valid.float() * weight
+        obj = (-(lt * w)).sum() / (planes.shape[0] * self.env.world_size)
         return obj, per, correct
 
-    def compute_grads(self, planes, targets, sym=None):
-        for p in self.params:
-            p.grad = None
-        obj, per, correct = self._loss(planes, targets, sym)
-        obj.backward()
-        for (name, p) in zip(self.fp.names, self.params):
-            self.fp.grad_views[name].copy_(p.grad)
-        if self.env.distributed:
-            agdist.all_reduce_sum_(self.fp.grad)
-        self._last = (per.detach(), correct.detach())
 
-    def step(self, planes, targets, sym=None):
-        self.compute_grads(planes, targets, sym)
-        with torch.no_grad():
-            self.fp.flat.add_(self.fp.grad, alpha=-self.sched.current())
-        self.sched.advance()
-        per, correct = self._last
-        return per.sum(), correct.sum()
+class TorchValueTrainer(_TorchTrainerBase):
+    def __init__(self, net: ValueNet, batch: int, lr: float = 0.003, decay: float = 0.0, device=None,
+                 dtype=torch.float32, iterations: int = 0):
+        named = []
+        tr = net.trunk
+        for l in range(tr.layers):
+            named.append(("w%d" % l, tr.weights[l]))
+            named.append(("b%d" % l, tr.biases[l]))
+        named += [("head_w", net.head_w), ("head_b", net.head_b), ("fc1_w", net.fc1_w), ("fc1_b", net.fc1_b),
+                  ("fc2_w", net.fc2_w), ("fc2_b", net.fc2_b)]
+        self._setup(net, batch, lr, decay, device, dtype, iterations, named)
 
-    @torch.no_grad()
-    def evaluate(self, planes, targets):
-        obj, per, correct = self._loss(planes, targets, None)
-        return per.sum(), correct.sum()
+    def _loss(self, planes, targets, sym, weight):
+        if sym is not None:
+            planes, _ = apply_symmetry(planes, None, sym, self.table)
+        v = self.net.forward_torch(planes.to(self.dtype))
+        z = targets.float()
+        err = (v - z) ** 2
+        w = err if weight is None else err * weight
+        obj = w.sum() / (planes.shape[0] * self.env.world_size)
+        return obj, err, (torch.sign(v) == torch.sign(z)).float()
+
+
+def make_value_trainer(net: ValueNet, batch: int, lr: float, decay: float = 0.0, backend: str = "auto",
+                       device=None, **kw):
+    dev = torch.device(device) if device is not None else agdist.env().device
+    if backend == "auto":
+        backend = "hip" if dev.type == "cuda" else "torch"
+    if backend == "hip":
+        return HipValueTrainer(net, batch, lr, decay, device=dev, **kw)
+    return TorchValueTrainer(net, batch, lr, decay, device=dev, iterations=kw.get("iterations", 0))
 
 
 def make_policy_trainer(net: PolicyNet, batch: int, lr: float, decay: float = 0.0, backend: str = "auto",

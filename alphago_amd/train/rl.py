@@ -1,0 +1,180 @@
+"""Reinforcement learning of the policy network by self-play
+(reference AlphaGo/training/reinforcement_policy_trainer.py).
+
+Each iteration: play ``game_batch_size`` games of the learner against an
+opponent drawn uniformly from the pool (on every rank, different seeds), then
+one policy-gradient update.  Default loss is REINFORCE as in the paper,
+    grad = -1/N * sum_games z_g * sum_t grad log p(a_t | s_t),
+with z = +1 for a learner win and -1 for a loss — computed by the fused HIP
+head kernel with per-board weights z.  ``--loss reference`` reproduces the
+reference's update (binary cross-entropy on the softmax with the learning rate
+negated for lost games; torch backend only).
+
+Fixes over the reference: per-game learner colour is used for the reward
+(Q7), training pairs use the state before the learner's move (Q6), snapshots
+are saved every ``save_every`` iterations and added to the opponent pool
+(the reference's TODOs at :123,164-175), positional
+``initial_weights initial_json`` are honoured.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .. import go
+from ..models.policy import CNNPolicy
+from ..parallel import dist as agdist
+from ..search.selfplay import BatchedSampler, play_games
+from ..utils.metrics import MetricsLogger
+from .engine import TorchPolicyTrainer, make_policy_trainer
+
+
+def rl_update(trainer, records, B: int, device, loss: str = "reinforce") -> dict:
+    """One policy-gradient step over all learner positions of a batch of games."""
+    X, T, Z = [], [], []
+    for planes, moves, w, c in zip(records.planes, records.moves, records.winners, records.learner_colors):
+        if len(moves) == 0:
+            continue
+        z = 1.0 if w == c else (-1.0 if w == -c else 0.0)
+        X.append(planes)
+        T.append(moves)
+        Z.append(np.full(len(moves), z, np.float32))
+    C = trainer.net.trunk.in_planes
+    S = trainer.net.board
+    if X:
+        X, T, Z = np.concatenate(X), np.concatenate(T).astype(np.int32), np.concatenate(Z)
+    else:
+        X, T, Z = np.zeros((0, C, S, S), np.uint8), np.zeros(0, np.int32), np.zeros(0, np.float32)
+    n = len(T)
+    n_chunks = int(agdist.all_reduce_max(float((n + B - 1) // B)))
+    if loss == "reference":
+        return _reference_bce_update(trainer, X, T, Z, B, device, n_chunks)
+    acc = torch.zeros_like(trainer.fp.grad)
+    scale = float(B) / max(1, n)
+    for c in range(max(1, n_chunks)):
+        sl = slice(c * B, (c + 1) * B)
+        xb, tb, zb = X[sl], T[sl], Z[sl]
+        pad = B - len(tb)
+        if pad:
+            xb = np.concatenate([xb, np.zeros((pad, C, S, S), np.uint8)])
+            tb = np.concatenate([tb, np.full(pad, -1, np.int32)])
+            zb = np.concatenate([zb, np.zeros(pad, np.float32)])
+        trainer.compute_grads(torch.from_numpy(xb).to(device), torch.from_numpy(tb).to(device), None,
+                              torch.from_numpy(zb * scale).to(device))
+        acc += trainer.fp.grad
+    trainer.fp.grad.copy_(acc)
+    trainer.apply_update()
+    return {"positions": n, "mean_reward": float(Z.mean()) if n else 0.0}
+
+
+def _reference_bce_update(trainer, X, T, Z, B, device, n_chunks) -> dict:
+    """reinforcement_policy_trainer.py:79-103: per game, lr = ±lr and
+    model.fit(X, one_hot(y)) with binary cross-entropy on the softmax output."""
+    if not isinstance(trainer, TorchPolicyTrainer):
+        raise ValueError("--loss reference needs the torch backend")
+    net = trainer.net
+    lr = trainer.sched.current()
+    S = net.board
+    for c in range(max(1, n_chunks)):
+        sl = slice(c * B, (c + 1) * B)
+        if len(T[sl]) == 0:
+            continue
+        x = torch.from_numpy(X[sl]).to(device).float()
+        y = torch.nn.functional.one_hot(torch.from_numpy(T[sl]).long(), S * S).float().to(device)
+        z = torch.from_numpy(Z[sl]).to(device)
+        for p in trainer.params:
+            p.grad = None
+        prob = torch.softmax(net.logits_torch(x), 1).clamp(1e-7, 1 - 1e-7)
+        bce = -(y * prob.log() + (1 - y) * (1 - prob).log()).mean(1)
+        (bce * torch.where(z < 0, -1.0, 1.0)).sum().backward()
+        with torch.no_grad():
+            for p in trainer.params:
+                if p.grad is not None:
+                    p -= lr * p.grad
+    trainer.sched.advance()
+    return {"positions": len(T), "mean_reward": float(Z.mean()) if len(Z) else 0.0}
+
+
+def _parser():
+    p = argparse.ArgumentParser(description="Perform reinforcement learning to improve given policy network. "
+                                            "Second phase of pipeline.")
+    p.add_argument("initial_weights", help="Path to file with weights to start from.")
+    p.add_argument("initial_json", help="Path to file with initial network params.")
+    p.add_argument("--model_folder", default=None, help="where snapshots / the opponent pool are saved")
+    p.add_argument("--learning_rate", type=float, default=.03)
+    p.add_argument("--save_every", type=int, default=500, help="save policy every n mini-batches")
+    p.add_argument("--game_batch_size", type=int, default=20, help="games per mini-batch (per rank)")
+    p.add_argument("--iterations", type=int, default=20, help="number of mini-batches")
+    p.add_argument("--minibatch", type=int, default=256, help="positions per gradient chunk")
+    p.add_argument("--temperature", type=float, default=1.0)
+    p.add_argument("--max-moves", type=int, default=500)
+    p.add_argument("--loss", default="reinforce", choices=["reinforce", "reference"])
+    p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--metrics", default=None)
+    p.add_argument("--verbose", "-v", action="store_true")
+    return p
+
+
+def run(cmd_line_args: Optional[List[str]] = None) -> dict:
+    args = _parser().parse_args(cmd_line_args)
+    env = agdist.init_from_env()
+    dev = env.device
+    rng = np.random.default_rng(args.seed * 7919 + env.rank)
+    learner_pol = CNNPolicy.load_model(args.initial_json, device=dev, weights_file=args.initial_weights)
+    opp_pol = CNNPolicy.load_model(args.initial_json, device=dev, weights_file=args.initial_weights)
+    backend = "torch" if args.loss == "reference" else args.backend
+    trainer = make_policy_trainer(learner_pol.model, args.minibatch, args.learning_rate, 0.0, backend=backend,
+                                  device=dev)
+    learner = BatchedSampler(learner_pol, args.temperature, seed=args.seed * 31 + env.rank)
+    opponent = BatchedSampler(opp_pol, args.temperature, seed=args.seed * 37 + env.rank + 1)
+    pool: List[Optional[str]] = [None]  # None = the initial weights
+    folder = args.model_folder
+    if folder:
+        if env.is_main:
+            os.makedirs(folder, exist_ok=True)
+        existing = sorted(f for f in os.listdir(folder) if f.startswith("weights.") and f.endswith(".hdf5")) \
+            if os.path.isdir(folder) else []
+        pool += [os.path.join(folder, f) for f in existing]
+        if env.is_main:
+            learner_pol.save_model(os.path.join(folder, "model.json"))
+    log = MetricsLogger(args.metrics if env.is_main else None)
+    history = []
+    size = learner_pol.model.board
+    for it in range(args.iterations):
+        t0 = time.perf_counter()
+        choice = pool[int(rng.integers(len(pool)))]
+        opp_pol.load_weights(choice if choice else args.initial_weights)
+        learner_pol.refresh()
+        rec = play_games(learner, opponent, args.game_batch_size, size=size, max_moves=args.max_moves, rng=rng)
+        info = rl_update(trainer, rec, args.minibatch, dev, args.loss)
+        learner_pol.refresh()
+        wins = sum(1 for w, c in zip(rec.winners, rec.learner_colors) if w == c)
+        tot = torch.tensor([float(wins), float(len(rec.winners)), float(sum(rec.lengths))], dtype=torch.float64,
+                           device=dev if env.backend == "nccl" else "cpu")
+        agdist.all_reduce_sum_(tot)
+        dt = time.perf_counter() - t0
+        row = {"iteration": it, "wins": int(tot[0]), "games": int(tot[1]), "win_rate": float(tot[0] / tot[1]),
+               "games_per_s": float(tot[1]) / dt, "moves_per_s": float(tot[2]) / dt, **info}
+        history.append(row)
+        log.log(**row)
+        if args.verbose and env.is_main:
+            print("Number of wins this batch: {}/{}  ({:.1f} games/s)".format(row["wins"], row["games"],
+                                                                             row["games_per_s"]), flush=True)
+        if folder and (it + 1) % args.save_every == 0:
+            path = os.path.join(folder, "weights.%05d.hdf5" % (it + 1))
+            if env.is_main:
+                learner_pol.save_weights(path)
+            agdist.barrier()
+            pool.append(path)
+    return {"history": history, "pool": pool}
+
+
+if __name__ == "__main__":
+    run()

@@ -1,0 +1,211 @@
+"""Value-network pipeline: self-play data generation + regression training.
+
+The reference only declares the value network (AlphaGo/models/value.py:12-43;
+``get_samples``/``train`` are TODO) and its trainer module is an empty file
+(AlphaGo/training/reinforcement_value_trainer.py).  This implements the
+paper's procedure:
+
+generate: for each game draw U ~ Uniform{1..max_u}; the SL policy plays moves
+  1..U-1, move U is uniformly random among sensible moves, then the RL policy
+  plays to the end.  The position after move U is recorded together with the
+  outcome z in {-1, 0, +1} from the perspective of the player to move there.
+  One position per game (avoids correlated samples).  Thousands of games run
+  in lock-step, two batched GPU forwards per ply.  Output: HDF5 with
+  ``states`` (N, 49, S, S) uint8 and ``outcomes`` (N,) int8.
+train: MSE regression with SGD (paper lr 0.003, value.py:8-9), DP across
+  ranks, HIP MFMA trunk + small fused head, random D4 augmentation.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .. import go
+from ..features import VALUE_FEATURES, Preprocess
+from ..io.h5lite import H5File, H5Writer
+from ..models.policy import CNNPolicy, CNNValue
+from ..parallel import dist as agdist
+from ..search.selfplay import BatchedSampler
+from ..utils.metrics import MetricsLogger
+from .engine import make_value_trainer
+
+LEARNING_RATE = .003
+DECAY = 8.664339379294006e-08
+
+
+def generate_positions(sl_policy: CNNPolicy, rl_policy: CNNPolicy, n_games: int, size: int = 19,
+                       max_u: int = 450, max_moves: int = 600, temperature: float = 1.0, seed: int = 0,
+                       features: Optional[List[str]] = None):
+    """Returns (planes uint8 (N, F, S, S), outcomes int8 (N,)) with N <= n_games."""
+    rng = np.random.default_rng(seed)
+    feats = Preprocess(features or VALUE_FEATURES)
+    sl = BatchedSampler(sl_policy, temperature, seed=seed)
+    rl = BatchedSampler(rl_policy, temperature, seed=seed + 1)
+    U = rng.integers(1, max_u + 1, size=n_games)
+    states = [go.GameState(size) for _ in range(n_games)]
+    recorded = [None] * n_games
+    rec_player = [0] * n_games
+    for ply in range(max_moves):
+        active = [i for i in range(n_games) if not states[i].is_end_of_game]
+        if not active:
+            break
+        g_sl = [i for i in active if ply < U[i] - 1]
+        g_rand = [i for i in active if ply == U[i] - 1]
+        g_rl = [i for i in active if ply > U[i] - 1]
+        for group, sampler in ((g_sl, sl), (g_rl, rl)):
+            if group:
+                moves, _, _ = sampler.select([states[i] for i in group])
+                for k, i in enumerate(group):
+                    states[i].do_move(moves[k])
+        for i in g_rand:
+            mask = states[i].legal_mask(False)
+            cand = np.flatnonzero(mask)
+            mv = go.PASS_MOVE if len(cand) == 0 else divmod(int(rng.choice(cand)), size)
+            states[i].do_move(mv)
+            recorded[i] = feats.state_to_uint8(states[i])
+            rec_player[i] = states[i].current_player
+    keep = [i for i in range(n_games) if recorded[i] is not None]
+    if not keep:
+        return np.zeros((0, feats.output_dim, size, size), np.uint8), np.zeros(0, np.int8)
+    planes = np.stack([recorded[i] for i in keep])
+    z = np.array([states[i].get_winner() * rec_player[i] for i in keep], dtype=np.int8)
+    return planes, z
+
+
+def generate_cli(argv=None):
+    p = argparse.ArgumentParser(description="Generate value-network training positions by self-play")
+    p.add_argument("sl_json")
+    p.add_argument("rl_json")
+    p.add_argument("outfile")
+    p.add_argument("--games", type=int, default=1024)
+    p.add_argument("--batch-games", type=int, default=512)
+    p.add_argument("--max-u", type=int, default=450)
+    p.add_argument("--seed", type=int, default=0)
+    a = p.parse_args(argv)
+    env = agdist.init_from_env()
+    sl = CNNPolicy.load_model(a.sl_json, device=env.device)
+    rl = CNNPolicy.load_model(a.rl_json, device=env.device)
+    out = a.outfile if env.world_size == 1 else "%s.rank%d" % (a.outfile, env.rank)
+    tmp = out + ".tmp"
+    n = 0
+    with H5Writer(tmp) as f:
+        f.attrs["features"] = np.array([x.encode() for x in VALUE_FEATURES])
+        st = f.stream_dataset("states", (Preprocess(VALUE_FEATURES).output_dim, sl.model.board, sl.model.board),
+                               np.uint8)
+        zs = []
+        done = 0
+        while done < a.games:
+            g = min(a.batch_games, a.games - done)
+            planes, z = generate_positions(sl, rl, g, size=sl.model.board, max_u=a.max_u,
+                                           seed=a.seed * 100003 + env.rank * 1009 + done)
+            st.append(planes)
+            zs.append(z)
+            done += g
+            n += len(z)
+        st.finish()
+        f.create_dataset("outcomes", data=np.concatenate(zs) if zs else np.zeros(0, np.int8))
+    os.replace(tmp, out)
+    return n
+
+
+class ValueDataset(object):
+    def __init__(self, path: str, device):
+        self.f = H5File(path)
+        self.states = torch.from_numpy(np.array(self.f["states"].read(), copy=True)).to(device)
+        self.z = torch.from_numpy(np.asarray(self.f["outcomes"].read()).astype(np.float32)).to(device)
+        self.device = device
+
+    def __len__(self):
+        return self.states.shape[0]
+
+    def batch(self, idx):
+        it = torch.from_numpy(np.asarray(idx, np.int64)).to(self.device)
+        return self.states.index_select(0, it), self.z.index_select(0, it)
+
+
+def train_cli(argv=None):
+    p = argparse.ArgumentParser(description="Train the value network on self-play positions")
+    p.add_argument("model", help="value-network JSON (CNNValue.save_model)")
+    p.add_argument("train_data")
+    p.add_argument("out_directory")
+    p.add_argument("--minibatch", "-B", type=int, default=32)
+    p.add_argument("--epochs", "-E", type=int, default=10)
+    p.add_argument("--learning-rate", "-r", type=float, default=LEARNING_RATE)
+    p.add_argument("--decay", "-d", type=float, default=DECAY)
+    p.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
+    p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--metrics", default=None)
+    p.add_argument("--verbose", "-v", action="store_true")
+    a = p.parse_args(argv)
+    env = agdist.init_from_env()
+    dev = env.device
+    val = CNNValue.load_model(a.model, device=dev)
+    data = ValueDataset(a.train_data, dev)
+    n = len(data)
+    perm = np.random.default_rng(a.seed).permutation(n)
+    n_train = int(a.train_val_test[0] * n)
+    n_val = int(a.train_val_test[1] * n)
+    tr_idx, va_idx = perm[:n_train], perm[n_train:n_train + n_val]
+    B, world, rank = a.minibatch, env.world_size, env.rank
+    trainer = make_value_trainer(val.model, B, a.learning_rate, a.decay, backend=a.backend, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(a.seed + rank)
+    if env.is_main:
+        os.makedirs(a.out_directory, exist_ok=True)
+    agdist.barrier()
+    meta = {"epochs": [], "best_epoch": 0, "training_data": a.train_data, "model_file": a.model}
+    log = MetricsLogger(a.metrics if env.is_main else None)
+    steps = max(1, n_train // (B * world))
+    cursor = 0
+    for ep in range(a.epochs):
+        t0 = time.perf_counter()
+        ls = torch.zeros((), device=dev, dtype=torch.float64)
+        for _ in range(steps):
+            gidx = np.take(tr_idx, np.arange(cursor, cursor + B * world) % max(1, n_train))
+            cursor = (cursor + B * world) % max(1, n_train)
+            x, z = data.batch(gidx[rank * B:(rank + 1) * B])
+            sym = torch.randint(0, 8, (B,), device=dev, dtype=torch.int32, generator=gen)
+            l, _ = trainer.step(x, z, sym)
+            ls += l.double()
+        agdist.all_reduce_sum_(ls)
+        logs = {"loss": float(ls) / (steps * B * world)}
+        if n_val:
+            vl, vn = torch.zeros((), device=dev, dtype=torch.float64), 0
+            mine = va_idx[rank::world]
+            for i in range(0, len(mine) - B + 1, B):
+                x, z = data.batch(mine[i:i + B])
+                l, _ = trainer.evaluate(x, z)
+                vl += l.double()
+                vn += B
+            st = torch.stack([vl, torch.tensor(float(vn), device=dev, dtype=torch.float64)])
+            agdist.all_reduce_sum_(st)
+            if float(st[1]) > 0:
+                logs["val_loss"] = float(st[0]) / float(st[1])
+        meta["epochs"].append(logs)
+        key = "val_loss" if "val_loss" in logs else "loss"
+        if logs[key] < meta["epochs"][meta["best_epoch"]][key]:
+            meta["best_epoch"] = ep
+        if env.is_main:
+            val.save_weights(os.path.join(a.out_directory, "weights.%05d.hdf5" % ep))
+            with open(os.path.join(a.out_directory, "metadata.json"), "w") as f:
+                json.dump(meta, f)
+            log.log(epoch=ep, positions_per_s=steps * B * world / (time.perf_counter() - t0), **logs)
+            if a.verbose:
+                print("epoch %d %s" % (ep, logs), flush=True)
+    return meta
+
+
+if __name__ == "__main__":
+    import sys
+
+    if len(sys.argv) > 1 and sys.argv[1] == "generate":
+        generate_cli(sys.argv[2:])
+    else:
+        train_cli(sys.argv[2:] if len(sys.argv) > 1 and sys.argv[1] == "train" else sys.argv[1:])

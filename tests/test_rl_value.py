@@ -1,0 +1,134 @@
+"""Self-play, RL policy training and value-network pipeline (small nets, 9x9)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from alphago_amd import go
+from alphago_amd.features import VALUE_FEATURES
+from alphago_amd.models.policy import CNNPolicy, CNNValue
+from alphago_amd.search.selfplay import BatchedSampler, play_games
+from alphago_amd.train import rl, value
+
+FEATS = ["board", "ones", "turns_since", "sensibleness"]
+
+
+def _policy(device, board=9):
+    return CNNPolicy(FEATS, board=board, filters_per_layer=16, layers=2, device=device)
+
+
+def _run_selfplay(device):
+    a, b = _policy(device), _policy(device)
+    rec = play_games(BatchedSampler(a, seed=1), BatchedSampler(b, seed=2), 6, size=9, max_moves=200,
+                     rng=np.random.default_rng(0))
+    assert len(rec.winners) == 6 and set(rec.learner_colors) <= {1, -1}
+    for planes, moves, st in zip(rec.planes, rec.moves, rec.states):
+        assert planes.shape[0] == moves.shape[0]
+        assert planes.shape[1:] == (a.preprocessor.output_dim, 9, 9)
+        assert len(st.history) <= 200
+    return rec
+
+
+def test_selfplay_cpu():
+    _run_selfplay(torch.device("cpu"))
+
+
+def test_sampler_respects_masks():
+    p = _policy(torch.device("cpu"))
+    gs = go.GameState(9)
+    for x in range(9):
+        for y in range(9):
+            if (x, y) != (0, 0):
+                gs.do_move((x, y), go.BLACK)
+    gs.current_player = go.BLACK
+    assert BatchedSampler(p).get_move(gs) is go.PASS_MOVE  # only an own eye left
+
+
+def _save_policy(tmp_path, device):
+    p = _policy(device)
+    j, w = str(tmp_path / "p.json"), str(tmp_path / "p.hdf5")
+    p.save_model(j, w)
+    return j, w
+
+
+def test_rl_cli_cpu(tmp_path):
+    j, w = _save_policy(tmp_path, "cpu")
+    folder = str(tmp_path / "pool")
+    out = rl.run([w, j, "--model_folder", folder, "--game_batch_size", "4", "--iterations", "2",
+                  "--save_every", "1", "--minibatch", "64", "--max-moves", "120", "--backend", "torch"])
+    assert len(out["history"]) == 2
+    assert os.path.exists(os.path.join(folder, "weights.00001.hdf5"))
+    assert len(out["pool"]) == 3
+    # reference-compat loss path
+    out2 = rl.run([w, j, "--game_batch_size", "2", "--iterations", "1", "--minibatch", "64", "--max-moves", "60",
+                   "--loss", "reference"])
+    assert out2["history"][0]["games"] == 2
+
+
+def test_reinforce_sign():
+    """A won game's moves become more likely, a lost game's less likely."""
+    from alphago_amd.search.selfplay import GameRecords
+    from alphago_amd.train.engine import TorchPolicyTrainer
+
+    torch.manual_seed(0)
+    pol = _policy(torch.device("cpu"))
+    tr = TorchPolicyTrainer(pol.model, 16, lr=1.0)
+    gs = go.GameState(9)
+    planes = pol.preprocessor.states_to_uint8([gs])
+    rec = GameRecords(planes=[planes, planes], moves=[np.array([40]), np.array([0])], winners=[1, 1],
+                      learner_colors=[1, -1])
+    p0 = torch.softmax(pol.model.logits_torch(torch.from_numpy(planes).float()), 1)[0]
+    rl.rl_update(tr, rec, 16, torch.device("cpu"))
+    p1 = torch.softmax(pol.model.logits_torch(torch.from_numpy(planes).float()), 1)[0]
+    assert p1[40] > p0[40] and p1[0] < p0[0]
+
+
+def test_value_generate_and_train_cpu(tmp_path):
+    cpu = torch.device("cpu")
+    sl, rlp = _policy(cpu), _policy(cpu)
+    planes, z = value.generate_positions(sl, rlp, 12, size=9, max_u=30, max_moves=150, seed=3,
+                                         features=FEATS + ["color"])
+    assert planes.shape[0] == z.shape[0] > 0 and set(np.unique(z)) <= {-1, 0, 1}
+    # full CLI path with the 49-plane value features
+    j, w = _save_policy(tmp_path, "cpu")
+    data = str(tmp_path / "v.h5")
+    n = value.generate_cli([j, j, data, "--games", "16", "--batch-games", "8", "--max-u", "20"])
+    assert n > 0
+    v = CNNValue(VALUE_FEATURES, board=9, filters_per_layer=8, layers=2, dense=16, device=cpu)
+    vj = str(tmp_path / "v.json")
+    v.save_model(vj)
+    meta = value.train_cli([vj, data, str(tmp_path / "vout"), "-B", "4", "-E", "2", "--backend", "torch"])
+    assert len(meta["epochs"]) == 2
+    assert os.path.exists(str(tmp_path / "vout" / "weights.00001.hdf5"))
+
+
+@pytest.mark.gpu
+def test_selfplay_and_rl_gpu(tmp_path, cuda_device):
+    _run_selfplay(cuda_device)
+    j, w = _save_policy(tmp_path, "cuda")
+    out = rl.run([w, j, "--game_batch_size", "8", "--iterations", "2", "--minibatch", "64", "--max-moves", "150",
+                  "--backend", "hip"])
+    assert len(out["history"]) == 2
+
+
+@pytest.mark.gpu
+def test_value_trainer_hip_matches_torch(cuda_device):
+    import copy
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import HipValueTrainer, TorchValueTrainer
+
+    torch.manual_seed(0)
+    net = ValueNet(49, board=19, filters_per_layer=64, layers=3, dense=32)
+    ref_net = copy.deepcopy(net)
+    B = 6
+    x = torch.randint(0, 2, (B, 49, 19, 19), dtype=torch.uint8, device=cuda_device)
+    z = torch.tensor([1, -1, 1, 0, -1, 1], dtype=torch.float32, device=cuda_device)
+    hip = HipValueTrainer(net, B, lr=0.01, device=cuda_device)
+    ref = TorchValueTrainer(ref_net, B, lr=0.01, device=cuda_device)
+    hip.compute_grads(x, z)
+    ref.compute_grads(x, z)
+    for name in hip.fp.names:
+        a, b = hip.fp.grad_views[name], ref.fp.grad_views[name]
+        cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
+        assert cos > 0.98, (name, cos)
