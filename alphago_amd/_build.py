@@ -135,10 +135,9 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
 
     def compile_one(src):
         obj = os.path.join(BUILD, "hip_" + os.path.basename(src) + ".o")
-        if src.endswith(".hip"):
-            cmd = [hipcc, "-x", "hip", *common, *hip_flags, *inc_flags, "-c", src, "-o", obj]
-        else:
-            cmd = [hipcc, *common, *inc_flags, "-c", src, "-o", obj]
+        # every translation unit is compiled for gfx950 only (the op registration
+        # file includes the kernel headers)
+        cmd = [hipcc, "-x", "hip", *common, *hip_flags, *inc_flags, "-c", src, "-o", obj]
         _run(cmd, verbose)
         return obj
 

@@ -12,6 +12,17 @@ typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 namespace agk {
 
+// Exact unsigned division by a runtime constant d (x < 2^32, d < 2^16):
+// q = (x * m) >> 40 with m = ceil(2^40 / d), computed once on the host.
+struct FastDiv {
+  uint32_t d;
+  uint64_t m;
+};
+inline FastDiv make_fastdiv(uint32_t d) { return FastDiv{d, ((1ull << 40) + d - 1) / d}; }
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)x * f.m) >> 40);
+}
+
 // 16-byte global -> LDS DMA (global_load_lds_dwordx4).  `lds_wave_base` must be
 // wave-uniform: the hardware writes lane i's 16 bytes at base + 16*i.
 __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {

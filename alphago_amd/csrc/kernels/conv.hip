@@ -34,15 +34,18 @@
 namespace agk {
 
 // ----------------------------------------------------------------- forward
-template <int BN, int MODE>
-__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvFwdArgs a) {
-  constexpr int BM = 128;
+template <int BN, int MODE, int BM>
+__global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
+  // BM/64 x 2 waves; each wave owns a 64(m) x BN/2(n) output tile
+  constexpr int NW = BM / 32;          // waves per workgroup
   constexpr int NB = BN / 32;  // 16-wide n blocks per wave (a wave covers BN/2 channels)
   constexpr int MB = 4;        // 16-wide m blocks per wave (a wave covers 64 pixels)
   constexpr int A_BYTES = BM * 128;
   constexpr int B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
-  constexpr int B_INSTR = BN / 32;  // glds instructions per wave for the weight tile
+  constexpr int B_ROWS_PW = BN / NW;   // weight rows staged per wave
+  constexpr int B_INSTR = B_ROWS_PW / 8;  // glds instructions per wave for the weight tile
+  static_assert(B_ROWS_PW % 8 == 0, "weight rows per wave must be a multiple of 8");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63;
@@ -61,9 +64,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvFwdArgs a) {
     const int r = wave * 32 + i * 8 + (lane >> 3);
     int m = m0 + r;
     m = m < a.M ? m : a.M - 1;
-    const int b = m / SS;
+    const int b = fdiv(m, a.divSS);
     const int rem = m - b * SS;
-    const int ii = rem / a.S;
+    const int ii = fdiv(rem, a.divS);
     const int jj = rem - ii * a.S;
     const int logical = (lane & 7) ^ ((r >> 1) & 7);
     arow[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + logical * 8;
@@ -71,7 +74,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvFwdArgs a) {
   int brow[B_INSTR];
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
-    const int r = wave * (BN / 4) + i * 8 + (lane >> 3);
+    const int r = wave * B_ROWS_PW + i * 8 + (lane >> 3);
     const int logical = (lane & 7) ^ ((r >> 1) & 7);
     brow[i] = (n0 + r) * a.Cin + logical * 8;
   }
@@ -88,7 +91,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvFwdArgs a) {
     for (int i = 0; i < 4; ++i) glds16(a.x + arow[i] + toff, base + (wave * 32 + i * 8) * 128);
     const __bf16* wt = a.w + (size_t)t * wtap + c0;
 #pragma unroll
-    for (int i = 0; i < B_INSTR; ++i) glds16(wt + brow[i], base + A_BYTES + (wave * (BN / 4) + i * 8) * 128);
+    for (int i = 0; i < B_INSTR; ++i) glds16(wt + brow[i], base + A_BYTES + (wave * B_ROWS_PW + i * 8) * 128);
   };
 
   f32x4 acc[NB][MB];
@@ -132,9 +135,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvFwdArgs a) {
   for (int j = 0; j < MB; ++j) {
     const int m = m0 + wm * 64 + j * 16 + (lane & 15);
     if (m >= a.M) continue;
-    const int b = m / SS;
+    const int b = fdiv(m, a.divSS);
     const int rem = m - b * SS;
-    const int ii = rem / a.S;
+    const int ii = fdiv(rem, a.divS);
     const int jj = rem - ii * a.S;
     const size_t ooff = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout;
 #pragma unroll
@@ -164,17 +167,30 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvFwdArgs a) {
   }
 }
 
-template <int BN, int MODE>
-static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
-  constexpr int smem = 2 * (128 * 128 + BN * 128);
+static int g_fwd_bm = 0;  // 0 = auto
+
+template <int BN, int MODE, int BM>
+static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int smem = 2 * (BM * 128 + BN * 128);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);
     attr = true;
   }
-  dim3 grid((a.M + 127) / 128, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE>), grid, dim3(256), smem, st, a);
+  dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM>), grid, dim3(BM * 2), smem, st, a);
 }
+
+template <int BN, int MODE>
+static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
+  int bm = g_fwd_bm;
+  if (bm == 0) bm = (a.M >= 256 * 512) ? 256 : 128;
+  if (bm == 256) launch_fwd_bm<BN, MODE, 256>(a, st);
+  else launch_fwd_bm<BN, MODE, 128>(a, st);
+}
+
+void set_conv_fwd_tile(int bm) { g_fwd_bm = bm; }
 
 template <int MODE>
 static void launch_fwd_mode(const ConvFwdArgs& a, hipStream_t st) {
@@ -183,22 +199,28 @@ static void launch_fwd_mode(const ConvFwdArgs& a, hipStream_t st) {
   else launch_fwd_t<64, MODE>(a, st);
 }
 
-void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st) {
+void launch_conv_fwd(const ConvFwdArgs& a_in, int mode, hipStream_t st) {
+  ConvFwdArgs a = a_in;
+  a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
+  a.divS = make_fastdiv((uint32_t)a.S);
   if (mode == MODE_BIAS_RELU) launch_fwd_mode<MODE_BIAS_RELU>(a, st);
   else if (mode == MODE_MASK) launch_fwd_mode<MODE_MASK>(a, st);
   else launch_fwd_mode<MODE_NONE>(a, st);
 }
 
 // ----------------------------------------------------------------- wgrad
-// 512 threads = 8 waves as 2 (n) x 4 (c).  K-step = 32 pixels.
-template <int WN, int WC>
+// 512 threads = 8 waves as 2 (n) x 4 (c).  One pipeline stage = KSUB sub-steps
+// of 32 pixels (one barrier per KSUB*32 pixels); each sub-step region is laid
+// out [16-channel block][32 px][16 ch] for the transpose reads.
+template <int WN, int WC, int KSUB>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int NBn = WN / 32;  // n blocks per wave (wave covers WN/2)
   constexpr int NBc = WC / 64;  // c blocks per wave (wave covers WC/4)
   constexpr int DZ_BYTES = WN * 64;  // [WN/16][32 px][16 ch] bf16
   constexpr int X_BYTES = WC * 64;
-  constexpr int STAGE = DZ_BYTES + X_BYTES;
-  constexpr int NINSTR = (WN + WC) / 16;  // 1 KB glds pieces per stage
+  constexpr int SUB = DZ_BYTES + X_BYTES;
+  constexpr int STAGE = SUB * KSUB;
+  constexpr int NINSTR = (WN + WC) / 16 * KSUB;  // 1 KB glds pieces per stage
   constexpr int IPW = (NINSTR + 7) / 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -213,31 +235,39 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int kh = t / a.K, kw = t - (t / a.K) * a.K;
   const int toff = (kh * a.HPi + kw) * a.Cin + c0;
   const int SS = a.S * a.S;
+  // a.ksteps_per_split is in units of one stage (KSUB*32 pixels)
   const int ks_begin = split * a.ksteps_per_split;
   int ks_end = ks_begin + a.ksteps_per_split;
-  const int nks_total = (a.M + 31) / 32;
+  const int nks_total = (a.M + 32 * KSUB - 1) / (32 * KSUB);
   if (ks_end > nks_total) ks_end = nks_total;
 
   auto stage = [&](int ks, int buf) {
-    const int px = ks * 32 + (lane >> 1);
-    int dzr, xr;
-    {
-      const int pm = px < a.M ? px : a.M - 1;
-      const int b = pm / SS;
-      const int rem = pm - b * SS;
-      const int ii = rem / a.S;
-      const int jj = rem - ii * a.S;
-      dzr = px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout : 0;  // 0 = zero border
-      xr = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + toff;
-    }
     const int half = (lane & 1) * 8;
     char* base = smem + buf * STAGE;
+    int dzr[KSUB], xr[KSUB];
+#pragma unroll
+    for (int sub = 0; sub < KSUB; ++sub) {
+      const int px = (ks * KSUB + sub) * 32 + (lane >> 1);
+      const int pm = px < a.M ? px : a.M - 1;
+      const int b = fdiv(pm, a.divSS);
+      const int rem = pm - b * SS;
+      const int ii = fdiv(rem, a.divS);
+      const int jx = rem - ii * a.S;
+      dzr[sub] = px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po) * a.Cout : 0;  // 0 = zero border
+      xr[sub] = ((b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi) * a.Cin + toff;
+    }
 #pragma unroll
     for (int i = 0; i < IPW; ++i) {
       const int j = wave * IPW + i;
       if (j < NINSTR) {
-        if (j < WN / 16) glds16(a.dz + dzr + n0 + j * 16 + half, base + j * 1024);
-        else glds16(a.x + xr + (j - WN / 16) * 16 + half, base + j * 1024);
+#pragma unroll
+        for (int sub = 0; sub < KSUB; ++sub) {
+          const int jj = j - sub * ((WN + WC) / 16);
+          if (jj < 0 || jj >= (WN + WC) / 16) continue;
+          char* dst = base + sub * SUB + jj * 1024;
+          if (jj < WN / 16) glds16(a.dz + dzr[sub] + n0 + jj * 16 + half, dst);
+          else glds16(a.x + xr[sub] + (jj - WN / 16) * 16 + half, dst);
+        }
       }
     }
   };
@@ -267,33 +297,36 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
   for (int ks = ks_begin; ks < ks_end; ++ks) {
     const int cur = (ks - ks_begin) & 1;
     if (ks + 1 < ks_end) stage(ks + 1, cur ^ 1);
-    const char* base = smem + cur * STAGE;
-    bf16x8 af[NBn], bfm[NBc];
 #pragma unroll
-    for (int i = 0; i < NBn; ++i) {
-      const char* cb = base + (wn * NBn + i) * 1024;
-      bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr0));
-      bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr1));
-      af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int j = 0; j < NBc; ++j) {
-      const char* cb = base + DZ_BYTES + (wc * NBc + j) * 1024;
-      bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr0));
-      bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr1));
-      bfm[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-#pragma unroll
-    for (int i = 0; i < NBn; ++i)
-#pragma unroll
-      for (int j = 0; j < NBc; ++j) acc[i][j] = mfma16x16x32(af[i], bfm[j], acc[i][j]);
-    if (do_bias) {
+    for (int sub = 0; sub < KSUB; ++sub) {
+      const char* base = smem + cur * STAGE + sub * SUB;
+      bf16x8 af[NBn], bfm[NBc];
 #pragma unroll
       for (int i = 0; i < NBn; ++i) {
-        float s = 0.f;
+        const char* cb = base + (wn * NBn + i) * 1024;
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr0));
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr1));
+        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
 #pragma unroll
-        for (int e = 0; e < 8; ++e) s += (float)af[i][e];
-        dbs[i] += s;
+      for (int j = 0; j < NBc; ++j) {
+        const char* cb = base + DZ_BYTES + (wc * NBc + j) * 1024;
+        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr0));
+        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr1));
+        bfm[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < NBn; ++i)
+#pragma unroll
+        for (int j = 0; j < NBc; ++j) acc[i][j] = mfma16x16x32(af[i], bfm[j], acc[i][j]);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < NBn; ++i) {
+          float s = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) s += (float)af[i][e];
+          dbs[i] += s;
+        }
       }
     }
     wait_vmcnt0();
@@ -324,19 +357,27 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
   }
 }
 
+constexpr int kWgradKsub = 1;
+
 template <int WN, int WC>
 static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
-  constexpr int smem = 2 * (WN + WC) * 64;
+  constexpr int KS = kWgradKsub;
+  constexpr int smem = 2 * (WN + WC) * 64 * KS;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
-  hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC>), grid, dim3(512), smem, st, a);
+  hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS>), grid, dim3(512), smem, st, a);
 }
 
-void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st) {
+int wgrad_stage_pixels() { return 32 * kWgradKsub; }
+
+void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
+  ConvWgradArgs a = a_in;
+  a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
+  a.divS = make_fastdiv((uint32_t)a.S);
   const bool n192 = a.Cout % 192 == 0, c192 = a.Cin % 192 == 0;
   const bool n128 = a.Cout % 128 == 0, c128 = a.Cin % 128 == 0;
   if (n192 && c192) launch_wgrad_t<192, 192>(a, st);

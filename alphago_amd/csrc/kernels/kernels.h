@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "common.h"
+
 namespace agk {
 
 enum { MODE_BIAS_RELU = 0, MODE_MASK = 1, MODE_NONE = 2 };
@@ -16,6 +18,7 @@ struct ConvFwdArgs {
   int M, S, Cin, Cout, K;
   int HPi, offi;       // input padded side, (input pad - K/2)
   int HPo, Po;         // output padded side and pad
+  FastDiv divSS, divS; // filled by the launcher
 };
 
 struct ConvWgradArgs {
@@ -26,6 +29,7 @@ struct ConvWgradArgs {
   int M, S, Cin, Cout, K, T;
   int HPi, offi, HPo, Po;
   int ksteps_per_split, nsplit;
+  FastDiv divSS, divS; // filled by the launcher
 };
 
 struct WgradReduceArgs {
@@ -76,7 +80,9 @@ struct PackWeightsArgs {
 };
 
 void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
+void set_conv_fwd_tile(int bm);  // 0 = auto, 128 or 256 (tuning / A-B tests)
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
+int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
 void launch_pack_input(const PackInputArgs& a, hipStream_t st);

@@ -76,7 +76,8 @@ void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Ten
   a.dbias_slab = dbslab.data_ptr<float>();
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K; a.T = (int)(K * K);
   a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
-  const int nks = (a.M + 31) / 32;
+  const int sp = agk::wgrad_stage_pixels();
+  const int nks = (a.M + sp - 1) / sp;
   a.nsplit = (int)nsplit;
   a.ksteps_per_split = (nks + a.nsplit - 1) / a.nsplit;
   agk::launch_conv_wgrad(a, cur_stream());
@@ -191,6 +192,8 @@ void pack_weights(at::TensorList ws, at::TensorList wf, at::TensorList wd) {
   }
 }
 
+void set_conv_tile(int64_t bm) { agk::set_conv_fwd_tile((int)bm); }
+
 void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
   CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
   TORCH_CHECK(p.numel() == g.numel(), "size mismatch");
@@ -209,6 +212,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P) -> ()");
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
+  m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {

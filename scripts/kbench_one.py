@@ -1,0 +1,19 @@
+"""Run one kernel many times (for PMC collection): fwd | dgrad | wgrad."""
+import sys, torch
+from alphago_amd import ops
+ops.load()
+which = sys.argv[1]; B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+dev = torch.device("cuda"); S, F = 19, 192; M = B * S * S
+x = ops.padded_empty(B, S, 1, F, dev); x[:, 1:20, 1:20].normal_()
+y = ops.padded_empty(B, S, 1, F, dev)
+w = torch.randn(F, F, 3, 3, device=dev) * 0.05
+wf = ops.packed_weight_like(w, F, F); wd = ops.packed_weight_like(w, F, F, True)
+ops.pack_weights([w], [wf], [wd])
+bias = torch.zeros(F, device=dev)
+ns = ops.wgrad_splits(M, 9)
+slab = torch.empty(ns, 9, F, F, device=dev); dbs = torch.zeros(ns, F, device=dev)
+for _ in range(10):
+    if which == "fwd": ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1)
+    elif which == "dgrad": ops.conv_fwd(x, wd, None, y, 3, S, 1, 1, mode=ops.MODE_MASK, mask=x)
+    else: ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1)
+torch.cuda.synchronize()
