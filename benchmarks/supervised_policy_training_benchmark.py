@@ -21,11 +21,20 @@ FIXTURE = "/root/reference/tests/test_data/hdf5/alphago-vs-lee-sedol-features.hd
 def main():
     backend = sys.argv[1] if len(sys.argv) > 1 else ("hip" if torch.cuda.is_available() else "torch")
     with tempfile.TemporaryDirectory() as d:
+        data = FIXTURE
+        if not os.path.exists(data):  # no reference checkout: same schema, synthetic content
+            import numpy as np
+            from alphago_amd.io.h5lite import H5Writer
+            data = os.path.join(d, "synthetic.h5")
+            rng = np.random.default_rng(0)
+            with H5Writer(data) as f:
+                f["states"] = rng.integers(0, 2, (1033, 12, 19, 19), dtype=np.uint8)
+                f["actions"] = rng.integers(0, 19, (1033, 2), dtype=np.uint8)
         pol = CNNPolicy(["board", "ones", "turns_since"], filters_per_layer=192, layers=12, device="cpu")
         j = os.path.join(d, "model.json")
         pol.save_model(j)
         metrics = os.path.join(d, "m.jsonl")
-        meta = run_training([j, FIXTURE, os.path.join(d, "out"), "-E", "3", "-B", "64", "-r", "0.003",
+        meta = run_training([j, data, os.path.join(d, "out"), "-E", "3", "-B", "64", "-r", "0.003",
                              "--backend", backend, "--metrics", metrics])
         rows = [json.loads(l) for l in open(metrics)]
         print(json.dumps({"backend": backend, "epochs": meta["epochs"],
