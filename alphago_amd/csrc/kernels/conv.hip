@@ -105,28 +105,42 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   const int xrow0 = (wm * 64 + (lane & 15)) * 128;
   const int wrow0 = A_BYTES + (wn * (BN / 2) + (lane & 15)) * 128;
 
+  auto read_frags = [&](const char* base, int kk, bf16x8 (&xf)[MB], bf16x8 (&wf)[NB]) {
+    const int choff = (((kk << 2) + (lane >> 4)) ^ swz) << 4;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) xf[j] = *(const bf16x8*)(base + xrow0 + j * 16 * 128 + choff);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) wf[i] = *(const bf16x8*)(base + wrow0 + i * 16 * 128 + choff);
+  };
+  auto mfmas = [&](const bf16x8 (&xf)[MB], const bf16x8 (&wf)[NB]) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+  };
+
+  // software pipeline: the first half (k 0..31) of step ks+1 is read right
+  // after the barrier that publishes it, so its LDS latency hides under the
+  // staging issue and the second-half reads of the next iteration.
+  bf16x8 xa[MB], wa[NB], xb[MB], wb[NB];
   stage(0, 0);
   wait_vmcnt0();
   __syncthreads();
+  read_frags(smem, 0, xa, wa);
   for (int ks = 0; ks < nK; ++ks) {
     const int cur = ks & 1;
-    if (ks + 1 < nK) stage(ks + 1, cur ^ 1);
     const char* base = smem + cur * STAGE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int choff = (((kk << 2) + (lane >> 4)) ^ swz) << 4;
-      bf16x8 xf[MB], wf[NB];
-#pragma unroll
-      for (int j = 0; j < MB; ++j) xf[j] = *(const bf16x8*)(base + xrow0 + j * 16 * 128 + choff);
-#pragma unroll
-      for (int i = 0; i < NB; ++i) wf[i] = *(const bf16x8*)(base + wrow0 + i * 16 * 128 + choff);
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
-    }
+    if (ks + 1 < nK) stage(ks + 1, cur ^ 1);
+    read_frags(base, 1, xb, wb);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mfmas(xa, wa);
+    mfmas(xb, wb);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
     wait_vmcnt0();
     __syncthreads();
+    if (ks + 1 < nK) read_frags(base + (cur ^ 1) * STAGE - cur * STAGE, 0, xa, wa);
   }
 
   // --- epilogue: lane owns channels n..n+3 of pixel m for every (i, j) block
@@ -167,6 +181,193 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   }
 }
 
+// ------------------------------------------------------ forward, halo variant
+// 3x3 convolutions whose input and output share the padded geometry (all
+// layers but the first): M runs over *padded* output positions, so tap t reads
+// input row q + off_t with a constant off_t = (kh-1)*HP + (kw-1).  A workgroup
+// owns 256 consecutive positions; the input rows [q0-HP-1, q0+256+HP+1) of one
+// 64-channel chunk are staged ONCE into LDS (the halo) and reused by all 9
+// taps, so per K-step only the 24 KB weight tile streams (3-deep ring, counted
+// vmcnt, raw s_barrier so the next loads stay in flight across barriers).
+// Border positions are computed (18% extra MFMA at S=19) and not stored.
+constexpr int HALO_BM = 256;
+constexpr int HALO_ROWS = 320;      // >= 256 + 2*(HP+1) for S <= 19, 40 x 1 KB pieces
+constexpr int HALO_PW = HALO_ROWS / 8 / 8;  // glds pieces per wave (8 waves)
+
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+template <int BN, int MODE>
+__global__ __launch_bounds__(512, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
+  constexpr int NB = BN / 32;           // 16-wide n blocks per wave (wave covers BN/2)
+  constexpr int MB = 4;                 // wave covers 64 positions
+  constexpr int W_BYTES = BN * 128;     // one (tap, 64-ch chunk) weight tile
+  constexpr int H_BYTES = HALO_ROWS * 128;
+  constexpr int NW_PW = BN / 64;        // weight glds pieces per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;                      // 2 x H_BYTES
+  char* const wbuf = smem + 2 * H_BYTES;        // 3 x W_BYTES
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wm = wave >> 1, wn = wave & 1;
+  const int q0 = blockIdx.x * HALO_BM;
+  const int n0 = blockIdx.y * BN;
+  const int HP = a.HPo;
+  const int G = HP + 1;                 // max |tap offset|
+  const int Q = a.M;                    // number of padded positions (B * HP * HP)
+  const int CC = a.Cin >> 6;
+  const int nK = 9 * CC;
+
+  // halo staging addresses: this lane's rows for each of its HALO_PW pieces
+  int hrow[HALO_PW];
+#pragma unroll
+  for (int i = 0; i < HALO_PW; ++i) {
+    const int r = (wave * HALO_PW + i) * 8 + (lane >> 3);
+    int q = q0 - G + r;
+    q = q < 0 ? 0 : (q >= Q ? Q - 1 : q);
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    hrow[i] = q * a.Cin + logical * 8;
+  }
+  int wrow[NW_PW];
+#pragma unroll
+  for (int i = 0; i < NW_PW; ++i) {
+    const int r = (wave * NW_PW + i) * 8 + (lane >> 3);
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    wrow[i] = (n0 + r) * a.Cin + logical * 8;
+  }
+  const size_t wtap = (size_t)a.Cout * a.Cin;
+  auto stage_halo = [&](int c, int buf) {
+    char* base = hbuf + buf * H_BYTES;
+#pragma unroll
+    for (int i = 0; i < HALO_PW; ++i) glds16(a.x + hrow[i] + (c << 6), base + (wave * HALO_PW + i) * 1024);
+  };
+  auto stage_w = [&](int ks, int slot) {
+    const int c = ks / 9;
+    const int t = ks - c * 9;
+    const __bf16* wt = a.w + (size_t)t * wtap + (c << 6);
+    char* base = wbuf + slot * W_BYTES;
+#pragma unroll
+    for (int i = 0; i < NW_PW; ++i) glds16(wt + wrow[i], base + (wave * NW_PW + i) * 1024);
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wr0 = (wn * (BN / 2) + (lane & 15)) * 128;
+  const int wswz = (lane & 15) >> 1;
+
+  stage_halo(0, 0);
+  stage_w(0, 0);
+  if (nK > 1) stage_w(1, 1);
+  wait_vmcnt0();
+  __syncthreads();
+
+  for (int ks = 0; ks < nK; ++ks) {
+    const int c = ks / 9;
+    const int t = ks - c * 9;
+    const bool issue_halo = (t == 4) && (c + 1 < CC);
+    const bool issue_w = ks + 2 < nK;
+    if (issue_halo) stage_halo(c + 1, (c + 1) & 1);
+    if (issue_w) stage_w(ks + 2, (ks + 2) % 3);
+    const char* hb = hbuf + (c & 1) * H_BYTES;
+    const char* wb = wbuf + (ks % 3) * W_BYTES;
+    const int kh = t / 3, kw = t - (t / 3) * 3;
+    const int rbase = wm * 64 + (lane & 15) + G + (kh - 1) * HP + (kw - 1);
+    const int xswz = (rbase >> 1) & 7;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = (kk << 2) + (lane >> 4);
+      bf16x8 xf[MB], wf[NB];
+#pragma unroll
+      for (int j = 0; j < MB; ++j) xf[j] = *(const bf16x8*)(hb + (rbase + j * 16) * 128 + ((ch ^ xswz) << 4));
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wf[i] = *(const bf16x8*)(wb + wr0 + i * 16 * 128 + ((ch ^ wswz) << 4));
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+    }
+    // the next K-step needs W(ks+1) (and the halo if a new chunk starts); the
+    // loads issued this iteration may stay in flight across the barrier
+    if (issue_w && issue_halo) vmcnt_wait<NW_PW + HALO_PW>();
+    else if (issue_w) vmcnt_wait<NW_PW>();
+    else if (issue_halo) vmcnt_wait<HALO_PW>();
+    else vmcnt_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+
+  // --- epilogue: skip border positions (they must stay zero)
+  const int nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    const int q = q0 + wm * 64 + j * 16 + (lane & 15);
+    if (q >= Q) continue;
+    const int b = fdiv(q, a.divSS);       // divSS = HP*HP here
+    const int rem = q - b * HP * HP;
+    const int ii = fdiv(rem, a.divS);     // divS = HP here
+    const int jj = rem - ii * HP;
+    if (ii < a.Po || ii >= a.Po + a.S || jj < a.Po || jj >= a.Po + a.S) continue;
+    const size_t ooff = (size_t)q * a.Cout;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int n = nbase + i * 16;
+      f32x4 v = acc[i][j];
+      if constexpr (MODE == MODE_BIAS_RELU) {
+        const f32x4 bb = *(const f32x4*)(a.bias + n);
+        v[0] = fmaxf(v[0] + bb[0], 0.f);
+        v[1] = fmaxf(v[1] + bb[1], 0.f);
+        v[2] = fmaxf(v[2] + bb[2], 0.f);
+        v[3] = fmaxf(v[3] + bb[3], 0.f);
+      } else if constexpr (MODE == MODE_MASK) {
+        const bf16x4 mk = *(const bf16x4*)(a.mask + ooff + n);
+        v[0] = (float)mk[0] > 0.f ? v[0] : 0.f;
+        v[1] = (float)mk[1] > 0.f ? v[1] : 0.f;
+        v[2] = (float)mk[2] > 0.f ? v[2] : 0.f;
+        v[3] = (float)mk[3] > 0.f ? v[3] : 0.f;
+      }
+      bf16x4 o;
+      o[0] = (__bf16)v[0];
+      o[1] = (__bf16)v[1];
+      o[2] = (__bf16)v[2];
+      o[3] = (__bf16)v[3];
+      *(bf16x4*)(a.y + ooff + n) = o;
+    }
+  }
+}
+
+template <int BN, int MODE>
+static void launch_fwd_halo(const ConvFwdArgs& a_in, hipStream_t st) {
+  constexpr int smem = 2 * HALO_ROWS * 128 + 3 * BN * 128;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_halo_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);
+    attr = true;
+  }
+  ConvFwdArgs a = a_in;
+  const int B = a.M / (a.S * a.S);
+  a.M = B * a.HPo * a.HPo;  // padded positions
+  a.divSS = make_fastdiv((uint32_t)(a.HPo * a.HPo));
+  a.divS = make_fastdiv((uint32_t)a.HPo);
+  dim3 grid((a.M + HALO_BM - 1) / HALO_BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_halo_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
+}
+
 static int g_fwd_bm = 0;  // 0 = auto
 
 template <int BN, int MODE, int BM>
@@ -184,8 +385,14 @@ static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
 
 template <int BN, int MODE>
 static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
+  const bool halo_ok = a.K == 3 && a.HPi == a.HPo && a.offi == 0 && a.Po == 1 && a.HPo + 1 <= 32 &&
+                       (a.S + 2) * (a.S + 2) * 0 + 256 + 2 * (a.HPo + 1) <= HALO_ROWS;
+  if (halo_ok && g_fwd_bm == -1) {  // opt-in: slower at S=19 (18% border work), see profiles/
+    launch_fwd_halo<BN, MODE>(a, st);
+    return;
+  }
   int bm = g_fwd_bm;
-  if (bm == 0) bm = (a.M >= 256 * 512) ? 256 : 128;
+  if (bm <= 0) bm = (a.M >= 256 * 512) ? 256 : 128;
   if (bm == 256) launch_fwd_bm<BN, MODE, 256>(a, st);
   else launch_fwd_bm<BN, MODE, 128>(a, st);
 }

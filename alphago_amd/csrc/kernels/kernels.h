@@ -80,7 +80,7 @@ struct PackWeightsArgs {
 };
 
 void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
-void set_conv_fwd_tile(int bm);  // 0 = auto, 128 or 256 (tuning / A-B tests)
+void set_conv_fwd_tile(int bm);  // 0 = auto, -1 = halo kernel, 128/256 = gather kernel tile (A/B tests)
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);

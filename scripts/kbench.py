@@ -36,7 +36,7 @@ def timeit(fn):
 res = {}
 fl3 = 2.0 * M * F * F * 9
 fl1 = 2.0 * M * F * 64 * 25
-for bm in (128, 256):
+for bm in (128, 256, -1):
     torch.ops.alphago_amd.set_conv_tile(bm)
     res["fwd3x3_bm%d" % bm] = timeit(lambda: ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1))
     res["dgrad3x3_bm%d" % bm] = timeit(lambda: ops.conv_fwd(x, wd, None, y, 3, S, 1, 1, mode=ops.MODE_MASK, mask=x))
