@@ -202,6 +202,37 @@ PYBIND11_MODULE(_engine, m) {
       },
       py::arg("states"), py::arg("features"), py::arg("threads") = 8);
 
+  m.def(
+      "encode_batch",
+      [](const std::vector<const GameState*>& states, bool ladder, int threads) -> py::tuple {
+        const ssize_t B = (ssize_t)states.size();
+        const int np = B ? states[0]->np : 0;
+        for (auto* s : states)
+          if (s->np != np) throw py::value_error("all states must have the same size");
+        py::array_t<int8_t> board({B, (ssize_t)np});
+        py::array_t<uint8_t> ages({B, (ssize_t)np});
+        py::array_t<int32_t> meta({B, (ssize_t)2});
+        py::array_t<uint8_t> lad({ladder ? B : (ssize_t)0, (ssize_t)np});
+        int8_t* pb = board.mutable_data();
+        uint8_t* pa = ages.mutable_data();
+        int32_t* pm = meta.mutable_data();
+        uint8_t* pl = ladder ? lad.mutable_data() : nullptr;
+        {
+          py::gil_scoped_release rel;
+          int T = std::max(1, std::min(threads, (int)B));
+          std::vector<std::thread> pool;
+          for (int t = 0; t < T; ++t)
+            pool.emplace_back([&, t]() {
+              for (ssize_t i = t; i < B; i += T)
+                encode_state(*states[i], pb + i * np, pa + i * np, pm + 2 * i, pl ? pl + i * np : nullptr);
+            });
+          for (auto& th : pool) th.join();
+        }
+        py::object l = ladder ? py::object(lad) : py::object(py::none());
+        return py::make_tuple(board, ages, meta, l);
+      },
+      py::arg("states"), py::arg("ladder") = false, py::arg("threads") = 8);
+
   bind_mcts(m);
   bind_lzf(m);
 }

@@ -109,6 +109,31 @@ bool ladder_escape_at(const GameState& s, int m) {
   return false;
 }
 
+// ---------------------------------------------------------------- GPU encoding
+void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder) {
+  const int np = s.np;
+  for (int p = 0; p < np; ++p) board[p] = (int8_t)s.board[p];
+  std::memset(ages, 255, np);
+  int depth = 0;
+  for (int k = (int)s.history.size() - 1; k >= 0; --k) {  // same walk as F_TURNS_SINCE
+    int mv = s.history[k];
+    if (mv != PASS && s.board[mv] != EMPTY && ages[mv] == 255) ages[mv] = (uint8_t)depth;
+    if (depth < 7) ++depth;
+  }
+  meta[0] = s.ko;
+  meta[1] = s.current_player;
+  if (ladder) {
+    for (int p = 0; p < np; ++p) {
+      uint8_t v = 0;
+      if (s.board[p] == EMPTY && s.is_legal(p)) {
+        if (ladder_capture_at(s, p)) v |= 1;
+        if (ladder_escape_at(s, p)) v |= 2;
+      }
+      ladder[p] = v;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- planes
 int featurize(const GameState& s, const int* fids, int nf, uint8_t* out) {
   const int np = s.np;

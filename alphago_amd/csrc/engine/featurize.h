@@ -36,6 +36,12 @@ const char* feature_name(int fid);
 // Write planes for one state; returns the number of planes written.
 int featurize(const GameState& s, const int* fids, int nf, uint8_t* out);
 
+// Compact encoding consumed by the GPU featurizer (kernels/featurize.hip):
+// board[p] in {-1,0,1}; ages[p] = turns_since plane (0..7) or 255; meta =
+// {ko or -1, player to move}; ladder (optional) bit0 = ladder capture,
+// bit1 = ladder escape (only computed when requested: it is the expensive part).
+void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder);
+
 // Ladder reading (paper features; NotImplementedError in the reference
 // preprocessing.py:147-152).  Exposed for tests.
 bool ladder_capture_at(const GameState& s, int move);

@@ -160,6 +160,25 @@ void Forest::leaf_features(uint8_t* out, int threads) const {
   for (auto& th : pool) th.join();
 }
 
+void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) const {
+  int L = (int)pending_.size();
+  if (L == 0) return;
+  const int np = leaf_states_[0].np;
+  int T = std::max(1, std::min(ladder ? threads : 1, L));  // without ladders this is a memcpy-class walk
+  auto work = [&](int t) {
+    for (int i = t; i < L; i += T)
+      encode_state(leaf_states_[i], board + (size_t)i * np, ages + (size_t)i * np, meta + 2 * i,
+                   ladder ? ladder + (size_t)i * np : nullptr);
+  };
+  if (T == 1) {
+    work(0);
+    return;
+  }
+  std::vector<std::thread> pool;
+  for (int t = 0; t < T; ++t) pool.emplace_back(work, t);
+  for (auto& th : pool) th.join();
+}
+
 void Forest::leaf_masks(uint8_t* out) const {
   for (size_t i = 0; i < pending_.size(); ++i) {
     const GameState& s = leaf_states_[i];
@@ -397,6 +416,21 @@ void bind_mcts(py::module_& m) {
             return L;
           },
           py::arg("ptr"), py::arg("capacity"), py::arg("threads") = 8)
+      .def(
+          "leaf_encode_into",
+          [](const Forest& f, uintptr_t board, uintptr_t ages, uintptr_t meta, uintptr_t ladder, size_t capacity,
+             int threads) {
+            int L = f.n_pending();
+            if (L == 0) return 0;
+            if ((size_t)L > capacity) throw py::value_error("leaf_encode_into: buffer too small");
+            py::gil_scoped_release r;
+            f.leaf_encode(reinterpret_cast<int8_t*>(board), reinterpret_cast<uint8_t*>(ages),
+                          reinterpret_cast<int32_t*>(meta), ladder ? reinterpret_cast<uint8_t*>(ladder) : nullptr,
+                          threads);
+            return L;
+          },
+          py::arg("board"), py::arg("ages"), py::arg("meta"), py::arg("ladder"), py::arg("capacity"),
+          py::arg("threads") = 8)
       .def("leaf_masks",
            [](const Forest& f) {
              int L = f.n_pending();

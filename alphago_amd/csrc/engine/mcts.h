@@ -62,6 +62,8 @@ class Forest {
   // uint8 features (L, F, n, n) and sensible-move masks (L, n*n); threaded.
   void leaf_features(uint8_t* out, int threads) const;
   void leaf_masks(uint8_t* out) const;
+  // compact GPU-featurizer encoding of the pending leaves (see encode_state)
+  void leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) const;
   // priors (L, n*n) float32 (any non-negative scores; renormalised over sensible moves), values (L,)
   void apply(const float* priors, const float* values);
   void add_root_noise(int t, double alpha, double eps);

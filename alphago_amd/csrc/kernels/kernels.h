@@ -79,6 +79,25 @@ struct PackWeightsArgs {
   int nlayers;
 };
 
+constexpr int kFzMaxFeatures = 16;
+constexpr int kFzMaxChannels = 64;
+struct FeaturizeArgs {
+  const int8_t* board;    // [B][S*S] in {-1,0,1}
+  const uint8_t* ages;    // [B][S*S] turns_since plane or 255
+  const int* meta;        // [B][2] {ko or -1, player to move}
+  const uint8_t* ladder;  // [B][S*S] bit0 capture, bit1 escape; or null
+  uint8_t* planes;        // [B][nplanes][S][S] or null
+  __bf16* nhwc;           // [B][S+2P][S+2P][Cp] or null
+  uint8_t* sensible;      // [B][S*S] or null
+  uint8_t* legal;         // [B][S*S] or null
+  int* overflow;          // [B] or null (set to 1 when the eye DFS overflowed)
+  int B, S, P, Cp, nf, nplanes, need_eye;
+  int fids[kFzMaxFeatures];
+  int fplanes[kFzMaxFeatures];
+  uint8_t chan_feat[kFzMaxChannels];
+  uint8_t chan_plane[kFzMaxChannels];
+};
+
 void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 void set_conv_fwd_tile(int bm);  // 0 = auto, -1 = halo kernel, 128/256 = gather kernel tile (A/B tests)
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
@@ -87,6 +106,7 @@ void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
 void launch_pack_input(const PackInputArgs& a, hipStream_t st);
 void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st);
+void launch_featurize(const FeaturizeArgs& a, hipStream_t st);
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
 
 }  // namespace agk

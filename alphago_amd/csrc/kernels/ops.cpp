@@ -192,6 +192,70 @@ void pack_weights(at::TensorList ws, at::TensorList wf, at::TensorList wd) {
   }
 }
 
+// board: (B, S*S) int8; ages: (B, S*S) uint8; meta: (B, 2) int32; fids: feature ids
+// (engine numbering) with their plane counts; every output optional.
+void featurize(const Tensor& board, const Tensor& ages, const Tensor& meta, const c10::optional<Tensor>& ladder,
+               at::IntArrayRef fids, at::IntArrayRef fplanes, const c10::optional<Tensor>& planes,
+               const c10::optional<Tensor>& nhwc, const c10::optional<Tensor>& sensible,
+               const c10::optional<Tensor>& legal, const c10::optional<Tensor>& overflow, int64_t S, int64_t P) {
+  TORCH_CHECK(board.scalar_type() == at::kChar && board.is_contiguous() && board.dim() == 2, "board: int8 (B, S*S)");
+  TORCH_CHECK(ages.scalar_type() == at::kByte && ages.is_contiguous() && ages.sizes() == board.sizes(), "ages: uint8 (B, S*S)");
+  TORCH_CHECK(meta.scalar_type() == at::kInt && meta.is_contiguous() && meta.dim() == 2 && meta.size(1) == 2, "meta: int32 (B, 2)");
+  TORCH_CHECK(S >= 2 && S <= 19 && board.size(1) == S * S, "board size");
+  TORCH_CHECK(fids.size() == fplanes.size() && (int)fids.size() <= agk::kFzMaxFeatures, "feature list");
+  CHECK_DEV(board); CHECK_DEV(ages); CHECK_DEV(meta);
+  const int64_t B = board.size(0), NP = S * S;
+  TORCH_CHECK(meta.size(0) == B, "meta rows");
+  agk::FeaturizeArgs a{};
+  a.board = board.data_ptr<int8_t>();
+  a.ages = ages.data_ptr<uint8_t>();
+  a.meta = meta.data_ptr<int>();
+  a.B = (int)B; a.S = (int)S; a.P = (int)P; a.nf = (int)fids.size();
+  int np = 0;
+  for (size_t i = 0; i < fids.size(); ++i) {
+    TORCH_CHECK(fids[i] >= 0 && fids[i] < 13 && fplanes[i] >= 1 && fplanes[i] <= 8, "bad feature");
+    a.fids[i] = (int)fids[i];
+    a.fplanes[i] = (int)fplanes[i];
+    for (int k = 0; k < fplanes[i]; ++k, ++np) {
+      TORCH_CHECK(np < agk::kFzMaxChannels, "too many planes");
+      a.chan_feat[np] = (uint8_t)fids[i];
+      a.chan_plane[np] = (uint8_t)k;
+    }
+    a.need_eye |= (fids[i] == 9);
+  }
+  a.nplanes = np;
+  if (sensible.has_value()) a.need_eye = 1;
+  if (ladder.has_value()) {
+    TORCH_CHECK(ladder->scalar_type() == at::kByte && ladder->is_contiguous() && ladder->sizes() == board.sizes(), "ladder");
+    a.ladder = ladder->data_ptr<uint8_t>();
+  }
+  if (planes.has_value()) {
+    TORCH_CHECK(planes->scalar_type() == at::kByte && planes->is_contiguous() && planes->numel() == B * np * NP, "planes");
+    a.planes = planes->data_ptr<uint8_t>();
+  }
+  if (nhwc.has_value()) {
+    CHECK_BF16(*nhwc); CHECK_CONTIG(*nhwc);
+    TORCH_CHECK(nhwc->dim() == 4 && nhwc->size(0) == B && nhwc->size(1) == S + 2 * P && nhwc->size(2) == S + 2 * P &&
+                nhwc->size(3) >= np && nhwc->size(3) % 8 == 0 && nhwc->size(3) <= agk::kFzMaxChannels, "nhwc");
+    a.nhwc = bfp_mut(*nhwc);
+    a.Cp = (int)nhwc->size(3);
+  }
+  if (sensible.has_value()) {
+    TORCH_CHECK(sensible->scalar_type() == at::kByte && sensible->is_contiguous() && sensible->numel() == B * NP, "sensible");
+    a.sensible = sensible->data_ptr<uint8_t>();
+  }
+  if (legal.has_value()) {
+    TORCH_CHECK(legal->scalar_type() == at::kByte && legal->is_contiguous() && legal->numel() == B * NP, "legal");
+    a.legal = legal->data_ptr<uint8_t>();
+  }
+  if (overflow.has_value()) {
+    TORCH_CHECK(overflow->scalar_type() == at::kInt && overflow->is_contiguous() && overflow->numel() == B, "overflow");
+    a.overflow = overflow->data_ptr<int>();
+  }
+  if (B == 0) return;
+  agk::launch_featurize(a, cur_stream());
+}
+
 void set_conv_tile(int64_t bm) { agk::set_conv_fwd_tile((int)bm); }
 
 void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
@@ -212,6 +276,9 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P) -> ()");
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
+  m.def(
+      "featurize(Tensor board, Tensor ages, Tensor meta, Tensor? ladder, int[] fids, int[] fplanes, Tensor(a!)? planes, "
+      "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
   m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
 }
 
@@ -223,4 +290,5 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("pack_input", &pack_input);
   m.impl("pack_weights", &pack_weights);
   m.impl("sgd_update", &sgd_update);
+  m.impl("featurize", &featurize);
 }

@@ -6,6 +6,12 @@ batch bucket into a HIP graph (torch.cuda.CUDAGraph is hipGraph on ROCm) and
 replayed: a search step is one H2D copy, one graph launch and one D2H copy,
 instead of ~15 kernel launches.  Batches are padded up to the next bucket.
 
+With a feature list, ``evaluate_encoded`` takes the engine's compact board
+encoding (~2 bytes/point, ``Forest.leaf_encode_into`` / ``encode_batch``)
+instead of uint8 planes: the GPU featurizer (ops/gpu_features.py) runs as the
+first node of the same graph, writing the conv input and the sensible-move
+mask directly (24x less H2D traffic than 48 uint8 planes, no CPU featurizing).
+
 Reference paths replaced: CNNPolicy.forward / batch_eval_state
 (policy.py:26-79) which featurised in Python and ran a Theano function per
 call; MCTS policy/value callables (mcts.py:107-118).
@@ -30,7 +36,8 @@ class _Bucket:
 class HipTrunkInference:
     """Forward-only runner of a ConvStack (+ head) on the HIP kernels."""
 
-    def __init__(self, net, device, buckets: Sequence[int] = DEFAULT_BUCKETS, use_graphs: bool = True):
+    def __init__(self, net, device, buckets: Sequence[int] = DEFAULT_BUCKETS, use_graphs: bool = True,
+                 feature_list: Optional[Sequence[str]] = None):
         ops.load()
         self.net = net
         self.device = torch.device(device)
@@ -48,7 +55,22 @@ class HipTrunkInference:
         self.head_w = torch.zeros(self.F, device=dev)
         self.head_b = torch.zeros(1, device=dev)
         self._b: Dict[int, _Bucket] = {}
+        self.fz = None
+        if feature_list is not None:
+            from ..ops.gpu_features import GpuFeaturizer
+            fz = GpuFeaturizer(feature_list, board=self.S, device=dev)
+            if fz.nplanes != self.C0:
+                raise ValueError("feature list has %d planes, network expects %d" % (fz.nplanes, self.C0))
+            self.fz = fz
         self.sync_weights()
+
+    @property
+    def supports_encoded(self) -> bool:
+        return self.fz is not None
+
+    @property
+    def needs_ladder(self) -> bool:
+        return self.fz is not None and self.fz.need_ladder
 
     @torch.no_grad()
     def sync_weights(self) -> None:
@@ -80,13 +102,26 @@ class HipTrunkInference:
         bk.Y = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(2)]
         self._alloc_outputs(bk)
         bk.graph = None
+        bk.graph_enc = None
+        if self.fz is not None:
+            NP = S * S
+            bk.e_board = torch.zeros((B, NP), dtype=torch.int8, device=dev)
+            bk.e_ages = torch.full((B, NP), 255, dtype=torch.uint8, device=dev)
+            bk.e_meta = torch.tensor([[-1, 1]] * B, dtype=torch.int32, device=dev)
+            bk.e_ladder = torch.zeros((B, NP), dtype=torch.uint8, device=dev) if self.fz.need_ladder else None
+            bk.ovf = torch.zeros((B,), dtype=torch.int32, device=dev)
         return bk
 
     def _alloc_outputs(self, bk):
         bk.probs = torch.zeros((bk.B, self.S * self.S), device=self.device)
 
-    def _trunk(self, bk) -> torch.Tensor:
-        ops.pack_input(bk.planes, bk.X0, self.P0)
+    def _trunk(self, bk, encoded: bool = False) -> torch.Tensor:
+        if encoded:
+            bk.ovf.zero_()
+            self.fz.run(bk.e_board, bk.e_ages, bk.e_meta, bk.e_ladder, nhwc=bk.X0, P=self.P0, sensible=bk.legal,
+                        overflow=bk.ovf)
+        else:
+            ops.pack_input(bk.planes, bk.X0, self.P0)
         x, pin = bk.X0, self.P0
         for l in range(self.L):
             y = bk.Y[l % 2]
@@ -97,32 +132,65 @@ class HipTrunkInference:
     def _head(self, bk, y):
         ops.policy_head_probs(y, self.head_w, self.head_b, bk.probs, self.S, legal=bk.legal)
 
-    def _run(self, bk):
-        self._head(bk, self._trunk(bk))
+    def _run(self, bk, encoded: bool = False):
+        self._head(bk, self._trunk(bk, encoded))
 
-    def _get(self, n: int) -> _Bucket:
+    def _capture(self, bk, encoded: bool):
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._run(bk, encoded)  # warm-up (also sets kernel attributes outside capture)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._run(bk, encoded)
+        return g
+
+    def _get(self, n: int, encoded: bool = False) -> _Bucket:
         B = self.bucket_for(n)
         if B not in self._b:
-            bk = self._make_bucket(B)
-            self._b[B] = bk
-            if self.use_graphs:
-                s = torch.cuda.Stream(device=self.device)
-                s.wait_stream(torch.cuda.current_stream(self.device))
-                with torch.cuda.stream(s):
-                    self._run(bk)  # warm-up (also sets kernel attributes outside capture)
-                torch.cuda.current_stream(self.device).wait_stream(s)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._run(bk)
-                bk.graph = g
-        return self._b[B]
+            self._b[B] = self._make_bucket(B)
+        bk = self._b[B]
+        if self.use_graphs:
+            if encoded and bk.graph_enc is None:
+                bk.graph_enc = self._capture(bk, True)
+            elif not encoded and bk.graph is None:
+                bk.graph = self._capture(bk, False)
+        return bk
+
+    @torch.no_grad()
+    def evaluate_encoded(self, board, ages, meta, ladder=None):
+        """Forward from the compact encoding (GPU featurizer in the graph).
+
+        Returns (outputs (n, ...), sensible mask (n, S*S) uint8 device tensor,
+        list of board indices whose eye recursion overflowed the kernel and
+        must be re-evaluated from CPU planes)."""
+        assert self.fz is not None, "engine built without a feature list"
+        n = board.shape[0]
+        bk = self._get(n, encoded=True)
+        bk.e_board[:n].copy_(torch.as_tensor(board), non_blocking=True)
+        bk.e_ages[:n].copy_(torch.as_tensor(ages), non_blocking=True)
+        bk.e_meta[:n].copy_(torch.as_tensor(meta), non_blocking=True)
+        if bk.e_ladder is not None:
+            if ladder is None:
+                raise ValueError("this feature list needs ladder bits")
+            bk.e_ladder[:n].copy_(torch.as_tensor(ladder), non_blocking=True)
+        if n < bk.B:
+            bk.e_board[n:].zero_()
+            bk.e_ages[n:].fill_(255)
+        if bk.graph_enc is not None:
+            bk.graph_enc.replay()
+        else:
+            self._run(bk, True)
+        bad = torch.nonzero(bk.ovf[:n]).flatten().tolist()
+        return self._outputs(bk, n), bk.legal[:n], bad
 
     @torch.no_grad()
     def evaluate(self, planes, legal=None):
         """planes: (n, C, S, S) uint8 (numpy or tensor); legal: (n, S*S) uint8 or None.
         Returns the bucket's output tensors (views of the first n rows)."""
         n = planes.shape[0]
-        bk = self._get(n)
+        bk = self._get(n, encoded=False)
         src = torch.as_tensor(planes)
         bk.planes[:n].copy_(src, non_blocking=True)
         if n < bk.B:
@@ -172,6 +240,9 @@ class HipValueInference(HipTrunkInference):
 class TorchPolicyInference:
     """CPU / reference path with the same interface."""
 
+    supports_encoded = False
+    needs_ladder = False
+
     def __init__(self, net: PolicyNet, device="cpu"):
         self.net, self.device = net, torch.device(device)
 
@@ -189,6 +260,9 @@ class TorchPolicyInference:
 
 
 class TorchValueInference:
+    supports_encoded = False
+    needs_ladder = False
+
     def __init__(self, net: ValueNet, device="cpu"):
         self.net, self.device = net, torch.device(device)
 
@@ -201,14 +275,15 @@ class TorchValueInference:
 
 
 def make_policy_inference(net, device, **kw):
+    """HIP engine on a GPU (pass ``feature_list`` to enable evaluate_encoded), torch on CPU."""
     device = torch.device(device)
     if device.type == "cuda":
         return HipTrunkInference(net, device, **kw)
-    return TorchPolicyInference(net, device)
+    return TorchPolicyInference(net, device)  # feature_list unused: CPU featurizer path
 
 
 def make_value_inference(net, device, **kw):
     device = torch.device(device)
     if device.type == "cuda":
         return HipValueInference(net, device, **kw)
-    return TorchValueInference(net, device)
+    return TorchValueInference(net, device)  # feature_list unused: CPU featurizer path

@@ -41,6 +41,12 @@ class _NetWrapper(object):
     def create_network(cls, **kwargs):
         return cls._net_cls(**kwargs)
 
+    def _engine_kw(self):
+        """GPU engines get the feature list so they can featurize on the device."""
+        if self.device.type == "cuda" and self.preprocessor.output_dim <= 64:
+            return {"feature_list": self.preprocessor.feature_list}
+        return {}
+
     @property
     def engine(self):
         if self._engine is None:
@@ -98,7 +104,7 @@ class CNNPolicy(_NetWrapper):
         super().__init__(feature_list, device=device, **kwargs)
 
     def _make_engine(self):
-        return make_policy_inference(self.model, self.device)
+        return make_policy_inference(self.model, self.device, **self._engine_kw())
 
     def forward(self, planes, legal=None) -> np.ndarray:
         """(B, F, S, S) planes -> (B, S*S) probabilities (numpy)."""
@@ -145,7 +151,7 @@ class CNNValue(_NetWrapper):
         super().__init__(feature_list, device=device, **kwargs)
 
     def _make_engine(self):
-        return make_value_inference(self.model, self.device)
+        return make_value_inference(self.model, self.device, **self._engine_kw())
 
     def forward(self, planes) -> np.ndarray:
         planes = np.asarray(planes).astype(np.uint8, copy=False)

@@ -128,3 +128,9 @@ def wgrad_splits(M: int, T: int, n_tiles: int = 1, target_wgs: int = 512) -> int
     nks = (M + 31) // 32
     s = max(1, target_wgs // max(1, T * n_tiles))
     return max(1, min(s, nks))
+
+
+def featurize(board, ages, meta, fids, fplanes, S: int, ladder=None, planes=None, nhwc=None, P: int = 0,
+              sensible=None, legal=None, overflow=None):
+    """GPU featurizer (csrc/kernels/featurize.hip); see alphago_amd.ops.gpu_features."""
+    _ops().featurize(board, ages, meta, ladder, list(fids), list(fplanes), planes, nhwc, sensible, legal, overflow, S, P)

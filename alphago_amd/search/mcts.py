@@ -3,10 +3,12 @@
 ``BatchedMCTS``: many independent trees searched together by the native
 ``Forest`` (csrc/engine/mcts.cpp: PUCT with virtual loss, negamax backup,
 subtree reuse, optional λ-mixed random rollouts).  Each round gathers up to
-``leaves_per_tree`` leaves from every tree, featurises them in native threads
-straight into a pinned buffer, evaluates ALL of them in one batched policy
-(+ value) forward on the GPU (HIP-graph replay per batch bucket) and applies
-priors/values back.  This replaces the reference's serial search that made a
+``leaves_per_tree`` leaves from every tree, writes their compact encoding
+(stones, move ages, ko, side to move; ~2 bytes/point) into pinned buffers,
+and evaluates ALL of them in one batched policy (+ value) forward on the GPU
+whose HIP graph starts with the device featurizer (ops/gpu_features.py);
+priors/values are applied back natively.  Engines without the encoded path
+(CPU) get uint8 planes featurised in native threads instead.  This replaces the reference's serial search that made a
 batch-1 network call per tree level (mcts.py:91-161; ParallelMCTS stub
 :174-175).
 
@@ -39,6 +41,7 @@ class BatchedMCTS(object):
         self._roots: List[Optional[list]] = []
         self.resize(n_trees)
         self._pinned = None
+        self._enc = None
 
     def resize(self, n_trees: int) -> None:
         if n_trees == self._n:
@@ -56,10 +59,57 @@ class BatchedMCTS(object):
             self._pinned = torch.empty(max(need, 1 << 20), dtype=torch.uint8, pin_memory=pin)
         return self._pinned[:need]
 
+    def _enc_buffers(self, L: int, np_: int):
+        if self._enc is None or self._enc[0].shape[0] < L or self._enc[0].shape[1] != np_:
+            pin = torch.cuda.is_available()
+            cap = max(L, 256)
+            self._enc = (torch.zeros((cap, np_), dtype=torch.int8, pin_memory=pin),
+                         torch.zeros((cap, np_), dtype=torch.uint8, pin_memory=pin),
+                         torch.zeros((cap, 2), dtype=torch.int32, pin_memory=pin),
+                         torch.zeros((cap, np_), dtype=torch.uint8, pin_memory=pin))
+        return self._enc
+
+    def _encoded_engines(self):
+        pe = self.policy.engine
+        ve = self.value.engine if self.value is not None else None
+        if getattr(pe, "supports_encoded", False) and (ve is None or getattr(ve, "supports_encoded", False)):
+            return pe, ve
+        return None
+
+    def _evaluate_encoded(self, pe, ve) -> None:
+        f = self.forest
+        L = f.n_pending
+        s0 = f.leaf_state(0)
+        np_ = s0.size * s0.size
+        ladder = pe.needs_ladder or (ve is not None and ve.needs_ladder)
+        b, a, m, l = self._enc_buffers(L, np_)
+        f.leaf_encode_into(b.data_ptr(), a.data_ptr(), m.data_ptr(), l.data_ptr() if ladder else 0, b.shape[0],
+                           self.threads)
+        lad = l[:L] if ladder else None
+        out, _, bad = pe.evaluate_encoded(b[:L], a[:L], m[:L], lad)
+        probs = out.float().cpu().numpy()
+        values = None
+        if ve is not None:
+            vout, _, vbad = ve.evaluate_encoded(b[:L], a[:L], m[:L], lad)
+            values = vout.float().cpu().numpy()
+            bad = sorted(set(bad) | set(vbad))
+        if bad:  # eye recursion too deep for the kernel: these rows from CPU planes
+            states = [f.leaf_state(i) for i in bad]
+            planes = self.policy.preprocessor.states_to_uint8(states)
+            masks = _engine().featurize_batch(states, ["sensibleness"], self.threads).reshape(len(bad), -1)
+            probs[bad] = pe.evaluate(planes, masks).float().cpu().numpy()
+            if ve is not None:
+                values[bad] = ve.evaluate(self.value.preprocessor.states_to_uint8(states)).float().cpu().numpy()
+        f.apply(probs, values)
+
     def _evaluate_pending(self) -> None:
         f = self.forest
         L = f.n_pending
         if L == 0:
+            return
+        enc = self._encoded_engines()
+        if enc is not None:
+            self._evaluate_encoded(*enc)
             return
         s0 = f.leaf_state(0)
         np_ = s0.size * s0.size

@@ -1,9 +1,11 @@
 """Vectorised self-play: many games advanced in lock-step, one batched forward per side per ply.
 
-``BatchedSampler.select(states)`` featurises all states in native threads,
-builds the sensible-move masks (legal and not filling an own eye, ai.py:15),
-runs ONE policy forward with the mask applied inside the fused head kernel,
-then samples p**(1/T) (or argmax) on the device.  This replaces the
+``BatchedSampler.select(states)`` encodes all states compactly in native
+threads and runs ONE policy forward whose graph featurises on the device and
+builds the sensible-move masks (legal and not filling an own eye, ai.py:15)
+that the fused head kernel applies; then samples p**(1/T) (or argmax) on the
+device.  When the caller needs the planes (RL training records) or the engine
+has no encoded path (CPU), planes are featurised natively on the host.  This replaces the
 reference's per-state Python move lists and CPU renormalisation
 (ai.py:51-68, policy.py:44-79).
 """
@@ -36,17 +38,34 @@ class BatchedSampler(object):
         m = _engine().featurize_batch(list(states), ["sensibleness"], self.threads)
         return m.reshape(len(states), -1)
 
-    def select(self, states: Sequence, planes: Optional[np.ndarray] = None):
-        """Returns (moves list, planes uint8 array, flat move indices (-1 = pass))."""
+    def _probs_encoded(self, states, eng):
+        E = _engine()
+        b, a, m, l = E.encode_batch(list(states), eng.needs_ladder, self.threads)
+        probs, sens, bad = eng.evaluate_encoded(b, a, m, l)
+        if bad:  # eye recursion too deep for the kernel: recompute those rows from CPU planes
+            sub = [states[i] for i in bad]
+            masks = self.masks(sub)
+            probs = probs.clone()
+            sens = sens.clone()
+            probs[bad] = eng.evaluate(self.featurize(sub), masks).to(probs.dtype)
+            sens[bad] = torch.from_numpy(masks).to(sens.device)
+        return probs, (sens != 0).any(1)
+
+    def select(self, states: Sequence, planes: Optional[np.ndarray] = None, need_planes: bool = True):
+        """Returns (moves list, planes uint8 array or None, flat move indices (-1 = pass))."""
         n = len(states)
         if n == 0:
             return [], None, np.zeros(0, np.int64)
         size = states[0].size
-        if planes is None:
-            planes = self.featurize(states)
-        masks = self.masks(states)
-        probs = self.policy.engine.evaluate(planes, masks)
-        has = torch.from_numpy(masks.any(axis=1)).to(probs.device)
+        eng = self.policy.engine
+        if planes is None and not need_planes and getattr(eng, "supports_encoded", False):
+            probs, has = self._probs_encoded(states, eng)
+        else:
+            if planes is None:
+                planes = self.featurize(states)
+            masks = self.masks(states)
+            probs = eng.evaluate(planes, masks)
+            has = torch.from_numpy(masks.any(axis=1)).to(probs.device)
         if self.greedy:
             idx = probs.argmax(1)
         else:
@@ -60,10 +79,10 @@ class BatchedSampler(object):
 
     # GreedyPolicyPlayer/ProbabilisticPolicyPlayer-compatible interface
     def get_moves(self, states):
-        return self.select(states)[0]
+        return self.select(states, need_planes=False)[0]
 
     def get_move(self, state):
-        return self.select([state])[0][0]
+        return self.select([state], need_planes=False)[0][0]
 
 
 @dataclass
@@ -98,7 +117,7 @@ def play_games(learner: BatchedSampler, opponent: BatchedSampler, n_games: int, 
         for group, sampler, is_learner in ((lturn, learner, True), (oturn, opponent, False)):
             if not group:
                 continue
-            moves, planes, idx = sampler.select([states[i] for i in group])
+            moves, planes, idx = sampler.select([states[i] for i in group], need_planes=record and is_learner)
             for k, i in enumerate(group):
                 if record and is_learner and moves[k] is not go.PASS_MOVE:
                     rec_p[i].append(planes[k])

@@ -60,7 +60,7 @@ def generate_positions(sl_policy: CNNPolicy, rl_policy: CNNPolicy, n_games: int,
         g_rl = [i for i in active if ply > U[i] - 1]
         for group, sampler in ((g_sl, sl), (g_rl, rl)):
             if group:
-                moves, _, _ = sampler.select([states[i] for i in group])
+                moves, _, _ = sampler.select([states[i] for i in group], need_planes=False)
                 for k, i in enumerate(group):
                     states[i].do_move(moves[k])
         for i in g_rand:

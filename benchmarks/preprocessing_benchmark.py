@@ -27,6 +27,40 @@ def positions(sgf_dir):
     return out
 
 
+def gpu_featurizer(states, B=1024, iters=50):
+    """Device featurizer: host encode (C++) + H2D + kernel, and the kernel alone."""
+    import torch
+
+    from alphago_amd import ops
+    from alphago_amd.ops.gpu_features import GpuFeaturizer
+
+    batch = (states * (B // max(1, len(states)) + 1))[:B]
+    out = {}
+    for name, feats in (("46_planes", ALL_NO_LADDER_FEATURES), ("48_planes_with_ladders", DEFAULT_FEATURES)):
+        fz = GpuFeaturizer(feats)
+        dev = fz.device
+        enc = fz.to_device(fz.encode(batch))
+        x = ops.padded_empty(B, 19, 2, 64, dev)
+        sens = torch.empty((B, 361), dtype=torch.uint8, device=dev)
+        for _ in range(3):
+            fz.run(*enc, nhwc=x, P=2, sensible=sens)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(iters):
+            fz.run(*enc, nhwc=x, P=2, sensible=sens)
+        torch.cuda.synchronize()
+        kern = (time.perf_counter() - t) / iters
+        t = time.perf_counter()
+        for _ in range(5):
+            e = fz.to_device(fz.encode(batch))
+            fz.run(*e, nhwc=x, P=2, sensible=sens)
+        torch.cuda.synchronize()
+        full = (time.perf_counter() - t) / 5
+        out[name] = {"batch": B, "kernel_us": round(kern * 1e6, 1), "kernel_pos_per_s": round(B / kern),
+                     "encode_h2d_kernel_pos_per_s": round(B / full)}
+    return out
+
+
 def main():
     sgf_dir = sys.argv[1] if len(sys.argv) > 1 else "/root/reference/tests/test_data/sgf"
     if not os.path.isdir(sgf_dir):  # synthetic fallback: random games
@@ -53,6 +87,9 @@ def main():
         batched = len(states) / (time.perf_counter() - t)
         res[name] = {"single_thread_pos_per_s": round(single), "batched_8_threads_pos_per_s": round(batched),
                      "vs_reference_265_pos_per_s": round(single / 265.0, 1)}
+    import torch
+    if torch.cuda.is_available():
+        res["gpu"] = gpu_featurizer(states)
     t = time.perf_counter()
     n = 0
     for s in states[:200]:

@@ -25,7 +25,7 @@ def main():
     small = dev.type == "cpu"
     F, L = (16, 2) if small else (192, 12)
     pol = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
-    val = CNNValue(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
+    val = CNNValue(VALUE_FEATURES, filters_per_layer=F, layers=L, device=dev)
     trees = int(sys.argv[1]) if len(sys.argv) > 1 else (4 if small else 64)
     playouts = int(sys.argv[2]) if len(sys.argv) > 2 else (32 if small else 800)
     lpt = 16
@@ -47,11 +47,13 @@ def main():
     games = int(sys.argv[3]) if len(sys.argv) > 3 else (8 if small else 256)
     a, b = BatchedSampler(pol, seed=1), BatchedSampler(pol, seed=2)
     play_games(a, b, min(games, 8), max_moves=20, record=False)  # warm-up
-    t = time.perf_counter()
-    rec = play_games(a, b, games, max_moves=722, record=True, rng=np.random.default_rng(0))
-    dt = time.perf_counter() - t
-    res.update({"selfplay_games": games, "selfplay_games_per_s": round(games / dt, 2),
-                "selfplay_moves_per_s": round(sum(rec.lengths) / dt), "mean_game_length": float(np.mean(rec.lengths))})
+    for record in (False, True):  # record=True also featurises the learner's planes on the host
+        t = time.perf_counter()
+        rec = play_games(a, b, games, max_moves=722, record=record, rng=np.random.default_rng(0))
+        dt = time.perf_counter() - t
+        key = "selfplay_recorded" if record else "selfplay"
+        res[key] = {"games": games, "games_per_s": round(games / dt, 2), "moves_per_s": round(sum(rec.lengths) / dt),
+                    "mean_game_length": float(np.mean(rec.lengths))}
     print(json.dumps(res))
 
 

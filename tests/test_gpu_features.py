@@ -1,0 +1,196 @@
+"""GPU featurizer (csrc/kernels/featurize.hip) vs the CPU featurizer.
+
+Every plane must be bit-identical to ``Preprocess`` (itself pinned to the
+reference goldens in test_features.py) on random game positions, on
+positions with chains of mutually-supporting eyes (the recursive is_eye
+path, go.py:230-259) and on a checkerboard that overflows the kernel's
+eye-frame stack (CPU fallback).
+"""
+import numpy as np
+import pytest
+
+from alphago_amd import go
+from alphago_amd._native import engine
+from alphago_amd.features import ALL_NO_LADDER_FEATURES, DEFAULT_FEATURES, VALUE_FEATURES, Preprocess
+
+
+def random_positions(n, size=19, seed=0, max_len=300):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        gs = go.GameState(size)
+        length = int(rng.integers(0, max_len))
+        for _ in range(length):
+            moves = gs.get_legal_moves(include_eyes=False)
+            if not moves or rng.random() < 0.01:
+                gs.do_move(go.PASS_MOVE)
+            else:
+                gs.do_move(moves[int(rng.integers(len(moves)))])
+            if gs.is_end_of_game:
+                break
+        out.append(gs)
+    return out
+
+
+def eye_chain_positions():
+    """Boards with diagonal chains of eyeish points (recursion through is_eye)."""
+    res = []
+    for size in (7, 9, 19):
+        gs = go.GameState(size)
+        # black checkerboard strip on rows 0..3 leaves diagonal eyes at odd parities
+        for x in range(min(size, 6)):
+            for y in range(min(size, 6)):
+                if (x + y) % 2 == 1:
+                    gs.do_move((x, y), go.BLACK)
+        gs.do_move((size - 1, size - 1), go.WHITE)
+        res.append(gs)
+        gs2 = go.GameState(size)
+        for x in range(size):
+            for y in range(size):
+                if (x + y) % 2 == 1 and x < 5:
+                    gs2.do_move((x, y), go.WHITE)
+        gs2.do_move((size - 1, size - 1), go.BLACK)  # white to move: white's eyes are evaluated
+        res.append(gs2)
+    return res
+
+
+def test_encode_batch_cpu():
+    states = random_positions(6, size=9, seed=3, max_len=60)
+    board, ages, meta, lad = engine().encode_batch(states, False, 2)
+    assert lad is None
+    for i, s in enumerate(states):
+        assert np.array_equal(board[i].reshape(9, 9), np.asarray(s.board))
+        ts = Preprocess(["turns_since"]).state_to_uint8(s)
+        exp = np.full(81, 255, np.uint8)
+        for k in range(8):
+            exp[ts[k].reshape(-1) == 1] = k
+        assert np.array_equal(ages[i], exp)
+        assert meta[i, 1] == s.current_player
+    _, _, _, lad = engine().encode_batch(states, True, 2)
+    assert lad.shape == (6, 81)
+    for i, s in enumerate(states):
+        f = Preprocess(["ladder_capture", "ladder_escape"]).state_to_uint8(s).reshape(2, -1)
+        assert np.array_equal(lad[i] & 1, f[0]) and np.array_equal((lad[i] >> 1) & 1, f[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("feats", [ALL_NO_LADDER_FEATURES, DEFAULT_FEATURES, VALUE_FEATURES + ["legal"]])
+def test_gpu_planes_match_cpu(cuda_device, feats):
+    from alphago_amd.ops.gpu_features import GpuFeaturizer
+
+    states = random_positions(48, seed=11) + eye_chain_positions()[-2:]
+    fz = GpuFeaturizer(feats, board=19, device=cuda_device)
+    got, sens = fz.planes(states, with_sensible=True)
+    got, sens = got.cpu().numpy(), sens.cpu().numpy()
+    pre = Preprocess(feats)
+    for i, s in enumerate(states):
+        exp = pre.state_to_uint8(s)
+        if not np.array_equal(got[i], exp):
+            bad = np.argwhere(got[i] != exp)
+            raise AssertionError("state %d: %d mismatches, first %s" % (i, len(bad), bad[:5].tolist()))
+        sm = Preprocess(["sensibleness"]).state_to_uint8(s).reshape(-1)
+        assert np.array_equal(sens[i], sm)
+
+
+@pytest.mark.gpu
+def test_gpu_small_boards_and_eye_chains(cuda_device):
+    from alphago_amd.ops.gpu_features import GpuFeaturizer
+
+    for size in (7, 9, 19):
+        states = [s for s in eye_chain_positions() if s.size == size] + random_positions(8, size, seed=size, max_len=80)
+        fz = GpuFeaturizer(ALL_NO_LADDER_FEATURES + ["legal"], board=size, device=cuda_device)
+        got = fz.planes(states).cpu().numpy()
+        pre = Preprocess(ALL_NO_LADDER_FEATURES + ["legal"])
+        for i, s in enumerate(states):
+            assert np.array_equal(got[i], pre.state_to_uint8(s)), (size, i)
+
+
+@pytest.mark.gpu
+def test_gpu_checkerboard_overflow_fallback(cuda_device):
+    import torch
+
+    from alphago_amd.ops.gpu_features import GpuFeaturizer
+
+    # 7x7 checkerboard: every empty point starts an eye recursion that
+    # re-explores the whole diagonal lattice (exponential; ~15 ms on the CPU,
+    # a 9x9 one takes ~30 s) -> the kernel's frame budget trips.
+    gs = go.GameState(7)
+    for x in range(7):
+        for y in range(7):
+            if (x + y) % 2 == 1:
+                gs.do_move((x, y), go.BLACK)
+    gs.do_move(go.PASS_MOVE, go.WHITE)  # black to move: every empty point is a black eye candidate
+    states = [gs] + random_positions(3, size=7, seed=5, max_len=40)
+    fz = GpuFeaturizer(["sensibleness", "legal"], board=7, device=cuda_device)
+    board, ages, meta, lad = fz.to_device(fz.encode(states))
+    ovf = torch.zeros(len(states), dtype=torch.int32, device=cuda_device)
+    out = torch.empty((len(states), 2, 7, 7), dtype=torch.uint8, device=cuda_device)
+    fz.run(board, ages, meta, lad, planes=out, overflow=ovf)
+    assert ovf[0].item() == 1  # deep eye chain overflows the frame stack ...
+    got = fz.planes(states).cpu().numpy()  # ... and is recomputed on the CPU
+    pre = Preprocess(["sensibleness", "legal"])
+    for i, s in enumerate(states):
+        assert np.array_equal(got[i], pre.state_to_uint8(s))
+
+
+@pytest.mark.gpu
+def test_gpu_featurize_into_padded_input(cuda_device):
+    import torch
+
+    from alphago_amd import ops
+    from alphago_amd.ops.gpu_features import GpuFeaturizer
+
+    states = random_positions(10, seed=2)
+    fz = GpuFeaturizer(DEFAULT_FEATURES, device=cuda_device)
+    planes = fz.planes(states)
+    ref = ops.padded_empty(len(states), 19, 2, 64, cuda_device)
+    ops.pack_input(planes, ref, 2)
+    board, ages, meta, lad = fz.to_device(fz.encode(states))
+    out = ops.padded_empty(len(states), 19, 2, 64, cuda_device)
+    sens = torch.empty((len(states), 361), dtype=torch.uint8, device=cuda_device)
+    fz.run(board, ages, meta, lad, nhwc=out, P=2, sensible=sens)
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+def test_encoded_inference_matches_planes(cuda_device):
+    """evaluate_encoded (featurizer inside the graph) == evaluate(CPU planes, CPU masks)."""
+    import torch
+
+    from alphago_amd.models.policy import CNNPolicy, CNNValue
+
+    torch.manual_seed(0)
+    states = random_positions(37, seed=9)
+    pol = CNNPolicy(DEFAULT_FEATURES, device=cuda_device, filters_per_layer=64, layers=3)
+    eng = pol.engine
+    assert eng.supports_encoded and eng.needs_ladder
+    E = engine()
+    b, a, m, l = E.encode_batch(states, True, 4)
+    probs, sens, bad = eng.evaluate_encoded(b, a, m, l)
+    probs, sens = probs.float().cpu().numpy().copy(), sens.cpu().numpy().copy()
+    assert bad == []
+    planes = Preprocess(DEFAULT_FEATURES).states_to_uint8(states)
+    masks = E.featurize_batch(states, ["sensibleness"], 4).reshape(len(states), -1)
+    ref = eng.evaluate(planes, masks).float().cpu().numpy()
+    assert np.array_equal(sens, masks)
+    np.testing.assert_array_equal(probs, ref)
+
+    val = CNNValue(VALUE_FEATURES, device=cuda_device, filters_per_layer=64, layers=3)
+    v_enc, _, _ = val.engine.evaluate_encoded(b, a, m, l)
+    v_ref = val.engine.evaluate(Preprocess(VALUE_FEATURES).states_to_uint8(states))
+    torch.testing.assert_close(v_enc.float().cpu(), v_ref.float().cpu())
+
+
+@pytest.mark.gpu
+def test_batched_mcts_encoded_path(cuda_device):
+    from alphago_amd.models.policy import CNNPolicy, CNNValue
+    from alphago_amd.search.mcts import BatchedMCTS
+
+    pol = CNNPolicy(DEFAULT_FEATURES, device=cuda_device, filters_per_layer=32, layers=2)
+    val = CNNValue(VALUE_FEATURES, device=cuda_device, filters_per_layer=32, layers=2)
+    states = random_positions(4, seed=1, max_len=50)
+    m = BatchedMCTS(pol, val, n_trees=4)
+    assert m._encoded_engines() is not None
+    moves = m.search(states, n_playout=64, leaves_per_tree=8)
+    for s, mv in zip(states, moves):
+        assert mv is None or s.is_legal(mv)
