@@ -37,6 +37,39 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   return r;
 }
 
+// Gradient of a 1x1 (F -> 1) head conv given dlogits g (in g_s, length S*S):
+// ReLU'-masked dY into the trunk's last activation and per-board partials of
+// dW_head (the dbias partial is written by the caller).
+__device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int b, const __bf16* base,
+                                                    const float* w_s, const float* g_s) {
+  const int tid = threadIdx.x;
+  const int SS = a.S * a.S;
+  const int HP = a.S + 2;
+  const int C8 = a.C >> 3;
+  __bf16* dzb = a.dz + (size_t)b * HP * HP * a.C;
+  for (int idx = tid; idx < SS * C8; idx += blockDim.x) {
+    const int p = idx / C8;
+    const int c8 = (idx - p * C8) << 3;
+    const int i = p / a.S, j = p - (p / a.S) * a.S;
+    const size_t off = (size_t)((i + 1) * HP + j + 1) * a.C + c8;
+    const bf16x8 v = *(const bf16x8*)(base + off);
+    const float g = g_s[p];
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (__bf16)((float)v[e] > 0.f ? g * w_s[c8 + e] : 0.f);
+    *(bf16x8*)(dzb + off) = o;
+  }
+  float* dh = a.dhead + (size_t)b * (a.C_real + 1);
+  for (int c = tid; c < a.C_real; c += blockDim.x) {
+    float s = 0.f;
+    for (int p = 0; p < SS; ++p) {
+      const int i = p / a.S, j = p - (p / a.S) * a.S;
+      s += g_s[p] * (float)base[(size_t)((i + 1) * HP + j + 1) * a.C + c];
+    }
+    dh[c] = s;
+  }
+}
+
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
   __shared__ float w_s[256];
@@ -126,36 +159,98 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
       z_s[p] = g;
     }
     __syncthreads();
-    // gradient into the last trunk activation, masked by ReLU'
-    const int C8 = a.C >> 3;
-    __bf16* dzb = a.dz + (size_t)b * HP * HP * a.C;
-    for (int idx = tid; idx < SS * C8; idx += 256) {
-      const int p = idx / C8;
-      const int c8 = (idx - p * C8) << 3;
-      const int i = p / a.S, j = p - (p / a.S) * a.S;
-      const size_t off = (size_t)((i + 1) * HP + j + 1) * a.C + c8;
-      const bf16x8 v = *(const bf16x8*)(base + off);
-      const float g = z_s[p];
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (__bf16)((float)v[e] > 0.f ? g * w_s[c8 + e] : 0.f);
-      *(bf16x8*)(dzb + off) = o;
-    }
-    // per-board head-weight / bias gradient partials
-    float* dh = a.dhead + (size_t)b * (a.C_real + 1);
-    for (int c = tid; c < a.C_real; c += 256) {
-      float s = 0.f;
-      for (int p = 0; p < SS; ++p) {
-        const int i = p / a.S, j = p - (p / a.S) * a.S;
-        s += z_s[p] * (float)base[(size_t)((i + 1) * HP + j + 1) * a.C + c];
-      }
-      dh[c] = s;
-    }
+    head_input_backward(a, b, base, w_s, z_s);
     float gs = 0.f;
     for (int p = tid; p < SS; p += 256) gs += z_s[p];
     gs = block_reduce_sum(gs, red);
-    if (tid == 0) dh[a.C_real] = gs;
+    if (tid == 0) a.dhead[(size_t)b * (a.C_real + 1) + a.C_real] = gs;
   }
+}
+
+// Head logits only: z[b][p] = y[b,p,:] . w + bias (value-net head input,
+// value.py:23-26); the board's activations are read once.
+__global__ __launch_bounds__(256) void head_logits_kernel(PolicyHeadArgs a) {
+  __shared__ float w_s[256];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int SS = a.S * a.S;
+  const int HP = a.S + 2;
+  for (int c = tid; c < a.C; c += 256) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
+  __syncthreads();
+  const __bf16* base = a.y + (size_t)b * HP * HP * a.C;
+  const float bias = a.b[0];
+  for (int p = tid; p < SS; p += 256) {
+    const int i = p / a.S, j = p - (p / a.S) * a.S;
+    const __bf16* row = base + (size_t)((i + 1) * HP + j + 1) * a.C;
+    float dot = 0.f;
+    for (int c8 = 0; c8 < a.C; c8 += 8) {
+      const bf16x8 v = *(const bf16x8*)(row + c8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dot += (float)v[e] * w_s[c8 + e];
+    }
+    a.probs[(size_t)b * SS + p] = dot + bias;  // probs slot carries the logits
+  }
+}
+
+// Head backward from an externally computed dlogits (value net: dz = dh W1^T).
+__global__ __launch_bounds__(256) void head_backward_kernel(PolicyHeadArgs a, const float* dlogits) {
+  __shared__ float w_s[256];
+  __shared__ float g_s[368];
+  __shared__ float red[8];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int SS = a.S * a.S;
+  const int HP = a.S + 2;
+  for (int c = tid; c < a.C; c += 256) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
+  float gs = 0.f;
+  for (int p = tid; p < SS; p += 256) {
+    const float g = dlogits[(size_t)b * SS + p];
+    g_s[p] = g;
+    gs += g;
+  }
+  __syncthreads();
+  head_input_backward(a, b, a.y + (size_t)b * HP * HP * a.C, w_s, g_s);
+  gs = block_reduce_sum(gs, red);
+  if (tid == 0) a.dhead[(size_t)b * (a.C_real + 1) + a.C_real] = gs;
+}
+
+// Value output layer: v = tanh(h . w2 + b2) (value.py:28-29) and, with
+// targets, MSE loss (v - t)^2, sign agreement, dv = 2 (v - t)(1 - v^2) * scale
+// * weight[b], dh = dv w2 and per-board partials [dw2 | db2].  One workgroup
+// per board, one thread per dense unit.
+__global__ __launch_bounds__(256) void value_out_kernel(ValueOutArgs a) {
+  __shared__ float red[8];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  float s = 0.f;
+  for (int j = tid; j < a.D; j += 256) s += a.h[(size_t)b * a.D + j] * a.w2[j];
+  s = block_reduce_sum(s, red);
+  const float v = tanhf(s + a.b2[0]);
+  if (tid == 0) a.v[b] = v;
+  if (!a.target) return;
+  const float t = a.target[b];
+  const float e = v - t;
+  if (tid == 0) {
+    a.loss[b] = e * e;
+    a.correct[b] = (v > 0.f ? 1.f : (v < 0.f ? -1.f : 0.f)) == (t > 0.f ? 1.f : (t < 0.f ? -1.f : 0.f)) ? 1.f : 0.f;
+  }
+  const float dv = 2.f * e * (1.f - v * v) * a.grad_scale * (a.weight ? a.weight[b] : 1.f);
+  float* dp = a.dout + (size_t)b * (a.D + 1);
+  for (int j = tid; j < a.D; j += 256) {
+    a.dh[(size_t)b * a.D + j] = dv * a.w2[j];
+    dp[j] = dv * a.h[(size_t)b * a.D + j];
+  }
+  if (tid == 0) dp[a.D] = dv;
+}
+
+void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(head_logits_kernel, dim3(a.B), dim3(256), 0, st, a);
+}
+void launch_head_backward(const PolicyHeadArgs& a, const float* dlogits, hipStream_t st) {
+  hipLaunchKernelGGL(head_backward_kernel, dim3(a.B), dim3(256), 0, st, a, dlogits);
+}
+void launch_value_out(const ValueOutArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(value_out_kernel, dim3(a.B), dim3(256), 0, st, a);
 }
 
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st) {

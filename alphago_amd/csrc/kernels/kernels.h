@@ -58,6 +58,21 @@ struct PolicyHeadArgs {
   float inv_temp;
 };
 
+struct ValueOutArgs {
+  const float* h;       // [B][D] dense-1 output
+  const float* w2;      // [D]
+  const float* b2;      // [1]
+  const float* target;  // [B] in [-1, 1] or null (inference)
+  const float* weight;  // [B] or null
+  float* v;             // [B]
+  float* loss;          // [B]
+  float* correct;       // [B]
+  float* dh;            // [B][D]
+  float* dout;          // [B][D + 1] per-board partials of [dw2 | db2]
+  int B, D;
+  float grad_scale;
+};
+
 struct PackInputArgs {
   const uint8_t* planes;  // [B][Creal][S][S]
   const int* sym;         // [B] in 0..7 or null (identity)
@@ -104,6 +119,9 @@ void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
+void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st);
+void launch_head_backward(const PolicyHeadArgs& a, const float* dlogits, hipStream_t st);
+void launch_value_out(const ValueOutArgs& a, hipStream_t st);
 void launch_pack_input(const PackInputArgs& a, hipStream_t st);
 void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st);
 void launch_featurize(const FeaturizeArgs& a, hipStream_t st);

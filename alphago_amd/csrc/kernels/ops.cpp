@@ -147,6 +147,62 @@ void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::o
   agk::launch_policy_head(a, train, cur_stream());
 }
 
+// z: (B, S*S) f32 <- y (B, S+2, S+2, C) bf16 . w + b
+void head_logits(const Tensor& y, const Tensor& w, const Tensor& b, const Tensor& z, int64_t S) {
+  CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(b); CHECK_F32(z); CHECK_CONTIG(z);
+  const int64_t B = y.size(0), C = y.size(3);
+  TORCH_CHECK(y.size(1) == S + 2 && C % 8 == 0 && C <= 256 && w.numel() <= C && S * S <= 368, "head geometry");
+  TORCH_CHECK(z.numel() == B * S * S, "z must be (B, S*S)");
+  agk::PolicyHeadArgs a{};
+  a.y = bfp(y); a.w = w.data_ptr<float>(); a.b = b.data_ptr<float>(); a.probs = z.data_ptr<float>();
+  a.B = (int)B; a.S = (int)S; a.C = (int)C; a.C_real = (int)w.numel();
+  if (B == 0) return;
+  agk::launch_head_logits(a, cur_stream());
+}
+
+// dz (B, S+2, S+2, C) bf16 <- ReLU'(y) * dlogits x w;  dhead (B, C_real+1) partials
+void head_backward(const Tensor& y, const Tensor& w, const Tensor& dlogits, const Tensor& dz, const Tensor& dhead,
+                   int64_t S) {
+  CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(dlogits); CHECK_CONTIG(dlogits);
+  CHECK_BF16(dz); CHECK_CONTIG(dz); CHECK_F32(dhead);
+  const int64_t B = y.size(0), C = y.size(3);
+  TORCH_CHECK(y.size(1) == S + 2 && C % 8 == 0 && C <= 256 && w.numel() <= C && S * S <= 368, "head geometry");
+  TORCH_CHECK(dz.sizes() == y.sizes() && dlogits.numel() == B * S * S && dhead.numel() >= B * (w.numel() + 1), "shapes");
+  agk::PolicyHeadArgs a{};
+  a.y = bfp(y); a.w = w.data_ptr<float>(); a.dz = bfp_mut(dz); a.dhead = dhead.data_ptr<float>();
+  a.B = (int)B; a.S = (int)S; a.C = (int)C; a.C_real = (int)w.numel();
+  if (B == 0) return;
+  agk::launch_head_backward(a, dlogits.data_ptr<float>(), cur_stream());
+}
+
+void value_out(const Tensor& h, const Tensor& w2, const Tensor& b2, const c10::optional<Tensor>& target,
+               const c10::optional<Tensor>& weight, const Tensor& v, const c10::optional<Tensor>& loss,
+               const c10::optional<Tensor>& correct, const c10::optional<Tensor>& dh, const c10::optional<Tensor>& dout,
+               double grad_scale) {
+  CHECK_F32(h); CHECK_CONTIG(h); CHECK_F32(w2); CHECK_F32(b2); CHECK_F32(v);
+  TORCH_CHECK(h.dim() == 2, "h must be (B, D)");
+  const int64_t B = h.size(0), D = h.size(1);
+  TORCH_CHECK(w2.numel() == D && v.numel() == B, "shapes");
+  agk::ValueOutArgs a{};
+  a.h = h.data_ptr<float>(); a.w2 = w2.data_ptr<float>(); a.b2 = b2.data_ptr<float>(); a.v = v.data_ptr<float>();
+  a.B = (int)B; a.D = (int)D; a.grad_scale = (float)grad_scale;
+  if (target.has_value()) {
+    TORCH_CHECK(loss && correct && dh && dout, "training needs loss, correct, dh, dout");
+    CHECK_F32(*target);
+    TORCH_CHECK(target->numel() == B && dh->numel() == B * D && dout->numel() >= B * (D + 1), "shapes");
+    a.target = target->data_ptr<float>();
+    a.loss = loss->data_ptr<float>(); a.correct = correct->data_ptr<float>();
+    a.dh = dh->data_ptr<float>(); a.dout = dout->data_ptr<float>();
+  }
+  if (weight.has_value()) {
+    CHECK_F32(*weight);
+    TORCH_CHECK(weight->numel() == B, "weight must be (B,)");
+    a.weight = weight->data_ptr<float>();
+  }
+  if (B == 0) return;
+  agk::launch_value_out(a, cur_stream());
+}
+
 void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c10::optional<Tensor>& target,
                 const c10::optional<Tensor>& target_out, const Tensor& out, int64_t P) {
   TORCH_CHECK(planes.scalar_type() == at::kByte && planes.is_contiguous() && planes.dim() == 4, "planes: uint8 (B,C,S,S)");
@@ -273,6 +329,11 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor? weight, Tensor(a!)? dz, Tensor(b!)? loss, "
       "Tensor(c!)? correct, Tensor(d!)? dhead, Tensor(e!)? probs, int S, float grad_scale, float temperature) -> ()");
+  m.def("head_logits(Tensor y, Tensor w, Tensor b, Tensor(a!) z, int S) -> ()");
+  m.def("head_backward(Tensor y, Tensor w, Tensor dlogits, Tensor(a!) dz, Tensor(b!) dhead, int S) -> ()");
+  m.def(
+      "value_out(Tensor h, Tensor w2, Tensor b2, Tensor? target, Tensor? weight, Tensor(a!) v, Tensor(b!)? loss, "
+      "Tensor(c!)? correct, Tensor(d!)? dh, Tensor(e!)? dout, float grad_scale) -> ()");
   m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P) -> ()");
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
@@ -288,6 +349,9 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);
   m.impl("policy_head", &policy_head);
   m.impl("pack_input", &pack_input);
+  m.impl("head_logits", &head_logits);
+  m.impl("head_backward", &head_backward);
+  m.impl("value_out", &value_out);
   m.impl("pack_weights", &pack_weights);
   m.impl("sgd_update", &sgd_update);
   m.impl("featurize", &featurize);

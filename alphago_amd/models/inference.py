@@ -212,7 +212,8 @@ class HipTrunkInference:
 
 
 class HipValueInference(HipTrunkInference):
-    """Value net: HIP trunk, then the (tiny) 1x1 conv + Dense(256) + Dense(1)+tanh head."""
+    """Value net: HIP trunk, then the head as head_logits (1x1 conv) -> addmm
+    (Dense 256) -> value_out (Dense 1 + tanh), all inside the captured graph."""
 
     def __init__(self, net: ValueNet, device, **kw):
         self.fc = None
@@ -224,14 +225,14 @@ class HipValueInference(HipTrunkInference):
 
     def _alloc_outputs(self, bk):
         bk.values = torch.zeros((bk.B,), device=self.device)
+        bk.z = torch.zeros((bk.B, self.S * self.S), device=self.device)
+        bk.h = torch.zeros((bk.B, self.fc[0].shape[1]), device=self.device)
 
     def _head(self, bk, y):
-        S, F = self.S, self.F
-        inner = y[:, 1:S + 1, 1:S + 1, :F].float().reshape(bk.B, S * S, F)
-        z = inner @ self.head_w + self.head_b  # (B, 361)
         w1, b1, w2, b2 = self.fc
-        h = z @ w1 + b1
-        torch.tanh(h @ w2 + b2, out=bk.values.view(bk.B, 1))
+        ops.head_logits(y, self.head_w, self.head_b, bk.z, self.S)
+        torch.addmm(b1, bk.z, w1, out=bk.h)
+        ops.value_out(bk.h, w2.view(-1), b2, bk.values)
 
     def _outputs(self, bk, n):
         return bk.values[:n]

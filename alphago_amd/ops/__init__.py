@@ -134,3 +134,21 @@ def featurize(board, ages, meta, fids, fplanes, S: int, ladder=None, planes=None
               sensible=None, legal=None, overflow=None):
     """GPU featurizer (csrc/kernels/featurize.hip); see alphago_amd.ops.gpu_features."""
     _ops().featurize(board, ages, meta, ladder, list(fids), list(fplanes), planes, nhwc, sensible, legal, overflow, S, P)
+
+
+def head_logits(y, w, b, z, S: int):
+    """z (B, S*S) fp32 = 1x1 conv of the padded NHWC activation y (value-net head)."""
+    _ops().head_logits(y, w, b, z, S)
+    return z
+
+
+def head_backward(y, w, dlogits, dz, dhead, S: int):
+    """ReLU'-masked dY of a 1x1 head conv from dlogits, plus per-board [dW | db] partials."""
+    _ops().head_backward(y, w, dlogits, dz, dhead, S)
+
+
+def value_out(h, w2, b2, v, target=None, weight=None, loss=None, correct=None, dh=None, dout=None,
+              grad_scale: float = 1.0):
+    """v = tanh(h w2 + b2); with target: MSE loss, sign agreement, dh and per-board [dw2 | db2]."""
+    _ops().value_out(h, w2, b2, target, weight, v, loss, correct, dh, dout, grad_scale)
+    return v

@@ -310,61 +310,72 @@ class HipPolicyTrainer(HipConvTrainer):
 
 
 class HipValueTrainer(HipConvTrainer):
-    """Value net (reference value.py): HIP trunk + 1x1 conv -> Dense(256) ->
-    Dense(1) -> tanh head; MSE against game outcomes in [-1, 1].  The head is
-    tiny (361x256 per board), so it runs as a few fused torch ops and feeds its
-    ReLU-masked input gradient back into the MFMA trunk backward.
-    ``correct`` accumulates the squared error sign agreement (sign(v) == z)."""
+    """Value net (reference value.py:12-31): HIP trunk + 1x1 conv -> Dense(256)
+    -> Dense(1) -> tanh head; MSE against game outcomes in [-1, 1].
+
+    Head forward: ``head_logits`` (one pass over the last activation) -> z
+    (B, 361) fp32; hipBLASLt ``addmm`` for the 361x256 dense layer (a plain
+    library GEMM); ``value_out`` fuses the 256->1 layer, tanh, MSE, sign
+    accuracy and its backward.  Head backward: dz = dh W1^T and dW1 = z^T dh
+    (library GEMMs written straight into the flat gradient buffer), then
+    ``head_backward`` writes the ReLU'-masked gradient into the MFMA trunk
+    backward plus per-board partials of the 1x1 conv weight/bias.
+    ``correct`` counts sign(v) == sign(z)."""
 
     def _head_named_params(self):
         n = self.net
         return [("head_w", n.head_w), ("head_b", n.head_b), ("fc1_w", n.fc1_w), ("fc1_b", n.fc1_b),
                 ("fc2_w", n.fc2_w), ("fc2_b", n.fc2_b)]
 
+    def _init_head(self):
+        B, NP, dev = self.batch, self.S * self.S, self.device
+        D = self.net.fc1_w.shape[1]
+        self.D = D
+        self.z = torch.zeros(B, NP, device=dev)
+        self.h = torch.zeros(B, D, device=dev)
+        self.dh = torch.zeros(B, D, device=dev)
+        self.dzl = torch.zeros(B, NP, device=dev)
+        self.val = torch.zeros(B, device=dev)
+        self.dout = torch.zeros(B, D + 1, device=dev)
+        self.dhead = torch.zeros(B, self.F + 1, device=dev)
+        self.tval = torch.zeros(B, device=dev)
+
     def _forward_for_head(self, planes, targets, sym):
         self.forward_trunk(planes, sym, None, None)
 
-    def _head_forward(self, requires_grad: bool):
-        S, F, B = self.S, self.F, self.batch
-        inner = self.Y[-1][:, 1:S + 1, 1:S + 1, :F].float().reshape(B, S * S, F)
-        if requires_grad:
-            inner.requires_grad_(True)
+    def _head_forward(self):
         v = self.fp.views
-        hp = [v[n].detach().requires_grad_(requires_grad) for n in self.head_names]
-        hw, hb, w1, b1, w2, b2 = hp
-        z = inner @ hw.view(-1) + hb
-        h = z @ w1 + b1
-        val = torch.tanh(h @ w2 + b2).squeeze(1)
-        return inner, hp, val
+        ops.head_logits(self.Y[-1], v["head_w"].view(-1), v["head_b"], self.z, self.S)
+        torch.addmm(v["fc1_b"], self.z, v["fc1_w"], out=self.h)
 
     def _head_train(self, targets, gscale, weight):
-        with torch.enable_grad():
-            inner, hp, val = self._head_forward(True)
-            z = targets.float()
-            err = (val - z) ** 2
-            wsum = err if weight is None else err * weight
-            (wsum.sum() * gscale).backward()
-        with torch.no_grad():
-            self.loss.copy_(err.detach())
-            self.correct.copy_((torch.sign(val.detach()) == torch.sign(z)).float())
-            for n, p in zip(self.head_names, hp):
-                self.fp.grad_views[n].copy_(p.grad.view(self.fp.grad_views[n].shape))
-            S, F = self.S, self.F
-            g = inner.grad.view(self.batch, S, S, F)
-            y = self.Y[-1][:, 1:S + 1, 1:S + 1, :F]
-            self.DZ[-1][:, 1:S + 1, 1:S + 1, :F] = torch.where(y > 0, g, torch.zeros_like(g)).to(torch.bfloat16)
+        v, gv = self.fp.views, self.fp.grad_views
+        self._head_forward()
+        self.tval.copy_(targets)
+        ops.value_out(self.h, v["fc2_w"].view(-1), v["fc2_b"], self.val, target=self.tval, weight=weight,
+                      loss=self.loss, correct=self.correct, dh=self.dh, dout=self.dout, grad_scale=gscale)
+        torch.mm(self.z.t(), self.dh, out=gv["fc1_w"])
+        torch.sum(self.dh, dim=0, out=gv["fc1_b"])
+        o2, n2 = self.fp.segments["fc2_w"]
+        torch.sum(self.dout, dim=0, out=self.fp.grad[o2:o2 + n2 + 1])  # [dw2 | db2]
+        torch.mm(self.dh, v["fc1_w"].t(), out=self.dzl)
+        ops.head_backward(self.Y[-1], v["head_w"].view(-1), self.dzl, self.DZ[-1], self.dhead, self.S)
+        ho, hn = self.fp.segments["head_w"]
+        torch.sum(self.dhead, dim=0, out=self.fp.grad[ho:ho + hn + 1])  # [dW_head | db_head]
 
     @torch.no_grad()
     def evaluate(self, planes: torch.Tensor, targets: torch.Tensor):
-        self.forward_trunk(planes, None, None, None)
-        _, _, val = self._head_forward(False)
+        val = self.predict(planes)
         z = targets.float()
         return ((val - z) ** 2).sum(), (torch.sign(val) == torch.sign(z)).float().sum()
 
     @torch.no_grad()
     def predict(self, planes: torch.Tensor) -> torch.Tensor:
         self.forward_trunk(planes, None, None, None)
-        return self._head_forward(False)[2]
+        self._head_forward()
+        v = self.fp.views
+        ops.value_out(self.h, v["fc2_w"].view(-1), v["fc2_b"], self.val)
+        return self.val.clone()
 
 
 class _TorchTrainerBase:

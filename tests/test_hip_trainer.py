@@ -103,3 +103,54 @@ def test_hip_grads_match_bf16_emulation(cuda_device):
             a = hip.fp.grad_views[name]
             cos = torch.nn.functional.cosine_similarity(a.flatten().double(), ref.flatten().double(), dim=0).item()
             assert cos > 0.999, (name, cos)
+
+
+def test_hip_value_grads_match_torch(cuda_device):
+    """HIP value head (head_logits -> addmm -> value_out -> head_backward) vs autograd."""
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import HipValueTrainer, TorchValueTrainer
+
+    torch.manual_seed(0)
+    B, C = 6, 49
+    net = ValueNet(C, filters_per_layer=64, layers=3)
+    net_ref = copy.deepcopy(net)
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    z = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
+    hip = HipValueTrainer(net, B, lr=0.01, device=cuda_device)
+    ref = TorchValueTrainer(net_ref, B, lr=0.01, device=cuda_device)
+    hip.compute_grads(planes, z, None)
+    ref.compute_grads(planes, z, None)
+    torch.cuda.synchronize()
+    for name in hip.fp.names:
+        a, b = hip.fp.grad_views[name], ref.fp.grad_views[name]
+        cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
+        ratio = a.norm().item() / max(b.norm().item(), 1e-12)
+        assert cos > 0.98 and abs(ratio - 1) < 0.05, (name, cos, ratio)
+    v_hip = hip.predict(planes)
+    v_ref = net_ref.forward_torch(planes.float())
+    torch.testing.assert_close(v_hip, v_ref.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_value_out_kernel(cuda_device):
+    from alphago_amd import ops
+
+    torch.manual_seed(3)
+    B, D = 7, 256
+    h = torch.randn(B, D, device=cuda_device)
+    w2 = torch.randn(D, device=cuda_device) * 0.05
+    b2 = torch.randn(1, device=cuda_device) * 0.1
+    t = torch.tensor([1., -1., 1., -1., 1., 1., -1.], device=cuda_device)
+    wt = torch.rand(B, device=cuda_device)
+    v, loss, corr = (torch.zeros(B, device=cuda_device) for _ in range(3))
+    dh = torch.zeros(B, D, device=cuda_device)
+    dout = torch.zeros(B, D + 1, device=cuda_device)
+    ops.value_out(h, w2, b2, v, target=t, weight=wt, loss=loss, correct=corr, dh=dh, dout=dout, grad_scale=0.5)
+    hr, w2r, b2r = h.clone().requires_grad_(), w2.clone().requires_grad_(), b2.clone().requires_grad_()
+    vr = torch.tanh(hr @ w2r + b2r)
+    ((vr - t) ** 2 * wt).sum().mul(0.5).backward()
+    torch.testing.assert_close(v, vr.detach(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(loss, ((vr - t) ** 2).detach(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(corr, (torch.sign(vr) == torch.sign(t)).float())
+    torch.testing.assert_close(dh, hr.grad, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(dout[:, :D].sum(0), w2r.grad, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(dout[:, D].sum(0, keepdim=True), b2r.grad, atol=1e-5, rtol=1e-4)
