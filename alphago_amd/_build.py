@@ -99,6 +99,28 @@ def build_engine(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_selftest(sanitize: str = "", force: bool = False, verbose: bool = False) -> str:
+    """Standalone engine self-test (csrc/tools/engine_selftest.cpp), optionally
+    with host sanitizers: ``address,undefined`` or ``thread``."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "engine", "*.cpp")))
+    srcs = [s for s in srcs if not s.endswith(("bindings.cpp", "lzf.cpp"))]  # pybind11-only files
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "engine", "*.h")))
+    main = os.path.join(CSRC, "tools", "engine_selftest.cpp")
+    tag = sanitize.replace(",", "_") if sanitize else "plain"
+    out = os.path.join(BUILD, "engine_selftest_" + tag)
+    flags = ["-std=c++17", "-g", "-mpopcnt", "-DAG_NO_PYBIND=1", "-Wall", "-Wno-sign-compare"]
+    flags += (["-O1", "-fno-omit-frame-pointer", "-fsanitize=" + sanitize] if sanitize else ["-O2"])
+    if sanitize and "undefined" in sanitize:
+        flags.append("-fno-sanitize-recover=undefined")
+    digest = _digest(srcs + hdrs + [main], " ".join(flags))
+    if not force and _up_to_date(out, digest):
+        return out
+    os.makedirs(BUILD, exist_ok=True)
+    _run(["g++", *flags, "-I" + os.path.join(CSRC, "engine"), *srcs, main, "-o", out, "-lpthread"], verbose)
+    _write_stamp(out, digest)
+    return out
+
+
 def _torch_paths():
     import torch
     from torch.utils import cpp_extension
@@ -180,3 +202,6 @@ if __name__ == "__main__":
         print("engine:", build_engine(force, verbose))
     if what in ("hip", "all"):
         print("hip:", build_hip(force, verbose))
+    if what == "selftest":
+        san = sys.argv[sys.argv.index("--sanitize") + 1] if "--sanitize" in sys.argv else ""
+        print("selftest:", build_selftest(san, force, verbose))

@@ -104,8 +104,13 @@ def _match(argv):
     return res
 
 
-def main(argv: Optional[List[str]] = None):
-    argv = list(sys.argv[1:] if argv is None else argv)
+def main(argv: Optional[List[str]] = None) -> int:
+    """Dispatch a command; returns a process exit code."""
+    r = _dispatch(list(sys.argv[1:] if argv is None else argv))
+    return r if isinstance(r, int) else 0
+
+
+def _dispatch(argv: List[str]):
     if not argv or argv[0] in ("-h", "--help"):
         print(__doc__)
         return 0

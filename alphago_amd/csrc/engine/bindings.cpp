@@ -15,6 +15,7 @@ namespace py = pybind11;
 using namespace ag;
 
 namespace ag {
+void bind_mcts(pybind11::module_& m);
 void bind_lzf(py::module_& m);
 }
 

@@ -12,7 +12,6 @@
 // rollouts are optional (λ = 0 is first class) and sample uniformly among
 // sensible moves instead of printing a warning at the limit (Q5).
 #pragma once
-#include <pybind11/pybind11.h>
 
 #include <cstdint>
 #include <random>
@@ -91,6 +90,6 @@ class Forest {
   int64_t total_evals_ = 0;
 };
 
-void bind_mcts(pybind11::module_& m);
+
 
 }  // namespace ag

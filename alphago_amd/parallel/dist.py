@@ -69,8 +69,17 @@ def init_from_env(device: str = "auto", timeout_s: float = 600.0) -> DistEnv:
         kw = {}
         if use_gpu and backend == "nccl":
             kw["device_id"] = dev
-        dist.init_process_group(backend=backend, rank=rank, world_size=world,
-                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+        tmo = datetime.timedelta(seconds=timeout_s)
+        attempt = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+        if attempt > 0:
+            # torchrun --max-restarts reuses the rendezvous store across
+            # attempts; namespace this attempt's keys so the new group does
+            # not pick up the dead group's peer addresses.
+            store, _, _ = next(dist.rendezvous("env://", rank, world, timeout=tmo))
+            store = dist.PrefixStore("attempt%d/" % attempt, store)
+            dist.init_process_group(backend=backend, store=store, rank=rank, world_size=world, timeout=tmo, **kw)
+        else:
+            dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=tmo, **kw)
     _ENV = DistEnv(rank=rank, local_rank=local, world_size=world, backend=backend, device=dev)
     return _ENV
 
@@ -113,6 +122,15 @@ def all_reduce_max(value: float) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_gather_object(obj):
+    """List of every rank's ``obj`` (rank order); ``[obj]`` when not distributed."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def make_buckets(segments: Sequence[Tuple[int, int]], bucket_bytes: int = 4 << 20,

@@ -1,0 +1,62 @@
+"""Native training checkpoints (SURVEY.md §5 "Checkpoint / resume", Q16).
+
+The reference saved only Keras weights per epoch (ModelCheckpoint,
+supervised_policy_trainer.py:161-162) and lost the optimizer iteration count
+and data position on resume.  A native checkpoint holds everything needed to
+continue *bit-identically* (in a deterministic configuration):
+
+* the flat fp32 master parameters (``trainer.fp.flat``);
+* the Keras-SGD iteration count (drives ``lr/(1+decay*t)``);
+* the data cursor, epoch and step-within-epoch, partial epoch sums;
+* the augmentation RNG state;
+* the run configuration (argparse namespace as a dict) for provenance.
+
+Written by rank 0 with tmp + ``os.replace`` (atomic on POSIX); read back with
+``torch.load(weights_only=True)`` — only tensors and plain containers.
+The Keras-format ``weights.%05d.hdf5`` export is separate (io/keras_compat).
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Dict, Optional
+
+import torch
+
+FORMAT = "alphago_amd.ckpt.v1"
+
+
+def trainer_state(trainer) -> Dict[str, Any]:
+    return {"flat": trainer.fp.flat.detach().to("cpu", copy=True),
+            "names": list(trainer.fp.names),
+            "iterations": int(trainer.sched.iterations)}
+
+
+def load_trainer_state(trainer, st: Dict[str, Any]) -> None:
+    flat = st["flat"]
+    if list(st["names"]) != list(trainer.fp.names) or flat.numel() != trainer.fp.flat.numel():
+        raise ValueError("checkpoint parameters do not match this model")
+    with torch.no_grad():
+        trainer.fp.flat.copy_(flat.to(trainer.fp.flat.device))
+    trainer.sched.iterations = int(st["iterations"])
+    if hasattr(trainer, "repack"):
+        trainer.repack()
+
+
+def save(path: str, trainer, **extra) -> None:
+    state = {"format": FORMAT, "trainer": trainer_state(trainer)}
+    for k, v in extra.items():
+        if isinstance(v, torch.Tensor):
+            v = v.detach().to("cpu", copy=True)
+        state[k] = v
+    tmp = path + ".tmp"
+    torch.save(state, tmp)
+    os.replace(tmp, path)
+
+
+def load(path: str) -> Optional[Dict[str, Any]]:
+    if not os.path.exists(path):
+        return None
+    st = torch.load(path, map_location="cpu", weights_only=True)
+    if st.get("format") != FORMAT:
+        return {"legacy": st}
+    return st

@@ -30,6 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
+from ..utils.profiling import trace_range
 from ..models.nets import PolicyNet, ValueNet
 from ..parallel import dist as agdist
 
@@ -260,14 +261,18 @@ class HipConvTrainer:
         B = planes.shape[0]
         if B != self.batch:
             raise ValueError("batch %d != configured %d" % (B, self.batch))
-        self._forward_for_head(planes, targets, sym)
-        self._head_train(targets, 1.0 / (B * self.env.world_size), weight)
-        self.backward_trunk()
+        with trace_range("forward"):
+            self._forward_for_head(planes, targets, sym)
+        with trace_range("head"):
+            self._head_train(targets, 1.0 / (B * self.env.world_size), weight)
+        with trace_range("backward+allreduce"):
+            self.backward_trunk()
 
     def apply_update(self) -> None:
-        ops.sgd_update(self.fp.flat, self.fp.grad, self.sched.current(), 1.0)
-        self.sched.advance()
-        self.repack()
+        with trace_range("sgd+repack"):
+            ops.sgd_update(self.fp.flat, self.fp.grad, self.sched.current(), 1.0)
+            self.sched.advance()
+            self.repack()
 
     def step(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None,
              weight: Optional[torch.Tensor] = None):

@@ -10,7 +10,13 @@ contents: ``metadata.json`` (epochs, best_epoch, training_data, model_file),
 Differences (all fixes from SURVEY.md §2.7):
 * targets are true one-hot moves (Q1: the reference built a 38-hot row);
 * resume continues epoch numbering and the Keras lr-decay iteration count and
-  data cursor from ``checkpoint.pt`` (Q16);
+  data cursor from ``checkpoint.pt`` (Q16); with ``--checkpoint-every N`` the
+  native checkpoint (train/checkpoint.py: master weights, step, RNG, cursor)
+  is also written mid-epoch and ``--resume`` continues bit-identically;
+* failure handling: ``--watchdog-timeout`` (utils/watchdog.py heartbeats +
+  hang exit), fault-injection hooks (utils/faults.py) and ``torchrun
+  --max-restarts`` + ``--resume`` for automatic recovery;
+* ``--profile DIR``: torch.profiler traces + roctx ranges (utils/profiling.py);
 * data parallel across GPUs (one process per GPU, RCCL all-reduce inside the
   step); each global minibatch of B*world positions is split across ranks;
 * per-board D4 augmentation happens on the GPU inside ``pack_input``.
@@ -32,7 +38,12 @@ import torch
 from ..data.dataset import PositionDataset
 from ..models.policy import CNNPolicy
 from ..parallel import dist as agdist
+from ..utils import faults
+from ..utils.config import RunConfig
 from ..utils.metrics import MetricsLogger
+from ..utils.profiling import Profiler, trace_range
+from ..utils.watchdog import Watchdog, enable_collective_timeouts
+from . import checkpoint as ckpt
 from .engine import make_policy_trainer
 
 
@@ -79,6 +90,13 @@ def _parser():
     p.add_argument("--no-symmetries", action="store_true", help="disable random D4 augmentation")
     p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
     p.add_argument("--metrics", default=None, help="JSONL per-step metrics file")
+    p.add_argument("--checkpoint-every", type=int, default=0,
+                   help="also write the native checkpoint every N steps (0: end of epoch only)")
+    p.add_argument("--resume", action="store_true",
+                   help="continue from out_directory/checkpoint.pt if it exists (exact step, RNG, cursor)")
+    p.add_argument("--watchdog-timeout", type=float, default=0.0,
+                   help="exit a rank that makes no progress for this many seconds (0: off)")
+    p.add_argument("--profile", default=None, help="write torch.profiler traces + summary to this directory")
     return p
 
 
@@ -112,6 +130,9 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
             meta.metadata = json.load(f)
     meta.metadata["training_data"] = args.train_data
     meta.metadata["model_file"] = args.model
+    run_cfg = RunConfig.capture("train-sl", args, env, kernel_backend=args.backend,
+                                dtype="bf16" if dev.type == "cuda" and args.backend != "torch" else "fp32")
+    meta.metadata["config"] = run_cfg.to_dict()
 
     shuffle_file = os.path.join(args.out_directory, "shuffle.npz")
     if resume and os.path.exists(shuffle_file):
@@ -127,9 +148,12 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
 
     ckpt_path = os.path.join(args.out_directory, "checkpoint.pt")
     iterations, cursor = 0, 0
-    if resume and os.path.exists(ckpt_path):
-        ck = torch.load(ckpt_path, map_location="cpu", weights_only=True)
-        iterations, cursor = int(ck["iterations"]), int(ck["cursor"])
+    state = ckpt.load(ckpt_path) if (resume or args.resume) else None
+    if state is not None and "legacy" in state:
+        iterations, cursor = int(state["legacy"]["iterations"]), int(state["legacy"]["cursor"])
+        state = None
+    if state is not None:
+        iterations, cursor = int(state["trainer"]["iterations"]), int(state["cursor"])
 
     B = args.minibatch
     trainer = make_policy_trainer(net, B, args.learning_rate, args.decay, backend=args.backend, device=dev,
@@ -141,41 +165,76 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
     steps_per_epoch = max(1, samples_per_epoch // global_B)
     log = MetricsLogger(args.metrics if env.is_main else None)
 
+    start_epoch = len(meta.metadata["epochs"])
+    end_epoch = start_epoch + args.epochs if resume else args.epochs
+    start_step = 0
+    sums = torch.zeros(2, device=dev, dtype=torch.float64)
+    if state is not None:
+        ckpt.load_trainer_state(trainer, state["trainer"])
+        gen.set_state(state["rng"][rank] if isinstance(state["rng"], list) else state["rng"])
+        start_epoch, start_step = int(state["epoch"]), int(state["step"])
+        if not resume:
+            end_epoch = int(state.get("end_epoch", end_epoch))
+        sums.copy_(state["sums"].to(dev))
+        meta.metadata = state.get("metadata", meta.metadata)
+        if args.verbose and env.is_main:
+            print("resumed at epoch %d step %d (iteration %d)" % (start_epoch, start_step, iterations), flush=True)
+
     def global_batch(cur):
         idx = np.take(train_idx, np.arange(cur, cur + global_B) % max(1, n_train))
         return idx[rank * B:(rank + 1) * B], (cur + global_B) % max(1, n_train)
 
-    start_epoch = len(meta.metadata["epochs"])
-    for epoch in range(start_epoch, start_epoch + args.epochs if resume else args.epochs):
-        t0 = time.perf_counter()
-        loss_sum = torch.zeros((), device=dev, dtype=torch.float64)
-        corr_sum = torch.zeros((), device=dev, dtype=torch.float64)
-        for step in range(steps_per_epoch):
-            idx, cursor = global_batch(cursor)
-            planes, tgt = dataset.batch(idx)
-            sym = None if args.no_symmetries else torch.randint(0, 8, (B,), device=dev, dtype=torch.int32,
-                                                                 generator=gen)
-            l, c = trainer.step(planes, tgt, sym)
-            loss_sum += l.double()
-            corr_sum += c.double()
-        stats = torch.stack([loss_sum, corr_sum]).double()
-        agdist.all_reduce_sum_(stats)
-        seen = steps_per_epoch * global_B
-        logs = {"loss": float(stats[0]) / seen, "acc": float(stats[1]) / seen}
-        if n_val > 0:
-            vl, vc, vn = _validate(trainer, dataset, val_idx, B, rank, world, dev)
-            logs.update({"val_loss": vl, "val_acc": vc})
-        dt = time.perf_counter() - t0
+    def save_native(epoch, step):
+        rng = gen.get_state()
+        if env.distributed:
+            rng = agdist.all_gather_object(rng)
         if env.is_main:
-            ep = meta.on_epoch_end(logs)
-            policy.save_weights(os.path.join(args.out_directory, "weights.%05d.hdf5" % ep))
-            tmp = ckpt_path + ".tmp"
-            torch.save({"iterations": trainer.sched.iterations, "cursor": cursor, "epoch": ep}, tmp)
-            os.replace(tmp, ckpt_path)
-            log.log(epoch=ep, positions_per_s=seen / dt, **logs)
-            if args.verbose:
-                print("epoch %d: %s (%.0f pos/s)" % (ep, logs, seen / dt), flush=True)
-        agdist.barrier()
+            ckpt.save(ckpt_path, trainer, cursor=cursor, epoch=epoch, step=step, end_epoch=end_epoch, rng=rng,
+                      sums=sums, metadata=meta.metadata, config=run_cfg.to_dict())
+
+    enable_collective_timeouts()
+    wd = Watchdog(args.out_directory if args.watchdog_timeout > 0 else None, rank, args.watchdog_timeout)
+    if args.watchdog_timeout > 0:
+        wd.start()
+    prof = Profiler(os.path.join(args.profile, "rank%d" % rank) if args.profile else None)
+    with prof:
+        for epoch in range(start_epoch, end_epoch):
+            t0 = time.perf_counter()
+            for step in range(start_step, steps_per_epoch):
+                gstep = epoch * steps_per_epoch + step
+                faults.maybe_inject(gstep, rank)
+                with trace_range("data"):
+                    idx, cursor = global_batch(cursor)
+                    planes, tgt = dataset.batch(idx)
+                    sym = None if args.no_symmetries else torch.randint(0, 8, (B,), device=dev, dtype=torch.int32,
+                                                                         generator=gen)
+                with trace_range("train_step"):
+                    l, c = trainer.step(planes, tgt, sym)
+                sums[0] += l.double()
+                sums[1] += c.double()
+                wd.beat(gstep)
+                prof.step()
+                if args.checkpoint_every and (gstep + 1) % args.checkpoint_every == 0 and step + 1 < steps_per_epoch:
+                    save_native(epoch, step + 1)
+            start_step = 0
+            stats = sums.clone()
+            sums.zero_()
+            agdist.all_reduce_sum_(stats)
+            seen = steps_per_epoch * global_B
+            logs = {"loss": float(stats[0]) / seen, "acc": float(stats[1]) / seen}
+            if n_val > 0:
+                vl, vc, vn = _validate(trainer, dataset, val_idx, B, rank, world, dev)
+                logs.update({"val_loss": vl, "val_acc": vc})
+            dt = time.perf_counter() - t0
+            if env.is_main:
+                ep = meta.on_epoch_end(logs)
+                policy.save_weights(os.path.join(args.out_directory, "weights.%05d.hdf5" % ep))
+                log.log(epoch=ep, positions_per_s=seen / dt, **logs)
+                if args.verbose:
+                    print("epoch %d: %s (%.0f pos/s)" % (ep, logs, seen / dt), flush=True)
+            save_native(epoch + 1, 0)
+            agdist.barrier()
+    wd.stop()
     dataset.close()
     return meta.metadata
 

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--pool", type=int, default=16384, help="synthetic positions resident on device")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--profile", default=None,
+                    help="after the timed run, profile 6 more steps (torch.profiler + roctx ranges) into DIR")
     args = ap.parse_args()
 
     env = agdist.init_from_env()
@@ -118,6 +120,14 @@ def main():
             },
         }
         print(json.dumps(out), flush=True)
+    if args.profile:  # outside the timed region
+        from alphago_amd.utils.profiling import Profiler
+        with Profiler(os.path.join(args.profile, "rank%d" % env.rank), wait=1, warmup=2, active=3) as prof:
+            for _ in range(6):
+                trainer.step(*batch())
+                prof.step()
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
     agdist.shutdown()
 
 

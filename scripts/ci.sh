@@ -8,7 +8,7 @@ export PYTHONPATH=$PWD
 python -c "import __graft_entry__ as g; g.build()"
 python -m compileall -q alphago_amd tests benchmarks bench.py __graft_entry__.py
 if python -c "import flake8" 2>/dev/null; then python -m flake8 --max-line-length 120 alphago_amd; fi
-python -m pytest tests -q -m "not gpu"
+python -m pytest tests -q -m "not gpu"   # includes the ASan/UBSan/TSan engine self-tests
 if [ "${CI_GPU:-0}" = "1" ]; then
   timeout -k 10 900 python -m pytest tests -q -m gpu
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"

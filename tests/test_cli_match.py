@@ -39,12 +39,14 @@ def test_external_gtp_engine(tmp_path):
         eng.close()
 
 
-def test_cli_init_model_and_match(tmp_path):
+def test_cli_init_model_and_match(tmp_path, capsys):
     j = str(tmp_path / "p.json")
     w = str(tmp_path / "p.hdf5")
     cli_main(["init-model", "policy", j, "--weights", w, "--board", "9", "--filters", "8", "--layers", "2",
               "--features", "board,ones,turns_since"])
     spec = json.load(open(j))
     assert spec["weights_file"] == w
-    res = cli_main(["match", "policy:%s:greedy" % j, "random", "--games", "2", "--size", "9"])
+    capsys.readouterr()
+    assert cli_main(["match", "policy:%s:greedy" % j, "random", "--games", "2", "--size", "9"]) == 0
+    res = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert res["player1_wins"] + res["player2_wins"] + res["draws"] == 2
