@@ -33,19 +33,93 @@
 
 namespace agk {
 
+// Shared epilogue of the forward/dgrad kernels: lane owns output channels
+// nbase + 16 i + [0, 4) of pixel mrow + 16 j.  load() issues every operand
+// load (bias, or the ReLU' mask of dgrad) with clamped pixel indices — no
+// per-element branches, so the loads overlap instead of forming 24
+// load -> wait -> store round trips; the kernels call it a few K-steps before
+// the end of the main loop so the mask read hides under the last MFMAs.
+template <int NB, int MB, int MODE>
+struct ConvEpilogue {
+  int ooff[MB];
+  f32x4 bb[NB];
+  bf16x4 mk[NB][MB];
+
+  __device__ __forceinline__ void load(const ConvFwdArgs& a, int mrow, int nbase) {
+    const int SS = a.S * a.S;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      int m = mrow + j * 16;
+      m = m < a.M ? m : a.M - 1;
+      const int b = fdiv(m, a.divSS);
+      const int rem = m - b * SS;
+      const int ii = fdiv(rem, a.divS);
+      const int jj = rem - ii * a.S;
+      ooff[j] = ((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout + nbase;
+    }
+    if constexpr (MODE == MODE_BIAS_RELU) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) bb[i] = *(const f32x4*)(a.bias + nbase + i * 16);
+    } else if constexpr (MODE == MODE_MASK) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) mk[i][j] = *(const bf16x4*)(a.mask + ooff[j] + i * 16);
+    }
+  }
+
+  __device__ __forceinline__ void store(const ConvFwdArgs& a, const f32x4 (&acc)[NB][MB], int mrow) const {
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      if (mrow + j * 16 >= a.M) continue;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        f32x4 v = acc[i][j];
+        if constexpr (MODE == MODE_BIAS_RELU) {
+          v[0] = fmaxf(v[0] + bb[i][0], 0.f);
+          v[1] = fmaxf(v[1] + bb[i][1], 0.f);
+          v[2] = fmaxf(v[2] + bb[i][2], 0.f);
+          v[3] = fmaxf(v[3] + bb[i][3], 0.f);
+        } else if constexpr (MODE == MODE_MASK) {
+          v[0] = (float)mk[i][j][0] > 0.f ? v[0] : 0.f;
+          v[1] = (float)mk[i][j][1] > 0.f ? v[1] : 0.f;
+          v[2] = (float)mk[i][j][2] > 0.f ? v[2] : 0.f;
+          v[3] = (float)mk[i][j][3] > 0.f ? v[3] : 0.f;
+        }
+        bf16x4 o;
+        o[0] = (__bf16)v[0];
+        o[1] = (__bf16)v[1];
+        o[2] = (__bf16)v[2];
+        o[3] = (__bf16)v[3];
+        *(bf16x4*)(a.y + ooff[j] + i * 16) = o;
+      }
+    }
+  }
+};
+
+template <int NB, int MB, int MODE>
+__device__ __forceinline__ void conv_store_tile(const ConvFwdArgs& a, const f32x4 (&acc)[NB][MB], int mrow,
+                                                int nbase) {
+  ConvEpilogue<NB, MB, MODE> ep;
+  ep.load(a, mrow, nbase);
+  ep.store(a, acc, mrow);
+}
+
 // ----------------------------------------------------------------- forward
-template <int BN, int MODE, int BM>
-__global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
-  // BM/64 x 2 waves; each wave owns a 64(m) x BN/2(n) output tile
-  constexpr int NW = BM / 32;          // waves per workgroup
+template <int BN, int MODE, int BM, int MBW, bool EPF = true>
+__global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
+  // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
+  constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
   constexpr int NB = BN / 32;  // 16-wide n blocks per wave (a wave covers BN/2 channels)
-  constexpr int MB = 4;        // 16-wide m blocks per wave (a wave covers 64 pixels)
+  constexpr int MB = MBW;      // 16-wide m blocks per wave
   constexpr int A_BYTES = BM * 128;
   constexpr int B_BYTES = BN * 128;
   constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_ROWS_PW = BM / NW;   // pixel rows staged per wave
+  constexpr int A_INSTR = A_ROWS_PW / 8;
   constexpr int B_ROWS_PW = BN / NW;   // weight rows staged per wave
   constexpr int B_INSTR = B_ROWS_PW / 8;  // glds instructions per wave for the weight tile
-  static_assert(B_ROWS_PW % 8 == 0, "weight rows per wave must be a multiple of 8");
+  static_assert(B_ROWS_PW % 8 == 0 && A_ROWS_PW % 8 == 0, "rows per wave must be multiples of 8");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63;
@@ -58,10 +132,10 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   const int nK = a.K * a.K * CC;
 
   // --- staging addresses (element offsets)
-  int arow[4];
+  int arow[A_INSTR];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = wave * 32 + i * 8 + (lane >> 3);
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int r = wave * A_ROWS_PW + i * 8 + (lane >> 3);
     int m = m0 + r;
     m = m < a.M ? m : a.M - 1;
     const int b = fdiv(m, a.divSS);
@@ -80,18 +154,27 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   }
   const size_t wtap = (size_t)a.Cout * a.Cin;
 
-  auto stage = [&](int ks, int buf) {
-    const int t = ks / CC;
-    const int c0 = (ks - t * CC) << 6;
-    const int kh = t / a.K;
-    const int kw = t - kh * a.K;
-    const int toff = (kh * a.HPi + kw) * a.Cin + c0;
+  // staging cursor over (tap, 64-channel chunk), advanced incrementally with
+  // scalar adds (no per-step integer divisions)
+  int st_c0 = 0, st_kw = 0, st_a = 0;
+  size_t st_w = 0;
+  auto stage = [&](int buf) {
     char* base = smem + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) glds16(a.x + arow[i] + toff, base + (wave * 32 + i * 8) * 128);
-    const __bf16* wt = a.w + (size_t)t * wtap + c0;
+    for (int i = 0; i < A_INSTR; ++i) glds16(a.x + arow[i] + st_a + st_c0, base + (wave * A_ROWS_PW + i * 8) * 128);
+    const __bf16* wt = a.w + st_w + st_c0;
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) glds16(wt + brow[i], base + A_BYTES + (wave * B_ROWS_PW + i * 8) * 128);
+    st_c0 += 64;
+    if (st_c0 == a.Cin) {
+      st_c0 = 0;
+      st_w += wtap;
+      st_a += a.Cin;
+      if (++st_kw == a.K) {
+        st_kw = 0;
+        st_a += (a.HPi - a.K) * a.Cin;
+      }
+    }
   };
 
   f32x4 acc[NB][MB];
@@ -102,7 +185,7 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
 
   // fragment read offsets: row*128 + (chunk ^ swz)*16, swz = ((row>>1)&7) = (lane&15)>>1
   const int swz = (lane & 15) >> 1;
-  const int xrow0 = (wm * 64 + (lane & 15)) * 128;
+  const int xrow0 = (wm * 16 * MB + (lane & 15)) * 128;
   const int wrow0 = A_BYTES + (wn * (BN / 2) + (lane & 15)) * 128;
 
   auto read_frags = [&](const char* base, int kk, bf16x8 (&xf)[MB], bf16x8 (&wf)[NB]) {
@@ -123,14 +206,19 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // after the barrier that publishes it, so its LDS latency hides under the
   // staging issue and the second-half reads of the next iteration.
   bf16x8 xa[MB], wa[NB], xb[MB], wb[NB];
-  stage(0, 0);
+  const int ep_mrow = m0 + wm * 16 * MB + (lane & 15);
+  const int ep_nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
+  ConvEpilogue<NB, MB, MODE> ep;
+  const int ep_at = EPF ? (nK > 2 ? nK - 2 : 0) : nK - 1;
+  stage(0);
   wait_vmcnt0();
   __syncthreads();
   read_frags(smem, 0, xa, wa);
   for (int ks = 0; ks < nK; ++ks) {
     const int cur = ks & 1;
     const char* base = smem + cur * STAGE;
-    if (ks + 1 < nK) stage(ks + 1, cur ^ 1);
+    if (ks + 1 < nK) stage(cur ^ 1);
+    if (ks == ep_at) ep.load(a, ep_mrow, ep_nbase);  // epilogue operands ride along with the last stages
     read_frags(base, 1, xb, wb);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -144,41 +232,7 @@ __global__ __launch_bounds__(BM * 2, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   }
 
   // --- epilogue: lane owns channels n..n+3 of pixel m for every (i, j) block
-  const int nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
-#pragma unroll
-  for (int j = 0; j < MB; ++j) {
-    const int m = m0 + wm * 64 + j * 16 + (lane & 15);
-    if (m >= a.M) continue;
-    const int b = fdiv(m, a.divSS);
-    const int rem = m - b * SS;
-    const int ii = fdiv(rem, a.divS);
-    const int jj = rem - ii * a.S;
-    const size_t ooff = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int n = nbase + i * 16;
-      f32x4 v = acc[i][j];
-      if constexpr (MODE == MODE_BIAS_RELU) {
-        const f32x4 bb = *(const f32x4*)(a.bias + n);
-        v[0] = fmaxf(v[0] + bb[0], 0.f);
-        v[1] = fmaxf(v[1] + bb[1], 0.f);
-        v[2] = fmaxf(v[2] + bb[2], 0.f);
-        v[3] = fmaxf(v[3] + bb[3], 0.f);
-      } else if constexpr (MODE == MODE_MASK) {
-        const bf16x4 mk = *(const bf16x4*)(a.mask + ooff + n);
-        v[0] = (float)mk[0] > 0.f ? v[0] : 0.f;
-        v[1] = (float)mk[1] > 0.f ? v[1] : 0.f;
-        v[2] = (float)mk[2] > 0.f ? v[2] : 0.f;
-        v[3] = (float)mk[3] > 0.f ? v[3] : 0.f;
-      }
-      bf16x4 o;
-      o[0] = (__bf16)v[0];
-      o[1] = (__bf16)v[1];
-      o[2] = (__bf16)v[2];
-      o[3] = (__bf16)v[3];
-      *(bf16x4*)(a.y + ooff + n) = o;
-    }
-  }
+  ep.store(a, acc, ep_mrow);
 }
 
 // ------------------------------------------------------ forward, halo variant
@@ -199,6 +253,7 @@ __device__ __forceinline__ void vmcnt_wait() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
   else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
   else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
   else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -350,6 +405,171 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_halo_kernel(ConvFwdArgs a) {
   }
 }
 
+
+// ------------------------------------------------------ forward, ring variant
+// Same gather/implicit-GEMM math as conv_fwd_kernel, restructured so the
+// global->LDS DMA stays in flight across barriers (the 2-buffer kernel's
+// __syncthreads() drains vmcnt every K-step):
+//   * K-step = one tap x 32 channels; A = 256 pixel rows x 64 B (16 KB),
+//     B = BN weight rows x 64 B; 4 LDS slots (112 KB at BN = 192);
+//   * loads run 3 steps ahead: at step ks the wave waits (counted vmcnt) only
+//     for its own pieces of step ks+1, passes a raw s_barrier, issues step
+//     ks+3 into the slot freed by step ks-1, reads step ks+1's fragments and
+//     only then issues step ks's 24 MFMAs, so the LDS latency hides under them;
+//   * 64-B rows swizzled phys = chunk ^ (((row >> 2) & 1) << 1) (conflict-free
+//     for the ds_read_b128 lane groups), applied on the DMA source address.
+constexpr int RING_BM = 256;
+constexpr int RING_SLOTS = 4;
+
+__device__ __forceinline__ void vmcnt_wait_dyn(int n) {
+  switch (n) {
+    case 0: vmcnt_wait<0>(); break;
+    case 1: vmcnt_wait<1>(); break;
+    case 2: vmcnt_wait<2>(); break;
+    case 3: vmcnt_wait<3>(); break;
+    default: vmcnt_wait<4>(); break;
+  }
+}
+
+template <int BN, int MODE>
+__global__ __launch_bounds__(512, 1) void conv_fwd_ring_kernel(ConvFwdArgs a) {
+  constexpr int NB = BN / 32;  // 16-wide n blocks per wave (wave covers BN/2 channels)
+  constexpr int MB = 4;        // 16-wide m blocks per wave (wave covers 64 pixels)
+  constexpr int A_BYTES = RING_BM * 64;
+  constexpr int SLOT = A_BYTES + BN * 64;
+  constexpr int BPIECES = BN / 16;  // 1 KB DMA pieces of the weight tile
+  constexpr int BP_MAX = (BPIECES + 7) / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * RING_BM;
+  const int n0 = blockIdx.y * BN;
+  const int SS = a.S * a.S;
+  const int CC2 = a.Cin >> 5;  // 32-channel chunks
+  const int nK = a.K * a.K * CC2;
+
+  // A pieces: wave w stages rows [16w, 16w+16) and [16(w+8), ...); lane -> row lane/4, 16-B chunk lane%4
+  int arow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * (wave + 8 * i) + (lane >> 2);
+    int m = m0 + r;
+    m = m < a.M ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    const int logical = (lane & 3) ^ (((r >> 2) & 1) << 1);
+    arow[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + logical * 8;
+  }
+  const int nbp = BPIECES / 8 + (wave < (BPIECES % 8) ? 1 : 0);  // wave-uniform
+  int brow[BP_MAX];
+#pragma unroll
+  for (int i = 0; i < BP_MAX; ++i) {
+    const int r = 16 * (wave + 8 * i) + (lane >> 2);
+    const int logical = (lane & 3) ^ (((r >> 2) & 1) << 1);
+    brow[i] = (n0 + (r < BN ? r : 0)) * a.Cin + logical * 8;
+  }
+  const int P = 2 + nbp;  // DMA pieces this wave issues per K-step
+  const size_t wtap = (size_t)a.Cout * a.Cin;
+
+  auto issue = [&](int ks) {
+    const int t = ks / CC2;
+    const int c = ks - t * CC2;
+    const int kh = t / a.K;
+    const int kw = t - kh * a.K;
+    const int toff = (kh * a.HPi + kw) * a.Cin + (c << 5);
+    char* base = smem + (ks % RING_SLOTS) * SLOT;
+    glds16(a.x + arow[0] + toff, base + wave * 1024);
+    glds16(a.x + arow[1] + toff, base + (wave + 8) * 1024);
+    const __bf16* wt = a.w + (size_t)t * wtap + (c << 5);
+#pragma unroll
+    for (int i = 0; i < BP_MAX; ++i)
+      if (i < nbp) glds16(wt + brow[i], base + A_BYTES + (wave + 8 * i) * 1024);
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r15 = lane & 15;
+  const int pch = (lane >> 4) ^ (((r15 >> 2) & 1) << 1);
+  const int xoff = (wm * 64 + r15) * 64 + pch * 16;
+  const int woff = A_BYTES + (wn * (BN / 2) + r15) * 64 + pch * 16;
+  auto read_frags = [&](int ks, bf16x8 (&xf)[MB], bf16x8 (&wf)[NB]) {
+    const char* base = smem + (ks % RING_SLOTS) * SLOT;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) xf[j] = *(const bf16x8*)(base + xoff + j * 16 * 64);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) wf[i] = *(const bf16x8*)(base + woff + i * 16 * 64);
+  };
+  auto mfmas = [&](const bf16x8 (&xf)[MB], const bf16x8 (&wf)[NB], int i0, int i1) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = i0; i < i1; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // one K-step: publish step ks+1 (counted vmcnt + raw barrier), half of
+  // step ks's MFMAs, refill the freed slot, read step ks+1's fragments, and
+  // the other half of the MFMAs (covering the LDS read latency)
+  auto step = [&](int ks, const bf16x8 (&xc)[MB], const bf16x8 (&wc)[NB], bf16x8 (&xn)[MB], bf16x8 (&wn_)[NB]) {
+    const bool more = ks + 1 < nK;
+    if (more) {
+      vmcnt_wait_dyn(ks + 2 < nK ? P : 0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(xc, wc, 0, NB / 2);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      if (ks + 3 < nK) issue(ks + 3);
+      read_frags(ks + 1, xn, wn_);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(xc, wc, NB / 2, NB);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  issue(0);
+  if (nK > 1) issue(1);
+  if (nK > 2) issue(2);
+  vmcnt_wait_dyn(nK > 2 ? 2 * P : (nK > 1 ? P : 0));
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  bf16x8 xa[MB], wa[NB], xb[MB], wb[NB];
+  read_frags(0, xa, wa);
+  int ks = 0;
+  for (; ks + 1 < nK; ks += 2) {
+    step(ks, xa, wa, xb, wb);
+    step(ks + 1, xb, wb, xa, wa);
+  }
+  if (ks < nK) step(ks, xa, wa, xb, wb);
+
+  // --- epilogue
+  conv_store_tile<NB, MB, MODE>(a, acc, m0 + wm * 64 + (lane & 15), n0 + wn * (BN / 2) + ((lane >> 4) << 2));
+}
+
+template <int BN, int MODE>
+static void launch_fwd_ring(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int smem = RING_SLOTS * (RING_BM * 64 + BN * 64);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_ring_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);
+    attr = true;
+  }
+  dim3 grid((a.M + RING_BM - 1) / RING_BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_ring_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
+}
+
 template <int BN, int MODE>
 static void launch_fwd_halo(const ConvFwdArgs& a_in, hipStream_t st) {
   constexpr int smem = 2 * HALO_ROWS * 128 + 3 * BN * 128;
@@ -370,17 +590,17 @@ static void launch_fwd_halo(const ConvFwdArgs& a_in, hipStream_t st) {
 
 static int g_fwd_bm = 0;  // 0 = auto
 
-template <int BN, int MODE, int BM>
+template <int BN, int MODE, int BM, int MBW, bool EPF = true>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        smem);
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM>), grid, dim3(BM * 2), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF>), grid, dim3(BM / MBW * 8), smem, st, a);
 }
 
 template <int BN, int MODE>
@@ -393,8 +613,12 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   }
   int bm = g_fwd_bm;
   if (bm <= 0) bm = (a.M >= 256 * 512) ? 256 : 128;
-  if (bm == 256) launch_fwd_bm<BN, MODE, 256>(a, st);
-  else launch_fwd_bm<BN, MODE, 128>(a, st);
+  // tile codes: 128 / 256 (64-pixel waves), 2568 (BM 256, 128-pixel waves: 4 waves, 1 per SIMD)
+  if (bm == 32) launch_fwd_ring<BN, MODE>(a, st);
+  else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
+  else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);  // epilogue loads after the loop
+  else if (bm == 2568) launch_fwd_bm<BN, MODE, 256, 8>(a, st);
+  else launch_fwd_bm<BN, MODE, 128, 4>(a, st);
 }
 
 void set_conv_fwd_tile(int bm) { g_fwd_bm = bm; }

@@ -36,10 +36,14 @@ def timeit(fn):
 res = {}
 fl3 = 2.0 * M * F * F * 9
 fl1 = 2.0 * M * F * 64 * 25
-for bm in (128, 256, -1):
+for bm in (256, 2560, 32, 256, 2560, 32):
     torch.ops.alphago_amd.set_conv_tile(bm)
-    res["fwd3x3_bm%d" % bm] = timeit(lambda: ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1))
-    res["dgrad3x3_bm%d" % bm] = timeit(lambda: ops.conv_fwd(x, wd, None, y, 3, S, 1, 1, mode=ops.MODE_MASK, mask=x))
+    for nm, fn in (("fwd3x3", lambda: ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1)),
+                   ("dgrad3x3", lambda: ops.conv_fwd(x, wd, None, y, 3, S, 1, 1, mode=ops.MODE_MASK, mask=x)),
+                   ("fwd5x5", lambda: ops.conv_fwd(x0, wf1, bias, y, 5, S, 2, 1))):
+        k = "%s_bm%d" % (nm, bm)
+        t = timeit(fn)
+        res[k] = min(t, res.get(k, 1e30))
 torch.ops.alphago_amd.set_conv_tile(0)
 res["fwd3x3"] = timeit(lambda: ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1))
 res["fwd5x5"] = timeit(lambda: ops.conv_fwd(x0, wf1, bias, y, 5, S, 2, 1))

@@ -175,3 +175,59 @@ def test_sgd_update(ops, cuda_device):
     ref = p - 0.01 * 0.5 * g
     ops.sgd_update(p, g, 0.01, 0.5)
     assert torch.allclose(p, ref)
+
+
+@pytest.mark.parametrize("tile", [128, 256, 2568, -1, 32])
+def test_conv_fwd_tile_variants(ops, cuda_device, tile):
+    """Every forward tiling (gather 128/256, 128-pixel waves, halo) on a batch
+    whose pixel count is not a multiple of any tile."""
+    torch.manual_seed(1)
+    B, C, S = 9, 192, 19
+    x = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w = _bf(torch.randn(C, C, 3, 3, device=cuda_device) * 0.05)
+    b = torch.randn(C, device=cuda_device) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    xp = ops.to_padded(x, 1)
+    wp = ops.packed_weight_like(w, C, C)
+    ops.pack_weights([w.contiguous()], [wp])
+    y = ops.padded_empty(B, S, 1, C, cuda_device)
+    try:
+        torch.ops.alphago_amd.set_conv_tile(tile)
+        ops.conv_fwd(xp, wp, b, y, 3, S, 1, 1)
+        torch.cuda.synchronize()
+    finally:
+        torch.ops.alphago_amd.set_conv_tile(0)
+    assert _rel_err(ops.from_padded(y, 1), ref) < 1e-2
+    assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
+
+
+@pytest.mark.parametrize("tile", [32, 256])
+def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
+    """Layer-1 geometry (Cin 64, 5x5, input pad 2) and the masked dgrad mode on each tiling."""
+    torch.manual_seed(2)
+    B, S = 7, 19
+    x = _bf(torch.randn(B, 64, S, S, device=cuda_device))
+    w = _bf(torch.randn(192, 64, 5, 5, device=cuda_device) * 0.05)
+    b = torch.randn(192, device=cuda_device) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=2))
+    xp = ops.to_padded(x, 2)
+    wp = ops.packed_weight_like(w, 64, 192)
+    ops.pack_weights([w.contiguous()], [wp])
+    y = ops.padded_empty(B, S, 1, 192, cuda_device)
+    g = _bf(torch.randn(B, 192, S, S, device=cuda_device))
+    w3 = _bf(torch.randn(192, 192, 3, 3, device=cuda_device) * 0.05)
+    mask = _bf(torch.randn(B, 192, S, S, device=cuda_device)).relu()
+    wd = ops.packed_weight_like(w3, 192, 192, True)
+    wf = ops.packed_weight_like(w3, 192, 192)
+    ops.pack_weights([w3.contiguous()], [wf], [wd])
+    dx = ops.padded_empty(B, S, 1, 192, cuda_device)
+    try:
+        torch.ops.alphago_amd.set_conv_tile(tile)
+        ops.conv_fwd(xp, wp, b, y, 5, S, 2, 1)
+        ops.conv_fwd(ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASK, mask=ops.to_padded(mask, 1))
+        torch.cuda.synchronize()
+    finally:
+        torch.ops.alphago_amd.set_conv_tile(0)
+    assert _rel_err(ops.from_padded(y, 1), ref) < 1e-2
+    ref_dx = torch.nn.grad.conv2d_input(x.shape[:1] + (192, S, S), w3, g, padding=1) * (mask > 0)
+    assert _rel_err(ops.from_padded(dx, 1), ref_dx) < 1e-2
