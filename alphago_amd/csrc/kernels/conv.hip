@@ -427,7 +427,11 @@ __device__ __forceinline__ void vmcnt_wait_dyn(int n) {
     case 1: vmcnt_wait<1>(); break;
     case 2: vmcnt_wait<2>(); break;
     case 3: vmcnt_wait<3>(); break;
-    default: vmcnt_wait<4>(); break;
+    case 4: vmcnt_wait<4>(); break;
+    case 5: vmcnt_wait<5>(); break;
+    case 6: vmcnt_wait<6>(); break;
+    case 7: vmcnt_wait<7>(); break;
+    default: vmcnt_wait<8>(); break;
   }
 }
 
@@ -640,24 +644,74 @@ void launch_conv_fwd(const ConvFwdArgs& a_in, int mode, hipStream_t st) {
 }
 
 // ----------------------------------------------------------------- wgrad
+template <int N>
+__device__ __forceinline__ void lgkm_fence(bf16x4 (&a)[N], bf16x4 (&b)[N]) {
+  static_assert(N >= 1 && N <= 15, "lgkm_fence supports 1..15 pairs (30 asm operands)");
+  if constexpr (N == 15)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]), "+v"(a[11]), "+v"(b[11]), "+v"(a[12]), "+v"(b[12]), "+v"(a[13]), "+v"(b[13]), "+v"(a[14]), "+v"(b[14]));
+  else if constexpr (N == 14)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]), "+v"(a[11]), "+v"(b[11]), "+v"(a[12]), "+v"(b[12]), "+v"(a[13]), "+v"(b[13]));
+  else if constexpr (N == 13)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]), "+v"(a[11]), "+v"(b[11]), "+v"(a[12]), "+v"(b[12]));
+  else if constexpr (N == 12)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]), "+v"(a[11]), "+v"(b[11]));
+  else if constexpr (N == 11)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]));
+  else if constexpr (N == 10)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]));
+  else if constexpr (N == 9)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]));
+  else if constexpr (N == 8)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]));
+  else if constexpr (N == 7)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]));
+  else if constexpr (N == 6)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]));
+  else if constexpr (N == 5)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]));
+  else if constexpr (N == 4)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]));
+  else if constexpr (N == 3)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]));
+  else if constexpr (N == 2)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]));
+  else if constexpr (N == 1)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]));
+}
+
+// ds_read_b64_tr_b16 through inline asm.  The builtin form makes hipcc wait
+// vmcnt(0) before every such read while any LDS-DMA is outstanding (it cannot
+// tell the read from the DMA target), which would drain the ring; the caller
+// waits lgkmcnt itself (lgkm_fence below) before touching the results.
+__device__ __forceinline__ bf16x4 ds_read_tr16_asm(const char* p) {
+  bf16x4 v;
+  const uint32_t off = (uint32_t)(uintptr_t)(AG_LDS(p));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(off));
+  return v;
+}
+
+
 // 512 threads = 8 waves as 2 (n) x 4 (c).  One pipeline stage = KSUB sub-steps
 // of 32 pixels (one barrier per KSUB*32 pixels); each sub-step region is laid
 // out [16-channel block][32 px][16 ch] for the transpose reads.
-template <int WN, int WC, int KSUB>
-__global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
-  constexpr int NBn = WN / 32;  // n blocks per wave (wave covers WN/2)
-  constexpr int NBc = WC / 64;  // c blocks per wave (wave covers WC/4)
+template <int WN, int WC, int KSUB, int NWC = 4>
+__global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
+  // 2 (n) x NWC (c) waves; NWC = 2 gives each wave a 96x96 tile at 192x192
+  // (a third fewer LDS fragment reads per MFMA than NWC = 4)
+  constexpr int NWAVES = 2 * NWC;
+  constexpr int NBn = WN / 32;          // n blocks per wave (wave covers WN/2)
+  constexpr int NBc = WC / (16 * NWC);  // c blocks per wave (wave covers WC/NWC)
   constexpr int DZ_BYTES = WN * 64;  // [WN/16][32 px][16 ch] bf16
   constexpr int X_BYTES = WC * 64;
   constexpr int SUB = DZ_BYTES + X_BYTES;
   constexpr int STAGE = SUB * KSUB;
   constexpr int NINSTR = (WN + WC) / 16 * KSUB;  // 1 KB glds pieces per stage
-  constexpr int IPW = (NINSTR + 7) / 8;
+  constexpr int IPW = (NINSTR + NWAVES - 1) / NWAVES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63;
   const int wave = wave_id();
-  const int wn = wave >> 2, wc = wave & 3;
+  const int wn = wave / NWC, wc = wave % NWC;
   const int split = blockIdx.x;
   const int t = blockIdx.y;
   const int ncb = a.Cin / WC;
@@ -687,18 +741,22 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
       dzr[sub] = px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po) * a.Cout : 0;  // 0 = zero border
       xr[sub] = ((b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi) * a.Cin + toff;
     }
+    // dz pieces and x pieces in separate loops: a per-piece select between the
+    // two source tensors makes hipcc drain vmcnt(0) before the LDS reads that
+    // follow, which would turn the double buffer into a synchronous load
 #pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const int j = wave * IPW + i;
-      if (j < NINSTR) {
+    for (int sub = 0; sub < KSUB; ++sub) {
+      const __bf16* dsrc = a.dz + dzr[sub] + n0 + half;
+      const __bf16* xsrc = a.x + xr[sub] + half;
 #pragma unroll
-        for (int sub = 0; sub < KSUB; ++sub) {
-          const int jj = j - sub * ((WN + WC) / 16);
-          if (jj < 0 || jj >= (WN + WC) / 16) continue;
-          char* dst = base + sub * SUB + jj * 1024;
-          if (jj < WN / 16) glds16(a.dz + dzr[sub] + n0 + jj * 16 + half, dst);
-          else glds16(a.x + xr[sub] + (jj - WN / 16) * 16 + half, dst);
-        }
+      for (int i = 0; i < IPW; ++i) {
+        const int jj = wave * IPW + i - sub * ((WN + WC) / 16);
+        if (jj >= 0 && jj < WN / 16) glds16(dsrc + jj * 16, base + sub * SUB + jj * 1024);
+      }
+#pragma unroll
+      for (int i = 0; i < IPW; ++i) {
+        const int jj = wave * IPW + i - sub * ((WN + WC) / 16);
+        if (jj >= WN / 16 && jj < (WN + WC) / 16) glds16(xsrc + (jj - WN / 16) * 16, base + sub * SUB + jj * 1024);
       }
     }
   };
@@ -731,21 +789,28 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
 #pragma unroll
     for (int sub = 0; sub < KSUB; ++sub) {
       const char* base = smem + cur * STAGE + sub * SUB;
-      bf16x8 af[NBn], bfm[NBc];
+      bf16x4 tl[NBn + NBc], th[NBn + NBc];
 #pragma unroll
       for (int i = 0; i < NBn; ++i) {
         const char* cb = base + (wn * NBn + i) * 1024;
-        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr0));
-        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr1));
-        af[i] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        tl[i] = ds_read_tr16_asm(cb + tr0);
+        th[i] = ds_read_tr16_asm(cb + tr1);
       }
 #pragma unroll
       for (int j = 0; j < NBc; ++j) {
         const char* cb = base + DZ_BYTES + (wc * NBc + j) * 1024;
-        bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr0));
-        bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((__attribute__((address_space(3))) bf16x4*)(cb + tr1));
-        bfm[j] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        tl[NBn + j] = ds_read_tr16_asm(cb + tr0);
+        th[NBn + j] = ds_read_tr16_asm(cb + tr1);
       }
+      lgkm_fence<NBn + NBc>(tl, th);
+      bf16x8 af[NBn], bfm[NBc];
+#pragma unroll
+      for (int i = 0; i < NBn; ++i)
+        af[i] = bf16x8{tl[i][0], tl[i][1], tl[i][2], tl[i][3], th[i][0], th[i][1], th[i][2], th[i][3]};
+#pragma unroll
+      for (int j = 0; j < NBc; ++j)
+        bfm[j] = bf16x8{tl[NBn + j][0], tl[NBn + j][1], tl[NBn + j][2], tl[NBn + j][3],
+                        th[NBn + j][0], th[NBn + j][1], th[NBn + j][2], th[NBn + j][3]};
 #pragma unroll
       for (int i = 0; i < NBn; ++i)
 #pragma unroll
@@ -765,6 +830,170 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
   }
 
   // --- write the split's partial tile: D[n][c], lane owns n..n+3 at column c
+  float* out = a.slab + ((size_t)split * a.T + t) * (size_t)a.Cout * a.Cin;
+  const int nb0 = n0 + wn * (WN / 2) + ((lane >> 4) << 2);
+  const int cbase = c0 + wc * (WC / NWC) + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < NBn; ++i)
+#pragma unroll
+    for (int j = 0; j < NBc; ++j) {
+      const int n = nb0 + i * 16;
+      const int c = cbase + j * 16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(size_t)(n + r) * a.Cin + c] = acc[i][j][r];
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < NBn; ++i) {
+      float s = dbs[i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 16) a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / 2) + i * 16 + lane] = s;
+    }
+  }
+}
+
+
+// wgrad, ring variant: same tile math and LDS image as conv_wgrad_kernel
+// (KSUB = 1, 32-pixel K-steps), but 4 LDS slots with the DMA running 3 steps
+// ahead, counted vmcnt for the wave's own pieces of the next step and a raw
+// s_barrier, so no barrier ever drains the loads in flight.
+template <int WN, int WC, int WRING_SLOTS>
+__global__ __launch_bounds__(512, 1) void conv_wgrad_ring_kernel(ConvWgradArgs a) {
+  constexpr int AHEAD = WRING_SLOTS - 1;  // steps the DMA runs ahead of the MFMAs
+  constexpr int NBn = WN / 32;
+  constexpr int NBc = WC / 64;
+  constexpr int DZ_BYTES = WN * 64;
+  constexpr int X_BYTES = WC * 64;
+  constexpr int SLOT = DZ_BYTES + X_BYTES;
+  constexpr int NINSTR = (WN + WC) / 16;
+  constexpr int IPW = (NINSTR + 7) / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wn = wave >> 2, wc = wave & 3;
+  const int split = blockIdx.x;
+  const int t = blockIdx.y;
+  const int ncb = a.Cin / WC;
+  const int n0 = (blockIdx.z / ncb) * WN;
+  const int c0 = (blockIdx.z % ncb) * WC;
+  const int kh = t / a.K, kw = t - (t / a.K) * a.K;
+  const int toff = (kh * a.HPi + kw) * a.Cin + c0;
+  const int SS = a.S * a.S;
+  const int ks_begin = split * a.ksteps_per_split;
+  int ks_end = ks_begin + a.ksteps_per_split;
+  const int nks_total = (a.M + 31) / 32;
+  if (ks_end > nks_total) ks_end = nks_total;
+  const int jlo = wave * IPW;
+  const int P = (NINSTR - jlo) < 0 ? 0 : ((NINSTR - jlo) < IPW ? (NINSTR - jlo) : IPW);  // pieces per step
+
+  auto issue = [&](int ks) {
+    const int half = (lane & 1) * 8;
+    char* base = smem + (ks % WRING_SLOTS) * SLOT;
+    const int px = ks * 32 + (lane >> 1);
+    const int pm = px < a.M ? px : a.M - 1;
+    const int b = fdiv(pm, a.divSS);
+    const int rem = pm - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jx = rem - ii * a.S;
+    const int dzr = px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po) * a.Cout : 0;  // 0 = zero border
+    const int xr = ((b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi) * a.Cin + toff;
+    // dz pieces and x pieces in separate (wave-uniform) loops: a per-piece
+    // select between the two source tensors makes hipcc drain vmcnt before the
+    // next LDS reads
+    const __bf16* dsrc = a.dz + dzr + n0 + half;
+    const __bf16* xsrc = a.x + xr + half;
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int j = jlo + i;
+      if (j < WN / 16) glds16(dsrc + j * 16, base + j * 1024);
+    }
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int j = jlo + i;
+      if (j >= WN / 16 && j < NINSTR) glds16(xsrc + (j - WN / 16) * 16, base + j * 1024);
+    }
+  };
+
+  f32x4 acc[NBn][NBc];
+#pragma unroll
+  for (int i = 0; i < NBn; ++i)
+#pragma unroll
+    for (int j = 0; j < NBc; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbs[NBn];
+#pragma unroll
+  for (int i = 0; i < NBn; ++i) dbs[i] = 0.f;
+  const bool do_bias = (t == 0) && (c0 == 0) && (wc == 0);
+
+  const int g = lane >> 4;
+  const int q = (lane & 15) >> 2;
+  const int p = lane & 3;
+  const int tr0 = (4 * g + q) * 32 + p * 8;
+  const int tr1 = (16 + 4 * g + q) * 32 + p * 8;
+
+  const int nst = ks_end - ks_begin;
+  if (nst > 0) {
+#pragma unroll
+    for (int d = 0; d < AHEAD; ++d)
+      if (d < nst) issue(ks_begin + d);
+    vmcnt_wait_dyn(P * (nst > AHEAD ? AHEAD - 1 : nst - 1));
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  for (int ks = ks_begin; ks < ks_end; ++ks) {
+    if (ks + AHEAD < ks_end) issue(ks + AHEAD);  // into the slot step ks-1 used (all waves are past its reads)
+    const char* base = smem + (ks % WRING_SLOTS) * SLOT;
+    bf16x4 tl[NBn + NBc], th[NBn + NBc];
+#pragma unroll
+    for (int i = 0; i < NBn; ++i) {
+      const char* cb = base + (wn * NBn + i) * 1024;
+      tl[i] = ds_read_tr16_asm(cb + tr0);
+      th[i] = ds_read_tr16_asm(cb + tr1);
+    }
+#pragma unroll
+    for (int j = 0; j < NBc; ++j) {
+      const char* cb = base + DZ_BYTES + (wc * NBc + j) * 1024;
+      tl[NBn + j] = ds_read_tr16_asm(cb + tr0);
+      th[NBn + j] = ds_read_tr16_asm(cb + tr1);
+    }
+    // lgkmcnt(0) with every read result as an in/out operand: nothing that
+    // uses them can be scheduled above the wait
+    lgkm_fence<NBn + NBc>(tl, th);
+    bf16x8 af[NBn], bfm[NBc];
+#pragma unroll
+    for (int i = 0; i < NBn; ++i)
+      af[i] = bf16x8{tl[i][0], tl[i][1], tl[i][2], tl[i][3], th[i][0], th[i][1], th[i][2], th[i][3]};
+#pragma unroll
+    for (int j = 0; j < NBc; ++j)
+      bfm[j] = bf16x8{tl[NBn + j][0], tl[NBn + j][1], tl[NBn + j][2], tl[NBn + j][3],
+                      th[NBn + j][0], th[NBn + j][1], th[NBn + j][2], th[NBn + j][3]};
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < NBn; ++i)
+#pragma unroll
+      for (int j = 0; j < NBc; ++j) acc[i][j] = mfma16x16x32(af[i], bfm[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < NBn; ++i) {
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += (float)af[i][e];
+        dbs[i] += s;
+      }
+    }
+    if (ks + 1 < ks_end) {
+      const int ahead = ks_end - ks - 2;  // steps issued beyond ks+1 (at most AHEAD-1)
+      vmcnt_wait_dyn(P * (ahead > AHEAD - 1 ? AHEAD - 1 : ahead));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
   float* out = a.slab + ((size_t)split * a.T + t) * (size_t)a.Cout * a.Cin;
   const int nb0 = n0 + wn * (WN / 2) + ((lane >> 4) << 2);
   const int cbase = c0 + wc * (WC / 4) + (lane & 15);
@@ -789,19 +1018,49 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
 }
 
 constexpr int kWgradKsub = 1;
+static int g_wgrad_variant = 0;  // 0 = 2-buffer, 3/4 = ring with that many LDS slots
+
+template <int WN, int WC, int NS>
+static void launch_wgrad_ring(const ConvWgradArgs& a, dim3 grid, hipStream_t st) {
+  constexpr int smem = NS * (WN + WC) * 64;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_wgrad_ring_kernel<WN, WC, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_wgrad_ring_kernel<WN, WC, NS>), grid, dim3(512), smem, st, a);
+}
 
 template <int WN, int WC>
 static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
+  dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
+  if (g_wgrad_variant == 3 || g_wgrad_variant == 4) {
+    if (g_wgrad_variant == 3) launch_wgrad_ring<WN, WC, 3>(a, grid, st);
+    else launch_wgrad_ring<WN, WC, 4>(a, grid, st);
+    return;
+  }
   constexpr int KS = kWgradKsub;
   constexpr int smem = 2 * (WN + WC) * 64 * KS;
+  if (g_wgrad_variant == 2 && WC % 32 == 0 && WC >= 64) {
+    static bool attr2 = false;
+    if (!attr2) {
+      hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          smem);
+      attr2 = true;
+    }
+    hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS, 2>), grid, dim3(256), smem, st, a);
+    return;
+  }
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
-  dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
   hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS>), grid, dim3(512), smem, st, a);
 }
+
+void set_wgrad_variant(int v) { g_wgrad_variant = v; }
 
 int wgrad_stage_pixels() { return 32 * kWgradKsub; }
 

@@ -116,7 +116,8 @@ struct FeaturizeArgs {
 void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 void set_conv_fwd_tile(int bm);  // 0 = auto, -1 = halo kernel, 128/256 = gather kernel tile (A/B tests)
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
-int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
+int wgrad_stage_pixels();
+void set_wgrad_variant(int v);  // 0 = 2-buffer (default), 3 / 4 = ring with that many LDS slots  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
 void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st);

@@ -313,6 +313,7 @@ void featurize(const Tensor& board, const Tensor& ages, const Tensor& meta, cons
 }
 
 void set_conv_tile(int64_t bm) { agk::set_conv_fwd_tile((int)bm); }
+void set_wgrad_variant(int64_t v) { agk::set_wgrad_variant((int)v); }
 
 void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
   CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
@@ -341,6 +342,7 @@ TORCH_LIBRARY(alphago_amd, m) {
       "featurize(Tensor board, Tensor ages, Tensor meta, Tensor? ladder, int[] fids, int[] fplanes, Tensor(a!)? planes, "
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
   m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
+  m.def("set_wgrad_variant(int v) -> ()", &set_wgrad_variant);
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {

@@ -51,7 +51,12 @@ res["dgrad3x3"] = timeit(lambda: ops.conv_fwd(x, wd, None, y, 3, S, 1, 1, mode=o
 splits = [int(s) for s in a.splits.split(",")] if a.splits else [ops.wgrad_splits(M, 9)]
 for ns in splits:
     slab = torch.empty(ns, 9, F, F, device=dev); dbs = torch.zeros(ns, F, device=dev)
-    res["wgrad3x3_s%d" % ns] = timeit(lambda: ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1))
+    for rep in range(2):
+        for v in (0, 2, 3):
+            torch.ops.alphago_amd.set_wgrad_variant(v)
+            k = "wgrad3x3_v%d_s%d" % (v, ns)
+            res[k] = min(res.get(k, 1e30), timeit(lambda: ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1)))
+    torch.ops.alphago_amd.set_wgrad_variant(0)
     res["reduce_s%d" % ns] = timeit(lambda: ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0))
 out = {k: {"us": round(v, 1), "TF": round((fl1 if "5x5" in k else fl3) / (v * 1e-6) / 1e12, 1) if "reduce" not in k else None} for k, v in res.items()}
 print(json.dumps({"batch": B, "F": F, **out}))

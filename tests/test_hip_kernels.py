@@ -80,8 +80,11 @@ def test_conv_dgrad_with_relu_mask(ops, cuda_device, B, C, K):
     assert _rel_err(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("B,Cin,Cout,K,Pin", [(6, 192, 192, 3, 1), (5, 64, 192, 5, 2), (3, 64, 64, 3, 1), (9, 128, 128, 3, 1)])
-def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin):
+@pytest.mark.parametrize("variant", [0, 2, 3, 4])
+@pytest.mark.parametrize("B,Cin,Cout,K,Pin,nsplit", [(6, 192, 192, 3, 1, None), (5, 64, 192, 5, 2, None),
+                                                    (3, 64, 64, 3, 1, None), (9, 128, 128, 3, 1, None),
+                                                    (7, 192, 192, 3, 1, 1), (4, 192, 192, 3, 1, 3)])
+def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     torch.manual_seed(2)
     S = 19
     x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
@@ -91,10 +94,14 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin):
     xp = ops.to_padded(x, Pin)
     dzp = ops.to_padded(dz, 1)
     M = B * S * S
-    ns = ops.wgrad_splits(M, K * K)
+    ns = nsplit or ops.wgrad_splits(M, K * K)
     slab = torch.empty(ns, K * K, Cout, Cin, device=cuda_device)
     dbs = torch.zeros(ns, Cout, device=cuda_device)
-    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1)
+    try:
+        torch.ops.alphago_amd.set_wgrad_variant(variant)
+        ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1)
+    finally:
+        torch.ops.alphago_amd.set_wgrad_variant(0)
     gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
     gb = torch.zeros(Cout, device=cuda_device)
     ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
