@@ -1,0 +1,275 @@
+// FP8 (OCP e4m3) implicit-GEMM convolution on the gfx950 block-scaled MFMA
+// v_mfma_scale_f32_16x16x128_f8f6f4 — twice the bf16 MFMA rate (BASELINE
+// config "fp8 MFMA conv path").
+//
+// Same gather structure as conv_fwd_kernel (conv.hip), re-cut for 1-byte
+// operands:
+//   * activations: zero-bordered NHWC e4m3, channels padded to 64 (one 64-B
+//     "chunk" per pixel per 64 channels); weights packed [chunk q][Cout][64 B]
+//     with q = tap * (Cin/64) + c, the chunk count padded to even with zeros;
+//   * a K-step is TWO chunks (K = 128, possibly two different taps): each
+//     128-B LDS row is assembled from two 64-B source rows by the per-lane
+//     source addresses of global_load_lds_dwordx4;
+//   * 16-B chunks of a row are XOR-swizzled by fp8_swz(row) (conflict-free
+//     for the two ds_read_b128 of a lane's 32-byte fragment);
+//   * per-tensor power-of-two scales are passed as the MFMA's E8M0 block
+//     scales (read from device memory, so a captured graph picks up new
+//     scales), the epilogue adds bias, applies ReLU, tracks the output amax
+//     (atomicMax, delayed scaling) and writes bf16 and/or e4m3 outputs.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace agk {
+
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+__device__ __forceinline__ int fp8_swz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 2); }
+
+__device__ __forceinline__ f32x4 mfma_fp8(const i32x8& a, const i32x8& b, const f32x4& c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+}
+
+template <int BN, bool OUT_BF16, bool OUT_FP8>
+__global__ __launch_bounds__(512, 1) void conv_fwd_fp8_kernel(ConvFp8Args a) {
+  constexpr int BM = 256;
+  constexpr int NB = BN / 32;  // 16-wide n blocks per wave (wave covers BN/2)
+  constexpr int MB = 4;        // 16-wide m blocks per wave (64 pixels)
+  constexpr int A_BYTES = BM * 128;
+  constexpr int B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int B_INSTR = BN / 64;  // 1-KB weight pieces per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int SS = a.S * a.S;
+  const int CC = a.Cin >> 6;
+  const int nK = a.nch >> 1;
+  const int qmax = a.K * a.K * CC - 1;  // last real chunk (padding chunks re-read it; their weights are 0)
+  const int sx = a.scales[0], sw = a.scales[1];
+
+  // A staging: 4 pieces per wave; lane -> row 8i + lane/8 of the wave's 32 rows,
+  // physical 16-B chunk lane%8 -> logical chunk (which half = which K chunk)
+  int abase[4], alc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = wave * 32 + i * 8 + (lane >> 3);
+    int m = m0 + r;
+    m = m < a.M ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    alc[i] = (lane & 7) ^ fp8_swz(r);
+    abase[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + (alc[i] & 3) * 16;
+  }
+  int bbase[B_INSTR], blc[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int r = wave * (BN / 8) + i * 8 + (lane >> 3);
+    blc[i] = (lane & 7) ^ fp8_swz(r);
+    bbase[i] = (n0 + r) * 64 + (blc[i] & 3) * 16;
+  }
+
+  auto chunk_off = [&](int q) {  // activation offset of chunk q (tap shift + channel block)
+    q = q < qmax ? q : qmax;
+    const int t = q / CC;
+    const int c = q - t * CC;
+    const int kh = t / a.K;
+    const int kw = t - kh * a.K;
+    return (kh * a.HPi + kw) * a.Cin + c * 64;
+  };
+  auto stage = [&](int ks, int buf) {
+    const int q0 = 2 * ks;
+    const int off0 = chunk_off(q0), off1 = chunk_off(q0 + 1);
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds16(a.x + abase[i] + ((alc[i] >> 2) ? off1 : off0), base + (wave * 32 + i * 8) * 128);
+    const size_t w0 = (size_t)q0 * a.Cout * 64;
+    const size_t w1 = w0 + (size_t)a.Cout * 64;
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i)
+      glds16(a.w + bbase[i] + ((blc[i] >> 2) ? w1 : w0), base + A_BYTES + (wave * (BN / 8) + i * 8) * 128);
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment: row (lane & 15) of a 16-row block, logical chunks 2g, 2g+1 (g = lane >> 4)
+  const int r15 = lane & 15;
+  const int g = lane >> 4;
+  const int c0 = ((2 * g) ^ fp8_swz(r15)) << 4;
+  const int c1 = ((2 * g + 1) ^ fp8_swz(r15)) << 4;
+  const int xrow = (wm * 64 + r15) * 128;
+  const int wrow = A_BYTES + (wn * (BN / 2) + r15) * 128;
+  auto frag = [&](const char* p) {
+    const int4 lo = *(const int4*)(p + c0);
+    const int4 hi = *(const int4*)(p + c1);
+    return i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  };
+
+  stage(0, 0);
+  wait_vmcnt0();
+  __syncthreads();
+  for (int ks = 0; ks < nK; ++ks) {
+    const int cur = ks & 1;
+    const char* base = smem + cur * STAGE;
+    if (ks + 1 < nK) stage(ks + 1, cur ^ 1);
+    i32x8 xf[MB], wf[NB];
+#pragma unroll
+    for (int j = 0; j < MB; ++j) xf[j] = frag(base + xrow + j * 16 * 128);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) wf[i] = frag(base + wrow + i * 16 * 128);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) acc[i][j] = mfma_fp8(wf[i], xf[j], acc[i][j], sw, sx);
+    __builtin_amdgcn_s_setprio(0);
+    wait_vmcnt0();
+    __syncthreads();
+  }
+
+  // --- epilogue: bias + ReLU, amax, bf16 and/or e4m3 stores (lane: 4 channels of one pixel per block)
+  const int nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
+  f32x4 bb[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) bb[i] = *(const f32x4*)(a.bias + nbase + i * 16);
+  const float osc = a.out_scale[0];
+  float vmax = 0.f;
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    int m = m0 + wm * 64 + j * 16 + (lane & 15);
+    const bool ok = m < a.M;
+    m = ok ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    const size_t ooff = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      f32x4 v = acc[i][j];
+      v[0] = fmaxf(v[0] + bb[i][0], 0.f);
+      v[1] = fmaxf(v[1] + bb[i][1], 0.f);
+      v[2] = fmaxf(v[2] + bb[i][2], 0.f);
+      v[3] = fmaxf(v[3] + bb[i][3], 0.f);
+      if (ok) vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+      const int n = nbase + i * 16;
+      if (!ok) continue;
+      if constexpr (OUT_BF16) {
+        bf16x4 o;
+        o[0] = (__bf16)v[0];
+        o[1] = (__bf16)v[1];
+        o[2] = (__bf16)v[2];
+        o[3] = (__bf16)v[3];
+        *(bf16x4*)(a.y_bf16 + ooff + n) = o;
+      }
+      if constexpr (OUT_FP8) {
+        const float s0 = fminf(v[0] * osc, 448.f), s1 = fminf(v[1] * osc, 448.f);
+        const float s2 = fminf(v[2] * osc, 448.f), s3 = fminf(v[3] * osc, 448.f);
+        int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+        pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+        *(int*)(a.y_fp8 + ooff + n) = pk;
+      }
+    }
+  }
+  if (a.amax) {
+    vmax = wave_max(vmax);
+    if (lane == 0) atomicMax(a.amax, __float_as_uint(vmax));
+  }
+}
+
+template <int BN, bool OB, bool OF>
+static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
+  constexpr int smem = 2 * (256 * 128 + BN * 128);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_fp8_kernel<BN, OB, OF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);
+    attr = true;
+  }
+  dim3 grid((a.M + 255) / 256, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_fp8_kernel<BN, OB, OF>), grid, dim3(512), smem, st, a);
+}
+
+template <int BN>
+static void launch_fp8_bn(const ConvFp8Args& a, hipStream_t st) {
+  const bool ob = a.y_bf16 != nullptr, of = a.y_fp8 != nullptr;
+  if (ob && of) launch_fp8_t<BN, true, true>(a, st);
+  else if (ob) launch_fp8_t<BN, true, false>(a, st);
+  else launch_fp8_t<BN, false, true>(a, st);
+}
+
+void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
+  ConvFp8Args a = a_in;
+  a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
+  a.divS = make_fastdiv((uint32_t)a.S);
+  if (a.Cout % 192 == 0) launch_fp8_bn<192>(a, st);
+  else if (a.Cout % 128 == 0) launch_fp8_bn<128>(a, st);
+  else launch_fp8_bn<64>(a, st);
+}
+
+// ------------------------------------------------------------- packing
+// weights: fp32 OIHW [Cout_real][Cin_real][K][K] -> e4m3 [nch][Cout_p][64] * 2^e
+__global__ void pack_weights_fp8_kernel(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p,
+                                        int Cin_p, int nch, float scale) {
+  const int CC = Cin_p >> 6;
+  const long total = (long)nch * Cout_p * 64;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
+    const int byte = (int)(idx & 63);
+    const long qn = idx >> 6;
+    const int n = (int)(qn % Cout_p);
+    const int q = (int)(qn / Cout_p);
+    const int t = q / CC;
+    const int c = (q - t * CC) * 64 + byte;
+    float v = 0.f;
+    if (t < K * K && n < Cout_real && c < Cin_real) {
+      const int kh = t / K, kw = t - (t / K) * K;
+      v = w[(((size_t)n * Cin_real + c) * K + kh) * K + kw] * scale;
+      v = fminf(fmaxf(v, -448.f), 448.f);
+    }
+    out[idx] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
+  }
+}
+
+void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p, int Cin_p,
+                             int nch, float scale, hipStream_t st) {
+  const long total = (long)nch * Cout_p * 64;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pack_weights_fp8_kernel, dim3(blocks), dim3(256), 0, st, w, out, Cout_real, Cin_real, K, Cout_p,
+                     Cin_p, nch, scale);
+}
+
+// e4m3 quantisation of a padded NHWC bf16 tensor (interior and borders alike: borders stay 0)
+__global__ void quantize_fp8_kernel(const __bf16* x, uint8_t* y, long n4, float scale) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const bf16x4 v = *(const bf16x4*)(x + 4 * i);
+    const float s0 = fminf(fmaxf((float)v[0] * scale, -448.f), 448.f);
+    const float s1 = fminf(fmaxf((float)v[1] * scale, -448.f), 448.f);
+    const float s2 = fminf(fmaxf((float)v[2] * scale, -448.f), 448.f);
+    const float s3 = fminf(fmaxf((float)v[3] * scale, -448.f), 448.f);
+    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+    pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+    *(int*)(y + 4 * i) = pk;
+  }
+}
+
+void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st) {
+  const long n4 = n / 4;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(quantize_fp8_kernel, dim3(blocks), dim3(256), 0, st, x, y, n4, scale);
+}
+
+}  // namespace agk

@@ -113,6 +113,21 @@ struct FeaturizeArgs {
   uint8_t chan_plane[kFzMaxChannels];
 };
 
+struct ConvFp8Args {
+  const uint8_t* x;         // padded NHWC e4m3 [B][HPi][HPi][Cin], Cin % 64 == 0
+  const uint8_t* w;         // e4m3 [nch][Cout][64], chunk q = tap * (Cin/64) + c, nch even (zero tail)
+  const float* bias;        // [Cout]
+  const int* scales;        // [2] E8M0 exponents for the MFMA: {activations, weights} (127 = 2^0)
+  const float* out_scale;   // [1] multiplier applied before the e4m3 output conversion
+  __bf16* y_bf16;           // optional padded NHWC bf16 output
+  uint8_t* y_fp8;           // optional padded NHWC e4m3 output
+  unsigned* amax;           // optional running max of the ReLU output (float bits)
+  int M, S, Cin, Cout, K;
+  int HPi, offi, HPo, Po;
+  int nch;
+  FastDiv divSS, divS;      // filled by the launcher
+};
+
 void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 void set_conv_fwd_tile(int bm);  // 0 = auto, -1 = halo kernel, 128/256 = gather kernel tile (A/B tests)
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
@@ -126,6 +141,10 @@ void launch_value_out(const ValueOutArgs& a, hipStream_t st);
 void launch_pack_input(const PackInputArgs& a, hipStream_t st);
 void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st);
 void launch_featurize(const FeaturizeArgs& a, hipStream_t st);
+void launch_conv_fwd_fp8(const ConvFp8Args& a, hipStream_t st);
+void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p, int Cin_p,
+                             int nch, float scale, hipStream_t st);
+void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st);
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
 
 }  // namespace agk

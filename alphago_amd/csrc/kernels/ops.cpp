@@ -312,6 +312,61 @@ void featurize(const Tensor& board, const Tensor& ages, const Tensor& meta, cons
   agk::launch_featurize(a, cur_stream());
 }
 
+// x: (B, HPi, HPi, Cin) uint8 (e4m3); w: (nch, Cout, 64) uint8; scales int32[2]; out_scale f32[1]
+void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales, const Tensor& out_scale,
+                  const c10::optional<Tensor>& amax, const c10::optional<Tensor>& y_bf16,
+                  const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S, int64_t Pin, int64_t Po) {
+  CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.scalar_type() == at::kByte && w.scalar_type() == at::kByte, "fp8 tensors are stored as uint8");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 3 && w.size(2) == 64, "x (B,HP,HP,C), w (nch, Cout, 64)");
+  TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2 && out_scale.scalar_type() == at::kFloat, "scales");
+  CHECK_F32(bias);
+  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3), nch = w.size(0), Cout = w.size(1);
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && nch % 2 == 0 && nch >= K * K * (Cin / 64), "channel geometry");
+  TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin, "padding/geometry mismatch");
+  TORCH_CHECK(y_bf16.has_value() || y_fp8.has_value(), "need an output");
+  agk::ConvFp8Args a{};
+  a.x = x.data_ptr<uint8_t>(); a.w = w.data_ptr<uint8_t>(); a.bias = bias.data_ptr<float>();
+  a.scales = scales.data_ptr<int>(); a.out_scale = out_scale.data_ptr<float>();
+  const int64_t HPo = S + 2 * Po;
+  if (y_bf16.has_value()) {
+    CHECK_BF16(*y_bf16); CHECK_CONTIG(*y_bf16);
+    TORCH_CHECK(y_bf16->size(0) == B && y_bf16->size(1) == HPo && y_bf16->size(3) == Cout, "y_bf16 shape");
+    a.y_bf16 = bfp_mut(*y_bf16);
+  }
+  if (y_fp8.has_value()) {
+    TORCH_CHECK(y_fp8->scalar_type() == at::kByte && y_fp8->is_contiguous(), "y_fp8 uint8");
+    TORCH_CHECK(y_fp8->size(0) == B && y_fp8->size(1) == HPo && y_fp8->size(3) == Cout, "y_fp8 shape");
+    a.y_fp8 = y_fp8->data_ptr<uint8_t>();
+  }
+  if (amax.has_value()) {
+    TORCH_CHECK(amax->scalar_type() == at::kInt && amax->numel() >= 1, "amax int32[1] (float bits)");
+    a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
+  }
+  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po; a.nch = (int)nch;
+  TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31), "tensor too large for int32 offsets");
+  if (a.M == 0) return;
+  agk::launch_conv_fwd_fp8(a, cur_stream());
+}
+
+void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale) {
+  CHECK_F32(w); CHECK_CONTIG(w);
+  TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.dim() == 3 && out.size(2) == 64, "out");
+  const int K = (int)w.size(2);
+  const int nch = (int)out.size(0), Cout_p = (int)out.size(1);
+  const int Cin_p = ((int)w.size(1) + 63) / 64 * 64;
+  TORCH_CHECK(nch % 2 == 0 && nch >= K * K * (Cin_p / 64) && Cout_p >= w.size(0), "packed geometry");
+  agk::launch_pack_weights_fp8(w.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)w.size(0), (int)w.size(1), K, Cout_p,
+                               Cin_p, nch, (float)scale, cur_stream());
+}
+
+void quantize_fp8(const Tensor& x, const Tensor& y, double scale) {
+  CHECK_BF16(x); CHECK_CONTIG(x);
+  TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 4 == 0, "y");
+  agk::launch_quantize_fp8(bfp(x), y.data_ptr<uint8_t>(), x.numel(), (float)scale, cur_stream());
+}
+
 void set_conv_tile(int64_t bm) { agk::set_conv_fwd_tile((int)bm); }
 void set_wgrad_variant(int64_t v) { agk::set_wgrad_variant((int)v); }
 
@@ -341,6 +396,11 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "featurize(Tensor board, Tensor ages, Tensor meta, Tensor? ladder, int[] fids, int[] fplanes, Tensor(a!)? planes, "
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
+  m.def(
+      "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
+      "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po) -> ()");
+  m.def("pack_weights_fp8(Tensor w, Tensor(a!) out, float scale) -> ()");
+  m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
   m.def("set_wgrad_variant(int v) -> ()", &set_wgrad_variant);
 }
@@ -357,4 +417,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("pack_weights", &pack_weights);
   m.impl("sgd_update", &sgd_update);
   m.impl("featurize", &featurize);
+  m.impl("conv_fwd_fp8", &conv_fwd_fp8);
+  m.impl("pack_weights_fp8", &pack_weights_fp8);
+  m.impl("quantize_fp8", &quantize_fp8);
 }

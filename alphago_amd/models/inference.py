@@ -18,6 +18,7 @@ call; MCTS policy/value callables (mcts.py:107-118).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -37,9 +38,12 @@ class HipTrunkInference:
     """Forward-only runner of a ConvStack (+ head) on the HIP kernels."""
 
     def __init__(self, net, device, buckets: Sequence[int] = DEFAULT_BUCKETS, use_graphs: bool = True,
-                 feature_list: Optional[Sequence[str]] = None):
+                 feature_list: Optional[Sequence[str]] = None, precision: Optional[str] = None):
         ops.load()
         self.net = net
+        self.precision = precision or os.environ.get("ALPHAGO_AMD_PRECISION", "bf16")
+        if self.precision not in ("bf16", "fp8"):
+            raise ValueError("precision must be bf16 or fp8")
         self.device = torch.device(device)
         tr = net.trunk
         self.S, self.L, self.K = net.board, tr.layers, list(tr.widths)
@@ -55,6 +59,15 @@ class HipTrunkInference:
         self.head_w = torch.zeros(self.F, device=dev)
         self.head_b = torch.zeros(1, device=dev)
         self._b: Dict[int, _Bucket] = {}
+        if self.precision == "fp8":
+            L = self.L
+            self.w8: List[torch.Tensor] = [None] * L
+            self.ew = [0] * L
+            self.ex = [0] * (L + 1)  # e4m3 exponent of each layer's input (layer 0: binary planes, exact at 0)
+            self.scales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
+            self.osc8 = torch.ones(L, device=dev)
+            self.amax8 = torch.zeros(L, dtype=torch.int32, device=dev)
+            self.calibrated = False
         self.fz = None
         if feature_list is not None:
             from ..ops.gpu_features import GpuFeaturizer
@@ -81,6 +94,11 @@ class HipTrunkInference:
             self.bias_p[l][:self.F].copy_(tr.biases[l].detach())
         self.head_w.copy_(self.net.head_w.detach().view(-1))
         self.head_b.copy_(self.net.head_b.detach().view(-1))
+        if self.precision == "fp8":
+            for l in range(self.L):
+                self.w8[l], self.ew[l] = ops.pack_weights_fp8(ws[l], self.Fp, self.C0p if l == 0 else self.Fp)
+                self.scales8[l, 1] = 127 - self.ew[l]
+            self.calibrated = False  # activation ranges change with the weights
         self._after_sync()
 
     def _after_sync(self):
@@ -100,6 +118,9 @@ class HipTrunkInference:
         bk.legal = torch.ones((B, S * S), dtype=torch.uint8, device=dev)
         bk.X0 = ops.padded_empty(B, S, self.P0, self.C0p, dev)
         bk.Y = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(2)]
+        if self.precision == "fp8":
+            bk.X08 = torch.zeros(bk.X0.shape, dtype=torch.uint8, device=dev)
+            bk.Y8 = [torch.zeros(bk.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(2)]
         self._alloc_outputs(bk)
         bk.graph = None
         bk.graph_enc = None
@@ -122,12 +143,54 @@ class HipTrunkInference:
                         overflow=bk.ovf)
         else:
             ops.pack_input(bk.planes, bk.X0, self.P0)
+        if self.precision == "fp8" and not getattr(self, "_calibrating", False):
+            return self._trunk_fp8(bk)
         x, pin = bk.X0, self.P0
         for l in range(self.L):
             y = bk.Y[l % 2]
             ops.conv_fwd(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1)
+            if getattr(self, "_calibrating", False):
+                self._cal_amax[l] = max(self._cal_amax[l], float(y.amax()))
             x, pin = y, 1
         return x
+
+    # ------------------------------------------------------------------ fp8
+    def _trunk_fp8(self, bk) -> torch.Tensor:
+        """e4m3 trunk on the block-scaled MFMA: every layer reads and (but the
+        last) writes e4m3 activations; the last writes bf16 for the head."""
+        ops.quantize_fp8(bk.X0, bk.X08, 0)  # 0/1 planes are exact in e4m3
+        x8, pin = bk.X08, self.P0
+        for l in range(self.L):
+            last = l == self.L - 1
+            ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l], self.S,
+                             pin, 1, y_bf16=bk.Y[0] if last else None, y_fp8=None if last else bk.Y8[l % 2],
+                             amax=self.amax8[l:l + 1])
+            x8, pin = bk.Y8[l % 2], 1
+        return bk.Y[0]
+
+    @torch.no_grad()
+    def calibrate(self, bk, encoded: bool = False, margin: int = 1) -> None:
+        """Set per-layer e4m3 activation scales from a bf16 forward of the
+        current bucket inputs (delayed scaling afterwards: recalibrate())."""
+        self._cal_amax = [0.0] * self.L
+        self._calibrating = True
+        try:
+            self._trunk(bk, encoded)
+        finally:
+            self._calibrating = False
+        self._set_act_exponents([ops.fp8_exponent(a, margin) for a in self._cal_amax])
+        self.calibrated = True
+
+    def recalibrate(self, margin: int = 1) -> None:
+        """Re-derive activation scales from the running amax tracked by the fp8 kernels."""
+        amax = self.amax8.view(torch.float32).tolist()
+        self._set_act_exponents([ops.fp8_exponent(a, margin) for a in amax])
+
+    def _set_act_exponents(self, out_exp) -> None:
+        self.ex = [0] + list(out_exp)
+        for l in range(self.L):
+            self.scales8[l, 0] = 127 - self.ex[l]
+            self.osc8[l] = 2.0 ** self.ex[l + 1]
 
     def _head(self, bk, y):
         ops.policy_head_probs(y, self.head_w, self.head_b, bk.probs, self.S, legal=bk.legal)
@@ -178,6 +241,8 @@ class HipTrunkInference:
         if n < bk.B:
             bk.e_board[n:].zero_()
             bk.e_ages[n:].fill_(255)
+        if self.precision == "fp8" and not self.calibrated:
+            self.calibrate(bk, encoded=True)
         if bk.graph_enc is not None:
             bk.graph_enc.replay()
         else:
@@ -201,6 +266,8 @@ class HipTrunkInference:
                 bk.legal[n:].fill_(1)
         else:
             bk.legal.fill_(1)
+        if self.precision == "fp8" and not self.calibrated:
+            self.calibrate(bk)
         if bk.graph is not None:
             bk.graph.replay()
         else:

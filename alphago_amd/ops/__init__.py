@@ -152,3 +152,48 @@ def value_out(h, w2, b2, v, target=None, weight=None, loss=None, correct=None, d
     """v = tanh(h w2 + b2); with target: MSE loss, sign agreement, dh and per-board [dw2 | db2]."""
     _ops().value_out(h, w2, b2, target, weight, v, loss, correct, dh, dout, grad_scale)
     return v
+
+
+# ----------------------------------------------------------------- fp8 (e4m3)
+FP8_MAX = 448.0
+
+
+def fp8_exponent(amax: float, margin: int = 1) -> int:
+    """Power-of-two scale exponent e so that amax * 2^e fits e4m3 with `margin` bits of headroom."""
+    import math
+
+    if not amax or amax <= 0 or not math.isfinite(amax):
+        return 0
+    return int(math.floor(math.log2(FP8_MAX / amax))) - margin
+
+
+def fp8_nchunks(K: int, cin_p: int) -> int:
+    n = K * K * (cin_p // 64)
+    return n + (n & 1)
+
+
+def pack_weights_fp8(w_oihw: torch.Tensor, cout_p: int, cin_p: int, exponent=None):
+    """fp32 OIHW -> (uint8 e4m3 (nch, cout_p, 64) scaled by 2^e, e)."""
+    w = w_oihw.detach().float().contiguous()
+    if exponent is None:
+        exponent = fp8_exponent(float(w.abs().max()), margin=0)
+    out = torch.empty((fp8_nchunks(w.shape[2], cin_p), cout_p, 64), dtype=torch.uint8, device=w.device)
+    _ops().pack_weights_fp8(w, out, float(2.0 ** exponent))
+    return out, exponent
+
+
+def quantize_fp8(x_bf16: torch.Tensor, out: torch.Tensor, exponent: int):
+    _ops().quantize_fp8(x_bf16, out, float(2.0 ** exponent))
+    return out
+
+
+def conv_fwd_fp8(x8, w8, bias, scales, out_scale, K: int, S: int, Pin: int, Po: int = 1, y_bf16=None, y_fp8=None,
+                 amax=None):
+    """fp8 conv + bias + ReLU.  scales: int32 device tensor {127 - e_x, 127 - e_w} (MFMA E8M0);
+    out_scale: f32 device tensor [2^e_y] for the e4m3 output; amax: int32[1] running max (float bits)."""
+    _ops().conv_fwd_fp8(x8, w8, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po)
+
+
+def fp8_to_float(t_u8: torch.Tensor, exponent: int = 0) -> torch.Tensor:
+    """Decode e4m3 bytes (and undo a 2^exponent scale)."""
+    return t_u8.view(torch.float8_e4m3fn).float() * (2.0 ** -exponent)

@@ -58,5 +58,13 @@ for ns in splits:
             res[k] = min(res.get(k, 1e30), timeit(lambda: ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1)))
     torch.ops.alphago_amd.set_wgrad_variant(0)
     res["reduce_s%d" % ns] = timeit(lambda: ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0))
+# fp8 forward (block-scaled MFMA), 3x3 and 5x5
+x8 = torch.zeros(x.shape, dtype=torch.uint8, device=dev); ops.quantize_fp8(x, x8, 0)
+x08 = torch.zeros(x0.shape, dtype=torch.uint8, device=dev); ops.quantize_fp8(x0, x08, 0)
+w8, _ = ops.pack_weights_fp8(w, F, F); w18, _ = ops.pack_weights_fp8(w1, F, 64)
+sc = torch.tensor([127, 127], dtype=torch.int32, device=dev); osc = torch.ones(1, device=dev)
+y8 = torch.zeros(y.shape, dtype=torch.uint8, device=dev)
+res["fp8_fwd3x3"] = timeit(lambda: ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8))
+res["fp8_fwd5x5"] = timeit(lambda: ops.conv_fwd_fp8(x08, w18, bias, sc, osc, 5, S, 2, 1, y_fp8=y8))
 out = {k: {"us": round(v, 1), "TF": round((fl1 if "5x5" in k else fl3) / (v * 1e-6) / 1e12, 1) if "reduce" not in k else None} for k, v in res.items()}
 print(json.dumps({"batch": B, "F": F, **out}))

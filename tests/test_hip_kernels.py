@@ -238,3 +238,35 @@ def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
     assert _rel_err(ops.from_padded(y, 1), ref) < 1e-2
     ref_dx = torch.nn.grad.conv2d_input(x.shape[:1] + (192, S, S), w3, g, padding=1) * (mask > 0)
     assert _rel_err(ops.from_padded(dx, 1), ref_dx) < 1e-2
+
+
+@pytest.mark.parametrize("K,Cin,Cout,B", [(3, 192, 192, 5), (5, 64, 192, 3), (3, 128, 128, 4), (3, 192, 64, 2)])
+def test_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B):
+    """e4m3 conv on the block-scaled MFMA vs fp32 conv of the dequantised operands."""
+    torch.manual_seed(3)
+    S, P = 19, K // 2
+    x = F.relu(torch.randn(B, Cin, S, S, device=cuda_device)) * 3.0
+    w = torch.randn(Cout, Cin, K, K, device=cuda_device) * 0.05
+    b = torch.randn(Cout, device=cuda_device) * 0.1
+    xp = ops.to_padded(x, P)
+    ex = ops.fp8_exponent(float(x.abs().max()), margin=0)
+    x8 = torch.empty(xp.shape, dtype=torch.uint8, device=cuda_device)
+    ops.quantize_fp8(xp, x8, ex)
+    w8, ew = ops.pack_weights_fp8(w, Cout, Cin)
+    # dequantised operands (what the MFMA multiplies)
+    xq = ops.fp8_to_float(x8, ex)[:, P:P + S, P:P + S, :Cin].permute(0, 3, 1, 2)
+    wq = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 0)).mul(2.0 ** ew).clamp(-448, 448)
+    wq = wq.to(torch.float8_e4m3fn).float() * 2.0 ** -ew
+    ref = F.relu(F.conv2d(xq, wq, b, padding=P))
+    scales = torch.tensor([127 - ex, 127 - ew], dtype=torch.int32, device=cuda_device)
+    ey = ops.fp8_exponent(float(ref.max()), margin=0)
+    osc = torch.tensor([2.0 ** ey], device=cuda_device)
+    amax = torch.zeros(1, dtype=torch.int32, device=cuda_device)
+    yb = ops.padded_empty(B, S, 1, Cout, cuda_device)
+    y8 = torch.zeros((B, S + 2, S + 2, Cout), dtype=torch.uint8, device=cuda_device)
+    ops.conv_fwd_fp8(x8, w8, b, scales, osc, K, S, P, 1, y_bf16=yb, y_fp8=y8, amax=amax)
+    torch.cuda.synchronize()
+    assert _rel_err(ops.from_padded(yb, 1), ref) < 1e-2
+    assert _rel_err(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1].permute(0, 3, 1, 2), ref) < 0.07
+    assert abs(amax.view(torch.float32).item() - ref.max().item()) <= 1e-2 * ref.max().item()
+    assert y8[:, 0].sum() == 0 and yb[:, :, -1].abs().sum() == 0
