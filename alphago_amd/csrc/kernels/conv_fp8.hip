@@ -184,8 +184,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_kernel(ConvFp8Args a) {
     }
   }
   if (a.amax) {
+    // workgroup max, then one atomic per workgroup into one of kFp8AmaxSlots
+    // slots (a single address would serialise ~10k atomics per layer)
     vmax = wave_max(vmax);
-    if (lane == 0) atomicMax(a.amax, __float_as_uint(vmax));
+    __syncthreads();  // LDS stages are dead; reuse the first bytes
+    float* red = reinterpret_cast<float*>(smem);
+    if (lane == 0) red[wave] = vmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = red[0];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w]);
+      atomicMax(a.amax + (blockIdx.x & (kFp8AmaxSlots - 1)), __float_as_uint(m));
+    }
   }
 }
 
@@ -222,8 +233,9 @@ void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
 // ------------------------------------------------------------- packing
 // weights: fp32 OIHW [Cout_real][Cin_real][K][K] -> e4m3 [nch][Cout_p][64] * 2^e
 __global__ void pack_weights_fp8_kernel(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p,
-                                        int Cin_p, int nch, float scale) {
+                                        int Cin_p, int nch, float scale, const float* scale_dev) {
   const int CC = Cin_p >> 6;
+  if (scale_dev) scale = *scale_dev;
   const long total = (long)nch * Cout_p * 64;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     const int byte = (int)(idx & 63);
@@ -243,12 +255,60 @@ __global__ void pack_weights_fp8_kernel(const float* w, uint8_t* out, int Cout_r
 }
 
 void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p, int Cin_p,
-                             int nch, float scale, hipStream_t st) {
+                             int nch, float scale, const float* scale_dev, hipStream_t st) {
   const long total = (long)nch * Cout_p * 64;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(pack_weights_fp8_kernel, dim3(blocks), dim3(256), 0, st, w, out, Cout_real, Cin_real, K, Cout_p,
-                     Cin_p, nch, scale);
+                     Cin_p, nch, scale, scale_dev);
+}
+
+// Per-layer weight scales, one workgroup per layer: e = floor(log2(448 / amax|w|)),
+// wscale[l] = 2^e (for packing) and the MFMA E8M0 exponent scales8[l][1] = 127 - e.
+__global__ __launch_bounds__(1024) void fp8_weight_scales_kernel(Fp8WeightScalesArgs a) {
+  __shared__ float red[16];
+  const int l = blockIdx.x;
+  const float* w = a.w[l];
+  const int n = a.n[l];
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, fabsf(w[i]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 16; ++i) m = fmaxf(m, red[i]);
+    m = fmaxf(m, red[0]);
+    int e = (m > 0.f) ? (int)floorf(log2f(448.f / m)) : 0;
+    e = e < -60 ? -60 : (e > 60 ? 60 : e);
+    a.wscale[l] = exp2f((float)e);
+    a.scales8[2 * l + 1] = 127 - e;
+  }
+}
+
+void launch_fp8_weight_scales(const Fp8WeightScalesArgs& a, int L, hipStream_t st) {
+  hipLaunchKernelGGL(fp8_weight_scales_kernel, dim3(L), dim3(1024), 0, st, a);
+}
+
+// Delayed activation scaling: from this step's per-layer output amax set the
+// next step's e4m3 exponents (input of layer l+1 = output of layer l) with
+// `margin` bits of headroom, then clear the amax accumulators.
+__global__ void fp8_act_scales_kernel(unsigned* amax, int* scales8, float* osc, int L, int margin) {
+  const int l = threadIdx.x;
+  if (l >= L) return;
+  unsigned mu = 0u;
+  for (int k = 0; k < kFp8AmaxSlots; ++k) mu = max(mu, amax[l * kFp8AmaxSlots + k]);
+  const float m = __uint_as_float(mu);
+  int e = (m > 0.f) ? (int)floorf(log2f(448.f / m)) - margin : 0;
+  e = e < -60 ? -60 : (e > 60 ? 60 : e);
+  if (l + 1 < L) {
+    osc[l] = exp2f((float)e);
+    scales8[2 * (l + 1)] = 127 - e;
+  }
+  for (int k = 0; k < kFp8AmaxSlots; ++k) amax[l * kFp8AmaxSlots + k] = 0u;
+}
+
+void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st) {
+  hipLaunchKernelGGL(fp8_act_scales_kernel, dim3(1), dim3(64), 0, st, amax, scales8, osc, L, margin);
 }
 
 // e4m3 quantisation of a padded NHWC bf16 tensor (interior and borders alike: borders stay 0)

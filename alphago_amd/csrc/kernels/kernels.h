@@ -113,6 +113,8 @@ struct FeaturizeArgs {
   uint8_t chan_plane[kFzMaxChannels];
 };
 
+constexpr int kFp8AmaxSlots = 64;  // per-layer amax accumulators (spread atomics)
+
 struct ConvFp8Args {
   const uint8_t* x;         // padded NHWC e4m3 [B][HPi][HPi][Cin], Cin % 64 == 0
   const uint8_t* w;         // e4m3 [nch][Cout][64], chunk q = tap * (Cin/64) + c, nch even (zero tail)
@@ -121,7 +123,7 @@ struct ConvFp8Args {
   const float* out_scale;   // [1] multiplier applied before the e4m3 output conversion
   __bf16* y_bf16;           // optional padded NHWC bf16 output
   uint8_t* y_fp8;           // optional padded NHWC e4m3 output
-  unsigned* amax;           // optional running max of the ReLU output (float bits)
+  unsigned* amax;           // optional running max of the ReLU output (float bits), kFp8AmaxSlots slots
   int M, S, Cin, Cout, K;
   int HPi, offi, HPo, Po;
   int nch;
@@ -143,7 +145,15 @@ void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st);
 void launch_featurize(const FeaturizeArgs& a, hipStream_t st);
 void launch_conv_fwd_fp8(const ConvFp8Args& a, hipStream_t st);
 void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p, int Cin_p,
-                             int nch, float scale, hipStream_t st);
+                             int nch, float scale, const float* scale_dev, hipStream_t st);
+struct Fp8WeightScalesArgs {
+  const float* w[kMaxPackLayers];
+  int n[kMaxPackLayers];
+  float* wscale;  // [L]
+  int* scales8;   // [L][2]
+};
+void launch_fp8_weight_scales(const Fp8WeightScalesArgs& a, int L, hipStream_t st);
+void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st);
 void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st);
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
 

@@ -340,7 +340,8 @@ void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Te
     a.y_fp8 = y_fp8->data_ptr<uint8_t>();
   }
   if (amax.has_value()) {
-    TORCH_CHECK(amax->scalar_type() == at::kInt && amax->numel() >= 1, "amax int32[1] (float bits)");
+    TORCH_CHECK(amax->scalar_type() == at::kInt && amax->numel() >= agk::kFp8AmaxSlots,
+                "amax int32[64] (float bits, per-workgroup slots)");
     a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
   }
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
@@ -350,15 +351,46 @@ void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Te
   agk::launch_conv_fwd_fp8(a, cur_stream());
 }
 
-void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale) {
+void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c10::optional<Tensor>& scale_dev) {
   CHECK_F32(w); CHECK_CONTIG(w);
   TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.dim() == 3 && out.size(2) == 64, "out");
   const int K = (int)w.size(2);
   const int nch = (int)out.size(0), Cout_p = (int)out.size(1);
   const int Cin_p = ((int)w.size(1) + 63) / 64 * 64;
   TORCH_CHECK(nch % 2 == 0 && nch >= K * K * (Cin_p / 64) && Cout_p >= w.size(0), "packed geometry");
+  const float* sd = nullptr;
+  if (scale_dev.has_value()) {
+    CHECK_F32(*scale_dev);
+    sd = scale_dev->data_ptr<float>();
+  }
   agk::launch_pack_weights_fp8(w.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)w.size(0), (int)w.size(1), K, Cout_p,
-                               Cin_p, nch, (float)scale, cur_stream());
+                               Cin_p, nch, (float)scale, sd, cur_stream());
+}
+
+// per-layer weight scales (device-side, no host sync)
+void fp8_weight_scales(at::TensorList ws, const Tensor& wscale, const Tensor& scales8) {
+  TORCH_CHECK((int)ws.size() <= agk::kMaxPackLayers, "too many layers");
+  TORCH_CHECK(wscale.scalar_type() == at::kFloat && scales8.scalar_type() == at::kInt, "dtypes");
+  TORCH_CHECK(wscale.numel() >= (int64_t)ws.size() && scales8.numel() >= 2 * (int64_t)ws.size(), "sizes");
+  agk::Fp8WeightScalesArgs a{};
+  for (size_t i = 0; i < ws.size(); ++i) {
+    CHECK_F32(ws[i]); CHECK_CONTIG(ws[i]);
+    a.w[i] = ws[i].data_ptr<float>();
+    a.n[i] = (int)ws[i].numel();
+  }
+  a.wscale = wscale.data_ptr<float>();
+  a.scales8 = scales8.data_ptr<int>();
+  if (ws.empty()) return;
+  agk::launch_fp8_weight_scales(a, (int)ws.size(), cur_stream());
+}
+
+void fp8_act_scales(const Tensor& amax, const Tensor& scales8, const Tensor& osc, int64_t margin) {
+  TORCH_CHECK(amax.scalar_type() == at::kInt && scales8.scalar_type() == at::kInt && osc.scalar_type() == at::kFloat, "dtypes");
+  const int L = (int)(amax.numel() / agk::kFp8AmaxSlots);
+  TORCH_CHECK(amax.numel() % agk::kFp8AmaxSlots == 0 && L <= 64 && scales8.numel() >= 2 * L && osc.numel() >= L,
+              "sizes (amax is (L, 64))");
+  agk::launch_fp8_act_scales(reinterpret_cast<unsigned*>(amax.data_ptr<int>()), scales8.data_ptr<int>(),
+                             osc.data_ptr<float>(), L, (int)margin, cur_stream());
 }
 
 void quantize_fp8(const Tensor& x, const Tensor& y, double scale) {
@@ -399,7 +431,9 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
       "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po) -> ()");
-  m.def("pack_weights_fp8(Tensor w, Tensor(a!) out, float scale) -> ()");
+  m.def("pack_weights_fp8(Tensor w, Tensor(a!) out, float scale, Tensor? scale_dev) -> ()");
+  m.def("fp8_weight_scales(Tensor[] ws, Tensor(a!) wscale, Tensor(b!) scales8) -> ()");
+  m.def("fp8_act_scales(Tensor(a!) amax, Tensor(b!) scales8, Tensor(c!) osc, int margin) -> ()");
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
   m.def("set_wgrad_variant(int v) -> ()", &set_wgrad_variant);
@@ -419,5 +453,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("featurize", &featurize);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8);
   m.impl("pack_weights_fp8", &pack_weights_fp8);
+  m.impl("fp8_weight_scales", &fp8_weight_scales);
+  m.impl("fp8_act_scales", &fp8_act_scales);
   m.impl("quantize_fp8", &quantize_fp8);
 }

@@ -66,7 +66,7 @@ class HipTrunkInference:
             self.ex = [0] * (L + 1)  # e4m3 exponent of each layer's input (layer 0: binary planes, exact at 0)
             self.scales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
             self.osc8 = torch.ones(L, device=dev)
-            self.amax8 = torch.zeros(L, dtype=torch.int32, device=dev)
+            self.amax8 = ops.fp8_amax_buffer(L, dev)
             self.calibrated = False
         self.fz = None
         if feature_list is not None:
@@ -164,7 +164,7 @@ class HipTrunkInference:
             last = l == self.L - 1
             ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l], self.S,
                              pin, 1, y_bf16=bk.Y[0] if last else None, y_fp8=None if last else bk.Y8[l % 2],
-                             amax=self.amax8[l:l + 1])
+                             amax=self.amax8[l])
             x8, pin = bk.Y8[l % 2], 1
         return bk.Y[0]
 
@@ -183,7 +183,7 @@ class HipTrunkInference:
 
     def recalibrate(self, margin: int = 1) -> None:
         """Re-derive activation scales from the running amax tracked by the fp8 kernels."""
-        amax = self.amax8.view(torch.float32).tolist()
+        amax = self.amax8.view(torch.float32).amax(1).tolist()
         self._set_act_exponents([ops.fp8_exponent(a, margin) for a in amax])
 
     def _set_act_exponents(self, out_exp) -> None:

@@ -156,6 +156,12 @@ def value_out(h, w2, b2, v, target=None, weight=None, loss=None, correct=None, d
 
 # ----------------------------------------------------------------- fp8 (e4m3)
 FP8_MAX = 448.0
+FP8_AMAX_SLOTS = 64  # per-layer amax accumulator slots (kFp8AmaxSlots)
+
+
+def fp8_amax_buffer(L: int, device) -> torch.Tensor:
+    """(L, 64) int32 per-layer amax accumulators (float bits); amax of layer l = view(float32)[l].max()."""
+    return torch.zeros((L, FP8_AMAX_SLOTS), dtype=torch.int32, device=device)
 
 
 def fp8_exponent(amax: float, margin: int = 1) -> int:
@@ -178,8 +184,23 @@ def pack_weights_fp8(w_oihw: torch.Tensor, cout_p: int, cin_p: int, exponent=Non
     if exponent is None:
         exponent = fp8_exponent(float(w.abs().max()), margin=0)
     out = torch.empty((fp8_nchunks(w.shape[2], cin_p), cout_p, 64), dtype=torch.uint8, device=w.device)
-    _ops().pack_weights_fp8(w, out, float(2.0 ** exponent))
+    _ops().pack_weights_fp8(w, out, float(2.0 ** exponent), None)
     return out, exponent
+
+
+def pack_weights_fp8_into(w_oihw: torch.Tensor, out: torch.Tensor, scale_dev: torch.Tensor):
+    """Re-pack into an existing buffer with a device-resident scale (no host sync)."""
+    _ops().pack_weights_fp8(w_oihw, out, 1.0, scale_dev)
+
+
+def fp8_weight_scales(ws, wscale, scales8):
+    """Per-layer e4m3 weight exponents on the device: wscale[l] = 2^e_l, scales8[l, 1] = 127 - e_l."""
+    _ops().fp8_weight_scales(list(ws), wscale, scales8)
+
+
+def fp8_act_scales(amax, scales8, osc, margin: int = 1):
+    """Delayed activation scaling from the per-layer output amax (also clears amax)."""
+    _ops().fp8_act_scales(amax, scales8, osc, margin)
 
 
 def quantize_fp8(x_bf16: torch.Tensor, out: torch.Tensor, exponent: int):
@@ -190,7 +211,7 @@ def quantize_fp8(x_bf16: torch.Tensor, out: torch.Tensor, exponent: int):
 def conv_fwd_fp8(x8, w8, bias, scales, out_scale, K: int, S: int, Pin: int, Po: int = 1, y_bf16=None, y_fp8=None,
                  amax=None):
     """fp8 conv + bias + ReLU.  scales: int32 device tensor {127 - e_x, 127 - e_w} (MFMA E8M0);
-    out_scale: f32 device tensor [2^e_y] for the e4m3 output; amax: int32[1] running max (float bits)."""
+    out_scale: f32 device tensor [2^e_y] for the e4m3 output; amax: int32[64] running max slots (float bits)."""
     _ops().conv_fwd_fp8(x8, w8, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po)
 
 

@@ -117,8 +117,11 @@ class HipConvTrainer:
     """MFMA conv-trunk training engine; subclasses provide the head."""
 
     def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
-                 overlap: bool = True, wgrad_target_wgs: int = 512, iterations: int = 0):
+                 overlap: bool = True, wgrad_target_wgs: int = 512, iterations: int = 0, precision: str = "bf16"):
         ops.load()
+        if precision not in ("bf16", "fp8"):
+            raise ValueError("precision must be bf16 or fp8")
+        self.precision = precision
         self.env = agdist.env()
         self.device = torch.device(device) if device is not None else self.env.device
         if self.device.type != "cuda":
@@ -193,6 +196,21 @@ class HipConvTrainer:
             last = ids[-1]
             self._bucket_after_layer[self._seg_layer[last] if self._seg_layer[last] is not None else -1] = bi
         self.reducer = agdist.BucketAllReducer(self.fp.grad, self.buckets)
+        if precision == "fp8":
+            # fp8 forward (block-scaled MFMA) with bf16 activations kept for the
+            # backward; per-tensor power-of-two scales, all device-side:
+            # weights from their amax at every repack, activations delayed by
+            # one step from the amax the fp8 kernels accumulate.
+            L = self.L
+            self.w8 = [torch.zeros((ops.fp8_nchunks(self.K[l], self.C0p if l == 0 else self.Fp), self.Fp, 64),
+                                   dtype=torch.uint8, device=dev) for l in range(L)]
+            self.wscale8 = torch.ones(L, device=dev)
+            self.scales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
+            self.osc8 = torch.ones(L, device=dev)
+            self.amax8 = ops.fp8_amax_buffer(L, dev)
+            self.X08 = torch.zeros(self.X0.shape, dtype=torch.uint8, device=dev)
+            self.Y8 = [torch.zeros(self.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self._fp8_calibrated = False
         self._init_head()
         self.repack()
 
@@ -210,16 +228,50 @@ class HipConvTrainer:
     def repack(self) -> None:
         for l in range(self.L):
             self.bias_p[l][:self.F].copy_(self.fp.views["b%d" % l])
-        ops.pack_weights([self.fp.views["w%d" % l] for l in range(self.L)], self.wf, self.wd)
+        ws = [self.fp.views["w%d" % l] for l in range(self.L)]
+        ops.pack_weights(ws, self.wf, self.wd)
+        if self.precision == "fp8":
+            ops.fp8_weight_scales(ws, self.wscale8, self.scales8)
+            for l in range(self.L):
+                ops.pack_weights_fp8_into(ws[l], self.w8[l], self.wscale8[l:l + 1])
 
     def _layer_in(self, l):
         return (self.X0, self.P0) if l == 0 else (self.Y[l - 1], 1)
 
     def forward_trunk(self, planes: torch.Tensor, sym=None, move_targets=None, target_out=None) -> None:
         ops.pack_input(planes, self.X0, self.P0, sym=sym, target=move_targets, target_out=target_out)
+        if self.precision == "fp8":
+            if not self._fp8_calibrated:
+                self._fp8_calibrate()
+            self._forward_fp8()
+            return
         for l in range(self.L):
             x, pin = self._layer_in(l)
             ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1)
+
+    def _forward_fp8(self) -> None:
+        ops.quantize_fp8(self.X0, self.X08, 0)  # binary planes: exact
+        x8, pin = self.X08, self.P0
+        for l in range(self.L):
+            last = l == self.L - 1
+            ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l], self.S,
+                             pin, 1, y_bf16=self.Y[l], y_fp8=None if last else self.Y8[l % 2],
+                             amax=self.amax8[l])
+            x8, pin = self.Y8[l % 2], 1
+        ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)  # next step's activation scales
+
+    @torch.no_grad()
+    def _fp8_calibrate(self) -> None:
+        """First step: activation scales from a bf16 forward of this batch."""
+        amax = []
+        for l in range(self.L):
+            x, pin = self._layer_in(l)
+            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1)
+            amax.append(self.Y[l].amax().float())
+        self.amax8.zero_()
+        self.amax8[:, 0].copy_(torch.stack(amax).view(torch.int32))
+        ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)
+        self._fp8_calibrated = True
 
     def _wgrad_layer(self, l: int) -> None:
         x, pin = self._layer_in(l)

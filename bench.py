@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--pool", type=int, default=16384, help="synthetic positions resident on device")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
+                    help="conv forward precision (fp8 = e4m3 block-scaled MFMA forward, bf16 backward)")
     ap.add_argument("--profile", default=None,
                     help="after the timed run, profile 6 more steps (torch.profiler + roctx ranges) into DIR")
     args = ap.parse_args()
@@ -52,7 +54,7 @@ def main():
     dev = env.device
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
-    kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap}
+    kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap, "precision": args.precision}
     trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
 
     # synthetic dataset, resident in HBM (uint8 one-hot planes + move targets)
@@ -104,7 +106,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / PAPER_SL_POS_PER_S, 2),
-            "dtype": "bf16" if args.backend == "hip" else "fp32",
+            "dtype": (args.precision if args.precision == "bf16" else "fp8-fwd/bf16-bwd") if args.backend == "hip"
+            else "fp32",
             "data": "synthetic (random uint8 planes/targets, random-init weights)",
             "top1_acc": round(float(stats[1]) / positions, 4),
             "mean_loss": round(float(stats[0]) / positions, 4),

@@ -1,0 +1,81 @@
+"""Value-network training throughput (BASELINE config 5: "Value-net training
+from self-play positions, DP=8, fp8 MFMA conv path").
+
+Paper/reference value net (AlphaGo/models/value.py:12-31): 49 planes, 5x5 +
+11x 3x3 convs of 152 filters (padded to 192 channels by the kernels), 1x1
+conv, Dense(256), Dense(1, tanh); MSE against +-1 outcomes.  Synthetic
+positions/outcomes, random init.  Runs under torchrun for DP (RCCL all-reduce).
+
+    python benchmarks/value_training_benchmark.py --precision fp8 --steps 20
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/value_training_benchmark.py
+Prints one JSON line (rank 0): positions/s for the whole job, ms/step, MSE.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from alphago_amd.models.nets import ValueNet  # noqa: E402
+from alphago_amd.parallel import dist as agdist  # noqa: E402
+from alphago_amd.train.engine import make_value_trainer  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024, help="per-GPU minibatch")
+    ap.add_argument("--filters", type=int, default=152)
+    ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--precision", default="fp8", choices=["bf16", "fp8"])
+    ap.add_argument("--pool", type=int, default=8192)
+    a = ap.parse_args()
+    env = agdist.init_from_env()
+    dev = env.device
+    torch.manual_seed(7 + env.rank)
+    net = ValueNet(49, filters_per_layer=a.filters, layers=a.layers)
+    kw = {"precision": a.precision} if dev.type == "cuda" else {}
+    tr = make_value_trainer(net, a.batch, lr=0.003, decay=8.664e-8, device=dev, **kw)
+    g = torch.Generator(device=dev).manual_seed(11 + env.rank)
+    pool = torch.randint(0, 2, (a.pool, 49, 19, 19), dtype=torch.uint8, device=dev, generator=g)
+    pz = (torch.randint(0, 2, (a.pool,), device=dev, generator=g) * 2 - 1).float()
+
+    def batch():
+        idx = torch.randint(0, a.pool, (a.batch,), device=dev, generator=g)
+        sym = torch.randint(0, 8, (a.batch,), device=dev, dtype=torch.int32, generator=g)
+        return pool.index_select(0, idx), pz.index_select(0, idx), sym
+
+    for _ in range(a.warmup):
+        tr.step(*batch())
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    agdist.barrier()
+    t0 = time.perf_counter()
+    ls = torch.zeros((), device=dev, dtype=torch.float64)
+    for _ in range(a.steps):
+        l, _ = tr.step(*batch())
+        ls += l.double()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    agdist.barrier()
+    dt = agdist.all_reduce_max(time.perf_counter() - t0)
+    agdist.all_reduce_sum_(ls)
+    n = env.world_size
+    pos = a.batch * n * a.steps
+    if env.is_main:
+        print(json.dumps({"metric": "value-net training positions/s (whole job)", "value": round(pos / dt, 1),
+                          "unit": "positions/s", "n_gpus": n, "ms_per_step": round(dt / a.steps * 1e3, 3),
+                          "precision": a.precision if dev.type == "cuda" else "fp32", "mse": round(float(ls) / pos, 4),
+                          "config": {"model": "value net %d-layer %d filters 49 planes" % (a.layers, a.filters),
+                                     "global_batch": a.batch * n, "parallelism": "dp%d" % n},
+                          "data": "synthetic positions/outcomes, random-init weights"}), flush=True)
+    agdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -65,6 +65,9 @@ w8, _ = ops.pack_weights_fp8(w, F, F); w18, _ = ops.pack_weights_fp8(w1, F, 64)
 sc = torch.tensor([127, 127], dtype=torch.int32, device=dev); osc = torch.ones(1, device=dev)
 y8 = torch.zeros(y.shape, dtype=torch.uint8, device=dev)
 res["fp8_fwd3x3"] = timeit(lambda: ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8))
+am = ops.fp8_amax_buffer(1, dev)[0]
+res["fp8_fwd3x3_amax"] = timeit(lambda: ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8, amax=am))
+res["fp8_fwd3x3_dual"] = timeit(lambda: ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8, y_bf16=y, amax=am))
 res["fp8_fwd5x5"] = timeit(lambda: ops.conv_fwd_fp8(x08, w18, bias, sc, osc, 5, S, 2, 1, y_fp8=y8))
 out = {k: {"us": round(v, 1), "TF": round((fl1 if "5x5" in k else fl3) / (v * 1e-6) / 1e12, 1) if "reduce" not in k else None} for k, v in res.items()}
 print(json.dumps({"batch": B, "F": F, **out}))

@@ -261,12 +261,12 @@ def test_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B):
     scales = torch.tensor([127 - ex, 127 - ew], dtype=torch.int32, device=cuda_device)
     ey = ops.fp8_exponent(float(ref.max()), margin=0)
     osc = torch.tensor([2.0 ** ey], device=cuda_device)
-    amax = torch.zeros(1, dtype=torch.int32, device=cuda_device)
+    amax = ops.fp8_amax_buffer(1, cuda_device)[0]
     yb = ops.padded_empty(B, S, 1, Cout, cuda_device)
     y8 = torch.zeros((B, S + 2, S + 2, Cout), dtype=torch.uint8, device=cuda_device)
     ops.conv_fwd_fp8(x8, w8, b, scales, osc, K, S, P, 1, y_bf16=yb, y_fp8=y8, amax=amax)
     torch.cuda.synchronize()
     assert _rel_err(ops.from_padded(yb, 1), ref) < 1e-2
     assert _rel_err(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1].permute(0, 3, 1, 2), ref) < 0.07
-    assert abs(amax.view(torch.float32).item() - ref.max().item()) <= 1e-2 * ref.max().item()
+    assert abs(amax.view(torch.float32).max().item() - ref.max().item()) <= 1e-2 * ref.max().item()
     assert y8[:, 0].sum() == 0 and yb[:, :, -1].abs().sum() == 0
