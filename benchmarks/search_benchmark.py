@@ -21,6 +21,7 @@ from alphago_amd.search.selfplay import BatchedSampler, play_games  # noqa: E402
 
 
 def main():
+    # ALPHAGO_AMD_PRECISION=fp8 runs the policy/value engines on the e4m3 MFMA path
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     small = dev.type == "cpu"
     F, L = (16, 2) if small else (192, 12)
@@ -41,7 +42,7 @@ def main():
     s.search(states, playouts, lpt)
     dt = time.perf_counter() - t
     evals = s.forest.total_evals - e0
-    res = {"device": str(dev), "trees": trees, "playouts_per_tree": playouts, "leaves_per_tree_per_round": lpt,
+    res = {"device": str(dev), "precision": os.environ.get("ALPHAGO_AMD_PRECISION", "bf16"), "trees": trees, "playouts_per_tree": playouts, "leaves_per_tree_per_round": lpt,
            "leaf_evals_per_s": round(evals / dt), "simulations_per_s": round(trees * playouts / dt),
            "seconds_per_move_all_trees": round(dt, 3)}
     games = int(sys.argv[3]) if len(sys.argv) > 3 else (8 if small else 256)
