@@ -83,16 +83,9 @@ void Forest::backup(SearchTree& tr, int leaf, double v_leaf_to_move, bool remove
   tr.sims += 1;
 }
 
-int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
-  if (!pending_.empty()) throw std::runtime_error("gather called with pending evaluations; call apply first");
-  leaf_states_.clear();
-  std::vector<int> all;
-  if (!which) {
-    all.resize(trees_.size());
-    for (size_t i = 0; i < trees_.size(); ++i) all[i] = (int)i;
-    which = &all;
-  }
-  for (int t : *which) {
+void Forest::gather_trees(const std::vector<int>& trees, int leaves_per_tree, std::vector<Leaf>& pend,
+                          std::vector<GameState>& states) {
+  for (int t : trees) {
     SearchTree& tr = trees_.at(t);
     for (int k = 0; k < leaves_per_tree; ++k) {
       GameState st = tr.root_state;
@@ -121,8 +114,8 @@ int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
           }
           if (nd.status == 0) {
             nd.status = 1;
-            pending_.push_back({t, u});
-            leaf_states_.push_back(st);
+            pend.push_back({t, u});
+            states.push_back(std::move(st));
             break;
           }
         }
@@ -138,6 +131,38 @@ int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
         ++depth;
       }
       if (stop_tree) break;
+    }
+  }
+}
+
+int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
+  if (!pending_.empty()) throw std::runtime_error("gather called with pending evaluations; call apply first");
+  leaf_states_.clear();
+  std::vector<int> all;
+  if (!which) {
+    all.resize(trees_.size());
+    for (size_t i = 0; i < trees_.size(); ++i) all[i] = (int)i;
+    which = &all;
+  }
+  const int n = (int)which->size();
+  const int T = std::max(1, std::min(threads_, n));
+  if (T == 1) {
+    gather_trees(*which, leaves_per_tree, pending_, leaf_states_);
+  } else {
+    // contiguous blocks of trees per worker; concatenated in tree order
+    std::vector<std::vector<Leaf>> pend(T);
+    std::vector<std::vector<GameState>> sts(T);
+    std::vector<std::thread> pool;
+    for (int w = 0; w < T; ++w)
+      pool.emplace_back([&, w]() {
+        const int lo = (int)((int64_t)n * w / T), hi = (int)((int64_t)n * (w + 1) / T);
+        std::vector<int> mine(which->begin() + lo, which->begin() + hi);
+        gather_trees(mine, leaves_per_tree, pend[w], sts[w]);
+      });
+    for (auto& th : pool) th.join();
+    for (int w = 0; w < T; ++w) {
+      pending_.insert(pending_.end(), pend[w].begin(), pend[w].end());
+      for (auto& s : sts[w]) leaf_states_.push_back(std::move(s));
     }
   }
   total_evals_ += (int64_t)pending_.size();
@@ -206,18 +231,20 @@ double Forest::rollout(GameState& s) {
   return (double)(s.get_winner() * p0);
 }
 
-void Forest::apply(const float* priors, const float* values) {
-  const int L = (int)pending_.size();
-  for (int i = 0; i < L; ++i) {
+void Forest::apply_range(int i0, int i1, const float* priors, const float* values, const uint8_t* mask) {
+  std::vector<int> moves;
+  std::vector<float> ps;
+  for (int i = i0; i < i1; ++i) {
     SearchTree& tr = trees_[pending_[i].tree];
     const int u = pending_[i].node;
     const GameState& st = leaf_states_[i];
     const float* pr = priors + (size_t)i * st.np;
-    std::vector<int> moves;
-    std::vector<float> ps;
+    const uint8_t* mk = mask ? mask + (size_t)i * st.np : nullptr;
+    moves.clear();
+    ps.clear();
     double sum = 0;
     for (int p = 0; p < st.np; ++p)
-      if (st.is_legal(p) && !st.is_eye(p, st.current_player)) {
+      if (mk ? (mk[p] != 0) : (st.is_legal(p) && !st.is_eye(p, st.current_player))) {
         moves.push_back(p);
         float v = std::max(pr[p], 0.f);
         ps.push_back(v);
@@ -244,6 +271,28 @@ void Forest::apply(const float* priors, const float* values) {
       v = (1.0 - lmbda_) * v + lmbda_ * z;
     }
     backup(tr, u, v, true);
+  }
+}
+
+void Forest::apply(const float* priors, const float* values, const uint8_t* mask) {
+  const int L = (int)pending_.size();
+  // rollouts draw from the shared RNG: keep them serial (and reproducible)
+  const int T = lmbda_ > 0 ? 1 : std::max(1, std::min(threads_, L / 64));
+  if (T == 1) {
+    apply_range(0, L, priors, values, mask);
+  } else {
+    // split at tree boundaries (pending_ is grouped by tree): no two workers touch one tree
+    std::vector<int> cut(T + 1, L);
+    cut[0] = 0;
+    for (int w = 1; w < T; ++w) {
+      int c = (int)((int64_t)L * w / T);
+      while (c < L && c > 0 && pending_[c].tree == pending_[c - 1].tree) ++c;
+      cut[w] = std::max(c, cut[w - 1]);
+    }
+    std::vector<std::thread> pool;
+    for (int w = 0; w < T; ++w)
+      pool.emplace_back([&, w]() { apply_range(cut[w], cut[w + 1], priors, values, mask); });
+    for (auto& th : pool) th.join();
   }
   pending_.clear();
 }

@@ -63,8 +63,11 @@ class Forest {
   void leaf_masks(uint8_t* out) const;
   // compact GPU-featurizer encoding of the pending leaves (see encode_state)
   void leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) const;
-  // priors (L, n*n) float32 (any non-negative scores; renormalised over sensible moves), values (L,)
-  void apply(const float* priors, const float* values);
+  // priors (L, n*n) float32 (any non-negative scores; renormalised over sensible moves), values (L,);
+  // mask (L, n*n) optional sensible-move mask (e.g. from the GPU featurizer) — skips the legality/eye scan
+  void apply(const float* priors, const float* values, const uint8_t* mask = nullptr);
+  // worker threads for gather/apply (trees are independent; results are identical for any count)
+  void set_threads(int n) { threads_ = n < 1 ? 1 : n; }
   void add_root_noise(int t, double alpha, double eps);
   // Root statistics
   void root_stats(int t, std::vector<int>& moves, std::vector<int>& visits, std::vector<float>& q) const;
@@ -88,6 +91,9 @@ class Forest {
   std::vector<int> fids_;
   int nplanes_ = 0;
   int64_t total_evals_ = 0;
+  int threads_ = 1;
+  void gather_trees(const std::vector<int>& trees, int lpt, std::vector<Leaf>& pend, std::vector<GameState>& states);
+  void apply_range(int i0, int i1, const float* priors, const float* values, const uint8_t* mask);
 };
 
 

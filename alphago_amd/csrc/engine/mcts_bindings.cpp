@@ -105,26 +105,33 @@ void bind_mcts(py::module_& m) {
            })
       .def(
           "apply",
-          [](Forest& f, py::array_t<float, py::array::c_style | py::array::forcecast> priors,
-             py::object values) {
+          [](Forest& f, py::array_t<float, py::array::c_style | py::array::forcecast> priors, py::object values,
+             py::object mask) {
             int L = f.n_pending();
             if (L == 0) return;
             int np = f.leaf_state(0).np;
             if (priors.ndim() != 2 || priors.shape(0) != L || priors.shape(1) != np)
               throw py::value_error("priors must be (n_pending, size*size)");
             const float* pv = priors.data();
-            if (values.is_none()) {
-              py::gil_scoped_release r;
-              f.apply(pv, nullptr);
-              return;
+            const float* vv = nullptr;
+            const uint8_t* mv = nullptr;
+            py::array_t<float, py::array::c_style | py::array::forcecast> va;
+            py::array_t<uint8_t, py::array::c_style | py::array::forcecast> ma;
+            if (!values.is_none()) {
+              va = values.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
+              if (va.size() != L) throw py::value_error("values must have n_pending entries");
+              vv = va.data();
             }
-            auto va = values.cast<py::array_t<float, py::array::c_style | py::array::forcecast>>();
-            if (va.size() != L) throw py::value_error("values must have n_pending entries");
-            const float* vv = va.data();
+            if (!mask.is_none()) {
+              ma = mask.cast<py::array_t<uint8_t, py::array::c_style | py::array::forcecast>>();
+              if (ma.size() != (ssize_t)L * np) throw py::value_error("mask must be (n_pending, size*size)");
+              mv = ma.data();
+            }
             py::gil_scoped_release r;
-            f.apply(pv, vv);
+            f.apply(pv, vv, mv);
           },
-          py::arg("priors"), py::arg("values") = py::none())
+          py::arg("priors"), py::arg("values") = py::none(), py::arg("mask") = py::none())
+      .def("set_threads", &Forest::set_threads, py::arg("n"))
       .def("add_root_noise", &Forest::add_root_noise, py::arg("tree"), py::arg("alpha") = 0.03,
            py::arg("eps") = 0.25)
       .def("root_stats",

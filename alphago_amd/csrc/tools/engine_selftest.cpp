@@ -149,37 +149,50 @@ int main(int argc, char** argv) {
       });
     for (auto& x : th) x.join();
   }
-  // forest: gather / threaded leaf featurize + encode / apply / advance
+  // forest: gather / threaded leaf featurize + encode / apply / advance, run
+  // with 1 and 4 worker threads: identical trees (workers own disjoint trees)
   {
     std::vector<int> pf;
     for (int f : {F_BOARD, F_ONES, F_TURNS_SINCE, F_LIBERTIES, F_SENSIBLENESS}) pf.push_back(f);
-    Forest forest(6, 5.0, 0.25, 60, 1000, 3, 7, pf);
-    for (int t = 0; t < 6; ++t) forest.set_root(t, pool[(t * 5) % pool.size()]);
-    std::uniform_real_distribution<float> u(0.f, 1.f);
-    for (int round = 0; round < 30; ++round) {
-      int L = forest.gather(4);
-      if (L == 0) continue;
-      const int np = forest.leaf_state(0).np;
-      std::vector<uint8_t> feat((size_t)L * forest.feature_planes() * np), masks((size_t)L * np);
-      forest.leaf_features(feat.data(), 4);
-      forest.leaf_masks(masks.data());
-      std::vector<int8_t> b((size_t)L * np);
-      std::vector<uint8_t> a((size_t)L * np), lad((size_t)L * np);
-      std::vector<int32_t> m(2 * L);
-      forest.leaf_encode(b.data(), a.data(), m.data(), lad.data(), 4);
-      std::vector<float> pri((size_t)L * np), val(L);
-      for (auto& x : pri) x = u(rng);
-      for (auto& x : val) x = 2.f * u(rng) - 1.f;
-      forest.apply(pri.data(), val.data());
+    std::vector<std::vector<int>> visits_by_threads;
+    for (int nthreads : {1, 4}) {
+      Forest forest(6, 5.0, 0.0, 60, 1000, 3, 7, pf);
+      forest.set_threads(nthreads);
+      for (int t = 0; t < 6; ++t) forest.set_root(t, pool[(t * 5) % pool.size()]);
+      std::mt19937_64 prng(99);
+      std::uniform_real_distribution<float> u(0.f, 1.f);
+      for (int round = 0; round < 30; ++round) {
+        int L = forest.gather(4);
+        if (L == 0) continue;
+        const int np = forest.leaf_state(0).np;
+        std::vector<uint8_t> feat((size_t)L * forest.feature_planes() * np), masks((size_t)L * np);
+        forest.leaf_features(feat.data(), 4);
+        forest.leaf_masks(masks.data());
+        std::vector<int8_t> b((size_t)L * np);
+        std::vector<uint8_t> a((size_t)L * np), lad((size_t)L * np);
+        std::vector<int32_t> m(2 * L);
+        forest.leaf_encode(b.data(), a.data(), m.data(), lad.data(), 4);
+        std::vector<float> pri((size_t)L * np), val(L);
+        for (auto& x : pri) x = u(prng);
+        for (auto& x : val) x = 2.f * u(prng) - 1.f;
+        forest.apply(pri.data(), val.data(), (round & 1) ? masks.data() : nullptr);
+      }
+      std::vector<int> vis;
+      for (int t = 0; t < 6; ++t) {
+        std::vector<int> mv, vs;
+        std::vector<float> q;
+        forest.root_stats(t, mv, vs, q);
+        vis.insert(vis.end(), vs.begin(), vs.end());
+        int best = forest.best_move(t, 0.0);
+        const GameState& r = forest.root_state(t);
+        CHECK(best == PASS || r.is_legal(best), "best move %d illegal", best);
+        forest.advance(t, best);
+        check_invariants(forest.root_state(t));
+      }
+      visits_by_threads.push_back(vis);
+      std::printf("forest (%d threads): ok (%lld evals)\n", nthreads, (long long)forest.total_evals());
     }
-    for (int t = 0; t < 6; ++t) {
-      int mv = forest.best_move(t, 0.0);
-      const GameState& r = forest.root_state(t);
-      CHECK(mv == PASS || r.is_legal(mv), "best move %d illegal", mv);
-      forest.advance(t, mv);
-      check_invariants(forest.root_state(t));
-    }
-    std::printf("forest: ok (%lld evals)\n", (long long)forest.total_evals());
+    CHECK(visits_by_threads[0] == visits_by_threads[1], "threaded search differs from serial search");
   }
   if (g_fail) {
     std::printf("FAILED (%d checks)\n", g_fail);

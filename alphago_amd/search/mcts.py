@@ -18,6 +18,7 @@ value/policy/rollout *callables*, ``get_move(state)`` and
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional, Sequence
 
 import numpy as np
@@ -30,10 +31,11 @@ from ..utils.gorecords import flatten_idx
 
 class BatchedMCTS(object):
     def __init__(self, policy, value=None, n_trees: int = 1, c_puct: float = 5.0, lmbda: float = 0.0,
-                 rollout_limit: int = 500, virtual_loss: int = 3, seed: int = 0, threads: int = 8):
+                 rollout_limit: int = 500, virtual_loss: int = 3, seed: int = 0, threads: Optional[int] = None):
         self.policy, self.value = policy, value
         self.c_puct, self.lmbda, self.rollout_limit, self.vl, self.seed = c_puct, lmbda, rollout_limit, virtual_loss, seed
-        self.threads = threads
+        # host worker threads (gather/apply/encode); a GPU box's process gets ~16 cores
+        self.threads = threads or min(16, os.cpu_count() or 1)
         pf = policy.preprocessor.feature_list
         vf = value.preprocessor.feature_list if value is not None else pf
         self._same_feats = list(pf) == list(vf)
@@ -49,6 +51,7 @@ class BatchedMCTS(object):
         pf = self.policy.preprocessor.feature_list
         self.forest = _engine().Forest(n_trees, self.c_puct, self.lmbda if self.value is None or self.lmbda > 0 else 0.0,
                                        self.rollout_limit, 1000, self.vl, self.seed, [f.lower() for f in pf])
+        self.forest.set_threads(self.threads)
         self._n = n_trees
         self._roots = [None] * n_trees
 
@@ -86,8 +89,9 @@ class BatchedMCTS(object):
         f.leaf_encode_into(b.data_ptr(), a.data_ptr(), m.data_ptr(), l.data_ptr() if ladder else 0, b.shape[0],
                            self.threads)
         lad = l[:L] if ladder else None
-        out, _, bad = pe.evaluate_encoded(b[:L], a[:L], m[:L], lad)
+        out, sens, bad = pe.evaluate_encoded(b[:L], a[:L], m[:L], lad)
         probs = out.float().cpu().numpy()
+        mask = sens.cpu().numpy()  # sensible moves from the GPU featurizer: apply() skips its own scan
         values = None
         if ve is not None:
             vout, _, vbad = ve.evaluate_encoded(b[:L], a[:L], m[:L], lad)
@@ -98,9 +102,10 @@ class BatchedMCTS(object):
             planes = self.policy.preprocessor.states_to_uint8(states)
             masks = _engine().featurize_batch(states, ["sensibleness"], self.threads).reshape(len(bad), -1)
             probs[bad] = pe.evaluate(planes, masks).float().cpu().numpy()
+            mask[bad] = masks
             if ve is not None:
                 values[bad] = ve.evaluate(self.value.preprocessor.states_to_uint8(states)).float().cpu().numpy()
-        f.apply(probs, values)
+        f.apply(probs, values, mask)
 
     def _evaluate_pending(self) -> None:
         f = self.forest
