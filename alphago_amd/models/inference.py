@@ -209,11 +209,12 @@ class HipTrunkInference:
             self._run(bk, encoded)
         return g
 
-    def _get(self, n: int, encoded: bool = False) -> _Bucket:
+    def _get(self, n: int, encoded: bool = False, slot: int = 0) -> _Bucket:
         B = self.bucket_for(n)
-        if B not in self._b:
-            self._b[B] = self._make_bucket(B)
-        bk = self._b[B]
+        key = (B, slot)
+        if key not in self._b:
+            self._b[key] = self._make_bucket(B)
+        bk = self._b[key]
         if self.use_graphs:
             if encoded and bk.graph_enc is None:
                 bk.graph_enc = self._capture(bk, True)
@@ -222,15 +223,14 @@ class HipTrunkInference:
         return bk
 
     @torch.no_grad()
-    def evaluate_encoded(self, board, ages, meta, ladder=None):
-        """Forward from the compact encoding (GPU featurizer in the graph).
-
-        Returns (outputs (n, ...), sensible mask (n, S*S) uint8 device tensor,
-        list of board indices whose eye recursion overflowed the kernel and
-        must be re-evaluated from CPU planes)."""
+    def submit_encoded(self, board, ages, meta, ladder=None, slot: int = 0):
+        """Asynchronous half of evaluate_encoded: H2D copies (non-blocking from
+        pinned host buffers) + graph replay on the current stream.  ``slot``
+        selects an independent set of bucket buffers, so two batches can be in
+        flight.  Returns a handle for collect()."""
         assert self.fz is not None, "engine built without a feature list"
         n = board.shape[0]
-        bk = self._get(n, encoded=True)
+        bk = self._get(n, encoded=True, slot=slot)
         bk.e_board[:n].copy_(torch.as_tensor(board), non_blocking=True)
         bk.e_ages[:n].copy_(torch.as_tensor(ages), non_blocking=True)
         bk.e_meta[:n].copy_(torch.as_tensor(meta), non_blocking=True)
@@ -247,8 +247,22 @@ class HipTrunkInference:
             bk.graph_enc.replay()
         else:
             self._run(bk, True)
+        return bk, n
+
+    def collect(self, handle):
+        """(outputs (n, ...), sensible mask (n, S*S) device tensors, overflow board indices) — syncs."""
+        bk, n = handle
         bad = torch.nonzero(bk.ovf[:n]).flatten().tolist()
         return self._outputs(bk, n), bk.legal[:n], bad
+
+    @torch.no_grad()
+    def evaluate_encoded(self, board, ages, meta, ladder=None, slot: int = 0):
+        """Forward from the compact encoding (GPU featurizer in the graph).
+
+        Returns (outputs (n, ...), sensible mask (n, S*S) uint8 device tensor,
+        list of board indices whose eye recursion overflowed the kernel and
+        must be re-evaluated from CPU planes)."""
+        return self.collect(self.submit_encoded(board, ages, meta, ladder, slot))
 
     @torch.no_grad()
     def evaluate(self, planes, legal=None):

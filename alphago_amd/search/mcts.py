@@ -8,7 +8,12 @@ subtree reuse, optional λ-mixed random rollouts).  Each round gathers up to
 and evaluates ALL of them in one batched policy (+ value) forward on the GPU
 whose HIP graph starts with the device featurizer (ops/gpu_features.py);
 priors/values are applied back natively.  Engines without the encoded path
-(CPU) get uint8 planes featurised in native threads instead.  This replaces the reference's serial search that made a
+(CPU) get uint8 planes featurised in native threads instead.
+
+With ``pipeline=True`` (default on a GPU) the trees are split into two
+forests whose rounds interleave: while the GPU evaluates one group's leaves
+(asynchronous graph replay into its own buffer slot), the host threads apply
+the other group's results and gather + encode its next leaves.  This replaces the reference's serial search that made a
 batch-1 network call per tree level (mcts.py:91-161; ParallelMCTS stub
 :174-175).
 
@@ -29,10 +34,60 @@ from .._native import engine as _engine
 from ..utils.gorecords import flatten_idx
 
 
+class _ForestGroup(object):
+    """Several native Forests presented as one (tree t -> (forest, local index))."""
+
+    def __init__(self, forests):
+        self.forests = forests
+        self.map = [(fi, j) for fi, f in enumerate(forests) for j in range(f.n_trees)]
+
+    def _at(self, t):
+        fi, j = self.map[t]
+        return self.forests[fi], j
+
+    def set_root(self, t, st):
+        f, j = self._at(t)
+        f.set_root(j, st)
+
+    def advance(self, t, move):
+        f, j = self._at(t)
+        f.advance(j, move)
+
+    def root_stats(self, t):
+        f, j = self._at(t)
+        return f.root_stats(j)
+
+    def best_move(self, t, temperature=0.0):
+        f, j = self._at(t)
+        return f.best_move(j, temperature)
+
+    def sims(self, t):
+        f, j = self._at(t)
+        return f.sims(j)
+
+    def add_root_noise(self, t, alpha=0.03, eps=0.25):
+        f, j = self._at(t)
+        f.add_root_noise(j, alpha, eps)
+
+    def root_state(self, t):
+        f, j = self._at(t)
+        return f.root_state(j)
+
+    @property
+    def total_evals(self):
+        return sum(f.total_evals for f in self.forests)
+
+    @property
+    def n_trees(self):
+        return len(self.map)
+
+
 class BatchedMCTS(object):
     def __init__(self, policy, value=None, n_trees: int = 1, c_puct: float = 5.0, lmbda: float = 0.0,
-                 rollout_limit: int = 500, virtual_loss: int = 3, seed: int = 0, threads: Optional[int] = None):
+                 rollout_limit: int = 500, virtual_loss: int = 3, seed: int = 0, threads: Optional[int] = None,
+                 pipeline: Optional[bool] = None):
         self.policy, self.value = policy, value
+        self.pipeline = pipeline
         self.c_puct, self.lmbda, self.rollout_limit, self.vl, self.seed = c_puct, lmbda, rollout_limit, virtual_loss, seed
         # host worker threads (gather/apply/encode); a GPU box's process gets ~16 cores
         self.threads = threads or min(16, os.cpu_count() or 1)
@@ -48,10 +103,19 @@ class BatchedMCTS(object):
     def resize(self, n_trees: int) -> None:
         if n_trees == self._n:
             return
-        pf = self.policy.preprocessor.feature_list
-        self.forest = _engine().Forest(n_trees, self.c_puct, self.lmbda if self.value is None or self.lmbda > 0 else 0.0,
-                                       self.rollout_limit, 1000, self.vl, self.seed, [f.lower() for f in pf])
-        self.forest.set_threads(self.threads)
+        pf = [f.lower() for f in self.policy.preprocessor.feature_list]
+        lm = self.lmbda if self.value is None or self.lmbda > 0 else 0.0
+        pipe = self.pipeline
+        if pipe is None:
+            pipe = self._encoded_engines() is not None and n_trees >= 8
+        sizes = [n_trees - n_trees // 2, n_trees // 2] if pipe and n_trees >= 2 else [n_trees]
+        forests = []
+        for k, n in enumerate(sizes):
+            f = _engine().Forest(n, self.c_puct, lm, self.rollout_limit, 1000, self.vl, self.seed + 7919 * k, pf)
+            f.set_threads(self.threads)
+            forests.append(f)
+        self._forests = forests
+        self.forest = forests[0] if len(forests) == 1 else _ForestGroup(forests)
         self._n = n_trees
         self._roots = [None] * n_trees
 
@@ -62,15 +126,19 @@ class BatchedMCTS(object):
             self._pinned = torch.empty(max(need, 1 << 20), dtype=torch.uint8, pin_memory=pin)
         return self._pinned[:need]
 
-    def _enc_buffers(self, L: int, np_: int):
-        if self._enc is None or self._enc[0].shape[0] < L or self._enc[0].shape[1] != np_:
+    def _enc_buffers(self, L: int, np_: int, slot: int = 0):
+        if self._enc is None:
+            self._enc = {}
+        e = self._enc.get(slot)
+        if e is None or e[0].shape[0] < L or e[0].shape[1] != np_:
             pin = torch.cuda.is_available()
             cap = max(L, 256)
-            self._enc = (torch.zeros((cap, np_), dtype=torch.int8, pin_memory=pin),
-                         torch.zeros((cap, np_), dtype=torch.uint8, pin_memory=pin),
-                         torch.zeros((cap, 2), dtype=torch.int32, pin_memory=pin),
-                         torch.zeros((cap, np_), dtype=torch.uint8, pin_memory=pin))
-        return self._enc
+            e = (torch.zeros((cap, np_), dtype=torch.int8, pin_memory=pin),
+                 torch.zeros((cap, np_), dtype=torch.uint8, pin_memory=pin),
+                 torch.zeros((cap, 2), dtype=torch.int32, pin_memory=pin),
+                 torch.zeros((cap, np_), dtype=torch.uint8, pin_memory=pin))
+            self._enc[slot] = e
+        return e
 
     def _encoded_engines(self):
         pe = self.policy.engine
@@ -79,22 +147,29 @@ class BatchedMCTS(object):
             return pe, ve
         return None
 
-    def _evaluate_encoded(self, pe, ve) -> None:
-        f = self.forest
+    def _submit(self, f, slot: int, pe, ve):
+        """Encode f's pending leaves into pinned buffers and launch the GPU evaluation (async)."""
         L = f.n_pending
         s0 = f.leaf_state(0)
         np_ = s0.size * s0.size
         ladder = pe.needs_ladder or (ve is not None and ve.needs_ladder)
-        b, a, m, l = self._enc_buffers(L, np_)
+        b, a, m, l = self._enc_buffers(L, np_, slot)
         f.leaf_encode_into(b.data_ptr(), a.data_ptr(), m.data_ptr(), l.data_ptr() if ladder else 0, b.shape[0],
                            self.threads)
         lad = l[:L] if ladder else None
-        out, sens, bad = pe.evaluate_encoded(b[:L], a[:L], m[:L], lad)
+        hp = pe.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot)
+        hv = ve.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot) if ve is not None else None
+        return hp, hv
+
+    def _finish(self, f, handles, pe, ve) -> None:
+        """Collect a submitted evaluation and apply it to f."""
+        hp, hv = handles
+        out, sens, bad = pe.collect(hp)
         probs = out.float().cpu().numpy()
         mask = sens.cpu().numpy()  # sensible moves from the GPU featurizer: apply() skips its own scan
         values = None
-        if ve is not None:
-            vout, _, vbad = ve.evaluate_encoded(b[:L], a[:L], m[:L], lad)
+        if hv is not None:
+            vout, _, vbad = ve.collect(hv)
             values = vout.float().cpu().numpy()
             bad = sorted(set(bad) | set(vbad))
         if bad:  # eye recursion too deep for the kernel: these rows from CPU planes
@@ -107,14 +182,18 @@ class BatchedMCTS(object):
                 values[bad] = ve.evaluate(self.value.preprocessor.states_to_uint8(states)).float().cpu().numpy()
         f.apply(probs, values, mask)
 
-    def _evaluate_pending(self) -> None:
-        f = self.forest
+    def _evaluate_encoded(self, pe, ve, f=None, slot: int = 0) -> None:
+        f = f if f is not None else self._forests[0]
+        self._finish(f, self._submit(f, slot, pe, ve), pe, ve)
+
+    def _evaluate_pending(self, f=None, slot: int = 0) -> None:
+        f = f if f is not None else self._forests[0]
         L = f.n_pending
         if L == 0:
             return
         enc = self._encoded_engines()
         if enc is not None:
-            self._evaluate_encoded(*enc)
+            self._evaluate_encoded(enc[0], enc[1], f, slot)
             return
         s0 = f.leaf_state(0)
         np_ = s0.size * s0.size
@@ -154,24 +233,63 @@ class BatchedMCTS(object):
         if len(states) != self._n:
             self.resize(len(states))
         self._sync_roots(states)
-        f = self.forest
+        fg = self.forest
         # expand roots first (needed for root noise)
-        f.gather(1)
-        self._evaluate_pending()
+        for k, f in enumerate(self._forests):
+            f.gather(1)
+            self._evaluate_pending(f, k)
         if noise:
             for i in range(self._n):
-                f.add_root_noise(i, noise, 0.25)
-        target = [f.sims(i) + n_playout for i in range(self._n)]
-        while True:
-            todo = [i for i in range(self._n) if f.sims(i) < target[i]]
-            if not todo:
-                break
-            n = f.gather(leaves_per_tree, todo)
-            if n == 0 and all(f.sims(i) < target[i] for i in todo):
-                # only terminal/collided paths this round; they still count as sims
-                continue
-            self._evaluate_pending()
-        return [f.best_move(i, temperature) for i in range(self._n)]
+                fg.add_root_noise(i, noise, 0.25)
+        offs = [0]
+        for f in self._forests:
+            offs.append(offs[-1] + f.n_trees)
+        targets = [[fg.sims(offs[k] + j) + n_playout for j in range(f.n_trees)] for k, f in enumerate(self._forests)]
+
+        def gather(k):
+            """Gather the next leaves of group k; False when its trees are done."""
+            f = self._forests[k]
+            while True:
+                todo = [j for j in range(f.n_trees) if f.sims(j) < targets[k][j]]
+                if not todo:
+                    return False
+                if f.gather(leaves_per_tree, todo) > 0:
+                    return True
+                # only terminal/collided paths this round: they still count as sims
+
+        enc = self._encoded_engines()
+        if len(self._forests) == 1 or enc is None:
+            for k, f in enumerate(self._forests):
+                while gather(k):
+                    self._evaluate_pending(f, k)
+        else:
+            pe, ve = enc
+            live = [gather(0), gather(1)]
+            inflight = [None, None]
+            if live[0]:
+                inflight[0] = self._submit(self._forests[0], 0, pe, ve)
+            k = 1
+            while live[0] or live[1]:
+                # host work for group k overlaps the GPU evaluation of group 1-k
+                if live[k]:
+                    if inflight[k] is not None:
+                        self._finish(self._forests[k], inflight[k], pe, ve)
+                        inflight[k] = None
+                        live[k] = gather(k)
+                    if live[k]:
+                        inflight[k] = self._submit(self._forests[k], k, pe, ve)
+                k ^= 1
+                if inflight[k] is not None and not live[k ^ 1]:
+                    # the other group is done: nothing to overlap with
+                    self._finish(self._forests[k], inflight[k], pe, ve)
+                    inflight[k] = None
+                    live[k] = gather(k)
+                    if live[k]:
+                        inflight[k] = self._submit(self._forests[k], k, pe, ve)
+            for k in (0, 1):
+                if inflight[k] is not None:
+                    self._finish(self._forests[k], inflight[k], pe, ve)
+        return [fg.best_move(i, temperature) for i in range(self._n)]
 
     def visit_distribution(self, tree: int, size: int) -> np.ndarray:
         moves, visits, _ = self.forest.root_stats(tree)

@@ -194,3 +194,13 @@ def test_batched_mcts_encoded_path(cuda_device):
     moves = m.search(states, n_playout=64, leaves_per_tree=8)
     for s, mv in zip(states, moves):
         assert mv is None or s.is_legal(mv)
+    # 9 trees -> two pipelined forests (5 + 4) whose GPU evaluations overlap host work
+    states = random_positions(9, seed=2, max_len=60)
+    mp = BatchedMCTS(pol, val, n_trees=9)
+    assert len(mp._forests) == 2
+    moves = mp.search(states, n_playout=48, leaves_per_tree=8)
+    for i, (s, mv) in enumerate(zip(states, moves)):
+        assert mv is None or s.is_legal(mv)
+        assert sum(mp.forest.root_stats(i)[1]) >= 48
+    mp.update_with_move(3, moves[3])
+    assert np.isclose(mp.visit_distribution(0, 19).sum(), 1.0)
