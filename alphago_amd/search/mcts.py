@@ -305,6 +305,57 @@ class BatchedMCTS(object):
             self._roots[tree].append(move)
 
 
+class TreeNode(object):
+    """Reference-compatible tree node (mcts.py:4-64), pure Python.
+
+    Same fields and methods (``expansion``, ``selection``, ``isLeaf``,
+    ``update``, ``toValue``) with the SURVEY Q3 fix: the exploration bonus is
+    recomputed at selection time from the parent's current visit count
+    (``u = c_puct * P * sqrt(N_parent) / (1 + N)``) instead of being frozen at
+    the node's last update, so children of the root keep being explored.
+    The production search runs on the native forest (BatchedMCTS / MCTS)."""
+
+    def __init__(self, parent, prior_p, c_puct: float = 5.0):
+        self.parent = parent
+        self.nVisits = 0
+        self.Q_value = 0.0
+        self.u_value = prior_p
+        self.children = {}
+        self.P = prior_p
+        self.c_puct = c_puct
+
+    def expansion(self, actions):
+        for action, prob in actions:
+            if action not in self.children:
+                self.children[action] = TreeNode(self, prob, self.c_puct)
+
+    def selection(self):
+        """(action, child) maximising Q + u."""
+        return max(self.children.items(), key=lambda an: an[1].toValue())
+
+    def isLeaf(self):
+        return self.children == {}
+
+    is_leaf = isLeaf
+
+    def is_root(self):
+        return self.parent is None
+
+    def update(self, leaf_value, c_puct=None):
+        """Count a visit and fold ``leaf_value`` (mover's perspective) into the running mean Q."""
+        if c_puct is not None:
+            self.c_puct = c_puct
+        self.nVisits += 1
+        self.Q_value += (leaf_value - self.Q_value) / self.nVisits
+        if self.parent is not None:
+            self.u_value = self.c_puct * self.P * np.sqrt(self.parent.nVisits) / (1 + self.nVisits)
+
+    def toValue(self):
+        if self.parent is not None and self.parent.nVisits > 0:
+            self.u_value = self.c_puct * self.P * np.sqrt(self.parent.nVisits) / (1 + self.nVisits)
+        return self.Q_value + self.u_value
+
+
 class MCTS(object):
     """Reference-compatible serial API on the native tree.
 
@@ -365,6 +416,36 @@ class MCTS(object):
     def root_visits(self):
         moves, visits, q = self.forest.root_stats(0)
         return dict(zip(moves, visits))
+
+    def _DFS(self, nDepth, treenode, state):
+        """One simulation on a Python TreeNode tree (reference mcts.py:91-126):
+        select/expand down to ``nDepth``, evaluate the leaf with
+        V = (1 - lambda) v + lambda z, back the value up.  Fixes Q4 (no None
+        nodes on early game end; negamax sign per ply) and Q3 (the root is
+        counted)."""
+        visited = [treenode]
+        for _ in range(nDepth):
+            if state.is_end_of_game:
+                break
+            if treenode.isLeaf():
+                treenode.expansion(self._policy(state))
+                if treenode.isLeaf():
+                    break
+            action, treenode = treenode.selection()
+            state.do_move(action)
+            visited.append(treenode)
+        if state.is_end_of_game:
+            v = float(state.get_winner() * state.current_player)
+        else:
+            v = float(self._value(state)) if self._value is not None else 0.0
+            if self._lmbda > 0 and self._rollout is not None:
+                v = (1 - self._lmbda) * v + self._lmbda * self._rollout_value(state)
+        # v is for the player to move at the leaf; the node entered by the
+        # opponent's move stores the mover's value -v, alternating upwards
+        value = -v
+        for node in reversed(visited):
+            node.update(value, self._c_puct)
+            value = -value
 
     def update_with_move(self, last_move) -> None:
         try:

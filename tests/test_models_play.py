@@ -182,3 +182,35 @@ def test_gtp_transcript():
     assert e2.disconnect
     assert out.getvalue().count("= pass") == 2
     assert format_vertex((8, 0)) == "J1"
+
+
+# --- reference tests/test_mcts.py (TreeNode / _DFS / get_move), Python 3 ---
+def _ref_policy(state):
+    moves = state.get_legal_moves(include_eyes=False)
+    probs = np.arange(361, dtype=np.float64)
+    probs = probs / probs.sum()
+    return list(zip(moves, probs))
+
+
+def test_reference_treenode_selection():
+    from alphago_amd.search.mcts import TreeNode
+
+    gs = go.GameState()
+    node = TreeNode(None, 1.0)
+    node.expansion(_ref_policy(gs))
+    action, child = node.selection()
+    assert action == (18, 18) and child is not None
+    assert not node.isLeaf() and child.isLeaf() and node.is_root()
+
+
+def test_reference_mcts_dfs_and_get_move():
+    from alphago_amd.search.mcts import TreeNode
+
+    gs = go.GameState()
+    m = MCTS(gs, lambda s: 0.0, _ref_policy, _ref_policy, n_search=2, lmbda=0.0)
+    root = TreeNode(None, 1.0)
+    m._DFS(8, root, gs.copy())
+    assert root.children[(18, 18)].nVisits == 1
+    assert root.nVisits == 1  # Q3 fix: the root is counted
+    move = m.get_move(gs)
+    m.update_with_move(move)
