@@ -223,11 +223,14 @@ class HipTrunkInference:
         return bk
 
     @torch.no_grad()
-    def submit_encoded(self, board, ages, meta, ladder=None, slot: int = 0):
+    def submit_encoded(self, board, ages, meta, ladder=None, slot: int = 0, to_host: bool = False):
         """Asynchronous half of evaluate_encoded: H2D copies (non-blocking from
-        pinned host buffers) + graph replay on the current stream.  ``slot``
-        selects an independent set of bucket buffers, so two batches can be in
-        flight.  Returns a handle for collect()."""
+        pinned host buffers) + graph replay on the current stream; with
+        ``to_host`` also the D2H copy of the results into pinned host buffers,
+        followed by an event.  ``slot`` selects an independent set of bucket
+        buffers, so two batches can be in flight; the GPU work stays serial on
+        one stream (two overlapping batches would delay each other's results).
+        Returns a handle for collect()."""
         assert self.fz is not None, "engine built without a feature list"
         n = board.shape[0]
         bk = self._get(n, encoded=True, slot=slot)
@@ -247,11 +250,30 @@ class HipTrunkInference:
             bk.graph_enc.replay()
         else:
             self._run(bk, True)
-        return bk, n
+        host = None
+        if to_host:
+            if not hasattr(bk, "h_out"):
+                out = self._outputs(bk, bk.B)
+                bk.h_out = torch.empty(out.shape, dtype=torch.float32, pin_memory=True)
+                bk.h_mask = torch.empty(bk.legal.shape, dtype=torch.uint8, pin_memory=True)
+                bk.h_ovf = torch.empty(bk.ovf.shape, dtype=torch.int32, pin_memory=True)
+            bk.h_out[:n].copy_(self._outputs(bk, n), non_blocking=True)
+            bk.h_mask[:n].copy_(bk.legal[:n], non_blocking=True)
+            bk.h_ovf[:n].copy_(bk.ovf[:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            host = ev
+        return bk, n, host
 
     def collect(self, handle):
-        """(outputs (n, ...), sensible mask (n, S*S) device tensors, overflow board indices) — syncs."""
-        bk, n = handle
+        """(outputs (n, ...), sensible mask (n, S*S), overflow board indices).
+        For a to_host submission: numpy views of the pinned host buffers (valid
+        until the slot is submitted again), waiting only for that batch's event."""
+        bk, n, ev = handle
+        if ev is not None:
+            ev.synchronize()
+            bad = np.nonzero(bk.h_ovf[:n].numpy())[0].tolist()
+            return bk.h_out[:n].numpy(), bk.h_mask[:n].numpy(), bad
         bad = torch.nonzero(bk.ovf[:n]).flatten().tolist()
         return self._outputs(bk, n), bk.legal[:n], bad
 

@@ -157,20 +157,21 @@ class BatchedMCTS(object):
         f.leaf_encode_into(b.data_ptr(), a.data_ptr(), m.data_ptr(), l.data_ptr() if ladder else 0, b.shape[0],
                            self.threads)
         lad = l[:L] if ladder else None
-        hp = pe.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot)
-        hv = ve.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot) if ve is not None else None
+        hp = pe.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot, to_host=True)
+        hv = ve.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot, to_host=True) if ve is not None else None
         return hp, hv
 
     def _finish(self, f, handles, pe, ve) -> None:
         """Collect a submitted evaluation and apply it to f."""
         hp, hv = handles
-        out, sens, bad = pe.collect(hp)
-        probs = out.float().cpu().numpy()
-        mask = sens.cpu().numpy()  # sensible moves from the GPU featurizer: apply() skips its own scan
+        # mask: sensible moves from the GPU featurizer, so apply() skips its own scan
+        probs, mask, bad = pe.collect(hp)
+        probs = np.array(probs, copy=True)
+        mask = np.array(mask, copy=True)
         values = None
         if hv is not None:
-            vout, _, vbad = ve.collect(hv)
-            values = vout.float().cpu().numpy()
+            values, _, vbad = ve.collect(hv)
+            values = np.array(values, copy=True)
             bad = sorted(set(bad) | set(vbad))
         if bad:  # eye recursion too deep for the kernel: these rows from CPU planes
             states = [f.leaf_state(i) for i in bad]

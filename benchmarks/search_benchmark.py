@@ -42,7 +42,18 @@ def main():
     s.search(states, playouts, lpt)
     dt = time.perf_counter() - t
     evals = s.forest.total_evals - e0
-    res = {"device": str(dev), "precision": os.environ.get("ALPHAGO_AMD_PRECISION", "bf16"), "trees": trees, "playouts_per_tree": playouts, "leaves_per_tree_per_round": lpt,
+    if dev.type == "cuda":  # the same search without the two-forest pipeline
+        s1 = BatchedMCTS(pol, val, n_trees=trees, seed=0, pipeline=False)
+        s1.search(states, 32, lpt)
+        torch.cuda.synchronize()
+        e1 = s1.forest.total_evals
+        t1 = time.perf_counter()
+        s1.search(states, playouts, lpt)
+        np_evals = (s1.forest.total_evals - e1) / (time.perf_counter() - t1)
+    else:
+        np_evals = None
+    res = {"device": str(dev), "precision": os.environ.get("ALPHAGO_AMD_PRECISION", "bf16"), "trees": trees,
+           "leaf_evals_per_s_no_pipeline": round(np_evals) if np_evals else None, "playouts_per_tree": playouts, "leaves_per_tree_per_round": lpt,
            "leaf_evals_per_s": round(evals / dt), "simulations_per_s": round(trees * playouts / dt),
            "seconds_per_move_all_trees": round(dt, 3)}
     games = int(sys.argv[3]) if len(sys.argv) > 3 else (8 if small else 256)
