@@ -28,6 +28,9 @@
 //   gradient (and the bias gradient, accumulated by the tap-0 workgroups).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <numeric>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -106,7 +109,7 @@ __device__ __forceinline__ void conv_store_tile(const ConvFwdArgs& a, const f32x
 }
 
 // ----------------------------------------------------------------- forward
-template <int BN, int MODE, int BM, int MBW, bool EPF = true>
+template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true>
 __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
   constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
@@ -213,6 +216,25 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   stage(0);
   wait_vmcnt0();
   __syncthreads();
+  if constexpr (!PIPE) {  // one fragment set (large wave tiles): read, then MFMA, per k-half
+    for (int ks = 0; ks < nK; ++ks) {
+      const int cur = ks & 1;
+      const char* base = smem + cur * STAGE;
+      if (ks + 1 < nK) stage(cur ^ 1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        read_frags(base, kk, xa, wa);
+        __builtin_amdgcn_s_setprio(1);
+        mfmas(xa, wa);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      wait_vmcnt0();
+      __syncthreads();
+    }
+    ep.load(a, ep_mrow, ep_nbase);
+    ep.store(a, acc, ep_mrow);
+    return;
+  }
   read_frags(smem, 0, xa, wa);
   for (int ks = 0; ks < nK; ++ks) {
     const int cur = ks & 1;
@@ -594,17 +616,192 @@ static void launch_fwd_halo(const ConvFwdArgs& a_in, hipStream_t st) {
 
 static int g_fwd_bm = 0;  // 0 = auto
 
-template <int BN, int MODE, int BM, int MBW, bool EPF = true>
+template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF>,
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF>), grid, dim3(BM / MBW * 8), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE>), grid, dim3(BM / MBW * 8), smem, st, a);
+}
+
+
+// ------------------------------------------- forward, interior-halo variant
+// The gather kernel re-fetches every input row once per tap (9x for 3x3).
+// Here a workgroup stages, per 64-channel chunk, the contiguous range of
+// padded input rows that its 256 interior pixels and all taps touch (the
+// "halo", <= H2_ROWS rows) ONCE, then runs all K*K taps against it: the A
+// fragments are gathered from LDS with per-lane row addresses (row = padded
+// position of the pixel + tap offset), so only interior pixels are computed
+// (no border waste, unlike conv_fwd_halo_kernel).  Per tap-step only the
+// weight tile (24 KB at BN = 192) streams through a double buffer.
+constexpr int H2_BM = 256;
+constexpr int H2_ROWS = 384;  // 48 KB of 128-B rows per halo buffer
+
+template <int BN, int MODE>
+__global__ __launch_bounds__(512, 1) void conv_fwd_halo2_kernel(ConvFwdArgs a) {
+  constexpr int NB = BN / 32;
+  constexpr int MB = 4;
+  constexpr int H_BYTES = H2_ROWS * 128;
+  constexpr int W_BYTES = BN * 128;
+  constexpr int B_INSTR = BN / 64;        // weight pieces per wave
+  constexpr int H_PIECES = H2_ROWS / 8;   // 1-KB halo pieces per chunk
+  constexpr int H_PW = H_PIECES / 8;      // per wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;                // 2 x H_BYTES
+  char* const wbuf = smem + 2 * H_BYTES;  // 2 x W_BYTES
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * H2_BM;
+  const int n0 = blockIdx.y * BN;
+  const int SS = a.S * a.S;
+  const int CC = a.Cin >> 6;
+  const int T = a.K * a.K;
+  const int HP = a.HPi;
+  const int Pc = a.offi + a.K / 2;  // interior offset of the input (its pad)
+  const int G = (a.K / 2) * (HP + 1);
+  const int Q = a.M / SS * HP * HP;  // padded input positions
+
+  auto qpos = [&](int m) {
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    return (b * HP + ii + Pc) * HP + jj + Pc;
+  };
+  const int mlast = (m0 + H2_BM - 1 < a.M ? m0 + H2_BM - 1 : a.M - 1);
+  const int qfirst = qpos(m0) - G;
+
+  // halo staging: lane -> row 8*piece + lane/8, physical chunk lane%8
+  int hsrc[H_PW];
+#pragma unroll
+  for (int i = 0; i < H_PW; ++i) {
+    const int r = (wave * H_PW + i) * 8 + (lane >> 3);
+    int q = qfirst + r;
+    q = q < 0 ? 0 : (q >= Q ? Q - 1 : q);
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    hsrc[i] = q * a.Cin + logical * 8;
+  }
+  int brow[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int r = wave * (BN / 8) + i * 8 + (lane >> 3);
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    brow[i] = (n0 + r) * a.Cin + logical * 8;
+  }
+  const size_t wtap = (size_t)a.Cout * a.Cin;
+  auto stage_halo = [&](int c, int buf) {
+    char* base = hbuf + buf * H_BYTES;
+#pragma unroll
+    for (int i = 0; i < H_PW; ++i) glds16(a.x + hsrc[i] + c * 64, base + (wave * H_PW + i) * 1024);
+  };
+  auto stage_w = [&](int t, int c, int buf) {
+    const __bf16* wt = a.w + (size_t)t * wtap + c * 64;
+    char* base = wbuf + buf * W_BYTES;
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i) glds16(wt + brow[i], base + (wave * (BN / 8) + i * 8) * 128);
+  };
+
+  // per-lane halo-relative rows of this lane's pixel in each m block
+  int qrel[MB];
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    int m = m0 + wm * 64 + j * 16 + (lane & 15);
+    m = m < a.M ? m : a.M - 1;
+    qrel[j] = qpos(m) - qfirst;
+  }
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int swzw = (lane & 15) >> 1;
+  const int wrow0 = (wn * (BN / 2) + (lane & 15)) * 128;
+  const int ep_mrow = m0 + wm * 64 + (lane & 15);
+  const int ep_nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
+  ConvEpilogue<NB, MB, MODE> ep;
+
+  const int nK = CC * T;
+  stage_halo(0, 0);
+  stage_w(0, 0, 0);
+  wait_vmcnt0();
+  __syncthreads();
+  int c = 0, t = 0;
+  for (int ks = 0; ks < nK; ++ks) {
+    // prefetch the next weight tile (and, on a chunk's first tap, the next chunk's halo)
+    const int tn = (t + 1 == T) ? 0 : t + 1;
+    const int cn = (t + 1 == T) ? c + 1 : c;
+    if (ks + 1 < nK) stage_w(tn, cn, (ks + 1) & 1);
+    if (t == 0 && c + 1 < CC) stage_halo(c + 1, (c + 1) & 1);
+    if (ks == (nK > 2 ? nK - 2 : 0)) ep.load(a, ep_mrow, ep_nbase);
+    const char* hb = hbuf + (c & 1) * H_BYTES;
+    const char* wb = wbuf + (ks & 1) * W_BYTES;
+    const int kh = t / a.K, kw = t - (t / a.K) * a.K;
+    const int toff = (kh - a.K / 2) * HP + (kw - a.K / 2) + G;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = (kk << 2) + (lane >> 4);
+      bf16x8 xf[MB], wf[NB];
+#pragma unroll
+      for (int j = 0; j < MB; ++j) {
+        const int row = qrel[j] + toff - G;  // halo row of (pixel, tap)
+        xf[j] = *(const bf16x8*)(hb + row * 128 + ((ch ^ ((row >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wf[i] = *(const bf16x8*)(wb + wrow0 + i * 16 * 128 + ((ch ^ swzw) << 4));
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    wait_vmcnt0();
+    __syncthreads();
+    t = tn;
+    c = cn;
+  }
+  ep.store(a, acc, ep_mrow);
+}
+
+// largest halo span (rows) of any 256-pixel tile, cached per geometry
+static int halo2_rows_needed(int M, int S, int HPi, int K, int offi) {
+  static int cM = -1, cS = -1, cH = -1, cK = -1, cO = -1, cR = 0;
+  if (M == cM && S == cS && HPi == cH && K == cK && offi == cO) return cR;
+  const int SS = S * S, Pc = offi + K / 2, G = (K / 2) * (HPi + 1);
+  auto q = [&](int m) {
+    const int b = m / SS, rem = m % SS;
+    return (b * HPi + rem / S + Pc) * HPi + rem % S + Pc;
+  };
+  int worst = 0;
+  // tiles start at multiples of 256; their offsets within a board repeat with period lcm(256, SS)
+  const int period_tiles = SS / std::__gcd(SS, H2_BM);
+  const int ntiles = (M + H2_BM - 1) / H2_BM;
+  for (int k = 0; k < ntiles && k < period_tiles + 2; ++k) {
+    const int m0 = k * H2_BM, m1 = std::min(m0 + H2_BM - 1, M - 1);
+    worst = std::max(worst, q(m1) - q(m0) + 2 * G + 1);
+  }
+  cM = M; cS = S; cH = HPi; cK = K; cO = offi; cR = worst;
+  return worst;
+}
+
+template <int BN, int MODE>
+static void launch_fwd_halo2(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int smem = 2 * H2_ROWS * 128 + 2 * BN * 128;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_halo2_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);
+    attr = true;
+  }
+  dim3 grid((a.M + H2_BM - 1) / H2_BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_halo2_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
 }
 
 template <int BN, int MODE>
@@ -616,12 +813,23 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     return;
   }
   int bm = g_fwd_bm;
-  if (bm <= 0) bm = (a.M >= 256 * 512) ? 256 : 128;
+  if (bm == 2) {  // interior-halo kernel when the tile's halo fits
+    if (halo2_rows_needed(a.M, a.S, a.HPi, a.K, a.offi) <= H2_ROWS && BN <= 192) {
+      launch_fwd_halo2<BN, MODE>(a, st);
+      return;
+    }
+    bm = 0;
+  }
+  // forward: 96x96-per-wave tiles (147 KB LDS).  dgrad keeps the 112-KB tile:
+  // it runs concurrently with wgrad (48 KB) on the other stream and the two
+  // only share a CU when their LDS fits together.
+  if (bm <= 0) bm = (MODE != MODE_MASK && a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
   // tile codes: 128 / 256 (64-pixel waves), 2568 (BM 256, 128-pixel waves: 4 waves, 1 per SIMD)
   if (bm == 32) launch_fwd_ring<BN, MODE>(a, st);
   else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
   else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);  // epilogue loads after the loop
   else if (bm == 2568) launch_fwd_bm<BN, MODE, 256, 8>(a, st);
+  else if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);  // 96x96 per wave, 147 KB LDS
   else launch_fwd_bm<BN, MODE, 128, 4>(a, st);
 }
 

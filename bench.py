@@ -34,8 +34,8 @@ PAPER_SL_POS_PER_S = 3000.0  # paper SL throughput, 50 GPUs agg
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1024, help="per-GPU minibatch (boards)")
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--layers", type=int, default=12)
@@ -52,6 +52,10 @@ def main():
 
     env = agdist.init_from_env()
     dev = env.device
+    if os.environ.get("ALPHAGO_AMD_CONV_TILE") and dev.type == "cuda":  # kernel A/B experiments
+        from alphago_amd import ops as _ops
+        _ops.load()
+        torch.ops.alphago_amd.set_conv_tile(int(os.environ["ALPHAGO_AMD_CONV_TILE"]))
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
     kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap, "precision": args.precision}

@@ -184,7 +184,7 @@ def test_sgd_update(ops, cuda_device):
     assert torch.allclose(p, ref)
 
 
-@pytest.mark.parametrize("tile", [128, 256, 2568, -1, 32])
+@pytest.mark.parametrize("tile", [128, 256, 2568, -1, 32, 2, 384])
 def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     """Every forward tiling (gather 128/256, 128-pixel waves, halo) on a batch
     whose pixel count is not a multiple of any tile."""
@@ -208,7 +208,7 @@ def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", [32, 256])
+@pytest.mark.parametrize("tile", [32, 256, 2, 384])
 def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
     """Layer-1 geometry (Cin 64, 5x5, input pad 2) and the masked dgrad mode on each tiling."""
     torch.manual_seed(2)
