@@ -37,35 +37,77 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   return r;
 }
 
+// z_s[p] = y[p, :] . w for every position of one board, coalesced: thread
+// (r, c8) reads 16 B of position p = r + k R (consecutive threads read
+// consecutive channel groups of one 384-B row) and adds its 8-term partial dot
+// product into z_s[p] with an LDS float atomic.
+__device__ __forceinline__ void head_dots(const __bf16* base, const float* w_s, float* z_s, int S, int C) {
+  const int tid = threadIdx.x;
+  const int SS = S * S;
+  const int HP = S + 2;
+  const int C8 = C >> 3;
+  for (int p = tid; p < SS; p += blockDim.x) z_s[p] = 0.f;
+  __syncthreads();
+  const int R = blockDim.x / C8;
+  const int r = tid / C8, cg = tid - r * C8;
+  if (r < R) {
+    const int c8 = cg << 3;
+    for (int p = r; p < SS; p += R) {
+      const int i = p / S, j = p - (p / S) * S;
+      const bf16x8 v = *(const bf16x8*)(base + (size_t)((i + 1) * HP + j + 1) * C + c8);
+      float d = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d += (float)v[e] * w_s[c8 + e];
+      atomicAdd(&z_s[p], d);
+    }
+  }
+  __syncthreads();
+}
+
 // Gradient of a 1x1 (F -> 1) head conv given dlogits g (in g_s, length S*S):
 // ReLU'-masked dY into the trunk's last activation and per-board partials of
 // dW_head (the dbias partial is written by the caller).
 __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int b, const __bf16* base,
                                                     const float* w_s, const float* g_s) {
+  // One pass over the board's activations: thread (r, c8) walks positions
+  // p = r, r + R, ... for its 8-channel group, writing the ReLU'-masked dY and
+  // accumulating sum_p g[p] * y[p, c] in registers; the R partials per
+  // channel are then reduced through LDS.  Consecutive threads cover
+  // consecutive 16-B channel groups of one position (coalesced rows).
+  __shared__ float part[256 * 8];
   const int tid = threadIdx.x;
   const int SS = a.S * a.S;
   const int HP = a.S + 2;
   const int C8 = a.C >> 3;
+  const int R = blockDim.x / C8;  // positions processed concurrently
+  const int r = tid / C8, cg = tid - r * C8;
   __bf16* dzb = a.dz + (size_t)b * HP * HP * a.C;
-  for (int idx = tid; idx < SS * C8; idx += blockDim.x) {
-    const int p = idx / C8;
-    const int c8 = (idx - p * C8) << 3;
-    const int i = p / a.S, j = p - (p / a.S) * a.S;
-    const size_t off = (size_t)((i + 1) * HP + j + 1) * a.C + c8;
-    const bf16x8 v = *(const bf16x8*)(base + off);
-    const float g = g_s[p];
-    bf16x8 o;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (r < R) {
+    const int c8 = cg << 3;
+    for (int p = r; p < SS; p += R) {
+      const int i = p / a.S, j = p - (p / a.S) * a.S;
+      const size_t off = (size_t)((i + 1) * HP + j + 1) * a.C + c8;
+      const bf16x8 v = *(const bf16x8*)(base + off);
+      const float g = g_s[p];
+      bf16x8 o;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = (__bf16)((float)v[e] > 0.f ? g * w_s[c8 + e] : 0.f);
-    *(bf16x8*)(dzb + off) = o;
+      for (int e = 0; e < 8; ++e) {
+        const float y = (float)v[e];
+        o[e] = (__bf16)(y > 0.f ? g * w_s[c8 + e] : 0.f);
+        acc[e] += g * y;
+      }
+      *(bf16x8*)(dzb + off) = o;
+    }
   }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[tid * 8 + e] = acc[e];
+  __syncthreads();
   float* dh = a.dhead + (size_t)b * (a.C_real + 1);
   for (int c = tid; c < a.C_real; c += blockDim.x) {
+    const int g8 = c >> 3, e = c & 7;
     float s = 0.f;
-    for (int p = 0; p < SS; ++p) {
-      const int i = p / a.S, j = p - (p / a.S) * a.S;
-      s += g_s[p] * (float)base[(size_t)((i + 1) * HP + j + 1) * a.C + c];
-    }
+    for (int rr = 0; rr < R; ++rr) s += part[(rr * C8 + g8) * 8 + e];
     dh[c] = s;
   }
 }
@@ -88,16 +130,9 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
 
   float lmax = -INFINITY;
   int lidx = 0x7fffffff;
+  head_dots(base, w_s, z_s, a.S, a.C);
   for (int p = tid; p < SS; p += 256) {
-    const int i = p / a.S, j = p - (p / a.S) * a.S;
-    const __bf16* row = base + (size_t)((i + 1) * HP + j + 1) * a.C;
-    float dot = 0.f;
-    for (int c8 = 0; c8 < a.C; c8 += 8) {
-      const bf16x8 v = *(const bf16x8*)(row + c8);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dot += (float)v[e] * w_s[c8 + e];
-    }
-    float z = (dot + bias) * a.inv_temp;
+    float z = (z_s[p] + bias) * a.inv_temp;
     if (legal && !legal[p]) z = -INFINITY;
     z_s[p] = z;
     if (z > lmax) {  // first max wins (p increases within a thread)
@@ -177,19 +212,11 @@ __global__ __launch_bounds__(256) void head_logits_kernel(PolicyHeadArgs a) {
   const int HP = a.S + 2;
   for (int c = tid; c < a.C; c += 256) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
   __syncthreads();
+  __shared__ float z_s[368];
   const __bf16* base = a.y + (size_t)b * HP * HP * a.C;
   const float bias = a.b[0];
-  for (int p = tid; p < SS; p += 256) {
-    const int i = p / a.S, j = p - (p / a.S) * a.S;
-    const __bf16* row = base + (size_t)((i + 1) * HP + j + 1) * a.C;
-    float dot = 0.f;
-    for (int c8 = 0; c8 < a.C; c8 += 8) {
-      const bf16x8 v = *(const bf16x8*)(row + c8);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dot += (float)v[e] * w_s[c8 + e];
-    }
-    a.probs[(size_t)b * SS + p] = dot + bias;  // probs slot carries the logits
-  }
+  head_dots(base, w_s, z_s, a.S, a.C);
+  for (int p = tid; p < SS; p += 256) a.probs[(size_t)b * SS + p] = z_s[p] + bias;  // probs slot carries the logits
 }
 
 // Head backward from an externally computed dlogits (value net: dz = dh W1^T).

@@ -69,5 +69,11 @@ am = ops.fp8_amax_buffer(1, dev)[0]
 res["fp8_fwd3x3_amax"] = timeit(lambda: ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8, amax=am))
 res["fp8_fwd3x3_dual"] = timeit(lambda: ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8, y_bf16=y, amax=am))
 res["fp8_fwd5x5"] = timeit(lambda: ops.conv_fwd_fp8(x08, w18, bias, sc, osc, 5, S, 2, 1, y_fp8=y8))
+# fused policy head (train) on the last activation
+hw = torch.randn(F, device=dev) * 0.05; hb = torch.zeros(1, device=dev)
+tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=dev)
+dz = ops.padded_empty(B, S, 1, F, dev); lo = torch.zeros(B, device=dev); co = torch.zeros(B, device=dev)
+dh = torch.zeros(B, F + 1, device=dev)
+res["policy_head_train"] = timeit(lambda: ops.policy_head_train(x, hw, hb, tgt, dz, lo, co, dh, S, 1.0 / B))
 out = {k: {"us": round(v, 1), "TF": round((fl1 if "5x5" in k else fl3) / (v * 1e-6) / 1e12, 1) if "reduce" not in k else None} for k, v in res.items()}
 print(json.dumps({"batch": B, "F": F, **out}))
