@@ -37,29 +37,30 @@ __device__ __forceinline__ float block_reduce_sum(float v, float* red) {
   return r;
 }
 
-// z_s[p] = y[p, :] . w for every position of one board, coalesced: thread
-// (r, c8) reads 16 B of position p = r + k R (consecutive threads read
-// consecutive channel groups of one 384-B row) and adds its 8-term partial dot
-// product into z_s[p] with an LDS float atomic.
+// z_s[p] = y[p, :] . w for every position of one board, coalesced and
+// deterministic: each 32-lane half-wave owns one position at a time, lane c8
+// (< C/8) reads 16 B of the position's row (one contiguous row per half-wave)
+// and the 8-term partial dot products are summed with a fixed xor-shuffle tree.
 __device__ __forceinline__ void head_dots(const __bf16* base, const float* w_s, float* z_s, int S, int C) {
   const int tid = threadIdx.x;
   const int SS = S * S;
   const int HP = S + 2;
-  const int C8 = C >> 3;
-  for (int p = tid; p < SS; p += blockDim.x) z_s[p] = 0.f;
-  __syncthreads();
-  const int R = blockDim.x / C8;
-  const int r = tid / C8, cg = tid - r * C8;
-  if (r < R) {
-    const int c8 = cg << 3;
-    for (int p = r; p < SS; p += R) {
+  const int C8 = C >> 3;  // <= 32
+  const int R = blockDim.x >> 5;
+  const int l32 = tid & 31, slot = tid >> 5;
+  const int c8 = l32 << 3;
+  for (int p0 = 0; p0 < SS; p0 += R) {
+    const int p = p0 + slot;
+    float d = 0.f;
+    if (p < SS && l32 < C8) {
       const int i = p / S, j = p - (p / S) * S;
       const bf16x8 v = *(const bf16x8*)(base + (size_t)((i + 1) * HP + j + 1) * C + c8);
-      float d = 0.f;
 #pragma unroll
       for (int e = 0; e < 8; ++e) d += (float)v[e] * w_s[c8 + e];
-      atomicAdd(&z_s[p], d);
     }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    if (l32 == 0 && p < SS) z_s[p] = d;
   }
   __syncthreads();
 }
