@@ -45,11 +45,20 @@ namespace agk {
 template <int NB, int MB, int MODE>
 struct ConvEpilogue {
   int ooff[MB];
+  int pix[MB];
   f32x4 bb[NB];
   bf16x4 mk[NB][MB];
+  uint32_t mw[MB];
+  int mslot, mwords;
 
-  __device__ __forceinline__ void load(const ConvFwdArgs& a, int mrow, int nbase) {
+  // ReLU' bitmask layout: per padded pixel, (Cout/BN)*8 32-bit words; word
+  // (blockIdx.y*8 + wn*4 + lane/16) holds bit 4i+r for channel nbase+16i+r —
+  // exactly the channels one lane owns, so producer and consumer never
+  // exchange data (12x less traffic than re-reading the bf16 activation).
+  __device__ __forceinline__ void load(const ConvFwdArgs& a, int mrow, int nbase, int wn = 0) {
     const int SS = a.S * a.S;
+    mslot = blockIdx.y * 8 + wn * 4 + ((threadIdx.x & 63) >> 4);
+    mwords = gridDim.y * 8;
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
       int m = mrow + j * 16;
@@ -58,7 +67,8 @@ struct ConvEpilogue {
       const int rem = m - b * SS;
       const int ii = fdiv(rem, a.divS);
       const int jj = rem - ii * a.S;
-      ooff[j] = ((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout + nbase;
+      pix[j] = (b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po;
+      ooff[j] = pix[j] * a.Cout + nbase;
     }
     if constexpr (MODE == MODE_BIAS_RELU) {
 #pragma unroll
@@ -68,6 +78,9 @@ struct ConvEpilogue {
       for (int j = 0; j < MB; ++j)
 #pragma unroll
         for (int i = 0; i < NB; ++i) mk[i][j] = *(const bf16x4*)(a.mask + ooff[j] + i * 16);
+    } else if constexpr (MODE == MODE_MASKBITS) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j) mw[j] = a.mbits_in[(size_t)pix[j] * mwords + mslot];
     }
   }
 
@@ -75,6 +88,7 @@ struct ConvEpilogue {
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
       if (mrow + j * 16 >= a.M) continue;
+      uint32_t bits = 0u;
 #pragma unroll
       for (int i = 0; i < NB; ++i) {
         f32x4 v = acc[i][j];
@@ -88,23 +102,33 @@ struct ConvEpilogue {
           v[1] = (float)mk[i][j][1] > 0.f ? v[1] : 0.f;
           v[2] = (float)mk[i][j][2] > 0.f ? v[2] : 0.f;
           v[3] = (float)mk[i][j][3] > 0.f ? v[3] : 0.f;
+        } else if constexpr (MODE == MODE_MASKBITS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = ((mw[j] >> (4 * i + r)) & 1u) ? v[r] : 0.f;
         }
         bf16x4 o;
         o[0] = (__bf16)v[0];
         o[1] = (__bf16)v[1];
         o[2] = (__bf16)v[2];
         o[3] = (__bf16)v[3];
+        if constexpr (MODE == MODE_BIAS_RELU) {
+          // the bit records what the bf16 value the dgrad would re-read says: y > 0
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bits |= ((float)o[r] > 0.f ? 1u : 0u) << (4 * i + r);
+        }
         *(bf16x4*)(a.y + ooff[j] + i * 16) = o;
       }
+      if constexpr (MODE == MODE_BIAS_RELU)
+        if (a.mbits_out) a.mbits_out[(size_t)pix[j] * mwords + mslot] = bits;
     }
   }
 };
 
 template <int NB, int MB, int MODE>
 __device__ __forceinline__ void conv_store_tile(const ConvFwdArgs& a, const f32x4 (&acc)[NB][MB], int mrow,
-                                                int nbase) {
+                                                int nbase, int wn) {
   ConvEpilogue<NB, MB, MODE> ep;
-  ep.load(a, mrow, nbase);
+  ep.load(a, mrow, nbase, wn);
   ep.store(a, acc, mrow);
 }
 
@@ -231,7 +255,7 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
       wait_vmcnt0();
       __syncthreads();
     }
-    ep.load(a, ep_mrow, ep_nbase);
+    ep.load(a, ep_mrow, ep_nbase, wn);
     ep.store(a, acc, ep_mrow);
     return;
   }
@@ -240,7 +264,7 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     const int cur = ks & 1;
     const char* base = smem + cur * STAGE;
     if (ks + 1 < nK) stage(cur ^ 1);
-    if (ks == ep_at) ep.load(a, ep_mrow, ep_nbase);  // epilogue operands ride along with the last stages
+    if (ks == ep_at) ep.load(a, ep_mrow, ep_nbase, wn);  // epilogue operands ride along with the last stages
     read_frags(base, 1, xb, wb);
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -580,7 +604,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_ring_kernel(ConvFwdArgs a) {
   if (ks < nK) step(ks, xa, wa, xb, wb);
 
   // --- epilogue
-  conv_store_tile<NB, MB, MODE>(a, acc, m0 + wm * 64 + (lane & 15), n0 + wn * (BN / 2) + ((lane >> 4) << 2));
+  conv_store_tile<NB, MB, MODE>(a, acc, m0 + wm * 64 + (lane & 15), n0 + wn * (BN / 2) + ((lane >> 4) << 2), wn);
 }
 
 template <int BN, int MODE>
@@ -739,7 +763,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_halo2_kernel(ConvFwdArgs a) {
     const int cn = (t + 1 == T) ? c + 1 : c;
     if (ks + 1 < nK) stage_w(tn, cn, (ks + 1) & 1);
     if (t == 0 && c + 1 < CC) stage_halo(c + 1, (c + 1) & 1);
-    if (ks == (nK > 2 ? nK - 2 : 0)) ep.load(a, ep_mrow, ep_nbase);
+    if (ks == (nK > 2 ? nK - 2 : 0)) ep.load(a, ep_mrow, ep_nbase, wn);
     const char* hb = hbuf + (c & 1) * H_BYTES;
     const char* wb = wbuf + (ks & 1) * W_BYTES;
     const int kh = t / a.K, kw = t - (t / a.K) * a.K;
@@ -808,7 +832,7 @@ template <int BN, int MODE>
 static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   const bool halo_ok = a.K == 3 && a.HPi == a.HPo && a.offi == 0 && a.Po == 1 && a.HPo + 1 <= 32 &&
                        (a.S + 2) * (a.S + 2) * 0 + 256 + 2 * (a.HPo + 1) <= HALO_ROWS;
-  if (halo_ok && g_fwd_bm == -1) {  // opt-in: slower at S=19 (18% border work), see profiles/
+  if (halo_ok && g_fwd_bm == -1 && !a.mbits_out && MODE != MODE_MASKBITS) {  // opt-in: slower at S=19 (18% border work), see profiles/
     launch_fwd_halo<BN, MODE>(a, st);
     return;
   }
@@ -823,7 +847,8 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // forward: 96x96-per-wave tiles (147 KB LDS).  dgrad keeps the 112-KB tile:
   // it runs concurrently with wgrad (48 KB) on the other stream and the two
   // only share a CU when their LDS fits together.
-  if (bm <= 0) bm = (MODE != MODE_MASK && a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
+  if (bm <= 0)
+    bm = (MODE != MODE_MASK && MODE != MODE_MASKBITS && a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
   // tile codes: 128 / 256 (64-pixel waves), 2568 (BM 256, 128-pixel waves: 4 waves, 1 per SIMD)
   if (bm == 32) launch_fwd_ring<BN, MODE>(a, st);
   else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
@@ -848,6 +873,7 @@ void launch_conv_fwd(const ConvFwdArgs& a_in, int mode, hipStream_t st) {
   a.divS = make_fastdiv((uint32_t)a.S);
   if (mode == MODE_BIAS_RELU) launch_fwd_mode<MODE_BIAS_RELU>(a, st);
   else if (mode == MODE_MASK) launch_fwd_mode<MODE_MASK>(a, st);
+  else if (mode == MODE_MASKBITS) launch_fwd_mode<MODE_MASKBITS>(a, st);
   else launch_fwd_mode<MODE_NONE>(a, st);
 }
 

@@ -7,7 +7,7 @@
 
 namespace agk {
 
-enum { MODE_BIAS_RELU = 0, MODE_MASK = 1, MODE_NONE = 2 };
+enum { MODE_BIAS_RELU = 0, MODE_MASK = 1, MODE_NONE = 2, MODE_MASKBITS = 3 };
 
 struct ConvFwdArgs {
   const __bf16* x;     // padded NHWC input
@@ -15,6 +15,8 @@ struct ConvFwdArgs {
   const float* bias;   // [Cout]           (MODE_BIAS_RELU)
   const __bf16* mask;  // layout of y      (MODE_MASK: keep where mask > 0)
   __bf16* y;           // padded NHWC output (interior written, borders untouched)
+  uint32_t* mbits_out;       // MODE_BIAS_RELU: optional ReLU'(y) bitmask, (Cout/BN)*8 words per padded pixel
+  const uint32_t* mbits_in;  // MODE_MASKBITS: the bitmask written by the layer's forward
   int M, S, Cin, Cout, K;
   int HPi, offi;       // input padded side, (input pad - K/2)
   int HPo, Po;         // output padded side and pad

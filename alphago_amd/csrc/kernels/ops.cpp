@@ -23,7 +23,8 @@ __bf16* bfp_mut(const Tensor& t) { return reinterpret_cast<__bf16*>(t.data_ptr()
 
 // x: (B, HPi, HPi, Cin) bf16; w: (T, Cout, Cin) bf16; y: (B, HPo, HPo, Cout) bf16
 void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const c10::optional<Tensor>& mask,
-              const Tensor& y, int64_t K, int64_t S, int64_t Pin, int64_t Po, int64_t mode) {
+              const Tensor& y, int64_t K, int64_t S, int64_t Pin, int64_t Po, int64_t mode,
+              const c10::optional<Tensor>& mbits) {
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
   CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
   CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y);
@@ -53,6 +54,15 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
     TORCH_CHECK(mask->sizes() == y.sizes(), "mask must match y");
     a.mask = bfp(*mask);
   }
+  if (mbits.has_value()) {
+    TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
+    const int64_t words = (Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
+    TORCH_CHECK(mbits->numel() >= B * HPo * HPo * words, "mbits too small: need B*HPo*HPo*words");
+    TORCH_CHECK(mode == agk::MODE_BIAS_RELU || mode == agk::MODE_MASKBITS, "mbits with modes 0 (write) / 3 (read)");
+    if (mode == agk::MODE_BIAS_RELU) a.mbits_out = reinterpret_cast<uint32_t*>(mbits->data_ptr<int>());
+    else a.mbits_in = reinterpret_cast<const uint32_t*>(mbits->data_ptr<int>());
+  }
+  TORCH_CHECK(mode != agk::MODE_MASKBITS || a.mbits_in, "mode 3 needs mbits");
   if (a.M == 0) return;
   agk::launch_conv_fwd(a, (int)mode, cur_stream());
 }
@@ -411,7 +421,9 @@ void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
 }  // namespace
 
 TORCH_LIBRARY(alphago_amd, m) {
-  m.def("conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode) -> ()");
+  m.def(
+      "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
+      "Tensor(b!)? mbits=None) -> ()");
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def(

@@ -22,7 +22,7 @@ from .. import _build
 _lock = threading.Lock()
 _loaded = False
 
-MODE_BIAS_RELU, MODE_MASK, MODE_NONE = 0, 1, 2
+MODE_BIAS_RELU, MODE_MASK, MODE_NONE, MODE_MASKBITS = 0, 1, 2, 3
 
 
 def library_path() -> str:
@@ -82,9 +82,18 @@ def from_padded(y: torch.Tensor, P: int, C: Optional[int] = None) -> torch.Tenso
 
 
 # ----------------------------------------------------------------- op wrappers
-def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: int = MODE_BIAS_RELU, mask=None):
-    _ops().conv_fwd(x, w_packed, bias, mask, y, K, S, Pin, Po, mode)
+def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: int = MODE_BIAS_RELU, mask=None,
+             mbits=None):
+    """Conv + epilogue.  mode 0: bias + ReLU (mbits: also write the ReLU' bitmask);
+    1: dgrad masked by ``mask`` > 0; 3: dgrad masked by the ``mbits`` bitmask."""
+    _ops().conv_fwd(x, w_packed, bias, mask, y, K, S, Pin, Po, mode, mbits)
     return y
+
+
+def mbits_words(cout_p: int) -> int:
+    """32-bit ReLU'-bitmask words per padded pixel for a conv with cout_p output channels."""
+    bn = 192 if cout_p % 192 == 0 else 128 if cout_p % 128 == 0 else 64
+    return cout_p // bn * 8
 
 
 def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1):

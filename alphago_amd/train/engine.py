@@ -163,6 +163,10 @@ class HipConvTrainer:
         self.X0 = ops.padded_empty(B, S, self.P0, self.C0p, dev)
         self.Y = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(self.L)]
         self.DZ = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(self.L)]
+        # ReLU' bitmasks of Y[0..L-2], written by the forward epilogue and read
+        # by the dgrad epilogue instead of the bf16 activations (12x fewer bytes)
+        hw = B * (S + 2) * (S + 2) * ops.mbits_words(self.Fp)
+        self.MBITS = [torch.zeros(hw, dtype=torch.int32, device=dev) for _ in range(self.L - 1)]
         self.loss = torch.zeros(B, device=dev)
         self.correct = torch.zeros(B, device=dev)
         M = B * S * S
@@ -247,7 +251,8 @@ class HipConvTrainer:
             return
         for l in range(self.L):
             x, pin = self._layer_in(l)
-            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1)
+            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1,
+                         mbits=self.MBITS[l] if l < self.L - 1 else None)
 
     def _forward_fp8(self) -> None:
         ops.quantize_fp8(self.X0, self.X08, 0)  # binary planes: exact
@@ -301,8 +306,12 @@ class HipConvTrainer:
                 if l in self._bucket_after_layer:
                     self.reducer.launch(self._bucket_after_layer[l])
             if l > 0:
-                ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
-                             mode=ops.MODE_MASK, mask=self.Y[l - 1])
+                if self.precision == "fp8":  # the fp8 forward does not write bitmasks
+                    ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
+                                 mode=ops.MODE_MASK, mask=self.Y[l - 1])
+                else:
+                    ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
+                                 mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1])
         if self.s_w is not None:
             main.wait_stream(self.s_w)
         self.reducer.wait()

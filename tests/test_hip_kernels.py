@@ -270,3 +270,34 @@ def test_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B):
     assert _rel_err(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1].permute(0, 3, 1, 2), ref) < 0.07
     assert abs(amax.view(torch.float32).max().item() - ref.max().item()) <= 1e-2 * ref.max().item()
     assert y8[:, 0].sum() == 0 and yb[:, :, -1].abs().sum() == 0
+
+
+@pytest.mark.parametrize("tile", [0, 128, 256, 384, 32, 2])
+@pytest.mark.parametrize("C", [192, 128])
+def test_relu_bitmask_dgrad_matches_mask(ops, cuda_device, tile, C):
+    """Forward writes the ReLU' bitmask; dgrad mode 3 (bitmask) == mode 1 (bf16 activation mask)."""
+    torch.manual_seed(4)
+    B, S = 6, 19
+    x = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w = _bf(torch.randn(C, C, 3, 3, device=cuda_device) * 0.05)
+    b = torch.randn(C, device=cuda_device) * 0.1
+    wf = ops.packed_weight_like(w, C, C)
+    wd = ops.packed_weight_like(w, C, C, True)
+    ops.pack_weights([w.contiguous()], [wf], [wd])
+    xp = ops.to_padded(x, 1)
+    y = ops.padded_empty(B, S, 1, C, cuda_device)
+    mb = torch.full((B * (S + 2) ** 2 * ops.mbits_words(C),), -1, dtype=torch.int32, device=cuda_device)
+    g = ops.to_padded(_bf(torch.randn(B, C, S, S, device=cuda_device)), 1)
+    d1 = ops.padded_empty(B, S, 1, C, cuda_device)
+    d3 = ops.padded_empty(B, S, 1, C, cuda_device)
+    try:
+        torch.ops.alphago_amd.set_conv_tile(tile)
+        ops.conv_fwd(xp, wf, b, y, 3, S, 1, 1, mbits=mb)
+        ops.conv_fwd(g, wd, None, d1, 3, S, 1, 1, mode=ops.MODE_MASK, mask=y)
+        ops.conv_fwd(g, wd, None, d3, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb)
+        torch.cuda.synchronize()
+    finally:
+        torch.ops.alphago_amd.set_conv_tile(0)
+    assert _rel_err(ops.from_padded(y, 1), F.relu(F.conv2d(x, w, b, padding=1))) < 1e-2
+    assert torch.equal(d1, d3)
+    assert (ops.from_padded(d3, 1) != 0).any()
