@@ -928,7 +928,13 @@ __device__ __forceinline__ bf16x4 ds_read_tr16_asm(const char* p) {
 // 512 threads = 8 waves as 2 (n) x 4 (c).  One pipeline stage = KSUB sub-steps
 // of 32 pixels (one barrier per KSUB*32 pixels); each sub-step region is laid
 // out [16-channel block][32 px][16 ch] for the transpose reads.
-template <int WN, int WC, int KSUB, int NWC = 4>
+//
+// TAPS > 1 (tap-merged, used when the c tile is 64 wide, i.e. the thin first
+// layer): one workgroup owns a whole kernel row (TAPS == K taps, kw = 0..K-1)
+// and reuses each staged dz tile for all of them; the x image of tap kw is the
+// tap-0 image shifted by kw columns (kw * Cin elements).  This triples (5x5:
+// quintuples) the MFMAs per staged dz byte, the limiter of the 64-wide tile.
+template <int WN, int WC, int KSUB, int NWC = 4, int TAPS = 1>
 __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
   // 2 (n) x NWC (c) waves; NWC = 2 gives each wave a 96x96 tile at 192x192
   // (a third fewer LDS fragment reads per MFMA than NWC = 4)
@@ -936,10 +942,11 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
   constexpr int NBn = WN / 32;          // n blocks per wave (wave covers WN/2)
   constexpr int NBc = WC / (16 * NWC);  // c blocks per wave (wave covers WC/NWC)
   constexpr int DZ_BYTES = WN * 64;  // [WN/16][32 px][16 ch] bf16
-  constexpr int X_BYTES = WC * 64;
+  constexpr int X_BYTES = WC * 64 * TAPS;  // [TAPS][WC/16][32 px][16 ch]
   constexpr int SUB = DZ_BYTES + X_BYTES;
   constexpr int STAGE = SUB * KSUB;
-  constexpr int NINSTR = (WN + WC) / 16 * KSUB;  // 1 KB glds pieces per stage
+  constexpr int XP = WC / 16;  // x pieces per tap
+  constexpr int NINSTR = (WN / 16 + XP * TAPS) * KSUB;  // 1 KB glds pieces per stage
   constexpr int IPW = (NINSTR + NWAVES - 1) / NWAVES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -947,7 +954,7 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
   const int wave = wave_id();
   const int wn = wave / NWC, wc = wave % NWC;
   const int split = blockIdx.x;
-  const int t = blockIdx.y;
+  const int t = blockIdx.y * TAPS;  // first tap of the group
   const int ncb = a.Cin / WC;
   const int n0 = (blockIdx.z / ncb) * WN;
   const int c0 = (blockIdx.z % ncb) * WC;
@@ -984,22 +991,27 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
       const __bf16* xsrc = a.x + xr[sub] + half;
 #pragma unroll
       for (int i = 0; i < IPW; ++i) {
-        const int jj = wave * IPW + i - sub * ((WN + WC) / 16);
+        const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
         if (jj >= 0 && jj < WN / 16) glds16(dsrc + jj * 16, base + sub * SUB + jj * 1024);
       }
 #pragma unroll
       for (int i = 0; i < IPW; ++i) {
-        const int jj = wave * IPW + i - sub * ((WN + WC) / 16);
-        if (jj >= WN / 16 && jj < (WN + WC) / 16) glds16(xsrc + (jj - WN / 16) * 16, base + sub * SUB + jj * 1024);
+        const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
+        if (jj >= WN / 16 && jj < NINSTR / KSUB) {
+          const int xj = jj - WN / 16;  // tap xj / XP, channel piece xj % XP
+          glds16(xsrc + (xj / XP) * a.Cin + (xj % XP) * 16, base + sub * SUB + jj * 1024);
+        }
       }
     }
   };
 
-  f32x4 acc[NBn][NBc];
+  f32x4 acc[TAPS][NBn][NBc];
 #pragma unroll
-  for (int i = 0; i < NBn; ++i)
+  for (int tp = 0; tp < TAPS; ++tp)
 #pragma unroll
-    for (int j = 0; j < NBc; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NBn; ++i)
+#pragma unroll
+      for (int j = 0; j < NBc; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float dbs[NBn];
 #pragma unroll
   for (int i = 0; i < NBn; ++i) dbs[i] = 0.f;
@@ -1011,6 +1023,7 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
   const int p = lane & 3;
   const int tr0 = (4 * g + q) * 32 + p * 8;         // rows 4g..4g+3
   const int tr1 = (16 + 4 * g + q) * 32 + p * 8;    // rows 16+4g..16+4g+3
+  constexpr int NF = NBn + TAPS * NBc;  // fragments read per sub-step
 
   if (ks_begin < ks_end) {
     stage(ks_begin, 0);
@@ -1023,7 +1036,7 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
 #pragma unroll
     for (int sub = 0; sub < KSUB; ++sub) {
       const char* base = smem + cur * STAGE + sub * SUB;
-      bf16x4 tl[NBn + NBc], th[NBn + NBc];
+      bf16x4 tl[NF], th[NF];
 #pragma unroll
       for (int i = 0; i < NBn; ++i) {
         const char* cb = base + (wn * NBn + i) * 1024;
@@ -1031,24 +1044,29 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
         th[i] = ds_read_tr16_asm(cb + tr1);
       }
 #pragma unroll
-      for (int j = 0; j < NBc; ++j) {
-        const char* cb = base + DZ_BYTES + (wc * NBc + j) * 1024;
-        tl[NBn + j] = ds_read_tr16_asm(cb + tr0);
-        th[NBn + j] = ds_read_tr16_asm(cb + tr1);
-      }
-      lgkm_fence<NBn + NBc>(tl, th);
-      bf16x8 af[NBn], bfm[NBc];
+      for (int tp = 0; tp < TAPS; ++tp)
+#pragma unroll
+        for (int j = 0; j < NBc; ++j) {
+          const char* cb = base + DZ_BYTES + (tp * XP + wc * NBc + j) * 1024;
+          tl[NBn + tp * NBc + j] = ds_read_tr16_asm(cb + tr0);
+          th[NBn + tp * NBc + j] = ds_read_tr16_asm(cb + tr1);
+        }
+      lgkm_fence<NF>(tl, th);
+      bf16x8 af[NBn], bfm[TAPS * NBc];
 #pragma unroll
       for (int i = 0; i < NBn; ++i)
         af[i] = bf16x8{tl[i][0], tl[i][1], tl[i][2], tl[i][3], th[i][0], th[i][1], th[i][2], th[i][3]};
 #pragma unroll
-      for (int j = 0; j < NBc; ++j)
+      for (int j = 0; j < TAPS * NBc; ++j)
         bfm[j] = bf16x8{tl[NBn + j][0], tl[NBn + j][1], tl[NBn + j][2], tl[NBn + j][3],
                         th[NBn + j][0], th[NBn + j][1], th[NBn + j][2], th[NBn + j][3]};
 #pragma unroll
-      for (int i = 0; i < NBn; ++i)
+      for (int tp = 0; tp < TAPS; ++tp)
 #pragma unroll
-        for (int j = 0; j < NBc; ++j) acc[i][j] = mfma16x16x32(af[i], bfm[j], acc[i][j]);
+        for (int i = 0; i < NBn; ++i)
+#pragma unroll
+          for (int j = 0; j < NBc; ++j)
+            acc[tp][i][j] = mfma16x16x32(af[i], bfm[tp * NBc + j], acc[tp][i][j]);
       if (do_bias) {
 #pragma unroll
         for (int i = 0; i < NBn; ++i) {
@@ -1064,18 +1082,21 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
   }
 
   // --- write the split's partial tile: D[n][c], lane owns n..n+3 at column c
-  float* out = a.slab + ((size_t)split * a.T + t) * (size_t)a.Cout * a.Cin;
   const int nb0 = n0 + wn * (WN / 2) + ((lane >> 4) << 2);
   const int cbase = c0 + wc * (WC / NWC) + (lane & 15);
 #pragma unroll
-  for (int i = 0; i < NBn; ++i)
+  for (int tp = 0; tp < TAPS; ++tp) {
+    float* out = a.slab + ((size_t)split * a.T + t + tp) * (size_t)a.Cout * a.Cin;
 #pragma unroll
-    for (int j = 0; j < NBc; ++j) {
-      const int n = nb0 + i * 16;
-      const int c = cbase + j * 16;
+    for (int i = 0; i < NBn; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(size_t)(n + r) * a.Cin + c] = acc[i][j][r];
-    }
+      for (int j = 0; j < NBc; ++j) {
+        const int n = nb0 + i * 16;
+        const int c = cbase + j * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(size_t)(n + r) * a.Cin + c] = acc[tp][i][j][r];
+      }
+  }
   if (do_bias) {
 #pragma unroll
     for (int i = 0; i < NBn; ++i) {
@@ -1266,6 +1287,25 @@ static void launch_wgrad_ring(const ConvWgradArgs& a, dim3 grid, hipStream_t st)
   hipLaunchKernelGGL((conv_wgrad_ring_kernel<WN, WC, NS>), grid, dim3(512), smem, st, a);
 }
 
+template <int WN, int TAPS>
+static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
+  constexpr int smem = 2 * (WN + 64 * TAPS) * 64 * kWgradKsub;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, 64, kWgradKsub, 4, TAPS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  dim3 grid(a.nsplit, a.T / TAPS, (a.Cout / WN) * (a.Cin / 64));
+  hipLaunchKernelGGL((conv_wgrad_kernel<WN, 64, kWgradKsub, 4, TAPS>), grid, dim3(512), smem, st, a);
+}
+
+int wgrad_tap_group(int Cout, int Cin, int K) {
+  const bool c64 = Cin % 192 != 0 && Cin % 128 != 0;
+  (void)Cout;
+  return (c64 && g_wgrad_variant == 0 && (K == 3 || K == 5)) ? K : 1;
+}
+
 template <int WN, int WC>
 static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
   dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
@@ -1285,6 +1325,14 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
     }
     hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS, 2>), grid, dim3(256), smem, st, a);
     return;
+  }
+  if constexpr (WC == 64) {
+    // tap-merged kernel rows (see conv_wgrad_kernel); variant 1 forces one tap per workgroup
+    if (g_wgrad_variant != 1 && (a.K == 3 || a.K == 5)) {
+      if (a.K == 3) launch_wgrad_taps<WN, 3>(a, st);
+      else launch_wgrad_taps<WN, 5>(a, st);
+      return;
+    }
   }
   static bool attr = false;
   if (!attr) {

@@ -113,6 +113,44 @@ __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int
   }
 }
 
+// Reference RL loss (reinforcement_policy_trainer.py:109, Keras 1.0
+// binary_crossentropy on the softmax output): per board
+//   L = -1/SS * sum_j [y_j log pc_j + (1 - y_j) log(1 - pc_j)],  pc = clip(p, 1e-7, 1 - 1e-7)
+// with y the one-hot move; clip has zero gradient outside its range (Theano
+// clip), and the softmax backward is dz_i = p_i (g_i - sum_j p_j g_j).
+__device__ void policy_bce_train(const PolicyHeadArgs& a, int b, int t, float wb, float zmax, float inv, int lidx,
+                                 const __bf16* base, const float* w_s, float* z_s, float* red) {
+  __shared__ float p_s[368];
+  const int tid = threadIdx.x;
+  const int SS = a.S * a.S;
+  const float eps = 1e-7f;
+  float ls = 0.f, pg = 0.f;
+  for (int p = tid; p < SS; p += 256) {
+    const float pr = (z_s[p] == -INFINITY) ? 0.f : __expf(z_s[p] - zmax) * inv;
+    const float pc = fminf(fmaxf(pr, eps), 1.f - eps);
+    const bool y = p == t;
+    ls += y ? __logf(pc) : __logf(1.f - pc);
+    const float g = (pr < eps || pr > 1.f - eps) ? 0.f : -(y ? 1.f / pr : -1.f / (1.f - pr)) / (float)SS;
+    p_s[p] = pr;
+    z_s[p] = g;
+    pg += pr * g;
+  }
+  ls = block_reduce_sum(ls, red);
+  pg = block_reduce_sum(pg, red);
+  if (tid == 0) {
+    a.loss[b] = t >= 0 ? -ls / (float)SS : 0.f;
+    a.correct[b] = (t >= 0 && lidx == t) ? 1.f : 0.f;
+  }
+  const float sc = t >= 0 ? a.grad_scale * wb : 0.f;
+  for (int p = tid; p < SS; p += 256) z_s[p] = p_s[p] * (z_s[p] - pg) * sc;
+  __syncthreads();
+  head_input_backward(a, b, base, w_s, z_s);
+  float gs = 0.f;
+  for (int p = tid; p < SS; p += 256) gs += z_s[p];
+  gs = block_reduce_sum(gs, red);
+  if (tid == 0) a.dhead[(size_t)b * (a.C_real + 1) + a.C_real] = gs;
+}
+
 template <bool TRAIN>
 __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
   __shared__ float w_s[256];
@@ -177,6 +215,10 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
   if constexpr (TRAIN) {
     const int t = a.target[b];
     const float wb = a.weight ? a.weight[b] : 1.f;
+    if (a.loss_kind == 1) {
+      policy_bce_train(a, b, t, wb, zmax, inv, lidx, base, w_s, z_s, red);
+      return;
+    }
     if (tid == 0) {
       if (t >= 0) {
         float pt = __expf(z_s[t] - zmax) * inv;

@@ -58,6 +58,7 @@ struct PolicyHeadArgs {
   int B, S, C, C_real;
   float grad_scale;    // d(mean loss)/d(logit) scale = 1/global_batch
   float inv_temp;
+  int loss_kind;       // 0 = categorical CE (SL / REINFORCE), 1 = reference RL binary CE on the softmax
 };
 
 struct ValueOutArgs {
@@ -136,6 +137,7 @@ void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 void set_conv_fwd_tile(int bm);  // 0 = auto, -1 = halo kernel, 128/256 = gather kernel tile (A/B tests)
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 int wgrad_stage_pixels();
+int wgrad_tap_group(int Cout, int Cin, int K);  // taps per wgrad workgroup (tap-merged 64-wide c tiles)
 void set_wgrad_variant(int v);  // 0 = 2-buffer (default), 3 / 4 = ring with that many LDS slots  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);

@@ -114,7 +114,7 @@ void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& g
 void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::optional<Tensor>& target,
                  const c10::optional<Tensor>& legal, const c10::optional<Tensor>& weight, const c10::optional<Tensor>& dz, const c10::optional<Tensor>& loss,
                  const c10::optional<Tensor>& correct, const c10::optional<Tensor>& dhead,
-                 const c10::optional<Tensor>& probs, int64_t S, double grad_scale, double temperature) {
+                 const c10::optional<Tensor>& probs, int64_t S, double grad_scale, double temperature, int64_t loss_kind) {
   CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(b);
   const int64_t B = y.size(0), C = y.size(3);
   TORCH_CHECK(y.size(1) == S + 2, "head input must have pad 1");
@@ -127,6 +127,8 @@ void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::o
   a.B = (int)B; a.S = (int)S; a.C = (int)C; a.C_real = (int)w.numel();
   a.grad_scale = (float)grad_scale;
   a.inv_temp = (float)(1.0 / temperature);
+  TORCH_CHECK(loss_kind == 0 || loss_kind == 1, "loss_kind must be 0 (CE) or 1 (reference BCE)");
+  a.loss_kind = (int)loss_kind;
   const bool train = target.has_value();
   if (train) {
     TORCH_CHECK(dz && loss && correct && dhead, "training head needs dz, loss, correct, dhead");
@@ -411,6 +413,7 @@ void quantize_fp8(const Tensor& x, const Tensor& y, double scale) {
 
 void set_conv_tile(int64_t bm) { agk::set_conv_fwd_tile((int)bm); }
 void set_wgrad_variant(int64_t v) { agk::set_wgrad_variant((int)v); }
+int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) { return agk::wgrad_tap_group((int)cout, (int)cin, (int)K); }
 
 void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
   CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
@@ -428,7 +431,8 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def(
       "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor? weight, Tensor(a!)? dz, Tensor(b!)? loss, "
-      "Tensor(c!)? correct, Tensor(d!)? dhead, Tensor(e!)? probs, int S, float grad_scale, float temperature) -> ()");
+      "Tensor(c!)? correct, Tensor(d!)? dhead, Tensor(e!)? probs, int S, float grad_scale, float temperature, "
+      "int loss_kind=0) -> ()");
   m.def("head_logits(Tensor y, Tensor w, Tensor b, Tensor(a!) z, int S) -> ()");
   m.def("head_backward(Tensor y, Tensor w, Tensor dlogits, Tensor(a!) dz, Tensor(b!) dhead, int S) -> ()");
   m.def(
@@ -449,6 +453,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
   m.def("set_wgrad_variant(int v) -> ()", &set_wgrad_variant);
+  m.def("wgrad_tap_group(int cout, int cin, int K) -> int", &wgrad_tap_group);
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {

@@ -104,8 +104,12 @@ def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, bet
     _ops().conv_wgrad_reduce(slab, dbslab, grad_w, grad_b, scale, beta)
 
 
-def policy_head_train(y, w, b, target, dz, loss, correct, dhead, S: int, grad_scale: float, weight=None):
-    _ops().policy_head(y, w, b, target, None, weight, dz, loss, correct, dhead, None, S, grad_scale, 1.0)
+def policy_head_train(y, w, b, target, dz, loss, correct, dhead, S: int, grad_scale: float, weight=None,
+                      bce: bool = False):
+    """Fused policy head training step; ``bce`` selects the reference RL loss
+    (binary CE on the softmax, reinforcement_policy_trainer.py:109) instead of CE."""
+    _ops().policy_head(y, w, b, target, None, weight, dz, loss, correct, dhead, None, S, grad_scale, 1.0,
+                       1 if bce else 0)
 
 
 def policy_head_probs(y, w, b, probs, S: int, legal=None, temperature: float = 1.0):
@@ -130,6 +134,11 @@ def packed_weight_like(w_oihw: torch.Tensor, cin_p: int, cout_p: int, transposed
     K = w_oihw.shape[2]
     shape = (K * K, cin_p, cout_p) if transposed else (K * K, cout_p, cin_p)
     return torch.zeros(shape, device=w_oihw.device, dtype=torch.bfloat16)
+
+
+def wgrad_tap_group(cout_p: int, cin_p: int, K: int) -> int:
+    """Kernel taps one wgrad workgroup covers (K for tap-merged 64-wide c tiles, else 1)."""
+    return int(_ops().wgrad_tap_group(cout_p, cin_p, K))
 
 
 def wgrad_splits(M: int, T: int, n_tiles: int = 1, target_wgs: int = 512) -> int:

@@ -151,7 +151,11 @@ class HipConvTrainer:
         if self.env.distributed:
             agdist.broadcast_(self.fp.flat, 0)
         dev, B, S = self.device, batch, self.S
-        self.bias_p = [torch.zeros(self.Fp, device=dev) for _ in range(self.L)]
+        # unpadded filters: the kernels read the biases straight from the flat
+        # master parameters (no per-step copies); padded: zero-tailed copies
+        self._bias_alias = self.Fp == self.F
+        self.bias_p = ([self.fp.views["b%d" % l] for l in range(self.L)] if self._bias_alias
+                       else [torch.zeros(self.Fp, device=dev) for _ in range(self.L)])
         self.wf, self.wd = [], []
         for l in range(self.L):
             cin_p = self.C0p if l == 0 else self.Fp
@@ -177,7 +181,8 @@ class HipConvTrainer:
             T = self.K[l] ** 2
             tiles = max(1, (self.Fp // (192 if self.Fp % 192 == 0 else 128 if self.Fp % 128 == 0 else 64))
                         * (cin_p // (192 if cin_p % 192 == 0 else 128 if cin_p % 128 == 0 else 64)))
-            ns = ops.wgrad_splits(M, T, tiles, wgrad_target_wgs)
+            taps = ops.wgrad_tap_group(self.Fp, cin_p, self.K[l])  # taps share one workgroup
+            ns = ops.wgrad_splits(M, T // taps, tiles, wgrad_target_wgs)
             self.nsplit.append(ns)
             slab_max = max(slab_max, ns * T * self.Fp * cin_p)
             db_max = max(db_max, ns * self.Fp)
@@ -230,8 +235,8 @@ class HipConvTrainer:
 
     # ------------------------------------------------------------------ helpers
     def repack(self) -> None:
-        for l in range(self.L):
-            self.bias_p[l][:self.F].copy_(self.fp.views["b%d" % l])
+        if not self._bias_alias:
+            torch._foreach_copy_([b[:self.F] for b in self.bias_p], [self.fp.views["b%d" % l] for l in range(self.L)])
         ws = [self.fp.views["w%d" % l] for l in range(self.L)]
         ops.pack_weights(ws, self.wf, self.wd)
         if self.precision == "fp8":
@@ -357,11 +362,13 @@ class HipPolicyTrainer(HipConvTrainer):
     def _forward_for_head(self, planes, targets, sym):
         self.forward_trunk(planes, sym, targets, self.tgt)
 
+    policy_loss = "ce"  # or "bce": the reference RL loss (binary CE on the softmax)
+
     def _head_train(self, targets, gscale, weight):
         hw = self.fp.views["head_w"].view(-1)
         hb = self.fp.views["head_b"]
         ops.policy_head_train(self.Y[-1], hw, hb, self.tgt, self.DZ[-1], self.loss, self.correct, self.dhead,
-                              self.S, gscale, weight=weight)
+                              self.S, gscale, weight=weight, bce=self.policy_loss == "bce")
         ho, hn = self.fp.segments["head_w"]
         torch.sum(self.dhead, dim=0, out=self.fp.grad[ho:ho + hn + 1])
 
@@ -492,6 +499,8 @@ class _TorchTrainerBase:
 class TorchPolicyTrainer(_TorchTrainerBase):
     """Autograd implementation of the same SL/RL step (fp32 by default)."""
 
+    policy_loss = "ce"  # or "bce" (reference RL loss), as HipPolicyTrainer
+
     def __init__(self, net: PolicyNet, batch: int, lr: float = 0.003, decay: float = 0.0, device=None,
                  dtype=torch.float32, iterations: int = 0):
         named = []
@@ -509,13 +518,21 @@ class TorchPolicyTrainer(_TorchTrainerBase):
         logits = self.net.logits_torch(x)
         t = targets.long()
         valid = t >= 0
+        correct = ((logits.argmax(1) == t) & valid).float()
+        w = valid.float() if weight is None else valid.float() * weight
+        norm = planes.shape[0] * self.env.world_size
+        if self.policy_loss == "bce":
+            # reference RL loss: Keras binary_crossentropy on the softmax output,
+            # mean over the S*S outputs, clipped probabilities
+            prob = torch.softmax(logits, 1).clamp(1e-7, 1 - 1e-7)
+            y = torch.nn.functional.one_hot(t.clamp_min(0), logits.shape[1]).to(prob.dtype)
+            per = -(y * prob.log() + (1 - y) * (1 - prob).log()).mean(1) * valid
+            return (per * w).sum() / norm, per, correct
         logp = torch.log_softmax(logits, 1)
         lt = logp.gather(1, t.clamp_min(0).unsqueeze(1)).squeeze(1)
         per = -torch.clamp(lt, min=math.log(1e-7), max=math.log(1 - 1e-7)) * valid
-        correct = ((logits.argmax(1) == t) & valid).float()
         # gradient of mean CE (unclipped, see kernels/head.hip); optional per-board weights (REINFORCE)
-        w = valid.float() if weight is None else valid.float() * weight
-        obj = (-(lt * w)).sum() / (planes.shape[0] * self.env.world_size)
+        obj = (-(lt * w)).sum() / norm
         return obj, per, correct
 
 

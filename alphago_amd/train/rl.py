@@ -7,8 +7,9 @@ one policy-gradient update.  Default loss is REINFORCE as in the paper,
     grad = -1/N * sum_games z_g * sum_t grad log p(a_t | s_t),
 with z = +1 for a learner win and -1 for a loss — computed by the fused HIP
 head kernel with per-board weights z.  ``--loss reference`` reproduces the
-reference's update (binary cross-entropy on the softmax with the learning rate
-negated for lost games; torch backend only).
+reference's update (one step per game of binary cross-entropy on the softmax
+with the learning rate negated for lost games; fused HIP head
+kernel or autograd).
 
 Fixes over the reference: per-game learner colour is used for the reward
 (Q7), training pairs use the state before the learner's move (Q6), snapshots
@@ -32,11 +33,14 @@ from ..models.policy import CNNPolicy
 from ..parallel import dist as agdist
 from ..search.selfplay import BatchedSampler, play_games
 from ..utils.metrics import MetricsLogger
-from .engine import TorchPolicyTrainer, make_policy_trainer
+from .engine import make_policy_trainer
 
 
 def rl_update(trainer, records, B: int, device, loss: str = "reinforce") -> dict:
-    """One policy-gradient step over all learner positions of a batch of games."""
+    """One policy-gradient step over all learner positions of a batch of games
+    (``loss="reference"``: the reference's per-game binary-CE steps instead)."""
+    if loss == "reference":
+        return _reference_bce_update(trainer, records, B, device)
     X, T, Z = [], [], []
     for planes, moves, w, c in zip(records.planes, records.moves, records.winners, records.learner_colors):
         if len(moves) == 0:
@@ -53,52 +57,65 @@ def rl_update(trainer, records, B: int, device, loss: str = "reinforce") -> dict
         X, T, Z = np.zeros((0, C, S, S), np.uint8), np.zeros(0, np.int32), np.zeros(0, np.float32)
     n = len(T)
     n_chunks = int(agdist.all_reduce_max(float((n + B - 1) // B)))
-    if loss == "reference":
-        return _reference_bce_update(trainer, X, T, Z, B, device, n_chunks)
-    acc = torch.zeros_like(trainer.fp.grad)
     scale = float(B) / max(1, n)
-    for c in range(max(1, n_chunks)):
-        sl = slice(c * B, (c + 1) * B)
-        xb, tb, zb = X[sl], T[sl], Z[sl]
-        pad = B - len(tb)
-        if pad:
-            xb = np.concatenate([xb, np.zeros((pad, C, S, S), np.uint8)])
-            tb = np.concatenate([tb, np.full(pad, -1, np.int32)])
-            zb = np.concatenate([zb, np.zeros(pad, np.float32)])
-        trainer.compute_grads(torch.from_numpy(xb).to(device), torch.from_numpy(tb).to(device), None,
-                              torch.from_numpy(zb * scale).to(device))
-        acc += trainer.fp.grad
-    trainer.fp.grad.copy_(acc)
+    _accumulate_grads(trainer, X, T, Z * scale, B, device, n_chunks)
     trainer.apply_update()
     return {"positions": n, "mean_reward": float(Z.mean()) if n else 0.0}
 
 
-def _reference_bce_update(trainer, X, T, Z, B, device, n_chunks) -> dict:
-    """reinforcement_policy_trainer.py:79-103: per game, lr = ±lr and
-    model.fit(X, one_hot(y)) with binary cross-entropy on the softmax output."""
-    if not isinstance(trainer, TorchPolicyTrainer):
-        raise ValueError("--loss reference needs the torch backend")
-    net = trainer.net
-    lr = trainer.sched.current()
-    S = net.board
+def _accumulate_grads(trainer, X, T, W, B, device, n_chunks) -> None:
+    """trainer.fp.grad <- sum over B-sized chunks of the weighted-loss gradients
+    (padding boards carry target -1 and weight 0)."""
+    C, S = trainer.net.trunk.in_planes, trainer.net.board
+    acc = torch.zeros_like(trainer.fp.grad)
     for c in range(max(1, n_chunks)):
         sl = slice(c * B, (c + 1) * B)
-        if len(T[sl]) == 0:
-            continue
-        x = torch.from_numpy(X[sl]).to(device).float()
-        y = torch.nn.functional.one_hot(torch.from_numpy(T[sl]).long(), S * S).float().to(device)
-        z = torch.from_numpy(Z[sl]).to(device)
-        for p in trainer.params:
-            p.grad = None
-        prob = torch.softmax(net.logits_torch(x), 1).clamp(1e-7, 1 - 1e-7)
-        bce = -(y * prob.log() + (1 - y) * (1 - prob).log()).mean(1)
-        (bce * torch.where(z < 0, -1.0, 1.0)).sum().backward()
-        with torch.no_grad():
-            for p in trainer.params:
-                if p.grad is not None:
-                    p -= lr * p.grad
-    trainer.sched.advance()
-    return {"positions": len(T), "mean_reward": float(Z.mean()) if len(Z) else 0.0}
+        xb, tb, wb = X[sl], T[sl], W[sl]
+        pad = B - len(tb)
+        if pad:
+            xb = np.concatenate([xb, np.zeros((pad, C, S, S), np.uint8)])
+            tb = np.concatenate([tb, np.full(pad, -1, np.int32)])
+            wb = np.concatenate([wb, np.zeros(pad, np.float32)])
+        trainer.compute_grads(torch.from_numpy(xb).to(device), torch.from_numpy(tb).to(device), None,
+                              torch.from_numpy(wb.astype(np.float32)).to(device))
+        acc += trainer.fp.grad
+    trainer.fp.grad.copy_(acc)
+
+
+def _reference_bce_update(trainer, records, B, device) -> dict:
+    """reinforcement_policy_trainer.py:79-103: for every game, one SGD step of
+    model.fit(X, one_hot(y), batch_size=len(X)) with binary cross-entropy on the
+    softmax output and the learning rate negated for a lost game.  The sign is
+    folded into per-board weights (p -= lr * sign * grad == p -= (sign*lr) * grad)
+    and 1/len(game) makes the step the game's mean loss, as Keras' fit does.
+    Runs on either backend (fused HIP head with loss_kind=1, or autograd).
+    With data parallelism, step k averages game k of every rank."""
+    C, S = trainer.net.trunk.in_planes, trainer.net.board
+    games = []
+    for planes, moves, w, c in zip(records.planes, records.moves, records.winners, records.learner_colors):
+        if len(moves):
+            games.append((planes, np.asarray(moves, np.int32), 1.0 if w == c else (-1.0 if w == -c else 0.0)))
+    n_steps = int(agdist.all_reduce_max(float(len(games))))
+    prev = trainer.policy_loss
+    trainer.policy_loss = "bce"
+    n_pos, rewards = 0, []
+    try:
+        for k in range(n_steps):
+            if k < len(games):
+                X, T, z = games[k]
+            else:  # this rank has run out of games: contribute a zero gradient
+                X, T, z = np.zeros((0, C, S, S), np.uint8), np.zeros(0, np.int32), 0.0
+            n = len(T)
+            W = np.full(n, z * B / max(1, n), np.float32)
+            n_chunks = int(agdist.all_reduce_max(float((n + B - 1) // B)))
+            _accumulate_grads(trainer, X, T, W, B, device, n_chunks)
+            trainer.apply_update()
+            n_pos += n
+            if n:
+                rewards.append(z)
+    finally:
+        trainer.policy_loss = prev
+    return {"positions": n_pos, "mean_reward": float(np.mean(rewards)) if rewards else 0.0, "steps": n_steps}
 
 
 def _parser():
@@ -129,7 +146,7 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
     rng = np.random.default_rng(args.seed * 7919 + env.rank)
     learner_pol = CNNPolicy.load_model(args.initial_json, device=dev, weights_file=args.initial_weights)
     opp_pol = CNNPolicy.load_model(args.initial_json, device=dev, weights_file=args.initial_weights)
-    backend = "torch" if args.loss == "reference" else args.backend
+    backend = args.backend
     trainer = make_policy_trainer(learner_pol.model, args.minibatch, args.learning_rate, 0.0, backend=backend,
                                   device=dev)
     learner = BatchedSampler(learner_pol, args.temperature, seed=args.seed * 31 + env.rank)

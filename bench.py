@@ -56,6 +56,10 @@ def main():
         from alphago_amd import ops as _ops
         _ops.load()
         torch.ops.alphago_amd.set_conv_tile(int(os.environ["ALPHAGO_AMD_CONV_TILE"]))
+    if os.environ.get("ALPHAGO_AMD_WGRAD_VARIANT") and dev.type == "cuda":
+        from alphago_amd import ops as _ops
+        _ops.load()
+        torch.ops.alphago_amd.set_wgrad_variant(int(os.environ["ALPHAGO_AMD_WGRAD_VARIANT"]))
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
     kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap, "precision": args.precision}

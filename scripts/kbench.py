@@ -58,6 +58,15 @@ for ns in splits:
             res[k] = min(res.get(k, 1e30), timeit(lambda: ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1)))
     torch.ops.alphago_amd.set_wgrad_variant(0)
     res["reduce_s%d" % ns] = timeit(lambda: ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0))
+# layer-0 wgrad (5x5, Cin 64): tap-merged (v0) vs one tap per workgroup (v1)
+dz1 = y
+for v, nss in ((1, (20,)), (0, (25, 51, 102))):
+    torch.ops.alphago_amd.set_wgrad_variant(v)
+    for ns in nss:
+        slab1 = torch.empty(ns, 25, F, 64, device=dev); dbs1 = torch.zeros(ns, F, device=dev)
+        k = "wgrad5x5_v%d_s%d" % (v, ns)
+        res[k] = min(res.get(k, 1e30), timeit(lambda: ops.conv_wgrad(x0, dz1, slab1, dbs1, 5, S, 2, 1)))
+torch.ops.alphago_amd.set_wgrad_variant(0)
 # fp8 forward (block-scaled MFMA), 3x3 and 5x5
 x8 = torch.zeros(x.shape, dtype=torch.uint8, device=dev); ops.quantize_fp8(x, x8, 0)
 x08 = torch.zeros(x0.shape, dtype=torch.uint8, device=dev); ops.quantize_fp8(x0, x08, 0)

@@ -80,7 +80,7 @@ def test_conv_dgrad_with_relu_mask(ops, cuda_device, B, C, K):
     assert _rel_err(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("B,Cin,Cout,K,Pin,nsplit", [(6, 192, 192, 3, 1, None), (5, 64, 192, 5, 2, None),
                                                     (3, 64, 64, 3, 1, None), (9, 128, 128, 3, 1, None),
                                                     (7, 192, 192, 3, 1, 1), (4, 192, 192, 3, 1, 3)])

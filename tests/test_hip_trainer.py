@@ -37,6 +37,35 @@ def test_hip_grads_match_torch(cuda_device, F, L, C, B):
     assert torch.allclose(hip.loss, ref._last[0], rtol=2e-2, atol=2e-2)
 
 
+def test_hip_bce_grads_match_torch(cuda_device):
+    """Reference RL loss (binary CE on the softmax, per-board signed weights) on
+    the fused HIP head (loss_kind=1) vs autograd."""
+    torch.manual_seed(5)
+    B, C = 6, 48
+    net = PolicyNet(C, filters_per_layer=64, layers=3)
+    net_ref = copy.deepcopy(net)
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    tgt[-1] = -1  # padding board: no loss, no gradient
+    wt = torch.tensor([1.0, -1.0, 2.0, -0.5, 1.0, 3.0], device=cuda_device)
+    hip = HipPolicyTrainer(net, B, lr=0.01, device=cuda_device)
+    ref = TorchPolicyTrainer(net_ref, B, lr=0.01, device=cuda_device)
+    hip.policy_loss = ref.policy_loss = "bce"
+    hip.compute_grads(planes, tgt, None, wt)
+    ref.compute_grads(planes, tgt, None, wt)
+    torch.cuda.synchronize()
+    for name in hip.fp.names:
+        a, b = hip.fp.grad_views[name], ref.fp.grad_views[name]
+        if name == "head_b":
+            assert abs(a.item()) < 1e-6 and abs(b.item()) < 1e-6
+            continue
+        cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
+        ratio = a.norm().item() / max(b.norm().item(), 1e-12)
+        assert cos > 0.98 and abs(ratio - 1) < 0.05, (name, cos, ratio)
+    assert torch.allclose(hip.loss, ref._last[0], rtol=2e-2, atol=1e-4)
+    assert hip.loss[-1].item() == 0.0
+
+
 def test_hip_step_reduces_loss(cuda_device):
     torch.manual_seed(1)
     B = 32

@@ -66,6 +66,40 @@ def test_rl_cli_cpu(tmp_path):
     assert out2["history"][0]["games"] == 2
 
 
+def test_reference_bce_update_matches_keras_semantics():
+    """loss="reference": one SGD step per game on the mean binary CE of the
+    softmax (Keras 1.0 binary_crossentropy, clipped), lr negated for a loss
+    (reinforcement_policy_trainer.py:79-103), checked against a hand-written update."""
+    import copy
+
+    from alphago_amd.search.selfplay import GameRecords
+    from alphago_amd.train.engine import TorchPolicyTrainer
+
+    torch.manual_seed(1)
+    pol = _policy(torch.device("cpu"))
+    net_ref = copy.deepcopy(pol.model)
+    lr = 0.5
+    tr = TorchPolicyTrainer(pol.model, 4, lr=lr)
+    rng = np.random.default_rng(0)
+    games = [(rng.integers(0, 2, (n, pol.preprocessor.output_dim, 9, 9), dtype=np.uint8),
+              rng.integers(0, 81, n).astype(np.int32)) for n in (3, 6)]
+    rec = GameRecords(planes=[g[0] for g in games], moves=[g[1] for g in games], winners=[1, 1],
+                      learner_colors=[1, -1])  # game 0 won, game 1 lost
+    out = rl.rl_update(tr, rec, 4, torch.device("cpu"), loss="reference")
+    assert out["steps"] == 2 and out["positions"] == 9 and tr.policy_loss == "ce"
+    params = [p for p in net_ref.parameters()]
+    for (X, T), sign in zip(games, (1.0, -1.0)):
+        prob = torch.softmax(net_ref.logits_torch(torch.from_numpy(X).float()), 1).clamp(1e-7, 1 - 1e-7)
+        y = torch.nn.functional.one_hot(torch.from_numpy(T).long(), 81).float()
+        loss = -(y * prob.log() + (1 - y) * (1 - prob).log()).mean(1).mean()
+        grads = torch.autograd.grad(loss, params)
+        with torch.no_grad():
+            for p, g in zip(params, grads):
+                p -= sign * lr * g
+    for a, b in zip(pol.model.parameters(), net_ref.parameters()):
+        assert torch.allclose(a, b, atol=1e-6), (a - b).abs().max()
+
+
 def test_reinforce_sign():
     """A won game's moves become more likely, a lost game's less likely."""
     from alphago_amd.search.selfplay import GameRecords
