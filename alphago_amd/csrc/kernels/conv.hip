@@ -133,7 +133,10 @@ __device__ __forceinline__ void conv_store_tile(const ConvFwdArgs& a, const f32x
 }
 
 // ----------------------------------------------------------------- forward
-template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true>
+template <int NB, int MB, int MODE>
+struct ConvEpilogue32;
+
+template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false>
 __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
   constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
@@ -240,6 +243,58 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   stage(0);
   wait_vmcnt0();
   __syncthreads();
+  if constexpr (M32) {
+    // v_mfma_f32_32x32x16_bf16: an MFMA holds the SIMD's vector issue for 8 of
+    // 32 cycles (8 of 16 for 16x16x32), leaving the co-resident wave more room
+    // for its LDS reads and DMA issue.  Wave tile 16*MBW pixels x BN/2 channels
+    // as (MBW/2) x (BN/64) 32x32 tiles; epilogue in the 32x32 C/D layout.
+    constexpr int NB2 = BN / 64, MB2 = MBW / 2;
+    static_assert(MBW % 2 == 0 && BN % 64 == 0, "32x32 tiles");
+    f32x16 acc2[NB2][MB2];
+#pragma unroll
+    for (int i = 0; i < NB2; ++i)
+#pragma unroll
+      for (int j = 0; j < MB2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc2[i][j][e] = 0.f;
+    const int h = lane >> 5;
+    const int l31 = lane & 31;
+    const int xr0 = wm * 16 * MB + l31;         // tile row of block 0 (blocks are 32-aligned)
+    const int wr0 = wn * (BN / 2) + l31;
+    const int sw = (l31 >> 1) & 7;               // (row >> 1) & 7 for every 32-aligned block
+    for (int ks = 0; ks < nK; ++ks) {
+      const int cur = ks & 1;
+      const char* base = smem + cur * STAGE;
+      if (ks + 1 < nK) stage(cur ^ 1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 xf2[2][MB2], wf2[2][NB2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int co = ((((2 * kk + s2) << 1) + h) ^ sw) << 4;
+#pragma unroll
+          for (int j = 0; j < MB2; ++j) xf2[s2][j] = *(const bf16x8*)(base + (xr0 + j * 32) * 128 + co);
+#pragma unroll
+          for (int i = 0; i < NB2; ++i) wf2[s2][i] = *(const bf16x8*)(base + A_BYTES + (wr0 + i * 32) * 128 + co);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+          for (int i = 0; i < NB2; ++i)
+#pragma unroll
+            for (int j = 0; j < MB2; ++j)
+              acc2[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf2[s2][i], xf2[s2][j], acc2[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      wait_vmcnt0();
+      __syncthreads();
+    }
+    ConvEpilogue32<NB2, MB2, MODE> ep2;
+    ep2.load(a, m0 + wm * 16 * MB + l31, n0 + wn * (BN / 2), wn);
+    ep2.store(a, acc2, m0 + wm * 16 * MB + l31);
+    return;
+  }
   if constexpr (!PIPE) {  // one fragment set (large wave tiles): read, then MFMA, per k-half
     for (int ks = 0; ks < nK; ++ks) {
       const int cur = ks & 1;
@@ -607,6 +662,230 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_ring_kernel(ConvFwdArgs a) {
   conv_store_tile<NB, MB, MODE>(a, acc, m0 + wm * 64 + (lane & 15), n0 + wn * (BN / 2) + ((lane >> 4) << 2), wn);
 }
 
+// ------------------------------------------------- forward, ping-pong variant
+// The 2-buffer kernels run both waves of a SIMD in lockstep: they read LDS
+// fragments together, then fight for the one matrix pipe together, and every
+// K-step ends in vmcnt(0) + barrier.  Here the 8 waves form two groups
+// (waves 0-3 / 4-7, i.e. one wave of each group per SIMD) that run one
+// barrier apart: while group 0 issues its 24 MFMAs, group 1 reads its next
+// fragments and issues its share of the DMA, and vice versa, so the matrix
+// pipe of every SIMD alternates between the two waves.
+//   * tile 256 pixels x BN channels, K-step (phase) = one tap x 32 channels,
+//     group g owns pixel rows [128g, 128g+128) (2x2 waves of 64 x BN/2);
+//   * 4-slot LDS ring of 64-B rows (16 KB pixels + BN*64 B weights per slot),
+//     the DMA runs 3 phases ahead; each wave retires its own pieces of phase
+//     p+1 with a counted vmcnt during phase p, and the barrier that follows
+//     publishes them to the other group (whose next read is >= 1 barrier later);
+//   * a group's LDS reads complete (lgkmcnt(0)) before the barrier that ends
+//     its read segment, so a slot refilled after that barrier is never read.
+// Same packed operands, padded geometry and epilogue (bias + ReLU + ReLU'
+// bitmask, or the dgrad mask) as conv_fwd_kernel.
+constexpr int PP_BM = 256;
+constexpr int PP_SLOTS = 4;
+
+template <int BN, int MODE, bool STAMP = false>
+__global__ __launch_bounds__(512, 1) void conv_fwd_pp_kernel(ConvFwdArgs a) {
+  constexpr int NB = BN / 32;  // 16-wide n blocks per wave (wave covers BN/2 channels)
+  constexpr int MB = 4;        // 16-wide m blocks per wave (64 pixels)
+  constexpr int A_BYTES = PP_BM * 64;
+  constexpr int SLOT = A_BYTES + BN * 64;
+  constexpr int BPIECES = BN / 16;  // 1 KB DMA pieces of the weight tile
+  constexpr int BP_MAX = (BPIECES + 7) / 8;
+  constexpr int BP_MIN = BPIECES / 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int grp = wave >> 2;
+  const int wm = grp * 2 + ((wave >> 1) & 1);  // 64-pixel row block of the tile
+  const int wn = wave & 1;                     // channel half
+  // XCD-aware bijective tile order: the 8 XCDs each get a contiguous tile range
+  const int nwg = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int m0 = tile * PP_BM;
+  const int n0 = blockIdx.y * BN;
+  const int SS = a.S * a.S;
+  const int CC2 = a.Cin >> 5;  // 32-channel chunks
+  const int nK = a.K * a.K * CC2;
+
+  // A pieces: wave w stages rows [16w, 16w+16) and [16(w+8), ...); lane -> row lane/4, 16-B chunk lane%4
+  int arow[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * (wave + 8 * i) + (lane >> 2);
+    int m = m0 + r;
+    m = m < a.M ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    const int logical = (lane & 3) ^ (((r >> 2) & 1) << 1);
+    arow[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + logical * 8;
+  }
+  const bool bfull = wave < (BPIECES & 7);  // this wave stages BP_MAX weight pieces (else BP_MIN)
+  int brow[BP_MAX];
+#pragma unroll
+  for (int i = 0; i < BP_MAX; ++i) {
+    const int r = 16 * (wave + 8 * i) + (lane >> 2);
+    const int logical = (lane & 3) ^ (((r >> 2) & 1) << 1);
+    brow[i] = (n0 + (r < BN ? r : 0)) * a.Cin + logical * 8;
+  }
+  const size_t wtap = (size_t)a.Cout * a.Cin;
+
+  // staging cursor (tap kh/kw, chunk c) of the next phase to issue, advanced incrementally
+  int is_c = 0, is_kw = 0, is_aoff = 0;
+  size_t is_w = 0;
+  int is_slot = 0;
+  auto issue_next = [&]() {
+    char* base = smem + is_slot * SLOT;
+    glds16(a.x + arow[0] + is_aoff + (is_c << 5), base + wave * 1024);
+    glds16(a.x + arow[1] + is_aoff + (is_c << 5), base + (wave + 8) * 1024);
+    const __bf16* wt = a.w + is_w + (is_c << 5);
+#pragma unroll
+    for (int i = 0; i < BP_MAX; ++i)
+      if (i < BP_MIN || bfull) glds16(wt + brow[i], base + A_BYTES + (wave + 8 * i) * 1024);
+    is_slot = (is_slot + 1) & (PP_SLOTS - 1);
+    if (++is_c == CC2) {
+      is_c = 0;
+      is_w += wtap;
+      is_aoff += a.Cin;
+      if (++is_kw == a.K) {
+        is_kw = 0;
+        is_aoff += (a.HPi - a.K) * a.Cin;
+      }
+    }
+  };
+  // retire the oldest phase in flight, leaving `ahead` younger phases' pieces outstanding
+  auto retire = [&](int ahead) {
+    if (BP_MAX == BP_MIN || bfull) {
+      if (ahead >= 2) vmcnt_wait<2 * (2 + BP_MAX)>();
+      else if (ahead == 1) vmcnt_wait<2 + BP_MAX>();
+      else vmcnt_wait<0>();
+    } else {
+      if (ahead >= 2) vmcnt_wait<2 * (2 + BP_MIN)>();
+      else if (ahead == 1) vmcnt_wait<2 + BP_MIN>();
+      else vmcnt_wait<0>();
+    }
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int r15 = lane & 15;
+  const int pch = (lane >> 4) ^ (((r15 >> 2) & 1) << 1);
+  const int xoff = (wm * 64 + r15) * 64 + pch * 16;
+  const int woff = A_BYTES + (wn * (BN / 2) + r15) * 64 + pch * 16;
+  const int ep_mrow = m0 + wm * 64 + r15;
+  const int ep_nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
+  ConvEpilogue<NB, MB, MODE> ep;
+  const int ep_at = nK > 3 ? nK - 3 : 0;
+
+  // prologue: phases 0..2 in flight, phase 0 retired and published
+  const int npro = nK < 3 ? nK : 3;
+  for (int p = 0; p < npro; ++p) issue_next();
+  retire(npro - 1);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger: group 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  bf16x8 xf[MB], wf[NB];
+  // diagnostic build only: cycles per segment summed over the phases
+  uint64_t st_sum[7] = {0, 0, 0, 0, 0, 0, 0};
+  const uint64_t st_begin = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  for (int p = 0; p < nK; ++p) {
+    // ---- read segment (the partner group is in its MFMA segment)
+    uint64_t ts[8];
+    if constexpr (STAMP) ts[0] = __builtin_amdgcn_s_memtime();
+    const char* base = smem + (p & (PP_SLOTS - 1)) * SLOT;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) xf[j] = *(const bf16x8*)(base + xoff + j * 16 * 64);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) wf[i] = *(const bf16x8*)(base + woff + i * 16 * 64);
+    const bool more = p + 3 < nK;
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      ts[7] = __builtin_amdgcn_s_memtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (more) issue_next();
+    if (p == ep_at) ep.load(a, ep_mrow, ep_nbase, wn);
+    if constexpr (STAMP) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STAMP) ts[1] = __builtin_amdgcn_s_memtime();
+    retire(more ? 2 : (nK - 2 - p > 0 ? nK - 2 - p : 0));  // retire phase p+1
+    if constexpr (STAMP) ts[2] = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (STAMP) ts[3] = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STAMP) ts[4] = __builtin_amdgcn_s_memtime();
+    // ---- MFMA segment (the partner group reads)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STAMP) ts[5] = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (STAMP) {
+      ts[6] = __builtin_amdgcn_s_memtime();
+#pragma unroll
+      for (int i = 0; i < 6; ++i) st_sum[i] += ts[i + 1] - ts[i];
+      st_sum[6] += ts[7] - ts[0];
+    }
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* d = a.dbg + ((size_t)blockIdx.x * 8 + wave) * 8;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) d[i] = st_sum[i];
+      d[6] = __builtin_amdgcn_s_memtime() - st_begin;
+      d[7] = nK | (st_sum[6] << 16);
+    }
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // equal barrier counts
+  ep.store(a, acc, ep_mrow);
+}
+
+static unsigned long long* g_conv_dbg = nullptr;
+void set_conv_debug(unsigned long long* buf) { g_conv_dbg = buf; }
+
+template <int BN, int MODE>
+static void launch_fwd_pp(const ConvFwdArgs& a_in, hipStream_t st) {
+  constexpr int smem = PP_SLOTS * (PP_BM * 64 + BN * 64);
+  if constexpr (BN == 192 && MODE == MODE_BIAS_RELU) {
+    if (g_conv_dbg) {  // diagnostic instantiation with segment stamps
+      static bool attr_d = false;
+      if (!attr_d) {
+        hipFuncSetAttribute((const void*)conv_fwd_pp_kernel<BN, MODE, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        attr_d = true;
+      }
+      ConvFwdArgs a = a_in;
+      a.dbg = g_conv_dbg;
+      dim3 grid((a.M + PP_BM - 1) / PP_BM, a.Cout / BN);
+      hipLaunchKernelGGL((conv_fwd_pp_kernel<BN, MODE, true>), grid, dim3(512), smem, st, a);
+      return;
+    }
+  }
+  const ConvFwdArgs& a = a_in;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_pp_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  dim3 grid((a.M + PP_BM - 1) / PP_BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_pp_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
+}
+
 template <int BN, int MODE>
 static void launch_fwd_ring(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = RING_SLOTS * (RING_BM * 64 + BN * 64);
@@ -640,17 +919,17 @@ static void launch_fwd_halo(const ConvFwdArgs& a_in, hipStream_t st) {
 
 static int g_fwd_bm = 0;  // 0 = auto
 
-template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true>
+template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE>,
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE>), grid, dim3(BM / MBW * 8), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32>), grid, dim3(BM / MBW * 8), smem, st, a);
 }
 
 
@@ -665,6 +944,9 @@ static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
 // weight tile (24 KB at BN = 192) streams through a double buffer.
 constexpr int H2_BM = 256;
 constexpr int H2_ROWS = 384;  // 48 KB of 128-B rows per halo buffer
+// compact halo of the halo + ping-pong kernel: 256 + 2*(S+1) pixel rows (S <= 23) + 8 zero rows
+constexpr int HC_DATA = 320;
+constexpr int HC_ROWS = HC_DATA + 8;
 
 template <int BN, int MODE>
 __global__ __launch_bounds__(512, 1) void conv_fwd_halo2_kernel(ConvFwdArgs a) {
@@ -794,6 +1076,582 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_halo2_kernel(ConvFwdArgs a) {
   ep.store(a, acc, ep_mrow);
 }
 
+// ------------------------------------ forward, halo + ping-pong variant (3x3)
+// The interior-halo staging of conv_fwd_halo2_kernel (per 64-channel chunk the
+// padded input rows of the tile's 256 pixels and all 9 taps are staged ONCE,
+// A fragments are gathered from LDS per tap) combined with the two-group
+// ping-pong of conv_fwd_pp_kernel (waves 0-3 / 4-7 alternate between an LDS
+// read segment and a 48-MFMA segment, one barrier apart).  Global traffic per
+// MFMA is ~3x lower than the gather kernels: per K-step (tap x 64 channels)
+// only the 24 KB weight tile streams, the 48 KB halo once per 9 steps.
+// The loads are split by group so that every DMA is retired (own vmcnt)
+// before a barrier that precedes its first reader in either group:
+//   * group 0 loads the weights: W(p+1) is issued in its read segment of
+//     step p into the slot W(p-1) used (both groups finished reading it one
+//     barrier earlier) and retired at the end of its MFMA segment of step p;
+//   * group 1 loads the next chunk's halo during steps 0..5 of a chunk and
+//     retires it in step 7 (the halo buffer it overwrites was last read in
+//     the previous chunk).
+// LDS: 2 x 48 KB halo + 2 x BN*128 B weights (144 KB at BN = 192).
+template <int BN, int MODE, bool STAMP = false>
+__global__ __launch_bounds__(512, 1) void conv_fwd_hpp_kernel(ConvFwdArgs a) {
+  // STAMP (diagnostic build): per-wave cycle sums of the loop segments into a.dbg
+  uint64_t st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ts[9];
+#define HPP_STAMP(i)                          \
+  if constexpr (STAMP) {                      \
+    __builtin_amdgcn_sched_barrier(0);        \
+    ts[i] = __builtin_amdgcn_s_memtime();     \
+    __builtin_amdgcn_sched_barrier(0);        \
+  }
+  constexpr int NB = BN / 32;
+  constexpr int MB = 4;
+  constexpr int H_BYTES = HC_ROWS * 128;
+  constexpr int W_BYTES = BN * 128;
+  constexpr int WP = BN / 32;              // weight pieces per group-0 wave (BN/8 1-KB pieces over 4 waves)
+  constexpr int H_PIECES = HC_DATA / 8;    // 1-KB halo pieces per chunk (40)
+  constexpr int HP1 = H_PIECES / 4;        // per group-1 wave in steady state (10)
+  constexpr int HP_STEP = 2;               // halo pieces a group-1 wave issues per step
+  constexpr int T = 9;                     // 3x3 only
+  static_assert(HP1 == 5 * HP_STEP && H_PIECES % 8 == 0, "halo pieces must be issued within steps 0..4");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;
+  char* const wbuf = smem + 2 * H_BYTES;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int grp = wave >> 2;
+  const int wq = wave & 3;
+  const int wm = grp * 2 + ((wave >> 1) & 1);
+  const int wn = wave & 1;
+  const int nwg = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int m0 = tile * H2_BM;
+  const int n0 = blockIdx.y * BN;
+  const int S = a.S;
+  const int SS = S * S;
+  const int CC = a.Cin >> 6;
+  const int HP = a.HPi;
+  const int Pc = a.offi + 1;
+  const int G = S + 1;  // largest |tap shift| in the compact (unpadded) pixel index
+  const int nK = CC * T;
+
+  // Halo rows are COMPACT pixel indices (no padding): row r holds interior
+  // pixel m0 - G + r, so the 16 pixels of an MFMA block read 16 consecutive
+  // rows for every tap (the padded layout skips 2 rows at each board-row end,
+  // which made 2-way bank conflicts unavoidable).  Taps that leave the board
+  // read the zero rows [HC_DATA, HC_ROWS) instead.
+  auto halo_piece = [&](int c, int k, int buf) {
+    const int r = k * 8 + (lane >> 3);
+    int m = m0 - G + r;
+    m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int q = (b * HP + ii + Pc) * HP + (rem - ii * S) + Pc;
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    glds16(a.x + (size_t)q * a.Cin + c * 64 + logical * 8, hbuf + buf * H_BYTES + k * 1024);
+  };
+  // weight tile of step (t, c) into slot: group-0 wave wq stages rows [8(wq*WP+i), +8)
+  int wrow[WP];
+#pragma unroll
+  for (int i = 0; i < WP; ++i) {
+    const int r = (wq * WP + i) * 8 + (lane >> 3);
+    wrow[i] = (n0 + r) * a.Cin + (((lane & 7) ^ ((r >> 1) & 7)) << 3);
+  }
+  const size_t wtap = (size_t)a.Cout * a.Cin;
+  auto stage_w = [&](int t, int c, int slot) {
+    const __bf16* wt = a.w + (size_t)t * wtap + c * 64;
+#pragma unroll
+    for (int i = 0; i < WP; ++i) glds16(wt + wrow[i], wbuf + slot * W_BYTES + (wq * WP + i) * 1024);
+  };
+
+  // Pixel order inside a 16-pixel MFMA block: lanes i = 0-3, 12-15 take the
+  // even pixels and i = 4-11 the odd ones.  A ds_read_b128 lane group reads
+  // rows i in {0-3, 12-15} at one 16-B chunk and i in {4-11} at the next, so
+  // the two chunk sets sit on rows of opposite parity (opposite 128-B bank
+  // halves) and the (row >> 1) swizzle keeps each set conflict-free for any
+  // row alignment (the per-tap shifts make every alignment occur).
+  const int li = lane & 15;
+  const int pix16 = li < 4 ? 2 * li : (li < 12 ? 2 * (li - 4) + 1 : 2 * (li - 12) + 8);
+  int prel[MB], px[MB], py[MB];
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    int m = m0 + wm * 64 + j * 16 + pix16;
+    m = m < a.M ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    py[j] = fdiv(rem, a.divS);
+    px[j] = rem - py[j] * S;
+    prel[j] = m - m0 + G;
+  }
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int swzw = (lane & 15) >> 1;
+  const int wrow0 = (wn * (BN / 2) + (lane & 15)) * 128;
+  const int ep_mrow = m0 + wm * 64 + pix16;
+  const int ep_nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
+  ConvEpilogue<NB, MB, MODE> ep;
+  const int ep_at = nK > 3 ? nK - 3 : 0;
+
+  // prologue: zero rows of both halo buffers, chunk 0's halo by all waves, W(0) by group 0
+  if (wave < 2) {
+    const int zb = (HC_ROWS - HC_DATA) * 128;  // zero-row bytes per buffer
+    for (int o = lane * 16; o < zb; o += 64 * 16)
+      *(uint4*)(hbuf + wave * H_BYTES + HC_DATA * 128 + o) = make_uint4(0u, 0u, 0u, 0u);
+  }
+#pragma unroll
+  for (int i = 0; i < H_PIECES / 8; ++i) halo_piece(0, wave * (H_PIECES / 8) + i, 0);
+  if (grp == 0) stage_w(0, 0, 0);
+  wait_vmcnt0();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger
+  __builtin_amdgcn_sched_barrier(0);
+
+  int c = 0, t = 0, kh = 0, kw = 0, wslot = 0;
+  const uint64_t st_begin = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  for (int p = 0; p < nK; ++p) {
+    // ---- read segment
+    HPP_STAMP(0);
+    const char* hb = hbuf + (c & 1) * H_BYTES;
+    const char* wb = wbuf + wslot * W_BYTES;
+    const int toff = (kh - 1) * S + (kw - 1);
+    int arow[MB];
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      const bool ok = (unsigned)(py[j] + kh - 1) < (unsigned)S && (unsigned)(px[j] + kw - 1) < (unsigned)S;
+      arow[j] = ok ? prel[j] + toff : HC_DATA;
+    }
+    bf16x8 xf[2][MB], wf[2][NB];
+    auto read_half = [&](int kk) {
+      const int ch = (kk << 2) + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < MB; ++j) {
+        const int row = arow[j];
+        xf[kk][j] = *(const bf16x8*)(hb + row * 128 + ((ch ^ ((row >> 1) & 7)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wf[kk][i] = *(const bf16x8*)(wb + wrow0 + i * 16 * 128 + ((ch ^ swzw) << 4));
+    };
+    read_half(0);  // k 0..31 here; k 32..63 is read under the first half's MFMAs
+    HPP_STAMP(1);
+    // step cursor of p+1
+    int tn = t + 1, cn = c, khn = kh, kwn = kw + 1;
+    if (kwn == 3) { kwn = 0; ++khn; }
+    if (tn == T) { tn = 0; ++cn; khn = 0; kwn = 0; }
+    if (grp == 0) {
+      if (p + 1 < nK) stage_w(tn, cn, wslot == 2 ? 0 : wslot + 1);
+    } else if (c + 1 < CC) {
+      if (t < 5) {
+#pragma unroll
+        for (int i = 0; i < HP_STEP; ++i) halo_piece(c + 1, wq * HP1 + t * HP_STEP + i, (c + 1) & 1);
+      } else if (t == 7) {
+        wait_vmcnt0();  // next chunk's halo landed (published by this step's barrier)
+      }
+    }
+    if (p == ep_at) ep.load(a, ep_mrow, ep_nbase, wn);
+    HPP_STAMP(2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    HPP_STAMP(3);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    HPP_STAMP(4);
+    // ---- MFMA segment: first half, with the second half's LDS reads interleaved
+    __builtin_amdgcn_s_setprio(1);
+    read_half(1);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[0][i], xf[0][j], acc[i][j]);
+#pragma unroll
+    for (int g = 0; g < MB + NB; ++g) {  // 1 ds_read per 2 MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NB * MB - 2 * (MB + NB), 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[1][i], xf[1][j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    HPP_STAMP(5);
+    __builtin_amdgcn_sched_barrier(0);
+    if (grp == 0) wait_vmcnt0();  // W(p+1) landed before the barrier that precedes its readers
+    HPP_STAMP(6);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    HPP_STAMP(7);
+    if constexpr (STAMP) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) st_sum[i] += ts[i + 1] - ts[i];
+    }
+    t = tn; c = cn; kh = khn; kw = kwn;
+    wslot = wslot == 2 ? 0 : wslot + 1;
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* d = a.dbg + ((size_t)blockIdx.x * 8 + wave) * 8;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) d[i] = st_sum[i];
+      d[7] = __builtin_amdgcn_s_memtime() - st_begin;
+    }
+  }
+#undef HPP_STAMP
+  if (grp == 0) __builtin_amdgcn_s_barrier();
+  ep.store(a, acc, ep_mrow);
+}
+
+// ---------------- epilogue for the 32x32x16 MFMA layout (weights as A, pixels as B)
+// acc[i][j] (f32x16) of a wave: output channel nbase + 32 i + 8 g + 4 h + r
+// (h = lane >> 5, reg = 4 g + r) of pixel mrow + 32 j, mrow = the lane's pixel
+// of block 0.  ReLU' bitmask: per padded pixel (Cout/BN)*8 words; the lane's
+// 16*NB bits (bit 16 i + 4 g + r) sit in words blockIdx.y*8 + wn*4 + 2h + {0, 1}.
+template <int NB, int MB, int MODE>
+struct ConvEpilogue32 {
+  int ooff[MB];
+  int pix[MB];
+  f32x4 bb[NB][4];
+  bf16x4 mk[NB][MB][4];
+  uint2 mw[MB];
+  int mslot, mwords;
+
+  __device__ __forceinline__ void load(const ConvFwdArgs& a, int mrow, int nbase, int wn) {
+    const int SS = a.S * a.S;
+    const int h = (threadIdx.x & 63) >> 5;
+    mslot = blockIdx.y * 8 + wn * 4 + 2 * h;
+    mwords = gridDim.y * 8;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      int m = mrow + j * 32;
+      m = m < a.M ? m : a.M - 1;
+      const int b = fdiv(m, a.divSS);
+      const int rem = m - b * SS;
+      const int ii = fdiv(rem, a.divS);
+      const int jj = rem - ii * a.S;
+      pix[j] = (b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po;
+      ooff[j] = pix[j] * a.Cout + nbase + 4 * h;
+    }
+    if constexpr (MODE == MODE_BIAS_RELU) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bb[i][g] = *(const f32x4*)(a.bias + nbase + 4 * h + i * 32 + g * 8);
+    } else if constexpr (MODE == MODE_MASK) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j)
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) mk[i][j][g] = *(const bf16x4*)(a.mask + ooff[j] + i * 32 + g * 8);
+    } else if constexpr (MODE == MODE_MASKBITS) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j) mw[j] = *(const uint2*)(a.mbits_in + (size_t)pix[j] * mwords + mslot);
+    }
+  }
+
+  __device__ __forceinline__ void store(const ConvFwdArgs& a, const f32x16 (&acc)[NB][MB], int mrow) const {
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      if (mrow + j * 32 >= a.M) continue;
+      uint32_t bits[2] = {0u, 0u};
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r];
+          const int bit0 = 16 * i + 4 * g;
+          if constexpr (MODE == MODE_BIAS_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bb[i][g][r], 0.f);
+          } else if constexpr (MODE == MODE_MASK) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (float)mk[i][j][g][r] > 0.f ? v[r] : 0.f;
+          } else if constexpr (MODE == MODE_MASKBITS) {
+            const uint32_t w = bit0 < 32 ? mw[j].x : mw[j].y;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = ((w >> ((bit0 & 31) + r)) & 1u) ? v[r] : 0.f;
+          }
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
+          if constexpr (MODE == MODE_BIAS_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bits[bit0 >> 5] |= ((float)o[r] > 0.f ? 1u : 0u) << ((bit0 & 31) + r);
+          }
+          *(bf16x4*)(a.y + ooff[j] + i * 32 + g * 8) = o;
+        }
+      if constexpr (MODE == MODE_BIAS_RELU)
+        if (a.mbits_out) *(uint2*)(a.mbits_out + (size_t)pix[j] * mwords + mslot) = make_uint2(bits[0], bits[1]);
+    }
+  }
+};
+
+// --------------------- forward, compact halo + ping-pong, 32x32x16 MFMA (3x3 / 5x5)
+// Same schedule as conv_fwd_hpp_kernel (two wave groups one barrier apart,
+// group 0 streams the weights through 3 slots, group 1 the next chunk's halo,
+// half of each step's fragment reads under the previous half's MFMAs), but on
+// v_mfma_f32_32x32x16_bf16: an MFMA holds the SIMD's vector issue for 8 of its
+// 32 cycles instead of 8 of 16, which leaves the partner wave 3x the issue
+// slots for its LDS reads, address math and DMA (the 16x16x32 form saturated
+// the issue port: measured with conv_stamps.py).  Per wave 64 pixels x BN/2
+// channels = 2 x (BN/64) MFMA tiles, 24 MFMAs per 64-channel step at BN=192.
+// The compact halo (rows = unpadded pixel indices, zero rows for taps leaving
+// the board) makes the 32 rows of a block contiguous: conflict-free reads.
+constexpr int H32_DATA3 = 320;  // K=3: 256 + 2*(S+1) <= 320 rows, 40 one-KB pieces (10 per group-1 wave)
+constexpr int H32_DATA5 = 344;  // K=5 (single 64-channel chunk): 256 + 4*(S+1) <= 344 rows
+
+template <int BN, int MODE, int K, bool STAMP = false>
+__global__ __launch_bounds__(512, 1) void conv_fwd_h32_kernel(ConvFwdArgs a) {
+  uint64_t st_sum[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ts[9];
+#define H32_STAMP(i)                          \
+  if constexpr (STAMP) {                      \
+    __builtin_amdgcn_sched_barrier(0);        \
+    ts[i] = __builtin_amdgcn_s_memtime();     \
+    __builtin_amdgcn_sched_barrier(0);        \
+  }
+  constexpr int NB = BN / 64;  // 32-channel MFMA tiles per wave (wave covers BN/2)
+  constexpr int MB = 2;        // 32-pixel MFMA tiles per wave
+  constexpr int T = K * K;
+  constexpr int HDATA = K == 3 ? H32_DATA3 : H32_DATA5;
+  constexpr int HROWS = HDATA + 16;  // + 16 zero rows (a redirected lane keeps its bank slot)
+  constexpr int NHBUF = K == 3 ? 2 : 1;
+  constexpr int H_BYTES = HROWS * 128;
+  constexpr int W_BYTES = BN * 128;
+  constexpr int WP = BN / 64;          // weight pieces per wave (each group stages half of every tile)
+  constexpr int H_PIECES = HDATA / 8;  // 1-KB halo pieces per chunk
+  constexpr int HP1 = H_PIECES / 4;
+  constexpr int HP_STEP = 2;
+  static_assert(K == 5 || HP1 == 5 * HP_STEP, "K=3 halo pieces are issued in steps 0..4");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const hbuf = smem;
+  char* const wbuf = smem + NHBUF * H_BYTES;
+
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int wave = wave_id();
+  const int grp = wave >> 2;
+  const int wq = wave & 3;
+  const int wm = grp * 2 + ((wave >> 1) & 1);
+  const int wn = wave & 1;
+  const int nwg = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int m0 = tile * H2_BM;
+  const int n0 = blockIdx.y * BN;
+  const int S = a.S;
+  const int SS = S * S;
+  const int CC = a.Cin >> 6;
+  const int HP = a.HPi;
+  const int Pc = a.offi + K / 2;
+  const int G = (K / 2) * (S + 1);
+  const int nK = CC * T;
+
+  auto halo_piece = [&](int c, int k, int buf) {
+    const int r = k * 8 + (lane >> 3);
+    int m = m0 - G + r;
+    m = m < 0 ? 0 : (m >= a.M ? a.M - 1 : m);
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int q = (b * HP + ii + Pc) * HP + (rem - ii * S) + Pc;
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    glds16(a.x + (size_t)q * a.Cin + c * 64 + logical * 8, hbuf + buf * H_BYTES + k * 1024);
+  };
+  // weight pieces: group g stages pieces [g*4*WP, (g+1)*4*WP) of every tile, WP per wave
+  const int wpiece0 = (grp * 4 + wq) * WP;
+  int wrow[WP];
+#pragma unroll
+  for (int i = 0; i < WP; ++i) {
+    const int r = (wpiece0 + i) * 8 + (lane >> 3);
+    wrow[i] = (n0 + r) * a.Cin + (((lane & 7) ^ ((r >> 1) & 7)) << 3);
+  }
+  const size_t wtap = (size_t)a.Cout * a.Cin;
+  auto stage_w = [&](int t, int c, int slot) {
+    const __bf16* wt = a.w + (size_t)t * wtap + c * 64;
+#pragma unroll
+    for (int i = 0; i < WP; ++i) glds16(wt + wrow[i], wbuf + slot * W_BYTES + (wpiece0 + i) * 1024);
+  };
+  // cursor (tap, chunk) of step q
+  auto step_tc = [&](int q, int& tq, int& cq) {
+    cq = q / T;
+    tq = q - cq * T;
+  };
+
+  // lane pixel of block j: m0 + 64 wm + 32 j + (lane & 31)
+  int prel[MB], px[MB], py[MB];
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    int m = m0 + wm * 64 + j * 32 + (lane & 31);
+    m = m < a.M ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    py[j] = fdiv(rem, a.divS);
+    px[j] = rem - py[j] * S;
+    prel[j] = m - m0 + G;
+  }
+  f32x16 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const int swzw = ((lane & 31) >> 1) & 7;
+  const int wrow0 = (wn * (BN / 2) + (lane & 31)) * 128;
+  const int ep_mrow = m0 + wm * 64 + (lane & 31);
+  const int ep_nbase = n0 + wn * (BN / 2);
+  ConvEpilogue32<NB, MB, MODE> ep;
+  const int ep_at = nK > 3 ? nK - 3 : 0;
+
+  // prologue: zero rows, chunk 0's halo by all waves, W(0) by group 0
+  if (wave < NHBUF) {
+    for (int o = lane * 16; o < 16 * 128; o += 64 * 16)
+      *(uint4*)(hbuf + wave * H_BYTES + HDATA * 128 + o) = make_uint4(0u, 0u, 0u, 0u);
+  }
+  for (int k = wave; k < H_PIECES; k += 8) halo_piece(0, k, 0);
+  stage_w(0, 0, 0);
+  wait_vmcnt0();
+  if (grp == 1 && nK > 1) {  // group 1 runs its weight half two steps ahead
+    int t1, c1;
+    step_tc(1, t1, c1);
+    stage_w(t1, c1, 1);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger
+  __builtin_amdgcn_sched_barrier(0);
+
+  int c = 0, t = 0, kh = 0, kw = 0, wslot = 0;
+  const uint64_t st_begin = STAMP ? __builtin_amdgcn_s_memtime() : 0;
+  for (int p = 0; p < nK; ++p) {
+    H32_STAMP(0);
+    const char* hb = hbuf + (NHBUF == 2 ? (c & 1) : 0) * H_BYTES;
+    const char* wb = wbuf + wslot * W_BYTES;
+    const int toff = (kh - K / 2) * S + (kw - K / 2);
+    int abase[MB], aswz[MB];
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      const bool ok = (unsigned)(py[j] + kh - K / 2) < (unsigned)S && (unsigned)(px[j] + kw - K / 2) < (unsigned)S;
+      const int r = prel[j] + toff;
+      const int row = ok ? r : HDATA + (r & 15);  // zero row with the same (parity, swizzle) bank slot
+      abase[j] = row * 128;
+      aswz[j] = (row >> 1) & 7;
+    }
+    bf16x8 xf[4][MB], wf[4][NB];
+    auto read_slice = [&](int s) {
+      const int kc = 2 * s + h;
+#pragma unroll
+      for (int j = 0; j < MB; ++j) xf[s][j] = *(const bf16x8*)(hb + abase[j] + ((kc ^ aswz[j]) << 4));
+      const int wo = wrow0 + ((kc ^ swzw) << 4);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wf[s][i] = *(const bf16x8*)(wb + wo + i * 32 * 128);
+    };
+    read_slice(0);
+    read_slice(1);
+    H32_STAMP(1);
+    int tn = t + 1, cn = c, khn = kh, kwn = kw + 1;
+    if (kwn == K) { kwn = 0; ++khn; }
+    if (tn == T) { tn = 0; ++cn; khn = 0; kwn = 0; }
+    if (p == ep_at) ep.load(a, ep_mrow, ep_nbase, wn);  // (older than this segment's DMA)
+    if (grp == 0) {
+      if (p + 1 < nK) stage_w(tn, cn, wslot == 2 ? 0 : wslot + 1);  // retired at the end of M0(p)
+    } else {
+      // group 1: next chunk's halo (steps 0..4 of a chunk), its half of W(p+2), then
+      // retire everything issued in earlier segments (W(p+1) half, older halo pieces)
+      int nh = 0;
+      if (K == 3 && c + 1 < CC && t < 5) {
+#pragma unroll
+        for (int i = 0; i < HP_STEP; ++i) halo_piece(c + 1, wq * HP1 + t * HP_STEP + i, (c + 1) & 1);
+        nh = HP_STEP;
+      }
+      const bool w2 = p + 2 < nK;
+      if (w2) {
+        int t2, c2;
+        step_tc(p + 2, t2, c2);
+        stage_w(t2, c2, wslot == 0 ? 2 : wslot - 1);
+      }
+      if (w2) {
+        if (nh) vmcnt_wait<HP_STEP + WP>();
+        else vmcnt_wait<WP>();
+      } else {
+        if (nh) vmcnt_wait<HP_STEP>();
+        else vmcnt_wait<0>();
+      }
+    }
+    H32_STAMP(2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    H32_STAMP(3);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    H32_STAMP(4);
+    // ---- MFMA segment: slices 0-1 with the reads of slices 2-3 interleaved
+    __builtin_amdgcn_s_setprio(1);
+    read_slice(2);
+    read_slice(3);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < MB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s][i], xf[s][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int g = 0; g < MB + NB; ++g) {  // 2 ds_reads per MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 2 * NB * MB - (MB + NB), 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 2; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < MB; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s][i], xf[s][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    H32_STAMP(5);
+    __builtin_amdgcn_sched_barrier(0);
+    if (grp == 0) wait_vmcnt0();  // W(p+1) landed before the barrier that precedes its readers
+    H32_STAMP(6);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    H32_STAMP(7);
+    if constexpr (STAMP) {
+#pragma unroll
+      for (int i = 0; i < 7; ++i) st_sum[i] += ts[i + 1] - ts[i];
+    }
+    t = tn; c = cn; kh = khn; kw = kwn;
+    wslot = wslot == 2 ? 0 : wslot + 1;
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) {
+      unsigned long long* d = a.dbg + ((size_t)blockIdx.x * 8 + wave) * 8;
+#pragma unroll
+      for (int i = 0; i < 7; ++i) d[i] = st_sum[i];
+      d[7] = __builtin_amdgcn_s_memtime() - st_begin;
+    }
+  }
+#undef H32_STAMP
+  if (grp == 0) __builtin_amdgcn_s_barrier();
+  ep.store(a, acc, ep_mrow);
+}
+
 // largest halo span (rows) of any 256-pixel tile, cached per geometry
 static int halo2_rows_needed(int M, int S, int HPi, int K, int offi) {
   static int cM = -1, cS = -1, cH = -1, cK = -1, cO = -1, cR = 0;
@@ -829,6 +1687,69 @@ static void launch_fwd_halo2(const ConvFwdArgs& a, hipStream_t st) {
 }
 
 template <int BN, int MODE>
+static void launch_fwd_hpp(const ConvFwdArgs& a_in, hipStream_t st) {
+  constexpr int smem = 2 * HC_ROWS * 128 + 3 * BN * 128;
+  if constexpr (BN == 192 && MODE == MODE_BIAS_RELU) {
+    if (g_conv_dbg) {  // diagnostic instantiation with segment stamps
+      static bool attr_d = false;
+      if (!attr_d) {
+        hipFuncSetAttribute((const void*)conv_fwd_hpp_kernel<BN, MODE, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        attr_d = true;
+      }
+      ConvFwdArgs a = a_in;
+      a.dbg = g_conv_dbg;
+      dim3 grid((a.M + H2_BM - 1) / H2_BM, a.Cout / BN);
+      hipLaunchKernelGGL((conv_fwd_hpp_kernel<BN, MODE, true>), grid, dim3(512), smem, st, a);
+      return;
+    }
+  }
+  const ConvFwdArgs& a = a_in;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_hpp_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);
+    attr = true;
+  }
+  dim3 grid((a.M + H2_BM - 1) / H2_BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_hpp_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
+}
+
+template <int BN, int MODE, int K>
+static void launch_fwd_h32(const ConvFwdArgs& a_in, hipStream_t st) {
+  constexpr int smem = (K == 3 ? 2 * (H32_DATA3 + 16) : (H32_DATA5 + 16)) * 128 + 3 * BN * 128;
+  ConvFwdArgs a = a_in;
+  dim3 grid((a.M + H2_BM - 1) / H2_BM, a.Cout / BN);
+  if constexpr (BN == 192 && MODE == MODE_BIAS_RELU && K == 3) {
+    if (g_conv_dbg) {  // diagnostic instantiation with segment stamps
+      static bool attr_d = false;
+      if (!attr_d) {
+        hipFuncSetAttribute((const void*)conv_fwd_h32_kernel<BN, MODE, K, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        attr_d = true;
+      }
+      a.dbg = g_conv_dbg;
+      hipLaunchKernelGGL((conv_fwd_h32_kernel<BN, MODE, K, true>), grid, dim3(512), smem, st, a);
+      return;
+    }
+  }
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_h32_kernel<BN, MODE, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_fwd_h32_kernel<BN, MODE, K>), grid, dim3(512), smem, st, a);
+}
+
+// the 32x32 halo kernel applies (3x3 any Cin; 5x5 with one 64-channel chunk)
+static bool h32_ok(const ConvFwdArgs& a) {
+  if (a.K == 3) return H2_BM + 2 * (a.S + 1) <= H32_DATA3;
+  if (a.K == 5) return a.Cin == 64 && H2_BM + 4 * (a.S + 1) <= H32_DATA5;
+  return false;
+}
+
+template <int BN, int MODE>
 static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   const bool halo_ok = a.K == 3 && a.HPi == a.HPo && a.offi == 0 && a.Po == 1 && a.HPo + 1 <= 32 &&
                        (a.S + 2) * (a.S + 2) * 0 + 256 + 2 * (a.HPo + 1) <= HALO_ROWS;
@@ -837,6 +1758,21 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     return;
   }
   int bm = g_fwd_bm;
+  if (bm == 6) {  // compact halo + ping-pong on 32x32x16 MFMA
+    if (h32_ok(a)) {
+      if (a.K == 3) launch_fwd_h32<BN, MODE, 3>(a, st);
+      else launch_fwd_h32<BN, MODE, 5>(a, st);
+      return;
+    }
+    bm = 0;
+  }
+  if (bm == 5) {  // halo + ping-pong kernel (3x3, halo fits)
+    if (a.K == 3 && H2_BM + 2 * (a.S + 1) <= HC_DATA) {
+      launch_fwd_hpp<BN, MODE>(a, st);
+      return;
+    }
+    bm = 0;
+  }
   if (bm == 2) {  // interior-halo kernel when the tile's halo fits
     if (halo2_rows_needed(a.M, a.S, a.HPi, a.K, a.offi) <= H2_ROWS && BN <= 192) {
       launch_fwd_halo2<BN, MODE>(a, st);
@@ -850,11 +1786,17 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   if (bm <= 0)
     bm = (MODE != MODE_MASK && MODE != MODE_MASKBITS && a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
   // tile codes: 128 / 256 (64-pixel waves), 2568 (BM 256, 128-pixel waves: 4 waves, 1 per SIMD)
-  if (bm == 32) launch_fwd_ring<BN, MODE>(a, st);
+  if (bm == 4) launch_fwd_pp<BN, MODE>(a, st);
+  else if (bm == 32) launch_fwd_ring<BN, MODE>(a, st);
   else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
   else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);  // epilogue loads after the loop
   else if (bm == 2568) launch_fwd_bm<BN, MODE, 256, 8>(a, st);
   else if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);  // 96x96 per wave, 147 KB LDS
+  else if (bm == 7) {  // 384-pixel tile on the 32x32x16 MFMA (BN multiple of 64)
+    if constexpr (BN % 64 == 0) launch_fwd_bm<BN, MODE, 384, 6, false, false, true>(a, st);
+  } else if (bm == 8) {  // 256-pixel tile on the 32x32x16 MFMA
+    if constexpr (BN % 64 == 0) launch_fwd_bm<BN, MODE, 256, 4, false, false, true>(a, st);
+  }
   else launch_fwd_bm<BN, MODE, 128, 4>(a, st);
 }
 

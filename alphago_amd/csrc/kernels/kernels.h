@@ -21,6 +21,7 @@ struct ConvFwdArgs {
   int HPi, offi;       // input padded side, (input pad - K/2)
   int HPo, Po;         // output padded side and pad
   FastDiv divSS, divS; // filled by the launcher
+  unsigned long long* dbg;  // diagnostic segment-cycle stamps (set_conv_debug), else null
 };
 
 struct ConvWgradArgs {
@@ -134,6 +135,7 @@ struct ConvFp8Args {
 };
 
 void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
+void set_conv_debug(unsigned long long* buf);  // non-null: the ping-pong forward records per-segment cycles
 void set_conv_fwd_tile(int bm);  // 0 = auto, -1 = halo kernel, 128/256 = gather kernel tile (A/B tests)
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 int wgrad_stage_pixels();

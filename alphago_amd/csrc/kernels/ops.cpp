@@ -412,6 +412,16 @@ void quantize_fp8(const Tensor& x, const Tensor& y, double scale) {
 }
 
 void set_conv_tile(int64_t bm) { agk::set_conv_fwd_tile((int)bm); }
+// diagnostic: per-wave segment cycle sums of the ping-pong forward, 8 uint64 per wave
+void set_conv_debug(const c10::optional<Tensor>& buf) {
+  if (buf.has_value()) {
+    CHECK_DEV(*buf);
+    TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "int64 buffer");
+    agk::set_conv_debug(reinterpret_cast<unsigned long long*>(buf->data_ptr<int64_t>()));
+  } else {
+    agk::set_conv_debug(nullptr);
+  }
+}
 void set_wgrad_variant(int64_t v) { agk::set_wgrad_variant((int)v); }
 int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) { return agk::wgrad_tap_group((int)cout, (int)cin, (int)K); }
 
@@ -452,6 +462,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("fp8_act_scales(Tensor(a!) amax, Tensor(b!) scales8, Tensor(c!) osc, int margin) -> ()");
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
+  m.def("set_conv_debug(Tensor? buf) -> ()", &set_conv_debug);
   m.def("set_wgrad_variant(int v) -> ()", &set_wgrad_variant);
   m.def("wgrad_tap_group(int cout, int cin, int K) -> int", &wgrad_tap_group);
 }

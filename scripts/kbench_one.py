@@ -3,9 +3,12 @@ import sys, torch
 from alphago_amd import ops
 ops.load()
 which = sys.argv[1]; B = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+import os
 if which.endswith("ring"):  # forward/dgrad on the ring-pipelined tiling
     torch.ops.alphago_amd.set_conv_tile(32)
     which = which[:-4]
+if os.environ.get("ALPHAGO_AMD_CONV_TILE"):
+    torch.ops.alphago_amd.set_conv_tile(int(os.environ["ALPHAGO_AMD_CONV_TILE"]))
 dev = torch.device("cuda"); S, F = 19, 192; M = B * S * S
 x = ops.padded_empty(B, S, 1, F, dev); x[:, 1:20, 1:20].normal_()
 y = ops.padded_empty(B, S, 1, F, dev)
