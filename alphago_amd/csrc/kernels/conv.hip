@@ -136,7 +136,7 @@ __device__ __forceinline__ void conv_store_tile(const ConvFwdArgs& a, const f32x
 template <int NB, int MB, int MODE>
 struct ConvEpilogue32;
 
-template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false>
+template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false>
 __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
   constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
@@ -195,16 +195,16 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     const __bf16* wt = a.w + st_w + st_c0;
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) glds16(wt + brow[i], base + A_BYTES + (wave * B_ROWS_PW + i * 8) * 128);
+    // branch-free cursor advance (selects), so a caller can interleave the
+    // DMA with MFMAs inside one basic block
     st_c0 += 64;
-    if (st_c0 == a.Cin) {
-      st_c0 = 0;
-      st_w += wtap;
-      st_a += a.Cin;
-      if (++st_kw == a.K) {
-        st_kw = 0;
-        st_a += (a.HPi - a.K) * a.Cin;
-      }
-    }
+    const bool wrap = st_c0 == a.Cin;
+    st_c0 = wrap ? 0 : st_c0;
+    st_w += wrap ? wtap : 0;
+    st_kw += wrap ? 1 : 0;
+    const bool wrap2 = st_kw == a.K;
+    st_kw = wrap2 ? 0 : st_kw;
+    st_a += (wrap ? a.Cin : 0) + (wrap2 ? (a.HPi - a.K) * a.Cin : 0);
   };
 
   f32x4 acc[NB][MB];
@@ -293,6 +293,64 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     ConvEpilogue32<NB2, MB2, MODE> ep2;
     ep2.load(a, m0 + wm * 16 * MB + l31, n0 + wn * (BN / 2), wn);
     ep2.store(a, acc2, m0 + wm * 16 * MB + l31);
+    return;
+  }
+  if constexpr (!PIPE && ILV) {
+    // The 2-buffer loop issues the next stage's LDS-DMA as one burst at the top
+    // of every step; with both waves of a SIMD in lockstep the matrix pipe
+    // idles while they wait on DMA issue.  Here the burst is spread through
+    // the first k-half's MFMAs (one DMA piece per MPD MFMAs, order pinned with
+    // sched_barrier) so DMA issue overlaps matrix work.
+    constexpr int NDMA = A_INSTR + B_INSTR;
+    constexpr int NMF = NB * MB;
+    constexpr int MPD = NMF / (NDMA + 1);
+    auto mfma_range = [&](int f0, int f1) {
+#pragma unroll
+      for (int f = 0; f < NMF; ++f)
+        if (f >= f0 && f < f1) acc[f / MB][f % MB] = mfma16x16x32(wa[f / MB], xa[f % MB], acc[f / MB][f % MB]);
+    };
+    for (int ks = 0; ks < nK; ++ks) {
+      const int cur = ks & 1;
+      const char* base = smem + cur * STAGE;
+      const bool more = ks + 1 < nK;
+      read_frags(base, 0, xa, wa);
+      char* nb = smem + (cur ^ 1) * STAGE;
+      const __bf16* wt = a.w + st_w + st_c0;
+      const __bf16* xs = a.x + st_a + st_c0;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int d = 0; d < NDMA; ++d) {
+        mfma_range(d * MPD, (d + 1) * MPD);
+        __builtin_amdgcn_sched_barrier(0);
+        if (more) {
+          if (d < A_INSTR) glds16(xs + arow[d], nb + (wave * A_ROWS_PW + d * 8) * 128);
+          else glds16(wt + brow[d - A_INSTR], nb + A_BYTES + (wave * B_ROWS_PW + (d - A_INSTR) * 8) * 128);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mfma_range(NDMA * MPD, NMF);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      // advance the staging cursor (branch-free)
+      st_c0 += 64;
+      const bool wrap = st_c0 == a.Cin;
+      st_c0 = wrap ? 0 : st_c0;
+      st_w += wrap ? wtap : 0;
+      st_kw += wrap ? 1 : 0;
+      const bool wrap2 = st_kw == a.K;
+      st_kw = wrap2 ? 0 : st_kw;
+      st_a += (wrap ? a.Cin : 0) + (wrap2 ? (a.HPi - a.K) * a.Cin : 0);
+      read_frags(base, 1, xa, wa);
+      __builtin_amdgcn_s_setprio(1);
+      mfmas(xa, wa);
+      __builtin_amdgcn_s_setprio(0);
+      wait_vmcnt0();
+      __syncthreads();
+    }
+    ep.load(a, ep_mrow, ep_nbase, wn);
+    ep.store(a, acc, ep_mrow);
     return;
   }
   if constexpr (!PIPE) {  // one fragment set (large wave tiles): read, then MFMA, per k-half
@@ -919,17 +977,18 @@ static void launch_fwd_halo(const ConvFwdArgs& a_in, hipStream_t st) {
 
 static int g_fwd_bm = 0;  // 0 = auto
 
-template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false>
+template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32>,
+    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32>), grid, dim3(BM / MBW * 8), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV>), grid, dim3(BM / MBW * 8), smem, st,
+                     a);
 }
 
 
@@ -1792,6 +1851,8 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);  // epilogue loads after the loop
   else if (bm == 2568) launch_fwd_bm<BN, MODE, 256, 8>(a, st);
   else if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);  // 96x96 per wave, 147 KB LDS
+  else if (bm == 9) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);  // DMA spread through MFMAs
+  else if (bm == 10) launch_fwd_bm<BN, MODE, 256, 4, false, false, false, true>(a, st);
   else if (bm == 7) {  // 384-pixel tile on the 32x32x16 MFMA (BN multiple of 64)
     if constexpr (BN % 64 == 0) launch_fwd_bm<BN, MODE, 384, 6, false, false, true>(a, st);
   } else if (bm == 8) {  // 256-pixel tile on the 32x32x16 MFMA
