@@ -27,7 +27,7 @@ def main():
     F, L = (16, 2) if small else (192, 12)
     pol = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
     val = CNNValue(VALUE_FEATURES, filters_per_layer=F, layers=L, device=dev)
-    trees = int(sys.argv[1]) if len(sys.argv) > 1 else (4 if small else 64)
+    trees = int(sys.argv[1]) if len(sys.argv) > 1 else (4 if small else 256)  # 256 trees x 16 leaves saturate the GPU better than 64 (150k vs 49k evals/s bf16)
     playouts = int(sys.argv[2]) if len(sys.argv) > 2 else (32 if small else 800)
     lpt = 16
     s = BatchedMCTS(pol, val, n_trees=trees, seed=0)

@@ -30,7 +30,7 @@ from alphago_amd.search.mcts import BatchedMCTS  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--trees", type=int, default=64, help="concurrent games (trees) per GPU")
+    ap.add_argument("--trees", type=int, default=256, help="concurrent games (trees) per GPU (256: ~150k leaf evals/s bf16 per GPU vs 49k at 64)")
     ap.add_argument("--playouts", type=int, default=1600)
     ap.add_argument("--moves", type=int, default=3, help="moves played per game in the timed region")
     ap.add_argument("--leaves", type=int, default=16, help="leaves per tree per round")
