@@ -35,7 +35,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=25)  # a cold GPU needs ~0.2 s of load before its clocks settle
     ap.add_argument("--batch", type=int, default=1024, help="per-GPU minibatch (boards)")
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--layers", type=int, default=12)
