@@ -1839,11 +1839,12 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     }
     bm = 0;
   }
-  // forward: 96x96-per-wave tiles (147 KB LDS).  dgrad keeps the 112-KB tile:
-  // it runs concurrently with wgrad (48 KB) on the other stream and the two
-  // only share a CU when their LDS fits together.
-  if (bm <= 0)
-    bm = (MODE != MODE_MASK && MODE != MODE_MASKBITS && a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
+  // forward and dgrad: 96x96-per-wave tiles (147 KB LDS).  dgrad used to keep
+  // a 112-KB tile so that a wgrad workgroup (48 KB) could share its CU, but the
+  // concurrent pair is bound by the same per-CU operand delivery either way;
+  // the larger tile moves fewer bytes per MFMA (bench: 106.2k -> 108.5k pos/s,
+  // scripts/bench_variants.sh).
+  if (bm <= 0) bm = (a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
   // tile codes: 128 / 256 (64-pixel waves), 2568 (BM 256, 128-pixel waves: 4 waves, 1 per SIMD)
   if (bm == 4) launch_fwd_pp<BN, MODE>(a, st);
   else if (bm == 32) launch_fwd_ring<BN, MODE>(a, st);
