@@ -1,0 +1,114 @@
+"""The reference's module paths and public names (AlphaGo/*, interface/*) are
+available under ``alphago_amd`` with the same call signatures, so code written
+against the reference switches by renaming the top-level package."""
+import importlib
+
+import numpy as np
+import pytest
+
+REFERENCE_API = {
+    # reference module -> names it defines (AlphaGo/go.py:3-352, ai.py, mcts.py, util.py, ...)
+    "go": ["WHITE", "BLACK", "EMPTY", "PASS_MOVE", "GameState", "IllegalMove"],
+    "ai": ["GreedyPolicyPlayer", "ProbabilisticPolicyPlayer"],
+    "mcts": ["TreeNode", "MCTS", "ParallelMCTS"],
+    "util": ["flatten_idx", "unflatten_idx", "_parse_sgf_move", "_sgf_init_gamestate", "sgf_to_gamestate",
+             "sgf_iter_states"],
+    "models.policy": ["CNNPolicy"],
+    "preprocessing.preprocessing": ["get_board", "get_turns_since", "get_liberties", "get_capture_size",
+                                    "get_self_atari_size", "get_liberties_after", "get_ladder_capture",
+                                    "get_ladder_escape", "get_sensibleness", "FEATURES", "DEFAULT_FEATURES",
+                                    "Preprocess"],
+    "preprocessing.game_converter": ["SizeMismatchError", "game_converter", "run_game_converter"],
+    "training.supervised_policy_trainer": ["one_hot_action", "shuffled_hdf5_batch_generator",
+                                           "MetadataWriterCallback", "BOARD_TRANSFORMATIONS", "run_training"],
+    "training.reinforcement_policy_trainer": ["make_training_pairs", "train_batch", "run"],
+    "training.reinforcement_value_trainer": [],
+    "interface.gtp_wrapper": ["GTPGameConnector", "run_gtp"],
+    "interface.Play": ["play_match"],
+}
+
+
+@pytest.mark.parametrize("mod", sorted(REFERENCE_API))
+def test_reference_names_exist(mod):
+    m = importlib.import_module("alphago_amd." + mod)
+    for name in REFERENCE_API[mod]:
+        assert hasattr(m, name), "alphago_amd.%s.%s missing" % (mod, name)
+
+
+def _position():
+    from alphago_amd import go
+    st = go.GameState(size=9)
+    for mv in [(2, 2), (3, 3), (2, 3), (3, 2), (4, 4), (2, 4), (5, 5), (3, 4), (6, 6)]:
+        st.do_move(mv)
+    return st
+
+
+def test_feature_functions_match_preprocess():
+    from alphago_amd.preprocessing import preprocessing as P
+    st = _position()
+    full = P.Preprocess(["board", "turns_since", "liberties", "capture_size", "self_atari_size",
+                         "liberties_after", "sensibleness"]).state_to_tensor(st)[0]
+    parts = [P.get_board(st), P.get_turns_since(st), P.get_liberties(st), P.get_capture_size(st),
+             P.get_self_atari_size(st), P.get_liberties_after(st), P.get_sensibleness(st)]
+    assert np.array_equal(np.concatenate(parts), full)
+    # a smaller ``maximum`` folds the tail planes into the last one
+    lib8, lib3 = P.get_liberties(st), P.get_liberties(st, maximum=3)
+    assert lib3.shape == (3, 9, 9)
+    assert np.array_equal(lib3[:2], lib8[:2]) and np.array_equal(lib3[2], lib8[2:].max(axis=0))
+
+
+def test_sl_trainer_helpers():
+    from alphago_amd.training import supervised_policy_trainer as T
+    y = T.one_hot_action(np.array([3, 5], dtype=np.uint8), 9)  # an h5py-style row (one cell)
+    assert y.sum() == 1 and y[3, 5] == 1
+    a = np.arange(81).reshape(9, 9)
+    ref = [a, np.rot90(a, 1), np.rot90(a, 2), np.rot90(a, 3), np.fliplr(a), np.flipud(a), a.T,
+           np.fliplr(np.rot90(a, 1))]
+    for f, r in zip(T.BOARD_TRANSFORMATIONS, ref):
+        assert np.array_equal(f(a), r)
+    states = np.random.default_rng(0).integers(0, 2, (5, 3, 9, 9)).astype(np.uint8)
+    actions = np.array([[0, 1], [2, 3], [4, 5], [6, 7], [8, 0]], dtype=np.uint8)
+    gen = T.shuffled_hdf5_batch_generator(states, actions, [0, 1, 2, 3, 4], 2, T.BOARD_TRANSFORMATIONS)
+    b1 = next(gen)
+    b2 = next(gen)
+    assert b1[0].shape == (2, 3, 9, 9) and b1[1].shape == (2, 81)
+    assert (b1[1].sum(axis=1) == 1).all() and b1[0] is not b2[0]  # fresh buffers
+
+
+def test_gtp_game_connector():
+    from alphago_amd import go
+    from alphago_amd.interface.gtp_wrapper import PASS, GTPGameConnector
+
+    class PassPlayer(object):
+        def get_move(self, state):
+            return go.PASS_MOVE
+
+    class CornerPlayer(object):
+        def get_move(self, state):
+            return (0, 0)
+
+    c = GTPGameConnector(PassPlayer())
+    c.set_size(9)
+    assert c.make_move(go.BLACK, (1, 1))
+    assert not c.make_move(go.WHITE, (1, 1))  # occupied
+    assert c.get_move(go.WHITE) == PASS
+    c2 = GTPGameConnector(CornerPlayer())
+    assert c2.get_move(go.BLACK) == (1, 1)
+
+
+def test_rl_make_training_pairs_and_train_batch_cpu():
+    import torch
+    from alphago_amd.models.policy import CNNPolicy
+    from alphago_amd.training import reinforcement_policy_trainer as R
+
+    torch.manual_seed(0)
+    feats = ["board", "ones", "turns_since"]
+    pol = CNNPolicy(feats, board=9, filters_per_layer=8, layers=2, device="cpu")
+    X, y, w = R.make_training_pairs(pol, pol, feats, 3, board_size=9, max_moves=12, seed=1)
+    assert len(X) == len(y) == len(w) == 3
+    for xi, yi in zip(X, y):
+        assert xi.shape[1:] == (12, 9, 9) and yi.shape == (len(xi), 81)
+        assert (yi.sum(axis=1) == 1).all()
+    before = [p.detach().clone() for p in pol.model.parameters()]
+    R.train_batch(pol, X, y, [1] * len(X), 0.05)
+    assert any(not torch.equal(a, b) for a, b in zip(before, pol.model.parameters()))
