@@ -26,3 +26,20 @@ for s, e, n in seg:
     tot[key] += (e - s) / 1e3; cnt[key] += 1
 for k, v in sorted(tot.items(), key=lambda kv: -kv[1]):
     print("  %-70s %6d calls %9.1f us/step" % (k, cnt[k] // steps, v / steps))
+# per-queue busy time (main stream vs the wgrad stream) and the serial tail after the last dgrad
+qcol = "Queue_Id" if "Queue_Id" in rows[0] else ("Stream_Id" if "Stream_Id" in rows[0] else None)
+if qcol:
+    kq = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r[qcol]) for r in rows),
+                key=lambda t: t[0])
+    segq = [k for k in kq if t0 <= k[0] <= t1]
+    per = collections.defaultdict(float)
+    for s, e, n, q in segq:
+        per[q] += (e - s) / 1e3
+    for q, v in sorted(per.items()):
+        print("  queue %-6s kernel time %9.1f us/step" % (q, v / steps))
+    # last step: time from the end of the last dgrad (conv_fwd in MODE 3) to the step end
+    last = [k for k in segq if k[0] >= ks[ends[-2] + 1][0]]
+    dg = [k for k in last if "conv_fwd" in k[2] and (", 3," in k[2] or "Li3E" in k[2] or "<192, 3" in k[2])]
+    if dg:
+        tail_start = max(e for s, e, n, q in dg)
+        print("  serial tail after the last dgrad: %.1f us" % ((last[-1][1] - tail_start) / 1e3))
