@@ -1,0 +1,227 @@
+// Shared pieces of the implicit-GEMM conv kernels (conv.hip: production
+// kernels and dispatch; conv_fwd_variants.hip: the forward kernel lab).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace agk {
+
+template <int N>
+__device__ __forceinline__ void vmcnt_wait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else static_assert(N < 0, "unsupported vmcnt");
+}
+
+__device__ __forceinline__ void vmcnt_wait_dyn(int n) {
+  switch (n) {
+    case 0: vmcnt_wait<0>(); break;
+    case 1: vmcnt_wait<1>(); break;
+    case 2: vmcnt_wait<2>(); break;
+    case 3: vmcnt_wait<3>(); break;
+    case 4: vmcnt_wait<4>(); break;
+    case 5: vmcnt_wait<5>(); break;
+    case 6: vmcnt_wait<6>(); break;
+    case 7: vmcnt_wait<7>(); break;
+    default: vmcnt_wait<8>(); break;
+  }
+}
+
+// Shared epilogue of the forward/dgrad kernels: lane owns output channels
+// nbase + 16 i + [0, 4) of pixel mrow + 16 j.  load() issues every operand
+// load (bias, or the ReLU' mask of dgrad) with clamped pixel indices — no
+// per-element branches, so the loads overlap instead of forming 24
+// load -> wait -> store round trips; the kernels call it a few K-steps before
+// the end of the main loop so the mask read hides under the last MFMAs.
+template <int NB, int MB, int MODE>
+struct ConvEpilogue {
+  int ooff[MB];
+  int pix[MB];
+  f32x4 bb[NB];
+  bf16x4 mk[NB][MB];
+  uint32_t mw[MB];
+  int mslot, mwords;
+
+  // ReLU' bitmask layout: per padded pixel, (Cout/BN)*8 32-bit words; word
+  // (blockIdx.y*8 + wn*4 + lane/16) holds bit 4i+r for channel nbase+16i+r —
+  // exactly the channels one lane owns, so producer and consumer never
+  // exchange data (12x less traffic than re-reading the bf16 activation).
+  __device__ __forceinline__ void load(const ConvFwdArgs& a, int mrow, int nbase, int wn = 0) {
+    const int SS = a.S * a.S;
+    mslot = blockIdx.y * 8 + wn * 4 + ((threadIdx.x & 63) >> 4);
+    mwords = gridDim.y * 8;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      int m = mrow + j * 16;
+      m = m < a.M ? m : a.M - 1;
+      const int b = fdiv(m, a.divSS);
+      const int rem = m - b * SS;
+      const int ii = fdiv(rem, a.divS);
+      const int jj = rem - ii * a.S;
+      pix[j] = (b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po;
+      ooff[j] = pix[j] * a.Cout + nbase;
+    }
+    if constexpr (MODE == MODE_BIAS_RELU) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) bb[i] = *(const f32x4*)(a.bias + nbase + i * 16);
+    } else if constexpr (MODE == MODE_MASK) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j)
+#pragma unroll
+        for (int i = 0; i < NB; ++i) mk[i][j] = *(const bf16x4*)(a.mask + ooff[j] + i * 16);
+    } else if constexpr (MODE == MODE_MASKBITS) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j) mw[j] = a.mbits_in[(size_t)pix[j] * mwords + mslot];
+    }
+  }
+
+  __device__ __forceinline__ void store(const ConvFwdArgs& a, const f32x4 (&acc)[NB][MB], int mrow) const {
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      if (mrow + j * 16 >= a.M) continue;
+      uint32_t bits = 0u;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        f32x4 v = acc[i][j];
+        if constexpr (MODE == MODE_BIAS_RELU) {
+          v[0] = fmaxf(v[0] + bb[i][0], 0.f);
+          v[1] = fmaxf(v[1] + bb[i][1], 0.f);
+          v[2] = fmaxf(v[2] + bb[i][2], 0.f);
+          v[3] = fmaxf(v[3] + bb[i][3], 0.f);
+        } else if constexpr (MODE == MODE_MASK) {
+          v[0] = (float)mk[i][j][0] > 0.f ? v[0] : 0.f;
+          v[1] = (float)mk[i][j][1] > 0.f ? v[1] : 0.f;
+          v[2] = (float)mk[i][j][2] > 0.f ? v[2] : 0.f;
+          v[3] = (float)mk[i][j][3] > 0.f ? v[3] : 0.f;
+        } else if constexpr (MODE == MODE_MASKBITS) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = ((mw[j] >> (4 * i + r)) & 1u) ? v[r] : 0.f;
+        }
+        bf16x4 o;
+        o[0] = (__bf16)v[0];
+        o[1] = (__bf16)v[1];
+        o[2] = (__bf16)v[2];
+        o[3] = (__bf16)v[3];
+        if constexpr (MODE == MODE_BIAS_RELU) {
+          // the bit records what the bf16 value the dgrad would re-read says: y > 0
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bits |= ((float)o[r] > 0.f ? 1u : 0u) << (4 * i + r);
+        }
+        *(bf16x4*)(a.y + ooff[j] + i * 16) = o;
+      }
+      if constexpr (MODE == MODE_BIAS_RELU)
+        if (a.mbits_out) a.mbits_out[(size_t)pix[j] * mwords + mslot] = bits;
+    }
+  }
+};
+
+template <int NB, int MB, int MODE>
+__device__ __forceinline__ void conv_store_tile(const ConvFwdArgs& a, const f32x4 (&acc)[NB][MB], int mrow,
+                                                int nbase, int wn) {
+  ConvEpilogue<NB, MB, MODE> ep;
+  ep.load(a, mrow, nbase, wn);
+  ep.store(a, acc, mrow);
+}
+
+// ---------------- epilogue for the 32x32x16 MFMA layout (weights as A, pixels as B)
+// acc[i][j] (f32x16) of a wave: output channel nbase + 32 i + 8 g + 4 h + r
+// (h = lane >> 5, reg = 4 g + r) of pixel mrow + 32 j, mrow = the lane's pixel
+// of block 0.  ReLU' bitmask: per padded pixel (Cout/BN)*8 words; the lane's
+// 16*NB bits (bit 16 i + 4 g + r) sit in words blockIdx.y*8 + wn*4 + 2h + {0, 1}.
+template <int NB, int MB, int MODE>
+struct ConvEpilogue32 {
+  int ooff[MB];
+  int pix[MB];
+  f32x4 bb[NB][4];
+  bf16x4 mk[NB][MB][4];
+  uint2 mw[MB];
+  int mslot, mwords;
+
+  __device__ __forceinline__ void load(const ConvFwdArgs& a, int mrow, int nbase, int wn) {
+    const int SS = a.S * a.S;
+    const int h = (threadIdx.x & 63) >> 5;
+    mslot = blockIdx.y * 8 + wn * 4 + 2 * h;
+    mwords = gridDim.y * 8;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      int m = mrow + j * 32;
+      m = m < a.M ? m : a.M - 1;
+      const int b = fdiv(m, a.divSS);
+      const int rem = m - b * SS;
+      const int ii = fdiv(rem, a.divS);
+      const int jj = rem - ii * a.S;
+      pix[j] = (b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po;
+      ooff[j] = pix[j] * a.Cout + nbase + 4 * h;
+    }
+    if constexpr (MODE == MODE_BIAS_RELU) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) bb[i][g] = *(const f32x4*)(a.bias + nbase + 4 * h + i * 32 + g * 8);
+    } else if constexpr (MODE == MODE_MASK) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j)
+#pragma unroll
+        for (int i = 0; i < NB; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) mk[i][j][g] = *(const bf16x4*)(a.mask + ooff[j] + i * 32 + g * 8);
+    } else if constexpr (MODE == MODE_MASKBITS) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j) mw[j] = *(const uint2*)(a.mbits_in + (size_t)pix[j] * mwords + mslot);
+    }
+  }
+
+  __device__ __forceinline__ void store(const ConvFwdArgs& a, const f32x16 (&acc)[NB][MB], int mrow) const {
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      if (mrow + j * 32 >= a.M) continue;
+      uint32_t bits[2] = {0u, 0u};
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][j][4 * g + r];
+          const int bit0 = 16 * i + 4 * g;
+          if constexpr (MODE == MODE_BIAS_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r] + bb[i][g][r], 0.f);
+          } else if constexpr (MODE == MODE_MASK) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (float)mk[i][j][g][r] > 0.f ? v[r] : 0.f;
+          } else if constexpr (MODE == MODE_MASKBITS) {
+            const uint32_t w = bit0 < 32 ? mw[j].x : mw[j].y;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = ((w >> ((bit0 & 31) + r)) & 1u) ? v[r] : 0.f;
+          }
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (__bf16)v[r];
+          if constexpr (MODE == MODE_BIAS_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) bits[bit0 >> 5] |= ((float)o[r] > 0.f ? 1u : 0u) << ((bit0 & 31) + r);
+          }
+          *(bf16x4*)(a.y + ooff[j] + i * 32 + g * 8) = o;
+        }
+      if constexpr (MODE == MODE_BIAS_RELU)
+        if (a.mbits_out) *(uint2*)(a.mbits_out + (size_t)pix[j] * mwords + mslot) = make_uint2(bits[0], bits[1]);
+    }
+  }
+};
+
+
+// forward variants in conv_fwd_variants.hip (tile codes -1, 2, 4, 5, 6, 32);
+// returns false when the variant does not apply to the geometry
+bool launch_conv_fwd_variant(int code, const ConvFwdArgs& a, int mode, hipStream_t st);
+
+}  // namespace agk
