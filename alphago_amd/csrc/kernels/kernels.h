@@ -32,6 +32,7 @@ struct ConvWgradArgs {
   int M, S, Cin, Cout, K, T;
   int HPi, offi, HPo, Po;
   int ksteps_per_split, nsplit;
+  int cin_real;        // real input channels (<= Cin); the zero padding above it is skipped when possible
   FastDiv divSS, divS; // filled by the launcher
 };
 

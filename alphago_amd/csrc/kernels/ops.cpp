@@ -69,7 +69,7 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
 
 // slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
-                int64_t Pin, int64_t Po) {
+                int64_t Pin, int64_t Po, int64_t cin_real) {
   CHECK_DEV(x); CHECK_DEV(dz); CHECK_DEV(slab); CHECK_DEV(dbslab);
   CHECK_BF16(x); CHECK_BF16(dz); CHECK_F32(slab); CHECK_F32(dbslab);
   CHECK_CONTIG(x); CHECK_CONTIG(dz); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
@@ -86,6 +86,7 @@ void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Ten
   a.dbias_slab = dbslab.data_ptr<float>();
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K; a.T = (int)(K * K);
   a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
+  a.cin_real = (cin_real > 0 && cin_real < Cin) ? (int)cin_real : (int)Cin;
   const int sp = agk::wgrad_stage_pixels();
   const int nks = (a.M + sp - 1) / sp;
   a.nsplit = (int)nsplit;
@@ -437,7 +438,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
       "Tensor(b!)? mbits=None) -> ()");
-  m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po) -> ()");
+  m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def(
       "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor? weight, Tensor(a!)? dz, Tensor(b!)? loss, "

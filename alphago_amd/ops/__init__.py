@@ -96,8 +96,10 @@ def mbits_words(cout_p: int) -> int:
     return cout_p // bn * 8
 
 
-def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1):
-    _ops().conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po)
+def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1, cin_real: int = 0):
+    """Split-K weight gradient into ``slab``; ``cin_real`` (< padded Cin) lets
+    the kernel skip zero-padded input channels (only slab columns < cin_real are written)."""
+    _ops().conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real)
 
 
 def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, beta: float = 0.0):

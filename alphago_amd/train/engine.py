@@ -290,7 +290,7 @@ class HipConvTrainer:
         ns = self.nsplit[l]
         slab = self._slab[:ns * T * self.Fp * cin_p].view(ns, T, self.Fp, cin_p)
         dbs = self._dbslab[:ns * self.Fp].view(ns, self.Fp)
-        ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1)
+        ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0)
         ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)
 
     def backward_trunk(self) -> None:

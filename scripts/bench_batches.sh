@@ -1,5 +1,7 @@
 #!/bin/bash
+# bench.py at several per-GPU batch sizes (after one warm-up run)
 export PYTHONPATH=$PWD
-for b in ${@:-1024 1536 2048 1024}; do
-  timeout -k 10 240 python bench.py --steps 20 --warmup 5 --batch $b 2>/dev/null | python -c "import sys,json; d=json.loads(sys.stdin.read()); print('batch', $b, d['value'], d['ms_per_step'])"
+timeout -k 10 120 python bench.py --steps 10 --warmup 10 > /dev/null 2>&1
+for b in ${@:-1024 1088 1024 1088}; do
+  timeout -k 10 240 python bench.py --steps 40 --warmup 20 --batch $b 2>/dev/null | python -c "import sys,json; d=json.loads(sys.stdin.read()); print('batch', $b, d['value'], d['ms_per_step'])"
 done

@@ -110,6 +110,30 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     assert _rel_err(gb, ref_b) < 2e-3
 
 
+@pytest.mark.parametrize("K,Pin", [(5, 2), (3, 1)])
+def test_conv_wgrad_thin_input(ops, cuda_device, K, Pin):
+    """48 real input planes padded to 64 (the policy net's first layer): the
+    cin_real path computes only the real channels, matching the fp32 reference."""
+    torch.manual_seed(5)
+    B, Cin, Cout, S = 5, 48, 192, 19
+    x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
+    dz = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
+    ref_w = torch.nn.grad.conv2d_weight(x, (Cout, Cin, K, K), dz, padding=K // 2)
+    ref_b = dz.sum(dim=(0, 2, 3))
+    xp = ops.to_padded(x, Pin, 64)
+    dzp = ops.to_padded(dz, 1)
+    ns = ops.wgrad_splits(B * S * S, K * K)
+    slab = torch.full((ns, K * K, Cout, 64), float("nan"), device=cuda_device)  # unwritten columns must be ignored
+    dbs = torch.zeros(ns, Cout, device=cuda_device)
+    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin)
+    gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
+    gb = torch.zeros(Cout, device=cuda_device)
+    ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert _rel_err(gw, ref_w) < 2e-3
+    assert _rel_err(gb, ref_b) < 2e-3
+
+
 def test_policy_head_train(ops, cuda_device):
     torch.manual_seed(3)
     B, C, S = 7, 192, 19
