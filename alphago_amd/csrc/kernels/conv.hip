@@ -298,6 +298,187 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
 
 static int g_fwd_bm = 0;  // 0 = auto
 
+// ------------------------------------ forward, pixel operand straight from L2
+// Probe (scripts/probes/glds_rate.hip): LDS-DMA fills a CU at ~46 B/clk and
+// serialises with ds_read traffic, so in the LDS-staged kernels the LDS port
+// (pixel + weight DMA, plus fragment reads) is about as busy as the matrix
+// pipe.  Here only the weights go through LDS; each wave loads its pixel
+// fragments (16 B per lane, 8 channels of one pixel row) with ordinary
+// global_load_dwordx4 into registers, one step ahead (register double
+// buffer).  Waves own disjoint pixels (8 x 48 = 384 per workgroup) and all BN
+// channels, so no pixel row is loaded twice in a workgroup; per 64-channel
+// step a CU moves 24 KB through LDS-DMA instead of 72 KB.
+// Epilogue and ReLU'-bitmask layout are those of conv_fwd_kernel (the wave's
+// two channel halves are stored as wn = 0 and wn = 1).
+template <int BN, int MODE>
+__global__ __launch_bounds__(512, 1) void conv_fwd_ga_kernel(ConvFwdArgs a) {
+  constexpr int MB = 3;          // 16-pixel blocks per wave (48 pixels)
+  constexpr int NB = BN / 16;    // 16-channel blocks per wave (all BN channels)
+  constexpr int NH = NB / 2;     // blocks per channel half
+  constexpr int BM = 8 * 16 * MB;
+  constexpr int W_BYTES = BN * 128;
+  constexpr int WPIECES = BN / 8;       // 1-KB weight pieces per step
+  constexpr int WPW = (WPIECES + 7) / 8;
+  static_assert(NB % 2 == 0, "two channel halves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int nwg = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int m0 = tile * BM;
+  const int n0 = blockIdx.y * BN;
+  const int SS = a.S * a.S;
+  const int CC = a.Cin >> 6;
+  const int nK = a.K * a.K * CC;
+
+  // Buffer resources: per-lane byte offsets stay fixed in one VGPR each, the
+  // (wave-uniform) step cursor goes in the scalar offset, and loads past the
+  // tensor return zero instead of faulting.
+  const int nimg = a.M / SS;
+  const long long xbytes = (long long)nimg * a.HPi * a.HPi * a.Cin * 2;
+  const long long wbytes = (long long)a.K * a.K * a.Cout * a.Cin * 2;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)(xbytes < 0x7fffffffLL ? xbytes : 0x7fffffffLL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w, (short)0, (int)(wbytes < 0x7fffffffLL ? wbytes : 0x7fffffffLL), 0x00020000);
+  // pixel fragment sources: lane -> pixel (block j, row lane&15), 16-B chunk lane>>4 of the k-half
+  int xrow[MB];
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    int m = m0 + wave * 16 * MB + j * 16 + (lane & 15);
+    m = m < a.M ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    xrow[j] = (((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + (lane >> 4) * 8) * 2;
+  }
+  // weight DMA: wave w stages pieces [w*WPW, ...) of the BN x 64-ch tile (128-B rows, swizzled)
+  int wrow[WPW];
+#pragma unroll
+  for (int i = 0; i < WPW; ++i) {
+    const int r = (wave * WPW + i) * 8 + (lane >> 3);
+    wrow[i] = ((n0 + (r < BN ? r : 0)) * a.Cin + (((lane & 7) ^ ((r >> 1) & 7)) << 3)) * 2;
+  }
+  const int wtap = a.Cout * a.Cin;
+
+  // step cursor in elements (branch-free advance; wave-uniform, lives in SGPRs)
+  int c0 = 0, kw = 0, aoff = 0, woff = 0;
+  auto advance = [&]() {
+    c0 += 64;
+    const bool wrap = c0 == a.Cin;
+    c0 = wrap ? 0 : c0;
+    woff += wrap ? wtap : 0;
+    kw += wrap ? 1 : 0;
+    const bool wrap2 = kw == a.K;
+    kw = wrap2 ? 0 : kw;
+    aoff += (wrap ? a.Cin : 0) + (wrap2 ? (a.HPi - a.K) * a.Cin : 0);
+  };
+  // Weights go global -> VGPR -> ds_write rather than by LDS-DMA: the compiler
+  // does not count LDS-DMA in its vmcnt bookkeeping, and a DMA issued between
+  // two register loads makes every later compiler wait over-strict.
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  u32x4 wreg[WPW];
+  auto load_w = [&]() {
+#pragma unroll
+    for (int i = 0; i < WPW; ++i) wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, wrow[i], (woff + c0) * 2, 0);
+  };
+  auto store_w = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < WPW; ++i)
+      if (wave * WPW + i < WPIECES) *(u32x4*)(smem + slot * W_BYTES + (wave * WPW + i) * 1024 + lane * 16) = wreg[i];
+  };
+  auto load_x = [&](bf16x8 (&xf)[MB], int kk) {
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(xr, xrow[j], (aoff + c0 + kk * 32) * 2, 0);
+      xf[j] = __builtin_bit_cast(bf16x8, v);
+    }
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int swz = (lane & 15) >> 1;
+  const int wr0 = (lane & 15) * 128;
+
+  // Rolling register buffer: x[kk] is refilled with the next step's k-half as
+  // soon as this step's MFMAs on it have issued, so a load has about one step
+  // of matrix work to land in.  vmcnt order per step: W(next) (WPW), x[0], x[1].
+  // The loads are unconditional (the last step's run past the tensors, where
+  // the buffer range check returns zeros): with a conditional issue the
+  // compiler's vmcnt bookkeeping merges the skip path and waits for loads that
+  // are a whole step younger than the ones the MFMAs need.  Issue order per
+  // step: W(next), x[0](next), x[1](next) -- each consumer waits for exactly
+  // its own loads.
+  bf16x8 x[2][MB];
+  load_w();
+  load_x(x[0], 0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_x(x[1], 1);
+  advance();
+  store_w(0);
+  __syncthreads();
+  for (int ks = 0; ks < nK; ++ks) {
+    const char* wb = smem + (ks & 1) * W_BYTES;
+    load_w();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = ((kk << 2) + (lane >> 4)) ^ swz;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 wf[NH];
+#pragma unroll
+        for (int i = 0; i < NH; ++i) wf[i] = *(const bf16x8*)(wb + wr0 + (h * NH + i) * 16 * 128 + (ch << 4));
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < NH; ++i)
+#pragma unroll
+          for (int j = 0; j < MB; ++j) acc[h * NH + i][j] = mfma16x16x32(wf[i], x[kk][j], acc[h * NH + i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      load_x(x[kk], kk);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    advance();
+    store_w((ks + 1) & 1);
+    __syncthreads();
+  }
+  wait_vmcnt0();
+
+  const int mrow = m0 + wave * 16 * MB + (lane & 15);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    f32x4 ah[NH][MB];
+#pragma unroll
+    for (int i = 0; i < NH; ++i)
+#pragma unroll
+      for (int j = 0; j < MB; ++j) ah[i][j] = acc[h * NH + i][j];
+    ConvEpilogue<NH, MB, MODE> ep;
+    ep.load(a, mrow, n0 + h * (BN / 2) + ((lane >> 4) << 2), h);
+    ep.store(a, ah, mrow);
+  }
+}
+
+template <int BN, int MODE>
+static void launch_fwd_ga(const ConvFwdArgs& a, hipStream_t st) {
+  constexpr int smem = 2 * BN * 128;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_ga_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  constexpr int BM = 8 * 16 * 3;
+  dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_ga_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
+}
+
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
@@ -334,6 +515,7 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);  // epilogue loads after the loop
   else if (bm == 2568) launch_fwd_bm<BN, MODE, 256, 8>(a, st);
   else if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);  // 96x96 per wave, 147 KB LDS
+  else if (bm == 11) launch_fwd_ga<BN, MODE>(a, st);  // pixel operand straight from L2, weights via LDS
   else if (bm == 9) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
   else if (bm == 10) launch_fwd_bm<BN, MODE, 256, 4, false, false, false, true>(a, st);
   else if (bm == 7) launch_fwd_bm<BN, MODE, 384, 6, false, false, true>(a, st);
