@@ -22,6 +22,14 @@ static constexpr int kLadderDepth = 96;  // plies; a corner-to-corner ladder is 
 
 static bool hunter_wins(const GameState& s, int prey, int depth);
 
+// Per-thread scratch states, one per ladder ply: copy-assigning into a reused
+// slot keeps the history vector's capacity, so reading a ladder allocates
+// nothing (a fresh GameState copy per ply was a malloc + free each).
+static GameState& ladder_slot(int depth) {
+  thread_local std::vector<GameState> slots(kLadderDepth + 3, GameState(19));
+  return slots[depth];
+}
+
 // prey to move, prey group in atari.  True if every prey reply loses.
 static bool prey_loses(const GameState& s, int prey, int depth) {
   if (depth > kLadderDepth) return false;
@@ -47,7 +55,8 @@ static bool prey_loses(const GameState& s, int prey, int depth) {
   for (int k = 0; k < nc; ++k) {
     int mv = cand[k];
     if (mv < 0 || !s.is_legal_for(mv, pc)) continue;
-    GameState s2 = s;
+    GameState& s2 = ladder_slot(depth + 1);
+    s2 = s;
     s2.try_move(mv, pc);
     if (s2.board[prey] != pc) continue;
     int lc = s2.libc[s2.head[prey]];
@@ -71,7 +80,8 @@ static bool hunter_wins(const GameState& s, int prey, int depth) {
     if (l < 0) break;
     b.clear(l);
     if (!s.is_legal_for(l, -pc)) continue;
-    GameState s2 = s;
+    GameState& s2 = ladder_slot(depth + 1);
+    s2 = s;
     s2.try_move(l, -pc);
     if (s2.board[prey] != pc) return true;  // captured outright
     if (s2.libc[s2.head[prey]] == 1 && prey_loses(s2, prey, depth + 1)) return true;
@@ -85,7 +95,8 @@ bool ladder_capture_at(const GameState& s, int m) {
   for (int i = 0; i < s.g->nnbr[m]; ++i) {
     int q = s.g->nbr[m][i];
     if (s.board[q] != -me || s.libc[s.head[q]] != 2) continue;
-    GameState s2 = s;
+    GameState& s2 = ladder_slot(0);
+    s2 = s;
     s2.try_move(m, me);
     if (s2.board[q] != -me) return true;  // captured
     if (s2.libc[s2.head[q]] == 1 && prey_loses(s2, q, 0)) return true;
@@ -99,7 +110,8 @@ bool ladder_escape_at(const GameState& s, int m) {
   for (int i = 0; i < s.g->nnbr[m]; ++i) {
     int q = s.g->nbr[m][i];
     if (s.board[q] != me || s.libc[s.head[q]] != 1) continue;
-    GameState s2 = s;
+    GameState& s2 = ladder_slot(0);
+    s2 = s;
     s2.try_move(m, me);
     if (s2.board[q] != me) continue;
     int lc = s2.libc[s2.head[q]];
@@ -123,14 +135,26 @@ void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* met
   meta[0] = s.ko;
   meta[1] = s.current_player;
   if (ladder) {
+    // Only liberties of an opponent group in (pre-)atari with 2 liberties
+    // (capture) or of an own group in atari (escape) can be non-zero: collect
+    // them from the group roots' liberty sets instead of testing every point.
+    std::memset(ladder, 0, np);
+    const int me = s.current_player;
+    Bits cand;
+    cand.zero();
     for (int p = 0; p < np; ++p) {
-      uint8_t v = 0;
-      if (s.board[p] == EMPTY && s.is_legal(p)) {
+      if (s.board[p] == EMPTY || s.head[p] != p) continue;
+      if ((s.board[p] == -me && s.libc[p] == 2) || (s.board[p] == me && s.libc[p] == 1)) cand.orr(s.libs[p]);
+    }
+    for (int i = 0; i < BW; ++i)
+      for (uint64_t w = cand.w[i]; w; w &= w - 1) {
+        const int p = i * 64 + __builtin_ctzll(w);
+        if (p >= np || s.board[p] != EMPTY || !s.is_legal(p)) continue;
+        uint8_t v = 0;
         if (ladder_capture_at(s, p)) v |= 1;
         if (ladder_escape_at(s, p)) v |= 2;
+        ladder[p] = v;
       }
-      ladder[p] = v;
-    }
   }
 }
 

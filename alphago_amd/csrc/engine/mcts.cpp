@@ -1,14 +1,32 @@
 #include "mcts.h"
 
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <cmath>
+#include <new>
 #include <thread>
 
 #include "featurize.h"
 
 
 namespace ag {
+
+static_assert(sizeof(Node) == 32, "NodeStore block size assumes 32-byte nodes");
+
+void NodeStore::grow() {
+  const size_t bytes = sizeof(Node) * (size_t)kBlock;
+  void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) throw std::bad_alloc();
+  // no populate: pages fault on first touch inside the apply() workers, in parallel
+  // (MAP_POPULATE / MADV_POPULATE_WRITE of whole blocks measured 3x slower with 8 workers)
+  blocks_.push_back(static_cast<Node*>(p));
+}
+
+NodeStore::~NodeStore() {
+  for (Node* b : blocks_) munmap(b, sizeof(Node) * (size_t)kBlock);
+}
 
 static Node make_node(int parent, int move, float P) {
   Node n;
@@ -83,12 +101,15 @@ void Forest::backup(SearchTree& tr, int leaf, double v_leaf_to_move, bool remove
   tr.sims += 1;
 }
 
-void Forest::gather_trees(const std::vector<int>& trees, int leaves_per_tree, std::vector<Leaf>& pend,
-                          std::vector<GameState>& states) {
-  for (int t : trees) {
+void Forest::gather_trees(const int* trees, int ntrees, int leaves_per_tree, std::vector<Leaf>& pend,
+                          std::vector<int>& slot_ids, int slot_base) {
+  int next = slot_base;  // this worker owns slots [slot_base, slot_base + ntrees * leaves_per_tree)
+  for (int ti = 0; ti < ntrees; ++ti) {
+    const int t = trees[ti];
     SearchTree& tr = trees_.at(t);
     for (int k = 0; k < leaves_per_tree; ++k) {
-      GameState st = tr.root_state;
+      GameState& st = slots_[next];
+      st = tr.root_state;
       int u = 0;
       tr.nodes[0].vl += 1;
       int depth = 0;
@@ -115,7 +136,7 @@ void Forest::gather_trees(const std::vector<int>& trees, int leaves_per_tree, st
           if (nd.status == 0) {
             nd.status = 1;
             pend.push_back({t, u});
-            states.push_back(std::move(st));
+            slot_ids.push_back(next++);
             break;
           }
         }
@@ -137,7 +158,7 @@ void Forest::gather_trees(const std::vector<int>& trees, int leaves_per_tree, st
 
 int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
   if (!pending_.empty()) throw std::runtime_error("gather called with pending evaluations; call apply first");
-  leaf_states_.clear();
+  leaf_slot_.clear();
   std::vector<int> all;
   if (!which) {
     all.resize(trees_.size());
@@ -145,24 +166,27 @@ int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
     which = &all;
   }
   const int n = (int)which->size();
+  const size_t need = (size_t)n * leaves_per_tree;
+  if (slots_.size() < need) slots_.resize(need, GameState(trees_.empty() ? 19 : trees_[0].root_state.n));
   const int T = std::max(1, std::min(threads_, n));
   if (T == 1) {
-    gather_trees(*which, leaves_per_tree, pending_, leaf_states_);
+    gather_trees(which->data(), n, leaves_per_tree, pending_, leaf_slot_, 0);
   } else {
-    // contiguous blocks of trees per worker; concatenated in tree order
+    // contiguous blocks of trees per worker (each with its own slot range); concatenated in tree order
     std::vector<std::vector<Leaf>> pend(T);
-    std::vector<std::vector<GameState>> sts(T);
+    std::vector<std::vector<int>> ids(T);
     std::vector<std::thread> pool;
     for (int w = 0; w < T; ++w)
       pool.emplace_back([&, w]() {
         const int lo = (int)((int64_t)n * w / T), hi = (int)((int64_t)n * (w + 1) / T);
-        std::vector<int> mine(which->begin() + lo, which->begin() + hi);
-        gather_trees(mine, leaves_per_tree, pend[w], sts[w]);
+        pend[w].reserve((size_t)(hi - lo) * leaves_per_tree);
+        ids[w].reserve((size_t)(hi - lo) * leaves_per_tree);
+        gather_trees(which->data() + lo, hi - lo, leaves_per_tree, pend[w], ids[w], lo * leaves_per_tree);
       });
     for (auto& th : pool) th.join();
     for (int w = 0; w < T; ++w) {
       pending_.insert(pending_.end(), pend[w].begin(), pend[w].end());
-      for (auto& s : sts[w]) leaf_states_.push_back(std::move(s));
+      leaf_slot_.insert(leaf_slot_.end(), ids[w].begin(), ids[w].end());
     }
   }
   total_evals_ += (int64_t)pending_.size();
@@ -172,12 +196,12 @@ int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
 void Forest::leaf_features(uint8_t* out, int threads) const {
   int L = (int)pending_.size();
   if (L == 0) return;
-  size_t stride = (size_t)nplanes_ * leaf_states_[0].np;
+  size_t stride = (size_t)nplanes_ * leaf_state(0).np;
   int T = std::max(1, std::min(threads, L));
   std::vector<std::thread> pool;
   for (int t = 0; t < T; ++t)
     pool.emplace_back([&, t]() {
-      for (int i = t; i < L; i += T) featurize(leaf_states_[i], fids_.data(), (int)fids_.size(), out + i * stride);
+      for (int i = t; i < L; i += T) featurize(leaf_state(i), fids_.data(), (int)fids_.size(), out + i * stride);
     });
   for (auto& th : pool) th.join();
 }
@@ -185,11 +209,11 @@ void Forest::leaf_features(uint8_t* out, int threads) const {
 void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) const {
   int L = (int)pending_.size();
   if (L == 0) return;
-  const int np = leaf_states_[0].np;
+  const int np = leaf_state(0).np;
   int T = std::max(1, std::min(ladder ? threads : 1, L));  // without ladders this is a memcpy-class walk
   auto work = [&](int t) {
     for (int i = t; i < L; i += T)
-      encode_state(leaf_states_[i], board + (size_t)i * np, ages + (size_t)i * np, meta + 2 * i,
+      encode_state(leaf_state(i), board + (size_t)i * np, ages + (size_t)i * np, meta + 2 * i,
                    ladder ? ladder + (size_t)i * np : nullptr);
   };
   if (T == 1) {
@@ -203,7 +227,7 @@ void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* l
 
 void Forest::leaf_masks(uint8_t* out) const {
   for (size_t i = 0; i < pending_.size(); ++i) {
-    const GameState& s = leaf_states_[i];
+    const GameState& s = leaf_state(i);
     for (int p = 0; p < s.np; ++p) out[i * s.np + p] = s.is_legal(p) && !s.is_eye(p, s.current_player);
   }
 }
@@ -237,7 +261,7 @@ void Forest::apply_range(int i0, int i1, const float* priors, const float* value
   for (int i = i0; i < i1; ++i) {
     SearchTree& tr = trees_[pending_[i].tree];
     const int u = pending_[i].node;
-    const GameState& st = leaf_states_[i];
+    const GameState& st = leaf_state(i);
     const float* pr = priors + (size_t)i * st.np;
     const uint8_t* mk = mask ? mask + (size_t)i * st.np : nullptr;
     moves.clear();
@@ -258,7 +282,7 @@ void Forest::apply_range(int i0, int i1, const float* priors, const float* value
       for (auto& v : ps) v = 1.f;
       sum = (double)ps.size();
     }
-    int first = (int)tr.nodes.size();
+    int first = tr.nodes.size();
     for (size_t j = 0; j < moves.size(); ++j) tr.nodes.push_back(make_node(u, moves[j], (float)(ps[j] / sum)));
     Node& nd = tr.nodes[u];
     nd.first_child = first;
@@ -295,6 +319,7 @@ void Forest::apply(const float* priors, const float* values, const uint8_t* mask
     for (auto& th : pool) th.join();
   }
   pending_.clear();
+  leaf_slot_.clear();
 }
 
 void Forest::add_root_noise(int t, double alpha, double eps) {
@@ -367,21 +392,21 @@ void Forest::advance(int t, int move) {
     return;
   }
   // BFS copy of the reused subtree (children stay contiguous)
-  std::vector<Node> nn;
-  nn.reserve(tr.nodes.size());
+  NodeStore& nn = tr.spare;
+  nn.clear();
   Node root = tr.nodes[found];
   root.parent = -1;
   nn.push_back(root);
   std::vector<int> old_of;  // old index of each new node
   old_of.push_back(found);
-  for (size_t k = 0; k < nn.size(); ++k) {
+  for (int k = 0; k < nn.size(); ++k) {
     int o = old_of[k];
     const Node& on = tr.nodes[o];
     if (on.nchild > 0 && on.first_child >= 0) {
-      int first = (int)nn.size();
+      int first = nn.size();
       for (int i = 0; i < on.nchild; ++i) {
         Node c = tr.nodes[on.first_child + i];
-        c.parent = (int)k;
+        c.parent = k;
         nn.push_back(c);
         old_of.push_back(on.first_child + i);
       }

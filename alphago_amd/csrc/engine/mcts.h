@@ -33,13 +33,46 @@ struct Node {
   int8_t status;  // 0 unexpanded, 1 pending evaluation, 2 expanded, 3 terminal
 };
 
+// Node storage in fixed 2-MiB blocks that are never moved or freed while the
+// forest lives: growth never copies a tree (a vector doubling would), node
+// references stay valid across appends, and clear() keeps the blocks (and
+// their faulted-in pages) for the next search.
+class NodeStore {
+ public:
+  static constexpr int kShift = 16;  // 65536 nodes x 32 B = 2 MiB per block
+  static constexpr int kBlock = 1 << kShift;
+  NodeStore() = default;
+  NodeStore(const NodeStore&) = delete;
+  NodeStore& operator=(const NodeStore&) = delete;
+  NodeStore(NodeStore&& o) noexcept : blocks_(std::move(o.blocks_)), size_(o.size_) { o.size_ = 0; }
+  ~NodeStore();
+  int size() const { return size_; }
+  void clear() { size_ = 0; }
+  Node& operator[](int i) { return blocks_[i >> kShift][i & (kBlock - 1)]; }
+  const Node& operator[](int i) const { return blocks_[i >> kShift][i & (kBlock - 1)]; }
+  void push_back(const Node& n) {
+    if ((size_ >> kShift) >= (int)blocks_.size()) grow();
+    (*this)[size_++] = n;
+  }
+  void swap(NodeStore& o) {
+    blocks_.swap(o.blocks_);
+    std::swap(size_, o.size_);
+  }
+
+ private:
+  void grow();
+  std::vector<Node*> blocks_;
+  int size_ = 0;
+};
+
 struct Leaf {
   int tree;
   int node;
 };
 
 struct SearchTree {
-  std::vector<Node> nodes;
+  NodeStore nodes;
+  NodeStore spare;  // scratch for advance()'s subtree copy (keeps its blocks)
   GameState root_state;
   int64_t sims = 0;
   SearchTree() : root_state(19) {}
@@ -56,7 +89,7 @@ class Forest {
   // Descend all (or the listed) trees; returns number of leaves queued for evaluation.
   int gather(int leaves_per_tree, const std::vector<int>* which = nullptr);
   int n_pending() const { return (int)pending_.size(); }
-  const GameState& leaf_state(int i) const { return leaf_states_[i]; }
+  const GameState& leaf_state(int i) const { return slots_[leaf_slot_[i]]; }
   int feature_planes() const { return nplanes_; }
   // uint8 features (L, F, n, n) and sensible-move masks (L, n*n); threaded.
   void leaf_features(uint8_t* out, int threads) const;
@@ -83,7 +116,11 @@ class Forest {
 
   std::vector<SearchTree> trees_;
   std::vector<Leaf> pending_;
-  std::vector<GameState> leaf_states_;
+  // Leaf states live in a persistent slot pool (a GameState is ~20 KB of
+  // inline arrays): each gather copies the root into a reused slot and plays
+  // the path there, so a leaf costs one copy and no allocation.
+  std::vector<GameState> slots_;
+  std::vector<int> leaf_slot_;
   std::vector<std::vector<int>> leaf_paths_;
   double c_puct_, lmbda_;
   int rollout_limit_, playout_depth_, vloss_;
@@ -92,7 +129,8 @@ class Forest {
   int nplanes_ = 0;
   int64_t total_evals_ = 0;
   int threads_ = 1;
-  void gather_trees(const std::vector<int>& trees, int lpt, std::vector<Leaf>& pend, std::vector<GameState>& states);
+  void gather_trees(const int* trees, int ntrees, int lpt, std::vector<Leaf>& pend, std::vector<int>& slot_ids,
+                    int slot_base);
   void apply_range(int i0, int i1, const float* priors, const float* values, const uint8_t* mask);
 };
 

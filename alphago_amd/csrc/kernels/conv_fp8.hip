@@ -200,8 +200,241 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_kernel(ConvFp8Args a) {
   }
 }
 
+// ------------------------------------------ pixel operand straight from L2
+// PMC on conv_fwd_fp8_kernel (profiles/r1_conv_pmc_fp8.md): the matrix pipe
+// is busy 27 % of the time and waves wait on the stage DMA -- each 128-B LDS
+// row is assembled from two 64-B activation rows, and a 24-MFMA step is too
+// short to cover 56 KB of LDS-DMA.  Here each wave loads its own pixel
+// fragments (32 B per lane: half of one 64-B chunk) with buffer loads into
+// registers, one step ahead, and only the weights (24 KB per step for BN 192)
+// go through LDS, by VGPR + ds_write so the compiler's vmcnt bookkeeping stays
+// exact.  Waves own disjoint pixels (8 x 32 = 256 per workgroup) and all BN
+// channels.
+template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8>
+__global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) {
+  // MB: 16-pixel blocks per wave; the BN/16 channel blocks are read from LDS in NPART parts
+  constexpr int NB = BN / 16;   // 16-channel blocks per wave
+  constexpr int NH = NB / NPART;
+  static_assert(NB % NPART == 0, "channel blocks must split evenly into parts");
+  constexpr int BM = 8 * 16 * MB;
+  constexpr int W_BYTES = BN * 128;
+  constexpr int WP = W_BYTES / 16 / 512;  // 16-B weight pieces per thread and step
+  static_assert(W_BYTES % (16 * 512) == 0, "weight tile must split evenly over 512 threads");
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int nwg = gridDim.x;
+  const int xcd = blockIdx.x & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (blockIdx.x >> 3);
+  const int m0 = tile * BM;
+  const int n0 = blockIdx.y * BN;
+  const int SS = a.S * a.S;
+  const int CC = a.Cin >> 6;
+  const int nK = a.nch >> 1;
+  const int qmax = a.K * a.K * CC - 1;
+  const int sx = a.scales[0], sw = a.scales[1];
+
+  const int nimg = a.M / SS;
+  const long long xbytes = (long long)nimg * a.HPi * a.HPi * a.Cin;
+  const long long wbytes = (long long)a.nch * a.Cout * 64;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.x, (short)0, (int)(xbytes < 0x7fffffffLL ? xbytes : 0x7fffffffLL), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.w, (short)0, (int)(wbytes < 0x7fffffffLL ? wbytes : 0x7fffffffLL), 0x00020000);
+
+  // B operand (pixels): lane -> pixel (block j, lane&15), K bytes [32g, 32g+32), g = lane>>4:
+  // g < 2 from chunk q0 of the step, g >= 2 from chunk q1
+  const int g = lane >> 4;
+  int xbase[MB];
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    int m = m0 + wave * 16 * MB + j * 16 + (lane & 15);
+    m = m < a.M ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    xbase[j] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + (g & 1) * 32;
+  }
+  // A operand (weights) staging: piece p = tid + 512 i -> LDS row p/8, physical 16-B chunk p%8
+  int wsrc[WP], wdst[WP];
+#pragma unroll
+  for (int i = 0; i < WP; ++i) {
+    const int p = threadIdx.x + 512 * i;
+    const int r = p >> 3, pc = p & 7;
+    const int lc = pc ^ fp8_swz(r);
+    wsrc[i] = (((lc >> 2) * a.Cout) + n0 + r) * 64 + (lc & 3) * 16;
+    wdst[i] = r * 128 + pc * 16;
+  }
+  auto chunk_off = [&](int q) {
+    q = q < qmax ? q : qmax;
+    const int t = q / CC;
+    const int c = q - t * CC;
+    const int kh = t / a.K;
+    const int kw = t - kh * a.K;
+    return (kh * a.HPi + kw) * a.Cin + c * 64;
+  };
+  u32x4 wreg[WP];
+  auto load_w = [&](int ks) {
+    const int q0 = 2 * ks < a.nch ? 2 * ks : a.nch - 2;
+#pragma unroll
+    for (int i = 0; i < WP; ++i) wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, wsrc[i], q0 * a.Cout * 64, 0);
+  };
+  auto store_w = [&](int slot) {
+#pragma unroll
+    for (int i = 0; i < WP; ++i) *(u32x4*)(smem + slot * W_BYTES + wdst[i]) = wreg[i];
+  };
+  auto load_x = [&](i32x8 (&xf)[MB], int ks) {
+    const int off0 = chunk_off(2 * ks), off1 = chunk_off(2 * ks + 1);
+    const int off = g >= 2 ? off1 : off0;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(xr, xbase[j] + off, 0, 0);
+      const u32x4 hi = __builtin_amdgcn_raw_buffer_load_b128(xr, xbase[j] + off + 16, 0, 0);
+      xf[j] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
+    }
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int r15 = lane & 15;
+  const int c0 = ((2 * g) ^ fp8_swz(r15)) << 4;
+  const int c1 = ((2 * g + 1) ^ fp8_swz(r15)) << 4;
+  const int wrow = r15 * 128;
+
+  // issue order per step: W(next) then x(next); every consumer waits for exactly its own loads
+  i32x8 xa[MB], xb[MB];
+  load_w(0);
+  load_x(xa, 0);
+  store_w(0);
+  __syncthreads();
+  auto body = [&](int ks, i32x8 (&xc)[MB], i32x8 (&xn)[MB]) {
+    const char* wb = smem + (ks & 1) * W_BYTES;
+    load_w(ks + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    load_x(xn, ks + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < NPART; ++h) {
+      i32x8 wf[NH];
+#pragma unroll
+      for (int i = 0; i < NH; ++i) {
+        const char* p = wb + wrow + (h * NH + i) * 16 * 128;
+        const int4 lo = *(const int4*)(p + c0);
+        const int4 hi = *(const int4*)(p + c1);
+        wf[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < NH; ++i)
+#pragma unroll
+        for (int j = 0; j < MB; ++j) acc[h * NH + i][j] = mfma_fp8(wf[i], xc[j], acc[h * NH + i][j], sw, sx);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    store_w((ks + 1) & 1);
+    __syncthreads();
+  };
+  int ks = 0;
+  for (; ks + 1 < nK; ks += 2) {
+    body(ks, xa, xb);
+    body(ks + 1, xb, xa);
+  }
+  if (ks < nK) body(ks, xa, xb);
+  wait_vmcnt0();
+
+  // --- epilogue: bias + ReLU, amax, bf16 and/or e4m3 stores (lane: 4 channels of one pixel per block)
+  const int nbase = n0 + ((lane >> 4) << 2);
+  const float osc = a.out_scale[0];
+  float vmax = 0.f;
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    int m = m0 + wave * 16 * MB + j * 16 + (lane & 15);
+    const bool ok = m < a.M;
+    m = ok ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    const size_t ooff = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int n = nbase + i * 16;
+      const f32x4 bb = *(const f32x4*)(a.bias + n);
+      f32x4 v = acc[i][j];
+      v[0] = fmaxf(v[0] + bb[0], 0.f);
+      v[1] = fmaxf(v[1] + bb[1], 0.f);
+      v[2] = fmaxf(v[2] + bb[2], 0.f);
+      v[3] = fmaxf(v[3] + bb[3], 0.f);
+      if (!ok) continue;
+      vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+      if constexpr (OUT_BF16) {
+        bf16x4 o;
+        o[0] = (__bf16)v[0];
+        o[1] = (__bf16)v[1];
+        o[2] = (__bf16)v[2];
+        o[3] = (__bf16)v[3];
+        *(bf16x4*)(a.y_bf16 + ooff + n) = o;
+      }
+      if constexpr (OUT_FP8) {
+        const float s0 = fminf(v[0] * osc, 448.f), s1 = fminf(v[1] * osc, 448.f);
+        const float s2 = fminf(v[2] * osc, 448.f), s3 = fminf(v[3] * osc, 448.f);
+        int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+        pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+        *(int*)(a.y_fp8 + ooff + n) = pk;
+      }
+    }
+  }
+  if (a.amax) {
+    vmax = wave_max(vmax);
+    float* red = reinterpret_cast<float*>(smem + 2 * W_BYTES);
+    if (lane == 0) red[wave] = vmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = red[0];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w]);
+      atomicMax(a.amax + (blockIdx.x & (kFp8AmaxSlots - 1)), __float_as_uint(m));
+    }
+  }
+}
+
+static int g_fp8_variant = 2;  // 0 = LDS-staged conv_fwd_fp8_kernel, 1-4 = pixel operand from L2 (tilings below)
+void set_fp8_variant(int v) { g_fp8_variant = v; }
+
+template <int BN, int MB, int NPART, bool OB, bool OF>
+static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
+  constexpr int smem = 2 * BN * 128 + 64;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  constexpr int BM = 128 * MB;
+  dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF>), grid, dim3(512), smem, st, a);
+}
+
 template <int BN, bool OB, bool OF>
 static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
+  if (g_fp8_variant != 0 && (BN * 128) % (16 * 512) == 0) {
+    if constexpr (BN == 192) {
+      // 1: 32 px/wave, weights read in 2 parts; 2: 48 px/wave, 4 parts (default);
+      // 3: 32 px/wave, 3 parts; 4: 48 px/wave, 6 parts
+      if (g_fp8_variant == 2) launch_fp8_ga<BN, 3, 4, OB, OF>(a, st);
+      else if (g_fp8_variant == 3) launch_fp8_ga<BN, 2, 3, OB, OF>(a, st);
+      else if (g_fp8_variant == 4) launch_fp8_ga<BN, 3, 6, OB, OF>(a, st);
+      else launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
+    } else {
+      launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
+    }
+    return;
+  }
   constexpr int smem = 2 * (256 * 128 + BN * 128);
   static bool attr = false;
   if (!attr) {

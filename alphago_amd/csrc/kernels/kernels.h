@@ -141,6 +141,7 @@ void set_conv_fwd_tile(int bm);  // 0 = auto, -1 = halo kernel, 128/256 = gather
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 int wgrad_stage_pixels();
 int wgrad_tap_group(int Cout, int Cin, int K);  // taps per wgrad workgroup (tap-merged 64-wide c tiles)
+void set_fp8_variant(int v);  // 0 = LDS-staged fp8 forward, 1-4 = pixel operand from L2 (2 = default)
 void set_wgrad_variant(int v);  // 0 = 2-buffer (default), 3 / 4 = ring with that many LDS slots  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);

@@ -424,6 +424,7 @@ void set_conv_debug(const c10::optional<Tensor>& buf) {
   }
 }
 void set_wgrad_variant(int64_t v) { agk::set_wgrad_variant((int)v); }
+void set_fp8_variant(int64_t v) { agk::set_fp8_variant((int)v); }
 int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) { return agk::wgrad_tap_group((int)cout, (int)cin, (int)K); }
 
 void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
@@ -465,6 +466,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
   m.def("set_conv_debug(Tensor? buf) -> ()", &set_conv_debug);
   m.def("set_wgrad_variant(int v) -> ()", &set_wgrad_variant);
+  m.def("set_fp8_variant(int v) -> ()", &set_fp8_variant);
   m.def("wgrad_tap_group(int cout, int cin, int K) -> int", &wgrad_tap_group);
 }
 

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                     help="conv forward precision (fp8 = e4m3 block-scaled MFMA forward, bf16 backward)")
+    ap.add_argument("--wgrad-wgs", type=int, default=512,
+                    help="target workgroups per wgrad launch (sets the split-K factor)")
     ap.add_argument("--profile", default=None,
                     help="after the timed run, profile 6 more steps (torch.profiler + roctx ranges) into DIR")
     args = ap.parse_args()
@@ -62,7 +64,8 @@ def main():
         torch.ops.alphago_amd.set_wgrad_variant(int(os.environ["ALPHAGO_AMD_WGRAD_VARIANT"]))
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
-    kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap, "precision": args.precision}
+    kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap, "precision": args.precision,
+                                             "wgrad_target_wgs": args.wgrad_wgs}
     trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
 
     # synthetic dataset, resident in HBM (uint8 one-hot planes + move targets)

@@ -18,8 +18,14 @@ ops.pack_weights([w], [wf], [wd])
 bias = torch.zeros(F, device=dev)
 ns = ops.wgrad_splits(M, 9)
 slab = torch.empty(ns, 9, F, F, device=dev); dbs = torch.zeros(ns, F, device=dev)
+if which == "fp8":
+    x8 = torch.zeros(x.shape, dtype=torch.uint8, device=dev); ops.quantize_fp8(x, x8, 0)
+    w8, _ = ops.pack_weights_fp8(w, F, F)
+    y8 = torch.zeros(x.shape, dtype=torch.uint8, device=dev)
+    sc = torch.tensor([127, 127], dtype=torch.int32, device=dev); osc = torch.ones(1, device=dev)
 for _ in range(10):
-    if which == "fwd": ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1)
+    if which == "fp8": ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8)
+    elif which == "fwd": ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1)
     elif which == "dgrad": ops.conv_fwd(x, wd, None, y, 3, S, 1, 1, mode=ops.MODE_MASK, mask=x)
     else: ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1)
 torch.cuda.synchronize()

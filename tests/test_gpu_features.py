@@ -73,6 +73,20 @@ def test_encode_batch_cpu():
         assert np.array_equal(lad[i] & 1, f[0]) and np.array_equal((lad[i] >> 1) & 1, f[1])
 
 
+def test_encoded_ladders_match_planes_19x19():
+    """The encoder only reads ladders at liberties of 2-liberty opponent groups
+    and 1-liberty own groups; on random 19x19 games (many ataris) its bits must
+    equal the ladder planes computed at every point."""
+    states = random_positions(40, size=19, seed=5, max_len=250)
+    _, _, _, lad = engine().encode_batch(states, True, 4)
+    nz = 0
+    for i, s in enumerate(states):
+        f = Preprocess(["ladder_capture", "ladder_escape"]).state_to_uint8(s).reshape(2, -1)
+        assert np.array_equal(lad[i] & 1, f[0]) and np.array_equal((lad[i] >> 1) & 1, f[1])
+        nz += int(f.sum())
+    assert nz > 0  # the sample does contain ladder moves
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("feats", [ALL_NO_LADDER_FEATURES, DEFAULT_FEATURES, VALUE_FEATURES + ["legal"]])
 def test_gpu_planes_match_cpu(cuda_device, feats):

@@ -264,9 +264,19 @@ def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
     assert _rel_err(ops.from_padded(dx, 1), ref_dx) < 1e-2
 
 
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("K,Cin,Cout,B", [(3, 192, 192, 5), (5, 64, 192, 3), (3, 128, 128, 4), (3, 192, 64, 2)])
-def test_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B):
-    """e4m3 conv on the block-scaled MFMA vs fp32 conv of the dequantised operands."""
+def test_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B, variant):
+    """e4m3 conv on the block-scaled MFMA vs fp32 conv of the dequantised operands
+    (variant 0: LDS-staged operands, 1-4: pixel operand loaded from L2 into registers)."""
+    torch.ops.alphago_amd.set_fp8_variant(variant)
+    try:
+        _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B)
+    finally:
+        torch.ops.alphago_amd.set_fp8_variant(2)
+
+
+def _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B):
     torch.manual_seed(3)
     S, P = 19, K // 2
     x = F.relu(torch.randn(B, Cin, S, S, device=cuda_device)) * 3.0
