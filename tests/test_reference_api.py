@@ -14,6 +14,7 @@ REFERENCE_API = {
     "util": ["flatten_idx", "unflatten_idx", "_parse_sgf_move", "_sgf_init_gamestate", "sgf_to_gamestate",
              "sgf_iter_states"],
     "models.policy": ["CNNPolicy"],
+    "models.value": ["K", "LEARNING_RATE", "DECAY", "value_trainer"],
     "preprocessing.preprocessing": ["get_board", "get_turns_since", "get_liberties", "get_capture_size",
                                     "get_self_atari_size", "get_liberties_after", "get_ladder_capture",
                                     "get_ladder_escape", "get_sensibleness", "FEATURES", "DEFAULT_FEATURES",
@@ -112,3 +113,21 @@ def test_rl_make_training_pairs_and_train_batch_cpu():
     before = [p.detach().clone() for p in pol.model.parameters()]
     R.train_batch(pol, X, y, [1] * len(X), 0.05)
     assert any(not torch.equal(a, b) for a, b in zip(before, pol.model.parameters()))
+
+
+def test_value_trainer_samples_and_trains_cpu():
+    import torch
+    from alphago_amd.models import value as V
+
+    torch.manual_seed(0)
+    rng = np.random.default_rng(0)
+    states = rng.integers(0, 2, (20, 49, 9, 9)).astype(np.uint8)
+    outcomes = rng.choice([-1, 1], 20).astype(np.int8)
+    vt = V.value_trainer(states, outcomes, minibatch=4, device="cpu", board=9, filters_per_layer=8, layers=2,
+                         dense=16)
+    x, z = next(vt.get_samples())
+    assert x.shape == (4, 49, 9, 9) and z.shape == (4,)
+    before = [p.detach().clone() for p in vt.model.parameters()]
+    loss = vt.train(steps=3, learning_rate=0.05)
+    assert np.isfinite(loss)
+    assert any(not torch.equal(a, b) for a, b in zip(before, vt.model.parameters()))
