@@ -1,0 +1,47 @@
+"""bench.py driver contract on CPU: torch.distributed.run with 1 and 4 gloo ranks.
+
+The driver runs ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``
+on one node; this rehearses the same launch (gloo instead of RCCL, tiny net, torch
+backend) and checks the single JSON line rank 0 prints: whole-job value, weak-scaling
+global batch, and the ``dpN`` parallelism tag.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("nproc", [1, 4])
+def test_bench_json_line_under_torchrun(nproc):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "2", "--warmup", "1",
+           "--backend", "torch", "--batch", "2", "--filters", "8", "--layers", "3", "--pool", "16"]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               PYTHONPATH=ROOT)
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in out
+    assert out["n_gpus"] == nproc and out["steps"] == 2 and out["warmup"] == 1
+    assert out["scaling"] == "weak" and out["higher_is_better"] is True
+    assert out["config"]["global_batch"] == 2 * nproc
+    assert out["config"]["parallelism"] == "dp%d" % nproc
+    assert out["value"] > 0
+    # value is the whole-job rate: global positions over the (max-over-ranks) timed span
+    assert abs(out["value"] - 2 * nproc * 2 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 0.01
