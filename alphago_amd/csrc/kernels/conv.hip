@@ -1045,46 +1045,83 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
 }
 
 // Sum split partials into the fp32 OIHW gradient (real channel counts) + bias.
-// Threads walk the slab in its natural [t][n][c] order (c fastest) so every
-// split read is coalesced; the OIHW write is strided but only touches the
-// (small) gradient once.
-__global__ void conv_wgrad_reduce_kernel(WgradReduceArgs a) {
-  const int total = a.T * a.Cout_real * a.Cin;
+// Fixed summation order per element (deterministic): four partial sums over
+// the splits, s_k = sum of splits sp = k (mod 4) below the last multiple of 4
+// in increasing order, the leftover splits added to s_0, then
+// (s0 + s1) + (s2 + s3).  Wave k of a 256-thread block computes s_k for 64
+// float4 elements (4 consecutive input channels of one tap and output
+// channel), 4 16-B loads in flight; the four partials meet in LDS.  The OIHW
+// write is strided but touches the (small) gradient once.
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(WgradReduceArgs a) {
+  __shared__ f32x4 part[4][64];
+  const int C4 = a.Cin >> 2;
+  const int total = a.T * a.Cout_real * C4;
   const size_t tile = (size_t)a.Cout * a.Cin;
   const size_t sstride = (size_t)a.T * tile;
-  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
-    const int c = idx % a.Cin;
-    const int tn = idx / a.Cin;
+  const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int n4 = a.nsplit & ~3;
+  for (int base = blockIdx.x * 64; base < total; base += gridDim.x * 64) {  // block-uniform trip count
+    const int idx = base + lane;
+    const int e = idx < total ? idx : total - 1;
+    const int c = (e % C4) << 2;
+    const int tn = e / C4;
     const int n = tn % a.Cout_real;
     const int t = tn / a.Cout_real;
-    if (c >= a.Cin_real) continue;
     const float* s = a.slab + (size_t)t * tile + (size_t)n * a.Cin + c;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    int sp = 0;
-    for (; sp + 4 <= a.nsplit; sp += 4) {
-      s0 += s[(size_t)sp * sstride];
-      s1 += s[(size_t)(sp + 1) * sstride];
-      s2 += s[(size_t)(sp + 2) * sstride];
-      s3 += s[(size_t)(sp + 3) * sstride];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (c < a.Cin_real) {
+      int sp = k;
+      for (; sp + 12 < n4; sp += 16) {
+        const f32x4 v0 = *(const f32x4*)(s + (size_t)sp * sstride);
+        const f32x4 v1 = *(const f32x4*)(s + (size_t)(sp + 4) * sstride);
+        const f32x4 v2 = *(const f32x4*)(s + (size_t)(sp + 8) * sstride);
+        const f32x4 v3 = *(const f32x4*)(s + (size_t)(sp + 12) * sstride);
+        acc += v0;
+        acc += v1;
+        acc += v2;
+        acc += v3;
+      }
+      for (; sp < n4; sp += 4) acc += *(const f32x4*)(s + (size_t)sp * sstride);
+      if (k == 0)
+        for (sp = n4; sp < a.nsplit; ++sp) acc += *(const f32x4*)(s + (size_t)sp * sstride);
     }
-    for (; sp < a.nsplit; ++sp) s0 += s[(size_t)sp * sstride];
-    const float sum = (s0 + s1) + (s2 + s3);
-    float* g = a.grad_w + ((size_t)n * a.Cin_real + c) * a.T + t;
-    *g = a.beta * *g + a.scale * sum;
+    part[k][lane] = acc;
+    __syncthreads();
+    if (k == 0 && idx < total && c < a.Cin_real) {
+      const f32x4 sum = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (c + i >= a.Cin_real) break;
+        float* g = a.grad_w + ((size_t)n * a.Cin_real + c + i) * a.T + t;
+        *g = (a.beta != 0.f ? a.beta * *g : 0.f) + a.scale * sum[i];  // beta 0: no read of g
+      }
+    }
+    __syncthreads();
   }
-  if (blockIdx.x == 0 && a.grad_b) {
+  if (blockIdx.x == gridDim.x - 1 && a.grad_b) {
+    // bias: one sequential sum per channel (fixed order) with 8 loads in flight --
+    // a load-add chain of nsplit dependent steps set this kernel's duration
     for (int n = threadIdx.x; n < a.Cout_real; n += blockDim.x) {
+      const float* d = a.dbias_slab + n;
       float sum = 0.f;
-      for (int sp = 0; sp < a.nsplit; ++sp) sum += a.dbias_slab[(size_t)sp * a.Cout + n];
+      int sp = 0;
+      for (; sp + 8 <= a.nsplit; sp += 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = d[(size_t)(sp + k) * a.Cout];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += v[k];
+      }
+      for (; sp < a.nsplit; ++sp) sum += d[(size_t)sp * a.Cout];
       a.grad_b[n] = a.beta * a.grad_b[n] + a.scale * sum;
     }
   }
 }
 
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st) {
-  const int total = a.T * a.Cout_real * a.Cin;
-  int blocks = (total + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
+  const int total = a.T * a.Cout_real * (a.Cin >> 2);
+  int blocks = (total + 63) / 64;
+  if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
 }
 

@@ -99,6 +99,7 @@ void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& g
   CHECK_F32(slab); CHECK_F32(grad_w); CHECK_CONTIG(grad_w);
   const int64_t nsplit = slab.size(0), T = slab.size(1), Cout = slab.size(2), Cin = slab.size(3);
   TORCH_CHECK(grad_w.dim() == 4 && grad_w.size(2) * grad_w.size(3) == T, "grad_w must be OIHW");
+  TORCH_CHECK(Cin % 4 == 0, "slab channels must be a multiple of 4 (16-byte split reads)");
   agk::WgradReduceArgs a{};
   a.slab = slab.data_ptr<float>();
   a.dbias_slab = dbslab.data_ptr<float>();

@@ -335,3 +335,38 @@ def test_relu_bitmask_dgrad_matches_mask(ops, cuda_device, tile, C):
     assert _rel_err(ops.from_padded(y, 1), F.relu(F.conv2d(x, w, b, padding=1))) < 1e-2
     assert torch.equal(d1, d3)
     assert (ops.from_padded(d3, 1) != 0).any()
+
+
+@pytest.mark.parametrize("ns,T,Cout,Cin,Cin_real,Cout_real", [(1, 9, 192, 192, 192, 192), (3, 9, 64, 64, 64, 64),
+                                                            (7, 25, 192, 64, 48, 192), (56, 9, 192, 192, 192, 192),
+                                                            (21, 9, 192, 192, 192, 152), (5, 25, 192, 64, 49, 192)])
+def test_conv_wgrad_reduce_vs_fp32(ops, cuda_device, ns, T, Cout, Cin, Cin_real, Cout_real):
+    """Split-K reduce alone: any split count (incl. < 4 and not a multiple of 4),
+    thin input (NaN in the unused slab columns), padded Cout, scale and beta
+    (accumulate into an existing gradient), bit-identical when repeated."""
+    torch.manual_seed(11)
+    K = int(round(T ** 0.5))
+    slab = torch.randn(ns, T, Cout, Cin, device=cuda_device)
+    slab[..., Cin_real:] = float("nan")
+    dbs = torch.randn(ns, Cout, device=cuda_device)
+    ref_w = slab[:, :, :Cout_real, :Cin_real].double().sum(0).permute(1, 2, 0).reshape(Cout_real, Cin_real, K, K)
+    ref_b = dbs[:, :Cout_real].double().sum(0)
+    g0w = torch.randn(Cout_real, Cin_real, K, K, device=cuda_device)
+    g0b = torch.randn(Cout_real, device=cuda_device)
+    outs = []
+    for _ in range(2):
+        gw, gb = g0w.clone(), g0b.clone()
+        ops.conv_wgrad_reduce(slab, dbs, gw, gb, 0.5, 2.0)
+        outs.append((gw, gb))
+    torch.cuda.synchronize()
+    exp_w = 2.0 * g0w.double() + 0.5 * ref_w
+    exp_b = 2.0 * g0b.double() + 0.5 * ref_b
+    assert (outs[0][0].double() - exp_w).abs().max().item() < 1e-4 * max(1.0, ns ** 0.5)
+    assert (outs[0][1].double() - exp_b).abs().max().item() < 1e-4 * max(1.0, ns ** 0.5)
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    gw = torch.full_like(g0w, float("nan"))  # beta 0 overwrites (never reads) the destination
+    gb = torch.zeros_like(g0b)
+    ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert torch.isfinite(gw).all()
+    assert (gw.double() - ref_w).abs().max().item() < 1e-4 * max(1.0, ns ** 0.5)
