@@ -62,7 +62,8 @@ PYBIND11_MODULE(_engine, m) {
   m.attr("EMPTY") = (int)EMPTY;
 
   py::class_<GameState>(m, "GameState")
-      .def(py::init<int, double>(), py::arg("size") = 19, py::arg("komi") = 7.5)
+      .def(py::init<int, double, bool>(), py::arg("size") = 19, py::arg("komi") = 7.5,
+           py::arg("standard_two_pass") = false)
       .def_readonly("size", &GameState::n)
       .def_property(
           "current_player", [](const GameState& s) { return (int)s.current_player; },
@@ -74,6 +75,7 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("num_black_prisoners", &GameState::num_black_prisoners)
       .def_readwrite("num_white_prisoners", &GameState::num_white_prisoners)
       .def_readwrite("is_end_of_game", &GameState::is_end_of_game)
+      .def_readwrite("standard_two_pass", &GameState::standard_two_pass)
       .def_property(
           "ko", [](const GameState& s) { return s.ko < 0 ? py::none() : to_move(s, s.ko); },
           [](GameState& s, py::object k) { s.ko = k.is_none() ? -1 : to_idx(s, k); })

@@ -40,7 +40,7 @@ const Geometry& geometry(int n) {
   return g_geoms[n];
 }
 
-GameState::GameState(int size, double komi_) {
+GameState::GameState(int size, double komi_, bool standard_two_pass_) : standard_two_pass(standard_two_pass_) {
   g = &geometry(size);
   n = size;
   np = size * size;
@@ -275,7 +275,7 @@ bool GameState::try_move(int p, int color) {
   turns_played += 1;
   history.push_back((int16_t)p);
   size_t hn = history.size();
-  if (hn > 1 && history[hn - 1] == PASS && history[hn - 2] == PASS && current_player == WHITE)
+  if (hn > 1 && history[hn - 1] == PASS && history[hn - 2] == PASS && (standard_two_pass || current_player == WHITE))
     is_end_of_game = true;
   return true;
 }

@@ -13,6 +13,8 @@
 // Deliberate fixes over the reference:
 //   Q2  copy() has value semantics (history, komi, passes, end flag copied).
 //   Q14 bounds are checked before the board is indexed.
+// Option (Q9): standard_two_pass ends the game after any two consecutive
+// passes; the default keeps the reference rule (second pass by black).
 #pragma once
 #include <cstdint>
 #include <cstring>
@@ -80,9 +82,10 @@ struct GameState {
   int passes_white, passes_black;
   int num_black_prisoners, num_white_prisoners;
   bool is_end_of_game;
+  bool standard_two_pass;  // Q9 option, see above
   std::vector<int16_t> history;  // PASS = -1
 
-  explicit GameState(int size = 19, double komi_ = 7.5);
+  explicit GameState(int size = 19, double komi_ = 7.5, bool standard_two_pass_ = false);
 
   inline int idx(int x, int y) const { return x * n + y; }
   inline bool on_board(int x, int y) const { return x >= 0 && y >= 0 && x < n && y < n; }

@@ -61,14 +61,15 @@ def play_match(player1, player2, n_games: int = 2, size: int = 19, komi: float =
 
 
 def batched_match(sampler1, sampler2, n_games: int, size: int = 19, komi: float = 7.5, max_moves: int = 722,
-                  seed: int = 0) -> Dict[str, float]:
+                  seed: int = 0, standard_two_pass: bool = False) -> Dict[str, float]:
     import numpy as np
 
     from .selfplay import play_games
 
     colors = [go.BLACK if i % 2 == 0 else go.WHITE for i in range(n_games)]
     rec = play_games(sampler1, sampler2, n_games, size=size, komi=komi, max_moves=max_moves,
-                     rng=np.random.default_rng(seed), record=False, learner_colors=colors)
+                     rng=np.random.default_rng(seed), record=False, learner_colors=colors,
+                     standard_two_pass=standard_two_pass)
     w1 = sum(1 for w, c in zip(rec.winners, rec.learner_colors) if w == c)
     d = sum(1 for w in rec.winners if w == 0)
     return {"player1_wins": w1, "player2_wins": n_games - w1 - d, "draws": d,

@@ -97,13 +97,15 @@ class GameRecords:
 
 def play_games(learner: BatchedSampler, opponent: BatchedSampler, n_games: int, size: int = 19,
                komi: float = 7.5, max_moves: int = 500, rng: Optional[np.random.Generator] = None,
-               record: bool = True, learner_colors: Optional[Sequence[int]] = None) -> GameRecords:
+               record: bool = True, learner_colors: Optional[Sequence[int]] = None,
+               standard_two_pass: bool = False) -> GameRecords:
     """Play n_games learner-vs-opponent games in lock-step (reference
     make_training_pairs, reinforcement_policy_trainer.py:16-76).  The learner's
     colour is drawn per game and its training pairs use the state
-    *before* its own move (Q6)."""
+    *before* its own move (Q6).  ``standard_two_pass`` ends a game after any two
+    consecutive passes instead of the reference rule (Q9, go.py:345-348)."""
     rng = rng or np.random.default_rng()
-    states = [go.GameState(size, komi) for _ in range(n_games)]
+    states = [go.GameState(size, komi, standard_two_pass) for _ in range(n_games)]
     colors = list(learner_colors) if learner_colors is not None else \
         [int(c) for c in rng.choice([go.BLACK, go.WHITE], size=n_games)]
     rec_p: List[List[np.ndarray]] = [[] for _ in range(n_games)]

@@ -131,6 +131,9 @@ def _parser():
     p.add_argument("--minibatch", type=int, default=256, help="positions per gradient chunk")
     p.add_argument("--temperature", type=float, default=1.0)
     p.add_argument("--max-moves", type=int, default=500)
+    p.add_argument("--standard-two-pass", action="store_true",
+                   help="end a game after any two consecutive passes (reference rule: only when the "
+                        "second pass is black's, go.py:345-348, SURVEY Q9)")
     p.add_argument("--loss", default="reinforce", choices=["reinforce", "reference"])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--seed", type=int, default=0)
@@ -169,7 +172,8 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
         choice = pool[int(rng.integers(len(pool)))]
         opp_pol.load_weights(choice if choice else args.initial_weights)
         learner_pol.refresh()
-        rec = play_games(learner, opponent, args.game_batch_size, size=size, max_moves=args.max_moves, rng=rng)
+        rec = play_games(learner, opponent, args.game_batch_size, size=size, max_moves=args.max_moves, rng=rng,
+                         standard_two_pass=args.standard_two_pass)
         info = rl_update(trainer, rec, args.minibatch, dev, args.loss)
         learner_pol.refresh()
         wins = sum(1 for w, c in zip(rec.winners, rec.learner_colors) if w == c)

@@ -116,3 +116,22 @@ def test_end_of_game_rule():
     assert s.do_move(None) is False      # W pass -> black to move: not over
     assert s.do_move(None) is True       # B pass -> white to move: over
     assert s.is_end_of_game
+
+
+def test_standard_two_pass_option():
+    """Q9 option: with standard_two_pass any two consecutive passes end the game;
+    the flag survives copies (search slots copy leaf states)."""
+    s = go.GameState(5, 7.5, standard_two_pass=True)
+    assert s.standard_two_pass
+    c = s.copy()
+    assert c.do_move(None) is False      # B pass
+    assert c.do_move(None) is True       # W pass -> over (reference rule would continue)
+    assert c.is_end_of_game
+    d = go.GameState(5)
+    assert not d.standard_two_pass
+    d.do_move((1, 1))
+    d.standard_two_pass = True
+    assert d.do_move(None) is False      # W pass
+    assert d.do_move((2, 2)) is False    # B move resets the pass streak
+    assert d.do_move(None) is False      # W pass
+    assert d.do_move(None) is True       # B pass -> over
