@@ -6,8 +6,9 @@ namespace ag {
 
 static const char* kNames[F_NUM] = {"board", "ones", "turns_since", "liberties", "capture_size",
                                      "self_atari_size", "liberties_after", "ladder_capture",
-                                     "ladder_escape", "sensibleness", "zeros", "color", "legal"};
-static const int kPlanes[F_NUM] = {3, 1, 8, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1};
+                                     "ladder_escape", "sensibleness", "zeros", "color", "legal",
+                                     "self_atari_size_exact", "liberties_after_exact"};
+static const int kPlanes[F_NUM] = {3, 1, 8, 8, 8, 8, 8, 1, 1, 1, 1, 1, 1, 8, 8};
 
 int feature_planes(int fid) { return (fid >= 0 && fid < F_NUM) ? kPlanes[fid] : 0; }
 const char* feature_name(int fid) { return (fid >= 0 && fid < F_NUM) ? kNames[fid] : ""; }
@@ -168,7 +169,8 @@ int featurize(const GameState& s, const int* fids, int nf, uint8_t* out) {
   for (int i = 0; i < nf; ++i) {
     int f = fids[i];
     need_legal |= (f == F_CAPTURE_SIZE || f == F_SELF_ATARI_SIZE || f == F_LIBERTIES_AFTER ||
-                   f == F_SENSIBLENESS || f == F_LADDER_CAPTURE || f == F_LADDER_ESCAPE || f == F_LEGAL);
+                   f == F_SENSIBLENESS || f == F_LADDER_CAPTURE || f == F_LADDER_ESCAPE || f == F_LEGAL ||
+                   f == F_SELF_ATARI_SIZE_EXACT || f == F_LIBERTIES_AFTER_EXACT);
   }
   if (need_legal)
     for (int p = 0; p < np; ++p) legal[p] = s.is_legal(p) ? 1 : 0;
@@ -249,6 +251,49 @@ int featurize(const GameState& s, const int* fids, int nf, uint8_t* out) {
             if (plane > 7) plane = 7;
             if (plane < 0) plane = 7;  // python index -1
             o[plane * np + p] = 1;
+          }
+        }
+        break;
+      case F_SELF_ATARI_SIZE_EXACT:
+      case F_LIBERTIES_AFTER_EXACT:
+        // Capture-aware liberties after playing p (Q10): the merged group's
+        // liberties plus the points of opponent groups that p captures and that
+        // touch the merged group; 0 liberties cannot happen for a legal move.
+        for (int p = 0; p < np; ++p) {
+          if (!legal[p]) continue;
+          Bits lib = s.liberty_set(p);
+          int gsz = 1;
+          int16_t roots[4];
+          const int k = s.groups_around(p, roots);
+          for (int j = 0; j < k; ++j)
+            if (s.board[roots[j]] == me) {
+              lib.orr(s.libs[roots[j]]);
+              gsz += s.gsize[roots[j]];
+            }
+          lib.clear(p);
+          for (int j = 0; j < k; ++j) {
+            const int r = roots[j];
+            if (s.board[r] != -me || s.libc[r] != 1) continue;  // not captured by p
+            int q = r;
+            do {  // captured stone q becomes a liberty if it touches p or the merged group
+              for (int e = 0; e < s.g->nnbr[q]; ++e) {
+                const int t = s.g->nbr[q][e];
+                bool merged = t == p;
+                for (int m = 0; m < k && !merged; ++m) merged = s.board[roots[m]] == me && s.board[t] == me &&
+                                                                   s.head[t] == roots[m];
+                if (merged) {
+                  lib.set(q);
+                  break;
+                }
+              }
+              q = s.next[q];
+            } while (q != r);
+          }
+          const int nl = lib.count();
+          if (f == F_SELF_ATARI_SIZE_EXACT) {
+            if (nl == 1) o[(gsz - 1 > 7 ? 7 : gsz - 1) * np + p] = 1;
+          } else if (nl >= 1) {
+            o[((nl > 8 ? 8 : nl) - 1) * np + p] = 1;  // planes 1..8+ liberties
           }
         }
         break;

@@ -26,6 +26,8 @@ enum FeatureId : int {
   F_ZEROS,
   F_COLOR,
   F_LEGAL,
+  F_SELF_ATARI_SIZE_EXACT,  // capture-aware variants, CPU only
+  F_LIBERTIES_AFTER_EXACT,
   F_NUM
 };
 

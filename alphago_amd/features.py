@@ -9,6 +9,9 @@ Same registry names, plane counts and ordering as the reference
 * ``color`` — the value network's 49th plane (paper "player colour"; the
   reference declares 49 inputs in value.py:16 but has no such feature, Q18).
 * ``legal`` — legal-move mask (used by search/players, not by the paper nets).
+* ``liberties_after_exact`` / ``self_atari_size_exact`` — capture-aware versions of
+  the reference planes, CPU featurizer only; the reference names keep
+  the reference semantics bit-exactly.
 
 A GPU featurizer (``alphago_amd.ops.featurize_gpu``) produces bit-identical
 planes for batches of boards on the device.
@@ -35,6 +38,10 @@ FEATURES = {
     "zeros": {"size": 1},
     "color": {"size": 1},
     "legal": {"size": 1},
+    # capture-aware variants (CPU featurizer only): liberties gained by
+    # capturing count, so a legal move never lands on the "0 liberties -> plane 7" quirk
+    "self_atari_size_exact": {"size": 8},
+    "liberties_after_exact": {"size": 8},
 }
 
 # 48 planes, preprocessing.py:211-214

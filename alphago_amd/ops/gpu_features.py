@@ -37,7 +37,8 @@ class GpuFeaturizer(object):
         self.features = [f.lower() for f in feature_list]
         for f in self.features:
             if f not in FEATURE_IDS:
-                raise ValueError("unknown feature: %s" % f)
+                raise ValueError("unknown feature: %s" % f if f not in FEATURES
+                                 else "feature %s is computed by the CPU featurizer only" % f)
         self.fids = [FEATURE_IDS[f] for f in self.features]
         self.fplanes = [FEATURES[f]["size"] for f in self.features]
         self.nplanes = sum(self.fplanes)

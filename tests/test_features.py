@@ -145,3 +145,46 @@ def test_batch_featurize_matches_single():
     batch = pp.states_to_uint8(states)
     for i, s in enumerate(states):
         assert np.array_equal(batch[i], pp.state_to_uint8(s))
+
+
+def _random_positions(n, size=9, seed=3):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        gs = go.GameState(size)
+        for _ in range(int(rng.integers(20, 70))):
+            moves = gs.get_legal_moves(include_eyes=False)
+            if not moves:
+                break
+            gs.do_move(moves[int(rng.integers(len(moves)))])
+        out.append(gs)
+    return out
+
+
+def test_capture_aware_liberties_after_matches_simulation():
+    """liberties_after_exact / self_atari_size_exact (Q10 fix): the liberty count
+    of the stone just played, checked against actually playing every legal move;
+    positions without a capturing move agree with the reference planes."""
+    feats = ["liberties_after_exact", "self_atari_size_exact", "liberties_after", "self_atari_size"]
+    n_capture_moves = 0
+    for gs in _random_positions(12):
+        pl = planes(gs, feats)  # (x, y, 32)
+        exact, satx, ref, sat = pl[..., 0:8], pl[..., 8:16], pl[..., 16:24], pl[..., 24:32]
+        for (x, y) in gs.get_legal_moves(include_eyes=True):
+            c = gs.copy()
+            c.do_move((x, y))
+            nl = int(c.liberty_counts[x][y])
+            gsz = len(c.get_group((x, y)))
+            want = np.zeros(8, np.uint8)
+            want[min(nl, 8) - 1] = 1
+            assert (exact[x, y] == want).all(), ((x, y), nl, exact[x, y])
+            want_sa = np.zeros(8, np.uint8)
+            if nl == 1:
+                want_sa[min(gsz, 8) - 1] = 1
+            assert (satx[x, y] == want_sa).all()
+            captured = c.num_black_prisoners + c.num_white_prisoners - gs.num_black_prisoners - gs.num_white_prisoners
+            if captured:
+                n_capture_moves += 1
+            else:
+                assert (exact[x, y] == ref[x, y]).all() and (satx[x, y] == sat[x, y]).all()
+    assert n_capture_moves > 0  # the positions exercise the capture path
