@@ -27,7 +27,8 @@ def test_bench_json_line_under_torchrun(nproc):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "2", "--warmup", "1",
-           "--backend", "torch", "--batch", "2", "--filters", "8", "--layers", "3", "--pool", "16"]
+           "--backend", "torch", "--batch", "2", "--filters", "8", "--layers", "3", "--pool", "16",
+           "--min-warmup-s", "0.5"]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
                PYTHONPATH=ROOT)
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
@@ -43,5 +44,7 @@ def test_bench_json_line_under_torchrun(nproc):
     assert out["config"]["global_batch"] == 2 * nproc
     assert out["config"]["parallelism"] == "dp%d" % nproc
     assert out["value"] > 0
+    # at least --warmup steps and at least --min-warmup-s seconds, same count on every rank
+    assert out["warmup_steps_run"] >= 1 and (out["warmup_steps_run"] - 1) % 10 == 0 and out["warmup_s"] >= 0.5
     # value is the whole-job rate: global positions over the (max-over-ranks) timed span
     assert abs(out["value"] - 2 * nproc * 2 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 0.01
