@@ -36,12 +36,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=25)
-    # The first process on a fresh box measured 97k positions/s after 150 warmup steps (1.5 s) and
-    # 110k after 500 (5 s), vs 111-112k for any later process: the GPU needs seconds of sustained
-    # load to reach its steady clocks.  Warmup therefore runs at least --warmup steps AND at least
-    # this many seconds (in chunks of 10 steps, the decision all-reduced so every rank runs the
-    # same number of steps); the timed region is unchanged.
-    ap.add_argument("--min-warmup-s", type=float, default=5.0)
+    # Warmup runs at least --warmup steps AND at least this many seconds of sustained load (chunks
+    # of 10 steps, the decision all-reduced so every rank runs the same number of steps); the timed
+    # region is unchanged.  Measured on fresh 1-GPU boxes: the FIRST process on a box usually runs
+    # 8-10 % slower (97-102k positions/s; once 110k) whatever its warmup (25 steps, 1.5 s or 5 s),
+    # with the host far ahead of the GPU (host_ms_per_step 2.0 of 10.7); later processes: 110-114k.
+    ap.add_argument("--min-warmup-s", type=float, default=3.0)
     # 1088 boards x 361 points = 1023 forward tiles of 384 pixels: four full rounds over the 256 CUs
     # (1024 boards leave the fourth round 76 % full); measured +2-4 % positions/s
     ap.add_argument("--batch", type=int, default=1088, help="per-GPU minibatch (boards)")
