@@ -42,9 +42,11 @@ def main():
     # 8-10 % slower (97-102k positions/s; once 110k) whatever its warmup (25 steps, 1.5 s or 5 s),
     # with the host far ahead of the GPU (host_ms_per_step 2.0 of 10.7); later processes: 110-114k.
     ap.add_argument("--min-warmup-s", type=float, default=3.0)
-    # 1088 boards x 361 points = 1023 forward tiles of 384 pixels: four full rounds over the 256 CUs
-    # (1024 boards leave the fourth round 76 % full); measured +2-4 % positions/s
-    ap.add_argument("--batch", type=int, default=1088, help="per-GPU minibatch (boards)")
+    # 2176 boards x 361 points = 2046 forward tiles of 384 pixels: eight full rounds over the 256 CUs.
+    # Alternating A/B on one box (3 rounds each, profiles/r1_batch_sweep_v8.md): 1088 -> 110.5-111.4k,
+    # 2176 -> 117.2-117.9k (+6 %: the per-step serial tail, head, wgrad reduce and SGD amortise over
+    # twice the boards), 3264 -> 119.9-120.1k, 4352 -> 120.0k (flat).
+    ap.add_argument("--batch", type=int, default=2176, help="per-GPU minibatch (boards)")
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--planes", type=int, default=48)
