@@ -37,10 +37,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=25)
     # Warmup runs at least --warmup steps AND at least this many seconds of sustained load (chunks
-    # of 10 steps, the decision all-reduced so every rank runs the same number of steps); the timed
-    # region is unchanged.  Measured on fresh 1-GPU boxes: the FIRST process on a box usually runs
-    # 8-10 % slower (97-102k positions/s; once 110k) whatever its warmup (25 steps, 1.5 s or 5 s),
-    # with the host far ahead of the GPU (host_ms_per_step 2.0 of 10.7); later processes: 110-114k.
+    # of 10 steps, the decision all-reduced so every rank runs the same number of steps).
     ap.add_argument("--min-warmup-s", type=float, default=3.0)
     # 2176 boards x 361 points = 2046 forward tiles of 384 pixels: eight full rounds over the 256 CUs.
     # Alternating A/B on one box (3 rounds each, profiles/r1_batch_sweep_v8.md): 1088 -> 110.5-111.4k,
@@ -89,32 +86,41 @@ def main():
         sym = torch.randint(0, 8, (args.batch,), device=dev, dtype=torch.int32, generator=g)
         return pool.index_select(0, idx), pool_tgt.index_select(0, idx), sym
 
+    loss_sum = torch.zeros((), device=dev)
+    corr_sum = torch.zeros((), device=dev)
+
+    def run(n):
+        # The warmup runs this exact loop body too: every kernel of the timed region (including the
+        # metric accumulation) is loaded before the clock starts.  On a fresh box the first launch of
+        # a not-yet-used kernel from libtorch's code objects cost ~52 ms of host time (cold page
+        # cache), which landed inside the timed region of the round-1 driver run: 20 x 18.4 ms of
+        # GPU work measured as 21.1 ms/step (profiles/r2_fresh_box_diagnosis.md).
+        for _ in range(n):
+            l, c = trainer.step(*batch())
+            loss_sum.add_(l)
+            corr_sum.add_(c)
+
     t_warm = time.perf_counter()
     warm_steps = 0
-    for _ in range(args.warmup):
-        trainer.step(*batch())
-        warm_steps += 1
+    run(args.warmup)
+    warm_steps += args.warmup
     while True:
         if dev.type == "cuda":
             torch.cuda.synchronize()
         if agdist.all_reduce_max(time.perf_counter() - t_warm) >= args.min_warmup_s:
             break
-        for _ in range(10):
-            trainer.step(*batch())
-            warm_steps += 1
+        run(10)
+        warm_steps += 10
     warm_s = time.perf_counter() - t_warm
+    loss_sum.zero_()
+    corr_sum.zero_()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     agdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    loss_sum = torch.zeros((), device=dev)
-    corr_sum = torch.zeros((), device=dev)
-    for _ in range(args.steps):
-        l, c = trainer.step(*batch())
-        loss_sum += l
-        corr_sum += c
+    run(args.steps)
     t_host = time.perf_counter() - t0  # host enqueue time: ~dt means the host, not the GPU, sets the pace
     if dev.type == "cuda":
         torch.cuda.synchronize()
