@@ -1,14 +1,16 @@
 """SGF -> HDF5 training-data converter (reference game_converter.py:16-214).
 
-Same output schema as the reference so existing datasets and
-tools interoperate:
-  states       uint8 (N, F, S, S) one-hot planes
-  actions      uint8 (N, 2)        move (x, y)
+Same output schema and storage layout as the reference so
+existing datasets and tools interoperate:
+  states       uint8 (N, F, S, S) one-hot planes, chunks (64, F, S, S), LZF
+  actions      uint8 (N, 2)        move (x, y),     chunks (1024, 2),    LZF
   file_offsets group: key = path with '/' -> ':', value = [start, n_pairs]
 plus a ``features`` attribute listing the planes (the reference's TODO,
 game_converter.py:62).  Featurisation runs in native threads; state rows are
-streamed straight into the file (no 1-row resizes, constant memory), written to
-a hidden temp file and atomically renamed on success.
+streamed straight into the file one compressed chunk at a time (no 1-row
+resizes, constant memory), written to a hidden temp file and atomically renamed
+on success.  ``compression=None`` writes contiguous datasets
+(memory-mappable, for host-streamed training without a decode step).
 """
 from __future__ import annotations
 
@@ -32,11 +34,15 @@ class SizeMismatchError(Exception):
 
 
 class GameConverter(object):
-    def __init__(self, features: List[str], threads: int = 8):
+    STATE_CHUNK_ROWS = 64     # game_converter.py:71-78
+    ACTION_CHUNK_ROWS = 1024  # game_converter.py:79-86
+
+    def __init__(self, features: List[str], threads: int = 8, compression: Optional[str] = "lzf"):
         self.feature_processor = Preprocess(features)
         self.n_features = self.feature_processor.output_dim
         self.features = list(features)
         self.threads = threads
+        self.compression = compression
 
     def convert_game(self, file_name: str, bd_size: int):
         """Yield (planes (1,F,S,S) uint8, move) for every non-pass move."""
@@ -81,7 +87,10 @@ class GameConverter(object):
             with H5Writer(tmp_file) as h5f:
                 h5f.attrs["features"] = np.array([f.encode() for f in self.features])
                 h5f.attrs["board_size"] = np.int64(bd_size)
-                states = h5f.stream_dataset("states", (self.n_features, bd_size, bd_size), np.uint8)
+                chunked = self.compression is not None
+                states = h5f.stream_dataset("states", (self.n_features, bd_size, bd_size), np.uint8,
+                                            chunk_rows=self.STATE_CHUNK_ROWS if chunked else 0,
+                                            compression=self.compression)
                 offsets = h5f.create_group("file_offsets")
                 all_actions = []
                 for file_name in sgf_files:
@@ -116,7 +125,10 @@ class GameConverter(object):
                         print("\t-no usable data-")
                 states.finish()
                 acts = np.concatenate(all_actions) if all_actions else np.zeros((0, 2), np.uint8)
-                h5f.create_dataset("actions", data=acts)
+                if chunked:
+                    h5f.create_chunked("actions", acts, self.ACTION_CHUNK_ROWS, self.compression)
+                else:
+                    h5f.create_dataset("actions", data=acts)
         except Exception:
             if os.path.exists(tmp_file):
                 os.remove(tmp_file)
@@ -159,6 +171,8 @@ def run_game_converter(cmd_line_args: Optional[List[str]] = None) -> int:
     parser.add_argument("--size", "-s", help="Size of the game board. SGFs not matching this are discarded with a "
                         "warning", type=int, default=19)
     parser.add_argument("--threads", type=int, default=8, help="featurizer threads")
+    parser.add_argument("--compression", default="lzf", choices=["lzf", "none"],
+                        help="lzf: chunked (64,F,S,S) LZF datasets as the reference writes; none: contiguous")
     parser.add_argument("--verbose", "-v", help="Turn on verbose mode", default=False, action="store_true")
     args = parser.parse_args(cmd_line_args)
     if args.features.lower() == "all":
@@ -167,7 +181,8 @@ def run_game_converter(cmd_line_args: Optional[List[str]] = None) -> int:
         feature_list = args.features.split(",")
     if args.verbose:
         print("using features", feature_list)
-    converter = GameConverter(feature_list, threads=args.threads)
+    converter = GameConverter(feature_list, threads=args.threads,
+                              compression=None if args.compression == "none" else "lzf")
     if args.directory:
         files = _walk_all_sgfs(args.directory) if args.recurse else _list_sgfs(args.directory)
     else:

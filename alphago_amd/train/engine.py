@@ -301,10 +301,13 @@ class HipConvTrainer:
         ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0)
         ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)
 
-    def backward_trunk(self) -> None:
-        """dZ[L-1] (and head grads) must be ready on the current stream."""
+    def backward_trunk(self, reduce: bool = True) -> None:
+        """dZ[L-1] (and head grads) must be ready on the current stream.
+        ``reduce=False`` leaves the local gradient (gradient accumulation: the
+        caller all-reduces the sum once)."""
         main = torch.cuda.current_stream(self.device)
-        if -1 in self._bucket_after_layer:
+        red = reduce and self.env.distributed
+        if red and -1 in self._bucket_after_layer:
             self.reducer.launch(self._bucket_after_layer[-1])
         for l in reversed(range(self.L)):
             if self.s_w is not None:
@@ -312,11 +315,11 @@ class HipConvTrainer:
                 with torch.cuda.stream(self.s_w):
                     self.s_w.wait_event(ev)
                     self._wgrad_layer(l)
-                    if l in self._bucket_after_layer:
+                    if red and l in self._bucket_after_layer:
                         self.reducer.launch(self._bucket_after_layer[l])
             else:
                 self._wgrad_layer(l)
-                if l in self._bucket_after_layer:
+                if red and l in self._bucket_after_layer:
                     self.reducer.launch(self._bucket_after_layer[l])
             if l > 0:
                 if self.precision == "fp8":  # the fp8 forward does not write bitmasks
@@ -327,11 +330,13 @@ class HipConvTrainer:
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1])
         if self.s_w is not None:
             main.wait_stream(self.s_w)
-        self.reducer.wait()
+        if red:
+            self.reducer.wait()
 
     def compute_grads(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None,
-                      weight: Optional[torch.Tensor] = None):
-        """Forward + backward into self.fp.grad (all-reduced when distributed)."""
+                      weight: Optional[torch.Tensor] = None, reduce: bool = True):
+        """Forward + backward into self.fp.grad (all-reduced when distributed,
+        unless ``reduce=False``)."""
         B = planes.shape[0]
         if B != self.batch:
             raise ValueError("batch %d != configured %d" % (B, self.batch))
@@ -340,7 +345,7 @@ class HipConvTrainer:
         with trace_range("head"):
             self._head_train(targets, 1.0 / (B * self.env.world_size), weight)
         with trace_range("backward+allreduce"):
-            self.backward_trunk()
+            self.backward_trunk(reduce)
 
     def apply_update(self) -> None:
         with trace_range("sgd+repack"):
@@ -473,7 +478,7 @@ class _TorchTrainerBase:
             agdist.broadcast_(self.fp.flat, 0)
         self.table = symmetry_tables(net.board, self.device)
 
-    def compute_grads(self, planes, targets, sym=None, weight=None):
+    def compute_grads(self, planes, targets, sym=None, weight=None, reduce: bool = True):
         for p in self.params:
             p.grad = None
         obj, per, metric = self._loss(planes, targets, sym, weight)
@@ -483,7 +488,7 @@ class _TorchTrainerBase:
                 self.fp.grad_views[name].zero_()
             else:
                 self.fp.grad_views[name].copy_(p.grad)
-        if self.env.distributed:
+        if reduce and self.env.distributed:
             agdist.all_reduce_sum_(self.fp.grad)
         self._last = (per.detach(), metric.detach())
 

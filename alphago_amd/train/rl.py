@@ -65,10 +65,12 @@ def rl_update(trainer, records, B: int, device, loss: str = "reinforce") -> dict
 
 def _accumulate_grads(trainer, X, T, W, B, device, n_chunks) -> None:
     """trainer.fp.grad <- sum over B-sized chunks of the weighted-loss gradients
-    (padding boards carry target -1 and weight 0)."""
+    (padding boards carry target -1 and weight 0).  Chunks accumulate locally
+    (``compute_grads(reduce=False)``); the sum is all-reduced ONCE."""
     C, S = trainer.net.trunk.in_planes, trainer.net.board
-    acc = torch.zeros_like(trainer.fp.grad)
-    for c in range(max(1, n_chunks)):
+    n_chunks = max(1, n_chunks)
+    acc = torch.zeros_like(trainer.fp.grad) if n_chunks > 1 else None
+    for c in range(n_chunks):
         sl = slice(c * B, (c + 1) * B)
         xb, tb, wb = X[sl], T[sl], W[sl]
         pad = B - len(tb)
@@ -77,9 +79,13 @@ def _accumulate_grads(trainer, X, T, W, B, device, n_chunks) -> None:
             tb = np.concatenate([tb, np.full(pad, -1, np.int32)])
             wb = np.concatenate([wb, np.zeros(pad, np.float32)])
         trainer.compute_grads(torch.from_numpy(xb).to(device), torch.from_numpy(tb).to(device), None,
-                              torch.from_numpy(wb.astype(np.float32)).to(device))
-        acc += trainer.fp.grad
-    trainer.fp.grad.copy_(acc)
+                              torch.from_numpy(wb.astype(np.float32)).to(device), reduce=False)
+        if acc is not None:
+            acc += trainer.fp.grad
+    if acc is not None:
+        trainer.fp.grad.copy_(acc)
+    if agdist.env().distributed:
+        agdist.all_reduce_sum_(trainer.fp.grad)
 
 
 def _reference_bce_update(trainer, records, B, device) -> dict:

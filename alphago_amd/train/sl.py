@@ -18,7 +18,12 @@ Differences (all fixes from SURVEY.md §2.7):
   --max-restarts`` + ``--resume`` for automatic recovery;
 * ``--profile DIR``: torch.profiler traces + roctx ranges (utils/profiling.py);
 * data parallel across GPUs (one process per GPU, RCCL all-reduce inside the
-  step); each global minibatch of B*world positions is split across ranks;
+  step); each rank owns a fixed shard of the shuffled permutation
+  (``train_idx[rank::world]``, data/dataset.py) and loads only those rows, so a
+  global minibatch is B positions from every rank's shard;
+* ``--resident no`` streams the shard from the host through a pinned ring,
+  a prefetch thread and a copy stream (block-shuffled order for LZF-chunked
+  files, so each chunk is decoded about once per pass);
 * per-board D4 augmentation happens on the GPU inside ``pack_input``.
 
 Run: ``python -m alphago_amd.train.sl model.json data.h5 outdir -B 256``
@@ -35,7 +40,8 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from ..data.dataset import PositionDataset
+from ..data.dataset import PositionDataset, block_shuffle, shard_rows
+from ..io.h5lite import H5File
 from ..models.policy import CNNPolicy
 from ..parallel import dist as agdist
 from ..utils import faults
@@ -114,10 +120,11 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
     if resume:
         policy.load_weights(os.path.join(args.out_directory, args.weights))
 
-    dataset = PositionDataset(args.train_data, device=dev, resident=args.resident)
-    if dataset.planes != policy.preprocessor.output_dim:
-        raise ValueError("dataset has %d planes, model expects %d" % (dataset.planes, policy.preprocessor.output_dim))
-    n_total = len(dataset)
+    with H5File(args.train_data) as f:
+        n_total, n_planes = f["states"].shape[0], f["states"].shape[1]
+        chunk_rows = f["states"].chunk_rows if f["states"].chunked else 0
+    if n_planes != policy.preprocessor.output_dim:
+        raise ValueError("dataset has %d planes, model expects %d" % (n_planes, policy.preprocessor.output_dim))
     n_train = int(args.train_val_test[0] * n_total)
     n_val = int(args.train_val_test[1] * n_total)
 
@@ -145,6 +152,19 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
                 np.save(f, shuffle_indices)
     train_idx = shuffle_indices[:n_train]
     val_idx = shuffle_indices[n_train:n_train + n_val]
+    # this rank's rows: a fixed partition of the permutation (no rank ever
+    # loads another rank's positions)
+    my_train = shard_rows(train_idx, rank, world)
+    my_val = shard_rows(val_idx, rank, world)
+    if args.resident == "no" and chunk_rows:
+        my_train = block_shuffle(my_train, chunk_rows, seed=args.seed * 1000 + rank)
+        my_val = np.sort(my_val)  # validation order does not matter; sorted = each chunk decoded once
+    dataset = PositionDataset(args.train_data, device=dev, resident=args.resident,
+                              rows=np.concatenate([my_train, my_val]))
+    n_my_train, n_my_val = len(my_train), len(my_val)
+    rows_per_rank = agdist.all_gather_object(len(dataset)) if env.distributed else [len(dataset)]
+    meta.metadata["data"] = {"rows_per_rank": rows_per_rank, "resident": bool(dataset.resident),
+                             "chunked": bool(chunk_rows)}
 
     ckpt_path = os.path.join(args.out_directory, "checkpoint.pt")
     iterations, cursor = 0, 0
@@ -175,28 +195,35 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
         start_epoch, start_step = int(state["epoch"]), int(state["step"])
         if not resume:
             end_epoch = int(state.get("end_epoch", end_epoch))
-        sums.copy_(state["sums"].to(dev))
+        saved = state["sums"]
+        sums.copy_((saved[rank] if isinstance(saved, list) else saved).to(dev))
         meta.metadata = state.get("metadata", meta.metadata)
         if args.verbose and env.is_main:
             print("resumed at epoch %d step %d (iteration %d)" % (start_epoch, start_step, iterations), flush=True)
 
-    def global_batch(cur):
-        idx = np.take(train_idx, np.arange(cur, cur + global_B) % max(1, n_train))
-        return idx[rank * B:(rank + 1) * B], (cur + global_B) % max(1, n_train)
+    # cursor = minibatches of B positions this rank has consumed from its shard
+    def local_batch(cur):
+        return np.arange(cur * B, (cur + 1) * B) % max(1, n_my_train)
 
     def save_native(epoch, step):
         rng = gen.get_state()
+        part = sums.detach().to("cpu", copy=True)
         if env.distributed:
             rng = agdist.all_gather_object(rng)
+            part = agdist.all_gather_object(part)  # every rank's partial epoch sums
         if env.is_main:
             ckpt.save(ckpt_path, trainer, cursor=cursor, epoch=epoch, step=step, end_epoch=end_epoch, rng=rng,
-                      sums=sums, metadata=meta.metadata, config=run_cfg.to_dict())
+                      sums=part, metadata=meta.metadata, config=run_cfg.to_dict())
 
     enable_collective_timeouts()
     wd = Watchdog(args.out_directory if args.watchdog_timeout > 0 else None, rank, args.watchdog_timeout)
     if args.watchdog_timeout > 0:
         wd.start()
     prof = Profiler(os.path.join(args.profile, "rank%d" % rank) if args.profile else None)
+    total_steps = (end_epoch - start_epoch) * steps_per_epoch - start_step
+    stream = None
+    if not dataset.resident:
+        stream = dataset.prefetch((local_batch(cursor + k) for k in range(total_steps)), B)
     with prof:
         for epoch in range(start_epoch, end_epoch):
             t0 = time.perf_counter()
@@ -204,8 +231,8 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
                 gstep = epoch * steps_per_epoch + step
                 faults.maybe_inject(gstep, rank)
                 with trace_range("data"):
-                    idx, cursor = global_batch(cursor)
-                    planes, tgt = dataset.batch(idx)
+                    planes, tgt = next(stream) if stream is not None else dataset.batch(local_batch(cursor))
+                    cursor += 1
                     sym = None if args.no_symmetries else torch.randint(0, 8, (B,), device=dev, dtype=torch.int32,
                                                                          generator=gen)
                 with trace_range("train_step"):
@@ -223,7 +250,7 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
             seen = steps_per_epoch * global_B
             logs = {"loss": float(stats[0]) / seen, "acc": float(stats[1]) / seen}
             if n_val > 0:
-                vl, vc, vn = _validate(trainer, dataset, val_idx, B, rank, world, dev)
+                vl, vc, vn = _validate(trainer, dataset, np.arange(n_my_train, n_my_train + n_my_val), B, dev)
                 logs.update({"val_loss": vl, "val_acc": vc})
             dt = time.perf_counter() - t0
             if env.is_main:
@@ -235,13 +262,15 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
             save_native(epoch + 1, 0)
             agdist.barrier()
     wd.stop()
+    if stream is not None:
+        stream.close()
     dataset.close()
     return meta.metadata
 
 
 @torch.no_grad()
-def _validate(trainer, dataset, val_idx, B, rank, world, dev):
-    mine = val_idx[rank::world]
+def _validate(trainer, dataset, mine, B, dev):
+    """``mine``: local positions of this rank's validation shard."""
     loss = torch.zeros((), device=dev, dtype=torch.float64)
     corr = torch.zeros((), device=dev, dtype=torch.float64)
     for i in range(0, len(mine), B):

@@ -76,3 +76,35 @@ def test_converter_cli(tmp_path):
     assert not os.path.exists(str(tmp_path / ".tmp.out.h5"))
     out2 = str(tmp_path / "rec.h5")
     assert run_game_converter(["-o", out2, "-d", REF, "-R"]) == n * 1 or os.path.exists(out2)
+
+
+@pytest.mark.skipif(not HAVE_REF, reason="reference fixtures absent")
+def test_converter_writes_reference_layout_and_matches_fixture(tmp_path):
+    """Converter output uses the reference's storage layout (states chunked
+    (64,F,S,S) + LZF, actions chunked (1024,2) + LZF, game_converter.py:71-86),
+    round-trips through h5lite (whole reads and chunk-sliced row reads), and its
+    contents equal the reference fixture's."""
+    out = str(tmp_path / "lee.h5")
+    sgfs = sorted(os.path.join(REF, "sgf", f) for f in os.listdir(os.path.join(REF, "sgf")) if "Lee" in f)
+    conv = GameConverter(["board", "ones", "turns_since"])
+    n = conv.sgfs_to_hdf5(sgfs, out, 19)
+    with H5File(os.path.join(REF, "hdf5", "alphago-vs-lee-sedol-features.hdf5")) as f:
+        ref_states, ref_actions = f["states"].read(), f["actions"].read()
+        ref_offs = {k.split("::")[-1]: tuple(f["file_offsets"][k].read()) for k in f["file_offsets"].keys()}
+    with H5File(out) as f:
+        st, ac = f["states"], f["actions"]
+        assert st.chunked and st._layout[2][:4] == (64, 12, 19, 19) and [x for x, _ in st._filters] == [32000]
+        assert ac.chunked and ac._layout[2][:2] == (1024, 2) and [x for x, _ in ac._filters] == [32000]
+        assert n == st.shape[0] == len(ref_states)
+        got_offs = {k.split(":")[-1]: tuple(f["file_offsets"][k].read()) for k in f["file_offsets"].keys()}
+        states, actions = st.read(), ac.read()
+        for name, (s0, cnt) in ref_offs.items():
+            g0, gcnt = got_offs[name]
+            assert gcnt == cnt
+            assert np.array_equal(states[g0:g0 + cnt], ref_states[s0:s0 + cnt]), name
+            assert np.array_equal(actions[g0:g0 + cnt], ref_actions[s0:s0 + cnt]), name
+        rng = np.random.default_rng(0)
+        idx = rng.integers(0, n, 300)
+        assert np.array_equal(st.rows(idx), states[idx])
+        assert np.array_equal(st.read_rows(70, 200), states[70:200])
+    assert os.path.getsize(out) < ref_states.nbytes // 4  # compressed

@@ -118,3 +118,13 @@ def test_torchrun_restart_recovers_crashed_rank(tmp_path):
     a = ckpt.load(str(tmp_path / "ref" / "checkpoint.pt"))
     b = ckpt.load(str(tmp_path / "run" / "checkpoint.pt"))
     assert torch.equal(a["trainer"]["flat"], b["trainer"]["flat"])
+    # the epoch metrics survive the restart too: every rank's partial epoch
+    # sums are checkpointed and restored per rank (not rank 0's for all)
+    import json
+    ma = json.load(open(str(tmp_path / "ref" / "metadata.json")))
+    mb = json.load(open(str(tmp_path / "run" / "metadata.json")))
+    assert [e["loss"] for e in ma["epochs"]] == [e["loss"] for e in mb["epochs"]]
+    assert [e["acc"] for e in ma["epochs"]] == [e["acc"] for e in mb["epochs"]]
+    # each rank holds only its shard of the data
+    n_rows = ma["data"]["rows_per_rank"]
+    assert len(n_rows) == 2 and abs(n_rows[0] - n_rows[1]) <= 1
