@@ -104,16 +104,21 @@ def _match(argv):
     return res
 
 
+class _Exit(int):
+    """An explicit process exit code (commands' own return values, e.g. a
+    position count, are results, not exit codes)."""
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     """Dispatch a command; returns a process exit code."""
     r = _dispatch(list(sys.argv[1:] if argv is None else argv))
-    return r if isinstance(r, int) else 0
+    return int(r) if isinstance(r, _Exit) else 0
 
 
 def _dispatch(argv: List[str]):
     if not argv or argv[0] in ("-h", "--help"):
         print(__doc__)
-        return 0
+        return _Exit(0)
     cmd, rest = argv[0], argv[1:]
     if cmd == "convert":
         from .data.convert import run_game_converter
@@ -143,7 +148,7 @@ def _dispatch(argv: List[str]):
         sys.argv = ["bench.py"] + rest
         return bench.main()
     print("unknown command %r\n%s" % (cmd, __doc__))
-    return 2
+    return _Exit(2)
 
 
 if __name__ == "__main__":

@@ -112,7 +112,8 @@ class _ChunkCache(object):
 
 class PositionDataset(object):
     def __init__(self, path: str, device=None, resident: str = "auto", budget_gb: float = 64.0,
-                 rows: Optional[np.ndarray] = None, threads: int = 0, cache_chunks: int = 64):
+                 rows: Optional[np.ndarray] = None, threads: int = 0, cache_chunks: int = 64,
+                 targets: str = "actions"):
         self.path = path
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.f = H5File(path)
@@ -122,8 +123,13 @@ class PositionDataset(object):
         self.n, self.planes, self.size = ds.shape[0], ds.shape[1], ds.shape[2]
         self.row_shape = tuple(ds.shape[1:])
         self.threads = threads or min(16, os.cpu_count() or 8)  # LZF decode threads
-        acts = np.asarray(self.f["actions"].read()).astype(np.int64)
-        self._targets_all = (acts[:, 0] * self.size + acts[:, 1]).astype(np.int32)
+        if targets == "actions":  # move (x, y) -> flat index x*S+y (util.py:6-8)
+            acts = np.asarray(self.f["actions"].read()).astype(np.int64)
+            self._targets_all = (acts[:, 0] * self.size + acts[:, 1]).astype(np.int32)
+        elif targets == "outcomes":  # value-network regression targets z in {-1, 0, 1}
+            self._targets_all = np.asarray(self.f["outcomes"].read()).astype(np.float32)
+        else:
+            raise ValueError("targets must be 'actions' or 'outcomes'")
         self.features = [x.decode() for x in self.f.attrs["features"]] if "features" in self.f.attrs else None
         self.chunked = ds.chunked
         self.chunk_rows = ds.chunk_rows if ds.chunked else 0
@@ -193,7 +199,7 @@ class PositionDataset(object):
         if self._stage is None or self._stage[0].shape[0] < n:
             pin = self.device.type == "cuda"
             self._stage = (torch.empty((n,) + self.row_shape, dtype=torch.uint8, pin_memory=pin),
-                           torch.empty((n,), dtype=torch.int32, pin_memory=pin))
+                           torch.empty((n,), dtype=torch.from_numpy(self.targets_np[:0]).dtype, pin_memory=pin))
         hx, ht = self._stage[0][:n], self._stage[1][:n]
         self._gather_host(pos, hx.numpy())
         ht.numpy()[:] = self.targets_np[pos]
@@ -219,11 +225,12 @@ class Prefetcher(object):
         dev = ds.device
         self.cuda = dev.type == "cuda"
         shape = (batch_size,) + ds.row_shape
+        tdt = torch.from_numpy(ds.targets_np[:0]).dtype
         self.hx = [torch.empty(shape, dtype=torch.uint8, pin_memory=self.cuda) for _ in range(self.depth)]
-        self.ht = [torch.empty((batch_size,), dtype=torch.int32, pin_memory=self.cuda) for _ in range(self.depth)]
+        self.ht = [torch.empty((batch_size,), dtype=tdt, pin_memory=self.cuda) for _ in range(self.depth)]
         if self.cuda:
             self.dx = [torch.empty(shape, dtype=torch.uint8, device=dev) for _ in range(self.depth)]
-            self.dt = [torch.empty((batch_size,), dtype=torch.int32, device=dev) for _ in range(self.depth)]
+            self.dt = [torch.empty((batch_size,), dtype=tdt, device=dev) for _ in range(self.depth)]
             self.copy_stream = torch.cuda.Stream(dev)
             self.copied = [torch.cuda.Event() for _ in range(self.depth)]
             self.consumed = [None] * self.depth

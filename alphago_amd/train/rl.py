@@ -16,6 +16,15 @@ Fixes over the reference: per-game learner colour is used for the reward
 are saved every ``save_every`` iterations and added to the opponent pool
 (the reference's TODOs at :123,164-175), positional
 ``initial_weights initial_json`` are honoured.
+
+Fault tolerance (the reference had none): a native checkpoint
+(``rl_checkpoint.pt`` in ``--checkpoint-dir``, default ``--model_folder``)
+holds the learner's master weights and SGD iteration, the next iteration, the
+opponent pool, every rank's RNG states (pool draws / learner colours, both
+samplers' move-sampling generators) and the metrics history; ``--resume``
+continues bit-identically after a crash (fault hooks ``utils/faults.py`` fire
+at iteration granularity), ``--watchdog-timeout`` turns a hang into an exit
+for ``torchrun --max-restarts``.
 """
 from __future__ import annotations
 
@@ -32,7 +41,10 @@ from .. import go
 from ..models.policy import CNNPolicy
 from ..parallel import dist as agdist
 from ..search.selfplay import BatchedSampler, play_games
+from ..utils import faults
 from ..utils.metrics import MetricsLogger
+from ..utils.watchdog import Watchdog, enable_collective_timeouts
+from . import checkpoint as ckpt
 from .engine import make_policy_trainer
 
 
@@ -145,6 +157,12 @@ def _parser():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--metrics", default=None)
     p.add_argument("--verbose", "-v", action="store_true")
+    p.add_argument("--checkpoint-dir", default=None,
+                   help="where rl_checkpoint.pt is written (default: --model_folder; none: no checkpoints)")
+    p.add_argument("--checkpoint-every", type=int, default=1, help="native checkpoint every N iterations")
+    p.add_argument("--resume", action="store_true", help="continue from rl_checkpoint.pt if it exists")
+    p.add_argument("--watchdog-timeout", type=float, default=0.0,
+                   help="exit a rank that makes no progress for this many seconds (0: off)")
     return p
 
 
@@ -173,7 +191,39 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
     log = MetricsLogger(args.metrics if env.is_main else None)
     history = []
     size = learner_pol.model.board
-    for it in range(args.iterations):
+    ck_dir = args.checkpoint_dir or folder
+    ck_path = os.path.join(ck_dir, "rl_checkpoint.pt") if ck_dir else None
+    if ck_dir and env.is_main:
+        os.makedirs(ck_dir, exist_ok=True)
+    start = 0
+    state = ckpt.load(ck_path) if (ck_path and args.resume) else None
+    if state is not None and "legacy" not in state:
+        ckpt.load_trainer_state(trainer, state["trainer"])
+        learner_pol.refresh()
+        start = int(state["iteration"])
+        pool = [None if p == "" else p for p in state["pool"]]
+        history = list(state["history"])
+        rs = state["rng"][env.rank]
+        rng.bit_generator.state = rs["numpy"]
+        learner.gen.set_state(rs["learner"])
+        opponent.gen.set_state(rs["opponent"])
+        if args.verbose and env.is_main:
+            print("resumed at iteration %d (pool of %d)" % (start, len(pool)), flush=True)
+
+    def save_checkpoint(next_it):
+        mine = {"numpy": rng.bit_generator.state, "learner": learner.gen.get_state(),
+                "opponent": opponent.gen.get_state()}
+        allr = agdist.all_gather_object(mine) if env.distributed else [mine]
+        if env.is_main:
+            ckpt.save(ck_path, trainer, iteration=next_it, pool=["" if p is None else p for p in pool],
+                      rng=allr, history=history, config=vars(args))
+
+    enable_collective_timeouts()
+    wd = Watchdog(ck_dir if args.watchdog_timeout > 0 else None, env.rank, args.watchdog_timeout)
+    if args.watchdog_timeout > 0:
+        wd.start()
+    for it in range(start, args.iterations):
+        faults.maybe_inject(it, env.rank)
         t0 = time.perf_counter()
         choice = pool[int(rng.integers(len(pool)))]
         opp_pol.load_weights(choice if choice else args.initial_weights)
@@ -200,6 +250,10 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
                 learner_pol.save_weights(path)
             agdist.barrier()
             pool.append(path)
+        wd.beat(it)
+        if ck_path and ((it + 1) % args.checkpoint_every == 0 or it + 1 == args.iterations):
+            save_checkpoint(it + 1)
+    wd.stop()
     return {"history": history, "pool": pool}
 
 

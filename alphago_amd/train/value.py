@@ -11,9 +11,13 @@ generate: for each game draw U ~ Uniform{1..max_u}; the SL policy plays moves
   outcome z in {-1, 0, +1} from the perspective of the player to move there.
   One position per game (avoids correlated samples).  Thousands of games run
   in lock-step, two batched GPU forwards per ply.  Output: HDF5 with
-  ``states`` (N, 49, S, S) uint8 and ``outcomes`` (N,) int8.
+  ``states`` (N, 49, S, S) uint8 (chunks of 64 rows, LZF) and ``outcomes``
+  (N,) int8.  Under torchrun every rank plays its own games into a per-rank
+  file and rank 0 merges them into ONE dataset (``merge_value_files``).
 train: MSE regression with SGD (paper lr 0.003, value.py:8-9), DP across
-  ranks, HIP MFMA trunk + small fused head, random D4 augmentation.
+  ranks (each rank loads only its shard of the permutation), HIP MFMA trunk +
+  small fused head, random D4 augmentation; native checkpoint / ``--resume``
+  (bit-identical) and ``--watchdog-timeout`` as in the SL trainer.
 """
 from __future__ import annotations
 
@@ -27,12 +31,16 @@ import numpy as np
 import torch
 
 from .. import go
+from ..data.dataset import PositionDataset, shard_rows
 from ..features import VALUE_FEATURES, Preprocess
 from ..io.h5lite import H5File, H5Writer
 from ..models.policy import CNNPolicy, CNNValue
 from ..parallel import dist as agdist
 from ..search.selfplay import BatchedSampler
+from ..utils import faults
 from ..utils.metrics import MetricsLogger
+from ..utils.watchdog import Watchdog, enable_collective_timeouts
+from . import checkpoint as ckpt
 from .engine import make_value_trainer
 
 LEARNING_RATE = .003
@@ -83,10 +91,11 @@ def generate_cli(argv=None):
     p.add_argument("sl_json")
     p.add_argument("rl_json")
     p.add_argument("outfile")
-    p.add_argument("--games", type=int, default=1024)
+    p.add_argument("--games", type=int, default=1024, help="games per rank")
     p.add_argument("--batch-games", type=int, default=512)
     p.add_argument("--max-u", type=int, default=450)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--keep-shards", action="store_true", help="keep the per-rank files after merging")
     a = p.parse_args(argv)
     env = agdist.init_from_env()
     sl = CNNPolicy.load_model(a.sl_json, device=env.device)
@@ -94,15 +103,16 @@ def generate_cli(argv=None):
     out = a.outfile if env.world_size == 1 else "%s.rank%d" % (a.outfile, env.rank)
     tmp = out + ".tmp"
     n = 0
+    C = Preprocess(VALUE_FEATURES).output_dim
+    S = sl.model.board
     with H5Writer(tmp) as f:
         f.attrs["features"] = np.array([x.encode() for x in VALUE_FEATURES])
-        st = f.stream_dataset("states", (Preprocess(VALUE_FEATURES).output_dim, sl.model.board, sl.model.board),
-                               np.uint8)
+        st = f.stream_dataset("states", (C, S, S), np.uint8, chunk_rows=STATE_CHUNK_ROWS, compression="lzf")
         zs = []
         done = 0
         while done < a.games:
             g = min(a.batch_games, a.games - done)
-            planes, z = generate_positions(sl, rl, g, size=sl.model.board, max_u=a.max_u,
+            planes, z = generate_positions(sl, rl, g, size=S, max_u=a.max_u,
                                            seed=a.seed * 100003 + env.rank * 1009 + done)
             st.append(planes)
             zs.append(z)
@@ -111,22 +121,65 @@ def generate_cli(argv=None):
         st.finish()
         f.create_dataset("outcomes", data=np.concatenate(zs) if zs else np.zeros(0, np.int8))
     os.replace(tmp, out)
+    if env.world_size > 1:
+        # one trainable dataset: rank 0 concatenates the per-rank files (chunk-sliced
+        # streaming copy, constant memory) into ``outfile``
+        agdist.barrier()
+        if env.is_main:
+            shards = ["%s.rank%d" % (a.outfile, r) for r in range(env.world_size)]
+            merge_value_files(shards, a.outfile)
+            if not a.keep_shards:
+                for sh in shards:
+                    os.remove(sh)
+        agdist.barrier()
+        tot = torch.tensor([float(n)], dtype=torch.float64,
+                           device=env.device if env.backend == "nccl" else "cpu")
+        agdist.all_reduce_sum_(tot)
+        n = int(tot.item())
     return n
 
 
-class ValueDataset(object):
-    def __init__(self, path: str, device):
-        self.f = H5File(path)
-        self.states = torch.from_numpy(np.array(self.f["states"].read(), copy=True)).to(device)
-        self.z = torch.from_numpy(np.asarray(self.f["outcomes"].read()).astype(np.float32)).to(device)
-        self.device = device
+STATE_CHUNK_ROWS = 64
 
-    def __len__(self):
-        return self.states.shape[0]
 
-    def batch(self, idx):
-        it = torch.from_numpy(np.asarray(idx, np.int64)).to(self.device)
-        return self.states.index_select(0, it), self.z.index_select(0, it)
+def merge_value_files(paths: List[str], outfile: str, block_rows: int = 4096) -> int:
+    """Concatenate value-position files (states + outcomes) into one file with
+    the same layout; rows are streamed a block at a time."""
+    tmp = outfile + ".tmp"
+    total = 0
+    with H5Writer(tmp) as w:
+        first = H5File(paths[0])
+        shape = first["states"].shape[1:]
+        if "features" in first.attrs:
+            w.attrs["features"] = first.attrs["features"]
+        first.close()
+        st = w.stream_dataset("states", shape, np.uint8, chunk_rows=STATE_CHUNK_ROWS, compression="lzf")
+        zs = []
+        for pth in paths:
+            with H5File(pth) as f:
+                ds = f["states"]
+                if ds.shape[1:] != shape:
+                    raise ValueError("%s: row shape %s != %s" % (pth, ds.shape[1:], shape))
+                for r0 in range(0, ds.shape[0], block_rows):
+                    st.append(ds.read_rows(r0, r0 + block_rows))
+                zs.append(np.asarray(f["outcomes"].read()).astype(np.int8))
+                total += ds.shape[0]
+        st.finish()
+        w.create_dataset("outcomes", data=np.concatenate(zs) if zs else np.zeros(0, np.int8))
+    os.replace(tmp, outfile)
+    return total
+
+
+class ValueDataset(PositionDataset):
+    """Value positions (``states`` + ``outcomes``) of one rank's shard; same
+    residency modes as the policy data (data/dataset.py)."""
+
+    def __init__(self, path: str, device, rows: Optional[np.ndarray] = None, resident: str = "auto"):
+        super().__init__(path, device, resident=resident, rows=rows, targets="outcomes")
+
+    @property
+    def z(self):
+        return self.targets
 
 
 def train_cli(argv=None):
@@ -134,51 +187,95 @@ def train_cli(argv=None):
     p.add_argument("model", help="value-network JSON (CNNValue.save_model)")
     p.add_argument("train_data")
     p.add_argument("out_directory")
-    p.add_argument("--minibatch", "-B", type=int, default=32)
+    p.add_argument("--minibatch", "-B", type=int, default=32, help="per-GPU minibatch")
     p.add_argument("--epochs", "-E", type=int, default=10)
     p.add_argument("--learning-rate", "-r", type=float, default=LEARNING_RATE)
     p.add_argument("--decay", "-d", type=float, default=DECAY)
     p.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
+    p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--metrics", default=None)
     p.add_argument("--verbose", "-v", action="store_true")
+    p.add_argument("--checkpoint-every", type=int, default=0,
+                   help="also write the native checkpoint every N steps (0: end of epoch only)")
+    p.add_argument("--resume", action="store_true",
+                   help="continue from out_directory/checkpoint.pt if it exists (exact step, RNG, cursor)")
+    p.add_argument("--watchdog-timeout", type=float, default=0.0,
+                   help="exit a rank that makes no progress for this many seconds (0: off)")
     a = p.parse_args(argv)
     env = agdist.init_from_env()
     dev = env.device
+    world, rank = env.world_size, env.rank
     val = CNNValue.load_model(a.model, device=dev)
-    data = ValueDataset(a.train_data, dev)
-    n = len(data)
+    with H5File(a.train_data) as f:
+        n = f["states"].shape[0]
     perm = np.random.default_rng(a.seed).permutation(n)
     n_train = int(a.train_val_test[0] * n)
     n_val = int(a.train_val_test[1] * n)
     tr_idx, va_idx = perm[:n_train], perm[n_train:n_train + n_val]
-    B, world, rank = a.minibatch, env.world_size, env.rank
-    trainer = make_value_trainer(val.model, B, a.learning_rate, a.decay, backend=a.backend, device=dev)
+    my_tr, my_va = shard_rows(tr_idx, rank, world), shard_rows(va_idx, rank, world)
+    data = ValueDataset(a.train_data, dev, rows=np.concatenate([my_tr, my_va]), resident=a.resident)
+    n_my_tr = len(my_tr)
+    B = a.minibatch
+    kw = {"precision": a.precision} if a.precision != "bf16" else {}
+    trainer = make_value_trainer(val.model, B, a.learning_rate, a.decay, backend=a.backend, device=dev, **kw)
     gen = torch.Generator(device=dev)
     gen.manual_seed(a.seed + rank)
     if env.is_main:
         os.makedirs(a.out_directory, exist_ok=True)
     agdist.barrier()
-    meta = {"epochs": [], "best_epoch": 0, "training_data": a.train_data, "model_file": a.model}
+    meta = {"epochs": [], "best_epoch": 0, "training_data": a.train_data, "model_file": a.model,
+            "data": {"rows_per_rank": agdist.all_gather_object(len(data)) if env.distributed else [len(data)]}}
     log = MetricsLogger(a.metrics if env.is_main else None)
     steps = max(1, n_train // (B * world))
-    cursor = 0
-    for ep in range(a.epochs):
+    ck_path = os.path.join(a.out_directory, "checkpoint.pt")
+    cursor, start_epoch, start_step = 0, 0, 0
+    ls = torch.zeros((), device=dev, dtype=torch.float64)
+    state = ckpt.load(ck_path) if a.resume else None
+    if state is not None and "legacy" not in state:
+        ckpt.load_trainer_state(trainer, state["trainer"])
+        cursor, start_epoch, start_step = int(state["cursor"]), int(state["epoch"]), int(state["step"])
+        gen.set_state(state["rng"][rank])
+        ls.copy_(state["sums"][rank].to(dev))
+        meta = state["metadata"]
+        if a.verbose and env.is_main:
+            print("resumed at epoch %d step %d" % (start_epoch, start_step), flush=True)
+
+    def save_native(epoch, step):
+        rng = agdist.all_gather_object(gen.get_state()) if env.distributed else [gen.get_state()]
+        part = ls.detach().to("cpu", copy=True)
+        part = agdist.all_gather_object(part) if env.distributed else [part]
+        if env.is_main:
+            ckpt.save(ck_path, trainer, cursor=cursor, epoch=epoch, step=step, rng=rng, sums=part, metadata=meta,
+                      config=vars(a))
+
+    enable_collective_timeouts()
+    wd = Watchdog(a.out_directory if a.watchdog_timeout > 0 else None, rank, a.watchdog_timeout)
+    if a.watchdog_timeout > 0:
+        wd.start()
+    for ep in range(start_epoch, a.epochs):
         t0 = time.perf_counter()
-        ls = torch.zeros((), device=dev, dtype=torch.float64)
-        for _ in range(steps):
-            gidx = np.take(tr_idx, np.arange(cursor, cursor + B * world) % max(1, n_train))
-            cursor = (cursor + B * world) % max(1, n_train)
-            x, z = data.batch(gidx[rank * B:(rank + 1) * B])
+        for step in range(start_step, steps):
+            gstep = ep * steps + step
+            faults.maybe_inject(gstep, rank)
+            x, z = data.batch(np.arange(cursor * B, (cursor + 1) * B) % max(1, n_my_tr))
+            cursor += 1
             sym = torch.randint(0, 8, (B,), device=dev, dtype=torch.int32, generator=gen)
             l, _ = trainer.step(x, z, sym)
             ls += l.double()
-        agdist.all_reduce_sum_(ls)
-        logs = {"loss": float(ls) / (steps * B * world)}
+            wd.beat(gstep)
+            if a.checkpoint_every and (gstep + 1) % a.checkpoint_every == 0 and step + 1 < steps:
+                save_native(ep, step + 1)
+        start_step = 0
+        tot = ls.clone()
+        ls.zero_()
+        agdist.all_reduce_sum_(tot)
+        logs = {"loss": float(tot) / (steps * B * world)}
         if n_val:
             vl, vn = torch.zeros((), device=dev, dtype=torch.float64), 0
-            mine = va_idx[rank::world]
+            mine = np.arange(n_my_tr, len(data))
             for i in range(0, len(mine) - B + 1, B):
                 x, z = data.batch(mine[i:i + B])
                 l, _ = trainer.evaluate(x, z)
@@ -191,7 +288,7 @@ def train_cli(argv=None):
         meta["epochs"].append(logs)
         key = "val_loss" if "val_loss" in logs else "loss"
         if logs[key] < meta["epochs"][meta["best_epoch"]][key]:
-            meta["best_epoch"] = ep
+            meta["best_epoch"] = len(meta["epochs"]) - 1
         if env.is_main:
             val.save_weights(os.path.join(a.out_directory, "weights.%05d.hdf5" % ep))
             with open(os.path.join(a.out_directory, "metadata.json"), "w") as f:
@@ -199,6 +296,10 @@ def train_cli(argv=None):
             log.log(epoch=ep, positions_per_s=steps * B * world / (time.perf_counter() - t0), **logs)
             if a.verbose:
                 print("epoch %d %s" % (ep, logs), flush=True)
+        save_native(ep + 1, 0)
+        agdist.barrier()
+    wd.stop()
+    data.close()
     return meta
 
 

@@ -166,3 +166,122 @@ def test_value_trainer_hip_matches_torch(cuda_device):
         a, b = hip.fp.grad_views[name], ref.fp.grad_views[name]
         cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
         assert cos > 0.98, (name, cos)
+
+
+def test_rl_resume_after_injected_fault_is_bit_identical(tmp_path, monkeypatch):
+    """RL crash at iteration 2 + --resume ends with the same learner weights,
+    opponent pool and history as an uninterrupted run (native rl_checkpoint.pt:
+    weights, SGD iteration, pool, every RNG)."""
+    from alphago_amd.train import checkpoint as ckpt
+    from alphago_amd.utils import faults
+
+    j, w = _save_policy(tmp_path, "cpu")
+
+    def args(folder):
+        return [w, j, "--model_folder", folder, "--game_batch_size", "3", "--iterations", "4", "--save_every", "1",
+                "--minibatch", "32", "--max-moves", "60", "--backend", "torch", "--resume", "--seed", "3"]
+
+    ref = rl.run(args(str(tmp_path / "ref")))
+    marker = str(tmp_path / "fired")
+    monkeypatch.setenv("ALPHAGO_AMD_FAULT", "raise@2:once=%s" % marker)
+    faults.reload_from_env()
+    try:
+        with pytest.raises(faults.InjectedFault):
+            rl.run(args(str(tmp_path / "run")))
+        mid = ckpt.load(str(tmp_path / "run" / "rl_checkpoint.pt"))
+        assert mid["iteration"] == 2
+        got = rl.run(args(str(tmp_path / "run")))
+    finally:
+        monkeypatch.delenv("ALPHAGO_AMD_FAULT")
+        faults.reload_from_env()
+    a = ckpt.load(str(tmp_path / "ref" / "rl_checkpoint.pt"))
+    b = ckpt.load(str(tmp_path / "run" / "rl_checkpoint.pt"))
+    assert torch.equal(a["trainer"]["flat"], b["trainer"]["flat"])
+    assert a["trainer"]["iterations"] == b["trainer"]["iterations"]
+    assert [os.path.basename(p) for p in a["pool"]] == [os.path.basename(p) for p in b["pool"]]
+    strip = lambda h: [{k: v for k, v in r.items() if not k.endswith("_per_s")} for r in h]  # noqa: E731
+    assert strip(ref["history"]) == strip(got["history"])
+
+
+def _torchrun_cli(argv, nproc=2, timeout=400):
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.pop("ALPHAGO_AMD_FAULT", None)
+    env["PYTHONPATH"] = root + os.pathsep + env.get("PYTHONPATH", "")
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    env["HIP_VISIBLE_DEVICES"] = ""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % nproc,
+           "--master-addr=127.0.0.1", "--master-port=%d" % port, "-m", "alphago_amd"] + argv
+    return subprocess.run(cmd, env=env, timeout=timeout, capture_output=True, text=True)
+
+
+def test_value_pipeline_two_ranks_cli(tmp_path):
+    """BASELINE config 5 as shipped, on 2 gloo ranks: value-generate writes one
+    merged dataset (each rank's games, LZF-chunked), train-value trains DP on
+    per-rank shards of it."""
+    import json
+
+    from alphago_amd.io.h5lite import H5File
+
+    j, w = _save_policy(tmp_path, "cpu")
+    data = str(tmp_path / "v.h5")
+    r = _torchrun_cli(["value-generate", j, j, data, "--games", "6", "--batch-games", "6", "--max-u", "15"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert not os.path.exists(data + ".rank0") and not os.path.exists(data + ".rank1")
+    with H5File(data) as f:
+        n = f["states"].shape[0]
+        assert f["states"].chunked and n == f["outcomes"].shape[0]
+        assert 6 < n <= 12  # both ranks' games
+        assert set(np.unique(f["outcomes"].read())) <= {-1, 0, 1}
+    v = CNNValue(VALUE_FEATURES, board=9, filters_per_layer=8, layers=2, dense=16, device=torch.device("cpu"))
+    vj = str(tmp_path / "v.json")
+    v.save_model(vj)
+    out = str(tmp_path / "vout")
+    r = _torchrun_cli(["train-value", vj, data, out, "-B", "2", "-E", "2", "--backend", "torch",
+                       "--train-val-test", "0.8", "0.2", "0.0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    meta = json.load(open(os.path.join(out, "metadata.json")))
+    assert len(meta["epochs"]) == 2 and sum(meta["data"]["rows_per_rank"]) == int(0.8 * n) + int(0.2 * n)
+    assert os.path.exists(os.path.join(out, "weights.00001.hdf5"))
+
+
+def test_value_resume_after_injected_fault_is_bit_identical(tmp_path, monkeypatch):
+    from alphago_amd.io.h5lite import H5Writer
+    from alphago_amd.train import checkpoint as ckpt
+    from alphago_amd.utils import faults
+
+    rng = np.random.default_rng(0)
+    data = str(tmp_path / "v.h5")
+    with H5Writer(data) as f:
+        f.create_chunked("states", rng.integers(0, 2, (150, len(VALUE_FEATURES) and 49, 9, 9), dtype=np.uint8), 64)
+        f["outcomes"] = rng.choice([-1, 1], 150).astype(np.int8)
+    torch.manual_seed(0)
+    v = CNNValue(VALUE_FEATURES, board=9, filters_per_layer=8, layers=2, dense=16, device=torch.device("cpu"))
+    vj = str(tmp_path / "v.json")
+    v.save_model(vj, str(tmp_path / "v0.hdf5"))
+
+    def args(out):
+        return [vj, data, out, "-B", "8", "-E", "3", "--backend", "torch", "--checkpoint-every", "2", "--resume"]
+
+    ref = value.train_cli(args(str(tmp_path / "ref")))
+    marker = str(tmp_path / "fired")
+    monkeypatch.setenv("ALPHAGO_AMD_FAULT", "raise@20:once=%s" % marker)  # epoch 1
+    faults.reload_from_env()
+    try:
+        with pytest.raises(faults.InjectedFault):
+            value.train_cli(args(str(tmp_path / "run")))
+        got = value.train_cli(args(str(tmp_path / "run")))
+    finally:
+        monkeypatch.delenv("ALPHAGO_AMD_FAULT")
+        faults.reload_from_env()
+    a = ckpt.load(str(tmp_path / "ref" / "checkpoint.pt"))
+    b = ckpt.load(str(tmp_path / "run" / "checkpoint.pt"))
+    assert torch.equal(a["trainer"]["flat"], b["trainer"]["flat"])
+    assert [e["loss"] for e in ref["epochs"]] == [e["loss"] for e in got["epochs"]]
