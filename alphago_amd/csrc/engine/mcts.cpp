@@ -38,6 +38,7 @@ static Node make_node(int parent, int move, float P) {
   n.N = 0;
   n.W = 0.f;
   n.vl = 0;
+  n.v0 = 0.f;
   n.status = 0;
   return n;
 }
@@ -87,6 +88,19 @@ int Forest::select_child(const SearchTree& tr, int u) const {
   return best;
 }
 
+int Forest::max_expanded_depth(int t) const {
+  const SearchTree& tr = trees_.at(t);
+  int best = -1;
+  const int n = (int)tr.nodes.size();
+  for (int i = 0; i < n; ++i) {
+    if (tr.nodes[i].status != 2) continue;
+    int d = 0;
+    for (int x = tr.nodes[i].parent; x >= 0; x = tr.nodes[x].parent) ++d;
+    best = std::max(best, d);
+  }
+  return best;
+}
+
 void Forest::backup(SearchTree& tr, int leaf, double v_leaf_to_move, bool remove_vl) {
   double val = -v_leaf_to_move;
   int x = leaf;
@@ -126,6 +140,14 @@ void Forest::gather_trees(const int* trees, int ntrees, int leaves_per_tree, std
           stop_tree = true;
           break;
         }
+        if (depth >= playout_depth_ && nd.status == 2) {
+          // depth-limited playout (reference mcts.py _DFS(nDepth=L)): the tree does not grow
+          // below L; the node at the cap is scored as a leaf again.  Its stored first
+          // evaluation is backed up -- what re-evaluating the same position with the same
+          // network returns (lambda = 0); with rollouts (lambda > 0) the first mix is reused.
+          backup(tr, u, (double)nd.v0, true);
+          break;
+        }
         if (nd.status == 0 || depth >= playout_depth_) {
           if (st.is_end_of_game) {
             nd.status = 3;
@@ -141,7 +163,7 @@ void Forest::gather_trees(const int* trees, int ntrees, int leaves_per_tree, std
           }
         }
         int c = select_child(tr, u);
-        if (c < 0) {  // expanded with no children cannot happen (pass is always a child)
+        if (c < 0) {  // defensive: apply_range gives every expanded node >= 1 child (PASS when nothing is sensible)
           for (int x = u; x >= 0; x = tr.nodes[x].parent) tr.nodes[x].vl -= 1;
           stop_tree = true;
           break;
@@ -294,6 +316,7 @@ void Forest::apply_range(int i0, int i1, const float* priors, const float* value
       double z = rollout(s2);
       v = (1.0 - lmbda_) * v + lmbda_ * z;
     }
+    nd.v0 = (float)v;
     backup(tr, u, v, true);
   }
 }

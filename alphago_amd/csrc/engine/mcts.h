@@ -29,9 +29,11 @@ struct Node {
   float P;
   int32_t N;
   float W;      // sum of values from the perspective of the player who moved into this node
-  int32_t vl;   // pending virtual-loss count
+  float v0;     // the evaluation backed up when the node was expanded (side to move at the node)
+  int16_t vl;   // pending virtual-loss count
   int8_t status;  // 0 unexpanded, 1 pending evaluation, 2 expanded, 3 terminal
 };
+static_assert(sizeof(Node) == 32, "Node stays 32 bytes (NodeStore blocks are 2 MiB)");
 
 // Node storage in fixed 2-MiB blocks that are never moved or freed while the
 // forest lives: growth never copies a tree (a vector doubling would), node
@@ -107,6 +109,8 @@ class Forest {
   int best_move(int t, double temperature);
   void advance(int t, int move);
   int64_t sims(int t) const { return trees_[t].sims; }
+  // deepest expanded node below the root (root = 0); bounded by playout_depth
+  int max_expanded_depth(int t) const;
   int64_t total_evals() const { return total_evals_; }
 
  private:

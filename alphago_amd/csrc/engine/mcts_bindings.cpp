@@ -148,7 +148,8 @@ void bind_mcts(py::module_& m) {
           [](Forest& f, int t, double temp) { return idx_to_tup(f.root_state(t), f.best_move(t, temp)); },
           py::arg("tree"), py::arg("temperature") = 0.0)
       .def("advance", [](Forest& f, int t, py::object mv) { f.advance(t, tup_to_idx(f.root_state(t), mv)); })
-      .def("sims", &Forest::sims);
+      .def("sims", &Forest::sims)
+      .def("max_expanded_depth", &Forest::max_expanded_depth, py::arg("tree"));
 }
 
 }  // namespace ag

@@ -214,3 +214,27 @@ def test_reference_mcts_dfs_and_get_move():
     assert root.nVisits == 1  # Q3 fix: the root is counted
     move = m.get_move(gs)
     m.update_with_move(move)
+
+
+def test_playout_depth_limits_tree_growth():
+    """playout_depth L (reference mcts.py _DFS(nDepth=L)): no node deeper than
+    L below the root is ever expanded; a simulation that reaches an expanded
+    node at depth L backs up that node's evaluation again (visits still count)."""
+    gs = go.GameState(9)
+    for L in (1, 3):
+        calls = []
+
+        def value(s, calls=calls):
+            calls.append(1)
+            return 0.25
+
+        m = MCTS(gs, value, _fake_policy, _fake_policy, lmbda=0.0, playout_depth=L, n_search=200)
+        m.get_move(gs)
+        assert m.forest.max_expanded_depth(0) <= L
+        assert sum(m.root_visits().values()) >= 200
+        if L == 1:  # 200 simulations over 81 root moves: every visited child is at the cap
+            assert m.forest.max_expanded_depth(0) == 1 and len(calls) < 200
+        # with the default (deep) cap the same search grows deeper than 1
+    deep = MCTS(gs, lambda s: 0.0, _fake_policy, _fake_policy, lmbda=0.0, playout_depth=20, n_search=200)
+    deep.get_move(gs)
+    assert deep.forest.max_expanded_depth(0) > 1
