@@ -1,16 +1,23 @@
 """In-tree native build for alphago_amd.
 
-Two shared objects are produced next to the package sources (so they travel to
+Shared objects are produced next to the package sources (so they travel to
 the GPU box with the repository snapshot):
 
 * ``alphago_amd/_engine*.so`` — C++17 rules engine, featurizer and batched MCTS
   (pybind11, built with g++).
-* ``alphago_amd/_hip_kernels.so`` — hand-written CDNA4 HIP kernels for gfx950
-  (compiled directly with hipcc; no hipify, no torch JIT cache), registered as
-  ``torch.ops.alphago_amd.*`` through TORCH_LIBRARY and loaded with
-  ``torch.ops.load_library``.
+* ``alphago_amd/_hip_kernels.so`` — the production hand-written CDNA4 HIP
+  kernels for gfx950 (compiled directly with hipcc; no hipify, no torch JIT
+  cache), registered as ``torch.ops.alphago_amd.*`` through TORCH_LIBRARY and
+  loaded with ``torch.ops.load_library``.  Only production kernels: the
+  kernel-lab tilings are not compiled into it.
+* ``alphago_amd/_hip_kernels_debug.so`` — the same library with -DAGK_DEBUG:
+  device bounds checks in the conv kernels, every op synchronises and raises
+  on a recorded violation (``ALPHAGO_AMD_KERNELS=debug`` selects it).
+* ``alphago_amd/_hip_kernels_lab.so`` — the kernel lab (forward-conv tiling
+  experiments, wgrad / fp8 variants, cycle stamps) as
+  ``torch.ops.alphago_amd_lab.*``, loadable next to the production library.
 
-Usage: ``python -m alphago_amd._build [engine|hip|all] [--force]``.
+Usage: ``python -m alphago_amd._build [engine|hip|debug|lab|all] [--force]``.
 """
 from __future__ import annotations
 
@@ -37,8 +44,20 @@ def engine_path() -> str:
     return os.path.join(PKG, "_engine" + _ext_suffix())
 
 
-def hip_path() -> str:
-    return os.path.join(PKG, "_hip_kernels.so")
+FLAVORS = ("prod", "debug", "lab")
+
+
+def hip_path(flavor: str = "prod") -> str:
+    return os.path.join(PKG, {"prod": "_hip_kernels.so", "debug": "_hip_kernels_debug.so",
+                              "lab": "_hip_kernels_lab.so"}[flavor])
+
+
+def _hip_sources(flavor: str):
+    kd = os.path.join(CSRC, "kernels")
+    if flavor == "lab":
+        return [os.path.join(kd, f) for f in ("conv.hip", "conv_fwd_variants.hip", "conv_fp8.hip", "ops_lab.cpp")]
+    srcs = sorted(glob.glob(os.path.join(kd, "*.hip")) + glob.glob(os.path.join(kd, "*.cpp")))
+    return [f for f in srcs if os.path.basename(f) not in ("conv_fwd_variants.hip", "ops_lab.cpp")]
 
 
 def _digest(paths, extra: str = "") -> str:
@@ -131,10 +150,10 @@ def _torch_paths():
     return incs, libdir, abi
 
 
-def build_hip(force: bool = False, verbose: bool = False) -> str:
-    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) + glob.glob(os.path.join(CSRC, "kernels", "*.cpp")))
+def build_hip(force: bool = False, verbose: bool = False, flavor: str = "prod") -> str:
+    srcs = _hip_sources(flavor)
     hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
-    out = hip_path()
+    out = hip_path(flavor)
     incs, libdir, abi = _torch_paths()
     common = [
         "-O3",
@@ -146,7 +165,8 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
         "-DTORCH_EXTENSION_NAME=_hip_kernels",
         "-Wno-unused-result",
         "-Wno-deprecated-declarations",
-    ]
+    ] + {"prod": [], "debug": ["-DAGK_DEBUG=1"],
+         "lab": ["-DAGK_KERNEL_LAB=1", "-Dagk=agk_lab", "-Dagk_ops=agk_lab_ops"]}[flavor]
     hip_flags = ["--offload-arch=" + ARCH, "-fgpu-rdc" if False else "-fno-gpu-rdc", "-munsafe-fp-atomics"]
     digest = _digest(srcs + hdrs, " ".join(common + hip_flags))
     if not force and _up_to_date(out, digest):
@@ -156,7 +176,7 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     hipcc = os.path.join(ROCM, "bin", "hipcc")
 
     def compile_one(src):
-        obj = os.path.join(BUILD, "hip_" + os.path.basename(src) + ".o")
+        obj = os.path.join(BUILD, "hip_%s_%s.o" % (flavor, os.path.basename(src)))
         # every translation unit is compiled for gfx950 only (the op registration
         # file includes the kernel headers)
         cmd = [hipcc, "-x", "hip", *common, *hip_flags, *inc_flags, "-c", src, "-o", obj]
@@ -190,8 +210,11 @@ def build_hip(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
-def build_all(force: bool = False, verbose: bool = False):
-    return build_engine(force, verbose), build_hip(force, verbose)
+def build_all(force: bool = False, verbose: bool = False, flavors=FLAVORS):
+    """Engine + every HIP library flavor; returns (engine path, production HIP path)."""
+    eng = build_engine(force, verbose)
+    paths = [build_hip(force, verbose, f) for f in flavors]
+    return eng, paths[0]
 
 
 if __name__ == "__main__":
@@ -202,6 +225,10 @@ if __name__ == "__main__":
         print("engine:", build_engine(force, verbose))
     if what in ("hip", "all"):
         print("hip:", build_hip(force, verbose))
+    if what in ("debug", "all"):
+        print("hip debug:", build_hip(force, verbose, "debug"))
+    if what in ("lab", "all"):
+        print("hip lab:", build_hip(force, verbose, "lab"))
     if what == "selftest":
         san = sys.argv[sys.argv.index("--sanitize") + 1] if "--sanitize" in sys.argv else ""
         print("selftest:", build_selftest(san, force, verbose))

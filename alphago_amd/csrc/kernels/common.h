@@ -3,6 +3,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdexcept>
+#include <string>
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -12,6 +15,12 @@ typedef __attribute__((ext_vector_type(2))) float f32x2;
 #define AG_LDS(p) ((__attribute__((address_space(3))) void*)(p))
 
 namespace agk {
+
+// Host: throw on a HIP error (checked hipFuncSetAttribute etc.); surfaces in
+// Python as a RuntimeError through the op wrappers.
+inline void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
 
 // Exact unsigned division by a runtime constant d (x < 2^32, d < 2^16):
 // q = (x * m) >> 40 with m = ceil(2^40 / d), computed once on the host.

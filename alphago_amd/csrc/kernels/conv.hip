@@ -92,11 +92,27 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   size_t st_w = 0;
   auto stage = [&](int buf) {
     char* base = smem + buf * STAGE;
+#ifdef AGK_DEBUG
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) {
+      const long long xo = (long long)arow[i] + st_a + st_c0;
+      const bool ok = AGK_DCHECK(xo >= 0 && xo + 8 <= a.x_elems, DBG_FWD_X);
+      glds16(a.x + (ok ? xo : 0), base + (wave * A_ROWS_PW + i * 8) * 128);
+    }
+    const __bf16* wt = a.w + st_w + st_c0;
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i) {
+      const long long wo = (long long)st_w + st_c0 + brow[i];
+      const bool ok = AGK_DCHECK(wo >= 0 && wo + 8 <= a.w_elems, DBG_FWD_W);
+      glds16(ok ? wt + brow[i] : a.w, base + A_BYTES + (wave * B_ROWS_PW + i * 8) * 128);
+    }
+#else
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) glds16(a.x + arow[i] + st_a + st_c0, base + (wave * A_ROWS_PW + i * 8) * 128);
     const __bf16* wt = a.w + st_w + st_c0;
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) glds16(wt + brow[i], base + A_BYTES + (wave * B_ROWS_PW + i * 8) * 128);
+#endif
     // branch-free cursor advance (selects), so a caller can interleave the
     // DMA with MFMAs inside one basic block
     st_c0 += 64;
@@ -296,8 +312,8 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   ep.store(a, acc, ep_mrow);
 }
 
-static int g_fwd_bm = 0;  // 0 = auto
 
+#ifdef AGK_KERNEL_LAB
 // ------------------------------------ forward, pixel operand straight from L2
 // Probe (scripts/probes/glds_rate.hip): LDS-DMA fills a CU at ~46 B/clk and
 // serialises with ds_read traffic, so in the LDS-staged kernels the LDS port
@@ -469,25 +485,21 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_ga_kernel(ConvFwdArgs a) {
 template <int BN, int MODE>
 static void launch_fwd_ga(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * BN * 128;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_ga_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_ga_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   constexpr int BM = 8 * 16 * 3;
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_ga_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
 }
 
+#endif  // AGK_KERNEL_LAB
+
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV>), grid, dim3(BM / MBW * 8), smem, st,
                      a);
@@ -496,34 +508,36 @@ static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
 
 template <int BN, int MODE>
 static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
-  int bm = g_fwd_bm;
-  // kernel-lab variants (conv_fwd_variants.hip); fall back to the default
-  // when one does not apply to this geometry
-  if (bm == -1 || bm == 2 || bm == 4 || bm == 5 || bm == 6 || bm == 32) {
-    if (launch_conv_fwd_variant(bm, a, MODE, st)) return;
-    bm = 0;
-  }
+  int bm = a.tile;
   // forward and dgrad: 96x96-per-wave tiles (147 KB LDS).  dgrad used to keep
   // a 112-KB tile so that a wgrad workgroup (48 KB) could share its CU, but the
   // concurrent pair is bound by the same per-CU operand delivery either way;
   // the larger tile moves fewer bytes per MFMA (bench: 106.2k -> 108.5k pos/s,
   // scripts/bench_variants.sh).
-  if (bm <= 0) bm = (a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
-  // tile codes: 128 / 256 (64-pixel waves), 2568 (BM 256, 128-pixel waves: 4 waves, 1 per SIMD),
-  // 384 (default), 9 / 10 (DMA spread through the MFMAs), 7 / 8 (32x32x16 MFMA)
-  if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
-  else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);  // epilogue loads after the loop
+  if (bm == 0) bm = (a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
+  // production tile codes: 128 / 256 (64-pixel waves), 384 (default, 96x96 per wave)
+  if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);
+  else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
+  else if (bm == 128) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
+#ifdef AGK_KERNEL_LAB
+  // kernel-lab tile codes (profiles/r1_fwd_kernel_experiments.md):
+  // conv_fwd_variants.hip (-1, 2, 4, 5, 6, 32), 2560 (epilogue loads after the loop),
+  // 2568 (BM 256, 128-pixel waves), 11 (pixel operand from L2), 9 / 10 (DMA spread
+  // through the MFMAs), 7 / 8 (32x32x16 MFMA)
+  else if ((bm == -1 || bm == 2 || bm == 4 || bm == 5 || bm == 6 || bm == 32) &&
+           launch_conv_fwd_variant(bm, a, MODE, st)) return;
+  else if (bm == -1 || bm == 2 || bm == 4 || bm == 5 || bm == 6 || bm == 32) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
+  else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);
   else if (bm == 2568) launch_fwd_bm<BN, MODE, 256, 8>(a, st);
-  else if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);  // 96x96 per wave, 147 KB LDS
-  else if (bm == 11) launch_fwd_ga<BN, MODE>(a, st);  // pixel operand straight from L2, weights via LDS
+  else if (bm == 11) launch_fwd_ga<BN, MODE>(a, st);
   else if (bm == 9) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
   else if (bm == 10) launch_fwd_bm<BN, MODE, 256, 4, false, false, false, true>(a, st);
   else if (bm == 7) launch_fwd_bm<BN, MODE, 384, 6, false, false, true>(a, st);
   else if (bm == 8) launch_fwd_bm<BN, MODE, 256, 4, false, false, true>(a, st);
-  else launch_fwd_bm<BN, MODE, 128, 4>(a, st);
+#endif
+  else throw std::invalid_argument("conv_fwd: unknown tile code " + std::to_string(bm));
 }
 
-void set_conv_fwd_tile(int bm) { g_fwd_bm = bm; }
 
 template <int MODE>
 static void launch_fwd_mode(const ConvFwdArgs& a, hipStream_t st) {
@@ -654,6 +668,27 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
     for (int sub = 0; sub < KSUB; ++sub) {
       const __bf16* dsrc = a.dz + dzr[sub] + n0 + half;
       const __bf16* xsrc = a.x + xr[sub] + half;
+#ifdef AGK_DEBUG
+#pragma unroll
+      for (int i = 0; i < IPW; ++i) {
+        const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
+        if (jj >= 0 && jj < WN / 16) {
+          const long long o = (long long)dzr[sub] + n0 + half + jj * 16;
+          const bool ok = AGK_DCHECK(o >= 0 && o + 8 <= a.dz_elems, DBG_WG_DZ);
+          glds16(ok ? dsrc + jj * 16 : a.dz, base + sub * SUB + jj * 1024);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < IPW; ++i) {
+        const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
+        if (jj >= WN / 16 && jj < NINSTR / KSUB) {
+          const int xj = jj - WN / 16;  // tap xj / XP, channel piece xj % XP
+          const long long o = (long long)xr[sub] + half + (xj / XP) * a.Cin + (xj % XP) * 16;
+          const bool ok = AGK_DCHECK(o >= 0 && o + 8 <= a.x_elems, DBG_WG_X);
+          glds16(ok ? xsrc + (xj / XP) * a.Cin + (xj % XP) * 16 : a.x, base + sub * SUB + jj * 1024);
+        }
+      }
+#else
 #pragma unroll
       for (int i = 0; i < IPW; ++i) {
         const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
@@ -667,6 +702,7 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
           glds16(xsrc + (xj / XP) * a.Cin + (xj % XP) * 16, base + sub * SUB + jj * 1024);
         }
       }
+#endif
     }
   };
 
@@ -938,19 +974,20 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_ring_kernel(ConvWgradArgs a
 }
 
 constexpr int kWgradKsub = 1;
-static int g_wgrad_variant = 0;  // 0 = 2-buffer, 3/4 = ring with that many LDS slots
+// ConvWgradArgs::variant: 0 = production 2-buffer kernel (tap-merged rows for
+// 64-wide c tiles); kernel-lab build only: 1 = one tap per workgroup,
+// 2 = 256-thread tile, 3 / 4 = LDS ring with that many slots
 
+#ifdef AGK_KERNEL_LAB
 template <int WN, int WC, int NS>
 static void launch_wgrad_ring(const ConvWgradArgs& a, dim3 grid, hipStream_t st) {
   constexpr int smem = NS * (WN + WC) * 64;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_wgrad_ring_kernel<WN, WC, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_ring_kernel<WN, WC, NS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   hipLaunchKernelGGL((conv_wgrad_ring_kernel<WN, WC, NS>), grid, dim3(512), smem, st, a);
 }
+#endif
 
 template <int WN, int TAPS>
 static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
@@ -960,72 +997,73 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
     // on the backward's serial tail; the slab columns 48..63 stay unwritten
     // (the reduce reads only cin_real of them)
     constexpr int smem = 2 * (WN + 48 * TAPS) * 64 * kWgradKsub;
-    static bool attr48 = false;
-    if (!attr48) {
-      hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-      attr48 = true;
-    }
+    static const hipError_t attr48 = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr48, "hipFuncSetAttribute(max dynamic LDS)");
     dim3 grid(a.nsplit, a.T / TAPS, a.Cout / WN);
     hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS>), grid, dim3(384), smem, st, a);
     return;
   }
   constexpr int smem = 2 * (WN + 64 * TAPS) * 64 * kWgradKsub;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, 64, kWgradKsub, 4, TAPS>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, 64, kWgradKsub, 4, TAPS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid(a.nsplit, a.T / TAPS, (a.Cout / WN) * (a.Cin / 64));
   hipLaunchKernelGGL((conv_wgrad_kernel<WN, 64, kWgradKsub, 4, TAPS>), grid, dim3(512), smem, st, a);
 }
 
-int wgrad_tap_group(int Cout, int Cin, int K) {
+int wgrad_tap_group(int Cout, int Cin, int K, int variant) {
   const bool c64 = Cin % 192 != 0 && Cin % 128 != 0;
   (void)Cout;
-  return (c64 && g_wgrad_variant == 0 && (K == 3 || K == 5)) ? K : 1;
+  return (c64 && variant == 0 && (K == 3 || K == 5)) ? K : 1;
 }
 
 template <int WN, int WC>
 static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
   dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
-  if (g_wgrad_variant == 3 || g_wgrad_variant == 4) {
-    if (g_wgrad_variant == 3) launch_wgrad_ring<WN, WC, 3>(a, grid, st);
+  constexpr int KS = kWgradKsub;
+  constexpr int smem = 2 * (WN + WC) * 64 * KS;
+#ifdef AGK_KERNEL_LAB
+  if (a.variant == 3 || a.variant == 4) {
+    if (a.variant == 3) launch_wgrad_ring<WN, WC, 3>(a, grid, st);
     else launch_wgrad_ring<WN, WC, 4>(a, grid, st);
     return;
   }
-  constexpr int KS = kWgradKsub;
-  constexpr int smem = 2 * (WN + WC) * 64 * KS;
-  if (g_wgrad_variant == 2 && WC % 32 == 0 && WC >= 64) {
-    static bool attr2 = false;
-    if (!attr2) {
-      hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          smem);
-      attr2 = true;
-    }
+  if (a.variant == 2 && WC % 32 == 0 && WC >= 64) {
+    static const hipError_t attr2 = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          smem);  // once per instantiation (thread-safe static)
+  hip_check(attr2, "hipFuncSetAttribute(max dynamic LDS)");
     hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS, 2>), grid, dim3(256), smem, st, a);
     return;
   }
+#else
+  if (a.variant != 0) throw std::invalid_argument("conv_wgrad: variant " + std::to_string(a.variant) +
+                                                  " is a kernel-lab variant");
+#endif
   if constexpr (WC == 64) {
-    // tap-merged kernel rows (see conv_wgrad_kernel); variant 1 forces one tap per workgroup
-    if (g_wgrad_variant != 1 && (a.K == 3 || a.K == 5)) {
+    // tap-merged kernel rows (see conv_wgrad_kernel); lab variant 1 forces one tap per workgroup
+    if (a.variant != 1 && (a.K == 3 || a.K == 5)) {
       if (a.K == 3) launch_wgrad_taps<WN, 3>(a, st);
       else launch_wgrad_taps<WN, 5>(a, st);
       return;
     }
   }
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS>), grid, dim3(512), smem, st, a);
 }
 
-void set_wgrad_variant(int v) { g_wgrad_variant = v; }
-
 int wgrad_stage_pixels() { return 32 * kWgradKsub; }
+
+#ifdef AGK_DEBUG
+unsigned debug_error_fetch_and_clear(hipStream_t st) {
+  hip_check(hipStreamSynchronize(st), "debug: stream synchronize");
+  unsigned code = 0, zero = 0;
+  hip_check(hipMemcpyFromSymbol(&code, HIP_SYMBOL(g_dbg_err), sizeof(code)), "debug: read error word");
+  if (code) hip_check(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_err), &zero, sizeof(zero)), "debug: clear error word");
+  return code;
+}
+#endif
 
 void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
   ConvWgradArgs a = a_in;

@@ -8,6 +8,26 @@
 
 namespace agk {
 
+// Debug build (AGK_DEBUG): device bounds checks.  AGK_DCHECK(cond, code)
+// evaluates to cond; when it is false the code is OR-ed into a per-module error
+// word (a vector atomic) and the caller skips / redirects the access, so a bad
+// offset is reported (debug_error_fetch_and_clear -> Python RuntimeError)
+// instead of touching memory outside the tensor.  Release builds: always true.
+#ifdef AGK_DEBUG
+static __device__ unsigned g_dbg_err;
+#define AGK_DCHECK(cond, code) \
+  ((cond) ? true : (atomicOr(&::agk::g_dbg_err, (unsigned)(code)), false))
+#else
+#define AGK_DCHECK(cond, code) true
+#endif
+enum : unsigned {
+  DBG_FWD_X = 1u << 0,   // conv_fwd: activation (pixel operand) staging offset
+  DBG_FWD_W = 1u << 1,   // conv_fwd: weight staging offset
+  DBG_FWD_Y = 1u << 2,   // conv_fwd: epilogue store offset
+  DBG_WG_X = 1u << 3,    // conv_wgrad: activation staging offset
+  DBG_WG_DZ = 1u << 4,   // conv_wgrad: gradient staging offset
+};
+
 template <int N>
 __device__ __forceinline__ void vmcnt_wait() {
   if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -116,7 +136,12 @@ struct ConvEpilogue {
 #pragma unroll
           for (int r = 0; r < 4; ++r) bits |= ((float)o[r] > 0.f ? 1u : 0u) << (4 * i + r);
         }
+#ifdef AGK_DEBUG
+        const long long yo = (long long)ooff[j] + i * 16;
+        if (AGK_DCHECK(yo >= 0 && yo + 4 <= a.y_elems, DBG_FWD_Y)) *(bf16x4*)(a.y + yo) = o;
+#else
         *(bf16x4*)(a.y + ooff[j] + i * 16) = o;
+#endif
       }
       if constexpr (MODE == MODE_BIAS_RELU)
         if (a.mbits_out) a.mbits_out[(size_t)pix[j] * mwords + mslot] = bits;

@@ -403,18 +403,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   }
 }
 
-static int g_fp8_variant = 2;  // 0 = LDS-staged conv_fwd_fp8_kernel, 1-4 = pixel operand from L2 (tilings below)
-void set_fp8_variant(int v) { g_fp8_variant = v; }
+// ConvFp8Args::variant: 0 = production (pixel operand from L2, 48 px/wave,
+// weights in 4 parts); kernel-lab build only: 1 / 3 / 4 = other L2-operand
+// tilings, 5 = LDS-staged conv_fwd_fp8_kernel
 
 template <int BN, int MB, int NPART, bool OB, bool OF>
 static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
   constexpr int smem = 2 * BN * 128 + 64;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   constexpr int BM = 128 * MB;
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF>), grid, dim3(512), smem, st, a);
@@ -422,28 +420,33 @@ static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
 
 template <int BN, bool OB, bool OF>
 static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
-  if (g_fp8_variant != 0 && (BN * 128) % (16 * 512) == 0) {
+#ifndef AGK_KERNEL_LAB
+  if (a.variant != 0) throw std::invalid_argument("conv_fwd_fp8: variant " + std::to_string(a.variant) +
+                                                  " is a kernel-lab variant");
+#endif
+  if (a.variant != 5 && (BN * 128) % (16 * 512) == 0) {
     if constexpr (BN == 192) {
-      // 1: 32 px/wave, weights read in 2 parts; 2: 48 px/wave, 4 parts (default);
+      // 0: 48 px/wave, weights read in 4 parts (production); lab: 1: 32 px/wave, 2 parts;
       // 3: 32 px/wave, 3 parts; 4: 48 px/wave, 6 parts
-      if (g_fp8_variant == 2) launch_fp8_ga<BN, 3, 4, OB, OF>(a, st);
-      else if (g_fp8_variant == 3) launch_fp8_ga<BN, 2, 3, OB, OF>(a, st);
-      else if (g_fp8_variant == 4) launch_fp8_ga<BN, 3, 6, OB, OF>(a, st);
+      if (a.variant == 0) launch_fp8_ga<BN, 3, 4, OB, OF>(a, st);
+#ifdef AGK_KERNEL_LAB
+      else if (a.variant == 3) launch_fp8_ga<BN, 2, 3, OB, OF>(a, st);
+      else if (a.variant == 4) launch_fp8_ga<BN, 3, 6, OB, OF>(a, st);
       else launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
+#endif
     } else {
       launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
     }
     return;
   }
+#ifdef AGK_KERNEL_LAB
   constexpr int smem = 2 * (256 * 128 + BN * 128);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_fp8_kernel<BN, OB, OF>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_fp8_kernel<BN, OB, OF>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + 255) / 256, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_fp8_kernel<BN, OB, OF>), grid, dim3(512), smem, st, a);
+#endif
 }
 
 template <int BN>

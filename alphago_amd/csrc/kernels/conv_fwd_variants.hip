@@ -513,33 +513,25 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pp_kernel(ConvFwdArgs a) {
   ep.store(a, acc, ep_mrow);
 }
 
-static unsigned long long* g_conv_dbg = nullptr;
-void set_conv_debug(unsigned long long* buf) { g_conv_dbg = buf; }
+// diagnostic stamps: the lab op passes a buffer in ConvFwdArgs::dbg (scripts/conv_stamps.py)
 
 template <int BN, int MODE>
 static void launch_fwd_pp(const ConvFwdArgs& a_in, hipStream_t st) {
   constexpr int smem = PP_SLOTS * (PP_BM * 64 + BN * 64);
   if constexpr (BN == 192 && MODE == MODE_BIAS_RELU) {
-    if (g_conv_dbg) {  // diagnostic instantiation with segment stamps
-      static bool attr_d = false;
-      if (!attr_d) {
-        hipFuncSetAttribute((const void*)conv_fwd_pp_kernel<BN, MODE, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        attr_d = true;
-      }
+    if (a_in.dbg) {  // diagnostic instantiation with segment stamps
+      static const hipError_t attr_d = hipFuncSetAttribute((const void*)conv_fwd_pp_kernel<BN, MODE, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr_d, "hipFuncSetAttribute(max dynamic LDS)");
       ConvFwdArgs a = a_in;
-      a.dbg = g_conv_dbg;
       dim3 grid((a.M + PP_BM - 1) / PP_BM, a.Cout / BN);
       hipLaunchKernelGGL((conv_fwd_pp_kernel<BN, MODE, true>), grid, dim3(512), smem, st, a);
       return;
     }
   }
   const ConvFwdArgs& a = a_in;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_pp_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_pp_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + PP_BM - 1) / PP_BM, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_pp_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
 }
@@ -547,12 +539,9 @@ static void launch_fwd_pp(const ConvFwdArgs& a_in, hipStream_t st) {
 template <int BN, int MODE>
 static void launch_fwd_ring(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = RING_SLOTS * (RING_BM * 64 + BN * 64);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_ring_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_ring_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + RING_BM - 1) / RING_BM, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_ring_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
 }
@@ -560,12 +549,9 @@ static void launch_fwd_ring(const ConvFwdArgs& a, hipStream_t st) {
 template <int BN, int MODE>
 static void launch_fwd_halo(const ConvFwdArgs& a_in, hipStream_t st) {
   constexpr int smem = 2 * HALO_ROWS * 128 + 3 * BN * 128;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_halo_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_halo_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   ConvFwdArgs a = a_in;
   const int B = a.M / (a.S * a.S);
   a.M = B * a.HPo * a.HPo;  // padded positions
@@ -1231,12 +1217,9 @@ static int halo2_rows_needed(int M, int S, int HPi, int K, int offi) {
 template <int BN, int MODE>
 static void launch_fwd_halo2(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * H2_ROWS * 128 + 2 * BN * 128;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_halo2_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_halo2_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + H2_BM - 1) / H2_BM, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_halo2_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
 }
@@ -1245,27 +1228,20 @@ template <int BN, int MODE>
 static void launch_fwd_hpp(const ConvFwdArgs& a_in, hipStream_t st) {
   constexpr int smem = 2 * HC_ROWS * 128 + 3 * BN * 128;
   if constexpr (BN == 192 && MODE == MODE_BIAS_RELU) {
-    if (g_conv_dbg) {  // diagnostic instantiation with segment stamps
-      static bool attr_d = false;
-      if (!attr_d) {
-        hipFuncSetAttribute((const void*)conv_fwd_hpp_kernel<BN, MODE, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        attr_d = true;
-      }
+    if (a_in.dbg) {  // diagnostic instantiation with segment stamps
+      static const hipError_t attr_d = hipFuncSetAttribute((const void*)conv_fwd_hpp_kernel<BN, MODE, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr_d, "hipFuncSetAttribute(max dynamic LDS)");
       ConvFwdArgs a = a_in;
-      a.dbg = g_conv_dbg;
       dim3 grid((a.M + H2_BM - 1) / H2_BM, a.Cout / BN);
       hipLaunchKernelGGL((conv_fwd_hpp_kernel<BN, MODE, true>), grid, dim3(512), smem, st, a);
       return;
     }
   }
   const ConvFwdArgs& a = a_in;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_hpp_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_hpp_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + H2_BM - 1) / H2_BM, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_hpp_kernel<BN, MODE>), grid, dim3(512), smem, st, a);
 }
@@ -1276,24 +1252,17 @@ static void launch_fwd_h32(const ConvFwdArgs& a_in, hipStream_t st) {
   ConvFwdArgs a = a_in;
   dim3 grid((a.M + H2_BM - 1) / H2_BM, a.Cout / BN);
   if constexpr (BN == 192 && MODE == MODE_BIAS_RELU && K == 3) {
-    if (g_conv_dbg) {  // diagnostic instantiation with segment stamps
-      static bool attr_d = false;
-      if (!attr_d) {
-        hipFuncSetAttribute((const void*)conv_fwd_h32_kernel<BN, MODE, K, true>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        attr_d = true;
-      }
-      a.dbg = g_conv_dbg;
+    if (a_in.dbg) {  // diagnostic instantiation with segment stamps
+      static const hipError_t attr_d = hipFuncSetAttribute((const void*)conv_fwd_h32_kernel<BN, MODE, K, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr_d, "hipFuncSetAttribute(max dynamic LDS)");
       hipLaunchKernelGGL((conv_fwd_h32_kernel<BN, MODE, K, true>), grid, dim3(512), smem, st, a);
       return;
     }
   }
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)conv_fwd_h32_kernel<BN, MODE, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        smem);
-    attr = true;
-  }
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_h32_kernel<BN, MODE, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        smem);  // once per instantiation (thread-safe static)
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   hipLaunchKernelGGL((conv_fwd_h32_kernel<BN, MODE, K>), grid, dim3(512), smem, st, a);
 }
 

@@ -21,7 +21,9 @@ struct ConvFwdArgs {
   int HPi, offi;       // input padded side, (input pad - K/2)
   int HPo, Po;         // output padded side and pad
   FastDiv divSS, divS; // filled by the launcher
-  unsigned long long* dbg;  // diagnostic segment-cycle stamps (set_conv_debug), else null
+  int tile;            // 0 = automatic; 128/256/384 fixed tiles; other codes: kernel-lab build only
+  unsigned long long* dbg;  // kernel lab: diagnostic segment-cycle stamps, else null
+  long long x_elems, w_elems, y_elems;  // tensor extents (debug-build bounds checks)
 };
 
 struct ConvWgradArgs {
@@ -34,6 +36,8 @@ struct ConvWgradArgs {
   int ksteps_per_split, nsplit;
   int cin_real;        // real input channels (<= Cin); the zero padding above it is skipped when possible
   FastDiv divSS, divS; // filled by the launcher
+  int variant;         // 0 = production kernel; 1-4 kernel-lab build only
+  long long x_elems, dz_elems;  // tensor extents (debug-build bounds checks)
 };
 
 struct WgradReduceArgs {
@@ -133,16 +137,23 @@ struct ConvFp8Args {
   int HPi, offi, HPo, Po;
   int nch;
   FastDiv divSS, divS;      // filled by the launcher
+  int variant;              // 0 = production (pixel operand from L2, 48 px/wave); lab: 1, 3, 4 other tilings,
+                            // 5 = LDS-staged operands
 };
 
+// Kernel choices are explicit launch arguments (ConvFwdArgs::tile,
+// ConvWgradArgs::variant, ConvFp8Args::variant): no process-global state.
 void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
-void set_conv_debug(unsigned long long* buf);  // non-null: the ping-pong forward records per-segment cycles
-void set_conv_fwd_tile(int bm);  // 0 = auto, -1 = halo kernel, 128/256 = gather kernel tile (A/B tests)
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
-int wgrad_stage_pixels();
-int wgrad_tap_group(int Cout, int Cin, int K);  // taps per wgrad workgroup (tap-merged 64-wide c tiles)
-void set_fp8_variant(int v);  // 0 = LDS-staged fp8 forward, 1-4 = pixel operand from L2 (2 = default)
-void set_wgrad_variant(int v);  // 0 = 2-buffer (default), 3 / 4 = ring with that many LDS slots  // pixels per wgrad pipeline stage (units of ksteps_per_split)
+int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
+int wgrad_tap_group(int Cout, int Cin, int K, int variant);  // taps per wgrad workgroup (tap-merged 64-wide c tiles)
+// a launch the runtime must reject (block of 2048 threads): tests the error path
+void launch_invalid_config_probe(hipStream_t st);
+#ifdef AGK_DEBUG
+// debug build: waits for the stream, returns and clears the bounds-violation
+// code recorded by the conv kernels (0 = none)
+unsigned debug_error_fetch_and_clear(hipStream_t st);
+#endif
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
 void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st);

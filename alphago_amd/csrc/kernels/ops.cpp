@@ -1,97 +1,27 @@
 // PyTorch custom-op registration for the gfx950 kernels: torch.ops.alphago_amd.*
 // All ops write into caller-provided buffers (no allocation inside), run on the
 // current HIP stream and are therefore safe to capture in HIP graphs.
-#include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <torch/library.h>
-
-#include "kernels.h"
+#include "ops_conv.h"
 
 namespace {
 
-using at::Tensor;
-
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
-
-#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a device tensor")
-#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
-#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
-#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
-
-const __bf16* bfp(const Tensor& t) { return reinterpret_cast<const __bf16*>(t.data_ptr()); }
-__bf16* bfp_mut(const Tensor& t) { return reinterpret_cast<__bf16*>(t.data_ptr()); }
+using namespace agk_ops;
 
 // x: (B, HPi, HPi, Cin) bf16; w: (T, Cout, Cin) bf16; y: (B, HPo, HPo, Cout) bf16
 void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const c10::optional<Tensor>& mask,
               const Tensor& y, int64_t K, int64_t S, int64_t Pin, int64_t Po, int64_t mode,
-              const c10::optional<Tensor>& mbits) {
-  CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
-  CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
-  CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y);
-  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && w.dim() == 3, "bad ranks");
-  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3);
-  const int64_t HPo = y.size(1), Cout = y.size(3);
-  TORCH_CHECK(x.size(2) == HPi && y.size(2) == HPo && y.size(0) == B, "bad spatial dims");
-  TORCH_CHECK(w.size(0) == K * K && w.size(1) == Cout && w.size(2) == Cin, "w must be (K*K, Cout, Cin)");
-  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "channels must be multiples of 64");
-  TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin && HPo == S + 2 * Po, "padding/geometry mismatch");
-  TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31) && B * HPo * HPo * Cout < (1ll << 31), "tensor too large for int32 offsets");
-  agk::ConvFwdArgs a{};
-  a.x = bfp(x);
-  a.w = bfp(w);
-  a.y = bfp_mut(y);
-  a.M = (int)(B * S * S);
-  a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
-  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
-  if (mode == agk::MODE_BIAS_RELU) {
-    TORCH_CHECK(bias.has_value(), "bias required");
-    CHECK_F32(*bias); CHECK_DEV(*bias);
-    TORCH_CHECK(bias->numel() >= Cout, "bias too small");
-    a.bias = bias->data_ptr<float>();
-  } else if (mode == agk::MODE_MASK) {
-    TORCH_CHECK(mask.has_value(), "mask required");
-    CHECK_BF16(*mask); CHECK_CONTIG(*mask);
-    TORCH_CHECK(mask->sizes() == y.sizes(), "mask must match y");
-    a.mask = bfp(*mask);
-  }
-  if (mbits.has_value()) {
-    TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
-    const int64_t words = (Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
-    TORCH_CHECK(mbits->numel() >= B * HPo * HPo * words, "mbits too small: need B*HPo*HPo*words");
-    TORCH_CHECK(mode == agk::MODE_BIAS_RELU || mode == agk::MODE_MASKBITS, "mbits with modes 0 (write) / 3 (read)");
-    if (mode == agk::MODE_BIAS_RELU) a.mbits_out = reinterpret_cast<uint32_t*>(mbits->data_ptr<int>());
-    else a.mbits_in = reinterpret_cast<const uint32_t*>(mbits->data_ptr<int>());
-  }
-  TORCH_CHECK(mode != agk::MODE_MASKBITS || a.mbits_in, "mode 3 needs mbits");
-  if (a.M == 0) return;
-  agk::launch_conv_fwd(a, (int)mode, cur_stream());
+              const c10::optional<Tensor>& mbits, int64_t tile) {
+  // production tilings only: 0 = automatic, or a fixed 128 / 256 / 384-pixel tile
+  TORCH_CHECK(tile == 0 || tile == 128 || tile == 256 || tile == 384,
+              "conv_fwd tile ", tile, " is not a production tiling (0, 128, 256, 384); kernel-lab variants are in "
+              "torch.ops.alphago_amd_lab (alphago_amd.ops.lab())");
+  conv_fwd_impl(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, (int)tile);
 }
 
 // slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
                 int64_t Pin, int64_t Po, int64_t cin_real) {
-  CHECK_DEV(x); CHECK_DEV(dz); CHECK_DEV(slab); CHECK_DEV(dbslab);
-  CHECK_BF16(x); CHECK_BF16(dz); CHECK_F32(slab); CHECK_F32(dbslab);
-  CHECK_CONTIG(x); CHECK_CONTIG(dz); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
-  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3);
-  const int64_t HPo = dz.size(1), Cout = dz.size(3);
-  const int64_t nsplit = slab.size(0);
-  TORCH_CHECK(slab.dim() == 4 && slab.size(1) == K * K && slab.size(2) == Cout && slab.size(3) == Cin, "bad slab");
-  TORCH_CHECK(dbslab.size(0) == nsplit && dbslab.size(1) == Cout, "bad dbias slab");
-  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "channels must be multiples of 64");
-  TORCH_CHECK(HPi == S + 2 * Pin && HPo == S + 2 * Po && Po >= 1 && Pin >= K / 2, "geometry mismatch");
-  agk::ConvWgradArgs a{};
-  a.x = bfp(x); a.dz = bfp(dz);
-  a.slab = slab.data_ptr<float>();
-  a.dbias_slab = dbslab.data_ptr<float>();
-  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K; a.T = (int)(K * K);
-  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
-  a.cin_real = (cin_real > 0 && cin_real < Cin) ? (int)cin_real : (int)Cin;
-  const int sp = agk::wgrad_stage_pixels();
-  const int nks = (a.M + sp - 1) / sp;
-  a.nsplit = (int)nsplit;
-  a.ksteps_per_split = (nks + a.nsplit - 1) / a.nsplit;
-  agk::launch_conv_wgrad(a, cur_stream());
+  conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, 0);
 }
 
 void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
@@ -111,6 +41,7 @@ void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& g
   a.nsplit = (int)nsplit;
   a.scale = (float)scale; a.beta = (float)beta;
   agk::launch_wgrad_reduce(a, cur_stream());
+  launch_check("conv_wgrad_reduce");
 }
 
 void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::optional<Tensor>& target,
@@ -159,6 +90,7 @@ void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::o
   }
   if (B == 0) return;
   agk::launch_policy_head(a, train, cur_stream());
+  launch_check("policy_head");
 }
 
 // z: (B, S*S) f32 <- y (B, S+2, S+2, C) bf16 . w + b
@@ -172,6 +104,7 @@ void head_logits(const Tensor& y, const Tensor& w, const Tensor& b, const Tensor
   a.B = (int)B; a.S = (int)S; a.C = (int)C; a.C_real = (int)w.numel();
   if (B == 0) return;
   agk::launch_head_logits(a, cur_stream());
+  launch_check("head_logits");
 }
 
 // dz (B, S+2, S+2, C) bf16 <- ReLU'(y) * dlogits x w;  dhead (B, C_real+1) partials
@@ -187,6 +120,7 @@ void head_backward(const Tensor& y, const Tensor& w, const Tensor& dlogits, cons
   a.B = (int)B; a.S = (int)S; a.C = (int)C; a.C_real = (int)w.numel();
   if (B == 0) return;
   agk::launch_head_backward(a, dlogits.data_ptr<float>(), cur_stream());
+  launch_check("head_backward");
 }
 
 void value_out(const Tensor& h, const Tensor& w2, const Tensor& b2, const c10::optional<Tensor>& target,
@@ -215,6 +149,7 @@ void value_out(const Tensor& h, const Tensor& w2, const Tensor& b2, const c10::o
   }
   if (B == 0) return;
   agk::launch_value_out(a, cur_stream());
+  launch_check("value_out");
 }
 
 void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c10::optional<Tensor>& target,
@@ -233,6 +168,7 @@ void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c1
   a.B = (int)B; a.S = (int)S; a.Creal = (int)C; a.Cp = (int)out.size(3); a.P = (int)P;
   if (B == 0) return;
   agk::launch_pack_input(a, cur_stream());
+  launch_check("pack_input");
 }
 
 // ws: list of OIHW fp32; wf: list of (T, Coutp, Cinp) bf16; wd: list (possibly empty entries skipped)
@@ -259,6 +195,7 @@ void pack_weights(at::TensorList ws, at::TensorList wf, at::TensorList wd) {
       }
     }
     agk::launch_pack_weights(a, cur_stream());
+    launch_check("pack_weights");
   }
 }
 
@@ -324,45 +261,14 @@ void featurize(const Tensor& board, const Tensor& ages, const Tensor& meta, cons
   }
   if (B == 0) return;
   agk::launch_featurize(a, cur_stream());
+  launch_check("featurize");
 }
 
 // x: (B, HPi, HPi, Cin) uint8 (e4m3); w: (nch, Cout, 64) uint8; scales int32[2]; out_scale f32[1]
 void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales, const Tensor& out_scale,
                   const c10::optional<Tensor>& amax, const c10::optional<Tensor>& y_bf16,
                   const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S, int64_t Pin, int64_t Po) {
-  CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
-  TORCH_CHECK(x.scalar_type() == at::kByte && w.scalar_type() == at::kByte, "fp8 tensors are stored as uint8");
-  TORCH_CHECK(x.dim() == 4 && w.dim() == 3 && w.size(2) == 64, "x (B,HP,HP,C), w (nch, Cout, 64)");
-  TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2 && out_scale.scalar_type() == at::kFloat, "scales");
-  CHECK_F32(bias);
-  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3), nch = w.size(0), Cout = w.size(1);
-  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && nch % 2 == 0 && nch >= K * K * (Cin / 64), "channel geometry");
-  TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin, "padding/geometry mismatch");
-  TORCH_CHECK(y_bf16.has_value() || y_fp8.has_value(), "need an output");
-  agk::ConvFp8Args a{};
-  a.x = x.data_ptr<uint8_t>(); a.w = w.data_ptr<uint8_t>(); a.bias = bias.data_ptr<float>();
-  a.scales = scales.data_ptr<int>(); a.out_scale = out_scale.data_ptr<float>();
-  const int64_t HPo = S + 2 * Po;
-  if (y_bf16.has_value()) {
-    CHECK_BF16(*y_bf16); CHECK_CONTIG(*y_bf16);
-    TORCH_CHECK(y_bf16->size(0) == B && y_bf16->size(1) == HPo && y_bf16->size(3) == Cout, "y_bf16 shape");
-    a.y_bf16 = bfp_mut(*y_bf16);
-  }
-  if (y_fp8.has_value()) {
-    TORCH_CHECK(y_fp8->scalar_type() == at::kByte && y_fp8->is_contiguous(), "y_fp8 uint8");
-    TORCH_CHECK(y_fp8->size(0) == B && y_fp8->size(1) == HPo && y_fp8->size(3) == Cout, "y_fp8 shape");
-    a.y_fp8 = y_fp8->data_ptr<uint8_t>();
-  }
-  if (amax.has_value()) {
-    TORCH_CHECK(amax->scalar_type() == at::kInt && amax->numel() >= agk::kFp8AmaxSlots,
-                "amax int32[64] (float bits, per-workgroup slots)");
-    a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
-  }
-  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
-  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po; a.nch = (int)nch;
-  TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31), "tensor too large for int32 offsets");
-  if (a.M == 0) return;
-  agk::launch_conv_fwd_fp8(a, cur_stream());
+  conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, 0);
 }
 
 void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c10::optional<Tensor>& scale_dev) {
@@ -379,6 +285,7 @@ void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c1
   }
   agk::launch_pack_weights_fp8(w.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)w.size(0), (int)w.size(1), K, Cout_p,
                                Cin_p, nch, (float)scale, sd, cur_stream());
+  launch_check("pack_weights_fp8");
 }
 
 // per-layer weight scales (device-side, no host sync)
@@ -396,6 +303,7 @@ void fp8_weight_scales(at::TensorList ws, const Tensor& wscale, const Tensor& sc
   a.scales8 = scales8.data_ptr<int>();
   if (ws.empty()) return;
   agk::launch_fp8_weight_scales(a, (int)ws.size(), cur_stream());
+  launch_check("fp8_weight_scales");
 }
 
 void fp8_act_scales(const Tensor& amax, const Tensor& scales8, const Tensor& osc, int64_t margin) {
@@ -405,41 +313,53 @@ void fp8_act_scales(const Tensor& amax, const Tensor& scales8, const Tensor& osc
               "sizes (amax is (L, 64))");
   agk::launch_fp8_act_scales(reinterpret_cast<unsigned*>(amax.data_ptr<int>()), scales8.data_ptr<int>(),
                              osc.data_ptr<float>(), L, (int)margin, cur_stream());
+  launch_check("fp8_act_scales");
 }
 
 void quantize_fp8(const Tensor& x, const Tensor& y, double scale) {
   CHECK_BF16(x); CHECK_CONTIG(x);
   TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 4 == 0, "y");
   agk::launch_quantize_fp8(bfp(x), y.data_ptr<uint8_t>(), x.numel(), (float)scale, cur_stream());
+  launch_check("quantize_fp8");
 }
 
-void set_conv_tile(int64_t bm) { agk::set_conv_fwd_tile((int)bm); }
-// diagnostic: per-wave segment cycle sums of the ping-pong forward, 8 uint64 per wave
-void set_conv_debug(const c10::optional<Tensor>& buf) {
-  if (buf.has_value()) {
-    CHECK_DEV(*buf);
-    TORCH_CHECK(buf->scalar_type() == at::kLong && buf->is_contiguous(), "int64 buffer");
-    agk::set_conv_debug(reinterpret_cast<unsigned long long*>(buf->data_ptr<int64_t>()));
-  } else {
-    agk::set_conv_debug(nullptr);
-  }
+int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) {
+  return agk::wgrad_tap_group((int)cout, (int)cin, (int)K, 0);
 }
-void set_wgrad_variant(int64_t v) { agk::set_wgrad_variant((int)v); }
-void set_fp8_variant(int64_t v) { agk::set_fp8_variant((int)v); }
-int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) { return agk::wgrad_tap_group((int)cout, (int)cin, (int)K); }
 
 void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
   CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
   TORCH_CHECK(p.numel() == g.numel(), "size mismatch");
   agk::launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(), p.numel(), (float)lr, (float)gscale, cur_stream());
+  launch_check("sgd_update");
 }
+
+// A deliberately invalid launch (2048 threads per block, above the 1024
+// limit): the runtime rejects it, launch_check turns that into a Python
+// RuntimeError -- the test of the error path every op shares.
+void selftest_bad_launch() {
+  agk::launch_invalid_config_probe(cur_stream());
+  launch_check("selftest_bad_launch");
+}
+
+#ifdef AGK_DEBUG
+// Debug build only: conv_fwd told that x holds half its real elements, so the
+// kernel's bounds checks see "out-of-range" staging offsets (the accesses are
+// redirected, the real buffer is never overrun) -- exercises the device check
+// -> RuntimeError path end to end.
+void debug_conv_fwd_understated(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& y, int64_t K,
+                                int64_t S, int64_t Pin, int64_t Po) {
+  conv_fwd_impl(x, w, bias, c10::nullopt, y, K, S, Pin, Po, agk::MODE_BIAS_RELU, c10::nullopt, 0, nullptr,
+                x.numel() / 2);
+}
+#endif
 
 }  // namespace
 
 TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
-      "Tensor(b!)? mbits=None) -> ()");
+      "Tensor(b!)? mbits=None, int tile=0) -> ()");
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def(
@@ -464,11 +384,18 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("fp8_weight_scales(Tensor[] ws, Tensor(a!) wscale, Tensor(b!) scales8) -> ()");
   m.def("fp8_act_scales(Tensor(a!) amax, Tensor(b!) scales8, Tensor(c!) osc, int margin) -> ()");
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
-  m.def("set_conv_tile(int bm) -> ()", &set_conv_tile);
-  m.def("set_conv_debug(Tensor? buf) -> ()", &set_conv_debug);
-  m.def("set_wgrad_variant(int v) -> ()", &set_wgrad_variant);
-  m.def("set_fp8_variant(int v) -> ()", &set_fp8_variant);
   m.def("wgrad_tap_group(int cout, int cin, int K) -> int", &wgrad_tap_group);
+  m.def("selftest_bad_launch() -> ()", &selftest_bad_launch);
+  m.def("is_debug_build() -> bool", []() -> bool {
+#ifdef AGK_DEBUG
+    return true;
+#else
+    return false;
+#endif
+  });
+#ifdef AGK_DEBUG
+  m.def("debug_conv_fwd_understated(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int K, int S, int Pin, int Po) -> ()");
+#endif
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
@@ -482,6 +409,9 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("value_out", &value_out);
   m.impl("pack_weights", &pack_weights);
   m.impl("sgd_update", &sgd_update);
+#ifdef AGK_DEBUG
+  m.impl("debug_conv_fwd_understated", &debug_conv_fwd_understated);
+#endif
   m.impl("featurize", &featurize);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8);
   m.impl("pack_weights_fp8", &pack_weights_fp8);

@@ -1,0 +1,166 @@
+// Tensor -> kernel-argument marshalling of the conv ops, shared by the
+// production op library (ops.cpp, torch.ops.alphago_amd) and the kernel-lab
+// library (ops_lab.cpp, torch.ops.alphago_amd_lab).  Every launch is followed
+// by launch_check(): a launch the runtime rejects raises a Python error; in a
+// debug build (AGK_DEBUG) the op also synchronises and raises on any device
+// bounds-check failure recorded by the kernels.
+#pragma once
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <string>
+
+#include "kernels.h"
+
+namespace agk_ops {
+
+using at::Tensor;
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a device tensor")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+#define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+
+inline const __bf16* bfp(const Tensor& t) { return reinterpret_cast<const __bf16*>(t.data_ptr()); }
+inline __bf16* bfp_mut(const Tensor& t) { return reinterpret_cast<__bf16*>(t.data_ptr()); }
+
+// Raise if the last launch on this thread failed (bad configuration, missing
+// code object, ...); with AGK_DEBUG also wait for the kernel and raise on a
+// recorded device bounds violation.
+inline void launch_check(const char* op) {
+  const hipError_t e = hipGetLastError();
+  TORCH_CHECK(e == hipSuccess, op, ": kernel launch failed: ", hipGetErrorString(e));
+#ifdef AGK_DEBUG
+  const unsigned code = agk::debug_error_fetch_and_clear(cur_stream());
+  TORCH_CHECK(code == 0, op, ": device bounds check failed (debug build), code 0x", std::to_string(code));
+#endif
+}
+
+inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+                          const c10::optional<Tensor>& mask, const Tensor& y, int64_t K, int64_t S, int64_t Pin,
+                          int64_t Po, int64_t mode, const c10::optional<Tensor>& mbits, int tile,
+                          unsigned long long* dbg = nullptr, long long x_elems_override = -1) {
+  CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
+  CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
+  CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y);
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && w.dim() == 3, "bad ranks");
+  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3);
+  const int64_t HPo = y.size(1), Cout = y.size(3);
+  TORCH_CHECK(x.size(2) == HPi && y.size(2) == HPo && y.size(0) == B, "bad spatial dims");
+  TORCH_CHECK(w.size(0) == K * K && w.size(1) == Cout && w.size(2) == Cin, "w must be (K*K, Cout, Cin)");
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "channels must be multiples of 64");
+  TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin && HPo == S + 2 * Po, "padding/geometry mismatch");
+  TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31) && B * HPo * HPo * Cout < (1ll << 31), "tensor too large for int32 offsets");
+  agk::ConvFwdArgs a{};
+  a.tile = tile;
+  a.dbg = dbg;
+  a.x_elems = x_elems_override >= 0 ? x_elems_override : x.numel();
+  a.w_elems = w.numel();
+  a.y_elems = y.numel();
+  a.x = bfp(x);
+  a.w = bfp(w);
+  a.y = bfp_mut(y);
+  a.M = (int)(B * S * S);
+  a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
+  if (mode == agk::MODE_BIAS_RELU) {
+    TORCH_CHECK(bias.has_value(), "bias required");
+    CHECK_F32(*bias); CHECK_DEV(*bias);
+    TORCH_CHECK(bias->numel() >= Cout, "bias too small");
+    a.bias = bias->data_ptr<float>();
+  } else if (mode == agk::MODE_MASK) {
+    TORCH_CHECK(mask.has_value(), "mask required");
+    CHECK_BF16(*mask); CHECK_CONTIG(*mask);
+    TORCH_CHECK(mask->sizes() == y.sizes(), "mask must match y");
+    a.mask = bfp(*mask);
+  }
+  if (mbits.has_value()) {
+    TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
+    const int64_t words = (Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
+    TORCH_CHECK(mbits->numel() >= B * HPo * HPo * words, "mbits too small: need B*HPo*HPo*words");
+    TORCH_CHECK(mode == agk::MODE_BIAS_RELU || mode == agk::MODE_MASKBITS, "mbits with modes 0 (write) / 3 (read)");
+    if (mode == agk::MODE_BIAS_RELU) a.mbits_out = reinterpret_cast<uint32_t*>(mbits->data_ptr<int>());
+    else a.mbits_in = reinterpret_cast<const uint32_t*>(mbits->data_ptr<int>());
+  }
+  TORCH_CHECK(mode != agk::MODE_MASKBITS || a.mbits_in, "mode 3 needs mbits");
+  if (a.M == 0) return;
+  agk::launch_conv_fwd(a, (int)mode, cur_stream());
+  launch_check("conv_fwd");
+}
+
+// slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
+inline void conv_wgrad_impl(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K,
+                            int64_t S, int64_t Pin, int64_t Po, int64_t cin_real, int variant) {
+  CHECK_DEV(x); CHECK_DEV(dz); CHECK_DEV(slab); CHECK_DEV(dbslab);
+  CHECK_BF16(x); CHECK_BF16(dz); CHECK_F32(slab); CHECK_F32(dbslab);
+  CHECK_CONTIG(x); CHECK_CONTIG(dz); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
+  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3);
+  const int64_t HPo = dz.size(1), Cout = dz.size(3);
+  const int64_t nsplit = slab.size(0);
+  TORCH_CHECK(slab.dim() == 4 && slab.size(1) == K * K && slab.size(2) == Cout && slab.size(3) == Cin, "bad slab");
+  TORCH_CHECK(dbslab.size(0) == nsplit && dbslab.size(1) == Cout, "bad dbias slab");
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "channels must be multiples of 64");
+  TORCH_CHECK(HPi == S + 2 * Pin && HPo == S + 2 * Po && Po >= 1 && Pin >= K / 2, "geometry mismatch");
+  agk::ConvWgradArgs a{};
+  a.variant = variant;
+  a.x_elems = x.numel();
+  a.dz_elems = dz.numel();
+  a.x = bfp(x); a.dz = bfp(dz);
+  a.slab = slab.data_ptr<float>();
+  a.dbias_slab = dbslab.data_ptr<float>();
+  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K; a.T = (int)(K * K);
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
+  a.cin_real = (cin_real > 0 && cin_real < Cin) ? (int)cin_real : (int)Cin;
+  const int sp = agk::wgrad_stage_pixels();
+  const int nks = (a.M + sp - 1) / sp;
+  a.nsplit = (int)nsplit;
+  a.ksteps_per_split = (nks + a.nsplit - 1) / a.nsplit;
+  agk::launch_conv_wgrad(a, cur_stream());
+  launch_check("conv_wgrad");
+}
+
+inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales,
+                              const Tensor& out_scale, const c10::optional<Tensor>& amax,
+                              const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K,
+                              int64_t S, int64_t Pin, int64_t Po, int variant) {
+  CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
+  TORCH_CHECK(x.scalar_type() == at::kByte && w.scalar_type() == at::kByte, "fp8 tensors are stored as uint8");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 3 && w.size(2) == 64, "x (B,HP,HP,C), w (nch, Cout, 64)");
+  TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2 && out_scale.scalar_type() == at::kFloat, "scales");
+  CHECK_F32(bias);
+  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3), nch = w.size(0), Cout = w.size(1);
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && nch % 2 == 0 && nch >= K * K * (Cin / 64), "channel geometry");
+  TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin, "padding/geometry mismatch");
+  TORCH_CHECK(y_bf16.has_value() || y_fp8.has_value(), "need an output");
+  agk::ConvFp8Args a{};
+  a.variant = variant;
+  a.x = x.data_ptr<uint8_t>(); a.w = w.data_ptr<uint8_t>(); a.bias = bias.data_ptr<float>();
+  a.scales = scales.data_ptr<int>(); a.out_scale = out_scale.data_ptr<float>();
+  const int64_t HPo = S + 2 * Po;
+  if (y_bf16.has_value()) {
+    CHECK_BF16(*y_bf16); CHECK_CONTIG(*y_bf16);
+    TORCH_CHECK(y_bf16->size(0) == B && y_bf16->size(1) == HPo && y_bf16->size(3) == Cout, "y_bf16 shape");
+    a.y_bf16 = bfp_mut(*y_bf16);
+  }
+  if (y_fp8.has_value()) {
+    TORCH_CHECK(y_fp8->scalar_type() == at::kByte && y_fp8->is_contiguous(), "y_fp8 uint8");
+    TORCH_CHECK(y_fp8->size(0) == B && y_fp8->size(1) == HPo && y_fp8->size(3) == Cout, "y_fp8 shape");
+    a.y_fp8 = y_fp8->data_ptr<uint8_t>();
+  }
+  if (amax.has_value()) {
+    TORCH_CHECK(amax->scalar_type() == at::kInt && amax->numel() >= agk::kFp8AmaxSlots,
+                "amax int32[64] (float bits, per-workgroup slots)");
+    a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
+  }
+  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po; a.nch = (int)nch;
+  TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31), "tensor too large for int32 offsets");
+  if (a.M == 0) return;
+  agk::launch_conv_fwd_fp8(a, cur_stream());
+  launch_check("conv_fwd_fp8");
+}
+
+}  // namespace agk_ops

@@ -1,0 +1,61 @@
+// Kernel-lab op library (torch.ops.alphago_amd_lab.*), built separately from
+// the production library (python -m alphago_amd._build lab): the forward-conv
+// tilings of conv_fwd_variants.hip and the other non-default tile codes, the
+// wgrad and fp8 variants, and the segment-cycle stamp buffer of the ping-pong
+// kernels.  Compiled with -DAGK_KERNEL_LAB and the kernel namespaces renamed
+// (agk -> agk_lab) so it loads next to the production library.  Every choice
+// is an explicit argument; nothing here is process-global.
+#include "ops_conv.h"
+
+namespace {
+
+using namespace agk_ops;
+
+void conv_fwd_lab(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
+                  const c10::optional<Tensor>& mask, const Tensor& y, int64_t K, int64_t S, int64_t Pin, int64_t Po,
+                  int64_t mode, const c10::optional<Tensor>& mbits, int64_t tile,
+                  const c10::optional<Tensor>& stamps) {
+  unsigned long long* dbg = nullptr;
+  if (stamps.has_value()) {
+    CHECK_DEV(*stamps);
+    TORCH_CHECK(stamps->scalar_type() == at::kLong && stamps->is_contiguous(), "int64 stamp buffer");
+    dbg = reinterpret_cast<unsigned long long*>(stamps->data_ptr<int64_t>());
+  }
+  conv_fwd_impl(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, (int)tile, dbg);
+}
+
+void conv_wgrad_lab(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
+                    int64_t Pin, int64_t Po, int64_t cin_real, int64_t variant) {
+  conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
+}
+
+void conv_fwd_fp8_lab(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales,
+                      const Tensor& out_scale, const c10::optional<Tensor>& amax,
+                      const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S,
+                      int64_t Pin, int64_t Po, int64_t variant) {
+  conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, (int)variant);
+}
+
+int64_t wgrad_tap_group_lab(int64_t cout, int64_t cin, int64_t K, int64_t variant) {
+  return agk::wgrad_tap_group((int)cout, (int)cin, (int)K, (int)variant);
+}
+
+}  // namespace
+
+TORCH_LIBRARY(alphago_amd_lab, m) {
+  m.def(
+      "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
+      "Tensor(b!)? mbits, int tile, Tensor(c!)? stamps=None) -> ()");
+  m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, "
+        "int cin_real, int variant) -> ()");
+  m.def(
+      "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
+      "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, int variant) -> ()");
+  m.def("wgrad_tap_group(int cout, int cin, int K, int variant) -> int", &wgrad_tap_group_lab);
+}
+
+TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {
+  m.impl("conv_fwd", &conv_fwd_lab);
+  m.impl("conv_wgrad", &conv_wgrad_lab);
+  m.impl("conv_fwd_fp8", &conv_fwd_fp8_lab);
+}

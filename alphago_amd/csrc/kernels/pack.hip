@@ -132,6 +132,16 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, i
     p[i] -= step * g[i];
 }
 
+__global__ void invalid_config_probe_kernel(int* p) {
+  if (p) p[threadIdx.x] = 0;
+}
+
+void launch_invalid_config_probe(hipStream_t st) {
+  // 2048 threads per block exceeds the 1024 limit: the runtime refuses the
+  // launch (hipErrorInvalidConfiguration); nothing executes on the device
+  hipLaunchKernelGGL(invalid_config_probe_kernel, dim3(1), dim3(2048), 0, st, nullptr);
+}
+
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st) {
   int64_t blocks = ((n >> 2) + 255) / 256;
   if (blocks > 2048) blocks = 2048;

@@ -25,8 +25,17 @@ _loaded = False
 MODE_BIAS_RELU, MODE_MASK, MODE_NONE, MODE_MASKBITS = 0, 1, 2, 3
 
 
+def flavor() -> str:
+    """Kernel library flavor: ``prod`` (default) or ``debug`` (device bounds
+    checks, synchronising ops; ``ALPHAGO_AMD_KERNELS=debug``)."""
+    f = os.environ.get("ALPHAGO_AMD_KERNELS", "prod")
+    if f not in ("prod", "debug"):
+        raise ValueError("ALPHAGO_AMD_KERNELS must be prod or debug")
+    return f
+
+
 def library_path() -> str:
-    return _build.hip_path()
+    return _build.hip_path(flavor())
 
 
 def load(build_if_missing: bool = True) -> None:
@@ -41,9 +50,27 @@ def load(build_if_missing: bool = True) -> None:
         if not os.path.exists(path) or os.environ.get("ALPHAGO_AMD_REBUILD"):
             if not build_if_missing:
                 raise RuntimeError("alphago_amd HIP kernels not built: %s" % path)
-            _build.build_hip()
+            _build.build_hip(flavor=flavor())
         torch.ops.load_library(path)
         _loaded = True
+
+
+_lab_loaded = False
+
+
+def lab():
+    """The kernel-lab library (non-production conv tilings and variants) as
+    ``torch.ops.alphago_amd_lab``; loads next to the production library."""
+    global _lab_loaded
+    load()
+    with _lock:
+        if not _lab_loaded:
+            path = _build.hip_path("lab")
+            if not os.path.exists(path):
+                _build.build_hip(flavor="lab")
+            torch.ops.load_library(path)
+            _lab_loaded = True
+    return torch.ops.alphago_amd_lab
 
 
 def is_loaded() -> bool:
@@ -83,10 +110,11 @@ def from_padded(y: torch.Tensor, P: int, C: Optional[int] = None) -> torch.Tenso
 
 # ----------------------------------------------------------------- op wrappers
 def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: int = MODE_BIAS_RELU, mask=None,
-             mbits=None):
+             mbits=None, tile: int = 0):
     """Conv + epilogue.  mode 0: bias + ReLU (mbits: also write the ReLU' bitmask);
-    1: dgrad masked by ``mask`` > 0; 3: dgrad masked by the ``mbits`` bitmask."""
-    _ops().conv_fwd(x, w_packed, bias, mask, y, K, S, Pin, Po, mode, mbits)
+    1: dgrad masked by ``mask`` > 0; 3: dgrad masked by the ``mbits`` bitmask.
+    ``tile``: 0 = automatic, or a production tiling 128 / 256 / 384."""
+    _ops().conv_fwd(x, w_packed, bias, mask, y, K, S, Pin, Po, mode, mbits, tile)
     return y
 
 

@@ -119,8 +119,9 @@ class HipConvTrainer:
 
     def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
                  overlap: bool = True, wgrad_target_wgs: int = 512, iterations: int = 0, precision: str = "bf16",
-                 wgrad_priority: Optional[int] = None):
+                 wgrad_priority: Optional[int] = None, conv_tile: int = 0):
         ops.load()
+        self.conv_tile = conv_tile  # forward/dgrad tiling: 0 = automatic, or 128 / 256 / 384
         if precision not in ("bf16", "fp8"):
             raise ValueError("precision must be bf16 or fp8")
         self.precision = precision
@@ -265,7 +266,7 @@ class HipConvTrainer:
         for l in range(self.L):
             x, pin = self._layer_in(l)
             ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1,
-                         mbits=self.MBITS[l] if l < self.L - 1 else None)
+                         mbits=self.MBITS[l] if l < self.L - 1 else None, tile=self.conv_tile)
 
     def _forward_fp8(self) -> None:
         ops.quantize_fp8(self.X0, self.X08, 0)  # binary planes: exact
@@ -327,7 +328,7 @@ class HipConvTrainer:
                                  mode=ops.MODE_MASK, mask=self.Y[l - 1])
                 else:
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
-                                 mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1])
+                                 mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=self.conv_tile)
         if self.s_w is not None:
             main.wait_stream(self.s_w)
         if red:

@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                     help="conv forward precision (fp8 = e4m3 block-scaled MFMA forward, bf16 backward)")
+    ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 128, 256, 384],
+                    help="forward/dgrad conv tiling (0 = automatic)")
     ap.add_argument("--wgrad-wgs", type=int, default=512,
                     help="target workgroups per wgrad launch (sets the split-K factor)")
     ap.add_argument("--profile", default=None,
@@ -61,18 +63,10 @@ def main():
 
     env = agdist.init_from_env()
     dev = env.device
-    if os.environ.get("ALPHAGO_AMD_CONV_TILE") and dev.type == "cuda":  # kernel A/B experiments
-        from alphago_amd import ops as _ops
-        _ops.load()
-        torch.ops.alphago_amd.set_conv_tile(int(os.environ["ALPHAGO_AMD_CONV_TILE"]))
-    if os.environ.get("ALPHAGO_AMD_WGRAD_VARIANT") and dev.type == "cuda":
-        from alphago_amd import ops as _ops
-        _ops.load()
-        torch.ops.alphago_amd.set_wgrad_variant(int(os.environ["ALPHAGO_AMD_WGRAD_VARIANT"]))
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
     kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap, "precision": args.precision,
-                                             "wgrad_target_wgs": args.wgrad_wgs}
+                                             "wgrad_target_wgs": args.wgrad_wgs, "conv_tile": args.conv_tile}
     trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
 
     # synthetic dataset, resident in HBM (uint8 one-hot planes + move targets)

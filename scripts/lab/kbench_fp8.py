@@ -1,6 +1,9 @@
 """fp8 forward conv: LDS-staged (variant 0) vs pixel operand from L2 (variant 1),
 3x3 192->192 and 5x5 64->192 at batch B (default 1024), random operands."""
 import argparse, json
+import os, sys  # noqa: E401
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from _lab import TILE, STAMPS, WGV, FP8V, FP8_OLD_TO_NEW, lab_conv_fwd, lab_conv_wgrad, lab_conv_fwd_fp8  # noqa: E402,F401
 import torch
 from alphago_amd import ops
 
@@ -40,18 +43,18 @@ fl3, fl5 = 2.0 * M * F * F * 9, 2.0 * M * F * 64 * 25
 ref = None
 out = {}
 for v in [int(t) for t in a.variants.split(",")]:
-    torch.ops.alphago_amd.set_fp8_variant(v)
+    FP8V[0] = FP8_OLD_TO_NEW[v]
     yb.zero_()
-    ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_bf16=yb)
+    lab_conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_bf16=yb)
     torch.cuda.synchronize()
     if ref is None:
         ref = yb.float().clone()
     d = float((yb.float() - ref).abs().max())
-    t3 = timeit(lambda: ops.conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8))
-    t5 = timeit(lambda: ops.conv_fwd_fp8(x08, w18, bias, sc, osc, 5, S, 2, 1, y_fp8=y8))
+    t3 = timeit(lambda: lab_conv_fwd_fp8(x8, w8, bias, sc, osc, 3, S, 1, 1, y_fp8=y8))
+    t5 = timeit(lambda: lab_conv_fwd_fp8(x08, w18, bias, sc, osc, 5, S, 2, 1, y_fp8=y8))
     r = {"fwd3_us": round(t3, 1), "fwd3_pf": round(fl3 / t3 / 1e9, 3), "fwd5_us": round(t5, 1),
          "fwd5_pf": round(fl5 / t5 / 1e9, 3), "maxdiff_vs_first": d}
     print(v, r, flush=True)
     out[str(v)] = r
-torch.ops.alphago_amd.set_fp8_variant(2)
+FP8V[0] = FP8_OLD_TO_NEW[2]
 print(json.dumps(out))

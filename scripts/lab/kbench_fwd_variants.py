@@ -1,5 +1,8 @@
 """Forward-conv tile-variant sweep (3x3 192->192 and 5x5 64->192, B boards)."""
 import argparse, json
+import os, sys  # noqa: E401
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from _lab import TILE, STAMPS, WGV, FP8V, FP8_OLD_TO_NEW, lab_conv_fwd, lab_conv_wgrad, lab_conv_fwd_fp8  # noqa: E402,F401
 import torch
 from alphago_amd import ops
 
@@ -36,16 +39,16 @@ fl5 = 2.0 * M * F * 64 * 25
 ref = None
 res = {}
 for t in [int(s) for s in a.tiles.split(",")]:
-    torch.ops.alphago_amd.set_conv_tile(t)
+    TILE[0] = t
     y.zero_()
-    ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1)
+    lab_conv_fwd(x, wf, bias, y, 3, S, 1, 1)
     torch.cuda.synchronize()
     if ref is None: ref = y.clone()
     err = (y.float() - ref.float()).abs().max().item()
-    t3 = timeit(lambda: ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1))
-    t5 = timeit(lambda: ops.conv_fwd(x0, wf1, bias, y, 5, S, 2, 1))
+    t3 = timeit(lambda: lab_conv_fwd(x, wf, bias, y, 3, S, 1, 1))
+    t5 = timeit(lambda: lab_conv_fwd(x0, wf1, bias, y, 5, S, 2, 1))
     res[t] = dict(fwd3_us=round(t3, 1), fwd3_pf=round(fl3 / t3 / 1e9, 3), fwd5_us=round(t5, 1),
                   fwd5_pf=round(fl5 / t5 / 1e9, 3), maxdiff_vs_first=err)
     print(t, res[t], flush=True)
-torch.ops.alphago_amd.set_conv_tile(0)
+TILE[0] = 0
 print(json.dumps(res))

@@ -1,4 +1,7 @@
 """Segment-cycle stamps of the ping-pong forward conv (diagnostic build path)."""
+import os, sys  # noqa: E401
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from _lab import TILE, STAMPS, WGV, FP8V, FP8_OLD_TO_NEW, lab_conv_fwd, lab_conv_wgrad, lab_conv_fwd_fp8  # noqa: E402,F401
 import torch
 from alphago_amd import ops
 ops.load()
@@ -13,14 +16,14 @@ bias = torch.zeros(F, device=dev)
 M = B * S * S
 nwg = (M + 255) // 256
 dbg = torch.zeros(nwg * 8 * 8, dtype=torch.int64, device=dev)
-torch.ops.alphago_amd.set_conv_tile(4)
+TILE[0] = 4
 for _ in range(3):
-    ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1)
-torch.ops.alphago_amd.set_conv_debug(dbg)
+    lab_conv_fwd(x, wf, bias, y, 3, S, 1, 1)
+STAMPS[0] = dbg
 for _ in range(3):
-    ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1)
+    lab_conv_fwd(x, wf, bias, y, 3, S, 1, 1)
 torch.cuda.synchronize()
-torch.ops.alphago_amd.set_conv_debug(None)
+STAMPS[0] = None
 d = dbg.view(nwg, 8, 8).double().cpu()
 raw = dbg.view(nwg, 8, 8)[..., 7].cpu()
 nk = float(raw[0, 0] & 0xFFFF)

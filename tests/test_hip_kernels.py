@@ -19,6 +19,18 @@ def _bf(x):
     return x.to(torch.bfloat16).float()
 
 
+PROD_TILES = (0, 128, 256, 384)
+
+
+def _conv_fwd(ops, tile, x, w, bias, y, K, S, Pin, Po=1, mode=0, mask=None, mbits=None):
+    """Production tilings through torch.ops.alphago_amd, the kernel-lab ones
+    through the separately built lab library (torch.ops.alphago_amd_lab)."""
+    if tile in PROD_TILES:
+        return ops.conv_fwd(x, w, bias, y, K, S, Pin, Po, mode=mode, mask=mask, mbits=mbits, tile=tile)
+    ops.lab().conv_fwd(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, tile)
+    return y
+
+
 def _rel_err(a, b):
     return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-6)
 
@@ -97,11 +109,10 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     ns = nsplit or ops.wgrad_splits(M, K * K)
     slab = torch.empty(ns, K * K, Cout, Cin, device=cuda_device)
     dbs = torch.zeros(ns, Cout, device=cuda_device)
-    try:
-        torch.ops.alphago_amd.set_wgrad_variant(variant)
+    if variant == 0:
         ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1)
-    finally:
-        torch.ops.alphago_amd.set_wgrad_variant(0)
+    else:  # kernel-lab variants
+        ops.lab().conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, 0, variant)
     gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
     gb = torch.zeros(Cout, device=cuda_device)
     ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
@@ -222,12 +233,8 @@ def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     wp = ops.packed_weight_like(w, C, C)
     ops.pack_weights([w.contiguous()], [wp])
     y = ops.padded_empty(B, S, 1, C, cuda_device)
-    try:
-        torch.ops.alphago_amd.set_conv_tile(tile)
-        ops.conv_fwd(xp, wp, b, y, 3, S, 1, 1)
-        torch.cuda.synchronize()
-    finally:
-        torch.ops.alphago_amd.set_conv_tile(0)
+    _conv_fwd(ops, tile, xp, wp, b, y, 3, S, 1, 1)
+    torch.cuda.synchronize()
     assert _rel_err(ops.from_padded(y, 1), ref) < 1e-2
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
@@ -252,31 +259,24 @@ def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
     wf = ops.packed_weight_like(w3, 192, 192)
     ops.pack_weights([w3.contiguous()], [wf], [wd])
     dx = ops.padded_empty(B, S, 1, 192, cuda_device)
-    try:
-        torch.ops.alphago_amd.set_conv_tile(tile)
-        ops.conv_fwd(xp, wp, b, y, 5, S, 2, 1)
-        ops.conv_fwd(ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASK, mask=ops.to_padded(mask, 1))
-        torch.cuda.synchronize()
-    finally:
-        torch.ops.alphago_amd.set_conv_tile(0)
+    _conv_fwd(ops, tile, xp, wp, b, y, 5, S, 2, 1)
+    _conv_fwd(ops, tile, ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASK, mask=ops.to_padded(mask, 1))
+    torch.cuda.synchronize()
     assert _rel_err(ops.from_padded(y, 1), ref) < 1e-2
     ref_dx = torch.nn.grad.conv2d_input(x.shape[:1] + (192, S, S), w3, g, padding=1) * (mask > 0)
     assert _rel_err(ops.from_padded(dx, 1), ref_dx) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5])
 @pytest.mark.parametrize("K,Cin,Cout,B", [(3, 192, 192, 5), (5, 64, 192, 3), (3, 128, 128, 4), (3, 192, 64, 2)])
 def test_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B, variant):
     """e4m3 conv on the block-scaled MFMA vs fp32 conv of the dequantised operands
-    (variant 0: LDS-staged operands, 1-4: pixel operand loaded from L2 into registers)."""
-    torch.ops.alphago_amd.set_fp8_variant(variant)
-    try:
-        _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B)
-    finally:
-        torch.ops.alphago_amd.set_fp8_variant(2)
+    (variant 0: production, pixel operand loaded from L2 into registers; lab:
+    1/3/4 other tilings of it, 5 LDS-staged operands)."""
+    _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B, variant)
 
 
-def _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B):
+def _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B, variant=0):
     torch.manual_seed(3)
     S, P = 19, K // 2
     x = F.relu(torch.randn(B, Cin, S, S, device=cuda_device)) * 3.0
@@ -298,7 +298,10 @@ def _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B):
     amax = ops.fp8_amax_buffer(1, cuda_device)[0]
     yb = ops.padded_empty(B, S, 1, Cout, cuda_device)
     y8 = torch.zeros((B, S + 2, S + 2, Cout), dtype=torch.uint8, device=cuda_device)
-    ops.conv_fwd_fp8(x8, w8, b, scales, osc, K, S, P, 1, y_bf16=yb, y_fp8=y8, amax=amax)
+    if variant == 0:
+        ops.conv_fwd_fp8(x8, w8, b, scales, osc, K, S, P, 1, y_bf16=yb, y_fp8=y8, amax=amax)
+    else:
+        ops.lab().conv_fwd_fp8(x8, w8, b, scales, osc, amax, yb, y8, K, S, P, 1, variant)
     torch.cuda.synchronize()
     assert _rel_err(ops.from_padded(yb, 1), ref) < 1e-2
     assert _rel_err(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1].permute(0, 3, 1, 2), ref) < 0.07
@@ -324,14 +327,10 @@ def test_relu_bitmask_dgrad_matches_mask(ops, cuda_device, tile, C):
     g = ops.to_padded(_bf(torch.randn(B, C, S, S, device=cuda_device)), 1)
     d1 = ops.padded_empty(B, S, 1, C, cuda_device)
     d3 = ops.padded_empty(B, S, 1, C, cuda_device)
-    try:
-        torch.ops.alphago_amd.set_conv_tile(tile)
-        ops.conv_fwd(xp, wf, b, y, 3, S, 1, 1, mbits=mb)
-        ops.conv_fwd(g, wd, None, d1, 3, S, 1, 1, mode=ops.MODE_MASK, mask=y)
-        ops.conv_fwd(g, wd, None, d3, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb)
-        torch.cuda.synchronize()
-    finally:
-        torch.ops.alphago_amd.set_conv_tile(0)
+    _conv_fwd(ops, tile, xp, wf, b, y, 3, S, 1, 1, mbits=mb)
+    _conv_fwd(ops, tile, g, wd, None, d1, 3, S, 1, 1, mode=ops.MODE_MASK, mask=y)
+    _conv_fwd(ops, tile, g, wd, None, d3, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb)
+    torch.cuda.synchronize()
     assert _rel_err(ops.from_padded(y, 1), F.relu(F.conv2d(x, w, b, padding=1))) < 1e-2
     assert torch.equal(d1, d3)
     assert (ops.from_padded(d3, 1) != 0).any()
@@ -370,3 +369,77 @@ def test_conv_wgrad_reduce_vs_fp32(ops, cuda_device, ns, T, Cout, Cin, Cin_real,
     torch.cuda.synchronize()
     assert torch.isfinite(gw).all()
     assert (gw.double() - ref_w).abs().max().item() < 1e-4 * max(1.0, ns ** 0.5)
+
+
+def test_bad_launch_raises(ops, cuda_device):
+    """A launch the runtime rejects surfaces as a Python RuntimeError (every op
+    runs launch_check after its kernels), not as silently unwritten output."""
+    with pytest.raises(RuntimeError, match="launch failed"):
+        torch.ops.alphago_amd.selftest_bad_launch()
+    # the error is consumed: the next op runs normally
+    p, g = torch.ones(8, device=cuda_device), torch.ones(8, device=cuda_device)
+    ops.sgd_update(p, g, 0.5, 1.0)
+    assert torch.allclose(p, torch.full_like(p, 0.5))
+
+
+def test_production_library_has_no_lab_variants(ops, cuda_device):
+    """Kernel-lab tilings/variants are not compiled into the production library:
+    asking for one raises instead of switching kernels."""
+    assert not torch.ops.alphago_amd.is_debug_build()
+    x = ops.padded_empty(1, 19, 1, 64, cuda_device)
+    w = torch.zeros(9, 64, 64, dtype=torch.bfloat16, device=cuda_device)
+    y = ops.padded_empty(1, 19, 1, 64, cuda_device)
+    with pytest.raises(RuntimeError, match="not a production tiling"):
+        ops.conv_fwd(x, w, torch.zeros(64, device=cuda_device), y, 3, 19, 1, 1, tile=11)
+    assert not hasattr(torch.ops.alphago_amd, "set_conv_tile")
+
+
+_DEBUG_CHILD = r"""
+import torch, torch.nn.functional as F
+from alphago_amd import ops
+ops.load(build_if_missing=False)
+assert torch.ops.alphago_amd.is_debug_build()
+dev = torch.device("cuda:0")
+torch.manual_seed(0)
+B, C, S = 5, 192, 19
+x = torch.randn(B, C, S, S, device=dev).bfloat16().float()
+w = (torch.randn(C, C, 3, 3, device=dev) * 0.05).bfloat16().float()
+b = torch.randn(C, device=dev) * 0.1
+xp = ops.to_padded(x, 1)
+wf = ops.packed_weight_like(w, C, C); wd = ops.packed_weight_like(w, C, C, True)
+ops.pack_weights([w.contiguous()], [wf], [wd])
+y = ops.padded_empty(B, S, 1, C, dev)
+mb = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(C), dtype=torch.int32, device=dev)
+ops.conv_fwd(xp, wf, b, y, 3, S, 1, 1, mbits=mb)          # bounds-checked forward
+ref = F.relu(F.conv2d(x, w, b, padding=1))
+err = (ops.from_padded(y, 1) - ref).abs().max().item() / ref.abs().max().item()
+assert err < 1e-2, err
+d = ops.padded_empty(B, S, 1, C, dev)
+ops.conv_fwd(y, wd, None, d, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb)  # bounds-checked dgrad
+ns = ops.wgrad_splits(B * S * S, 9)
+slab = torch.empty(ns, 9, C, C, device=dev); dbs = torch.zeros(ns, C, device=dev)
+ops.conv_wgrad(xp, y, slab, dbs, 3, S, 1, 1)               # bounds-checked wgrad
+try:
+    torch.ops.alphago_amd.debug_conv_fwd_understated(xp, wf, b, y, 3, S, 1, 1)
+except RuntimeError as e:
+    assert "bounds check failed" in str(e), e
+    print("DEBUG-OK")
+else:
+    raise SystemExit("device bounds check did not fire")
+"""
+
+
+def test_debug_build_bounds_checks(cuda_device, tmp_path):
+    """The AGK_DEBUG library (device bounds checks in the conv kernels) runs the
+    forward, bitmask dgrad and wgrad of a real layer clean, and an understated
+    tensor extent makes the next op raise a RuntimeError naming the check."""
+    import os
+    import subprocess
+    import sys
+    from alphago_amd import _build
+    if not os.path.exists(_build.hip_path("debug")):
+        pytest.skip("debug library not built")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, ALPHAGO_AMD_KERNELS="debug", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", _DEBUG_CHILD], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "DEBUG-OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
