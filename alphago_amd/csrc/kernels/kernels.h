@@ -175,5 +175,7 @@ void launch_fp8_weight_scales(const Fp8WeightScalesArgs& a, int L, hipStream_t s
 void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st);
 void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st);
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
+// device-side schedule (graph-capturable): sched = {lr0, decay, iterations, lr_current} f64
+void launch_sgd_sched(float* p, const float* g, int64_t n, double* sched, float gscale, hipStream_t st);
 
 }  // namespace agk

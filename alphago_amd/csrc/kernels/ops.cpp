@@ -334,6 +334,16 @@ void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
   launch_check("sgd_update");
 }
 
+void sgd_update_sched(const Tensor& p, const Tensor& g, const Tensor& sched, double gscale) {
+  CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g); CHECK_DEV(sched);
+  TORCH_CHECK(p.numel() == g.numel(), "size mismatch");
+  TORCH_CHECK(sched.scalar_type() == at::kDouble && sched.numel() == 4 && sched.is_contiguous(),
+              "sched must be float64[4] {lr0, decay, iterations, lr}");
+  agk::launch_sgd_sched(p.data_ptr<float>(), g.data_ptr<float>(), p.numel(), sched.data_ptr<double>(), (float)gscale,
+                        cur_stream());
+  launch_check("sgd_update_sched");
+}
+
 // A deliberately invalid launch (2048 threads per block, above the 1024
 // limit): the runtime rejects it, launch_check turns that into a Python
 // RuntimeError -- the test of the error path every op shares.
@@ -374,6 +384,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P) -> ()");
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
+  m.def("sgd_update_sched(Tensor(a!) p, Tensor g, Tensor(b!) sched, float gscale) -> ()");
   m.def(
       "featurize(Tensor board, Tensor ages, Tensor meta, Tensor? ladder, int[] fids, int[] fplanes, Tensor(a!)? planes, "
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
@@ -409,6 +420,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("value_out", &value_out);
   m.impl("pack_weights", &pack_weights);
   m.impl("sgd_update", &sgd_update);
+  m.impl("sgd_update_sched", &sgd_update_sched);
 #ifdef AGK_DEBUG
   m.impl("debug_conv_fwd_understated", &debug_conv_fwd_understated);
 #endif

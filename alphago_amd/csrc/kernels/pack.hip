@@ -132,6 +132,46 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, i
     p[i] -= step * g[i];
 }
 
+// Keras-SGD schedule kept on the device so a whole training step can be
+// captured in a HIP graph: sched = {lr0, decay, iterations, lr_current} (f64).
+// One thread computes lr = lr0 / (1 + decay * iterations) -- the same double
+// expression as KerasSGDSchedule.current() -- and advances the counter.
+__global__ void sgd_sched_kernel(double* sched) {
+  if (threadIdx.x == 0) {
+    const double lr = sched[0] / (1.0 + sched[1] * sched[2]);
+    sched[3] = lr;
+    sched[2] = sched[2] + 1.0;
+  }
+}
+
+__global__ void sgd_dev_kernel(float* __restrict__ p, const float* __restrict__ g, int64_t n,
+                               const double* __restrict__ sched, float gscale) {
+  const float step = (float)sched[3] * gscale;  // == launch_sgd's (float)lr * gscale
+  const int64_t n4 = n >> 2;
+  float4* p4 = (float4*)p;
+  const float4* g4 = (const float4*)g;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 pv = p4[i];
+    const float4 gv = g4[i];
+    pv.x -= step * gv.x;
+    pv.y -= step * gv.y;
+    pv.z -= step * gv.z;
+    pv.w -= step * gv.w;
+    p4[i] = pv;
+  }
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] -= step * g[i];
+}
+
+void launch_sgd_sched(float* p, const float* g, int64_t n, double* sched, float gscale, hipStream_t st) {
+  hipLaunchKernelGGL(sgd_sched_kernel, dim3(1), dim3(64), 0, st, sched);
+  int64_t blocks = ((n >> 2) + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(sgd_dev_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, g, n, (const double*)sched, gscale);
+}
+
 __global__ void invalid_config_probe_kernel(int* p) {
   if (p) p[threadIdx.x] = 0;
 }

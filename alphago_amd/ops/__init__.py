@@ -160,6 +160,12 @@ def sgd_update(p, g, lr: float, gscale: float = 1.0):
     _ops().sgd_update(p, g, lr, gscale)
 
 
+def sgd_update_sched(p, g, sched, gscale: float = 1.0):
+    """SGD with the Keras decay schedule on the device: sched = float64
+    {lr0, decay, iterations, lr}; advances iterations (HIP-graph capturable)."""
+    _ops().sgd_update_sched(p, g, sched, gscale)
+
+
 def packed_weight_like(w_oihw: torch.Tensor, cin_p: int, cout_p: int, transposed: bool = False) -> torch.Tensor:
     K = w_oihw.shape[2]
     shape = (K * K, cin_p, cout_p) if transposed else (K * K, cout_p, cin_p)

@@ -38,6 +38,8 @@ def load_trainer_state(trainer, st: Dict[str, Any]) -> None:
     with torch.no_grad():
         trainer.fp.flat.copy_(flat.to(trainer.fp.flat.device))
     trainer.sched.iterations = int(st["iterations"])
+    if hasattr(trainer, "sync_schedule"):
+        trainer.sync_schedule()  # graph replays read the schedule from the device
     if hasattr(trainer, "repack"):
         trainer.repack()
 

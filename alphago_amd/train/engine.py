@@ -229,8 +229,37 @@ class HipConvTrainer:
             self.X08 = torch.zeros(self.X0.shape, dtype=torch.uint8, device=dev)
             self.Y8 = [torch.zeros(self.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(2)]
             self._fp8_calibrated = False
+        # Keras-SGD schedule mirrored on the device (float64 {lr0, decay, iterations, lr}) so that
+        # the SGD step reads its learning rate from memory: the whole step is graph-capturable
+        self._sched_dev = torch.zeros(4, dtype=torch.float64, device=dev)
+        self.use_graph = False
+        self._graphs = None
+        self._g_in = None
         self._init_head()
         self.repack()
+
+    # ------------------------------------------------------------------ schedule / graphs
+    def sync_schedule(self) -> None:
+        """Copy the host schedule (lr, decay, iterations) to the device copy used by graph replays."""
+        self._sched_dev.copy_(torch.tensor([self.sched.lr, self.sched.decay, float(self.sched.iterations), 0.0],
+                                           dtype=torch.float64))
+
+    def enable_graphs(self, on: bool = True) -> None:
+        """Run ``step`` as HIP-graph replays (bf16, per-board weights not supported): the first
+        call runs eagerly (loads code objects, sets kernel attributes), the second captures
+        the step -- pack, forward, head, backward (wgrad on its stream), SGD, repack -- and
+        every call replays it.  With world > 1 the gradient all-reduce runs eagerly between a
+        forward/backward graph and an update graph.  Replays are bitwise identical to eager steps.
+        The learning-rate schedule is read from its device copy (synced from ``self.sched`` at
+        capture); changing ``sched.lr`` afterwards needs ``sync_schedule()``."""
+        if on and self.precision != "bf16":
+            raise ValueError("graph-captured steps support the bf16 trainer only")
+        self.use_graph = on
+        self._graphs = None
+        self._g_in = None
+        self._graph_warm = False
+        if on:
+            self.sync_schedule()
 
     # ------------------------------------------------------------------ head API
     def _head_named_params(self):
@@ -348,18 +377,83 @@ class HipConvTrainer:
         with trace_range("backward+allreduce"):
             self.backward_trunk(reduce)
 
-    def apply_update(self) -> None:
+    def apply_update(self, device_schedule: bool = False) -> None:
         with trace_range("sgd+repack"):
-            ops.sgd_update(self.fp.flat, self.fp.grad, self.sched.current(), 1.0)
+            if device_schedule:
+                # graph replays: lr = lr0 / (1 + decay * t) evaluated on the device (the same f64
+                # expression as KerasSGDSchedule.current()) from the copy synced at capture time
+                ops.sgd_update_sched(self.fp.flat, self.fp.grad, self._sched_dev, 1.0)
+            else:
+                ops.sgd_update(self.fp.flat, self.fp.grad, self.sched.current(), 1.0)
             self.sched.advance()
             self.repack()
 
     def step(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None,
              weight: Optional[torch.Tensor] = None):
-        """One SGD step.  Returns (sum of per-board loss, metric sum) as device scalars (local)."""
+        """One SGD step.  Returns (sum of per-board loss, metric sum) as device scalars (local;
+        in graph mode static tensors, valid until the next step)."""
+        if self.use_graph and weight is None:
+            return self._graph_step(planes, targets, sym)
         self.compute_grads(planes, targets, sym, weight)
         self.apply_update()
         return self.loss.sum(), self.correct.sum()
+
+    def _graph_step(self, planes, targets, sym):
+        if self._g_in is None:
+            self._g_in = (torch.empty_like(planes), torch.empty_like(targets),
+                          None if sym is None else torch.empty_like(sym))
+            self._g_out = (torch.zeros((), device=self.device), torch.zeros((), device=self.device))
+        gp, gt, gs = self._g_in
+        if (sym is None) != (gs is None) or planes.shape != gp.shape:
+            raise ValueError("graph mode: inputs must keep their shape and symmetry argument")
+        gp.copy_(planes, non_blocking=True)
+        gt.copy_(targets, non_blocking=True)
+        if gs is not None:
+            gs.copy_(sym, non_blocking=True)
+        dist = self.env.distributed
+
+        def grads():
+            self.compute_grads(gp, gt, gs, None, reduce=not dist)
+
+        def update():
+            self.apply_update(device_schedule=True)
+            torch.sum(self.loss, dim=0, out=self._g_out[0])
+            torch.sum(self.correct, dim=0, out=self._g_out[1])
+
+        if self._graphs is None:
+            if not self._graph_warm:  # eager first step: code objects loaded, LDS attributes set
+                self.sync_schedule()
+                grads()
+                if dist:
+                    agdist.all_reduce_sum_(self.fp.grad)
+                update()
+                self._graph_warm = True
+                return self._g_out
+            torch.cuda.synchronize(self.device)
+            self.sync_schedule()  # the device schedule continues from the host counter
+            parts = [grads, update] if dist else [lambda: (grads(), update())]
+            self._graphs = []
+            # the wgrad side stream is captured as a parallel branch only on request
+            # (ALPHAGO_AMD_GRAPH_OVERLAP=1); by default the graph is one serial chain
+            keep_sw = self.s_w
+            if os.environ.get("ALPHAGO_AMD_GRAPH_OVERLAP", "0") != "1":
+                self.s_w = None
+            try:
+                for fn in parts:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                        fn()
+                    self._graphs.append(g)
+            finally:
+                self.s_w = keep_sw
+            # the capture ran nothing; the iteration counters it advanced on the host are undone
+            self.sched.iterations -= 1
+        self._graphs[0].replay()
+        if dist:
+            agdist.all_reduce_sum_(self.fp.grad)
+            self._graphs[1].replay()
+        self.sched.advance()
+        return self._g_out
 
 
 class HipPolicyTrainer(HipConvTrainer):

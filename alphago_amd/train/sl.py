@@ -103,6 +103,8 @@ def _parser():
     p.add_argument("--watchdog-timeout", type=float, default=0.0,
                    help="exit a rank that makes no progress for this many seconds (0: off)")
     p.add_argument("--profile", default=None, help="write torch.profiler traces + summary to this directory")
+    p.add_argument("--graph", action="store_true",
+                   help="HIP backend: run each step as a HIP-graph replay (launch-bound small minibatches)")
     return p
 
 
@@ -178,6 +180,8 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
     B = args.minibatch
     trainer = make_policy_trainer(net, B, args.learning_rate, args.decay, backend=args.backend, device=dev,
                                   iterations=iterations)
+    if args.graph and hasattr(trainer, "enable_graphs"):
+        trainer.enable_graphs()
     gen = torch.Generator(device=dev)
     gen.manual_seed(args.seed * 1000 + rank)
     global_B = B * world
@@ -223,7 +227,8 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
     total_steps = (end_epoch - start_epoch) * steps_per_epoch - start_step
     stream = None
     if not dataset.resident:
-        stream = dataset.prefetch((local_batch(cursor + k) for k in range(total_steps)), B)
+        c0 = cursor  # bound now: the loop below advances ``cursor`` while the worker thread runs ahead
+        stream = dataset.prefetch((local_batch(c0 + k) for k in range(total_steps)), B)
     with prof:
         for epoch in range(start_epoch, end_epoch):
             t0 = time.perf_counter()

@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                     help="conv forward precision (fp8 = e4m3 block-scaled MFMA forward, bf16 backward)")
+    ap.add_argument("--graph", action="store_true", help="run each training step as a HIP-graph replay")
     ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 128, 256, 384],
                     help="forward/dgrad conv tiling (0 = automatic)")
     ap.add_argument("--wgrad-wgs", type=int, default=512,
@@ -68,6 +69,8 @@ def main():
     kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap, "precision": args.precision,
                                              "wgrad_target_wgs": args.wgrad_wgs, "conv_tile": args.conv_tile}
     trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
+    if args.graph:
+        trainer.enable_graphs()
 
     # synthetic dataset, resident in HBM (uint8 one-hot planes + move targets)
     g = torch.Generator(device=dev)
@@ -156,6 +159,7 @@ def main():
                 "seq_len": 361,
                 "parallelism": "dp%d" % n,
                 "backend": args.backend,
+                "graph": bool(args.graph),
                 "baseline": "paper SL throughput ~3.0k pos/s (50 GPUs), BASELINE.md (A)",
             },
         }

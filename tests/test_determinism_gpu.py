@@ -47,3 +47,38 @@ def test_hip_training_same_with_and_without_wgrad_stream(cuda_device):
     p2, g2, _ = _train(cuda_device, overlap=False)
     assert torch.equal(g1, g2)
     assert torch.equal(p1, p2)
+
+
+@pytest.mark.parametrize("B", [16, 64])
+def test_graph_step_bitwise_equals_eager(cuda_device, B):
+    """HIP-graph-captured training steps (pack, 12 convs, head, wgrad stream,
+    SGD with the device-side Keras decay schedule, repack) produce exactly the
+    weights and losses of the eager steps, step by step."""
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.train.engine import HipPolicyTrainer
+
+    def run(graph):
+        torch.manual_seed(0)
+        net = PolicyNet(48, filters_per_layer=192, layers=12)
+        tr = HipPolicyTrainer(net, B, lr=0.003, decay=1e-3, device=cuda_device)
+        if graph:
+            tr.enable_graphs()
+        g = torch.Generator(device=cuda_device)
+        g.manual_seed(7)
+        losses = []
+        for _ in range(5):
+            planes = torch.randint(0, 2, (B, 48, 19, 19), dtype=torch.uint8, device=cuda_device, generator=g)
+            tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device, generator=g)
+            sym = torch.randint(0, 8, (B,), dtype=torch.int32, device=cuda_device, generator=g)
+            l, c = tr.step(planes, tgt, sym)
+            losses.append((l.clone(), c.clone()))
+        torch.cuda.synchronize()
+        return tr.fp.flat.clone(), losses, tr.sched.iterations, tr
+
+    fe, le, ie, _ = run(False)
+    fg, lg, ig, tr = run(True)
+    assert tr._graphs is not None and len(tr._graphs) == 1
+    assert ie == ig == 5
+    assert torch.equal(fe, fg)
+    for (a, b), (c, d) in zip(le, lg):
+        assert torch.equal(a, c) and torch.equal(b, d)
