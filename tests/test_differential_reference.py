@@ -64,3 +64,75 @@ def test_features_match_reference(size, seed):
         assert a.shape == b.shape
         bad = np.argwhere(a != b)
         assert bad.size == 0, "plane mismatch at %s (move %d)" % (bad[:5], i)
+
+
+def _sweep_positions(size, n_positions, seed):
+    """Random games (restarted at game end) yielding (ours, ref) after every move."""
+    rg = refshim.ref_go()
+    rnd = random.Random(seed)
+    ours, ref = go.GameState(size), rg.GameState(size)
+    done = 0
+    while done < n_positions:
+        legal = ref.get_legal_moves()
+        mv = None if (not legal or rnd.random() < 0.03) else rnd.choice(legal)
+        ref.do_move(mv)
+        ours.do_move(mv)
+        done += 1
+        yield ours, ref
+        if ref.is_end_of_game or len(ref.history) > 3 * size * size:
+            ours, ref = go.GameState(size), rg.GameState(size)
+
+
+def test_rules_and_features_10k_positions():
+    """>= 10^4 positions (random games on 9x9, 13x13 and
+    19x19) -- rules state (board, liberties, ko, side to move, prisoners, legal
+    moves, winner) after every move and all 46 reference feature planes of every
+    position equal the reference implementation's."""
+    rpp = refshim.ref_preprocessing().Preprocess(ALL_NO_LADDER_FEATURES)
+    pp = Preprocess(ALL_NO_LADDER_FEATURES)
+    total = 0
+    for size, n, seed in ((9, 6000, 101), (13, 2500, 102), (19, 1500, 103)):
+        for ours, ref in _sweep_positions(size, n, seed):
+            assert np.array_equal(ours.board, ref.board)
+            assert np.array_equal(ours.liberty_counts, ref.liberty_counts)
+            assert ours.ko == ref.ko and ours.current_player == ref.current_player
+            assert (ours.num_black_prisoners, ours.num_white_prisoners) == \
+                (ref.num_black_prisoners, ref.num_white_prisoners)
+            assert ours.get_legal_moves() == ref.get_legal_moves()
+            assert ours.get_winner() == ref.get_winner()
+            a = pp.state_to_uint8(ours)
+            b = rpp.state_to_tensor(ref)[0]
+            if not np.array_equal(a, b):
+                bad = np.argwhere(a != b)
+                raise AssertionError("size %d position %d: plane mismatch at %s" % (size, total, bad[:5].tolist()))
+            total += 1
+    assert total >= 10000
+
+
+try:
+    from hypothesis import given, settings, strategies as st
+
+    @settings(max_examples=60, deadline=None, derandomize=True)
+    @given(size=st.sampled_from([5, 7, 9]), picks=st.lists(st.integers(0, 1 << 20), min_size=1, max_size=150))
+    def test_rules_property_random_move_sequences(size, picks):
+        """Property test (hypothesis): any sequence of choices among the legal
+        moves (pick % (n_legal + 1) == n_legal means pass) keeps the native
+        engine and the reference in the same state, including captures, ko and
+        the reference's end-of-game rule (Q9)."""
+        rg = refshim.ref_go()
+        ours, ref = go.GameState(size), rg.GameState(size)
+        for p in picks:
+            legal = ref.get_legal_moves()
+            k = p % (len(legal) + 1)
+            mv = None if k == len(legal) else legal[k]
+            ref.do_move(mv)
+            ours.do_move(mv)
+            assert np.array_equal(ours.board, ref.board)
+            assert np.array_equal(ours.liberty_counts, ref.liberty_counts)
+            assert ours.ko == ref.ko and ours.is_end_of_game == ref.is_end_of_game
+            assert ours.get_legal_moves() == ref.get_legal_moves()
+            if ref.is_end_of_game:
+                break
+        assert ours.get_winner() == ref.get_winner()
+except ImportError:  # pragma: no cover
+    pass

@@ -19,7 +19,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, F=64, L=3, NB=16):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0", ALPHAGO_AMD_DIST_BACKEND="gloo")
     from alphago_amd.models.nets import PolicyNet
@@ -29,28 +29,35 @@ def _worker(rank, world, port, q):
     env = agdist.init_from_env()
     dev = env.device
     torch.manual_seed(0)
-    net = PolicyNet(48, filters_per_layer=64, layers=3)
+    net = PolicyNet(48, filters_per_layer=F, layers=L)
     g = torch.Generator().manual_seed(5)
-    planes = torch.randint(0, 2, (16, 48, 19, 19), dtype=torch.uint8, generator=g)
-    tgt = torch.randint(0, 361, (16,), dtype=torch.int32, generator=g)
-    B = 16 // world
-    tr = HipPolicyTrainer(net, B, lr=0.1, device=dev, bucket_mb=0.05)
+    planes = torch.randint(0, 2, (NB, 48, 19, 19), dtype=torch.uint8, generator=g)
+    tgt = torch.randint(0, 361, (NB,), dtype=torch.int32, generator=g)
+    B = NB // world
+    tr = HipPolicyTrainer(net, B, lr=0.1, device=dev, bucket_mb=0.05 if F == 64 else 2.0)
     sl = slice(rank * B, (rank + 1) * B)
     tr.compute_grads(planes[sl].to(dev), tgt[sl].to(dev))
     torch.cuda.synchronize()
-    q.put((rank, tr.fp.grad.cpu().clone(), len(tr.buckets)))
+    grad = tr.fp.grad.cpu().clone()
+    tr.apply_update()
+    torch.cuda.synchronize()
+    q.put((rank, grad, len(tr.buckets), tr.fp.flat.cpu().clone()))
     agdist.barrier()
     agdist.shutdown()
 
 
-def test_hip_dp_matches_single(cuda_device):
+@pytest.mark.parametrize("F,L,NB", [(64, 3, 16), (192, 12, 32)])
+def test_hip_dp_matches_single(cuda_device, F, L, NB):
+    """2-rank DP (bucketed async all-reduce launched from the wgrad stream) ==
+    one process on the union batch: gradients and the weights after the SGD
+    step, on a small net and on the full 12-layer 192-filter benchmark net."""
     from alphago_amd.models.nets import PolicyNet
     from alphago_amd.train.engine import HipPolicyTrainer
 
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, F, L, NB)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
@@ -59,15 +66,18 @@ def test_hip_dp_matches_single(cuda_device):
         assert p.exitcode == 0
     assert res[0][2] > 1  # several buckets exercised
     torch.manual_seed(0)
-    net = PolicyNet(48, filters_per_layer=64, layers=3)
+    net = PolicyNet(48, filters_per_layer=F, layers=L)
     g = torch.Generator().manual_seed(5)
-    planes = torch.randint(0, 2, (16, 48, 19, 19), dtype=torch.uint8, generator=g)
-    tgt = torch.randint(0, 361, (16,), dtype=torch.int32, generator=g)
-    tr = HipPolicyTrainer(net, 16, lr=0.1, device=cuda_device)
+    planes = torch.randint(0, 2, (NB, 48, 19, 19), dtype=torch.uint8, generator=g)
+    tgt = torch.randint(0, 361, (NB,), dtype=torch.int32, generator=g)
+    tr = HipPolicyTrainer(net, NB, lr=0.1, device=cuda_device)
     tr.compute_grads(planes.to(cuda_device), tgt.to(cuda_device))
-    ref = tr.fp.grad.cpu()
-    for _, grad, _ in res:
+    ref = tr.fp.grad.cpu().clone()
+    tr.apply_update()
+    ref_w = tr.fp.flat.cpu()
+    for _, grad, _, w in res:
         cos = torch.nn.functional.cosine_similarity(grad.double(), ref.double(), dim=0).item()
         assert cos > 0.9999
         assert torch.allclose(grad, ref, rtol=5e-3, atol=1e-5)
-    assert torch.equal(res[0][1], res[1][1])
+        assert torch.allclose(w, ref_w, rtol=1e-4, atol=1e-6)
+    assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][3], res[1][3])  # replicas identical

@@ -218,3 +218,29 @@ def test_batched_mcts_encoded_path(cuda_device):
         assert sum(mp.forest.root_stats(i)[1]) >= 48
     mp.update_with_move(3, moves[3])
     assert np.isclose(mp.visit_distribution(0, 19).sum(), 1.0)
+
+
+@pytest.mark.gpu
+def test_gpu_planes_match_cpu_1000_positions(cuda_device):
+    """>= 1,000 random 19x19 positions (every game length 0..330): every plane of
+    the GPU featurizer (46 reference planes + ladders from the encoder + colour
+    + legal) equals the CPU featurizer's, plus the sensible-move masks."""
+    from alphago_amd.ops.gpu_features import GpuFeaturizer
+
+    feats = DEFAULT_FEATURES + ["color", "legal"]
+    states = random_positions(1000, seed=21, max_len=330) + eye_chain_positions()
+    states = [s for s in states if s.size == 19]
+    assert len(states) >= 1000
+    fz = GpuFeaturizer(feats, board=19, device=cuda_device)
+    pre = Preprocess(feats)
+    exp_all = pre.states_to_uint8(states)
+    sens_all = Preprocess(["sensibleness"]).states_to_uint8(states).reshape(len(states), -1)
+    for k in range(0, len(states), 256):
+        got, sens = fz.planes(states[k:k + 256], with_sensible=True)
+        got, sens = got.cpu().numpy(), sens.cpu().numpy()
+        exp = exp_all[k:k + 256]
+        if not np.array_equal(got, exp):
+            i = int(np.argwhere((got != exp).reshape(len(got), -1).any(1))[0][0])
+            bad = np.argwhere(got[i] != exp[i])
+            raise AssertionError("state %d: %d mismatches, first %s" % (k + i, len(bad), bad[:5].tolist()))
+        assert np.array_equal(sens, sens_all[k:k + 256])
