@@ -175,6 +175,22 @@ void launch_fp8_weight_scales(const Fp8WeightScalesArgs& a, int L, hipStream_t s
 void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st);
 void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st);
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
+
+// fp32 dense layer GEMM (value head): C[M][N] = beta*C + A.B (+ bias[n]);
+// A is [M][K] (lda) or, transposed, [K][M]; B is [K][N] (ldb) or [N][K]
+struct DenseArgs {
+  const float* A;
+  const float* B;
+  const float* bias;  // [N] or null
+  float* C;
+  int M, N, K, lda, ldb, ldc;
+  float beta;
+  int splits;  // split-K factor (dense_splits); > 1 needs ws of splits*M*N floats
+  int kchunk;  // set by the launcher
+  float* ws;
+};
+int dense_splits(int M, int N, int K);
+void launch_dense_f32(const DenseArgs& a, bool transA, bool transB, hipStream_t st);
 // device-side schedule (graph-capturable): sched = {lr0, decay, iterations, lr_current} f64
 void launch_sgd_sched(float* p, const float* g, int64_t n, double* sched, float gscale, hipStream_t st);
 

@@ -344,6 +344,37 @@ void sgd_update_sched(const Tensor& p, const Tensor& g, const Tensor& sched, dou
   launch_check("sgd_update_sched");
 }
 
+// C = beta*C + op(A) op(B) (+ bias); op(X) = X or X^T (no copies of transposed operands)
+void dense_f32(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bias, const Tensor& C, bool transA,
+               bool transB, double beta) {
+  CHECK_F32(A); CHECK_F32(B); CHECK_F32(C); CHECK_DEV(A); CHECK_DEV(B); CHECK_DEV(C);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "2-D operands");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "row-major operands (unit column stride)");
+  const int64_t M = transA ? A.size(1) : A.size(0), K = transA ? A.size(0) : A.size(1);
+  const int64_t KB = transB ? B.size(1) : B.size(0), N = transB ? B.size(0) : B.size(1);
+  TORCH_CHECK(K == KB, "inner dimensions differ: ", K, " vs ", KB);
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N, "C must be (", M, ", ", N, ")");
+  agk::DenseArgs a{};
+  a.A = A.data_ptr<float>(); a.B = B.data_ptr<float>(); a.C = C.data_ptr<float>();
+  if (bias.has_value()) {
+    CHECK_F32(*bias);
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "bias must be (N,)");
+    a.bias = bias->data_ptr<float>();
+  }
+  a.M = (int)M; a.N = (int)N; a.K = (int)K;
+  a.lda = (int)A.stride(0); a.ldb = (int)B.stride(0); a.ldc = (int)C.stride(0);
+  a.beta = (float)beta;
+  if (M == 0 || N == 0) return;
+  a.splits = agk::dense_splits((int)M, (int)N, (int)K);
+  Tensor ws;
+  if (a.splits > 1) {
+    ws = at::empty({(int64_t)a.splits * M * N}, C.options());
+    a.ws = ws.data_ptr<float>();
+  }
+  agk::launch_dense_f32(a, transA, transB, cur_stream());
+  launch_check("dense_f32");
+}
+
 // A deliberately invalid launch (2048 threads per block, above the 1024
 // limit): the runtime rejects it, launch_check turns that into a Python
 // RuntimeError -- the test of the error path every op shares.
@@ -385,6 +416,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
   m.def("sgd_update_sched(Tensor(a!) p, Tensor g, Tensor(b!) sched, float gscale) -> ()");
+  m.def("dense_f32(Tensor A, Tensor B, Tensor? bias, Tensor(a!) C, bool transA, bool transB, float beta) -> ()");
   m.def(
       "featurize(Tensor board, Tensor ages, Tensor meta, Tensor? ladder, int[] fids, int[] fplanes, Tensor(a!)? planes, "
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
@@ -421,6 +453,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("pack_weights", &pack_weights);
   m.impl("sgd_update", &sgd_update);
   m.impl("sgd_update_sched", &sgd_update_sched);
+  m.impl("dense_f32", &dense_f32);
 #ifdef AGK_DEBUG
   m.impl("debug_conv_fwd_understated", &debug_conv_fwd_understated);
 #endif

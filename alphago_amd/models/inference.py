@@ -315,8 +315,9 @@ class HipTrunkInference:
 
 
 class HipValueInference(HipTrunkInference):
-    """Value net: HIP trunk, then the head as head_logits (1x1 conv) -> addmm
-    (Dense 256) -> value_out (Dense 1 + tanh), all inside the captured graph."""
+    """Value net: HIP trunk, then the head as head_logits (1x1 conv) -> dense_f32
+    (Dense 256, fp32 MFMA GEMM) -> value_out (Dense 1 + tanh), all inside the
+    captured graph."""
 
     def __init__(self, net: ValueNet, device, **kw):
         self.fc = None
@@ -334,7 +335,7 @@ class HipValueInference(HipTrunkInference):
     def _head(self, bk, y):
         w1, b1, w2, b2 = self.fc
         ops.head_logits(y, self.head_w, self.head_b, bk.z, self.S)
-        torch.addmm(b1, bk.z, w1, out=bk.h)
+        ops.dense_f32(bk.z, w1, bk.h, bias=b1)
         ops.value_out(bk.h, w2.view(-1), b2, bk.values)
 
     def _outputs(self, bk, n):

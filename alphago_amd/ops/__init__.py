@@ -160,6 +160,13 @@ def sgd_update(p, g, lr: float, gscale: float = 1.0):
     _ops().sgd_update(p, g, lr, gscale)
 
 
+def dense_f32(A, B, C, bias=None, trans_a: bool = False, trans_b: bool = False, beta: float = 0.0):
+    """C = beta*C + op(A) @ op(B) (+ bias) in exact fp32 on the f32 MFMA (value-head dense layers);
+    op(X) = X.T when trans_* (read in place, no copies)."""
+    _ops().dense_f32(A, B, bias, C, trans_a, trans_b, beta)
+    return C
+
+
 def sgd_update_sched(p, g, sched, gscale: float = 1.0):
     """SGD with the Keras decay schedule on the device: sched = float64
     {lr0, decay, iterations, lr}; advances iterations (HIP-graph capturable)."""

@@ -495,10 +495,11 @@ class HipValueTrainer(HipConvTrainer):
     -> Dense(1) -> tanh head; MSE against game outcomes in [-1, 1].
 
     Head forward: ``head_logits`` (one pass over the last activation) -> z
-    (B, 361) fp32; hipBLASLt ``addmm`` for the 361x256 dense layer (a plain
-    library GEMM); ``value_out`` fuses the 256->1 layer, tanh, MSE, sign
-    accuracy and its backward.  Head backward: dz = dh W1^T and dW1 = z^T dh
-    (library GEMMs written straight into the flat gradient buffer), then
+    (B, 361) fp32; the 361x256 dense layer on the hand-written fp32 MFMA GEMM
+    (``dense_f32``, csrc/kernels/dense.hip); ``value_out`` fuses the 256->1
+    layer, tanh, MSE, sign accuracy and its backward.  Head backward:
+    dz = dh W1^T and dW1 = z^T dh (the same kernel, operands read transposed
+    in place, dW1 written straight into the flat gradient buffer), then
     ``head_backward`` writes the ReLU'-masked gradient into the MFMA trunk
     backward plus per-board partials of the 1x1 conv weight/bias.
     ``correct`` counts sign(v) == sign(z)."""
@@ -527,7 +528,7 @@ class HipValueTrainer(HipConvTrainer):
     def _head_forward(self):
         v = self.fp.views
         ops.head_logits(self.Y[-1], v["head_w"].view(-1), v["head_b"], self.z, self.S)
-        torch.addmm(v["fc1_b"], self.z, v["fc1_w"], out=self.h)
+        ops.dense_f32(self.z, v["fc1_w"], self.h, bias=v["fc1_b"])  # h = z W1 + b1
 
     def _head_train(self, targets, gscale, weight):
         v, gv = self.fp.views, self.fp.grad_views
@@ -535,11 +536,11 @@ class HipValueTrainer(HipConvTrainer):
         self.tval.copy_(targets)
         ops.value_out(self.h, v["fc2_w"].view(-1), v["fc2_b"], self.val, target=self.tval, weight=weight,
                       loss=self.loss, correct=self.correct, dh=self.dh, dout=self.dout, grad_scale=gscale)
-        torch.mm(self.z.t(), self.dh, out=gv["fc1_w"])
+        ops.dense_f32(self.z, self.dh, gv["fc1_w"], trans_a=True)  # dW1 = z^T dh
         torch.sum(self.dh, dim=0, out=gv["fc1_b"])
         o2, n2 = self.fp.segments["fc2_w"]
         torch.sum(self.dout, dim=0, out=self.fp.grad[o2:o2 + n2 + 1])  # [dw2 | db2]
-        torch.mm(self.dh, v["fc1_w"].t(), out=self.dzl)
+        ops.dense_f32(self.dh, v["fc1_w"], self.dzl, trans_b=True)  # dz = dh W1^T
         ops.head_backward(self.Y[-1], v["head_w"].view(-1), self.dzl, self.DZ[-1], self.dhead, self.S)
         ho, hn = self.fp.segments["head_w"]
         torch.sum(self.dhead, dim=0, out=self.fp.grad[ho:ho + hn + 1])  # [dW_head | db_head]

@@ -443,3 +443,29 @@ def test_debug_build_bounds_checks(cuda_device, tmp_path):
     env = dict(os.environ, ALPHAGO_AMD_KERNELS="debug", PYTHONPATH=root)
     r = subprocess.run([sys.executable, "-c", _DEBUG_CHILD], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "DEBUG-OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb,bias,beta", [(2176, 256, 361, False, False, True, 0.0),
+                                                   (361, 256, 2176, True, False, False, 0.0),
+                                                   (2176, 361, 256, False, True, False, 0.0),
+                                                   (37, 70, 5, False, False, True, 0.5),
+                                                   (81, 16, 9, True, True, False, 1.0)])
+def test_dense_f32_vs_torch(ops, cuda_device, M, N, K, ta, tb, bias, beta):
+    """Value-head dense GEMM (fp32 MFMA) vs fp64 torch: the three shapes of the
+    value head (forward, dW1 = z^T dh, dz = dh W1^T) and ragged/transposed ones."""
+    torch.manual_seed(9)
+    A = torch.randn((K, M) if ta else (M, K), device=cuda_device)
+    B = torch.randn((N, K) if tb else (K, N), device=cuda_device)
+    b = torch.randn(N, device=cuda_device) if bias else None
+    C0 = torch.randn(M, N, device=cuda_device)
+    C = C0.clone()
+    ops.dense_f32(A, B, C, bias=b, trans_a=ta, trans_b=tb, beta=beta)
+    ref = (A.double().t() if ta else A.double()) @ (B.double().t() if tb else B.double())
+    if bias:
+        ref = ref + b.double()
+    ref = ref + beta * C0.double()
+    torch.cuda.synchronize()
+    assert (C.double() - ref).abs().max().item() < 1e-5 * max(1.0, K ** 0.5) * ref.abs().max().item()
+    C2 = C0.clone()
+    ops.dense_f32(A, B, C2, bias=b, trans_a=ta, trans_b=tb, beta=beta)
+    assert torch.equal(C, C2)  # deterministic
