@@ -152,7 +152,8 @@ def _torch_paths():
 
 def build_hip(force: bool = False, verbose: bool = False, flavor: str = "prod") -> str:
     srcs = _hip_sources(flavor)
-    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")))
+    # kernels include engine/ladder_bb.h (shared host/device ladder reader)
+    hdrs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.h")) + [os.path.join(CSRC, "engine", "ladder_bb.h")])
     out = hip_path(flavor)
     incs, libdir, abi = _torch_paths()
     common = [

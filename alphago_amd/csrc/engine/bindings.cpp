@@ -3,6 +3,8 @@
 // (x, y) tuples for moves and None for pass.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+
+#include "ladder_bb.h"
 #include <pybind11/stl.h>
 
 #include <thread>
@@ -235,6 +237,47 @@ PYBIND11_MODULE(_engine, m) {
         return py::make_tuple(board, ages, meta, l);
       },
       py::arg("states"), py::arg("ladder") = false, py::arg("threads") = 8);
+
+  m.def(
+      "ladder_bits_bb",
+      [](py::array_t<int8_t, py::array::c_style> board, py::array_t<int32_t, py::array::c_style> meta, int n,
+         int threads) {
+        // host run of the bitboard ladder reader (ladder_bb.h, the code of the GPU kernel)
+        // from the compact encoding: bit 0 capture, bit 1 escape, per point
+        const ssize_t B = board.shape(0), np = board.shape(1);
+        if (np != (ssize_t)n * n || meta.shape(0) != B) throw py::value_error("shape mismatch");
+        py::array_t<uint8_t> out({B, np});
+        const int8_t* pb = board.data();
+        const int32_t* pm = meta.data();
+        uint8_t* po = out.mutable_data();
+        {
+          py::gil_scoped_release rel;
+          lb::Geo g;
+          lb::make_geo(g, n);
+          const int T = std::max(1, std::min(threads, (int)B));
+          std::vector<std::thread> pool;
+          for (int t = 0; t < T; ++t)
+            pool.emplace_back([&, t]() {
+              std::vector<lb::Frame> stack(lb::kMaxFrames);
+              for (ssize_t i = t; i < B; i += T) {
+                lb::LState s;
+                lb::bzero(s.black);
+                lb::bzero(s.white);
+                for (int p = 0; p < np; ++p) {
+                  if (pb[i * np + p] > 0) lb::bset(s.black, p);
+                  if (pb[i * np + p] < 0) lb::bset(s.white, p);
+                }
+                s.ko = pm[2 * i];
+                const int me = pm[2 * i + 1];
+                for (int p = 0; p < np; ++p)
+                  po[i * np + p] = lb::is_candidate(s, p, me, g) ? (uint8_t)lb::ladder_bits_at(s, p, me, stack, g) : 0;
+              }
+            });
+          for (auto& th : pool) th.join();
+        }
+        return out;
+      },
+      py::arg("board"), py::arg("meta"), py::arg("n"), py::arg("threads") = 8);
 
   bind_mcts(m);
   bind_lzf(m);

@@ -190,6 +190,26 @@ struct DenseArgs {
   float* ws;
 };
 int dense_splits(int M, int N, int K);
+
+// GPU ladder planes (ladder.hip; search code ../engine/ladder_bb.h)
+struct LadderBoard {
+  uint64_t black[6], white[6], cand[6];
+  int ko, me;
+};
+struct LadderArgs {
+  const int8_t* board;     // [B][S*S] +1 black, -1 white, 0 empty
+  const int32_t* meta;     // [B][2] {ko point or -1, player to move}
+  LadderBoard* boards;     // [B] prep output
+  int32_t* counts;         // [B] candidate points per board
+  const int32_t* offsets;  // [B] exclusive prefix sum of counts
+  int32_t* counter;        // zeroed task counter of the search kernel
+  void* frames;            // search threads x ladder_frame_bytes() (frame stacks)
+  uint8_t* out;            // [B][S*S] zeroed; bit 0 = ladder capture, bit 1 = ladder escape
+  int B, S;
+};
+size_t ladder_frame_bytes();
+void launch_ladder_prep(const LadderArgs& a, hipStream_t st);
+void launch_ladder_search(const LadderArgs& a, int threads, hipStream_t st);
 void launch_dense_f32(const DenseArgs& a, bool transA, bool transB, hipStream_t st);
 // device-side schedule (graph-capturable): sched = {lr0, decay, iterations, lr_current} f64
 void launch_sgd_sched(float* p, const float* g, int64_t n, double* sched, float gscale, hipStream_t st);

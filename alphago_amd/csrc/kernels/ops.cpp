@@ -375,6 +375,43 @@ void dense_f32(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bi
   launch_check("dense_f32");
 }
 
+// Ladder planes from the compact board encoding: out (B, S*S) uint8, bit 0 =
+// ladder capture, bit 1 = ladder escape (the encoder's CPU ladder bits).
+void ladder_planes(const Tensor& board, const Tensor& meta, const Tensor& out, int64_t S) {
+  CHECK_DEV(board); CHECK_DEV(meta); CHECK_DEV(out);
+  TORCH_CHECK(board.scalar_type() == at::kChar && board.dim() == 2 && board.size(1) == S * S && board.is_contiguous(),
+              "board int8 (B, S*S)");
+  TORCH_CHECK(meta.scalar_type() == at::kInt && meta.size(0) == board.size(0) && meta.is_contiguous(), "meta int32 (B, 2)");
+  TORCH_CHECK(out.scalar_type() == at::kByte && out.sizes() == board.sizes() && out.is_contiguous(), "out uint8 (B, S*S)");
+  TORCH_CHECK(S >= 2 && S <= 19, "board size 2..19");
+  const int64_t B = board.size(0);
+  if (B == 0) return;
+  auto i32 = board.options().dtype(at::kInt);
+  Tensor boards = at::empty({B, (int64_t)sizeof(agk::LadderBoard)}, board.options().dtype(at::kByte));
+  Tensor counts = at::empty({B + 1}, i32);  // [B] = search task counter
+  agk::LadderArgs a{};
+  a.board = board.data_ptr<int8_t>();
+  a.meta = meta.data_ptr<int32_t>();
+  a.boards = reinterpret_cast<agk::LadderBoard*>(boards.data_ptr<uint8_t>());
+  a.counts = counts.data_ptr<int32_t>();
+  a.out = out.data_ptr<uint8_t>();
+  a.B = (int)B;
+  a.S = (int)S;
+  a.counter = a.counts + B;
+  out.zero_();
+  counts.zero_();
+  agk::launch_ladder_prep(a, cur_stream());
+  launch_check("ladder_prep");
+  Tensor c = counts.narrow(0, 0, B);
+  Tensor offsets = (at::cumsum(c, 0, at::kInt) - c).contiguous();
+  a.offsets = offsets.data_ptr<int32_t>();
+  const int threads = (int)std::min<int64_t>(16384, B * 32);
+  Tensor frames = at::empty({(int64_t)threads * (int64_t)agk::ladder_frame_bytes()}, board.options().dtype(at::kByte));
+  a.frames = frames.data_ptr<uint8_t>();
+  agk::launch_ladder_search(a, threads, cur_stream());
+  launch_check("ladder_search");
+}
+
 // A deliberately invalid launch (2048 threads per block, above the 1024
 // limit): the runtime rejects it, launch_check turns that into a Python
 // RuntimeError -- the test of the error path every op shares.
@@ -417,6 +454,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
   m.def("sgd_update_sched(Tensor(a!) p, Tensor g, Tensor(b!) sched, float gscale) -> ()");
   m.def("dense_f32(Tensor A, Tensor B, Tensor? bias, Tensor(a!) C, bool transA, bool transB, float beta) -> ()");
+  m.def("ladder_planes(Tensor board, Tensor meta, Tensor(a!) out, int S) -> ()");
   m.def(
       "featurize(Tensor board, Tensor ages, Tensor meta, Tensor? ladder, int[] fids, int[] fplanes, Tensor(a!)? planes, "
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
@@ -454,6 +492,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("sgd_update", &sgd_update);
   m.impl("sgd_update_sched", &sgd_update_sched);
   m.impl("dense_f32", &dense_f32);
+  m.impl("ladder_planes", &ladder_planes);
 #ifdef AGK_DEBUG
   m.impl("debug_conv_fwd_understated", &debug_conv_fwd_understated);
 #endif

@@ -83,7 +83,9 @@ class HipTrunkInference:
 
     @property
     def needs_ladder(self) -> bool:
-        return self.fz is not None and self.fz.need_ladder
+        """Whether callers must encode ladder bits on the host (False when the
+        GPU featurizer reads ladders on the device)."""
+        return self.fz is not None and self.fz.host_needs_ladder
 
     @torch.no_grad()
     def sync_weights(self) -> None:
@@ -237,7 +239,7 @@ class HipTrunkInference:
         bk.e_board[:n].copy_(torch.as_tensor(board), non_blocking=True)
         bk.e_ages[:n].copy_(torch.as_tensor(ages), non_blocking=True)
         bk.e_meta[:n].copy_(torch.as_tensor(meta), non_blocking=True)
-        if bk.e_ladder is not None:
+        if bk.e_ladder is not None and self.fz.host_needs_ladder:
             if ladder is None:
                 raise ValueError("this feature list needs ladder bits")
             bk.e_ladder[:n].copy_(torch.as_tensor(ladder), non_blocking=True)

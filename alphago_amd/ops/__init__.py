@@ -167,6 +167,14 @@ def dense_f32(A, B, C, bias=None, trans_a: bool = False, trans_b: bool = False, 
     return C
 
 
+def ladder_planes(board, meta, out, S: int):
+    """Ladder bits on the device from the compact encoding (board int8 (B, S*S),
+    meta int32 (B, 2) {ko, player to move}): out uint8 (B, S*S), bit 0 = ladder
+    capture, bit 1 = ladder escape -- the host encoder's ladder bits."""
+    _ops().ladder_planes(board, meta, out, S)
+    return out
+
+
 def sgd_update_sched(p, g, sched, gscale: float = 1.0):
     """SGD with the Keras decay schedule on the device: sched = float64
     {lr0, decay, iterations, lr}; advances iterations (HIP-graph capturable)."""

@@ -3,12 +3,16 @@
 The reference featurizes one board at a time in numpy
 (AlphaGo/preprocessing/preprocessing.py:217-245, ~265 positions/s).  Here the
 C++ engine writes a ~2-byte-per-point encoding of each board (stones, move
-ages, ko, side to move; plus ladder bits only when a ladder plane is asked
-for, since ladder reading is a sequential tree search that stays on the CPU)
-and ``featurize_kernel`` expands it on the device — chain labelling, liberty
-sets, legality, capture/self-atari/liberties-after and the recursive true-eye
-test — into uint8 planes, or straight into the conv trunk's padded NHWC bf16
-input together with the sensible-move mask.
+ages, ko, side to move) and ``featurize_kernel`` expands it on the device —
+chain labelling, liberty sets, legality, capture/self-atari/liberties-after
+and the recursive true-eye test — into uint8 planes, or straight into the
+conv trunk's padded NHWC bf16 input together with the sensible-move mask.
+Ladder planes (a tree search per candidate point; NotImplementedError in the
+reference, preprocessing.py:147-152) come from the host encoder by default:
+its incremental-liberty reader is several times faster than the device
+reader ``ladder_planes`` (csrc/kernels/ladder.hip, bit-identical), because a
+ladder search is one long serial chain of dependent board updates
+(profiles/r2_gpu_ladders.md).  ``gpu_ladders=True`` reads them on the device.
 
 Boards whose eye recursion is deeper than the kernel's frame stack (only
 pathological positions such as a full-board checkerboard) are flagged and
@@ -33,7 +37,8 @@ LADDER_FEATURES = ("ladder_capture", "ladder_escape")
 
 
 class GpuFeaturizer(object):
-    def __init__(self, feature_list: Sequence[str], board: int = 19, device="cuda", threads: int = 8):
+    def __init__(self, feature_list: Sequence[str], board: int = 19, device="cuda", threads: int = 8,
+                 gpu_ladders: bool = False):
         self.features = [f.lower() for f in feature_list]
         for f in self.features:
             if f not in FEATURE_IDS:
@@ -45,16 +50,22 @@ class GpuFeaturizer(object):
         if self.nplanes > 64:
             raise ValueError("GPU featurizer supports at most 64 planes")
         self.need_ladder = any(f in LADDER_FEATURES for f in self.features)
+        self.gpu_ladders = gpu_ladders
         self.S = board
         self.device = torch.device(device)
         self.threads = threads
         self._E = _engine()
         ops.load()
 
+    @property
+    def host_needs_ladder(self) -> bool:
+        """Whether the host encoder must supply ladder bits (GPU ladders off)."""
+        return self.need_ladder and not self.gpu_ladders
+
     # ------------------------------------------------------------ host side
     def encode(self, states):
         """numpy (board int8 (B,S*S), ages uint8, meta int32 (B,2), ladder uint8 or None)."""
-        return self._E.encode_batch(list(states), self.need_ladder, self.threads)
+        return self._E.encode_batch(list(states), self.host_needs_ladder, self.threads)
 
     def to_device(self, enc):
         b, a, m, l = enc
@@ -65,6 +76,14 @@ class GpuFeaturizer(object):
     # ------------------------------------------------------------ device side
     def run(self, board, ages, meta, ladder=None, planes=None, nhwc=None, P: int = 0, sensible=None, legal=None,
             overflow=None):
+        """With GPU ladders, ``ladder`` (a (B, S*S) uint8 buffer, or None) is
+        written on the device from ``board``/``meta`` before featurising."""
+        if self.need_ladder and self.gpu_ladders:
+            if ladder is None:
+                ladder = torch.empty(board.shape, dtype=torch.uint8, device=board.device)
+            ops.ladder_planes(board, meta, ladder, self.S)
+            if overflow is not None:  # bit 2: search budget exhausted -> recompute on the CPU
+                overflow |= (ladder & 4).amax(1).to(overflow.dtype)
         ops.featurize(board, ages, meta, self.fids, self.fplanes, self.S, ladder=ladder, planes=planes, nhwc=nhwc,
                       P=P, sensible=sensible, legal=legal, overflow=overflow)
 

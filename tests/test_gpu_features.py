@@ -177,7 +177,8 @@ def test_encoded_inference_matches_planes(cuda_device):
     states = random_positions(37, seed=9)
     pol = CNNPolicy(DEFAULT_FEATURES, device=cuda_device, filters_per_layer=64, layers=3)
     eng = pol.engine
-    assert eng.supports_encoded and eng.needs_ladder
+    assert eng.supports_encoded
+    assert eng.needs_ladder == eng.fz.host_needs_ladder  # host ladder bits only without GPU ladders
     E = engine()
     b, a, m, l = E.encode_batch(states, True, 4)
     probs, sens, bad = eng.evaluate_encoded(b, a, m, l)
@@ -244,3 +245,47 @@ def test_gpu_planes_match_cpu_1000_positions(cuda_device):
             bad = np.argwhere(got[i] != exp[i])
             raise AssertionError("state %d: %d mismatches, first %s" % (k + i, len(bad), bad[:5].tolist()))
         assert np.array_equal(sens, sens_all[k:k + 256])
+
+
+def test_bitboard_ladder_reader_matches_cpu_reader():
+    """The bitboard ladder reader (csrc/engine/ladder_bb.h -- the code the GPU
+    ladder kernel runs), executed on the host, gives exactly the CPU reader's
+    ladder bits on 1000 random 19x19 positions and smaller boards."""
+    for size, n, seed, max_len in ((19, 1000, 5, 330), (13, 300, 2, 150), (9, 300, 1, 100)):
+        states = random_positions(n, size=size, seed=seed, max_len=max_len)
+        board, _, meta, lad = engine().encode_batch(states, True, 8)
+        got = engine().ladder_bits_bb(board, meta, size, 8)
+        assert np.array_equal(got, lad), (size, np.argwhere(got != lad)[:5].tolist())
+        if size == 19:
+            assert int((lad & 1).sum()) > 0 and int((lad & 2).sum()) > 0
+
+
+@pytest.mark.gpu
+def test_gpu_ladder_planes_match_cpu(cuda_device):
+    """ladder_planes (csrc/kernels/ladder.hip) on >= 1000 random 19x19 positions
+    and on 9x9 / 13x13 boards: bit-equal to the CPU ladder reader."""
+    import torch
+    from alphago_amd import ops
+
+    for size, n, seed, max_len in ((19, 1200, 7, 330), (13, 200, 2, 150), (9, 200, 1, 100)):
+        states = random_positions(n, size=size, seed=seed, max_len=max_len)
+        board, _, meta, lad = engine().encode_batch(states, True, 8)
+        out = torch.empty(board.shape, dtype=torch.uint8, device=cuda_device)
+        ops.ladder_planes(torch.from_numpy(board).to(cuda_device), torch.from_numpy(meta).to(cuda_device), out, size)
+        got = out.cpu().numpy()
+        assert np.array_equal(got, lad), (size, np.argwhere(got != lad)[:5].tolist())
+
+
+@pytest.mark.gpu
+def test_gpu_featurizer_device_ladders(cuda_device):
+    """GpuFeaturizer(gpu_ladders=True): ladder planes read on the device equal
+    the CPU featurizer's, including the deep eye-chain positions."""
+    from alphago_amd.ops.gpu_features import GpuFeaturizer
+
+    feats = ["board", "ladder_capture", "ladder_escape", "sensibleness"]
+    states = random_positions(64, seed=13, max_len=330) + eye_chain_positions()[-2:]
+    states = [s for s in states if s.size == 19]
+    fz = GpuFeaturizer(feats, board=19, device=cuda_device, gpu_ladders=True)
+    assert not fz.host_needs_ladder
+    got = fz.planes(states).cpu().numpy()
+    assert np.array_equal(got, Preprocess(feats).states_to_uint8(states))
