@@ -38,7 +38,16 @@
 namespace agk {
 
 // ----------------------------------------------------------------- forward
-template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false>
+// STR (Cin % 64 == 32, e.g. the value net's 152 filters padded to 160): a
+// 64-channel K-step may straddle two taps -- the 32-channel half h of every
+// staged row comes from its own (tap, channel) source, selected per lane by
+// the row piece's logical chunk, so no MFMA multiplies padding.  The last
+// step's second half (K = taps * Cin is an odd multiple of 32) reads an extra
+// all-zero weight tap (packed weights then hold K*K + 1 taps).
+// BN whose per-wave weight rows are not a multiple of 8 (BN = 160) stage the
+// weight tile as 8-row pieces dealt round-robin over the waves.
+template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
+          bool STR = false>
 __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
   constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
@@ -49,9 +58,12 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   constexpr int STAGE = A_BYTES + B_BYTES;
   constexpr int A_ROWS_PW = BM / NW;   // pixel rows staged per wave
   constexpr int A_INSTR = A_ROWS_PW / 8;
-  constexpr int B_ROWS_PW = BN / NW;   // weight rows staged per wave
-  constexpr int B_INSTR = B_ROWS_PW / 8;  // glds instructions per wave for the weight tile
-  static_assert(B_ROWS_PW % 8 == 0 && A_ROWS_PW % 8 == 0, "rows per wave must be multiples of 8");
+  constexpr bool BDIST = (BN / NW) % 8 != 0;  // weight pieces dealt round-robin
+  constexpr int B_ROWS_PW = BN / NW;   // weight rows staged per wave (contiguous layout)
+  constexpr int B_INSTR = BDIST ? (BN / 8 + NW - 1) / NW : B_ROWS_PW / 8;  // glds instructions per wave
+  static_assert(BN % 32 == 0 && BN % 8 == 0 && A_ROWS_PW % 8 == 0, "tile geometry");
+  static_assert(!(BDIST && (M32 || ILV)), "round-robin weight staging: production loops only");
+  static_assert(!(STR && (M32 || ILV)), "straddled K-steps: production loops only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63;
@@ -61,13 +73,15 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   const int n0 = blockIdx.y * BN;
   const int SS = a.S * a.S;
   const int CC = a.Cin >> 6;  // 64-channel chunks
-  const int nK = a.K * a.K * CC;
+  const int nK = STR ? (a.K * a.K * a.Cin + 63) >> 6 : a.K * a.K * CC;
 
   // --- staging addresses (element offsets)
   int arow[A_INSTR];
+  bool ahi[A_INSTR], bhi[B_INSTR];  // STR: the piece's 32-channel half of the K-step
 #pragma unroll
   for (int i = 0; i < A_INSTR; ++i) {
     const int r = wave * A_ROWS_PW + i * 8 + (lane >> 3);
+    ahi[i] = (((lane & 7) ^ ((r >> 1) & 7)) >> 2) != 0;
     int m = m0 + r;
     m = m < a.M ? m : a.M - 1;
     const int b = fdiv(m, a.divSS);
@@ -75,50 +89,68 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     const int ii = fdiv(rem, a.divS);
     const int jj = rem - ii * a.S;
     const int logical = (lane & 7) ^ ((r >> 1) & 7);
-    arow[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + logical * 8;
+    // STR: channel part (logical & 3) * 8 only; the half (logical >> 2) picks the source
+    arow[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + (STR ? (logical & 3) : logical) * 8;
   }
-  int brow[B_INSTR];
+  int brow[B_INSTR], bldsrow[B_INSTR];
 #pragma unroll
   for (int i = 0; i < B_INSTR; ++i) {
-    const int r = wave * B_ROWS_PW + i * 8 + (lane >> 3);
+    const int piece = BDIST ? wave + i * NW : wave * (B_ROWS_PW / 8) + i;  // 8-row piece of the weight tile
+    const int r = piece * 8 + (lane >> 3);
     const int logical = (lane & 7) ^ ((r >> 1) & 7);
-    brow[i] = (n0 + r) * a.Cin + logical * 8;
+    bhi[i] = (logical >> 2) != 0;
+    brow[i] = (n0 + (r < BN ? r : BN - 1)) * a.Cin + (STR ? (logical & 3) : logical) * 8;
+    bldsrow[i] = piece * 8;
   }
+
   const size_t wtap = (size_t)a.Cout * a.Cin;
 
   // staging cursor over (tap, 64-channel chunk), advanced incrementally with
   // scalar adds (no per-step integer divisions)
-  int st_c0 = 0, st_kw = 0, st_a = 0;
+  int st_c0 = 0, st_kw = 0, st_a = 0, st_t = 0;
   size_t st_w = 0;
   auto stage = [&](int buf) {
     char* base = smem + buf * STAGE;
-#ifdef AGK_DEBUG
+    // source offsets (without the lane's row/channel part) of the step's two
+    // 32-channel halves; equal unless STR
+    int xo0 = st_a + st_c0, xo1 = xo0;
+    size_t wo0 = st_w + st_c0, wo1 = wo0;
+    if constexpr (STR) {
+      const int c1 = st_c0 + 32;
+      const bool nx = c1 >= a.Cin;  // the second half opens the next tap
+      const int a_next = st_a + (st_kw + 1 == a.K ? (a.HPi - a.K + 1) * a.Cin : a.Cin);
+      // past the last tap: any in-range pixel rows (the weight tap there is all zero)
+      xo1 = nx ? (st_t + 1 < a.K * a.K ? a_next : xo0) : st_a + c1;
+      wo1 = nx ? st_w + wtap : st_w + c1;
+    }
 #pragma unroll
     for (int i = 0; i < A_INSTR; ++i) {
-      const long long xo = (long long)arow[i] + st_a + st_c0;
-      const bool ok = AGK_DCHECK(xo >= 0 && xo + 8 <= a.x_elems, DBG_FWD_X);
+      const int xo = arow[i] + ((STR && ahi[i]) ? xo1 : xo0);
+#ifdef AGK_DEBUG
+      const bool ok = AGK_DCHECK(xo >= 0 && (long long)xo + 8 <= a.x_elems, DBG_FWD_X);
       glds16(a.x + (ok ? xo : 0), base + (wave * A_ROWS_PW + i * 8) * 128);
+#else
+      glds16(a.x + xo, base + (wave * A_ROWS_PW + i * 8) * 128);
+#endif
     }
-    const __bf16* wt = a.w + st_w + st_c0;
 #pragma unroll
     for (int i = 0; i < B_INSTR; ++i) {
-      const long long wo = (long long)st_w + st_c0 + brow[i];
-      const bool ok = AGK_DCHECK(wo >= 0 && wo + 8 <= a.w_elems, DBG_FWD_W);
-      glds16(ok ? wt + brow[i] : a.w, base + A_BYTES + (wave * B_ROWS_PW + i * 8) * 128);
-    }
+      if (BDIST && wave + i * NW >= BN / 8) continue;  // wave-uniform: fewer pieces on the last waves
+      const size_t wo = ((STR && bhi[i]) ? wo1 : wo0) + brow[i];
+#ifdef AGK_DEBUG
+      const bool ok = AGK_DCHECK((long long)wo + 8 <= a.w_elems, DBG_FWD_W);
+      glds16(ok ? a.w + wo : a.w, base + A_BYTES + bldsrow[i] * 128);
 #else
-#pragma unroll
-    for (int i = 0; i < A_INSTR; ++i) glds16(a.x + arow[i] + st_a + st_c0, base + (wave * A_ROWS_PW + i * 8) * 128);
-    const __bf16* wt = a.w + st_w + st_c0;
-#pragma unroll
-    for (int i = 0; i < B_INSTR; ++i) glds16(wt + brow[i], base + A_BYTES + (wave * B_ROWS_PW + i * 8) * 128);
+      glds16(a.w + wo, base + A_BYTES + bldsrow[i] * 128);
 #endif
+    }
     // branch-free cursor advance (selects), so a caller can interleave the
     // DMA with MFMAs inside one basic block
     st_c0 += 64;
-    const bool wrap = st_c0 == a.Cin;
-    st_c0 = wrap ? 0 : st_c0;
+    const bool wrap = STR ? st_c0 >= a.Cin : st_c0 == a.Cin;
+    st_c0 = wrap ? st_c0 - a.Cin : st_c0;
     st_w += wrap ? wtap : 0;
+    st_t += wrap ? 1 : 0;
     st_kw += wrap ? 1 : 0;
     const bool wrap2 = st_kw == a.K;
     st_kw = wrap2 ? 0 : st_kw;
@@ -494,15 +526,27 @@ static void launch_fwd_ga(const ConvFwdArgs& a, hipStream_t st) {
 
 #endif  // AGK_KERNEL_LAB
 
-template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false>
+template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
+          bool STR = false>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR>,
+      hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV>), grid, dim3(BM / MBW * 8), smem, st,
-                     a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR>), grid, dim3(BM / MBW * 8), smem,
+                     st, a);
+}
+
+// 160-wide output tile (value net: 152 filters padded to 160 instead of 192);
+// Cin % 64 == 32 uses straddled K-steps
+template <int MODE, bool STR>
+static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
+  if (bm == 384) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR>(a, st);
+  else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
+  else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
+  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 128 / 256 / 384");
 }
 
 
@@ -515,33 +559,40 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // the larger tile moves fewer bytes per MFMA (bench: 106.2k -> 108.5k pos/s,
   // scripts/bench_variants.sh).
   if (bm == 0) bm = (a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
-  // production tile codes: 128 / 256 (64-pixel waves), 384 (default, 96x96 per wave)
-  if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);
-  else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
-  else if (bm == 128) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
+  if constexpr (BN == 160) {
+    if (a.Cin % 64 == 32) launch_fwd_160<MODE, true>(a, bm, st);
+    else launch_fwd_160<MODE, false>(a, bm, st);
+  } else {
+    if (a.Cin % 64 != 0) throw std::invalid_argument("conv_fwd: Cin % 64 == 32 needs the 160-wide tile");
+    // production tile codes: 128 / 256 (64-pixel waves), 384 (default, 96x96 per wave)
+    if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);
+    else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
+    else if (bm == 128) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
 #ifdef AGK_KERNEL_LAB
-  // kernel-lab tile codes (profiles/r1_fwd_kernel_experiments.md):
-  // conv_fwd_variants.hip (-1, 2, 4, 5, 6, 32), 2560 (epilogue loads after the loop),
-  // 2568 (BM 256, 128-pixel waves), 11 (pixel operand from L2), 9 / 10 (DMA spread
-  // through the MFMAs), 7 / 8 (32x32x16 MFMA)
-  else if ((bm == -1 || bm == 2 || bm == 4 || bm == 5 || bm == 6 || bm == 32) &&
-           launch_conv_fwd_variant(bm, a, MODE, st)) return;
-  else if (bm == -1 || bm == 2 || bm == 4 || bm == 5 || bm == 6 || bm == 32) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
-  else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);
-  else if (bm == 2568) launch_fwd_bm<BN, MODE, 256, 8>(a, st);
-  else if (bm == 11) launch_fwd_ga<BN, MODE>(a, st);
-  else if (bm == 9) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
-  else if (bm == 10) launch_fwd_bm<BN, MODE, 256, 4, false, false, false, true>(a, st);
-  else if (bm == 7) launch_fwd_bm<BN, MODE, 384, 6, false, false, true>(a, st);
-  else if (bm == 8) launch_fwd_bm<BN, MODE, 256, 4, false, false, true>(a, st);
+    // kernel-lab tile codes (profiles/r1_fwd_kernel_experiments.md):
+    // conv_fwd_variants.hip (-1, 2, 4, 5, 6, 32), 2560 (epilogue loads after the loop),
+    // 2568 (BM 256, 128-pixel waves), 11 (pixel operand from L2), 9 / 10 (DMA spread
+    // through the MFMAs), 7 / 8 (32x32x16 MFMA)
+    else if ((bm == -1 || bm == 2 || bm == 4 || bm == 5 || bm == 6 || bm == 32) &&
+             launch_conv_fwd_variant(bm, a, MODE, st)) return;
+    else if (bm == -1 || bm == 2 || bm == 4 || bm == 5 || bm == 6 || bm == 32) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
+    else if (bm == 2560) launch_fwd_bm<BN, MODE, 256, 4, false>(a, st);
+    else if (bm == 2568) launch_fwd_bm<BN, MODE, 256, 8>(a, st);
+    else if (bm == 11) launch_fwd_ga<BN, MODE>(a, st);
+    else if (bm == 9) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
+    else if (bm == 10) launch_fwd_bm<BN, MODE, 256, 4, false, false, false, true>(a, st);
+    else if (bm == 7) launch_fwd_bm<BN, MODE, 384, 6, false, false, true>(a, st);
+    else if (bm == 8) launch_fwd_bm<BN, MODE, 256, 4, false, false, true>(a, st);
 #endif
-  else throw std::invalid_argument("conv_fwd: unknown tile code " + std::to_string(bm));
+    else throw std::invalid_argument("conv_fwd: unknown tile code " + std::to_string(bm));
+  }
 }
 
 
 template <int MODE>
 static void launch_fwd_mode(const ConvFwdArgs& a, hipStream_t st) {
-  if (a.Cout % 192 == 0) launch_fwd_t<192, MODE>(a, st);
+  if (a.Cout == 160) launch_fwd_t<160, MODE>(a, st);
+  else if (a.Cout % 192 == 0) launch_fwd_t<192, MODE>(a, st);
   else if (a.Cout % 128 == 0) launch_fwd_t<128, MODE>(a, st);
   else launch_fwd_t<64, MODE>(a, st);
 }
@@ -1013,7 +1064,7 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
 }
 
 int wgrad_tap_group(int Cout, int Cin, int K, int variant) {
-  const bool c64 = Cin % 192 != 0 && Cin % 128 != 0;
+  const bool c64 = Cin != 160 && Cin % 192 != 0 && Cin % 128 != 0;
   (void)Cout;
   return (c64 && variant == 0 && (K == 3 || K == 5)) ? K : 1;
 }
@@ -1053,6 +1104,19 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS>), grid, dim3(512), smem, st, a);
 }
 
+// 160 x 160 tile on 4 waves (2 n x 2 c, 80 x 80 per wave): the value net's
+// padded width; 40 KB of LDS, so several workgroups share a CU
+static void launch_wgrad_160x160(const ConvWgradArgs& a, hipStream_t st) {
+  if (a.variant != 0) throw std::invalid_argument("conv_wgrad: 160-wide tiles have no lab variants");
+  constexpr int KS = kWgradKsub;
+  constexpr int smem = 2 * (160 + 160) * 64 * KS;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<160, 160, KS, 2>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+  dim3 grid(a.nsplit, a.T, 1);
+  hipLaunchKernelGGL((conv_wgrad_kernel<160, 160, KS, 2>), grid, dim3(256), smem, st, a);
+}
+
 int wgrad_stage_pixels() { return 32 * kWgradKsub; }
 
 #ifdef AGK_DEBUG
@@ -1071,7 +1135,13 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
   a.divS = make_fastdiv((uint32_t)a.S);
   const bool n192 = a.Cout % 192 == 0, c192 = a.Cin % 192 == 0;
   const bool n128 = a.Cout % 128 == 0, c128 = a.Cin % 128 == 0;
-  if (n192 && c192) launch_wgrad_t<192, 192>(a, st);
+  if (a.Cout == 160) {  // value net (152 filters padded to 160)
+    if (a.Cin == 160) launch_wgrad_160x160(a, st);
+    else if (a.Cin % 64 == 0 && a.Cin % 128 != 0 && a.Cin % 192 != 0) launch_wgrad_t<160, 64>(a, st);
+    else throw std::invalid_argument("conv_wgrad: Cout 160 supports Cin 160 or an odd multiple of 64");
+  } else if (a.Cin == 160) {
+    throw std::invalid_argument("conv_wgrad: Cin 160 needs Cout 160");
+  } else if (n192 && c192) launch_wgrad_t<192, 192>(a, st);
   else if (n192 && c128) launch_wgrad_t<192, 128>(a, st);
   else if (n192) launch_wgrad_t<192, 64>(a, st);
   else if (n128 && c128) launch_wgrad_t<128, 128>(a, st);

@@ -186,7 +186,9 @@ void pack_weights(at::TensorList ws, at::TensorList wf, at::TensorList wd) {
       L.Cout_real = (int)w.size(0); L.Cin_real = (int)w.size(1); L.K = (int)w.size(2);
       L.wf = bfp_mut(wf[i]);
       L.Cout_p = (int)wf[i].size(1); L.Cin_p = (int)wf[i].size(2);
-      TORCH_CHECK(wf[i].size(0) == L.K * L.K && L.Cout_p >= L.Cout_real && L.Cin_p >= L.Cin_real, "bad wf");
+      // K*K taps, or K*K + 1 with a trailing all-zero tap (Cin % 64 == 32; never written here)
+      TORCH_CHECK((wf[i].size(0) == L.K * L.K || wf[i].size(0) == L.K * L.K + 1) && L.Cout_p >= L.Cout_real &&
+                  L.Cin_p >= L.Cin_real, "bad wf");
       L.wd = nullptr;
       if (wd.size() && wd[i].numel() > 0) {
         CHECK_BF16(wd[i]);

@@ -50,8 +50,12 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
   const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3);
   const int64_t HPo = y.size(1), Cout = y.size(3);
   TORCH_CHECK(x.size(2) == HPi && y.size(2) == HPo && y.size(0) == B, "bad spatial dims");
-  TORCH_CHECK(w.size(0) == K * K && w.size(1) == Cout && w.size(2) == Cin, "w must be (K*K, Cout, Cin)");
-  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "channels must be multiples of 64");
+  // Cin % 64 == 32 (straddled K-steps, 160-wide tile only): one extra all-zero weight tap
+  const int64_t taps = K * K + (Cin % 64 == 32 ? 1 : 0);
+  TORCH_CHECK(w.size(0) == taps && w.size(1) == Cout && w.size(2) == Cin,
+              "w must be (K*K, Cout, Cin), or (K*K + 1, Cout, Cin) when Cin % 64 == 32");
+  TORCH_CHECK((Cout % 64 == 0 && Cin % 64 == 0) || (Cout == 160 && (Cin % 64 == 0 || Cin == 160)),
+              "channels must be multiples of 64, or Cout 160 with Cin 160 / a multiple of 64");
   TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin && HPo == S + 2 * Po, "padding/geometry mismatch");
   TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31) && B * HPo * HPo * Cout < (1ll << 31), "tensor too large for int32 offsets");
   agk::ConvFwdArgs a{};
@@ -79,7 +83,7 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
   }
   if (mbits.has_value()) {
     TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
-    const int64_t words = (Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
+    const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
     TORCH_CHECK(mbits->numel() >= B * HPo * HPo * words, "mbits too small: need B*HPo*HPo*words");
     TORCH_CHECK(mode == agk::MODE_BIAS_RELU || mode == agk::MODE_MASKBITS, "mbits with modes 0 (write) / 3 (read)");
     if (mode == agk::MODE_BIAS_RELU) a.mbits_out = reinterpret_cast<uint32_t*>(mbits->data_ptr<int>());
@@ -102,7 +106,8 @@ inline void conv_wgrad_impl(const Tensor& x, const Tensor& dz, const Tensor& sla
   const int64_t nsplit = slab.size(0);
   TORCH_CHECK(slab.dim() == 4 && slab.size(1) == K * K && slab.size(2) == Cout && slab.size(3) == Cin, "bad slab");
   TORCH_CHECK(dbslab.size(0) == nsplit && dbslab.size(1) == Cout, "bad dbias slab");
-  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0, "channels must be multiples of 64");
+  TORCH_CHECK((Cin % 64 == 0 && Cout % 64 == 0) || (Cout == 160 && (Cin == 160 || Cin % 64 == 0)),
+              "channels must be multiples of 64, or Cout 160 with Cin 160 / a multiple of 64");
   TORCH_CHECK(HPi == S + 2 * Pin && HPo == S + 2 * Po && Po >= 1 && Pin >= K / 2, "geometry mismatch");
   agk::ConvWgradArgs a{};
   a.variant = variant;

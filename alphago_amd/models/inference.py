@@ -48,7 +48,8 @@ class HipTrunkInference:
         tr = net.trunk
         self.S, self.L, self.K = net.board, tr.layers, list(tr.widths)
         self.C0, self.F = tr.in_planes, tr.filters
-        self.C0p, self.Fp = ops.round_up(self.C0, 64), ops.round_up(self.F, 64)
+        self.C0p = ops.round_up(self.C0, 64)
+        self.Fp = ops.round_up(self.F, 64) if self.precision == "fp8" else ops.pad_filters(self.F)
         self.P0 = self.K[0] // 2
         self.buckets = sorted(buckets)
         self.use_graphs = use_graphs

@@ -86,6 +86,18 @@ def round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+def pad_filters(F: int) -> int:
+    """Padded trunk width for the bf16 conv kernels: multiples of 64, except
+    129..160 -> 160 (the value net's 152 filters, AlphaGo/models/value.py:7),
+    which runs on 160-wide tiles with straddled K-steps instead of 192."""
+    return 160 if 128 < F <= 160 else round_up(F, 64)
+
+
+def conv_n_tile(C: int) -> int:
+    """Output-channel tile of the conv kernels for C padded channels."""
+    return 160 if C == 160 else 192 if C % 192 == 0 else 128 if C % 128 == 0 else 64
+
+
 # ----------------------------------------------------------------- layout helpers
 def padded_empty(B: int, S: int, P: int, C: int, device, dtype=torch.bfloat16) -> torch.Tensor:
     """Zero-initialised padded NHWC buffer (borders must stay zero)."""
@@ -120,8 +132,7 @@ def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: 
 
 def mbits_words(cout_p: int) -> int:
     """32-bit ReLU'-bitmask words per padded pixel for a conv with cout_p output channels."""
-    bn = 192 if cout_p % 192 == 0 else 128 if cout_p % 128 == 0 else 64
-    return cout_p // bn * 8
+    return cout_p // conv_n_tile(cout_p) * 8
 
 
 def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1, cin_real: int = 0):
@@ -182,8 +193,13 @@ def sgd_update_sched(p, g, sched, gscale: float = 1.0):
 
 
 def packed_weight_like(w_oihw: torch.Tensor, cin_p: int, cout_p: int, transposed: bool = False) -> torch.Tensor:
+    """Zeroed packed bf16 weights (K*K, Cout, Cin) -- transposed (K*K, Cin, Cout) for dgrad.  When the
+    reduction width (Cin, or Cout for dgrad) is an odd multiple of 32 there is one extra all-zero tap:
+    the straddled K-steps' last half reads it."""
     K = w_oihw.shape[2]
-    shape = (K * K, cin_p, cout_p) if transposed else (K * K, cout_p, cin_p)
+    red = cout_p if transposed else cin_p
+    T = K * K + (1 if red % 64 == 32 else 0)
+    shape = (T, cin_p, cout_p) if transposed else (T, cout_p, cin_p)
     return torch.zeros(shape, device=w_oihw.device, dtype=torch.bfloat16)
 
 

@@ -140,7 +140,8 @@ class HipConvTrainer:
         self.C0 = tr.in_planes
         self.C0p = ops.round_up(self.C0, 64)
         self.F = tr.filters
-        self.Fp = ops.round_up(self.F, 64)
+        # fp8 kernels tile in 64-channel chunks; bf16 runs 152 filters on 160-wide tiles
+        self.Fp = ops.round_up(self.F, 64) if precision == "fp8" else ops.pad_filters(self.F)
         if self.F > 256:
             raise ValueError("head kernels support up to 256 filters")
         self.P0 = self.K[0] // 2
@@ -182,8 +183,7 @@ class HipConvTrainer:
         for l in range(self.L):
             cin_p = self.C0p if l == 0 else self.Fp
             T = self.K[l] ** 2
-            tiles = max(1, (self.Fp // (192 if self.Fp % 192 == 0 else 128 if self.Fp % 128 == 0 else 64))
-                        * (cin_p // (192 if cin_p % 192 == 0 else 128 if cin_p % 128 == 0 else 64)))
+            tiles = max(1, (self.Fp // ops.conv_n_tile(self.Fp)) * (cin_p // ops.conv_n_tile(cin_p)))
             taps = ops.wgrad_tap_group(self.Fp, cin_p, self.K[l])  # taps share one workgroup
             ns = ops.wgrad_splits(M, T // taps, tiles, wgrad_target_wgs)
             self.nsplit.append(ns)

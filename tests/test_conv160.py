@@ -1,0 +1,112 @@
+"""160-wide conv tiles (value net: 152 filters padded to 160, AlphaGo/models/value.py:7)
+vs plain PyTorch fp32: forward with straddled K-steps (Cin % 64 == 32), the
+ReLU'-bitmask dgrad, and the 160x160 / tap-merged 160x64 wgrad tiles."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops(cuda_device):
+    from alphago_amd import ops as _ops
+
+    _ops.load()
+    return _ops
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+def _rel_err(a, b):
+    return (a - b).abs().max().item() / max(b.abs().max().item(), 1e-6)
+
+
+def test_padding_helpers(ops):
+    assert ops.pad_filters(152) == 160 and ops.pad_filters(192) == 192 and ops.pad_filters(64) == 64
+    assert ops.mbits_words(160) == 8 and ops.conv_n_tile(160) == 160
+    w = torch.zeros(152, 152, 3, 3)
+    assert ops.packed_weight_like(w, 160, 160).shape == (10, 160, 160)  # extra zero tap
+    assert ops.packed_weight_like(torch.zeros(152, 49, 5, 5), 64, 160).shape == (25, 160, 64)
+
+
+@pytest.mark.parametrize("tile", [0, 128, 256, 384])
+@pytest.mark.parametrize("B,Cin,Cin_p,K", [(5, 152, 160, 3), (3, 49, 64, 5), (1, 152, 160, 3)])
+def test_conv_fwd_160(ops, cuda_device, tile, B, Cin, Cin_p, K):
+    torch.manual_seed(0)
+    S, P, Cout, Cp = 19, K // 2, 152, 160
+    x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
+    w = _bf(torch.randn(Cout, Cin, K, K, device=cuda_device) * 0.05)
+    b = torch.randn(Cout, device=cuda_device) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=P))
+    xp = ops.to_padded(x, P, Cin_p)
+    wp = ops.packed_weight_like(w, Cin_p, Cp)
+    ops.pack_weights([w.contiguous()], [wp])
+    bp = torch.zeros(Cp, device=cuda_device)
+    bp[:Cout] = b
+    y = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=cuda_device)
+    ops.conv_fwd(xp, wp, bp, y, K, S, P, 1, mbits=mbits, tile=tile)
+    torch.cuda.synchronize()
+    out = ops.from_padded(y, 1)
+    assert _rel_err(out[:, :Cout], ref) < 1e-2
+    assert out[:, Cout:].abs().sum() == 0  # padded channels: zero weights, zero bias
+    assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
+
+
+@pytest.mark.parametrize("tile", [0, 128, 384])
+def test_conv_dgrad_160_bitmask(ops, cuda_device, tile):
+    """dgrad with transposed 160-wide weights and the ReLU' bitmask written by
+    the forward epilogue == conv2d_input * (y > 0)."""
+    torch.manual_seed(1)
+    B, S, K, C, Cp = 4, 19, 3, 152, 160
+    xin = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w0 = _bf(torch.randn(C, C, K, K, device=cuda_device) * 0.05)
+    b0 = torch.randn(C, device=cuda_device) * 0.1
+    w = _bf(torch.randn(C, C, K, K, device=cuda_device) * 0.05)
+    dz = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    # forward of the previous layer: y = relu(conv(xin, w0) + b0), bitmask written alongside
+    wp0 = ops.packed_weight_like(w0, Cp, Cp)
+    ops.pack_weights([w0], [wp0])
+    bp0 = torch.zeros(Cp, device=cuda_device)
+    bp0[:C] = b0
+    y = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=cuda_device)
+    ops.conv_fwd(ops.to_padded(xin, 1, Cp), wp0, bp0, y, K, S, 1, 1, mbits=mbits, tile=tile)
+    yv = ops.from_padded(y, 1)[:, :C]
+    ref = torch.nn.grad.conv2d_input((B, C, S, S), w, dz, padding=K // 2) * (yv > 0)
+    wf = ops.packed_weight_like(w, Cp, Cp)
+    wd = ops.packed_weight_like(w, Cp, Cp, transposed=True)
+    ops.pack_weights([w], [wf], [wd])
+    dx = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    ops.conv_fwd(ops.to_padded(dz, 1, Cp), wd, None, dx, K, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mbits, tile=tile)
+    torch.cuda.synchronize()
+    out = ops.from_padded(dx, 1)
+    assert _rel_err(out[:, :C], ref) < 1e-2
+    assert out[:, C:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("B,Cin,Cin_p,K,Pin", [(6, 152, 160, 3, 1), (5, 49, 64, 5, 2), (3, 152, 160, 3, 1)])
+def test_conv_wgrad_160(ops, cuda_device, B, Cin, Cin_p, K, Pin):
+    torch.manual_seed(2)
+    S, Cout, Cp = 19, 152, 160
+    x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
+    dz = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
+    ref_w = torch.nn.grad.conv2d_weight(x, (Cout, Cin, K, K), dz, padding=K // 2)
+    ref_b = dz.sum(dim=(0, 2, 3))
+    xp = ops.to_padded(x, Pin, Cin_p)
+    dzp = ops.to_padded(dz, 1, Cp)
+    taps = ops.wgrad_tap_group(Cp, Cin_p, K)
+    assert taps == (K if Cin_p == 64 else 1)
+    ns = ops.wgrad_splits(B * S * S, K * K // taps)
+    slab = torch.full((ns, K * K, Cp, Cin_p), float("nan"), device=cuda_device)
+    dbs = torch.zeros(ns, Cp, device=cuda_device)
+    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin if Cin_p == 64 else 0)
+    gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
+    gb = torch.zeros(Cout, device=cuda_device)
+    ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert _rel_err(gw, ref_w) < 2e-3
+    assert _rel_err(gb, ref_b) < 2e-3

@@ -134,18 +134,21 @@ def test_hip_grads_match_bf16_emulation(cuda_device):
             assert cos > 0.999, (name, cos)
 
 
-def test_hip_value_grads_match_torch(cuda_device):
-    """HIP value head (head_logits -> addmm -> value_out -> head_backward) vs autograd."""
+@pytest.mark.parametrize("F", [64, 152])
+def test_hip_value_grads_match_torch(cuda_device, F):
+    """HIP value trunk + head (head_logits -> dense -> value_out -> head_backward)
+    vs autograd; F = 152 is the reference width, run on 160-wide tiles."""
     from alphago_amd.models.nets import ValueNet
     from alphago_amd.train.engine import HipValueTrainer, TorchValueTrainer
 
     torch.manual_seed(0)
     B, C = 6, 49
-    net = ValueNet(C, filters_per_layer=64, layers=3)
+    net = ValueNet(C, filters_per_layer=F, layers=3)
     net_ref = copy.deepcopy(net)
     planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
     z = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
     hip = HipValueTrainer(net, B, lr=0.01, device=cuda_device)
+    assert hip.Fp == (160 if F == 152 else F)
     ref = TorchValueTrainer(net_ref, B, lr=0.01, device=cuda_device)
     hip.compute_grads(planes, z, None)
     ref.compute_grads(planes, z, None)
