@@ -48,7 +48,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_kernel(ConvFp8Args a) {
   const int m0 = blockIdx.x * BM;
   const int n0 = blockIdx.y * BN;
   const int SS = a.S * a.S;
-  const int CC = a.Cin >> 6;
+  const int CC = (a.Cin + 63) >> 6;  // Cin 160: the third chunk's upper half is the next pixel (zero weights)
   const int nK = a.nch >> 1;
   const int qmax = a.K * a.K * CC - 1;  // last real chunk (padding chunks re-read it; their weights are 0)
   const int sx = a.scales[0], sw = a.scales[1];
@@ -217,9 +217,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   constexpr int NH = NB / NPART;
   static_assert(NB % NPART == 0, "channel blocks must split evenly into parts");
   constexpr int BM = 8 * 16 * MB;
-  constexpr int W_BYTES = BN * 128;
+  // weight slot rows: BN rounded up so that every thread stages the same number
+  // of 16-B pieces (BN 160 -> 192 rows; rows >= BN hold copies, never read)
+  constexpr int WROWS = (BN * 8) % 512 == 0 ? BN : ((BN * 8 + 511) / 512 * 512) / 8;
+  constexpr int W_BYTES = WROWS * 128;
   constexpr int WP = W_BYTES / 16 / 512;  // 16-B weight pieces per thread and step
-  static_assert(W_BYTES % (16 * 512) == 0, "weight tile must split evenly over 512 threads");
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   const int m0 = tile * BM;
   const int n0 = blockIdx.y * BN;
   const int SS = a.S * a.S;
-  const int CC = a.Cin >> 6;
+  const int CC = (a.Cin + 63) >> 6;  // Cin 160: the third chunk's upper half is the next pixel (zero weights)
   const int nK = a.nch >> 1;
   const int qmax = a.K * a.K * CC - 1;
   const int sx = a.scales[0], sw = a.scales[1];
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     const int p = threadIdx.x + 512 * i;
     const int r = p >> 3, pc = p & 7;
     const int lc = pc ^ fp8_swz(r);
-    wsrc[i] = (((lc >> 2) * a.Cout) + n0 + r) * 64 + (lc & 3) * 16;
+    wsrc[i] = (((lc >> 2) * a.Cout) + n0 + (r < BN ? r : BN - 1)) * 64 + (lc & 3) * 16;
     wdst[i] = r * 128 + pc * 16;
   }
   auto chunk_off = [&](int q) {
@@ -409,7 +411,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 
 template <int BN, int MB, int NPART, bool OB, bool OF>
 static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
-  constexpr int smem = 2 * BN * 128 + 64;
+  constexpr int WROWS = (BN * 8) % 512 == 0 ? BN : ((BN * 8 + 511) / 512 * 512) / 8;  // as in the kernel
+  constexpr int smem = 2 * WROWS * 128 + 64;
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
@@ -424,29 +427,34 @@ static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
   if (a.variant != 0) throw std::invalid_argument("conv_fwd_fp8: variant " + std::to_string(a.variant) +
                                                   " is a kernel-lab variant");
 #endif
-  if (a.variant != 5 && (BN * 128) % (16 * 512) == 0) {
-    if constexpr (BN == 192) {
-      // 0: 48 px/wave, weights read in 4 parts (production); lab: 1: 32 px/wave, 2 parts;
-      // 3: 32 px/wave, 3 parts; 4: 48 px/wave, 6 parts
-      if (a.variant == 0) launch_fp8_ga<BN, 3, 4, OB, OF>(a, st);
+  if constexpr (BN == 160) {  // value net (152 filters): L2-operand kernel only
+    if (a.variant != 0) throw std::invalid_argument("conv_fwd_fp8: 160-wide tiles have no lab variants");
+    launch_fp8_ga<160, 3, 5, OB, OF>(a, st);  // 48 px per wave, weights read in 5 parts (2 parts spill)
+  } else {
+    if (a.variant != 5 && (BN * 128) % (16 * 512) == 0) {
+      if constexpr (BN == 192) {
+        // 0: 48 px/wave, weights read in 4 parts (production); lab: 1: 32 px/wave, 2 parts;
+        // 3: 32 px/wave, 3 parts; 4: 48 px/wave, 6 parts
+        if (a.variant == 0) launch_fp8_ga<BN, 3, 4, OB, OF>(a, st);
 #ifdef AGK_KERNEL_LAB
-      else if (a.variant == 3) launch_fp8_ga<BN, 2, 3, OB, OF>(a, st);
-      else if (a.variant == 4) launch_fp8_ga<BN, 3, 6, OB, OF>(a, st);
-      else launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
+        else if (a.variant == 3) launch_fp8_ga<BN, 2, 3, OB, OF>(a, st);
+        else if (a.variant == 4) launch_fp8_ga<BN, 3, 6, OB, OF>(a, st);
+        else launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
 #endif
-    } else {
-      launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
+      } else {
+        launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
+      }
+      return;
     }
-    return;
-  }
 #ifdef AGK_KERNEL_LAB
-  constexpr int smem = 2 * (256 * 128 + BN * 128);
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_fp8_kernel<BN, OB, OF>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
-  dim3 grid((a.M + 255) / 256, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_fp8_kernel<BN, OB, OF>), grid, dim3(512), smem, st, a);
+    constexpr int smem = 2 * (256 * 128 + BN * 128);
+    static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_fp8_kernel<BN, OB, OF>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+    dim3 grid((a.M + 255) / 256, a.Cout / BN);
+    hipLaunchKernelGGL((conv_fwd_fp8_kernel<BN, OB, OF>), grid, dim3(512), smem, st, a);
 #endif
+  }
 }
 
 template <int BN>
@@ -461,7 +469,8 @@ void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
   ConvFp8Args a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
-  if (a.Cout % 192 == 0) launch_fp8_bn<192>(a, st);
+  if (a.Cout == 160) launch_fp8_bn<160>(a, st);
+  else if (a.Cout % 192 == 0) launch_fp8_bn<192>(a, st);
   else if (a.Cout % 128 == 0) launch_fp8_bn<128>(a, st);
   else launch_fp8_bn<64>(a, st);
 }

@@ -137,7 +137,9 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
   TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2 && out_scale.scalar_type() == at::kFloat, "scales");
   CHECK_F32(bias);
   const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3), nch = w.size(0), Cout = w.size(1);
-  TORCH_CHECK(Cin % 64 == 0 && Cout % 64 == 0 && nch % 2 == 0 && nch >= K * K * (Cin / 64), "channel geometry");
+  TORCH_CHECK((Cin % 64 == 0 || Cin == 160) && (Cout % 64 == 0 || Cout == 160) && nch % 2 == 0 &&
+                  nch >= K * K * ((Cin + 63) / 64),
+              "channel geometry (multiples of 64, or 160)");
   TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin, "padding/geometry mismatch");
   TORCH_CHECK(y_bf16.has_value() || y_fp8.has_value(), "need an output");
   agk::ConvFp8Args a{};

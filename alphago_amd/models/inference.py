@@ -49,7 +49,7 @@ class HipTrunkInference:
         self.S, self.L, self.K = net.board, tr.layers, list(tr.widths)
         self.C0, self.F = tr.in_planes, tr.filters
         self.C0p = ops.round_up(self.C0, 64)
-        self.Fp = ops.round_up(self.F, 64) if self.precision == "fp8" else ops.pad_filters(self.F)
+        self.Fp = ops.pad_filters(self.F)
         self.P0 = self.K[0] // 2
         self.buckets = sorted(buckets)
         self.use_graphs = use_graphs

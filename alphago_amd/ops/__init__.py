@@ -259,7 +259,8 @@ def fp8_exponent(amax: float, margin: int = 1) -> int:
 
 
 def fp8_nchunks(K: int, cin_p: int) -> int:
-    n = K * K * (cin_p // 64)
+    """64-channel e4m3 weight chunks (even count); cin_p = 160 uses three chunks per tap."""
+    n = K * K * ((cin_p + 63) // 64)
     return n + (n & 1)
 
 

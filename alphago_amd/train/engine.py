@@ -140,8 +140,8 @@ class HipConvTrainer:
         self.C0 = tr.in_planes
         self.C0p = ops.round_up(self.C0, 64)
         self.F = tr.filters
-        # fp8 kernels tile in 64-channel chunks; bf16 runs 152 filters on 160-wide tiles
-        self.Fp = ops.round_up(self.F, 64) if precision == "fp8" else ops.pad_filters(self.F)
+        # 152 filters (value net) run on 160-wide tiles, bf16 and fp8
+        self.Fp = ops.pad_filters(self.F)
         if self.F > 256:
             raise ValueError("head kernels support up to 256 filters")
         self.P0 = self.K[0] // 2

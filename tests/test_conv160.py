@@ -110,3 +110,39 @@ def test_conv_wgrad_160(ops, cuda_device, B, Cin, Cin_p, K, Pin):
     torch.cuda.synchronize()
     assert _rel_err(gw, ref_w) < 2e-3
     assert _rel_err(gb, ref_b) < 2e-3
+
+
+@pytest.mark.parametrize("B,Cin,Cin_p,K", [(5, 152, 160, 3), (3, 49, 64, 5)])
+def test_conv_fwd_fp8_160(ops, cuda_device, B, Cin, Cin_p, K):
+    """e4m3 conv with 160-channel activations (three 64-channel chunks per tap,
+    the third one's upper half reads the next pixel against zero weights) and a
+    160-wide output tile vs fp32 conv of the dequantised operands."""
+    torch.manual_seed(3)
+    S, P, Cout, Cp = 19, K // 2, 152, 160
+    x = F.relu(torch.randn(B, Cin, S, S, device=cuda_device)) * 3.0
+    w = torch.randn(Cout, Cin, K, K, device=cuda_device) * 0.05
+    b = torch.randn(Cout, device=cuda_device) * 0.1
+    bp = torch.zeros(Cp, device=cuda_device)
+    bp[:Cout] = b
+    xp = ops.to_padded(x, P, Cin_p)
+    ex = ops.fp8_exponent(float(x.abs().max()), margin=0)
+    x8 = torch.empty(xp.shape, dtype=torch.uint8, device=cuda_device)
+    ops.quantize_fp8(xp, x8, ex)
+    w8, ew = ops.pack_weights_fp8(w, Cp, Cin_p)
+    assert w8.shape[0] == ops.fp8_nchunks(K, Cin_p)
+    xq = ops.fp8_to_float(x8, ex)[:, P:P + S, P:P + S, :Cin].permute(0, 3, 1, 2)
+    wq = (w * 2.0 ** ew).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** -ew
+    ref = F.relu(F.conv2d(xq, wq, b, padding=P))
+    scales = torch.tensor([127 - ex, 127 - ew], dtype=torch.int32, device=cuda_device)
+    ey = ops.fp8_exponent(float(ref.max()), margin=0)
+    osc = torch.tensor([2.0 ** ey], device=cuda_device)
+    amax = ops.fp8_amax_buffer(1, cuda_device)[0]
+    yb = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    y8 = torch.zeros((B, S + 2, S + 2, Cp), dtype=torch.uint8, device=cuda_device)
+    ops.conv_fwd_fp8(x8, w8, bp, scales, osc, K, S, P, 1, y_bf16=yb, y_fp8=y8, amax=amax)
+    torch.cuda.synchronize()
+    out = ops.from_padded(yb, 1)
+    assert _rel_err(out[:, :Cout], ref) < 1e-2
+    assert out[:, Cout:].abs().sum() == 0
+    assert _rel_err(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1, :Cout].permute(0, 3, 1, 2), ref) < 0.07
+    assert abs(amax.view(torch.float32).max().item() - ref.max().item()) <= 1e-2 * ref.max().item()

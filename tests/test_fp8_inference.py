@@ -38,12 +38,13 @@ def test_fp8_policy_engine_matches_bf16(cuda_device):
     assert torch.allclose(e8.evaluate(x).float().cpu(), p8, atol=0.05)
 
 
-def test_fp8_value_engine_matches_bf16(cuda_device):
+@pytest.mark.parametrize("F", [192, 152])
+def test_fp8_value_engine_matches_bf16(cuda_device, F):
     from alphago_amd.models.inference import HipValueInference
     from alphago_amd.models.nets import ValueNet
 
     torch.manual_seed(1)
-    net = ValueNet(49, filters_per_layer=192, layers=4).to(cuda_device)
+    net = ValueNet(49, filters_per_layer=F, layers=4).to(cuda_device)
     e16 = HipValueInference(net, cuda_device, precision="bf16")
     e8 = HipValueInference(net, cuda_device, precision="fp8")
     x = _planes(32, 49, seed=3)
@@ -52,9 +53,11 @@ def test_fp8_value_engine_matches_bf16(cuda_device):
     assert (v8 - v16).abs().max().item() < 0.05 + 0.1 * v16.abs().max().item()
 
 
-def test_fp8_value_training_tracks_bf16(cuda_device):
+@pytest.mark.parametrize("F", [192, 152])
+def test_fp8_value_training_tracks_bf16(cuda_device, F):
     """Value-net training with the fp8 forward: gradients close to the bf16
-    trainer's, loss goes down, activation scales are updated on the device."""
+    trainer's, loss goes down, activation scales are updated on the device
+    (F = 152: 160-channel e4m3 activations, 160-wide tiles)."""
     import copy
 
     from alphago_amd.models.nets import ValueNet
@@ -62,7 +65,7 @@ def test_fp8_value_training_tracks_bf16(cuda_device):
 
     torch.manual_seed(0)
     B = 32
-    net = ValueNet(49, filters_per_layer=192, layers=4)
+    net = ValueNet(49, filters_per_layer=F, layers=4)
     net16 = copy.deepcopy(net)
     planes = _planes(B, 49, seed=5).to(cuda_device)
     z = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
