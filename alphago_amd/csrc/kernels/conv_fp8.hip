@@ -30,6 +30,10 @@ __device__ __forceinline__ int fp8_swz(int row) { return ((row >> 1) & 1) | (((r
 __device__ __forceinline__ f32x4 mfma_fp8(const i32x8& a, const i32x8& b, const f32x4& c, int sa, int sb) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
+// A e4m3 (weights), B e5m2 (gradients): the dgrad operand formats
+__device__ __forceinline__ f32x4 mfma_fp8_bf8(const i32x8& a, const i32x8& b, const f32x4& c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 1, 0, sa, 0, sb);
+}
 
 template <int BN, bool OUT_BF16, bool OUT_FP8>
 __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_kernel(ConvFp8Args a) {
@@ -210,7 +214,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_kernel(ConvFp8Args a) {
 // go through LDS, by VGPR + ds_write so the compiler's vmcnt bookkeeping stays
 // exact.  Waves own disjoint pixels (8 x 32 = 256 per workgroup) and all BN
 // channels.
-template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8>
+// DG: dgrad (e5m2 gradient operand, ReLU' mask from a.mask, no bias, max |dx|, e5m2 output)
+template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8, bool DG = false>
 __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) {
   // MB: 16-pixel blocks per wave; the BN/16 channel blocks are read from LDS in NPART parts
   constexpr int NB = BN / 16;   // 16-channel blocks per wave
@@ -335,7 +340,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 #pragma unroll
       for (int i = 0; i < NH; ++i)
 #pragma unroll
-        for (int j = 0; j < MB; ++j) acc[h * NH + i][j] = mfma_fp8(wf[i], xc[j], acc[h * NH + i][j], sw, sx);
+        for (int j = 0; j < MB; ++j)
+          acc[h * NH + i][j] = DG ? mfma_fp8_bf8(wf[i], xc[j], acc[h * NH + i][j], sw, sx)
+                                  : mfma_fp8(wf[i], xc[j], acc[h * NH + i][j], sw, sx);
       __builtin_amdgcn_s_setprio(0);
     }
     store_w((ks + 1) & 1);
@@ -366,14 +373,23 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int n = nbase + i * 16;
-      const f32x4 bb = *(const f32x4*)(a.bias + n);
       f32x4 v = acc[i][j];
-      v[0] = fmaxf(v[0] + bb[0], 0.f);
-      v[1] = fmaxf(v[1] + bb[1], 0.f);
-      v[2] = fmaxf(v[2] + bb[2], 0.f);
-      v[3] = fmaxf(v[3] + bb[3], 0.f);
+      if constexpr (DG) {
+        const bf16x4 mk = *(const bf16x4*)(a.mask + ooff + n);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (float)mk[r] > 0.f ? v[r] : 0.f;
+      } else {
+        const f32x4 bb = *(const f32x4*)(a.bias + n);
+        v[0] = fmaxf(v[0] + bb[0], 0.f);
+        v[1] = fmaxf(v[1] + bb[1], 0.f);
+        v[2] = fmaxf(v[2] + bb[2], 0.f);
+        v[3] = fmaxf(v[3] + bb[3], 0.f);
+      }
       if (!ok) continue;
-      vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+      if constexpr (DG)
+        vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+      else
+        vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
       if constexpr (OUT_BF16) {
         bf16x4 o;
         o[0] = (__bf16)v[0];
@@ -383,11 +399,20 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
         *(bf16x4*)(a.y_bf16 + ooff + n) = o;
       }
       if constexpr (OUT_FP8) {
-        const float s0 = fminf(v[0] * osc, 448.f), s1 = fminf(v[1] * osc, 448.f);
-        const float s2 = fminf(v[2] * osc, 448.f), s3 = fminf(v[3] * osc, 448.f);
-        int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
-        pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
-        *(int*)(a.y_fp8 + ooff + n) = pk;
+        if constexpr (DG) {
+          float sv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sv[r] = fminf(fmaxf(v[r] * osc, -57344.f), 57344.f);
+          int pk = __builtin_amdgcn_cvt_pk_bf8_f32(sv[0], sv[1], 0, false);
+          pk = __builtin_amdgcn_cvt_pk_bf8_f32(sv[2], sv[3], pk, true);
+          *(int*)(a.y_fp8 + ooff + n) = pk;
+        } else {
+          const float s0 = fminf(v[0] * osc, 448.f), s1 = fminf(v[1] * osc, 448.f);
+          const float s2 = fminf(v[2] * osc, 448.f), s3 = fminf(v[3] * osc, 448.f);
+          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+          pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+          *(int*)(a.y_fp8 + ooff + n) = pk;
+        }
       }
     }
   }
@@ -409,16 +434,32 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 // weights in 4 parts); kernel-lab build only: 1 / 3 / 4 = other L2-operand
 // tilings, 5 = LDS-staged conv_fwd_fp8_kernel
 
-template <int BN, int MB, int NPART, bool OB, bool OF>
+template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false>
 static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
   constexpr int WROWS = (BN * 8) % 512 == 0 ? BN : ((BN * 8 + 511) / 512 * 512) / 8;  // as in the kernel
   constexpr int smem = 2 * WROWS * 128 + 64;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF>,
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   constexpr int BM = 128 * MB;
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF>), grid, dim3(512), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG>), grid, dim3(512), smem, st, a);
+}
+
+// fp8 dgrad: production tilings only, bf16 output always (the wgrad reads it)
+template <int BN, bool OF>
+static void launch_fp8_dgrad_t(const ConvFp8Args& a, hipStream_t st) {
+  if (a.variant != 0) throw std::invalid_argument("conv_dgrad_fp8: production kernel only");
+  if constexpr (BN == 160) launch_fp8_ga<160, 3, 5, true, OF, true>(a, st);
+  else if constexpr (BN == 192) launch_fp8_ga<192, 3, 4, true, OF, true>(a, st);
+  else launch_fp8_ga<BN, 2, 2, true, OF, true>(a, st);
+}
+
+template <int BN>
+static void launch_fp8_dgrad_bn(const ConvFp8Args& a, hipStream_t st) {
+  if (a.y_bf16 == nullptr) throw std::invalid_argument("conv_dgrad_fp8: needs the bf16 output");
+  if (a.y_fp8 != nullptr) launch_fp8_dgrad_t<BN, true>(a, st);
+  else launch_fp8_dgrad_t<BN, false>(a, st);
 }
 
 template <int BN, bool OB, bool OF>
@@ -469,6 +510,13 @@ void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
   ConvFp8Args a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
+  if (a.dgrad) {
+    if (a.Cout == 160) launch_fp8_dgrad_bn<160>(a, st);
+    else if (a.Cout % 192 == 0) launch_fp8_dgrad_bn<192>(a, st);
+    else if (a.Cout % 128 == 0) launch_fp8_dgrad_bn<128>(a, st);
+    else launch_fp8_dgrad_bn<64>(a, st);
+    return;
+  }
   if (a.Cout == 160) launch_fp8_bn<160>(a, st);
   else if (a.Cout % 192 == 0) launch_fp8_bn<192>(a, st);
   else if (a.Cout % 128 == 0) launch_fp8_bn<128>(a, st);
@@ -476,11 +524,16 @@ void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
 }
 
 // ------------------------------------------------------------- packing
-// weights: fp32 OIHW [Cout_real][Cin_real][K][K] -> e4m3 [nch][Cout_p][64] * 2^e
+// weights: fp32 OIHW [Cout_real][Cin_real][K][K] -> e4m3 [nch][Cout_p][64] * 2^e, chunks over
+// the input channels.  transposed (dgrad): rows = input channels, chunks over the output
+// channels, taps flipped -- w'[ci][co][kh][kw] = w[co][ci][K-1-kh][K-1-kw]; Cout_p / Cin_p are
+// then the padded row / chunked extents.
 __global__ void pack_weights_fp8_kernel(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p,
-                                        int Cin_p, int nch, float scale, const float* scale_dev) {
+                                        int Cin_p, int nch, float scale, const float* scale_dev, int transposed) {
   const int CC = Cin_p >> 6;
   if (scale_dev) scale = *scale_dev;
+  const int rows_real = transposed ? Cin_real : Cout_real;
+  const int chans_real = transposed ? Cout_real : Cin_real;
   const long total = (long)nch * Cout_p * 64;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
     const int byte = (int)(idx & 63);
@@ -490,9 +543,11 @@ __global__ void pack_weights_fp8_kernel(const float* w, uint8_t* out, int Cout_r
     const int t = q / CC;
     const int c = (q - t * CC) * 64 + byte;
     float v = 0.f;
-    if (t < K * K && n < Cout_real && c < Cin_real) {
+    if (t < K * K && n < rows_real && c < chans_real) {
       const int kh = t / K, kw = t - (t / K) * K;
-      v = w[(((size_t)n * Cin_real + c) * K + kh) * K + kw] * scale;
+      const size_t src = transposed ? (((size_t)c * Cin_real + n) * K + (K - 1 - kh)) * K + (K - 1 - kw)
+                                    : (((size_t)n * Cin_real + c) * K + kh) * K + kw;
+      v = w[src] * scale;
       v = fminf(fmaxf(v, -448.f), 448.f);
     }
     out[idx] = (uint8_t)(__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xff);
@@ -500,12 +555,12 @@ __global__ void pack_weights_fp8_kernel(const float* w, uint8_t* out, int Cout_r
 }
 
 void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p, int Cin_p,
-                             int nch, float scale, const float* scale_dev, hipStream_t st) {
+                             int nch, float scale, const float* scale_dev, int transposed, hipStream_t st) {
   const long total = (long)nch * Cout_p * 64;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(pack_weights_fp8_kernel, dim3(blocks), dim3(256), 0, st, w, out, Cout_real, Cin_real, K, Cout_p,
-                     Cin_p, nch, scale, scale_dev);
+                     Cin_p, nch, scale, scale_dev, transposed);
 }
 
 // Per-layer weight scales, one workgroup per layer: e = floor(log2(448 / amax|w|)),
@@ -554,6 +609,56 @@ __global__ void fp8_act_scales_kernel(unsigned* amax, int* scales8, float* osc, 
 
 void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st) {
   hipLaunchKernelGGL(fp8_act_scales_kernel, dim3(1), dim3(64), 0, st, amax, scales8, osc, L, margin);
+}
+
+// Delayed gradient scaling for the fp8 dgrad chain: from this step's amax of dZ_l set the next
+// step's e5m2 exponent of dZ_l (gosc[l] = 2^e multiplies before conversion, gscales8[l][0] =
+// 127 - e is the MFMA's E8M0 dequantisation), `margin` bits of headroom; clears the amax.
+__global__ void fp8_grad_scales_kernel(unsigned* amax, int* gscales8, float* gosc, int L, int margin) {
+  const int l = threadIdx.x;
+  if (l >= L) return;
+  unsigned mu = 0u;
+  for (int k = 0; k < kFp8AmaxSlots; ++k) mu = max(mu, amax[l * kFp8AmaxSlots + k]);
+  const float m = __uint_as_float(mu);
+  int e = (m > 0.f) ? (int)floorf(log2f(57344.f / m)) - margin : 0;
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  gosc[l] = exp2f((float)e);
+  gscales8[2 * l] = 127 - e;
+  for (int k = 0; k < kFp8AmaxSlots; ++k) amax[l * kFp8AmaxSlots + k] = 0u;
+}
+
+void launch_fp8_grad_scales(unsigned* amax, int* gscales8, float* gosc, int L, int margin, hipStream_t st) {
+  hipLaunchKernelGGL(fp8_grad_scales_kernel, dim3(1), dim3(64), 0, st, amax, gscales8, gosc, L, margin);
+}
+
+// e5m2 quantisation with a device-resident scale, tracking max |x| (the head's dZ, the first
+// input of the fp8 dgrad chain)
+__global__ __launch_bounds__(256) void quantize_bf8_dev_kernel(const __bf16* x, uint8_t* y, long n4, const float* scale,
+                                                               unsigned* amax) {
+  const float sc = *scale;
+  float m = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const bf16x4 v = *(const bf16x4*)(x + 4 * i);
+    float f[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      f[r] = (float)v[r];
+      m = fmaxf(m, fabsf(f[r]));
+      f[r] = fminf(fmaxf(f[r] * sc, -57344.f), 57344.f);
+    }
+    int pk = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], 0, false);
+    pk = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], pk, true);
+    *(int*)(y + 4 * i) = pk;
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(amax + (blockIdx.x & (kFp8AmaxSlots - 1)), __float_as_uint(m));
+}
+
+void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st) {
+  const long n4 = n / 4;
+  int blocks = (int)((n4 + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(quantize_bf8_dev_kernel, dim3(blocks), dim3(256), 0, st, x, y, n4, scale, amax);
 }
 
 // e4m3 quantisation of a padded NHWC bf16 tensor (interior and borders alike: borders stay 0)

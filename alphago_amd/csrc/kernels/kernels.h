@@ -139,6 +139,11 @@ struct ConvFp8Args {
   FastDiv divSS, divS;      // filled by the launcher
   int variant;              // 0 = production (pixel operand from L2, 48 px/wave); lab: 1, 3, 4 other tilings,
                             // 5 = LDS-staged operands
+  // dgrad mode (production kernel only): x holds e5m2 gradients, w the transposed/flipped e4m3
+  // weights; the epilogue masks by mask > 0 (the forward's bf16 activation), takes no bias,
+  // tracks max |dx| and writes bf16 and/or e5m2 (out_scale) outputs
+  int dgrad;
+  const __bf16* mask;
 };
 
 // Kernel choices are explicit launch arguments (ConvFwdArgs::tile,
@@ -164,7 +169,7 @@ void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st);
 void launch_featurize(const FeaturizeArgs& a, hipStream_t st);
 void launch_conv_fwd_fp8(const ConvFp8Args& a, hipStream_t st);
 void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p, int Cin_p,
-                             int nch, float scale, const float* scale_dev, hipStream_t st);
+                             int nch, float scale, const float* scale_dev, int transposed, hipStream_t st);
 struct Fp8WeightScalesArgs {
   const float* w[kMaxPackLayers];
   int n[kMaxPackLayers];
@@ -173,6 +178,8 @@ struct Fp8WeightScalesArgs {
 };
 void launch_fp8_weight_scales(const Fp8WeightScalesArgs& a, int L, hipStream_t st);
 void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st);
+void launch_fp8_grad_scales(unsigned* amax, int* gscales8, float* gosc, int L, int margin, hipStream_t st);
+void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st);
 void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st);
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
 

@@ -273,20 +273,52 @@ void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Te
   conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, 0);
 }
 
-void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c10::optional<Tensor>& scale_dev) {
+// fp8 dgrad: dx = conv(dz (e5m2, scales[0]), flipped/transposed e4m3 weights (scales[1])) masked
+// by mask > 0; y_bf16 always, y_fp8 (e5m2, times out_scale) optional; amax = max |dx|
+void conv_dgrad_fp8(const Tensor& dz8, const Tensor& w, const Tensor& mask, const Tensor& scales,
+                    const Tensor& out_scale, const c10::optional<Tensor>& amax, const Tensor& y_bf16,
+                    const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S) {
+  conv_fwd_fp8_impl(dz8, w, out_scale, scales, out_scale, amax, y_bf16, y_fp8, K, S, 1, 1, 0, mask);
+}
+
+void fp8_grad_scales(const Tensor& amax, const Tensor& gscales8, const Tensor& gosc, int64_t margin) {
+  TORCH_CHECK(amax.scalar_type() == at::kInt && gscales8.scalar_type() == at::kInt && gosc.scalar_type() == at::kFloat,
+              "dtypes");
+  const int L = (int)(amax.numel() / agk::kFp8AmaxSlots);
+  TORCH_CHECK(amax.numel() % agk::kFp8AmaxSlots == 0 && L <= 64 && gscales8.numel() >= 2 * L && gosc.numel() >= L,
+              "sizes (amax is (L, 64))");
+  agk::launch_fp8_grad_scales(reinterpret_cast<unsigned*>(amax.data_ptr<int>()), gscales8.data_ptr<int>(),
+                              gosc.data_ptr<float>(), L, (int)margin, cur_stream());
+  launch_check("fp8_grad_scales");
+}
+
+// e5m2 quantisation with a device scale; amax (int32[64], float bits) accumulates max |x|
+void quantize_bf8(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor& amax) {
+  CHECK_BF16(x); CHECK_CONTIG(x); CHECK_DEV(x);
+  TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 4 == 0, "y");
+  TORCH_CHECK(scale.scalar_type() == at::kFloat && amax.scalar_type() == at::kInt &&
+                  amax.numel() >= agk::kFp8AmaxSlots, "scale f32[1], amax int32[64]");
+  agk::launch_quantize_bf8_dev(bfp(x), y.data_ptr<uint8_t>(), x.numel(), scale.data_ptr<float>(),
+                               reinterpret_cast<unsigned*>(amax.data_ptr<int>()), cur_stream());
+  launch_check("quantize_bf8");
+}
+
+void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c10::optional<Tensor>& scale_dev,
+                      bool transposed) {
   CHECK_F32(w); CHECK_CONTIG(w);
   TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.dim() == 3 && out.size(2) == 64, "out");
   const int K = (int)w.size(2);
   const int nch = (int)out.size(0), Cout_p = (int)out.size(1);
-  const int Cin_p = ((int)w.size(1) + 63) / 64 * 64;
-  TORCH_CHECK(nch % 2 == 0 && nch >= K * K * (Cin_p / 64) && Cout_p >= w.size(0), "packed geometry");
+  // chunked extent: input channels, or output channels for the transposed (dgrad) packing
+  const int Cin_p = ((int)w.size(transposed ? 0 : 1) + 63) / 64 * 64;
+  TORCH_CHECK(nch % 2 == 0 && nch >= K * K * (Cin_p / 64) && Cout_p >= w.size(transposed ? 1 : 0), "packed geometry");
   const float* sd = nullptr;
   if (scale_dev.has_value()) {
     CHECK_F32(*scale_dev);
     sd = scale_dev->data_ptr<float>();
   }
   agk::launch_pack_weights_fp8(w.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)w.size(0), (int)w.size(1), K, Cout_p,
-                               Cin_p, nch, (float)scale, sd, cur_stream());
+                               Cin_p, nch, (float)scale, sd, transposed ? 1 : 0, cur_stream());
   launch_check("pack_weights_fp8");
 }
 
@@ -463,7 +495,11 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
       "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po) -> ()");
-  m.def("pack_weights_fp8(Tensor w, Tensor(a!) out, float scale, Tensor? scale_dev) -> ()");
+  m.def("pack_weights_fp8(Tensor w, Tensor(a!) out, float scale, Tensor? scale_dev, bool transposed=False) -> ()");
+  m.def("conv_dgrad_fp8(Tensor dz8, Tensor w, Tensor mask, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
+        "Tensor(b!) y_bf16, Tensor(c!)? y_fp8, int K, int S) -> ()");
+  m.def("fp8_grad_scales(Tensor(a!) amax, Tensor(b!) gscales8, Tensor(c!) gosc, int margin) -> ()");
+  m.def("quantize_bf8(Tensor x, Tensor(a!) y, Tensor scale, Tensor(b!) amax) -> ()");
   m.def("fp8_weight_scales(Tensor[] ws, Tensor(a!) wscale, Tensor(b!) scales8) -> ()");
   m.def("fp8_act_scales(Tensor(a!) amax, Tensor(b!) scales8, Tensor(c!) osc, int margin) -> ()");
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
@@ -501,6 +537,9 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("featurize", &featurize);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8);
   m.impl("pack_weights_fp8", &pack_weights_fp8);
+  m.impl("conv_dgrad_fp8", &conv_dgrad_fp8);
+  m.impl("fp8_grad_scales", &fp8_grad_scales);
+  m.impl("quantize_bf8", &quantize_bf8);
   m.impl("fp8_weight_scales", &fp8_weight_scales);
   m.impl("fp8_act_scales", &fp8_act_scales);
   m.impl("quantize_fp8", &quantize_fp8);

@@ -130,12 +130,15 @@ inline void conv_wgrad_impl(const Tensor& x, const Tensor& dz, const Tensor& sla
 inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales,
                               const Tensor& out_scale, const c10::optional<Tensor>& amax,
                               const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K,
-                              int64_t S, int64_t Pin, int64_t Po, int variant) {
+                              int64_t S, int64_t Pin, int64_t Po, int variant,
+                              const c10::optional<Tensor>& dgrad_mask = c10::nullopt) {
+  // dgrad_mask given: fp8 dgrad (x = e5m2 gradients, w = transposed e4m3 weights, output masked
+  // by dgrad_mask > 0, no bias, e5m2 y_fp8)
   CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.scalar_type() == at::kByte && w.scalar_type() == at::kByte, "fp8 tensors are stored as uint8");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 3 && w.size(2) == 64, "x (B,HP,HP,C), w (nch, Cout, 64)");
   TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2 && out_scale.scalar_type() == at::kFloat, "scales");
-  CHECK_F32(bias);
+  if (!dgrad_mask.has_value()) CHECK_F32(bias);
   const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3), nch = w.size(0), Cout = w.size(1);
   TORCH_CHECK((Cin % 64 == 0 || Cin == 160) && (Cout % 64 == 0 || Cout == 160) && nch % 2 == 0 &&
                   nch >= K * K * ((Cin + 63) / 64),
@@ -144,7 +147,8 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
   TORCH_CHECK(y_bf16.has_value() || y_fp8.has_value(), "need an output");
   agk::ConvFp8Args a{};
   a.variant = variant;
-  a.x = x.data_ptr<uint8_t>(); a.w = w.data_ptr<uint8_t>(); a.bias = bias.data_ptr<float>();
+  a.x = x.data_ptr<uint8_t>(); a.w = w.data_ptr<uint8_t>();
+  a.bias = dgrad_mask.has_value() ? nullptr : bias.data_ptr<float>();
   a.scales = scales.data_ptr<int>(); a.out_scale = out_scale.data_ptr<float>();
   const int64_t HPo = S + 2 * Po;
   if (y_bf16.has_value()) {
@@ -164,6 +168,13 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
   }
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
   a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po; a.nch = (int)nch;
+  if (dgrad_mask.has_value()) {
+    CHECK_BF16(*dgrad_mask); CHECK_CONTIG(*dgrad_mask);
+    TORCH_CHECK(y_bf16.has_value() && dgrad_mask->sizes() == y_bf16->sizes(), "dgrad: mask must match y_bf16");
+    TORCH_CHECK(variant == 0, "dgrad: production kernel only");
+    a.dgrad = 1;
+    a.mask = bfp(*dgrad_mask);
+  }
   TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31), "tensor too large for int32 offsets");
   if (a.M == 0) return;
   agk::launch_conv_fwd_fp8(a, cur_stream());

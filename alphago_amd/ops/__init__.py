@@ -274,9 +274,33 @@ def pack_weights_fp8(w_oihw: torch.Tensor, cout_p: int, cin_p: int, exponent=Non
     return out, exponent
 
 
-def pack_weights_fp8_into(w_oihw: torch.Tensor, out: torch.Tensor, scale_dev: torch.Tensor):
-    """Re-pack into an existing buffer with a device-resident scale (no host sync)."""
-    _ops().pack_weights_fp8(w_oihw, out, 1.0, scale_dev)
+def pack_weights_fp8_into(w_oihw: torch.Tensor, out: torch.Tensor, scale_dev: torch.Tensor, transposed: bool = False):
+    """Re-pack into an existing buffer with a device-resident scale (no host sync); ``transposed``:
+    the dgrad weights (rows = input channels, chunks over output channels, taps flipped)."""
+    _ops().pack_weights_fp8(w_oihw, out, 1.0, scale_dev, transposed)
+
+
+def conv_dgrad_fp8(dz8, w8t, mask, scales, out_scale, K: int, S: int, y_bf16, y_fp8=None, amax=None):
+    """fp8 dgrad: dx = conv(dz8 (e5m2, E8M0 scale scales[0]), w8t (transposed e4m3, scales[1]))
+    masked by mask > 0 (bf16 activation of the layer below); bf16 y_bf16 and optional e5m2
+    y_fp8 (x out_scale); amax accumulates max |dx|."""
+    _ops().conv_dgrad_fp8(dz8, w8t, mask, scales, out_scale, amax, y_bf16, y_fp8, K, S)
+
+
+def fp8_grad_scales(amax, gscales8, gosc, margin: int = 1):
+    """Delayed e5m2 gradient scaling: gosc[l] = 2^e, gscales8[l, 0] = 127 - e from amax[l] (cleared)."""
+    _ops().fp8_grad_scales(amax, gscales8, gosc, margin)
+
+
+def quantize_bf8(x_bf16: torch.Tensor, out: torch.Tensor, scale_dev: torch.Tensor, amax: torch.Tensor):
+    """e5m2 quantisation (x * scale_dev[0]) with max |x| accumulated into amax (int32[64])."""
+    _ops().quantize_bf8(x_bf16, out, scale_dev, amax)
+    return out
+
+
+def bf8_to_float(t_u8: torch.Tensor, exponent: int = 0) -> torch.Tensor:
+    """Decode e5m2 bytes (and undo a 2^exponent scale)."""
+    return t_u8.view(torch.float8_e5m2).float() * (2.0 ** -exponent)
 
 
 def fp8_weight_scales(ws, wscale, scales8):

@@ -8,13 +8,16 @@ fixed sequence of hand-written kernels over preallocated buffers:
   L x conv_fwd (implicit GEMM on MFMA, fused bias+ReLU)
   policy_head (1x1 conv + softmax + clipped CE + top-1 + head backward)
   for l = L..1:
-     [wgrad stream]  conv_wgrad(l) -> split slab -> reduce into the flat fp32 grad
-                     -> async RCCL all-reduce of the bucket once complete
-     [main stream]   conv_fwd in dgrad mode (flipped weights, ReLU' mask fused)
+     conv_wgrad(l) -> split slab -> reduce into the flat fp32 grad
+        -> async RCCL all-reduce of the bucket once complete (RCCL's own stream)
+     conv_fwd in dgrad mode (flipped weights, ReLU' mask fused)
   sgd (flat fp32 master) + pack_weights (bf16 forward and dgrad copies)
 
-dgrad and wgrad of a layer are independent and run on two HIP streams; the
-gradient all-reduce of a bucket overlaps the remaining backward.  Every
+The gradient all-reduce of a bucket overlaps the remaining backward.  dgrad
+and wgrad of a layer are independent; ``overlap=True`` runs the wgrad on a
+second HIP stream, but on MI355X the two big-LDS kernels then split the CUs
+and the step is slower (alternating A/B, scripts/overlap_ab.sh: SL 118.7k vs
+120.3k, value 131.2k vs 136.8k positions/s), so the default is serial.  Every
 activation and gradient has its own buffer (HBM is plentiful: ~2 GB at
 batch 512), so there are no cross-stream reuse hazards.
 
@@ -118,8 +121,8 @@ class HipConvTrainer:
     """MFMA conv-trunk training engine; subclasses provide the head."""
 
     def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
-                 overlap: bool = True, wgrad_target_wgs: int = 512, iterations: int = 0, precision: str = "bf16",
-                 wgrad_priority: Optional[int] = None, conv_tile: int = 0):
+                 overlap: bool = False, wgrad_target_wgs: int = 512, iterations: int = 0, precision: str = "bf16",
+                 wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: bool = False):
         ops.load()
         self.conv_tile = conv_tile  # forward/dgrad tiling: 0 = automatic, or 128 / 256 / 384
         if precision not in ("bf16", "fp8"):
@@ -229,6 +232,19 @@ class HipConvTrainer:
             self.X08 = torch.zeros(self.X0.shape, dtype=torch.uint8, device=dev)
             self.Y8 = [torch.zeros(self.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(2)]
             self._fp8_calibrated = False
+            # fp8 dgrad (opt-in): e5m2 gradients x transposed e4m3 weights; per-layer delayed
+            # gradient scales from the max |dZ| of the previous step (the first step runs bf16
+            # dgrads and calibrates them).  The kernel is faster than the bf16 dgrad (213 vs
+            # 253 us per 3x3 layer at B=1024), but the e5m2 quantisation pass and the transposed
+            # weight packs eat the gain: value training 142.2k vs 143.5k positions/s
+            self.fp8_dgrad = fp8_dgrad
+            self.wd8 = [None] + [torch.zeros((ops.fp8_nchunks(self.K[l], self.Fp), self.Fp, 64), dtype=torch.uint8,
+                                             device=dev) for l in range(1, L)]
+            self.gscales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
+            self.gosc8 = torch.ones(L, device=dev)
+            self.gamax8 = ops.fp8_amax_buffer(L, dev)
+            self.DZ8 = [torch.zeros(self.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self._g8_calibrated = False
         # Keras-SGD schedule mirrored on the device (float64 {lr0, decay, iterations, lr}) so that
         # the SGD step reads its learning rate from memory: the whole step is graph-capturable
         self._sched_dev = torch.zeros(4, dtype=torch.float64, device=dev)
@@ -281,6 +297,10 @@ class HipConvTrainer:
             ops.fp8_weight_scales(ws, self.wscale8, self.scales8)
             for l in range(self.L):
                 ops.pack_weights_fp8_into(ws[l], self.w8[l], self.wscale8[l:l + 1])
+            if self.fp8_dgrad:
+                for l in range(1, self.L):
+                    ops.pack_weights_fp8_into(ws[l], self.wd8[l], self.wscale8[l:l + 1], transposed=True)
+                self.gscales8[:, 1].copy_(self.scales8[:, 1])
 
     def _layer_in(self, l):
         return (self.X0, self.P0) if l == 0 else (self.Y[l - 1], 1)
@@ -352,16 +372,36 @@ class HipConvTrainer:
                 if red and l in self._bucket_after_layer:
                     self.reducer.launch(self._bucket_after_layer[l])
             if l > 0:
-                if self.precision == "fp8":  # the fp8 forward does not write bitmasks
+                if self.precision == "fp8" and self.fp8_dgrad and self._g8_calibrated:
+                    if l == self.L - 1:  # the head's dZ enters the e5m2 chain
+                        ops.quantize_bf8(self.DZ[l], self.DZ8[l % 2], self.gosc8[l:l + 1], self.gamax8[l])
+                    ops.conv_dgrad_fp8(self.DZ8[l % 2], self.wd8[l], self.Y[l - 1], self.gscales8[l],
+                                       self.gosc8[l - 1:l], self.K[l], self.S, self.DZ[l - 1],
+                                       y_fp8=self.DZ8[(l - 1) % 2] if l > 1 else None, amax=self.gamax8[l - 1])
+                elif self.precision == "fp8":  # the fp8 forward does not write bitmasks
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASK, mask=self.Y[l - 1])
                 else:
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=self.conv_tile)
+        if self.precision == "fp8" and self.fp8_dgrad:
+            if self._g8_calibrated:
+                ops.fp8_grad_scales(self.gamax8, self.gscales8, self.gosc8, 1)  # next step's gradient scales
+            else:
+                self._fp8_grad_calibrate()
         if self.s_w is not None:
             main.wait_stream(self.s_w)
         if red:
             self.reducer.wait()
+
+    @torch.no_grad()
+    def _fp8_grad_calibrate(self) -> None:
+        """First backward (bf16 dgrads): e5m2 scales of dZ_1..dZ_{L-1} from this step's max |dZ|."""
+        amax = torch.stack([self.DZ[l].abs().amax().float() for l in range(self.L)])
+        self.gamax8.zero_()
+        self.gamax8[:, 0].copy_(amax.view(torch.int32))
+        ops.fp8_grad_scales(self.gamax8, self.gscales8, self.gosc8, 1)
+        self._g8_calibrated = True
 
     def compute_grads(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None,
                       weight: Optional[torch.Tensor] = None, reduce: bool = True):

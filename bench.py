@@ -50,7 +50,8 @@ def main():
     ap.add_argument("--lr", type=float, default=0.003)
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
     ap.add_argument("--pool", type=int, default=16384, help="synthetic positions resident on device")
-    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--overlap", action="store_true",
+                    help="run the wgrad on a second stream beside the dgrad (slower on MI355X; default serial)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                     help="conv forward precision (fp8 = e4m3 block-scaled MFMA forward, bf16 backward)")
     ap.add_argument("--graph", action="store_true", help="run each training step as a HIP-graph replay")
@@ -66,7 +67,7 @@ def main():
     dev = env.device
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
-    kw = {} if args.backend == "torch" else {"overlap": not args.no_overlap, "precision": args.precision,
+    kw = {} if args.backend == "torch" else {"overlap": args.overlap, "precision": args.precision,
                                              "wgrad_target_wgs": args.wgrad_wgs, "conv_tile": args.conv_tile}
     trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
     if args.graph:

@@ -36,12 +36,15 @@ def main():
     ap.add_argument("--pool", type=int, default=8192)
     ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 128, 256, 384],
                     help="forward/dgrad conv tiling (0 = automatic)")
+    ap.add_argument("--overlap", action="store_true", help="wgrad on a second stream beside the dgrad")
+    ap.add_argument("--fp8-dgrad", action="store_true", help="fp8 precision: e5m2 x e4m3 dgrad too")
     a = ap.parse_args()
     env = agdist.init_from_env()
     dev = env.device
     torch.manual_seed(7 + env.rank)
     net = ValueNet(49, filters_per_layer=a.filters, layers=a.layers)
-    kw = {"precision": a.precision, "conv_tile": a.conv_tile} if dev.type == "cuda" else {}
+    kw = ({"precision": a.precision, "conv_tile": a.conv_tile, "overlap": a.overlap,
+           "fp8_dgrad": a.fp8_dgrad} if dev.type == "cuda" else {})
     tr = make_value_trainer(net, a.batch, lr=0.003, decay=8.664e-8, device=dev, **kw)
     g = torch.Generator(device=dev).manual_seed(11 + env.rank)
     pool = torch.randint(0, 2, (a.pool, 49, 19, 19), dtype=torch.uint8, device=dev, generator=g)

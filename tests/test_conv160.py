@@ -146,3 +146,39 @@ def test_conv_fwd_fp8_160(ops, cuda_device, B, Cin, Cin_p, K):
     assert out[:, Cout:].abs().sum() == 0
     assert _rel_err(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1, :Cout].permute(0, 3, 1, 2), ref) < 0.07
     assert abs(amax.view(torch.float32).max().item() - ref.max().item()) <= 1e-2 * ref.max().item()
+
+
+@pytest.mark.parametrize("C,Cp", [(152, 160), (192, 192)])
+def test_conv_dgrad_fp8(ops, cuda_device, C, Cp):
+    """fp8 dgrad (e5m2 gradients x transposed e4m3 weights on the block-scaled MFMA)
+    masked by the bf16 activation vs fp32 conv2d_input of the dequantised operands."""
+    torch.manual_seed(4)
+    B, S, K = 3, 19, 3
+    dz = torch.randn(B, C, S, S, device=cuda_device) * 1e-3
+    w = torch.randn(C, C, K, K, device=cuda_device) * 0.05
+    yprev = _bf(torch.randn(B, C, S, S, device=cuda_device)).clamp_min(0)
+    amax_in = ops.fp8_amax_buffer(1, cuda_device)[0]
+    eg = ops.fp8_exponent(float(dz.abs().max()), margin=0) + 7  # e5m2 max 57344 = 448 * 2^7
+    dzp = ops.to_padded(dz, 1, Cp)
+    dz8 = torch.empty(dzp.shape, dtype=torch.uint8, device=cuda_device)
+    ops.quantize_bf8(dzp, dz8, torch.tensor([2.0 ** eg], device=cuda_device), amax_in)
+    assert abs(amax_in.view(torch.float32).max().item() - _bf(dz).abs().max().item()) < 1e-6
+    ew = ops.fp8_exponent(float(w.abs().max()), margin=0)
+    w8t = torch.zeros((ops.fp8_nchunks(K, Cp), Cp, 64), dtype=torch.uint8, device=cuda_device)
+    ops.pack_weights_fp8_into(w, w8t, torch.tensor([2.0 ** ew], device=cuda_device), transposed=True)
+    dzq = ops.bf8_to_float(dz8, eg)[:, 1:S + 1, 1:S + 1, :C].permute(0, 3, 1, 2)
+    wq = (w * 2.0 ** ew).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** -ew
+    ref = torch.nn.grad.conv2d_input((B, C, S, S), wq, dzq, padding=K // 2) * (yprev > 0)
+    scales = torch.tensor([127 - eg, 127 - ew], dtype=torch.int32, device=cuda_device)
+    ey = ops.fp8_exponent(float(ref.abs().max()), margin=0) + 7
+    osc = torch.tensor([2.0 ** ey], device=cuda_device)
+    amax = ops.fp8_amax_buffer(1, cuda_device)[0]
+    dx = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    dx8 = torch.zeros((B, S + 2, S + 2, Cp), dtype=torch.uint8, device=cuda_device)
+    ops.conv_dgrad_fp8(dz8, w8t, ops.to_padded(yprev, 1, Cp), scales, osc, K, S, dx, y_fp8=dx8, amax=amax)
+    torch.cuda.synchronize()
+    out = ops.from_padded(dx, 1)
+    assert _rel_err(out[:, :C], ref) < 1e-2
+    assert out[:, C:].abs().sum() == 0
+    assert _rel_err(ops.bf8_to_float(dx8, ey)[:, 1:S + 1, 1:S + 1, :C].permute(0, 3, 1, 2), ref) < 0.13
+    assert abs(amax.view(torch.float32).max().item() - ref.abs().max().item()) <= 1e-2 * ref.abs().max().item()

@@ -53,11 +53,12 @@ def test_fp8_value_engine_matches_bf16(cuda_device, F):
     assert (v8 - v16).abs().max().item() < 0.05 + 0.1 * v16.abs().max().item()
 
 
-@pytest.mark.parametrize("F", [192, 152])
-def test_fp8_value_training_tracks_bf16(cuda_device, F):
+@pytest.mark.parametrize("F,fp8_dgrad", [(192, False), (152, False), (152, True)])
+def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad):
     """Value-net training with the fp8 forward: gradients close to the bf16
     trainer's, loss goes down, activation scales are updated on the device
-    (F = 152: 160-channel e4m3 activations, 160-wide tiles)."""
+    (F = 152: 160-channel e4m3 activations, 160-wide tiles; fp8_dgrad: e5m2 x e4m3
+    dgrad from the second step on, after the first step calibrated its scales)."""
     import copy
 
     from alphago_amd.models.nets import ValueNet
@@ -69,7 +70,7 @@ def test_fp8_value_training_tracks_bf16(cuda_device, F):
     net16 = copy.deepcopy(net)
     planes = _planes(B, 49, seed=5).to(cuda_device)
     z = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
-    t8 = HipValueTrainer(net, B, lr=0.05, device=cuda_device, precision="fp8")
+    t8 = HipValueTrainer(net, B, lr=0.05, device=cuda_device, precision="fp8", fp8_dgrad=fp8_dgrad)
     t16 = HipValueTrainer(net16, B, lr=0.05, device=cuda_device)
     t8.compute_grads(planes, z)
     t16.compute_grads(planes, z)
@@ -77,6 +78,14 @@ def test_fp8_value_training_tracks_bf16(cuda_device, F):
         a, b = t8.fp.grad_views[name], t16.fp.grad_views[name]
         cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
         assert cos > 0.9, (name, cos)
+    if fp8_dgrad:  # second backward on the e5m2 path, same weights as the bf16 trainer
+        t8.compute_grads(planes, z)
+        t16.compute_grads(planes, z)
+        for name in t8.fp.names:
+            a, b = t8.fp.grad_views[name], t16.fp.grad_views[name]
+            cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
+            assert cos > 0.9, (name, cos)
+        assert (t8.gscales8[1:, 0] != 127).all()  # gradient exponents calibrated
     l0 = t8.evaluate(planes, z)[0].item()
     for _ in range(15):
         t8.step(planes, z)
