@@ -269,8 +269,10 @@ PYBIND11_MODULE(_engine, m) {
                 }
                 s.ko = pm[2 * i];
                 const int me = pm[2 * i + 1];
+                const int budget = ladder_budget();
                 for (int p = 0; p < np; ++p)
-                  po[i * np + p] = lb::is_candidate(s, p, me, g) ? (uint8_t)lb::ladder_bits_at(s, p, me, stack, g) : 0;
+                  po[i * np + p] =
+                      lb::is_candidate(s, p, me, g) ? (uint8_t)lb::ladder_bits_at(s, p, me, stack, g, budget) : 0;
               }
             });
           for (auto& th : pool) th.join();
@@ -278,6 +280,9 @@ PYBIND11_MODULE(_engine, m) {
         return out;
       },
       py::arg("board"), py::arg("meta"), py::arg("n"), py::arg("threads") = 8);
+  m.def("set_ladder_budget", &set_ladder_budget, py::arg("visits"),
+        "node budget of one ladder capture / escape read (CPU, bitboard and GPU readers); 0 = default");
+  m.def("ladder_budget", &ladder_budget);
 
   bind_mcts(m);
   bind_lzf(m);

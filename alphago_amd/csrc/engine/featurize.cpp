@@ -1,6 +1,10 @@
 #include "featurize.h"
 
+#include <atomic>
 #include <cstring>
+#include <utility>
+
+#include "ladder_bb.h"
 
 namespace ag {
 
@@ -21,6 +25,16 @@ int feature_id(const std::string& name) {
 // ---------------------------------------------------------------- ladders
 static constexpr int kLadderDepth = 96;  // plies; a corner-to-corner ladder is < 80
 
+// Node budget per capture / escape test (lb::kLadderVisits, ladder_bb.h: the
+// same rule in the bitboard and GPU readers): each prey_loses / hunter_wins
+// call is one visit; past the budget a node gives up like one past
+// kLadderDepth.  Runtime-settable for tests (set_ladder_budget).
+static std::atomic<int> g_ladder_budget{lb::kLadderVisits};
+static thread_local int t_ladder_visits = 0;
+
+void set_ladder_budget(int visits) { g_ladder_budget.store(visits > 0 ? visits : lb::kLadderVisits); }
+int ladder_budget() { return g_ladder_budget.load(std::memory_order_relaxed); }
+
 static bool hunter_wins(const GameState& s, int prey, int depth);
 
 // Per-thread scratch states, one per ladder ply: copy-assigning into a reused
@@ -33,26 +47,42 @@ static GameState& ladder_slot(int depth) {
 
 // prey to move, prey group in atari.  True if every prey reply loses.
 static bool prey_loses(const GameState& s, int prey, int depth) {
+  if (++t_ladder_visits > ladder_budget()) return false;
   if (depth > kLadderDepth) return false;
   const int pc = s.board[prey];
   int16_t cand[8];
   int nc = 0;
   int h = s.head[prey];
   cand[nc++] = (int16_t)s.libs[h].first();
-  // captures of adjacent hunter groups in atari
+  // captures of adjacent hunter groups in atari, in the order of each group's
+  // lowest stone index next to the prey chain (the bitboard reader's order,
+  // ladder_bb.h: the node budget then cuts both searches at the same node)
+  int gkey[64], ghead[64], ng = 0;
   int st = prey;
   do {
     for (int i = 0; i < s.g->nnbr[st]; ++i) {
       int q = s.g->nbr[st][i];
       if (s.board[q] == -pc && s.libc[s.head[q]] == 1) {
-        int l = s.libs[s.head[q]].first();
-        bool dup = false;
-        for (int j = 0; j < nc; ++j) dup |= (cand[j] == l);
-        if (!dup && nc < 8) cand[nc++] = (int16_t)l;
+        const int hq = s.head[q];
+        int j = 0;
+        while (j < ng && ghead[j] != hq) ++j;
+        if (j < ng) gkey[j] = q < gkey[j] ? q : gkey[j];
+        else if (ng < 64) { ghead[ng] = hq; gkey[ng] = q; ++ng; }
       }
     }
     st = s.next[st];
   } while (st != prey);
+  for (int a = 1; a < ng; ++a)  // insertion sort by key (few groups)
+    for (int b = a; b > 0 && gkey[b] < gkey[b - 1]; --b) {
+      std::swap(gkey[b], gkey[b - 1]);
+      std::swap(ghead[b], ghead[b - 1]);
+    }
+  for (int j = 0; j < ng; ++j) {
+    const int l = s.libs[ghead[j]].first();
+    bool dup = false;
+    for (int k = 0; k < nc; ++k) dup |= (cand[k] == l);
+    if (!dup && nc < 8) cand[nc++] = (int16_t)l;
+  }
   for (int k = 0; k < nc; ++k) {
     int mv = cand[k];
     if (mv < 0 || !s.is_legal_for(mv, pc)) continue;
@@ -69,6 +99,7 @@ static bool prey_loses(const GameState& s, int prey, int depth) {
 
 // hunter to move against the prey group.
 static bool hunter_wins(const GameState& s, int prey, int depth) {
+  if (++t_ladder_visits > ladder_budget()) return false;
   if (depth > kLadderDepth) return false;
   const int pc = s.board[prey];
   int h = s.head[prey];
@@ -92,6 +123,7 @@ static bool hunter_wins(const GameState& s, int prey, int depth) {
 
 bool ladder_capture_at(const GameState& s, int m) {
   if (!s.is_legal(m)) return false;
+  t_ladder_visits = 0;
   const int me = s.current_player;
   for (int i = 0; i < s.g->nnbr[m]; ++i) {
     int q = s.g->nbr[m][i];
@@ -107,6 +139,7 @@ bool ladder_capture_at(const GameState& s, int m) {
 
 bool ladder_escape_at(const GameState& s, int m) {
   if (!s.is_legal(m)) return false;
+  t_ladder_visits = 0;
   const int me = s.current_player;
   for (int i = 0; i < s.g->nnbr[m]; ++i) {
     int q = s.g->nbr[m][i];

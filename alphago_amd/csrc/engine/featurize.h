@@ -48,5 +48,8 @@ void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* met
 // preprocessing.py:147-152).  Exposed for tests.
 bool ladder_capture_at(const GameState& s, int move);
 bool ladder_escape_at(const GameState& s, int move);
+// node budget of one capture / escape read (default lb::kLadderVisits); 0 restores the default
+void set_ladder_budget(int visits);
+int ladder_budget();
 
 }  // namespace ag

@@ -44,6 +44,13 @@ constexpr int kMaxCand = 8;
 #endif
 constexpr int kMaxSteps = LB_MAX_STEPS;
 constexpr int kBudgetHit = 4;  // ladder_bits_at bit: budget exhausted (result unknown)
+// Node budget per root read (one capture or one escape test of a point): every
+// prey_loses / hunter_wins node counts one visit; past the budget a node gives
+// up like one past kLadderDepth (prey survives).  Same rule, and the same
+// candidate order, in featurize.cpp.  No read of 3448 random positions (~62k
+// roots) is cut at 4096 (one is at 2048); the budget bounds the rare
+// exponential searches that stalled whole MCTS encode batches.
+constexpr int kLadderVisits = 4096;
 
 struct BB {
   uint64_t w[W];
@@ -261,9 +268,10 @@ struct Frame {
 
 // Returns the first `res` of a new frame when it is decided without search
 // (1 = hunter wins / prey loses, 0 = not), else -1 after filling the frame.
-LB_HD int frame_init(Frame& f, const LState& st, const Geo& g) {
+LB_HD int frame_init(Frame& f, const LState& st, const Geo& g, int& visits, int budget) {
   f.k = 0;
   f.nc = 0;
+  if (++visits > budget) return 0;       // node budget spent: give up, prey survives
   if (f.depth > kLadderDepth) return 0;  // both give up: prey survives
   const int pc = color_at(st, f.prey);
   const BB grp = group_of(st, f.prey, g);
@@ -306,10 +314,10 @@ LB_HD int frame_init(Frame& f, const LState& st, const Geo& g) {
 // in registers; a frame's snapshot is written only when a child is pushed and
 // read back only when the search returns to that frame.
 template <class Stack>
-LB_HD int ladder_eval(Stack& stack, const Geo& g) {
+LB_HD int ladder_eval(Stack& stack, const Geo& g, int& visits, int budget) {
   int top = 0;
   LState cur = stack[0].s;
-  int res = frame_init(stack[0], cur, g);
+  int res = frame_init(stack[0], cur, g, visits, budget);
   if (res >= 0) return res;
   res = -1;
   bool reload = false;
@@ -351,7 +359,7 @@ LB_HD int ladder_eval(Stack& stack, const Geo& g) {
       c.prey = prey;
       c.kind = kind == F_HUNTER ? F_PREY : F_HUNTER;
       c.depth = f.depth + 1;
-      const int r = frame_init(c, ns, g);
+      const int r = frame_init(c, ns, g, visits, budget);
       if (r >= 0) {
         if (kind == F_HUNTER && r == 1) ret = 1;
         if (kind == F_PREY && r == 0) ret = 0;
@@ -377,8 +385,9 @@ LB_HD int ladder_eval(Stack& stack, const Geo& g) {
 // featurize.cpp ladder_capture_at / ladder_escape_at on a root state whose
 // player to move is `me`; bit 0 = capture, bit 1 = escape.
 template <class Stack>
-LB_HD int ladder_bits_at(const LState& s, int m, int me, Stack& stack, const Geo& g) {
+LB_HD int ladder_bits_at(const LState& s, int m, int me, Stack& stack, const Geo& g, int budget = kLadderVisits) {
   if (!is_legal_for(s, m, me, g)) return 0;
+  int visits = 0;  // per capture test, then per escape test (featurize.cpp resets per call)
   int nb[4];
   neighbours(m, g, nb);
   int out = 0;
@@ -394,10 +403,11 @@ LB_HD int ladder_bits_at(const LState& s, int m, int me, Stack& stack, const Geo
     f.prey = q;
     f.kind = F_PREY;
     f.depth = 0;
-    const int r = ladder_eval(stack, g);
+    const int r = ladder_eval(stack, g, visits, budget);
     if (r == -2) return out | kBudgetHit;
     if (r == 1) out |= 1;
   }
+  visits = 0;
   for (int i = 0; i < 4 && !(out & 2); ++i) {  // escape
     const int q = nb[i];
     if (q < 0 || color_at(s, q) != me || prey_libcount(s, q, g) != 1) continue;
@@ -412,7 +422,7 @@ LB_HD int ladder_bits_at(const LState& s, int m, int me, Stack& stack, const Geo
     f.prey = q;
     f.kind = F_HUNTER;
     f.depth = 0;
-    const int r = ladder_eval(stack, g);
+    const int r = ladder_eval(stack, g, visits, budget);
     if (r == -2) return out | kBudgetHit;
     if (r == 0) out |= 2;
   }

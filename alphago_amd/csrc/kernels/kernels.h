@@ -211,6 +211,7 @@ struct LadderArgs {
   const int32_t* offsets;  // [B] exclusive prefix sum of counts
   int32_t* counter;        // zeroed task counter of the search kernel
   void* frames;            // search threads x ladder_frame_bytes() (frame stacks)
+  int budget;              // node visits per capture / escape read (lb::kLadderVisits)
   uint8_t* out;            // [B][S*S] zeroed; bit 0 = ladder capture, bit 1 = ladder escape
   int B, S;
 };

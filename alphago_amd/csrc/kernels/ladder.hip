@@ -111,7 +111,7 @@ __global__ __launch_bounds__(64) void ladder_search_kernel(LadderArgs a) {
       s.white.w[k] = bd.white[k];
     }
     s.ko = bd.ko;
-    a.out[(size_t)b * np + p] = (uint8_t)lb::ladder_bits_at(s, p, bd.me, stack, g);
+    a.out[(size_t)b * np + p] = (uint8_t)lb::ladder_bits_at(s, p, bd.me, stack, g, a.budget);
   }
 }
 

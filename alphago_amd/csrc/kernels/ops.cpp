@@ -411,7 +411,7 @@ void dense_f32(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bi
 
 // Ladder planes from the compact board encoding: out (B, S*S) uint8, bit 0 =
 // ladder capture, bit 1 = ladder escape (the encoder's CPU ladder bits).
-void ladder_planes(const Tensor& board, const Tensor& meta, const Tensor& out, int64_t S) {
+void ladder_planes(const Tensor& board, const Tensor& meta, const Tensor& out, int64_t S, int64_t budget) {
   CHECK_DEV(board); CHECK_DEV(meta); CHECK_DEV(out);
   TORCH_CHECK(board.scalar_type() == at::kChar && board.dim() == 2 && board.size(1) == S * S && board.is_contiguous(),
               "board int8 (B, S*S)");
@@ -431,6 +431,8 @@ void ladder_planes(const Tensor& board, const Tensor& meta, const Tensor& out, i
   a.out = out.data_ptr<uint8_t>();
   a.B = (int)B;
   a.S = (int)S;
+  TORCH_CHECK(budget > 0, "ladder budget must be positive");
+  a.budget = (int)budget;
   a.counter = a.counts + B;
   out.zero_();
   counts.zero_();
@@ -488,7 +490,8 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
   m.def("sgd_update_sched(Tensor(a!) p, Tensor g, Tensor(b!) sched, float gscale) -> ()");
   m.def("dense_f32(Tensor A, Tensor B, Tensor? bias, Tensor(a!) C, bool transA, bool transB, float beta) -> ()");
-  m.def("ladder_planes(Tensor board, Tensor meta, Tensor(a!) out, int S) -> ()");
+  // budget: node visits per capture / escape read; 4096 = lb::kLadderVisits (ladder_bb.h)
+  m.def("ladder_planes(Tensor board, Tensor meta, Tensor(a!) out, int S, int budget=4096) -> ()");
   m.def(
       "featurize(Tensor board, Tensor ages, Tensor meta, Tensor? ladder, int[] fids, int[] fplanes, Tensor(a!)? planes, "
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");

@@ -178,11 +178,16 @@ def dense_f32(A, B, C, bias=None, trans_a: bool = False, trans_b: bool = False, 
     return C
 
 
-def ladder_planes(board, meta, out, S: int):
+def ladder_planes(board, meta, out, S: int, budget: int = 0):
     """Ladder bits on the device from the compact encoding (board int8 (B, S*S),
     meta int32 (B, 2) {ko, player to move}): out uint8 (B, S*S), bit 0 = ladder
-    capture, bit 1 = ladder escape -- the host encoder's ladder bits."""
-    _ops().ladder_planes(board, meta, out, S)
+    capture, bit 1 = ladder escape -- the host encoder's ladder bits.  ``budget``:
+    node visits per read (0 = the engine's current budget, as the CPU reader)."""
+    if budget <= 0:
+        from .._native import engine
+
+        budget = engine().ladder_budget()
+    _ops().ladder_planes(board, meta, out, S, budget)
     return out
 
 

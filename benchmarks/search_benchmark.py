@@ -1,5 +1,5 @@
 """Batched MCTS and self-play throughput on the GPU (policy 12x192, 48 planes;
-value 12x192 49 planes; random-init weights).  The reference MCTS made one
+value 12x152 49 planes; random-init weights).  The reference MCTS made one
 batch-1 network call per tree level and ran 10^4 serial simulations per move
 (mcts.py:142-161).  Prints JSON: leaf evaluations/s, simulations/s, and
 self-play games/s + moves/s for lock-step batched games."""
@@ -26,7 +26,7 @@ def main():
     small = dev.type == "cpu"
     F, L = (16, 2) if small else (192, 12)
     pol = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
-    val = CNNValue(VALUE_FEATURES, filters_per_layer=F, layers=L, device=dev)
+    val = CNNValue(VALUE_FEATURES, filters_per_layer=152 if not small else F, layers=L, device=dev)  # reference K=152
     trees = int(sys.argv[1]) if len(sys.argv) > 1 else (4 if small else 256)  # 256 trees x 16 leaves saturate the GPU better than 64 (150k vs 49k evals/s bf16)
     playouts = int(sys.argv[2]) if len(sys.argv) > 2 else (32 if small else 800)
     lpt = 16

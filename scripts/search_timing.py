@@ -36,7 +36,7 @@ def main():
     playouts = int(sys.argv[2]) if len(sys.argv) > 2 else 800
     dev = torch.device("cuda")
     pol = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=192, layers=12, device=dev)
-    val = CNNValue(VALUE_FEATURES, filters_per_layer=192, layers=12, device=dev)
+    val = CNNValue(VALUE_FEATURES, filters_per_layer=152, layers=12, device=dev)
     s = M.BatchedMCTS(pol, val, n_trees=trees, seed=0)
     states = [go.GameState() for _ in range(trees)]
     for i, st in enumerate(states):

@@ -260,6 +260,28 @@ def test_bitboard_ladder_reader_matches_cpu_reader():
             assert int((lad & 1).sum()) > 0 and int((lad & 2).sum()) > 0
 
 
+def test_ladder_node_budget_same_in_both_readers():
+    """The node budget (a read gives up past N prey_loses / hunter_wins visits, like
+    past the depth cap) has the same semantics and candidate order in the CPU and
+    bitboard readers: they agree at every budget; a small one changes some bits."""
+    E = engine()
+    states = random_positions(400, size=19, seed=31, max_len=330)
+    try:
+        full = None
+        for budget in (10 ** 9, 64, 0):
+            E.set_ladder_budget(budget)
+            board, _, meta, lad = E.encode_batch(states, True, 8)
+            assert np.array_equal(E.ladder_bits_bb(board, meta, 19, 8), lad), budget
+            if budget == 10 ** 9:
+                full = lad
+            elif budget == 64:
+                assert (lad != full).any()
+            else:
+                assert E.ladder_budget() == 4096
+    finally:
+        E.set_ladder_budget(0)
+
+
 @pytest.mark.gpu
 def test_gpu_ladder_planes_match_cpu(cuda_device):
     """ladder_planes (csrc/kernels/ladder.hip) on >= 1000 random 19x19 positions
@@ -274,6 +296,15 @@ def test_gpu_ladder_planes_match_cpu(cuda_device):
         ops.ladder_planes(torch.from_numpy(board).to(cuda_device), torch.from_numpy(meta).to(cuda_device), out, size)
         got = out.cpu().numpy()
         assert np.array_equal(got, lad), (size, np.argwhere(got != lad)[:5].tolist())
+    # a small node budget: the device reader gives up exactly where the CPU reader does
+    try:
+        engine().set_ladder_budget(64)
+        board, _, meta, lad = engine().encode_batch(random_positions(300, seed=31, max_len=330), True, 8)
+        out = torch.empty(board.shape, dtype=torch.uint8, device=cuda_device)
+        ops.ladder_planes(torch.from_numpy(board).to(cuda_device), torch.from_numpy(meta).to(cuda_device), out, 19)
+        assert np.array_equal(out.cpu().numpy(), lad)
+    finally:
+        engine().set_ladder_budget(0)
 
 
 @pytest.mark.gpu
