@@ -74,8 +74,10 @@ LB_HD int ctz(uint64_t x) {
 LB_HD void bzero(BB& b) {
   for (int i = 0; i < W; ++i) b.w[i] = 0;
 }
-// Word selection by compare-and-select over the W words rather than b.w[p >> 6]:
-// a dynamically indexed register array would live in GPU scratch memory.
+// Word selection: on the GPU by compare-and-select over the W words (a
+// dynamically indexed register array would live in scratch memory); on the
+// host by plain indexing.
+#if defined(__HIP_DEVICE_COMPILE__)
 LB_HD uint64_t bword(const BB& b, int i) {
   uint64_t r = 0;
   for (int k = 0; k < W; ++k) r |= b.w[k] & (0ull - (uint64_t)(i == k));
@@ -90,6 +92,12 @@ LB_HD void bclr(BB& b, int p) {
   const uint64_t m = 1ull << (p & 63);
   for (int k = 0; k < W; ++k) b.w[k] &= ~(m & (0ull - (uint64_t)(k == (p >> 6))));
 }
+#else
+LB_HD uint64_t bword(const BB& b, int i) { return b.w[i]; }
+LB_HD bool btest(const BB& b, int p) { return (b.w[p >> 6] >> (p & 63)) & 1ull; }
+LB_HD void bset(BB& b, int p) { b.w[p >> 6] |= 1ull << (p & 63); }
+LB_HD void bclr(BB& b, int p) { b.w[p >> 6] &= ~(1ull << (p & 63)); }
+#endif
 LB_HD int bcount(const BB& b) {
   int c = 0;
   for (int i = 0; i < W; ++i) c += popc(b.w[i]);
@@ -181,6 +189,13 @@ LB_HD BB group_of(const LState& s, int p, const Geo& g) {
   return grp;
 }
 
+// group_of with the caller's known chain (the ladder's prey group, tracked
+// incrementally): a long prey chain is never flood-filled again
+LB_HD BB group_hint(const LState& s, int q, const Geo& g, const BB& known) {
+  if (btest(known, q)) return known;
+  return group_of(s, q, g);
+}
+
 LB_HD BB libs_of(const LState& s, const BB& grp, const Geo& g) {
   BB d = dilate(grp, g);
   for (int i = 0; i < W; ++i) d.w[i] &= ~(s.black.w[i] | s.white.w[i]);
@@ -198,7 +213,7 @@ LB_HD void neighbours(int p, const Geo& g, int* out) {
 }
 
 // go.cpp GameState::is_suicide_for (go.py:181-202)
-LB_HD bool is_suicide_for(const LState& s, int p, int color, const Geo& g) {
+LB_HD bool is_suicide_for(const LState& s, int p, int color, const Geo& g, const BB& known) {
   int nb[4];
   neighbours(p, g, nb);
   for (int i = 0; i < 4; ++i)
@@ -206,7 +221,7 @@ LB_HD bool is_suicide_for(const LState& s, int p, int color, const Geo& g) {
   for (int i = 0; i < 4; ++i) {
     const int q = nb[i];
     if (q < 0) continue;
-    const BB grp = group_of(s, q, g);
+    const BB grp = group_hint(s, q, g, known);
     const BB lb = libs_of(s, grp, g);
     const int other = bcount(lb) - (btest(lb, p) ? 1 : 0);
     const int cq = color_at(s, q);
@@ -216,16 +231,17 @@ LB_HD bool is_suicide_for(const LState& s, int p, int color, const Geo& g) {
   return true;
 }
 
-LB_HD bool is_legal_for(const LState& s, int p, int color, const Geo& g) {
+// `known`: a chain of s whose membership the caller knows (or an empty set)
+LB_HD bool is_legal_for(const LState& s, int p, int color, const Geo& g, const BB& known) {
   if (p < 0 || p >= g.np) return false;
   if (color_at(s, p) != 0) return false;
   if (p == s.ko) return false;
-  return !is_suicide_for(s, p, color, g);
+  return !is_suicide_for(s, p, color, g, known);
 }
 
 // go.cpp GameState::try_move for a legal non-pass move (capture order and ko
 // detection in neighbour order, go.py:312-331)
-LB_HD void play(LState& s, int p, int c, const Geo& g) {
+LB_HD void play(LState& s, int p, int c, const Geo& g, const BB& known) {
   s.ko = -1;
   const uint64_t selb = 0ull - (uint64_t)(c > 0);  // all ones when black moves
   {
@@ -241,7 +257,7 @@ LB_HD void play(LState& s, int p, int c, const Geo& g) {
   for (int i = 0; i < 4; ++i) {
     const int q = nb[i];
     if (q < 0 || color_at(s, q) != -c) continue;
-    const BB grp = group_of(s, q, g);
+    const BB grp = group_hint(s, q, g, known);
     if (bany(libs_of(s, grp, g))) continue;
     for (int j = 0; j < W; ++j) {
       s.white.w[j] &= ~(grp.w[j] & selb);
@@ -258,10 +274,31 @@ LB_HD int prey_libcount(const LState& s, int prey, const Geo& g) {
   return bcount(libs_of(s, group_of(s, prey, g), g));
 }
 
+// the prey chain after the prey played p (pg: the chain before): if p touches
+// it, p joins it with every own-colour chain next to p; a move elsewhere (a
+// capture escape on a hunter's last liberty) leaves it as it was
+LB_HD BB grow_chain(const LState& s, const BB& pg, int p, int color, const Geo& g) {
+  int nb[4];
+  neighbours(p, g, nb);
+  bool touches = false;
+  for (int i = 0; i < 4; ++i) touches |= nb[i] >= 0 && btest(pg, nb[i]);
+  if (!touches) return pg;
+  BB r = pg;
+  bset(r, p);
+  for (int i = 0; i < 4; ++i) {
+    const int q = nb[i];
+    if (q < 0 || color_at(s, q) != color || btest(r, q)) continue;
+    const BB o = group_of(s, q, g);
+    for (int k = 0; k < W; ++k) r.w[k] |= o.w[k];
+  }
+  return r;
+}
+
 enum : int { F_HUNTER = 0, F_PREY = 1 };
 
 struct Frame {
   LState s;
+  BB pg;  // the prey chain in s (tracked incrementally, never re-flood-filled)
   int prey, kind, depth, nc, k;
   int16_t cand[kMaxCand];
 };
@@ -274,7 +311,7 @@ LB_HD int frame_init(Frame& f, const LState& st, const Geo& g, int& visits, int 
   if (++visits > budget) return 0;       // node budget spent: give up, prey survives
   if (f.depth > kLadderDepth) return 0;  // both give up: prey survives
   const int pc = color_at(st, f.prey);
-  const BB grp = group_of(st, f.prey, g);
+  const BB& grp = f.pg;
   const BB lb = libs_of(st, grp, g);
   if (f.kind == F_HUNTER) {
     const int lc = bcount(lb);
@@ -340,22 +377,26 @@ LB_HD int ladder_eval(Stack& stack, const Geo& g, int& visits, int budget) {
     int k = f.k;
     const int nc = f.nc < kMaxCand ? f.nc : kMaxCand;
     LState ns;
+    BB npg;
     while (ret < 0 && k < nc) {
       const int mv = f.cand[k++];
       const int mover = kind == F_HUNTER ? -pc : pc;
-      if (mv < 0 || !is_legal_for(cur, mv, mover, g)) continue;
+      if (mv < 0 || !is_legal_for(cur, mv, mover, g, f.pg)) continue;
       ns = cur;
-      play(ns, mv, mover, g);
+      play(ns, mv, mover, g, f.pg);
       if (kind == F_HUNTER) {
         if (color_at(ns, prey) != pc) { ret = 1; break; }  // captured outright
-        if (prey_libcount(ns, prey, g) != 1) continue;
+        npg = f.pg;  // a hunter move leaves the prey chain as it was
+        if (bcount(libs_of(ns, npg, g)) != 1) continue;
       } else {
         if (color_at(ns, prey) != pc) continue;
-        const int lc = prey_libcount(ns, prey, g);
+        npg = grow_chain(ns, f.pg, mv, pc, g);
+        const int lc = bcount(libs_of(ns, npg, g));
         if (lc >= 3) { ret = 0; break; }
         if (lc != 2) continue;
       }
       Frame& c = stack[top + 1];
+      c.pg = npg;
       c.prey = prey;
       c.kind = kind == F_HUNTER ? F_PREY : F_HUNTER;
       c.depth = f.depth + 1;
@@ -386,20 +427,25 @@ LB_HD int ladder_eval(Stack& stack, const Geo& g, int& visits, int budget) {
 // player to move is `me`; bit 0 = capture, bit 1 = escape.
 template <class Stack>
 LB_HD int ladder_bits_at(const LState& s, int m, int me, Stack& stack, const Geo& g, int budget = kLadderVisits) {
-  if (!is_legal_for(s, m, me, g)) return 0;
+  BB none;
+  bzero(none);
+  if (!is_legal_for(s, m, me, g, none)) return 0;
   int visits = 0;  // per capture test, then per escape test (featurize.cpp resets per call)
   int nb[4];
   neighbours(m, g, nb);
   int out = 0;
   for (int i = 0; i < 4 && !(out & 1); ++i) {  // capture
     const int q = nb[i];
-    if (q < 0 || color_at(s, q) != -me || prey_libcount(s, q, g) != 2) continue;
+    if (q < 0 || color_at(s, q) != -me) continue;
+    const BB pg = group_of(s, q, g);
+    if (bcount(libs_of(s, pg, g)) != 2) continue;
     Frame& f = stack[0];
     LState ns = s;
-    play(ns, m, me, g);
+    play(ns, m, me, g, pg);
     if (color_at(ns, q) != -me) { out |= 1; break; }
-    if (prey_libcount(ns, q, g) != 1) continue;
+    if (bcount(libs_of(ns, pg, g)) != 1) continue;
     f.s = ns;
+    f.pg = pg;
     f.prey = q;
     f.kind = F_PREY;
     f.depth = 0;
@@ -410,15 +456,19 @@ LB_HD int ladder_bits_at(const LState& s, int m, int me, Stack& stack, const Geo
   visits = 0;
   for (int i = 0; i < 4 && !(out & 2); ++i) {  // escape
     const int q = nb[i];
-    if (q < 0 || color_at(s, q) != me || prey_libcount(s, q, g) != 1) continue;
+    if (q < 0 || color_at(s, q) != me) continue;
+    const BB pg0 = group_of(s, q, g);
+    if (bcount(libs_of(s, pg0, g)) != 1) continue;
     Frame& f = stack[0];
     LState ns = s;
-    play(ns, m, me, g);
+    play(ns, m, me, g, pg0);
     if (color_at(ns, q) != me) continue;
-    const int lc = prey_libcount(ns, q, g);
+    const BB pg = grow_chain(ns, pg0, m, me, g);
+    const int lc = bcount(libs_of(ns, pg, g));
     if (lc >= 3) { out |= 2; break; }
     if (lc != 2) continue;
     f.s = ns;
+    f.pg = pg;
     f.prey = q;
     f.kind = F_HUNTER;
     f.depth = 0;
