@@ -3,6 +3,7 @@
 #include <atomic>
 #include <cstring>
 #include <utility>
+#include <vector>
 
 #include "ladder_bb.h"
 
@@ -180,14 +181,32 @@ void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* met
       if (s.board[p] == EMPTY || s.head[p] != p) continue;
       if ((s.board[p] == -me && s.libc[p] == 2) || (s.board[p] == me && s.libc[p] == 1)) cand.orr(s.libs[p]);
     }
+    // the searches run on the bitboard reader (ladder_bb.h: 100-byte states,
+    // the prey chain tracked incrementally) -- bit-identical to
+    // ladder_capture_at / ladder_escape_at, without a 20 KB GameState copy per
+    // ply (tests/test_gpu_features.py compares the two at several budgets)
+    static thread_local lb::Geo geo[20];
+    static thread_local bool geo_ok[20] = {};
+    if (!geo_ok[s.n]) {
+      lb::make_geo(geo[s.n], s.n);
+      geo_ok[s.n] = true;
+    }
+    const lb::Geo& g = geo[s.n];
+    static thread_local std::vector<lb::Frame> stack(lb::kMaxFrames);
+    lb::LState ls;
+    lb::bzero(ls.black);
+    lb::bzero(ls.white);
+    for (int p = 0; p < np; ++p) {
+      if (s.board[p] > 0) lb::bset(ls.black, p);
+      else if (s.board[p] < 0) lb::bset(ls.white, p);
+    }
+    ls.ko = s.ko;
+    const int budget = ladder_budget();
     for (int i = 0; i < BW; ++i)
       for (uint64_t w = cand.w[i]; w; w &= w - 1) {
         const int p = i * 64 + __builtin_ctzll(w);
         if (p >= np || s.board[p] != EMPTY || !s.is_legal(p)) continue;
-        uint8_t v = 0;
-        if (ladder_capture_at(s, p)) v |= 1;
-        if (ladder_escape_at(s, p)) v |= 2;
-        ladder[p] = v;
+        ladder[p] = (uint8_t)(lb::ladder_bits_at(ls, p, me, stack, g, budget) & 3);
       }
   }
 }

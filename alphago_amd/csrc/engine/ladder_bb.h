@@ -196,6 +196,24 @@ LB_HD BB group_hint(const LState& s, int q, const Geo& g, const BB& known) {
   return group_of(s, q, g);
 }
 
+// points with at least two empty 4-neighbours (e = empty points)
+LB_HD BB two_empty_nbrs(const BB& e, const Geo& g) {
+  const int n = g.n;
+  BB r;
+  for (int i = 0; i < W; ++i) {
+    const uint64_t lo1 = i ? e.w[i - 1] >> 63 : 0;
+    const uint64_t hi1 = i + 1 < W ? e.w[i + 1] << 63 : 0;
+    const uint64_t lon = i ? e.w[i - 1] >> (64 - n) : 0;
+    const uint64_t hin = i + 1 < W ? e.w[i + 1] << (64 - n) : 0;
+    const uint64_t a = ((e.w[i] << 1) | lo1) & g.not_y0.w[i];     // empty at p - 1
+    const uint64_t b = ((e.w[i] >> 1) | hi1) & g.not_ylast.w[i];  // empty at p + 1
+    const uint64_t c = (e.w[i] << n) | lon;                        // empty at p - n
+    const uint64_t d = (e.w[i] >> n) | hin;                        // empty at p + n
+    r.w[i] = ((a & b) | (a & c) | (a & d) | (b & c) | (b & d) | (c & d)) & g.on.w[i];
+  }
+  return r;
+}
+
 LB_HD BB libs_of(const LState& s, const BB& grp, const Geo& g) {
   BB d = dilate(grp, g);
   for (int i = 0; i < W; ++i) d.w[i] &= ~(s.black.w[i] | s.white.w[i]);
@@ -257,6 +275,12 @@ LB_HD void play(LState& s, int p, int c, const Geo& g, const BB& known) {
   for (int i = 0; i < 4; ++i) {
     const int q = nb[i];
     if (q < 0 || color_at(s, q) != -c) continue;
+    // a stone with an empty neighbour keeps its chain alive: no flood fill
+    int qn[4];
+    neighbours(q, g, qn);
+    bool open = false;
+    for (int j = 0; j < 4; ++j) open |= qn[j] >= 0 && color_at(s, qn[j]) == 0;
+    if (open) continue;
     const BB grp = group_hint(s, q, g, known);
     if (bany(libs_of(s, grp, g))) continue;
     for (int j = 0; j < W; ++j) {
@@ -331,6 +355,15 @@ LB_HD int frame_init(Frame& f, const LState& st, const Geo& g, int& visits, int 
   BB around = dilate(grp, g);
   BB hunters = stones_copy(st, -pc);
   for (int i = 0; i < W; ++i) hunters.w[i] &= around.w[i];
+  // A chain holding a stone with two empty neighbours has two liberties: it is
+  // not in atari, and none of its stones can be the key of an atari chain, so
+  // dropping such stones keeps the candidate list and its order.
+  {
+    BB e;
+    for (int i = 0; i < W; ++i) e.w[i] = g.on.w[i] & ~(st.black.w[i] | st.white.w[i]);
+    const BB ge2 = two_empty_nbrs(e, g);
+    for (int i = 0; i < W; ++i) hunters.w[i] &= ~ge2.w[i];
+  }
   for (int it = 0; it < g.np && bany(hunters); ++it) {
     const int q = bfirst(hunters);
     const BB hg = group_of(st, q, g);

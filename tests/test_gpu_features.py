@@ -262,8 +262,9 @@ def test_bitboard_ladder_reader_matches_cpu_reader():
 
 def test_ladder_node_budget_same_in_both_readers():
     """The node budget (a read gives up past N prey_loses / hunter_wins visits, like
-    past the depth cap) has the same semantics and candidate order in the CPU and
-    bitboard readers: they agree at every budget; a small one changes some bits."""
+    past the depth cap) has the same semantics and candidate order in the
+    GameState-copy reader (featurize planes) and the bitboard reader (encoder,
+    GPU kernel): they agree at every budget; a small one changes some bits."""
     E = engine()
     states = random_positions(400, size=19, seed=31, max_len=330)
     try:
@@ -272,6 +273,9 @@ def test_ladder_node_budget_same_in_both_readers():
             E.set_ladder_budget(budget)
             board, _, meta, lad = E.encode_batch(states, True, 8)
             assert np.array_equal(E.ladder_bits_bb(board, meta, 19, 8), lad), budget
+            # the encoder's bitboard searches vs the GameState-copy reader of the planes path
+            pl = E.featurize_batch(states, ["ladder_capture", "ladder_escape"], 8).reshape(len(states), 2, -1)
+            assert np.array_equal(pl[:, 0] | (pl[:, 1] << 1), lad), budget
             if budget == 10 ** 9:
                 full = lad
             elif budget == 64:
