@@ -234,9 +234,9 @@ class HipConvTrainer:
             self._fp8_calibrated = False
             # fp8 dgrad (opt-in): e5m2 gradients x transposed e4m3 weights; per-layer delayed
             # gradient scales from the max |dZ| of the previous step (the first step runs bf16
-            # dgrads and calibrates them).  The kernel is faster than the bf16 dgrad (213 vs
-            # 253 us per 3x3 layer at B=1024), but the e5m2 quantisation pass and the transposed
-            # weight packs eat the gain: value training 142.2k vs 143.5k positions/s
+            # dgrads and calibrates them).  The kernel is barely faster than the bf16 dgrad (219
+            # vs 225 us per 3x3 layer at B=1024, serial) and the e5m2 quantisation pass and the
+            # transposed weight packs make it a net loss: value training 142.2k vs 143.5k
             self.fp8_dgrad = fp8_dgrad
             self.wd8 = [None] + [torch.zeros((ops.fp8_nchunks(self.K[l], self.Fp), self.Fp, 64), dtype=torch.uint8,
                                              device=dev) for l in range(1, L)]
