@@ -360,8 +360,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   const int nbase = n0 + ((lane >> 4) << 2);
   const float osc = a.out_scale[0];
   float vmax = 0.f;
+  // ReLU' bitmask in conv_fwd_kernel's layout: channel block i belongs to its wave half
+  // wn = i / (NB/2), bit 4*(i % (NB/2)) + r of word blockIdx.y*8 + wn*4 + lane/16
+  const int mwords = gridDim.y * 8;
 #pragma unroll
   for (int j = 0; j < MB; ++j) {
+    uint32_t mb[2] = {0u, 0u};
     int m = m0 + wave * 16 * MB + j * 16 + (lane & 15);
     const bool ok = m < a.M;
     m = ok ? m : a.M - 1;
@@ -397,6 +401,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
         o[2] = (__bf16)v[2];
         o[3] = (__bf16)v[3];
         *(bf16x4*)(a.y_bf16 + ooff + n) = o;
+        if constexpr (!DG && NB % 2 == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) mb[i / (NB / 2)] |= ((float)o[r] > 0.f ? 1u : 0u) << (4 * (i % (NB / 2)) + r);
+        }
       }
       if constexpr (OUT_FP8) {
         if constexpr (DG) {
@@ -413,6 +421,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
           pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
           *(int*)(a.y_fp8 + ooff + n) = pk;
         }
+      }
+    }
+    if constexpr (!DG && OUT_BF16 && NB % 2 == 0) {
+      if (a.mbits_out && ok) {
+        const size_t pw = (size_t)(ooff / a.Cout) * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
+        a.mbits_out[pw] = mb[0];
+        a.mbits_out[pw + 4] = mb[1];
       }
     }
   }

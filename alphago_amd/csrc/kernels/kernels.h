@@ -144,6 +144,9 @@ struct ConvFp8Args {
   // tracks max |dx| and writes bf16 and/or e5m2 (out_scale) outputs
   int dgrad;
   const __bf16* mask;
+  // forward, production kernel: optional ReLU'(y) bitmask in conv_fwd_kernel's layout
+  // (ConvEpilogue: (Cout/BN)*8 words per padded pixel) so the bf16 dgrad can run MODE_MASKBITS
+  uint32_t* mbits_out;
 };
 
 // Kernel choices are explicit launch arguments (ConvFwdArgs::tile,

@@ -269,8 +269,9 @@ void featurize(const Tensor& board, const Tensor& ages, const Tensor& meta, cons
 // x: (B, HPi, HPi, Cin) uint8 (e4m3); w: (nch, Cout, 64) uint8; scales int32[2]; out_scale f32[1]
 void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales, const Tensor& out_scale,
                   const c10::optional<Tensor>& amax, const c10::optional<Tensor>& y_bf16,
-                  const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S, int64_t Pin, int64_t Po) {
-  conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, 0);
+                  const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S, int64_t Pin, int64_t Po,
+                  const c10::optional<Tensor>& mbits) {
+  conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, 0, c10::nullopt, mbits);
 }
 
 // fp8 dgrad: dx = conv(dz (e5m2, scales[0]), flipped/transposed e4m3 weights (scales[1])) masked
@@ -497,7 +498,7 @@ TORCH_LIBRARY(alphago_amd, m) {
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
   m.def(
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
-      "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po) -> ()");
+      "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, Tensor(d!)? mbits=None) -> ()");
   m.def("pack_weights_fp8(Tensor w, Tensor(a!) out, float scale, Tensor? scale_dev, bool transposed=False) -> ()");
   m.def("conv_dgrad_fp8(Tensor dz8, Tensor w, Tensor mask, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
         "Tensor(b!) y_bf16, Tensor(c!)? y_fp8, int K, int S) -> ()");

@@ -131,7 +131,8 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
                               const Tensor& out_scale, const c10::optional<Tensor>& amax,
                               const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K,
                               int64_t S, int64_t Pin, int64_t Po, int variant,
-                              const c10::optional<Tensor>& dgrad_mask = c10::nullopt) {
+                              const c10::optional<Tensor>& dgrad_mask = c10::nullopt,
+                              const c10::optional<Tensor>& mbits = c10::nullopt) {
   // dgrad_mask given: fp8 dgrad (x = e5m2 gradients, w = transposed e4m3 weights, output masked
   // by dgrad_mask > 0, no bias, e5m2 y_fp8)
   CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -174,6 +175,14 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
     TORCH_CHECK(variant == 0, "dgrad: production kernel only");
     a.dgrad = 1;
     a.mask = bfp(*dgrad_mask);
+  }
+  if (mbits.has_value()) {
+    TORCH_CHECK(!dgrad_mask.has_value() && variant == 0 && y_bf16.has_value(),
+                "mbits: production forward with a bf16 output only");
+    TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
+    const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
+    TORCH_CHECK(mbits->numel() >= B * HPo * HPo * words, "mbits too small: need B*HPo*HPo*words");
+    a.mbits_out = reinterpret_cast<uint32_t*>(mbits->data_ptr<int>());
   }
   TORCH_CHECK(B * HPi * HPi * Cin < (1ll << 31), "tensor too large for int32 offsets");
   if (a.M == 0) return;

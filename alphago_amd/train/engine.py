@@ -324,7 +324,7 @@ class HipConvTrainer:
             last = l == self.L - 1
             ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l], self.S,
                              pin, 1, y_bf16=self.Y[l], y_fp8=None if last else self.Y8[l % 2],
-                             amax=self.amax8[l])
+                             amax=self.amax8[l], mbits=None if last else self.MBITS[l])
             x8, pin = self.Y8[l % 2], 1
         ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)  # next step's activation scales
 
@@ -378,10 +378,7 @@ class HipConvTrainer:
                     ops.conv_dgrad_fp8(self.DZ8[l % 2], self.wd8[l], self.Y[l - 1], self.gscales8[l],
                                        self.gosc8[l - 1:l], self.K[l], self.S, self.DZ[l - 1],
                                        y_fp8=self.DZ8[(l - 1) % 2] if l > 1 else None, amax=self.gamax8[l - 1])
-                elif self.precision == "fp8":  # the fp8 forward does not write bitmasks
-                    ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
-                                 mode=ops.MODE_MASK, mask=self.Y[l - 1])
-                else:
+                else:  # ReLU' bitmask from the forward epilogue (bf16 and fp8 forwards write it)
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=self.conv_tile)
         if self.precision == "fp8" and self.fp8_dgrad:

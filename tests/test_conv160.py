@@ -139,13 +139,25 @@ def test_conv_fwd_fp8_160(ops, cuda_device, B, Cin, Cin_p, K):
     amax = ops.fp8_amax_buffer(1, cuda_device)[0]
     yb = ops.padded_empty(B, S, 1, Cp, cuda_device)
     y8 = torch.zeros((B, S + 2, S + 2, Cp), dtype=torch.uint8, device=cuda_device)
-    ops.conv_fwd_fp8(x8, w8, bp, scales, osc, K, S, P, 1, y_bf16=yb, y_fp8=y8, amax=amax)
+    mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=cuda_device)
+    ops.conv_fwd_fp8(x8, w8, bp, scales, osc, K, S, P, 1, y_bf16=yb, y_fp8=y8, amax=amax, mbits=mbits)
     torch.cuda.synchronize()
     out = ops.from_padded(yb, 1)
     assert _rel_err(out[:, :Cout], ref) < 1e-2
     assert out[:, Cout:].abs().sum() == 0
     assert _rel_err(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1, :Cout].permute(0, 3, 1, 2), ref) < 0.07
     assert abs(amax.view(torch.float32).max().item() - ref.max().item()) <= 1e-2 * ref.max().item()
+    # the ReLU' bitmask written by the fp8 epilogue == masking by y_bf16 > 0 in the bf16 dgrad
+    w2 = _bf(torch.randn(Cout, Cout, 3, 3, device=cuda_device) * 0.05)
+    wf2 = ops.packed_weight_like(w2, Cp, Cp)
+    wd2 = ops.packed_weight_like(w2, Cp, Cp, transposed=True)
+    ops.pack_weights([w2], [wf2], [wd2])
+    dz = ops.to_padded(_bf(torch.randn(B, Cout, S, S, device=cuda_device)), 1, Cp)
+    d_bits, d_mask = (ops.padded_empty(B, S, 1, Cp, cuda_device) for _ in range(2))
+    ops.conv_fwd(dz, wd2, None, d_bits, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mbits)
+    ops.conv_fwd(dz, wd2, None, d_mask, 3, S, 1, 1, mode=ops.MODE_MASK, mask=yb)
+    torch.cuda.synchronize()
+    assert torch.equal(d_bits, d_mask)
 
 
 @pytest.mark.parametrize("C,Cp", [(152, 160), (192, 192)])
