@@ -197,15 +197,12 @@ int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
     // contiguous blocks of trees per worker (each with its own slot range); concatenated in tree order
     std::vector<std::vector<Leaf>> pend(T);
     std::vector<std::vector<int>> ids(T);
-    std::vector<std::thread> pool;
-    for (int w = 0; w < T; ++w)
-      pool.emplace_back([&, w]() {
-        const int lo = (int)((int64_t)n * w / T), hi = (int)((int64_t)n * (w + 1) / T);
-        pend[w].reserve((size_t)(hi - lo) * leaves_per_tree);
-        ids[w].reserve((size_t)(hi - lo) * leaves_per_tree);
-        gather_trees(which->data() + lo, hi - lo, leaves_per_tree, pend[w], ids[w], lo * leaves_per_tree);
-      });
-    for (auto& th : pool) th.join();
+    run_parts(T, [&](int w) {
+      const int lo = (int)((int64_t)n * w / T), hi = (int)((int64_t)n * (w + 1) / T);
+      pend[w].reserve((size_t)(hi - lo) * leaves_per_tree);
+      ids[w].reserve((size_t)(hi - lo) * leaves_per_tree);
+      gather_trees(which->data() + lo, hi - lo, leaves_per_tree, pend[w], ids[w], lo * leaves_per_tree);
+    });
     for (int w = 0; w < T; ++w) {
       pending_.insert(pending_.end(), pend[w].begin(), pend[w].end());
       leaf_slot_.insert(leaf_slot_.end(), ids[w].begin(), ids[w].end());
@@ -219,32 +216,32 @@ void Forest::leaf_features(uint8_t* out, int threads) const {
   int L = (int)pending_.size();
   if (L == 0) return;
   size_t stride = (size_t)nplanes_ * leaf_state(0).np;
-  int T = std::max(1, std::min(threads, L));
-  std::vector<std::thread> pool;
-  for (int t = 0; t < T; ++t)
-    pool.emplace_back([&, t]() {
-      for (int i = t; i < L; i += T) featurize(leaf_state(i), fids_.data(), (int)fids_.size(), out + i * stride);
-    });
-  for (auto& th : pool) th.join();
+  ensure_pool(threads);  // the forest's persistent pool (set_threads) runs the parts
+  constexpr int kChunk = 8;
+  run_parts((L + kChunk - 1) / kChunk, [&](int c) {
+    for (int i = c * kChunk; i < std::min(L, (c + 1) * kChunk); ++i)
+      featurize(leaf_state(i), fids_.data(), (int)fids_.size(), out + i * stride);
+  });
 }
 
 void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) const {
   int L = (int)pending_.size();
   if (L == 0) return;
   const int np = leaf_state(0).np;
-  int T = std::max(1, std::min(ladder ? threads : 1, L));  // without ladders this is a memcpy-class walk
-  auto work = [&](int t) {
-    for (int i = t; i < L; i += T)
+  ensure_pool(threads);  // the forest's persistent pool (set_threads) runs the parts
+  // small chunks claimed dynamically: ladder reads make a few boards far costlier than the rest
+  constexpr int kChunk = 4;
+  auto work = [&](int c) {
+    for (int i = c * kChunk; i < std::min(L, (c + 1) * kChunk); ++i)
       encode_state(leaf_state(i), board + (size_t)i * np, ages + (size_t)i * np, meta + 2 * i,
                    ladder ? ladder + (size_t)i * np : nullptr);
   };
-  if (T == 1) {
-    work(0);
+  const int nchunks = (L + kChunk - 1) / kChunk;
+  if (!ladder) {  // without ladders this is a memcpy-class walk
+    for (int c = 0; c < nchunks; ++c) work(c);
     return;
   }
-  std::vector<std::thread> pool;
-  for (int t = 0; t < T; ++t) pool.emplace_back(work, t);
-  for (auto& th : pool) th.join();
+  run_parts(nchunks, work);
 }
 
 void Forest::leaf_masks(uint8_t* out) const {
@@ -336,10 +333,7 @@ void Forest::apply(const float* priors, const float* values, const uint8_t* mask
       while (c < L && c > 0 && pending_[c].tree == pending_[c - 1].tree) ++c;
       cut[w] = std::max(c, cut[w - 1]);
     }
-    std::vector<std::thread> pool;
-    for (int w = 0; w < T; ++w)
-      pool.emplace_back([&, w]() { apply_range(cut[w], cut[w + 1], priors, values, mask); });
-    for (auto& th : pool) th.join();
+    run_parts(T, [&](int w) { apply_range(cut[w], cut[w + 1], priors, values, mask); });
   }
   pending_.clear();
   leaf_slot_.clear();

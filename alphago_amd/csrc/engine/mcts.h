@@ -14,10 +14,12 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <random>
 #include <vector>
 
 #include "go.h"
+#include "workpool.h"
 
 namespace ag {
 
@@ -102,7 +104,20 @@ class Forest {
   // mask (L, n*n) optional sensible-move mask (e.g. from the GPU featurizer) — skips the legality/eye scan
   void apply(const float* priors, const float* values, const uint8_t* mask = nullptr);
   // worker threads for gather/apply (trees are independent; results are identical for any count)
-  void set_threads(int n) { threads_ = n < 1 ? 1 : n; }
+  void set_threads(int n) {
+    threads_ = n < 1 ? 1 : n;
+    if (!pool_ || pool_->workers() != threads_ - 1) pool_.reset(threads_ > 1 ? new WorkPool(threads_ - 1) : nullptr);
+  }
+  // a pool for callers that pass a thread count without set_threads
+  void ensure_pool(int threads) const {
+    if (!pool_ && threads > 1) pool_.reset(new WorkPool(threads - 1));
+  }
+  // run fn(0..nparts-1) on the persistent workers (serially without a pool)
+  void run_parts(int nparts, const std::function<void(int)>& fn) const {
+    if (pool_) pool_->run(nparts, fn);
+    else
+      for (int p = 0; p < nparts; ++p) fn(p);
+  }
   void add_root_noise(int t, double alpha, double eps);
   // Root statistics
   void root_stats(int t, std::vector<int>& moves, std::vector<int>& visits, std::vector<float>& q) const;
@@ -133,6 +148,7 @@ class Forest {
   int nplanes_ = 0;
   int64_t total_evals_ = 0;
   int threads_ = 1;
+  mutable std::unique_ptr<WorkPool> pool_;  // threads_ - 1 persistent workers (set_threads)
   void gather_trees(const int* trees, int ntrees, int lpt, std::vector<Leaf>& pend, std::vector<int>& slot_ids,
                     int slot_base);
   void apply_range(int i0, int i1, const float* priors, const float* values, const uint8_t* mask);
