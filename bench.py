@@ -105,11 +105,11 @@ def main():
     while True:
         if dev.type == "cuda":
             torch.cuda.synchronize()
-        if agdist.all_reduce_max(time.perf_counter() - t_warm) >= args.min_warmup_s:
+        warm_s = agdist.all_reduce_max(time.perf_counter() - t_warm)  # the slowest rank's warmup time
+        if warm_s >= args.min_warmup_s:
             break
         run(10)
         warm_steps += 10
-    warm_s = time.perf_counter() - t_warm
     loss_sum.zero_()
     corr_sum.zero_()
     if dev.type == "cuda":

@@ -35,7 +35,9 @@ def _worker(rank, world, port, q):
     tr.compute_grads(planes[sl], tgt[sl])
     grad = tr.fp.grad.clone()
     tr.step(planes[sl], tgt[sl])
-    q.put((rank, grad, tr.fp.flat.clone()))
+    # numpy copies travel by value (a torch tensor is shared through a file descriptor that dies with
+    # the worker if the parent has not unpickled it yet)
+    q.put((rank, grad.numpy().copy(), tr.fp.flat.numpy().copy()))
     agdist.barrier()
     agdist.shutdown()
 
@@ -51,6 +53,7 @@ def test_dp_gradients_equal_single_process():
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    res = [(r, torch.from_numpy(g), torch.from_numpy(f)) for r, g, f in res]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -41,7 +41,8 @@ def _worker(rank, world, port, q, F=64, L=3, NB=16):
     grad = tr.fp.grad.cpu().clone()
     tr.apply_update()
     torch.cuda.synchronize()
-    q.put((rank, grad, len(tr.buckets), tr.fp.flat.cpu().clone()))
+    # numpy copies travel by value (a shared torch tensor dies with the worker's file descriptor)
+    q.put((rank, grad.numpy().copy(), len(tr.buckets), tr.fp.flat.cpu().numpy().copy()))
     agdist.barrier()
     agdist.shutdown()
 
@@ -61,6 +62,7 @@ def test_hip_dp_matches_single(cuda_device, F, L, NB):
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    res = [(r, torch.from_numpy(g), nb, torch.from_numpy(w)) for r, g, nb, w in res]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
