@@ -484,8 +484,17 @@ static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
                                                   " is a kernel-lab variant");
 #endif
   if constexpr (BN == 160) {  // value net (152 filters): L2-operand kernel only
-    if (a.variant != 0) throw std::invalid_argument("conv_fwd_fp8: 160-wide tiles have no lab variants");
-    launch_fp8_ga<160, 3, 5, OB, OF>(a, st);  // 48 px per wave, weights read in 5 parts (2 parts spill)
+    // production: 48 px per wave, weights read in 5 parts (230 VGPRs, no spills).  Value layer,
+    // B=1024, round-robin min (scripts/lab/fp8_160_variants.py): 149.5 us; lab 1 (48 px, 2 parts,
+    // 254 VGPRs) 146.1; lab 3 (32 px, 5 parts) 158.8; lab 4 (32 px, 2 parts) 157.0 (as the
+    // default it cost value fp8 training 144.9k -> 142.9k)
+    if (a.variant == 0) launch_fp8_ga<160, 3, 5, OB, OF>(a, st);
+#ifdef AGK_KERNEL_LAB
+    else if (a.variant == 1) launch_fp8_ga<160, 3, 2, OB, OF>(a, st);
+    else if (a.variant == 3) launch_fp8_ga<160, 2, 5, OB, OF>(a, st);
+    else if (a.variant == 4) launch_fp8_ga<160, 2, 2, OB, OF>(a, st);
+#endif
+    else throw std::invalid_argument("conv_fwd_fp8: 160-wide tile variant " + std::to_string(a.variant));
   } else {
     if (a.variant != 5 && (BN * 128) % (16 * 512) == 0) {
       if constexpr (BN == 192) {
