@@ -543,7 +543,7 @@ static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
 // Cin % 64 == 32 uses straddled K-steps
 template <int MODE, bool STR>
 static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
-  if (bm == 384) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR>(a, st);
+  if (bm == 384 || bm == 385) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR>(a, st);
   else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
   else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
   else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 128 / 256 / 384");
@@ -558,16 +558,23 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // concurrent pair is bound by the same per-CU operand delivery either way;
   // the larger tile moves fewer bytes per MFMA (bench: 106.2k -> 108.5k pos/s,
   // scripts/bench_variants.sh).
-  if (bm == 0) bm = (a.M >= 384 * 512) ? 384 : (a.M >= 256 * 512) ? 256 : 128;
+  // automatic: 385 (the 384 tile with its DMA spread through the MFMAs) on
+  // 192/128/64-wide tiles, 384 on 160-wide ones; alternating A/B of the SL
+  // bench, serial backward: 121.5-121.7k vs 120.0-120.4k pos/s (profiles/r2_ab/tile_ab.txt)
+  if (bm == 0) bm = (a.M >= 384 * 512) ? 385 : (a.M >= 256 * 512) ? 256 : 128;
   if constexpr (BN == 160) {
     if (a.Cin % 64 == 32) launch_fwd_160<MODE, true>(a, bm, st);
     else launch_fwd_160<MODE, false>(a, bm, st);
   } else {
     if (a.Cin % 64 != 0) throw std::invalid_argument("conv_fwd: Cin % 64 == 32 needs the 160-wide tile");
-    // production tile codes: 128 / 256 (64-pixel waves), 384 (default, 96x96 per wave)
+    // production tile codes: 128 / 256 (64-pixel waves), 384 / 385 (96x96 per wave;
+    // 385 = default, DMA spread through the MFMAs)
     if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);
     else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
     else if (bm == 128) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
+    // 385: the 384 tile with the next stage's LDS-DMA spread through the first
+    // k-half's MFMAs instead of issued as one burst (kernel-lab tile 9)
+    else if (bm == 385) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
 #ifdef AGK_KERNEL_LAB
     // kernel-lab tile codes (profiles/r1_fwd_kernel_experiments.md):
     // conv_fwd_variants.hip (-1, 2, 4, 5, 6, 32), 2560 (epilogue loads after the loop),

@@ -11,9 +11,10 @@ using namespace agk_ops;
 void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const c10::optional<Tensor>& mask,
               const Tensor& y, int64_t K, int64_t S, int64_t Pin, int64_t Po, int64_t mode,
               const c10::optional<Tensor>& mbits, int64_t tile) {
-  // production tilings only: 0 = automatic, or a fixed 128 / 256 / 384-pixel tile
-  TORCH_CHECK(tile == 0 || tile == 128 || tile == 256 || tile == 384,
-              "conv_fwd tile ", tile, " is not a production tiling (0, 128, 256, 384); kernel-lab variants are in "
+  // production tilings only: 0 = automatic, or a fixed 128 / 256 / 384-pixel tile (385: 384 with the
+  // LDS-DMA issue spread through the MFMAs)
+  TORCH_CHECK(tile == 0 || tile == 128 || tile == 256 || tile == 384 || tile == 385,
+              "conv_fwd tile ", tile, " is not a production tiling (0, 128, 256, 384, 385); kernel-lab variants are in "
               "torch.ops.alphago_amd_lab (alphago_amd.ops.lab())");
   conv_fwd_impl(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, (int)tile);
 }

@@ -125,7 +125,8 @@ def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: 
              mbits=None, tile: int = 0):
     """Conv + epilogue.  mode 0: bias + ReLU (mbits: also write the ReLU' bitmask);
     1: dgrad masked by ``mask`` > 0; 3: dgrad masked by the ``mbits`` bitmask.
-    ``tile``: 0 = automatic, or a production tiling 128 / 256 / 384."""
+    ``tile``: 0 = automatic, or a production tiling 128 / 256 / 384 / 385 (384 with the DMA issue
+    spread through the MFMAs; the automatic choice for large batches)."""
     _ops().conv_fwd(x, w_packed, bias, mask, y, K, S, Pin, Po, mode, mbits, tile)
     return y
 

@@ -124,7 +124,7 @@ class HipConvTrainer:
                  overlap: bool = False, wgrad_target_wgs: int = 512, iterations: int = 0, precision: str = "bf16",
                  wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: bool = False):
         ops.load()
-        self.conv_tile = conv_tile  # forward/dgrad tiling: 0 = automatic, or 128 / 256 / 384
+        self.conv_tile = conv_tile  # forward/dgrad tiling: 0 = automatic, or 128 / 256 / 384 / 385
         if precision not in ("bf16", "fp8"):
             raise ValueError("precision must be bf16 or fp8")
         self.precision = precision
