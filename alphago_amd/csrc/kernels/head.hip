@@ -49,18 +49,33 @@ __device__ __forceinline__ void head_dots(const __bf16* base, const float* w_s, 
   const int R = blockDim.x >> 5;
   const int l32 = tid & 31, slot = tid >> 5;
   const int c8 = l32 << 3;
-  for (int p0 = 0; p0 < SS; p0 += R) {
-    const int p = p0 + slot;
-    float d = 0.f;
-    if (p < SS && l32 < C8) {
-      const int i = p / S, j = p - (p / S) * S;
-      const bf16x8 v = *(const bf16x8*)(base + (size_t)((i + 1) * HP + j + 1) * C + c8);
+  // HU rows in flight per half-wave: the loop is bound by load latency (one
+  // workgroup per board, every workgroup resident at once), not bandwidth
+  constexpr int HU = 8;
+  for (int p0 = 0; p0 < SS; p0 += HU * R) {
+    bf16x8 v[HU];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d += (float)v[e] * w_s[c8 + e];
+    for (int u = 0; u < HU; ++u) {
+      const int p = p0 + u * R + slot;
+      if (p < SS && l32 < C8) {
+        const int i = p / S, j = p - (p / S) * S;
+        v[u] = *(const bf16x8*)(base + (size_t)((i + 1) * HP + j + 1) * C + c8);
+      } else {
+        v[u] = bf16x8{};
+      }
     }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-    if (l32 == 0 && p < SS) z_s[p] = d;
+    for (int u = 0; u < HU; ++u) {
+      const int p = p0 + u * R + slot;
+      float d = 0.f;
+      if (l32 < C8) {  // w_s holds only the C real slots: lanes past them must not read it
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)v[u][e] * w_s[c8 + e];
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      if (l32 == 0 && p < SS) z_s[p] = d;
+    }
   }
   __syncthreads();
 }
@@ -86,19 +101,34 @@ __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (r < R) {
     const int c8 = cg << 3;
-    for (int p = r; p < SS; p += R) {
-      const int i = p / a.S, j = p - (p / a.S) * a.S;
-      const size_t off = (size_t)((i + 1) * HP + j + 1) * a.C + c8;
-      const bf16x8 v = *(const bf16x8*)(base + off);
-      const float g = g_s[p];
-      bf16x8 o;
+    // BU positions' loads issued before their stores (latency-bound loop)
+    constexpr int BU = 8;
+    for (int p0 = r; p0 < SS; p0 += BU * R) {
+      bf16x8 v[BU];
+      size_t off[BU];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float y = (float)v[e];
-        o[e] = (__bf16)(y > 0.f ? g * w_s[c8 + e] : 0.f);
-        acc[e] += g * y;
+      for (int u = 0; u < BU; ++u) {
+        const int p = p0 + u * R;
+        const int pc = p < SS ? p : SS - 1;
+        const int i = pc / a.S, j = pc - (pc / a.S) * a.S;
+        off[u] = (size_t)((i + 1) * HP + j + 1) * a.C + c8;
+        v[u] = *(const bf16x8*)(base + off[u]);
       }
-      *(bf16x8*)(dzb + off) = o;
+#pragma unroll
+      for (int u = 0; u < BU; ++u) {
+        const int p = p0 + u * R;
+        if (p < SS) {
+          const float g = g_s[p];
+          bf16x8 o;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float y = (float)v[u][e];
+            o[e] = (__bf16)(y > 0.f ? g * w_s[c8 + e] : 0.f);
+            acc[e] += g * y;
+          }
+          *(bf16x8*)(dzb + off[u]) = o;
+        }
+      }
     }
   }
 #pragma unroll

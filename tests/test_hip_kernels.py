@@ -145,9 +145,10 @@ def test_conv_wgrad_thin_input(ops, cuda_device, K, Pin):
     assert _rel_err(gb, ref_b) < 2e-3
 
 
-def test_policy_head_train(ops, cuda_device):
+@pytest.mark.parametrize("C", [192, 64, 128])
+def test_policy_head_train(ops, cuda_device, C):
     torch.manual_seed(3)
-    B, C, S = 7, 192, 19
+    B, S = 7, 19
     y = _bf(torch.randn(B, C, S, S, device=cuda_device)).clamp_min(0)
     w = torch.randn(C, device=cuda_device) * 0.05
     b = torch.randn(1, device=cuda_device)

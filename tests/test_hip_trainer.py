@@ -66,11 +66,14 @@ def test_hip_bce_grads_match_torch(cuda_device):
     assert hip.loss[-1].item() == 0.0
 
 
-def test_hip_step_reduces_loss(cuda_device):
-    torch.manual_seed(1)
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_hip_step_reduces_loss(cuda_device, seed):
+    # lr 0.05: at 0.5 this 20-step fit of one batch is chaotic, and a last-bit change in the
+    # head's reductions flipped its outcome (loss 188.5 -> 515.8 instead of down)
+    torch.manual_seed(seed)
     B = 32
     net = PolicyNet(48, filters_per_layer=64, layers=3)
-    tr = HipPolicyTrainer(net, B, lr=0.5, device=cuda_device)
+    tr = HipPolicyTrainer(net, B, lr=0.05, device=cuda_device)
     planes = torch.randint(0, 2, (B, 48, 19, 19), dtype=torch.uint8, device=cuda_device)
     tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
     l0, _ = tr.evaluate(planes, tgt)
