@@ -62,8 +62,8 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   constexpr int B_ROWS_PW = BN / NW;   // weight rows staged per wave (contiguous layout)
   constexpr int B_INSTR = BDIST ? (BN / 8 + NW - 1) / NW : B_ROWS_PW / 8;  // glds instructions per wave
   static_assert(BN % 32 == 0 && BN % 8 == 0 && A_ROWS_PW % 8 == 0, "tile geometry");
-  static_assert(!(BDIST && (M32 || ILV)), "round-robin weight staging: production loops only");
-  static_assert(!(STR && (M32 || ILV)), "straddled K-steps: production loops only");
+  static_assert(!(BDIST && M32), "round-robin weight staging: not in the 32x32 loop");
+  static_assert(!(STR && M32), "straddled K-steps: not in the 32x32 loop");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63;
@@ -109,12 +109,13 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   // scalar adds (no per-step integer divisions)
   int st_c0 = 0, st_kw = 0, st_a = 0, st_t = 0;
   size_t st_w = 0;
-  auto stage = [&](int buf) {
-    char* base = smem + buf * STAGE;
-    // source offsets (without the lane's row/channel part) of the step's two
-    // 32-channel halves; equal unless STR
-    int xo0 = st_a + st_c0, xo1 = xo0;
-    size_t wo0 = st_w + st_c0, wo1 = wo0;
+  // source offsets (without the lane's row/channel part) of the step's two
+  // 32-channel halves; equal unless STR
+  auto st_offsets = [&](int& xo0, int& xo1, size_t& wo0, size_t& wo1) {
+    xo0 = st_a + st_c0;
+    xo1 = xo0;
+    wo0 = st_w + st_c0;
+    wo1 = wo0;
     if constexpr (STR) {
       const int c1 = st_c0 + 32;
       const bool nx = c1 >= a.Cin;  // the second half opens the next tap
@@ -123,19 +124,20 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
       xo1 = nx ? (st_t + 1 < a.K * a.K ? a_next : xo0) : st_a + c1;
       wo1 = nx ? st_w + wtap : st_w + c1;
     }
-#pragma unroll
-    for (int i = 0; i < A_INSTR; ++i) {
-      const int xo = arow[i] + ((STR && ahi[i]) ? xo1 : xo0);
+  };
+  // DMA piece d of a stage: pixel pieces 0 .. A_INSTR-1, then weight pieces
+  auto st_piece = [&](int d, char* base, int xo0, int xo1, size_t wo0, size_t wo1) {
+    if (d < A_INSTR) {
+      const int xo = arow[d] + ((STR && ahi[d]) ? xo1 : xo0);
 #ifdef AGK_DEBUG
       const bool ok = AGK_DCHECK(xo >= 0 && (long long)xo + 8 <= a.x_elems, DBG_FWD_X);
-      glds16(a.x + (ok ? xo : 0), base + (wave * A_ROWS_PW + i * 8) * 128);
+      glds16(a.x + (ok ? xo : 0), base + (wave * A_ROWS_PW + d * 8) * 128);
 #else
-      glds16(a.x + xo, base + (wave * A_ROWS_PW + i * 8) * 128);
+      glds16(a.x + xo, base + (wave * A_ROWS_PW + d * 8) * 128);
 #endif
-    }
-#pragma unroll
-    for (int i = 0; i < B_INSTR; ++i) {
-      if (BDIST && wave + i * NW >= BN / 8) continue;  // wave-uniform: fewer pieces on the last waves
+    } else {
+      const int i = d - A_INSTR;
+      if (BDIST && wave + i * NW >= BN / 8) return;  // wave-uniform: fewer pieces on the last waves
       const size_t wo = ((STR && bhi[i]) ? wo1 : wo0) + brow[i];
 #ifdef AGK_DEBUG
       const bool ok = AGK_DCHECK((long long)wo + 8 <= a.w_elems, DBG_FWD_W);
@@ -144,8 +146,10 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
       glds16(a.w + wo, base + A_BYTES + bldsrow[i] * 128);
 #endif
     }
-    // branch-free cursor advance (selects), so a caller can interleave the
-    // DMA with MFMAs inside one basic block
+  };
+  // branch-free cursor advance (selects), so a caller can interleave the
+  // DMA with MFMAs inside one basic block
+  auto st_advance = [&]() {
     st_c0 += 64;
     const bool wrap = STR ? st_c0 >= a.Cin : st_c0 == a.Cin;
     st_c0 = wrap ? st_c0 - a.Cin : st_c0;
@@ -155,6 +159,15 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     const bool wrap2 = st_kw == a.K;
     st_kw = wrap2 ? 0 : st_kw;
     st_a += (wrap ? a.Cin : 0) + (wrap2 ? (a.HPi - a.K) * a.Cin : 0);
+  };
+  auto stage = [&](int buf) {
+    char* base = smem + buf * STAGE;
+    int xo0, xo1;
+    size_t wo0, wo1;
+    st_offsets(xo0, xo1, wo0, wo1);
+#pragma unroll
+    for (int d = 0; d < A_INSTR + B_INSTR; ++d) st_piece(d, base, xo0, xo1, wo0, wo1);
+    st_advance();
   };
 
   f32x4 acc[NB][MB];
@@ -265,8 +278,9 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
       const bool more = ks + 1 < nK;
       read_frags(base, 0, xa, wa);
       char* nb = smem + (cur ^ 1) * STAGE;
-      const __bf16* wt = a.w + st_w + st_c0;
-      const __bf16* xs = a.x + st_a + st_c0;
+      int xo0, xo1;
+      size_t wo0, wo1;
+      st_offsets(xo0, xo1, wo0, wo1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
@@ -274,24 +288,13 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
       for (int d = 0; d < NDMA; ++d) {
         mfma_range(d * MPD, (d + 1) * MPD);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) {
-          if (d < A_INSTR) glds16(xs + arow[d], nb + (wave * A_ROWS_PW + d * 8) * 128);
-          else glds16(wt + brow[d - A_INSTR], nb + A_BYTES + (wave * B_ROWS_PW + (d - A_INSTR) * 8) * 128);
-        }
+        if (more) st_piece(d, nb, xo0, xo1, wo0, wo1);
         __builtin_amdgcn_sched_barrier(0);
       }
       mfma_range(NDMA * MPD, NMF);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      // advance the staging cursor (branch-free)
-      st_c0 += 64;
-      const bool wrap = st_c0 == a.Cin;
-      st_c0 = wrap ? 0 : st_c0;
-      st_w += wrap ? wtap : 0;
-      st_kw += wrap ? 1 : 0;
-      const bool wrap2 = st_kw == a.K;
-      st_kw = wrap2 ? 0 : st_kw;
-      st_a += (wrap ? a.Cin : 0) + (wrap2 ? (a.HPi - a.K) * a.Cin : 0);
+      st_advance();
       read_frags(base, 1, xa, wa);
       __builtin_amdgcn_s_setprio(1);
       mfmas(xa, wa);
@@ -543,7 +546,8 @@ static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
 // Cin % 64 == 32 uses straddled K-steps
 template <int MODE, bool STR>
 static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
-  if (bm == 384 || bm == 385) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR>(a, st);
+  if (bm == 384) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR>(a, st);
+  else if (bm == 385) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR>(a, st);
   else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
   else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
   else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 128 / 256 / 384");
@@ -558,9 +562,9 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // concurrent pair is bound by the same per-CU operand delivery either way;
   // the larger tile moves fewer bytes per MFMA (bench: 106.2k -> 108.5k pos/s,
   // scripts/bench_variants.sh).
-  // automatic: 385 (the 384 tile with its DMA spread through the MFMAs) on
-  // 192/128/64-wide tiles, 384 on 160-wide ones; alternating A/B of the SL
-  // bench, serial backward: 121.5-121.7k vs 120.0-120.4k pos/s (profiles/r2_ab/tile_ab.txt)
+  // automatic: 385 (the 384 tile with its DMA spread through the MFMAs);
+  // alternating A/B, serial backward: SL 121.5-121.9k vs 120.0-120.7k pos/s,
+  // value (160-wide, straddled K-steps) 140.1k vs 136.7k bf16 (profiles/r2_dma_spread.md)
   if (bm == 0) bm = (a.M >= 384 * 512) ? 385 : (a.M >= 256 * 512) ? 256 : 128;
   if constexpr (BN == 160) {
     if (a.Cin % 64 == 32) launch_fwd_160<MODE, true>(a, bm, st);
