@@ -122,7 +122,8 @@ class HipConvTrainer:
 
     def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
                  overlap: bool = False, wgrad_target_wgs: int = 512, iterations: int = 0, precision: str = "bf16",
-                 wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: bool = False):
+                 wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: bool = False,
+                 reduce_stream: Optional[bool] = None):
         ops.load()
         self.conv_tile = conv_tile  # forward/dgrad tiling: 0 = automatic, or 128 / 256 / 384 / 385
         if precision not in ("bf16", "fp8"):
@@ -192,8 +193,17 @@ class HipConvTrainer:
             self.nsplit.append(ns)
             slab_max = max(slab_max, ns * T * self.Fp * cin_p)
             db_max = max(db_max, ns * self.Fp)
-        self._slab = torch.empty(slab_max, device=dev)
-        self._dbslab = torch.zeros(db_max, device=dev)
+        # Split-K reduce on a side stream (serial backward only): the memory-bound reduce of
+        # layer l runs beside dgrad(l) instead of between the two big conv kernels.  The
+        # slabs are double-buffered by layer parity, so wgrad(l-1) never waits for
+        # reduce(l); wgrad(l-2) waits for reduce(l) through an event.
+        if reduce_stream is None:
+            reduce_stream = os.environ.get("ALPHAGO_AMD_REDUCE_STREAM", "0") == "1"
+        self.s_r = (torch.cuda.Stream(device=dev, priority=-1) if reduce_stream and not overlap else None)
+        nslab = 2 if self.s_r is not None else 1
+        self._slabs = [torch.empty(slab_max, device=dev) for _ in range(nslab)]
+        self._dbslabs = [torch.zeros(db_max, device=dev) for _ in range(nslab)]
+        self._slab_free = [None] * nslab  # event: the reduce that last read slab i has finished
         # wgrad stream at high priority (-1): its workgroups are dispatched ahead of the
         # concurrent dgrad's, so the wgrad/reduce/all-reduce chain of a layer finishes
         # earlier and less of it is left after the last dgrad (+0.9 % positions/s,
@@ -341,15 +351,34 @@ class HipConvTrainer:
         ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)
         self._fp8_calibrated = True
 
-    def _wgrad_layer(self, l: int) -> None:
+    def _wgrad_layer(self, l: int, red: bool = False) -> None:
+        """wgrad(l) into a split slab, then the deterministic reduce into the flat grad (and
+        the async all-reduce of a completed bucket when ``red``).  With the reduce stream the
+        reduce and the all-reduce launch run there; the caller's stream goes on to dgrad(l)."""
         x, pin = self._layer_in(l)
         T = self.K[l] ** 2
         cin_p = x.shape[3]
         ns = self.nsplit[l]
-        slab = self._slab[:ns * T * self.Fp * cin_p].view(ns, T, self.Fp, cin_p)
-        dbs = self._dbslab[:ns * self.Fp].view(ns, self.Fp)
+        i = l % len(self._slabs)
+        slab = self._slabs[i][:ns * T * self.Fp * cin_p].view(ns, T, self.Fp, cin_p)
+        dbs = self._dbslabs[i][:ns * self.Fp].view(ns, self.Fp)
+        sr = self.s_r
+        if sr is not None and self._slab_free[i] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._slab_free[i])
         ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0)
-        ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)
+
+        def reduce():
+            ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)
+            if red and l in self._bucket_after_layer:
+                self.reducer.launch(self._bucket_after_layer[l])
+
+        if sr is None:
+            reduce()
+            return
+        sr.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(sr):
+            reduce()
+            self._slab_free[i] = sr.record_event()
 
     def backward_trunk(self, reduce: bool = True) -> None:
         """dZ[L-1] (and head grads) must be ready on the current stream.
@@ -364,13 +393,9 @@ class HipConvTrainer:
                 ev = main.record_event()
                 with torch.cuda.stream(self.s_w):
                     self.s_w.wait_event(ev)
-                    self._wgrad_layer(l)
-                    if red and l in self._bucket_after_layer:
-                        self.reducer.launch(self._bucket_after_layer[l])
+                    self._wgrad_layer(l, red)
             else:
-                self._wgrad_layer(l)
-                if red and l in self._bucket_after_layer:
-                    self.reducer.launch(self._bucket_after_layer[l])
+                self._wgrad_layer(l, red)
             if l > 0:
                 if self.precision == "fp8" and self.fp8_dgrad and self._g8_calibrated:
                     if l == self.L - 1:  # the head's dZ enters the e5m2 chain
@@ -388,6 +413,8 @@ class HipConvTrainer:
                 self._fp8_grad_calibrate()
         if self.s_w is not None:
             main.wait_stream(self.s_w)
+        if self.s_r is not None:
+            main.wait_stream(self.s_r)
         if red:
             self.reducer.wait()
 
@@ -472,7 +499,8 @@ class HipConvTrainer:
             self._graphs = []
             # the wgrad side stream is captured as a parallel branch only on request
             # (ALPHAGO_AMD_GRAPH_OVERLAP=1); by default the graph is one serial chain
-            keep_sw = self.s_w
+            keep_sw, keep_sr = self.s_w, self.s_r
+            self.s_r = None  # captured serially: its slab events were recorded outside the capture
             if os.environ.get("ALPHAGO_AMD_GRAPH_OVERLAP", "0") != "1":
                 self.s_w = None
             try:
@@ -482,7 +510,7 @@ class HipConvTrainer:
                         fn()
                     self._graphs.append(g)
             finally:
-                self.s_w = keep_sw
+                self.s_w, self.s_r = keep_sw, keep_sr
             # the capture ran nothing; the iteration counters it advanced on the host are undone
             self.sched.iterations -= 1
         self._graphs[0].replay()

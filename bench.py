@@ -59,6 +59,8 @@ def main():
                     help="forward/dgrad conv tiling (0 = automatic)")
     ap.add_argument("--wgrad-wgs", type=int, default=512,
                     help="target workgroups per wgrad launch (sets the split-K factor)")
+    ap.add_argument("--reduce-stream", type=int, default=None, choices=[0, 1],
+                    help="1: split-K wgrad reduce on a side stream beside the dgrad (default: engine default)")
     ap.add_argument("--profile", default=None,
                     help="after the timed run, profile 6 more steps (torch.profiler + roctx ranges) into DIR")
     args = ap.parse_args()
@@ -68,7 +70,9 @@ def main():
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
     kw = {} if args.backend == "torch" else {"overlap": args.overlap, "precision": args.precision,
-                                             "wgrad_target_wgs": args.wgrad_wgs, "conv_tile": args.conv_tile}
+                                             "wgrad_target_wgs": args.wgrad_wgs, "conv_tile": args.conv_tile,
+                                             "reduce_stream": None if args.reduce_stream is None
+                                             else bool(args.reduce_stream)}
     trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
     if args.graph:
         trainer.enable_graphs()

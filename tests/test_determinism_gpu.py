@@ -14,14 +14,15 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _train(device, overlap: bool, steps: int = 3):
+def _train(device, overlap: bool, steps: int = 3, reduce_stream: bool = False):
     from alphago_amd.models.nets import PolicyNet
     from alphago_amd.train.engine import HipPolicyTrainer
 
     torch.manual_seed(0)
     net = PolicyNet(48, filters_per_layer=192, layers=4)
     B = 64
-    tr = HipPolicyTrainer(net, B, lr=0.01, device=device, overlap=overlap)
+    tr = HipPolicyTrainer(net, B, lr=0.01, device=device, overlap=overlap, reduce_stream=reduce_stream)
+    assert (tr.s_r is not None) == (reduce_stream and not overlap)
     g = torch.Generator().manual_seed(3)
     losses = []
     for _ in range(steps):
@@ -45,6 +46,16 @@ def test_hip_training_bitwise_reproducible(cuda_device):
 def test_hip_training_same_with_and_without_wgrad_stream(cuda_device):
     p1, g1, _ = _train(cuda_device, overlap=True)
     p2, g2, _ = _train(cuda_device, overlap=False)
+    assert torch.equal(g1, g2)
+    assert torch.equal(p1, p2)
+
+
+def test_hip_training_same_with_and_without_reduce_stream(cuda_device):
+    """Split-K reduce on its own stream beside the dgrad (double-buffered slabs):
+    the same gradients and weights as the one-stream backward."""
+    p1, g1, l1 = _train(cuda_device, overlap=False, steps=4)
+    p2, g2, l2 = _train(cuda_device, overlap=False, steps=4, reduce_stream=True)
+    assert l1 == l2
     assert torch.equal(g1, g2)
     assert torch.equal(p1, p2)
 
