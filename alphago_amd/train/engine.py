@@ -137,6 +137,7 @@ class HipConvTrainer:
         self.batch = batch
         self.sched = KerasSGDSchedule(lr, decay, iterations)
         self.overlap = overlap
+        self.comm_events = None  # list: record the all-reduce wait of each backward as (start, end) events
         tr = net.trunk
         self.S = net.board
         self.L = tr.layers
@@ -416,7 +417,14 @@ class HipConvTrainer:
         if self.s_r is not None:
             main.wait_stream(self.s_r)
         if red:
+            if self.comm_events is not None:  # exposed all-reduce time (utils.metrics.StepMetrics)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(main)
             self.reducer.wait()
+            if self.comm_events is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(main)
+                self.comm_events.append((e0, e1))
 
     @torch.no_grad()
     def _fp8_grad_calibrate(self) -> None:

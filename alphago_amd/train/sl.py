@@ -46,7 +46,7 @@ from ..models.policy import CNNPolicy
 from ..parallel import dist as agdist
 from ..utils import faults
 from ..utils.config import RunConfig
-from ..utils.metrics import MetricsLogger
+from ..utils.metrics import MetricsLogger, StepMetrics
 from ..utils.profiling import Profiler, trace_range
 from ..utils.watchdog import Watchdog, enable_collective_timeouts
 from . import checkpoint as ckpt
@@ -95,7 +95,10 @@ def _parser():
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-symmetries", action="store_true", help="disable random D4 augmentation")
     p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
-    p.add_argument("--metrics", default=None, help="JSONL per-step metrics file")
+    p.add_argument("--metrics", default=None, help="JSONL metrics file (per-epoch and per-step records)")
+    p.add_argument("--log-every", type=int, default=100,
+                   help="with --metrics: one per-step record (loss, acc, pos/s, TFLOP/s, HBM, exposed "
+                        "all-reduce ms) every N steps; 0 = epoch records only")
     p.add_argument("--checkpoint-every", type=int, default=0,
                    help="also write the native checkpoint every N steps (0: end of epoch only)")
     p.add_argument("--resume", action="store_true",
@@ -188,6 +191,8 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
     samples_per_epoch = args.epoch_length or n_train
     steps_per_epoch = max(1, samples_per_epoch // global_B)
     log = MetricsLogger(args.metrics if env.is_main else None)
+    step_log = StepMetrics(log, args.log_every if args.metrics else 0, global_B, net.flops_per_position(), dev,
+                           trainer)
 
     start_epoch = len(meta.metadata["epochs"])
     end_epoch = start_epoch + args.epochs if resume else args.epochs
@@ -244,6 +249,7 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
                     l, c = trainer.step(planes, tgt, sym)
                 sums[0] += l.double()
                 sums[1] += c.double()
+                step_log.on_step(gstep, epoch, l, c)
                 wd.beat(gstep)
                 prof.step()
                 if args.checkpoint_every and (gstep + 1) % args.checkpoint_every == 0 and step + 1 < steps_per_epoch:

@@ -59,3 +59,36 @@ def test_train_one_epoch_hip(tmp_path, cuda_device):
     assert len(meta["epochs"]) == 2
     assert os.path.exists(os.path.join(out, "weights.00001.hdf5"))
     assert meta["epochs"][1]["loss"] < meta["epochs"][0]["loss"] + 0.5
+
+
+def _step_records(path):
+    with open(path) as f:
+        recs = [json.loads(line) for line in f]
+    return [r for r in recs if "step" in r], [r for r in recs if "step" not in r]
+
+
+def test_step_metrics_jsonl_cpu(tmp_path):
+    """--metrics/--log-every: one per-step record every N steps (SURVEY.md §5 metrics row)
+    next to the per-epoch record."""
+    out = str(tmp_path / "out")
+    mpath = str(tmp_path / "m.jsonl")
+    run_training([_model(tmp_path, "cpu"), _data(tmp_path), out, "--epochs", "1", "-l", "64", "-B", "8",
+                  "--backend", "torch", "--metrics", mpath, "--log-every", "2"])
+    steps, epochs = _step_records(mpath)
+    assert [r["step"] for r in steps] == [2, 4, 6, 8]
+    assert len(epochs) == 1
+    for r in steps:
+        assert r["world"] == 1 and r["positions_per_s"] > 0 and r["tflops"] > 0
+        assert 0.0 <= r["acc"] <= 1.0 and np.isfinite(r["loss"])
+        assert "allreduce_exposed_ms_per_step" not in r  # torch backend, one rank
+
+
+@pytest.mark.gpu
+def test_step_metrics_jsonl_hip(tmp_path, cuda_device):
+    out = str(tmp_path / "out")
+    mpath = str(tmp_path / "m.jsonl")
+    run_training([_model(tmp_path, "cuda"), _data(tmp_path), out, "--epochs", "1", "-l", "128", "-B", "16",
+                  "--backend", "hip", "--metrics", mpath, "--log-every", "4"])
+    steps, _ = _step_records(mpath)
+    assert [r["step"] for r in steps] == [4, 8]
+    assert all(r["hbm_gb"] > 0 and r["positions_per_s"] > 0 for r in steps)
