@@ -10,6 +10,7 @@ Commands
   gtp            run a GTP v2 engine on stdin/stdout (reference interface/gtp_wrapper)
   match          play games between two players (policy / mcts / random / external GTP)
   bench          the headline SL throughput benchmark (bench.py)
+  serve          HTTP/JSON policy/value/genmove service with dynamic batching
 
 Player specs (gtp/match): ``random``, ``policy:MODEL.json[:greedy|:T]``,
 ``mcts:POLICY.json[,VALUE.json]:PLAYOUTS``, ``gtp:COMMAND LINE``.
@@ -125,6 +126,9 @@ def _dispatch(argv: List[str]):
         return run_game_converter(rest)
     if cmd == "init-model":
         return _init_model(rest)
+    if cmd == "serve":
+        from .serve.server import serve_cli
+        return _Exit(serve_cli(rest))
     if cmd == "train-sl":
         from .train.sl import run_training
         return run_training(rest)

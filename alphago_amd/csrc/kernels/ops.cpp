@@ -11,6 +11,7 @@ using namespace agk_ops;
 void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const c10::optional<Tensor>& mask,
               const Tensor& y, int64_t K, int64_t S, int64_t Pin, int64_t Po, int64_t mode,
               const c10::optional<Tensor>& mbits, int64_t tile) {
+  check_dev("conv_fwd", x, w, bias, mask, y, mbits);
   // production tilings only: 0 = automatic, or a fixed 128 / 256 / 384-pixel tile (385: 384 with the
   // LDS-DMA issue spread through the MFMAs)
   TORCH_CHECK(tile == 0 || tile == 128 || tile == 256 || tile == 384 || tile == 385,
@@ -22,11 +23,13 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
 // slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
                 int64_t Pin, int64_t Po, int64_t cin_real) {
+  check_dev("conv_wgrad", x, dz, slab, dbslab);
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, 0);
 }
 
 void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
                        double scale, double beta) {
+  check_dev("conv_wgrad_reduce", slab, dbslab, grad_w, grad_b);
   CHECK_F32(slab); CHECK_F32(grad_w); CHECK_CONTIG(grad_w);
   const int64_t nsplit = slab.size(0), T = slab.size(1), Cout = slab.size(2), Cin = slab.size(3);
   TORCH_CHECK(grad_w.dim() == 4 && grad_w.size(2) * grad_w.size(3) == T, "grad_w must be OIHW");
@@ -49,6 +52,7 @@ void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::o
                  const c10::optional<Tensor>& legal, const c10::optional<Tensor>& weight, const c10::optional<Tensor>& dz, const c10::optional<Tensor>& loss,
                  const c10::optional<Tensor>& correct, const c10::optional<Tensor>& dhead,
                  const c10::optional<Tensor>& probs, int64_t S, double grad_scale, double temperature, int64_t loss_kind) {
+  check_dev("policy_head", y, w, b, target, legal, weight, dz, loss, correct, dhead, probs);
   CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(b);
   const int64_t B = y.size(0), C = y.size(3);
   TORCH_CHECK(y.size(1) == S + 2, "head input must have pad 1");
@@ -96,6 +100,7 @@ void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::o
 
 // z: (B, S*S) f32 <- y (B, S+2, S+2, C) bf16 . w + b
 void head_logits(const Tensor& y, const Tensor& w, const Tensor& b, const Tensor& z, int64_t S) {
+  check_dev("head_logits", y, w, b, z);
   CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(b); CHECK_F32(z); CHECK_CONTIG(z);
   const int64_t B = y.size(0), C = y.size(3);
   TORCH_CHECK(y.size(1) == S + 2 && C % 8 == 0 && C <= 256 && w.numel() <= C && S * S <= 368, "head geometry");
@@ -111,6 +116,7 @@ void head_logits(const Tensor& y, const Tensor& w, const Tensor& b, const Tensor
 // dz (B, S+2, S+2, C) bf16 <- ReLU'(y) * dlogits x w;  dhead (B, C_real+1) partials
 void head_backward(const Tensor& y, const Tensor& w, const Tensor& dlogits, const Tensor& dz, const Tensor& dhead,
                    int64_t S) {
+  check_dev("head_backward", y, w, dlogits, dz, dhead);
   CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(dlogits); CHECK_CONTIG(dlogits);
   CHECK_BF16(dz); CHECK_CONTIG(dz); CHECK_F32(dhead);
   const int64_t B = y.size(0), C = y.size(3);
@@ -128,6 +134,7 @@ void value_out(const Tensor& h, const Tensor& w2, const Tensor& b2, const c10::o
                const c10::optional<Tensor>& weight, const Tensor& v, const c10::optional<Tensor>& loss,
                const c10::optional<Tensor>& correct, const c10::optional<Tensor>& dh, const c10::optional<Tensor>& dout,
                double grad_scale) {
+  check_dev("value_out", h, w2, b2, target, weight, v, loss, correct, dh, dout);
   CHECK_F32(h); CHECK_CONTIG(h); CHECK_F32(w2); CHECK_F32(b2); CHECK_F32(v);
   TORCH_CHECK(h.dim() == 2, "h must be (B, D)");
   const int64_t B = h.size(0), D = h.size(1);
@@ -155,6 +162,7 @@ void value_out(const Tensor& h, const Tensor& w2, const Tensor& b2, const c10::o
 
 void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c10::optional<Tensor>& target,
                 const c10::optional<Tensor>& target_out, const Tensor& out, int64_t P) {
+  check_dev("pack_input", planes, sym, target, target_out, out);
   TORCH_CHECK(planes.scalar_type() == at::kByte && planes.is_contiguous() && planes.dim() == 4, "planes: uint8 (B,C,S,S)");
   CHECK_BF16(out); CHECK_CONTIG(out);
   const int64_t B = planes.size(0), C = planes.size(1), S = planes.size(2);
@@ -174,6 +182,7 @@ void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c1
 
 // ws: list of OIHW fp32; wf: list of (T, Coutp, Cinp) bf16; wd: list (possibly empty entries skipped)
 void pack_weights(at::TensorList ws, at::TensorList wf, at::TensorList wd) {
+  check_dev("pack_weights", ws, wf, wd);
   TORCH_CHECK(ws.size() == wf.size() && (wd.size() == 0 || wd.size() == ws.size()), "list sizes");
   size_t i = 0;
   while (i < ws.size()) {
@@ -208,6 +217,7 @@ void featurize(const Tensor& board, const Tensor& ages, const Tensor& meta, cons
                at::IntArrayRef fids, at::IntArrayRef fplanes, const c10::optional<Tensor>& planes,
                const c10::optional<Tensor>& nhwc, const c10::optional<Tensor>& sensible,
                const c10::optional<Tensor>& legal, const c10::optional<Tensor>& overflow, int64_t S, int64_t P) {
+  check_dev("featurize", board, ages, meta, ladder, planes, nhwc, sensible, legal, overflow);
   TORCH_CHECK(board.scalar_type() == at::kChar && board.is_contiguous() && board.dim() == 2, "board: int8 (B, S*S)");
   TORCH_CHECK(ages.scalar_type() == at::kByte && ages.is_contiguous() && ages.sizes() == board.sizes(), "ages: uint8 (B, S*S)");
   TORCH_CHECK(meta.scalar_type() == at::kInt && meta.is_contiguous() && meta.dim() == 2 && meta.size(1) == 2, "meta: int32 (B, 2)");
@@ -272,6 +282,7 @@ void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Te
                   const c10::optional<Tensor>& amax, const c10::optional<Tensor>& y_bf16,
                   const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S, int64_t Pin, int64_t Po,
                   const c10::optional<Tensor>& mbits) {
+  check_dev("conv_fwd_fp8", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, mbits);
   conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, 0, c10::nullopt, mbits);
 }
 
@@ -280,10 +291,12 @@ void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Te
 void conv_dgrad_fp8(const Tensor& dz8, const Tensor& w, const Tensor& mask, const Tensor& scales,
                     const Tensor& out_scale, const c10::optional<Tensor>& amax, const Tensor& y_bf16,
                     const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S) {
+  check_dev("conv_dgrad_fp8", dz8, w, mask, scales, out_scale, amax, y_bf16, y_fp8);
   conv_fwd_fp8_impl(dz8, w, out_scale, scales, out_scale, amax, y_bf16, y_fp8, K, S, 1, 1, 0, mask);
 }
 
 void fp8_grad_scales(const Tensor& amax, const Tensor& gscales8, const Tensor& gosc, int64_t margin) {
+  check_dev("fp8_grad_scales", amax, gscales8, gosc);
   TORCH_CHECK(amax.scalar_type() == at::kInt && gscales8.scalar_type() == at::kInt && gosc.scalar_type() == at::kFloat,
               "dtypes");
   const int L = (int)(amax.numel() / agk::kFp8AmaxSlots);
@@ -296,6 +309,7 @@ void fp8_grad_scales(const Tensor& amax, const Tensor& gscales8, const Tensor& g
 
 // e5m2 quantisation with a device scale; amax (int32[64], float bits) accumulates max |x|
 void quantize_bf8(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor& amax) {
+  check_dev("quantize_bf8", x, y, scale, amax);
   CHECK_BF16(x); CHECK_CONTIG(x); CHECK_DEV(x);
   TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 4 == 0, "y");
   TORCH_CHECK(scale.scalar_type() == at::kFloat && amax.scalar_type() == at::kInt &&
@@ -307,6 +321,7 @@ void quantize_bf8(const Tensor& x, const Tensor& y, const Tensor& scale, const T
 
 void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c10::optional<Tensor>& scale_dev,
                       bool transposed) {
+  check_dev("pack_weights_fp8", w, out, scale_dev);
   CHECK_F32(w); CHECK_CONTIG(w);
   TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.dim() == 3 && out.size(2) == 64, "out");
   const int K = (int)w.size(2);
@@ -326,6 +341,7 @@ void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c1
 
 // per-layer weight scales (device-side, no host sync)
 void fp8_weight_scales(at::TensorList ws, const Tensor& wscale, const Tensor& scales8) {
+  check_dev("fp8_weight_scales", ws, wscale, scales8);
   TORCH_CHECK((int)ws.size() <= agk::kMaxPackLayers, "too many layers");
   TORCH_CHECK(wscale.scalar_type() == at::kFloat && scales8.scalar_type() == at::kInt, "dtypes");
   TORCH_CHECK(wscale.numel() >= (int64_t)ws.size() && scales8.numel() >= 2 * (int64_t)ws.size(), "sizes");
@@ -343,6 +359,7 @@ void fp8_weight_scales(at::TensorList ws, const Tensor& wscale, const Tensor& sc
 }
 
 void fp8_act_scales(const Tensor& amax, const Tensor& scales8, const Tensor& osc, int64_t margin) {
+  check_dev("fp8_act_scales", amax, scales8, osc);
   TORCH_CHECK(amax.scalar_type() == at::kInt && scales8.scalar_type() == at::kInt && osc.scalar_type() == at::kFloat, "dtypes");
   const int L = (int)(amax.numel() / agk::kFp8AmaxSlots);
   TORCH_CHECK(amax.numel() % agk::kFp8AmaxSlots == 0 && L <= 64 && scales8.numel() >= 2 * L && osc.numel() >= L,
@@ -353,6 +370,7 @@ void fp8_act_scales(const Tensor& amax, const Tensor& scales8, const Tensor& osc
 }
 
 void quantize_fp8(const Tensor& x, const Tensor& y, double scale) {
+  check_dev("quantize_fp8", x, y);
   CHECK_BF16(x); CHECK_CONTIG(x);
   TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 4 == 0, "y");
   agk::launch_quantize_fp8(bfp(x), y.data_ptr<uint8_t>(), x.numel(), (float)scale, cur_stream());
@@ -364,6 +382,7 @@ int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) {
 }
 
 void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
+  check_dev("sgd_update", p, g);
   CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
   TORCH_CHECK(p.numel() == g.numel(), "size mismatch");
   agk::launch_sgd(p.data_ptr<float>(), g.data_ptr<float>(), p.numel(), (float)lr, (float)gscale, cur_stream());
@@ -371,6 +390,7 @@ void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
 }
 
 void sgd_update_sched(const Tensor& p, const Tensor& g, const Tensor& sched, double gscale) {
+  check_dev("sgd_update_sched", p, g, sched);
   CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g); CHECK_DEV(sched);
   TORCH_CHECK(p.numel() == g.numel(), "size mismatch");
   TORCH_CHECK(sched.scalar_type() == at::kDouble && sched.numel() == 4 && sched.is_contiguous(),
@@ -383,6 +403,7 @@ void sgd_update_sched(const Tensor& p, const Tensor& g, const Tensor& sched, dou
 // C = beta*C + op(A) op(B) (+ bias); op(X) = X or X^T (no copies of transposed operands)
 void dense_f32(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bias, const Tensor& C, bool transA,
                bool transB, double beta) {
+  check_dev("dense_f32", A, B, bias, C);
   CHECK_F32(A); CHECK_F32(B); CHECK_F32(C); CHECK_DEV(A); CHECK_DEV(B); CHECK_DEV(C);
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "2-D operands");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "row-major operands (unit column stride)");
@@ -414,6 +435,7 @@ void dense_f32(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bi
 // Ladder planes from the compact board encoding: out (B, S*S) uint8, bit 0 =
 // ladder capture, bit 1 = ladder escape (the encoder's CPU ladder bits).
 void ladder_planes(const Tensor& board, const Tensor& meta, const Tensor& out, int64_t S, int64_t budget) {
+  check_dev("ladder_planes", board, meta, out);
   CHECK_DEV(board); CHECK_DEV(meta); CHECK_DEV(out);
   TORCH_CHECK(board.scalar_type() == at::kChar && board.dim() == 2 && board.size(1) == S * S && board.is_contiguous(),
               "board int8 (B, S*S)");
@@ -465,6 +487,7 @@ void selftest_bad_launch() {
 // -> RuntimeError path end to end.
 void debug_conv_fwd_understated(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& y, int64_t K,
                                 int64_t S, int64_t Pin, int64_t Po) {
+  check_dev("debug_conv_fwd_understated", x, w, bias, y);
   conv_fwd_impl(x, w, bias, c10::nullopt, y, K, S, Pin, Po, agk::MODE_BIAS_RELU, c10::nullopt, 0, nullptr,
                 x.numel() / 2);
 }

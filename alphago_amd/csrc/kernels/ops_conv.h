@@ -20,6 +20,24 @@ using at::Tensor;
 inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a device tensor")
+
+// Every tensor argument of an op must live on the GPU: a host pointer handed to a
+// kernel faults the device (an illegal access can take the whole card down), so the
+// ops refuse it on the host first.  check_dev("op", a, b, ...) accepts tensors,
+// optional tensors and tensor lists.
+inline void check_dev_one(const char* op, const Tensor& t) {
+  TORCH_CHECK(!t.defined() || t.is_cuda(), op, ": tensor argument on ", t.device(), ", expected a GPU tensor");
+}
+inline void check_dev_one(const char* op, const c10::optional<Tensor>& t) {
+  if (t.has_value()) check_dev_one(op, *t);
+}
+inline void check_dev_one(const char* op, at::TensorList l) {
+  for (const Tensor& t : l) check_dev_one(op, t);
+}
+template <typename... Ts>
+inline void check_dev(const char* op, const Ts&... ts) {
+  (check_dev_one(op, ts), ...);
+}
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
 #define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
@@ -43,6 +61,7 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
                           const c10::optional<Tensor>& mask, const Tensor& y, int64_t K, int64_t S, int64_t Pin,
                           int64_t Po, int64_t mode, const c10::optional<Tensor>& mbits, int tile,
                           unsigned long long* dbg = nullptr, long long x_elems_override = -1) {
+  check_dev("conv_fwd_impl", x, w, bias, mask, y, mbits);
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
   CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
   CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y);
@@ -98,6 +117,7 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
 // slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
 inline void conv_wgrad_impl(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K,
                             int64_t S, int64_t Pin, int64_t Po, int64_t cin_real, int variant) {
+  check_dev("conv_wgrad_impl", x, dz, slab, dbslab);
   CHECK_DEV(x); CHECK_DEV(dz); CHECK_DEV(slab); CHECK_DEV(dbslab);
   CHECK_BF16(x); CHECK_BF16(dz); CHECK_F32(slab); CHECK_F32(dbslab);
   CHECK_CONTIG(x); CHECK_CONTIG(dz); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
@@ -133,6 +153,7 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
                               int64_t S, int64_t Pin, int64_t Po, int variant,
                               const c10::optional<Tensor>& dgrad_mask = c10::nullopt,
                               const c10::optional<Tensor>& mbits = c10::nullopt) {
+  check_dev("conv_fwd_fp8_impl", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, c10::nullopt, c10::nullopt);
   // dgrad_mask given: fp8 dgrad (x = e5m2 gradients, w = transposed e4m3 weights, output masked
   // by dgrad_mask > 0, no bias, e5m2 y_fp8)
   CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);

@@ -15,6 +15,7 @@ void conv_fwd_lab(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
                   const c10::optional<Tensor>& mask, const Tensor& y, int64_t K, int64_t S, int64_t Pin, int64_t Po,
                   int64_t mode, const c10::optional<Tensor>& mbits, int64_t tile,
                   const c10::optional<Tensor>& stamps) {
+  check_dev("conv_fwd_lab", x, w, bias, mask, y, mbits, stamps);
   unsigned long long* dbg = nullptr;
   if (stamps.has_value()) {
     CHECK_DEV(*stamps);
@@ -26,6 +27,7 @@ void conv_fwd_lab(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
 
 void conv_wgrad_lab(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
                     int64_t Pin, int64_t Po, int64_t cin_real, int64_t variant) {
+  check_dev("conv_wgrad_lab", x, dz, slab, dbslab);
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }
 
@@ -33,6 +35,7 @@ void conv_fwd_fp8_lab(const Tensor& x, const Tensor& w, const Tensor& bias, cons
                       const Tensor& out_scale, const c10::optional<Tensor>& amax,
                       const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S,
                       int64_t Pin, int64_t Po, int64_t variant) {
+  check_dev("conv_fwd_fp8_lab", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8);
   conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, (int)variant);
 }
 

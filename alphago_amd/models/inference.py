@@ -54,7 +54,8 @@ class HipTrunkInference:
         self.buckets = sorted(buckets)
         self.use_graphs = use_graphs
         dev = self.device
-        self.wf = [ops.packed_weight_like(tr.weights[l], self.C0p if l == 0 else self.Fp, self.Fp)
+        # packed on the engine's device whatever device the module's parameters are on
+        self.wf = [ops.packed_weight_like(tr.weights[l], self.C0p if l == 0 else self.Fp, self.Fp, device=dev)
                    for l in range(self.L)]
         self.bias_p = [torch.zeros(self.Fp, device=dev) for _ in range(self.L)]
         self.head_w = torch.zeros(self.F, device=dev)

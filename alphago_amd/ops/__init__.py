@@ -198,7 +198,8 @@ def sgd_update_sched(p, g, sched, gscale: float = 1.0):
     _ops().sgd_update_sched(p, g, sched, gscale)
 
 
-def packed_weight_like(w_oihw: torch.Tensor, cin_p: int, cout_p: int, transposed: bool = False) -> torch.Tensor:
+def packed_weight_like(w_oihw: torch.Tensor, cin_p: int, cout_p: int, transposed: bool = False,
+                       device=None) -> torch.Tensor:
     """Zeroed packed bf16 weights (K*K, Cout, Cin) -- transposed (K*K, Cin, Cout) for dgrad.  When the
     reduction width (Cin, or Cout for dgrad) is an odd multiple of 32 there is one extra all-zero tap:
     the straddled K-steps' last half reads it."""
@@ -206,7 +207,7 @@ def packed_weight_like(w_oihw: torch.Tensor, cin_p: int, cout_p: int, transposed
     red = cout_p if transposed else cin_p
     T = K * K + (1 if red % 64 == 32 else 0)
     shape = (T, cin_p, cout_p) if transposed else (T, cout_p, cin_p)
-    return torch.zeros(shape, device=w_oihw.device, dtype=torch.bfloat16)
+    return torch.zeros(shape, device=w_oihw.device if device is None else device, dtype=torch.bfloat16)
 
 
 def wgrad_tap_group(cout_p: int, cin_p: int, K: int) -> int:

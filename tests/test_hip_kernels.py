@@ -470,3 +470,21 @@ def test_dense_f32_vs_torch(ops, cuda_device, M, N, K, ta, tb, bias, beta):
     C2 = C0.clone()
     ops.dense_f32(A, B, C2, bias=b, trans_a=ta, trans_b=tb, beta=beta)
     assert torch.equal(C, C2)  # deterministic
+
+
+@pytest.mark.gpu
+def test_ops_refuse_host_tensors(cuda_device):
+    """A host tensor handed to a kernel would fault the device; every op checks the
+    devices of its tensor arguments on the host and raises instead."""
+    from alphago_amd import ops
+
+    ops.load()
+    w = torch.randn(192, 64, 3, 3, device=cuda_device)
+    wf_host = torch.zeros(9, 192, 64, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="expected a GPU tensor"):
+        ops.pack_weights([w], [wf_host])
+    p = torch.zeros(1000, device=cuda_device)
+    with pytest.raises(RuntimeError, match="expected a GPU tensor"):
+        ops.sgd_update(p, torch.zeros(1000), 0.1)
+    torch.cuda.synchronize()  # the device is still healthy
+    assert float(p.sum()) == 0.0
