@@ -33,6 +33,7 @@ class DistEnv:
     world_size: int = 1
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    forced: bool = False  # ALPHAGO_AMD_FORCE_DIST=1: a process group even at world 1
 
     @property
     def is_main(self) -> bool:
@@ -40,7 +41,7 @@ class DistEnv:
 
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.forced
 
 
 _ENV: Optional[DistEnv] = None
@@ -62,7 +63,12 @@ def init_from_env(device: str = "auto", timeout_s: float = 600.0) -> DistEnv:
     else:
         dev = torch.device("cpu")
     backend = "none"
-    if world > 1:
+    # ALPHAGO_AMD_FORCE_DIST=1 creates the process group at world 1 too, so every collective of
+    # the data-parallel path (broadcast, bucketed async all-reduce, barrier, metric reductions)
+    # runs through RCCL on a one-GPU box: RCCL refuses two ranks on one device
+    # (profiles/r2_rccl_same_gpu.md).
+    forced = world == 1 and os.environ.get("ALPHAGO_AMD_FORCE_DIST", "0") == "1"
+    if world > 1 or forced:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29500")
         backend = os.environ.get("ALPHAGO_AMD_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
@@ -80,7 +86,7 @@ def init_from_env(device: str = "auto", timeout_s: float = 600.0) -> DistEnv:
             dist.init_process_group(backend=backend, store=store, rank=rank, world_size=world, timeout=tmo, **kw)
         else:
             dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=tmo, **kw)
-    _ENV = DistEnv(rank=rank, local_rank=local, world_size=world, backend=backend, device=dev)
+    _ENV = DistEnv(rank=rank, local_rank=local, world_size=world, backend=backend, device=dev, forced=forced)
     return _ENV
 
 

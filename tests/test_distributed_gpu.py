@@ -83,3 +83,60 @@ def test_hip_dp_matches_single(cuda_device, F, L, NB):
         assert torch.allclose(grad, ref, rtol=5e-3, atol=1e-5)
         assert torch.allclose(w, ref_w, rtol=1e-4, atol=1e-6)
     assert torch.equal(res[0][1], res[1][1]) and torch.equal(res[0][3], res[1][3])  # replicas identical
+
+
+def _rccl_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      ALPHAGO_AMD_FORCE_DIST="1")
+    os.environ.pop("ALPHAGO_AMD_DIST_BACKEND", None)
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.parallel import dist as agdist
+    from alphago_amd.train.engine import HipPolicyTrainer
+
+    env = agdist.init_from_env()
+    assert env.backend == "nccl" and env.distributed
+    dev = env.device
+    torch.manual_seed(0)
+    net = PolicyNet(48, filters_per_layer=192, layers=12)
+    g = torch.Generator().manual_seed(5)
+    tr = HipPolicyTrainer(net, 32, lr=0.1, device=dev, bucket_mb=2.0)
+    tr.comm_events = []
+    for _ in range(3):
+        planes = torch.randint(0, 2, (32, 48, 19, 19), dtype=torch.uint8, generator=g).to(dev)
+        tgt = torch.randint(0, 361, (32,), dtype=torch.int32, generator=g).to(dev)
+        tr.step(planes, tgt)
+    stats = torch.ones(2, device=dev, dtype=torch.float64)
+    agdist.all_reduce_sum_(stats)
+    mx = agdist.all_reduce_max(3.5)
+    agdist.barrier()
+    torch.cuda.synchronize()
+    q.put((tr.fp.flat.cpu().numpy().copy(), len(tr.buckets), len(tr.comm_events), float(stats.sum()), mx))
+    agdist.shutdown()
+
+
+def test_rccl_path_world1_matches_local(cuda_device):
+    """The data-parallel collectives on RCCL itself (nccl backend, forced process group at
+    world 1 -- RCCL needs one GPU per rank): parameter broadcast, bucketed async all-reduce
+    during the backward, barrier and metric reductions run, and the weights equal the
+    non-distributed trainer's bit for bit (a 1-rank sum is the identity)."""
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.train.engine import HipPolicyTrainer
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    w, nb, nev, ssum, mx = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert nb > 1 and nev == 3 and ssum == 2.0 and mx == 3.5
+    torch.manual_seed(0)
+    net = PolicyNet(48, filters_per_layer=192, layers=12)
+    g = torch.Generator().manual_seed(5)
+    tr = HipPolicyTrainer(net, 32, lr=0.1, device=cuda_device, bucket_mb=2.0)
+    for _ in range(3):
+        planes = torch.randint(0, 2, (32, 48, 19, 19), dtype=torch.uint8, generator=g).to(cuda_device)
+        tgt = torch.randint(0, 361, (32,), dtype=torch.int32, generator=g).to(cuda_device)
+        tr.step(planes, tgt)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.from_numpy(w), tr.fp.flat.cpu())
