@@ -134,6 +134,16 @@ class ValueNet(nn.Module):
     def input_dim(self):
         return self.arch["input_dim"]
 
+    def flops_per_position(self) -> float:
+        """Forward FLOPs per board (2*MACs): trunk, 1x1 head conv, Dense(S*S -> dense), Dense(dense -> 1)."""
+        s2 = self.board * self.board
+        tot, cin = 0.0, self.trunk.in_planes
+        for k in self.trunk.widths:
+            tot += 2.0 * s2 * cin * self.trunk.filters * k * k
+            cin = self.trunk.filters
+        d = self.arch["dense"]
+        return tot + 2.0 * s2 * cin + 2.0 * s2 * d + 2.0 * d
+
     def forward_torch(self, x: torch.Tensor) -> torch.Tensor:
         h = self.trunk.forward_torch(x)
         z = F.conv2d(h, self.head_w.to(h.dtype), self.head_b.to(h.dtype)).flatten(1).float()

@@ -38,7 +38,7 @@ from ..models.policy import CNNPolicy, CNNValue
 from ..parallel import dist as agdist
 from ..search.selfplay import BatchedSampler
 from ..utils import faults
-from ..utils.metrics import MetricsLogger
+from ..utils.metrics import MetricsLogger, StepMetrics
 from ..utils.watchdog import Watchdog, enable_collective_timeouts
 from . import checkpoint as ckpt
 from .engine import make_value_trainer
@@ -196,7 +196,9 @@ def train_cli(argv=None):
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
     p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--metrics", default=None)
+    p.add_argument("--metrics", default=None, help="JSONL metrics file (per-epoch and per-step records)")
+    p.add_argument("--log-every", type=int, default=100,
+                   help="with --metrics: one per-step record every N steps (0 = epoch records only)")
     p.add_argument("--verbose", "-v", action="store_true")
     p.add_argument("--checkpoint-every", type=int, default=0,
                    help="also write the native checkpoint every N steps (0: end of epoch only)")
@@ -229,6 +231,9 @@ def train_cli(argv=None):
     meta = {"epochs": [], "best_epoch": 0, "training_data": a.train_data, "model_file": a.model,
             "data": {"rows_per_rank": agdist.all_gather_object(len(data)) if env.distributed else [len(data)]}}
     log = MetricsLogger(a.metrics if env.is_main else None)
+    # per-step records: "acc" is the sign agreement of v and z (the trainer's metric sum)
+    step_log = StepMetrics(log, a.log_every if a.metrics else 0, B * world, val.model.flops_per_position(), dev,
+                           trainer)
     steps = max(1, n_train // (B * world))
     ck_path = os.path.join(a.out_directory, "checkpoint.pt")
     cursor, start_epoch, start_step = 0, 0, 0
@@ -263,8 +268,9 @@ def train_cli(argv=None):
             x, z = data.batch(np.arange(cursor * B, (cursor + 1) * B) % max(1, n_my_tr))
             cursor += 1
             sym = torch.randint(0, 8, (B,), device=dev, dtype=torch.int32, generator=gen)
-            l, _ = trainer.step(x, z, sym)
+            l, c = trainer.step(x, z, sym)
             ls += l.double()
+            step_log.on_step(gstep, ep, l, c)
             wd.beat(gstep)
             if a.checkpoint_every and (gstep + 1) % a.checkpoint_every == 0 and step + 1 < steps:
                 save_native(ep, step + 1)

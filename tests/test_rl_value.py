@@ -132,9 +132,16 @@ def test_value_generate_and_train_cpu(tmp_path):
     v = CNNValue(VALUE_FEATURES, board=9, filters_per_layer=8, layers=2, dense=16, device=cpu)
     vj = str(tmp_path / "v.json")
     v.save_model(vj)
-    meta = value.train_cli([vj, data, str(tmp_path / "vout"), "-B", "4", "-E", "2", "--backend", "torch"])
+    mpath = str(tmp_path / "vm.jsonl")
+    meta = value.train_cli([vj, data, str(tmp_path / "vout"), "-B", "4", "-E", "2", "--backend", "torch",
+                            "--metrics", mpath, "--log-every", "2"])
     assert len(meta["epochs"]) == 2
     assert os.path.exists(str(tmp_path / "vout" / "weights.00001.hdf5"))
+    import json
+    recs = [json.loads(line) for line in open(mpath)]
+    steps = [r for r in recs if "step" in r]
+    assert steps and all(r["step"] % 2 == 0 and r["positions_per_s"] > 0 and r["tflops"] > 0 for r in steps)
+    assert len([r for r in recs if "step" not in r]) == 2
 
 
 @pytest.mark.gpu
