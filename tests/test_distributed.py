@@ -123,10 +123,21 @@ def test_dp_sharded_data_equals_single_process(tmp_path, resident):
     model = _model(tmp_path, "cpu")
     common = ["--epochs", "1", "-l", "64", "--backend", "torch", "--no-symmetries", "-r", "0.05",
               "--resident", resident]
-    r = _sl_cli_torchrun([model, data, str(tmp_path / "dp")] + common + ["-B", "8"], 2)
+    mdp, msp = str(tmp_path / "dp.jsonl"), str(tmp_path / "sp.jsonl")
+    r = _sl_cli_torchrun([model, data, str(tmp_path / "dp")] + common + ["-B", "8", "--metrics", mdp,
+                                                                       "--log-every", "2"], 2)
     assert r.returncode == 0, r.stderr[-3000:]
-    r = _sl_cli_torchrun([model, data, str(tmp_path / "sp")] + common + ["-B", "16"], 1)
+    r = _sl_cli_torchrun([model, data, str(tmp_path / "sp")] + common + ["-B", "16", "--metrics", msp,
+                                                                       "--log-every", "2"], 1)
     assert r.returncode == 0, r.stderr[-3000:]
+    # per-step records: the window loss is all-reduced over the ranks (a collective every
+    # rank joins), so 2 ranks x 8 boards report the loss of the same 16-board windows
+    sa = [json.loads(x) for x in open(mdp) if '"step"' in x]
+    sb = [json.loads(x) for x in open(msp) if '"step"' in x]
+    assert [x["step"] for x in sa] == [x["step"] for x in sb] == [2, 4]
+    assert all(x["world"] == 2 for x in sa) and all(x["world"] == 1 for x in sb)
+    for x, y in zip(sa, sb):
+        assert np.isclose(x["loss"], y["loss"], rtol=1e-4) and x["acc"] == y["acc"]
     a = ckpt.load(str(tmp_path / "dp" / "checkpoint.pt"))["trainer"]["flat"]
     b = ckpt.load(str(tmp_path / "sp" / "checkpoint.pt"))["trainer"]["flat"]
     assert torch.allclose(a, b, atol=1e-6, rtol=1e-4)
