@@ -54,6 +54,7 @@ class BatchingEvaluator(object):
         self._rows = 0  # boards queued
         self._cv = threading.Condition()
         self._closed = False
+        self._kind: Optional[str] = None  # "planes" or "items": one payload kind per batcher
         self._stats: Dict[str, float] = {"requests": 0, "boards": 0, "rounds": 0, "eval_s": 0.0, "errors": 0}
         self._worker = threading.Thread(target=self._loop, name="batcher-%s" % name, daemon=True)
         self._worker.start()
@@ -77,8 +78,7 @@ class BatchingEvaluator(object):
         fut: Future = Future()
         fut._ag_single = single  # type: ignore[attr-defined]
         with self._cv:
-            if self._closed:
-                raise RuntimeError("batcher %s is closed" % self.name)
+            self._check_open("planes")
             self._q.append(_Request(p, lg, fut, time.perf_counter()))
             self._rows += p.shape[0]
             self._cv.notify()
@@ -93,12 +93,20 @@ class BatchingEvaluator(object):
         fut: Future = Future()
         fut._ag_single = False  # type: ignore[attr-defined]
         with self._cv:
-            if self._closed:
-                raise RuntimeError("batcher %s is closed" % self.name)
+            self._check_open("items")
             self._q.append(_Request(items, None, fut, time.perf_counter()))
             self._rows += len(items)
             self._cv.notify()
         return fut
+
+    def _check_open(self, kind: str) -> None:
+        """(lock held) Refuse submissions after close() and a second payload kind."""
+        if self._closed:
+            raise RuntimeError("batcher %s is closed" % self.name)
+        if self._kind is None:
+            self._kind = kind
+        elif self._kind != kind:
+            raise ValueError("batcher %s takes %s requests, not %s" % (self.name, self._kind, kind))
 
     def evaluate(self, planes, legal=None, timeout: Optional[float] = None) -> np.ndarray:
         fut = self.submit(planes, legal)

@@ -52,6 +52,8 @@ def test_batcher_single_board_legal_and_oversized():
         big = np.ones((10, 3, 5, 5), np.uint8)
         assert b.evaluate(big).shape == (10, 1)  # larger than max_batch: a round of its own
         assert 10 in calls
+        with pytest.raises(ValueError, match="takes planes requests"):
+            b.submit_items([object()])  # one payload kind per batcher
 
 
 def test_batcher_errors_reach_every_client_and_worker_survives():
