@@ -242,3 +242,50 @@ def latency_summary(lat_s: List[float]) -> Tuple[float, float, float]:
         return 0.0, 0.0, 0.0
     a = np.sort(np.asarray(lat_s)) * 1e3
     return float(np.percentile(a, 50)), float(np.percentile(a, 99)), float(a[-1])
+
+
+class BatcherPool(object):
+    """Several batchers (typically one per GPU of a node, each owning that GPU's engine) behind
+    one ``submit``: a request goes to the batcher with the fewest queued boards, so load spreads
+    over the devices while each batcher still forms its own rounds.  ``evaluate`` / ``submit`` /
+    ``submit_items`` / ``stats`` / ``close`` mirror ``BatchingEvaluator``."""
+
+    def __init__(self, batchers: List[BatchingEvaluator]):
+        if not batchers:
+            raise ValueError("BatcherPool needs at least one batcher")
+        self.batchers = list(batchers)
+        self._rr = 0
+        self._lock = threading.Lock()
+
+    def _pick(self) -> BatchingEvaluator:
+        with self._lock:
+            self._rr = (self._rr + 1) % len(self.batchers)
+            order = self.batchers[self._rr:] + self.batchers[:self._rr]  # rotate: ties spread round-robin
+        return min(order, key=lambda b: b._rows)
+
+    def submit(self, planes, legal=None) -> Future:
+        return self._pick().submit(planes, legal)
+
+    def submit_items(self, items: list) -> Future:
+        return self._pick().submit_items(items)
+
+    def evaluate(self, planes, legal=None, timeout: Optional[float] = None) -> np.ndarray:
+        return self._pick().evaluate(planes, legal, timeout)
+
+    def stats(self) -> Dict[str, float]:
+        per = [b.stats() for b in self.batchers]
+        out: Dict[str, float] = {k: sum(s[k] for s in per) for k in ("requests", "boards", "rounds", "errors",
+                                                                     "queued_boards")}
+        out["mean_batch"] = out["boards"] / out["rounds"] if out["rounds"] else 0.0
+        out["per_device_boards"] = [s["boards"] for s in per]  # type: ignore[assignment]
+        return out
+
+    def close(self, timeout: float = 10.0) -> None:
+        for b in self.batchers:
+            b.close(timeout)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -27,7 +27,7 @@ from typing import Iterable, List, Optional, Sequence
 
 import numpy as np
 
-from .batcher import BatchingEvaluator, state_eval_fn
+from .batcher import BatcherPool, BatchingEvaluator, state_eval_fn
 
 
 class BadRequest(ValueError):
@@ -56,19 +56,28 @@ def _extend(st, moves, first: int, size: int) -> None:
             raise BadRequest("move %d: %r is illegal" % (i, m))
 
 
+def _batcher(nets, max_batch, max_wait_ms, name):
+    """One batcher per network copy (one per GPU); a pool when there are several."""
+    bs = [BatchingEvaluator(state_eval_fn(n), max_batch, max_wait_ms, "%s%d" % (name, i)) for i, n in enumerate(nets)]
+    return bs[0] if len(bs) == 1 else BatcherPool(bs)
+
+
 class GoService(object):
-    """Thread-safe evaluation front end over a policy (and optional value) network."""
+    """Thread-safe evaluation front end over a policy (and optional value) network.
+    ``policy`` / ``value`` may be lists of copies of one network on different GPUs: each
+    copy gets its own batcher and requests go to the least-loaded one."""
 
     def __init__(self, policy, value=None, max_batch: int = 256, max_wait_ms: float = 2.0, seed: int = 0,
                  cache_size: int = 4096):
-        self.policy = policy
-        self.value = value
-        self.size = policy.model.board
+        pols = list(policy) if isinstance(policy, (list, tuple)) else [policy]
+        vals = (list(value) if isinstance(value, (list, tuple)) else [value]) if value is not None else []
+        self.policy = pols[0]
+        self.value = vals[0] if vals else None
+        self.size = self.policy.model.board
         # requests carry GameStates; each round is featurised in one batched call
         # (GPU featurizer inside the HIP graph when the engine has one)
-        self.pol_batcher = BatchingEvaluator(state_eval_fn(policy), max_batch, max_wait_ms, "policy")
-        self.val_batcher = (BatchingEvaluator(state_eval_fn(value), max_batch, max_wait_ms, "value")
-                            if value is not None else None)
+        self.pol_batcher = _batcher(pols, max_batch, max_wait_ms, "policy")
+        self.val_batcher = _batcher(vals, max_batch, max_wait_ms, "value") if vals else None
         self._rng = np.random.default_rng(seed)
         self._rng_lock = threading.Lock()
         # Positions by move list (LRU).  A client that plays a game through a stateless API
@@ -236,9 +245,13 @@ def serve_cli(argv: Sequence[str]) -> int:
     p.add_argument("--max-batch", type=int, default=256)
     p.add_argument("--max-wait-ms", type=float, default=2.0)
     p.add_argument("--device", default=None, help="cuda:N or cpu (default: cuda:0 when available)")
+    p.add_argument("--devices", default=None,
+                   help="comma-separated devices (e.g. cuda:0,cuda:1,...): one network copy and batcher per "
+                        "device, requests to the least-loaded one")
     a = p.parse_args(list(argv))
-    pol = CNNPolicy.load_model(a.policy, device=a.device)
-    val = CNNValue.load_model(a.value, device=a.device) if a.value else None
+    devs = a.devices.split(",") if a.devices else [a.device]
+    pol = [CNNPolicy.load_model(a.policy, device=d) for d in devs]
+    val = [CNNValue.load_model(a.value, device=d) for d in devs] if a.value else None
     svc = GoService(pol, val, a.max_batch, a.max_wait_ms)
     srv = make_server(svc, a.host, a.port)
     print("serving on http://%s:%d" % srv.server_address[:2], flush=True)

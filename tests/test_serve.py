@@ -56,6 +56,32 @@ def test_batcher_single_board_legal_and_oversized():
             b.submit_items([object()])  # one payload kind per batcher
 
 
+def test_batcher_pool_spreads_load_and_keeps_rows():
+    """One batcher per device behind a pool: every request gets its own rows back and
+    both devices take work."""
+    from alphago_amd.serve import BatcherPool
+
+    calls0, calls1 = [], []
+    rng = np.random.default_rng(1)
+    reqs = [rng.integers(0, 2, (1, 3, 5, 5), dtype=np.uint8) for _ in range(96)]
+    out = [None] * len(reqs)
+    with BatcherPool([BatchingEvaluator(_rowsum_fn(calls0), max_batch=8, max_wait_ms=10),
+                      BatchingEvaluator(_rowsum_fn(calls1), max_batch=8, max_wait_ms=10)]) as pool:
+        def worker(k):
+            for i in range(k, len(reqs), 12):
+                out[i] = pool.evaluate(reqs[i])
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(12)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        st = pool.stats()
+    for r, o in zip(reqs, out):
+        np.testing.assert_array_equal(o[:, 0], r.reshape(1, -1).sum(1))
+    assert st["requests"] == 96 and sum(st["per_device_boards"]) == 96
+    assert min(st["per_device_boards"]) > 0 and calls0 and calls1
+
+
 def test_batcher_errors_reach_every_client_and_worker_survives():
     state = {"fail": True}
 
@@ -104,6 +130,33 @@ def test_service_matches_direct_evaluation():
             assert tuple(mv) == best
     finally:
         svc.close()
+
+
+def test_service_over_two_network_copies():
+    """GoService over two copies of the network (one per device in production): same answers."""
+    from alphago_amd.models.policy import CNNPolicy
+
+    torch.manual_seed(0)
+    pol = CNNPolicy(["board", "ones", "turns_since"], board=9, filters_per_layer=8, layers=2, device="cpu")
+    j = None
+    import tempfile, os
+    with tempfile.TemporaryDirectory() as d:
+        j = os.path.join(d, "m.json")
+        w = os.path.join(d, "w.hdf5")
+        pol.save_model(j, w)
+        copies = [CNNPolicy.load_model(j, device="cpu", weights_file=w) for _ in range(2)]
+    one = GoService(pol, None, max_batch=8, max_wait_ms=2)
+    two = GoService(copies, None, max_batch=8, max_wait_ms=2)
+    try:
+        for moves in random_positions(9, 8, max_moves=20, seed=4):
+            a, b = one.policy_moves(moves, top_k=3), two.policy_moves(moves, top_k=3)
+            assert [m[:2] for m in a["moves"]] == [m[:2] for m in b["moves"]]
+            for x, y in zip(a["moves"], b["moves"]):
+                assert abs(x[2] - y[2]) < 1e-6
+        assert "per_device_boards" in two.stats()["policy"]
+    finally:
+        one.close()
+        two.close()
 
 
 def test_position_cache_game_sessions():
