@@ -6,6 +6,7 @@
 // bounds-check failure recorded by the kernels.
 #pragma once
 #include <ATen/ATen.h>
+#include <c10/hip/HIPFunctions.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -21,23 +22,27 @@ inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a device tensor")
 
-// Every tensor argument of an op must live on the GPU: a host pointer handed to a
-// kernel faults the device (an illegal access can take the whole card down), so the
-// ops refuse it on the host first.  check_dev("op", a, b, ...) accepts tensors,
-// optional tensors and tensor lists.
-inline void check_dev_one(const char* op, const Tensor& t) {
+// Every tensor argument of an op must live on the current GPU: a host pointer (or another
+// device's memory) handed to a kernel faults the device (an illegal access can take the
+// whole card down), so the ops refuse it on the host first.  check_dev("op", a, b, ...)
+// accepts tensors, optional tensors and tensor lists.
+inline void check_dev_one(const char* op, c10::DeviceIndex dev, const Tensor& t) {
   TORCH_CHECK(!t.defined() || t.is_cuda(), op, ": tensor argument on ", t.device(), ", expected a GPU tensor");
+  TORCH_CHECK(!t.defined() || t.get_device() == dev, op, ": tensor argument on ", t.device(),
+              " but the current device is ", static_cast<int>(dev), " (kernels launch on the current device)");
 }
-inline void check_dev_one(const char* op, const c10::optional<Tensor>& t) {
-  if (t.has_value()) check_dev_one(op, *t);
+inline void check_dev_one(const char* op, c10::DeviceIndex dev, const c10::optional<Tensor>& t) {
+  if (t.has_value()) check_dev_one(op, dev, *t);
 }
-inline void check_dev_one(const char* op, at::TensorList l) {
-  for (const Tensor& t : l) check_dev_one(op, t);
+inline void check_dev_one(const char* op, c10::DeviceIndex dev, at::TensorList l) {
+  for (const Tensor& t : l) check_dev_one(op, dev, t);
 }
 template <typename... Ts>
 inline void check_dev(const char* op, const Ts&... ts) {
-  (check_dev_one(op, ts), ...);
+  const c10::DeviceIndex dev = c10::hip::current_device();
+  (check_dev_one(op, dev, ts), ...);
 }
+
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 #define CHECK_BF16(t) TORCH_CHECK((t).scalar_type() == at::kBFloat16, #t " must be bfloat16")
 #define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")

@@ -43,10 +43,12 @@ class BatchingEvaluator(object):
     whose result holds the request's rows, in order.  A request of k boards is never split
     across rounds.  A request larger than ``max_batch`` runs as a round of its own."""
 
-    def __init__(self, evaluate_fn: EvalFn, max_batch: int = 256, max_wait_ms: float = 2.0, name: str = "eval"):
+    def __init__(self, evaluate_fn: EvalFn, max_batch: int = 256, max_wait_ms: float = 2.0, name: str = "eval",
+                 device=None):
         if max_batch < 1:
             raise ValueError("max_batch must be >= 1")
         self.fn = evaluate_fn
+        self.device = device  # the engine's GPU: the worker thread makes it current before any launch
         self.max_batch = int(max_batch)
         self.max_wait = max(0.0, float(max_wait_ms)) / 1e3
         self.name = name
@@ -157,6 +159,12 @@ class BatchingEvaluator(object):
             return batch
 
     def _loop(self) -> None:
+        if self.device is not None:
+            import torch
+
+            dev = torch.device(self.device)
+            if dev.type == "cuda":
+                torch.cuda.set_device(dev)  # a thread's current device starts at 0
         while True:
             batch = self._take()
             if batch is None:
@@ -208,9 +216,10 @@ def state_eval_fn(net, threads: int = 8) -> Callable:
     get the round featurized in one native call (``states_to_uint8``)."""
     from .._native import engine as _native
 
-    eng = net.engine
-
     def fn(states, _legal):
+        # the engine is built on first use, in the batcher's worker thread, whose current
+        # device is the network's GPU (its weight packing and graph capture launch there)
+        eng = net.engine
         if getattr(eng, "supports_encoded", False):
             b, a, m, lad = _native().encode_batch(list(states), eng.needs_ladder, threads)
             out, _, bad = eng.evaluate_encoded(b, a, m, lad)

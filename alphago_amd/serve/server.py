@@ -58,7 +58,8 @@ def _extend(st, moves, first: int, size: int) -> None:
 
 def _batcher(nets, max_batch, max_wait_ms, name):
     """One batcher per network copy (one per GPU); a pool when there are several."""
-    bs = [BatchingEvaluator(state_eval_fn(n), max_batch, max_wait_ms, "%s%d" % (name, i)) for i, n in enumerate(nets)]
+    bs = [BatchingEvaluator(state_eval_fn(n), max_batch, max_wait_ms, "%s%d" % (name, i), device=n.device)
+          for i, n in enumerate(nets)]
     return bs[0] if len(bs) == 1 else BatcherPool(bs)
 
 
