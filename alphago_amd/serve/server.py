@@ -30,6 +30,9 @@ import numpy as np
 from .batcher import BatcherPool, BatchingEvaluator, state_eval_fn
 
 
+MAX_BODY = 1 << 20  # a 19x19 move list is a few KB
+
+
 class BadRequest(ValueError):
     pass
 
@@ -205,6 +208,10 @@ def _handler(service: GoService):
         def do_POST(self):
             try:
                 n = int(self.headers.get("Content-Length", "0"))
+                if n > MAX_BODY:
+                    self.close_connection = True  # the unread body stays on the socket
+                    self._send(413, {"error": "request body over %d bytes" % MAX_BODY})
+                    return
                 req = json.loads(self.rfile.read(n) or b"{}")
                 if not isinstance(req, dict):
                     raise BadRequest("body must be a JSON object")

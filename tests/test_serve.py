@@ -215,6 +215,9 @@ def test_http_endpoints_concurrent_clients():
         with pytest.raises(urllib.error.HTTPError) as e:
             post_json(url + "/v1/policy", {"moves": [[4, 4], [4, 4]]})  # occupied point
         assert e.value.code == 400
+        with pytest.raises(urllib.error.HTTPError) as e:
+            post_json(url + "/v1/policy", {"moves": [[0, 0]] * 200000})  # over the body cap
+        assert e.value.code == 413
         st = svc.stats()["policy"]
         assert st["requests"] >= 24 + 1
     finally:
