@@ -253,10 +253,17 @@ def serve_cli(argv: Sequence[str]) -> int:
     p.add_argument("--max-batch", type=int, default=256)
     p.add_argument("--max-wait-ms", type=float, default=2.0)
     p.add_argument("--device", default=None, help="cuda:N or cpu (default: cuda:0 when available)")
+    p.add_argument("--precision", default=None, choices=["bf16", "fp8"],
+                   help="GPU engine precision (fp8: e4m3 block-scaled MFMA convs; default bf16 or "
+                        "$ALPHAGO_AMD_PRECISION)")
     p.add_argument("--devices", default=None,
                    help="comma-separated devices (e.g. cuda:0,cuda:1,...): one network copy and batcher per "
                         "device, requests to the least-loaded one")
     a = p.parse_args(list(argv))
+    if a.precision:
+        import os
+
+        os.environ["ALPHAGO_AMD_PRECISION"] = a.precision  # read when each engine is built
     devs = a.devices.split(",") if a.devices else [a.device]
     pol = [CNNPolicy.load_model(a.policy, device=d) for d in devs]
     val = [CNNValue.load_model(a.value, device=d) for d in devs] if a.value else None

@@ -92,6 +92,8 @@ def _parser():
     p.add_argument("--weights", default=None, help="weights file (in out_directory) to resume from")
     p.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
+                   help="HIP backend conv forward precision (fp8: e4m3 block-scaled MFMA forward, bf16 backward)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-symmetries", action="store_true", help="disable random D4 augmentation")
     p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
@@ -181,8 +183,9 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
         iterations, cursor = int(state["trainer"]["iterations"]), int(state["cursor"])
 
     B = args.minibatch
+    pkw = {"precision": args.precision} if args.precision != "bf16" else {}
     trainer = make_policy_trainer(net, B, args.learning_rate, args.decay, backend=args.backend, device=dev,
-                                  iterations=iterations)
+                                  iterations=iterations, **pkw)
     if args.graph and hasattr(trainer, "enable_graphs"):
         trainer.enable_graphs()
     gen = torch.Generator(device=dev)

@@ -92,3 +92,12 @@ def test_step_metrics_jsonl_hip(tmp_path, cuda_device):
     steps, _ = _step_records(mpath)
     assert [r["step"] for r in steps] == [4, 8]
     assert all(r["hbm_gb"] > 0 and r["positions_per_s"] > 0 for r in steps)
+
+
+@pytest.mark.gpu
+def test_train_sl_fp8_forward_hip(tmp_path, cuda_device):
+    """train-sl --precision fp8: e4m3 block-scaled forward, bf16 backward, through the CLI."""
+    out = str(tmp_path / "out")
+    meta = run_training([_model(tmp_path, "cuda"), _data(tmp_path), out, "--epochs", "2", "-B", "32",
+                         "--backend", "hip", "--precision", "fp8", "-r", "0.05"])
+    assert len(meta["epochs"]) == 2 and np.isfinite(meta["epochs"][1]["loss"])
