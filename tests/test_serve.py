@@ -293,3 +293,37 @@ def test_service_gpu_featurizer_path_matches_planes_path(cuda_device):
                 assert abs(d[(x, y)] - p) < 1e-4
     finally:
         svc.close()
+
+
+def test_batcher_property_rows_and_bounds():
+    """Property check (hypothesis): for any mix of request sizes and any max_batch, each
+    request gets exactly its own rows back, and no round exceeds max_batch unless a single
+    oversized request fills it alone."""
+    from hypothesis import given, settings, strategies as st
+
+    @settings(max_examples=25, deadline=None)
+    @given(sizes=st.lists(st.integers(1, 9), min_size=1, max_size=40), mb=st.integers(1, 12))
+    def check(sizes, mb):
+        rounds = []
+
+        def fn(planes, legal):
+            rounds.append(planes.shape[0])
+            return planes[:, 0, 0, :1].astype(np.int64) * 1000 + planes[:, 0, 0, 1:2]
+
+        reqs = []
+        for i, k in enumerate(sizes):
+            p = np.zeros((k, 1, 1, 2), np.uint8)
+            p[:, 0, 0, 0] = i % 250
+            p[:, 0, 0, 1] = np.arange(k)
+            reqs.append(p)
+        with BatchingEvaluator(fn, max_batch=mb, max_wait_ms=0.5) as b:
+            futs = [b.submit(p) for p in reqs]
+            outs = [f.result(10) for f in futs]
+        for i, (k, o) in enumerate(zip(sizes, outs)):
+            assert o.shape == (k, 1)
+            np.testing.assert_array_equal(o[:, 0], (i % 250) * 1000 + np.arange(k))
+        for r in rounds:
+            assert r <= mb or r in sizes
+        assert sum(rounds) == sum(sizes)
+
+    check()
