@@ -140,15 +140,20 @@ def all_gather_object(obj):
 
 
 def make_buckets(segments: Sequence[Tuple[int, int]], bucket_bytes: int = 4 << 20,
-                 elem_bytes: int = 4) -> List[Tuple[int, int, List[int]]]:
+                 elem_bytes: int = 4, last_alone: bool = False) -> List[Tuple[int, int, List[int]]]:
     """Group per-layer flat segments (offset, numel) — given in *backward*
-    order — into contiguous buckets.  Returns [(offset, numel, [segment ids])]."""
+    order — into contiguous buckets.  Returns [(offset, numel, [segment ids])].
+    ``last_alone``: the last segment (the first layer, whose gradient is ready only at
+    the very end of the backward) gets a bucket of its own, so the bucket before it is
+    launched one layer earlier and overlaps the final dgrad + wgrad; only the small
+    first-layer all-reduce is left exposed."""
     buckets: List[Tuple[int, int, List[int]]] = []
     cur_lo = cur_hi = None
     cur_ids: List[int] = []
     for sid, (off, n) in enumerate(segments):
         lo, hi = off, off + n
-        if cur_ids and (hi - lo + (cur_hi - cur_lo)) * elem_bytes > bucket_bytes:
+        tail = last_alone and sid == len(segments) - 1 and len(segments) > 1
+        if cur_ids and (tail or (hi - lo + (cur_hi - cur_lo)) * elem_bytes > bucket_bytes):
             buckets.append((cur_lo, cur_hi - cur_lo, cur_ids))
             cur_ids, cur_lo, cur_hi = [], None, None
         if not cur_ids:

@@ -222,7 +222,7 @@ class HipConvTrainer:
             _, nb = self.fp.segments["b%d" % l]
             segs.append((ow, nw + nb))
             self._seg_layer.append(l)
-        self.buckets = agdist.make_buckets(segs, int(bucket_mb * (1 << 20)))
+        self.buckets = agdist.make_buckets(segs, int(bucket_mb * (1 << 20)), last_alone=True)
         self._bucket_after_layer = {}
         for bi, (_, _, ids) in enumerate(self.buckets):
             last = ids[-1]

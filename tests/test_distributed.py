@@ -81,6 +81,9 @@ def test_buckets_cover_flat_buffer():
     for (a0, a1), (b0, b1) in zip(covered, covered[1:]):
         assert a1 == b0
     assert [i for _, _, ids in b for i in ids] == [0, 1, 2, 3]
+    # the first layer (last in backward order) alone in the final bucket
+    b = agdist.make_buckets(segs, bucket_bytes=1 << 20, last_alone=True)
+    assert [ids for _, _, ids in b] == [[0, 1, 2], [3]] and b[-1][:2] == (0, 20)
 
 
 def _sl_cli_torchrun(args, nproc, timeout=300):
