@@ -1,6 +1,5 @@
 """Serving path: dynamic batcher and the HTTP/JSON position service."""
 import threading
-import time
 
 import numpy as np
 import pytest
