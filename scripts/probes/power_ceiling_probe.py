@@ -41,5 +41,11 @@ else:
     ops.pack_weights([w], [wf])
     bias = torch.zeros(F, device=dev)
     y = ops.padded_empty(B, S, 1, F, dev)
-    pf = run_for(lambda: ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1), 2 * B * S * S * F * F * 9)
+    flops = 2 * B * S * S * F * F * 9
+    if which == "conv":
+        pf = run_for(lambda: ops.conv_fwd(x, wf, bias, y, 3, S, 1, 1), flops)
+    else:  # kernel-lab tilings, e.g. lab5 = compact halo + ping-pong, lab2 = interior halo
+        tile = int(which[3:])
+        L = ops.lab()
+        pf = run_for(lambda: L.conv_fwd(x, wf, bias, None, y, 3, S, 1, 1, 0, None, tile, None), flops)
 print(json.dumps({"kernel": which, "pflops": round(pf, 3)}), flush=True)
