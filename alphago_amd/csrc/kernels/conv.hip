@@ -46,8 +46,14 @@ namespace agk {
 // all-zero weight tap (packed weights then hold K*K + 1 taps).
 // BN whose per-wave weight rows are not a multiple of 8 (BN = 160) stage the
 // weight tile as 8-row pieces dealt round-robin over the waves.
+// CO (chunk outer): the K loop runs the 64-channel chunk in the outer loop and
+// the taps inside it, instead of all chunks of one tap before the next tap.
+// A tile's pixel rows for one chunk (BM + 2 halo rows x 128 B) are then re-read
+// by the 9 taps while they are hot in the XCD's L2, where the tap-outer order
+// cycles through every chunk of the tile (BM x Cin x 2 B per tile, ~5 MB for
+// the 32 tiles of an XCD at Cin 192 -- more than its 4 MB L2).
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
-          bool STR = false>
+          bool STR = false, bool CO = false>
 __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
   constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
@@ -64,6 +70,7 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   static_assert(BN % 32 == 0 && BN % 8 == 0 && A_ROWS_PW % 8 == 0, "tile geometry");
   static_assert(!(BDIST && M32), "round-robin weight staging: not in the 32x32 loop");
   static_assert(!(STR && M32), "straddled K-steps: not in the 32x32 loop");
+  static_assert(!(STR && CO), "straddled K-steps: tap-outer order only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63;
@@ -150,6 +157,21 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   // branch-free cursor advance (selects), so a caller can interleave the
   // DMA with MFMAs inside one basic block
   auto st_advance = [&]() {
+    if constexpr (CO) {
+      st_t += 1;
+      st_kw += 1;
+      st_w += wtap;
+      st_a += a.Cin;
+      const bool wrap2 = st_kw == a.K;
+      st_kw = wrap2 ? 0 : st_kw;
+      st_a += wrap2 ? (a.HPi - a.K) * a.Cin : 0;
+      const bool wrapt = st_t == a.K * a.K;  // all taps of the chunk done: next chunk, tap 0
+      st_t = wrapt ? 0 : st_t;
+      st_w = wrapt ? 0 : st_w;
+      st_a = wrapt ? 0 : st_a;
+      st_c0 += wrapt ? 64 : 0;
+      return;
+    }
     st_c0 += 64;
     const bool wrap = STR ? st_c0 >= a.Cin : st_c0 == a.Cin;
     st_c0 = wrap ? st_c0 - a.Cin : st_c0;
@@ -530,16 +552,16 @@ static void launch_fwd_ga(const ConvFwdArgs& a, hipStream_t st) {
 #endif  // AGK_KERNEL_LAB
 
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
-          bool STR = false>
+          bool STR = false, bool CO = false>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR>,
+      (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR>), grid, dim3(BM / MBW * 8), smem,
-                     st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO>), grid, dim3(BM / MBW * 8),
+                     smem, st, a);
 }
 
 // 160-wide output tile (value net: 152 filters padded to 160 instead of 192);
@@ -548,9 +570,14 @@ template <int MODE, bool STR>
 static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
   if (bm == 384) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR>(a, st);
   else if (bm == 385) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR>(a, st);
+  else if (bm == 386 || bm == 387) {  // chunk-outer order: not with straddled K-steps (they keep tap-outer)
+    if constexpr (STR) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR>(a, st);
+    else if (bm == 386) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, false, true>(a, st);
+    else launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, false, true>(a, st);
+  }
   else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
   else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
-  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 128 / 256 / 384");
+  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 128 / 256 / 384-387");
 }
 
 
@@ -565,7 +592,10 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // automatic: 385 (the 384 tile with its DMA spread through the MFMAs);
   // alternating A/B, serial backward: SL 121.5-121.9k vs 120.0-120.7k pos/s,
   // value (160-wide, straddled K-steps) 140.1k vs 136.7k bf16 (profiles/r2_dma_spread.md)
-  if (bm == 0) bm = (a.M >= 384 * 512) ? 385 : (a.M >= 256 * 512) ? 256 : 128;
+  // automatic (round 3): 386 = 385 with the chunk-outer K order.  10 s power-limited runs at
+  // B = 2176 (profiles/r3_chunk_outer.md): 3x3 forward 515 -> 480 us, bitmask dgrad 497 -> 463 us;
+  // bench 120.8k -> 126.0k positions/s.  (The 160-wide straddled tiles keep the tap-outer order.)
+  if (bm == 0) bm = (a.M >= 384 * 512) ? (BN == 160 ? 385 : 386) : (a.M >= 256 * 512) ? 256 : 128;
   if constexpr (BN == 160) {
     if (a.Cin % 64 == 32) launch_fwd_160<MODE, true>(a, bm, st);
     else launch_fwd_160<MODE, false>(a, bm, st);
@@ -579,6 +609,9 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     // 385: the 384 tile with the next stage's LDS-DMA spread through the first
     // k-half's MFMAs instead of issued as one burst (kernel-lab tile 9)
     else if (bm == 385) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
+    // 386 / 387: 385 / 384 with the chunk-outer K order (CO above)
+    else if (bm == 386) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true, false, true>(a, st);
+    else if (bm == 387) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, false, false, true>(a, st);
 #ifdef AGK_KERNEL_LAB
     // kernel-lab tile codes (profiles/r1_fwd_kernel_experiments.md):
     // conv_fwd_variants.hip (-1, 2, 4, 5, 6, 32), 2560 (epilogue loads after the loop),

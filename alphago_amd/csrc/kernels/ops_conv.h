@@ -106,6 +106,7 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
     a.mask = bfp(*mask);
   }
   if (mbits.has_value()) {
+    CHECK_DEV(*mbits);
     TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
     const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
     TORCH_CHECK(mbits->numel() >= B * HPo * HPo * words, "mbits too small: need B*HPo*HPo*words");
@@ -126,6 +127,9 @@ inline void conv_wgrad_impl(const Tensor& x, const Tensor& dz, const Tensor& sla
   CHECK_DEV(x); CHECK_DEV(dz); CHECK_DEV(slab); CHECK_DEV(dbslab);
   CHECK_BF16(x); CHECK_BF16(dz); CHECK_F32(slab); CHECK_F32(dbslab);
   CHECK_CONTIG(x); CHECK_CONTIG(dz); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
+  TORCH_CHECK(x.dim() == 4 && dz.dim() == 4 && dz.size(0) == x.size(0), "x, dz: (B, HP, HP, C) with the same B");
+  TORCH_CHECK(x.size(2) == x.size(1) && dz.size(2) == dz.size(1), "x, dz: square padded boards");
+  TORCH_CHECK(x.numel() < (1ll << 31) && dz.numel() < (1ll << 31), "tensor too large for int32 offsets");
   const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3);
   const int64_t HPo = dz.size(1), Cout = dz.size(3);
   const int64_t nsplit = slab.size(0);
@@ -158,7 +162,7 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
                               int64_t S, int64_t Pin, int64_t Po, int variant,
                               const c10::optional<Tensor>& dgrad_mask = c10::nullopt,
                               const c10::optional<Tensor>& mbits = c10::nullopt) {
-  check_dev("conv_fwd_fp8_impl", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, c10::nullopt, c10::nullopt);
+  check_dev("conv_fwd_fp8_impl", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, dgrad_mask, mbits);
   // dgrad_mask given: fp8 dgrad (x = e5m2 gradients, w = transposed e4m3 weights, output masked
   // by dgrad_mask > 0, no bias, e5m2 y_fp8)
   CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -196,7 +200,7 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
   a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po; a.nch = (int)nch;
   if (dgrad_mask.has_value()) {
-    CHECK_BF16(*dgrad_mask); CHECK_CONTIG(*dgrad_mask);
+    CHECK_DEV(*dgrad_mask); CHECK_BF16(*dgrad_mask); CHECK_CONTIG(*dgrad_mask);
     TORCH_CHECK(y_bf16.has_value() && dgrad_mask->sizes() == y_bf16->sizes(), "dgrad: mask must match y_bf16");
     TORCH_CHECK(variant == 0, "dgrad: production kernel only");
     a.dgrad = 1;
@@ -205,6 +209,7 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
   if (mbits.has_value()) {
     TORCH_CHECK(!dgrad_mask.has_value() && variant == 0 && y_bf16.has_value(),
                 "mbits: production forward with a bf16 output only");
+    CHECK_DEV(*mbits);
     TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
     const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
     TORCH_CHECK(mbits->numel() >= B * HPo * HPo * words, "mbits too small: need B*HPo*HPo*words");

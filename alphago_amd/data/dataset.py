@@ -73,9 +73,14 @@ def block_shuffle(rows: np.ndarray, chunk_rows: int, seed: int, window: int = 16
 
 class _ChunkCache(object):
     """LRU of decoded chunks of one chunked dataset, kept in one preallocated
-    slot array so a batch gather is a single ``np.take`` (GIL released)."""
+    slot array so a batch gather is a single ``np.take`` (GIL released).
+
+    ``gather`` holds a lock for its whole duration: the prefetch worker and the
+    main thread (validation batches) share one cache, and an unlocked gather
+    could evict or overwrite a slot the other thread is about to read."""
 
     def __init__(self, ds, capacity: int, threads: int):
+        self.lock = threading.Lock()
         self.ds, self.cap, self.threads = ds, max(1, capacity), threads
         self.cr = ds.chunk_rows
         self.slots = np.zeros((self.cap * self.cr,) + tuple(ds.shape[1:]), ds.dtype)  # touched once
@@ -83,6 +88,10 @@ class _ChunkCache(object):
         self.free = list(range(self.cap))
 
     def gather(self, rows: np.ndarray, out: np.ndarray) -> None:
+        with self.lock:
+            self._gather(rows, out)
+
+    def _gather(self, rows: np.ndarray, out: np.ndarray) -> None:
         cids = rows // self.cr
         uniq = np.unique(cids)
         if len(uniq) > self.cap:  # batch wider than the cache: grow it

@@ -483,6 +483,8 @@ class H5File(H5Group):
                     out[self._heap_str(heap, noff)] = oaddr
 
     def _walk_chunk_btree(self, addr: int, rank: int):
+        if addr == UNDEF:  # no chunk written yet (libhdf5: UNDEF index address in the layout)
+            return
         h = self._read(addr, 24)
         if h[:4] != b"TREE":
             raise H5Error("bad chunk B-tree node")
@@ -793,8 +795,10 @@ class H5Writer(_WGroup):
         def key(row_off, size=0, mask=0):
             return struct.pack("<II", size, mask) + struct.pack("<%dQ" % rank, row_off, *([0] * (rank - 1)))
 
+        if not d.chunks:  # empty dataset: libhdf5 writes an UNDEF index address, not a fake chunk record
+            return UNDEF
         # level 0: (first key, last-bound key, node addr)
-        ents = d.chunks if d.chunks else [(0, UNDEF, 0, 0)]
+        ents = d.chunks
         level, nodes = 0, []
         groups = [ents[i:i + cap] for i in range(0, len(ents), cap)]
         base = self._tell()
@@ -841,7 +845,7 @@ class H5Writer(_WGroup):
             msgs = [
                 (0x0001, _space_msg(d.shape, (None,) + tuple(d.shape[1:]))),
                 (0x0003, _dtype_msg(d.dtype)),
-                (0x0005, bytes([2, 2, 2, 0])),  # fill value v2: alloc incremental, write if set, undefined
+                (0x0005, bytes([2, 3, 2, 0])),  # fill value v2: alloc incremental (3, as h5py for chunked), write if set, undefined
                 (0x0008, layout),
             ]
             if d.compression == "lzf":

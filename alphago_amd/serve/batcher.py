@@ -57,6 +57,7 @@ class BatchingEvaluator(object):
         self._cv = threading.Condition()
         self._closed = False
         self._kind: Optional[str] = None  # "planes" or "items": one payload kind per batcher
+        self._plane_shape: Optional[Tuple[int, int, int]] = None  # (C, S, S), pinned by the first request
         self._stats: Dict[str, float] = {"requests": 0, "boards": 0, "rounds": 0, "eval_s": 0.0, "errors": 0}
         self._worker = threading.Thread(target=self._loop, name="batcher-%s" % name, daemon=True)
         self._worker.start()
@@ -75,12 +76,19 @@ class BatchingEvaluator(object):
         if legal is not None:
             lg = np.asarray(legal, dtype=np.uint8)
             lg = lg[None] if lg.ndim == 1 else lg
-            if lg.shape[0] != p.shape[0]:
+            if lg.ndim != 2 or lg.shape[0] != p.shape[0]:
                 raise ValueError("legal mask rows do not match the planes")
+            if lg.shape[1] != p.shape[2] * p.shape[3]:
+                raise ValueError("legal mask width %d != S*S = %d" % (lg.shape[1], p.shape[2] * p.shape[3]))
         fut: Future = Future()
         fut._ag_single = single  # type: ignore[attr-defined]
         with self._cv:
             self._check_open("planes")
+            shp = tuple(p.shape[1:])
+            if self._plane_shape is None:
+                self._plane_shape = shp  # type: ignore[assignment]
+            elif shp != self._plane_shape:
+                raise ValueError("planes %s do not match this batcher's %s" % (shp, self._plane_shape))
             self._q.append(_Request(p, lg, fut, time.perf_counter()))
             self._rows += p.shape[0]
             self._cv.notify()
@@ -173,18 +181,20 @@ class BatchingEvaluator(object):
             if not live:
                 continue
             sizes = [r.n for r in live]
-            if isinstance(live[0].planes, list):
-                planes = [x for r in live for x in r.planes]
-            else:
-                planes = live[0].planes if len(live) == 1 else np.concatenate([r.planes for r in live])
             nrows = sum(sizes)
-            legal = None
-            if not isinstance(planes, list) and any(r.legal is not None for r in live):
-                S2 = planes.shape[2] * planes.shape[3]
-                legal = np.concatenate([r.legal if r.legal is not None else np.ones((r.planes.shape[0], S2), np.uint8)
-                                        for r in live])
             t0 = time.perf_counter()
             try:
+                # batch assembly inside the try: a failure reaches this round's futures instead of
+                # killing the worker (and with it every queued and later request)
+                if isinstance(live[0].planes, list):
+                    planes = [x for r in live for x in r.planes]
+                else:
+                    planes = live[0].planes if len(live) == 1 else np.concatenate([r.planes for r in live])
+                legal = None
+                if not isinstance(planes, list) and any(r.legal is not None for r in live):
+                    S2 = planes.shape[2] * planes.shape[3]
+                    legal = np.concatenate([r.legal if r.legal is not None
+                                            else np.ones((r.planes.shape[0], S2), np.uint8) for r in live])
                 out = np.asarray(self.fn(planes, legal))
                 if out.shape[0] != nrows:
                     raise RuntimeError("evaluate_fn returned %d rows for %d boards" % (out.shape[0], nrows))

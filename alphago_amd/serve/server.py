@@ -90,11 +90,15 @@ class GoService(object):
         self._cache: "OrderedDict[tuple, object]" = OrderedDict()
         self._cache_lock = threading.Lock()
         self.cache_size = cache_size
+        self.max_moves = 4 * self.size * self.size  # a few times S*S covers any real game
         self.cache_hits = 0
 
     # ------------------------------------------------------------ positions
     def position(self, moves: Optional[Iterable]) -> object:
-        key = tuple(None if m is None else tuple(int(v) for v in m) for m in (moves or []))
+        moves = list(moves or [])
+        if len(moves) > self.max_moves:  # bounds the parse work and the cached positions' history
+            raise BadRequest("%d moves: at most %d per request" % (len(moves), self.max_moves))
+        key = tuple(None if m is None else tuple(int(v) for v in m) for m in moves)
         if self.cache_size <= 0:
             return position_from_moves(self.size, key)
         base, done = None, 0
@@ -208,6 +212,10 @@ def _handler(service: GoService):
         def do_POST(self):
             try:
                 n = int(self.headers.get("Content-Length", "0"))
+                if n < 0:  # rfile.read(-1) would block this handler until the client closes
+                    self.close_connection = True
+                    self._send(400, {"error": "negative Content-Length"})
+                    return
                 if n > MAX_BODY:
                     self.close_connection = True  # the unread body stays on the socket
                     self._send(413, {"error": "request body over %d bytes" % MAX_BODY})

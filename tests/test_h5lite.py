@@ -69,3 +69,19 @@ def test_multilevel_group_btree(tmp_path):
     with H5File(p) as f:
         assert f.keys() == names
         assert f["k050"].read()[0] == 96 - 50
+
+
+def test_empty_chunked_dataset_has_no_chunk_records(tmp_path):
+    """an empty chunked dataset is written with an UNDEF chunk-index address (as libhdf5
+    does), not a fake chunk record; it reads back empty with an empty chunk index."""
+    p = str(tmp_path / "empty.h5")
+    with H5Writer(p) as f:
+        s = f.stream_dataset("states", (3, 5, 5), np.uint8, chunk_rows=16, compression="lzf")
+        s.finish()
+        f.create_chunked("full", np.arange(40, dtype=np.uint8).reshape(40, 1), chunk_rows=16)
+    r = H5File(p)
+    d = r["states"]
+    assert d.shape == (0, 3, 5, 5) and d.chunked
+    assert d.chunk_index() == []
+    assert d.read().shape == (0, 3, 5, 5)
+    assert np.array_equal(r["full"].read().ravel(), np.arange(40))

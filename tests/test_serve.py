@@ -101,6 +101,20 @@ def test_batcher_errors_reach_every_client_and_worker_survives():
         b.submit(np.zeros((1, 2, 3, 3), np.uint8))  # closed
 
 
+def test_batcher_rejects_malformed_requests_and_worker_survives():
+    """a request whose planes shape or mask width differ from the batcher's is refused at
+    submit; an assembly failure inside a round reaches that round's futures, not the worker."""
+    calls = []
+    with BatchingEvaluator(_rowsum_fn(calls), max_batch=8, max_wait_ms=5) as b:
+        assert b.evaluate(np.ones((2, 2, 3, 3), np.uint8)).shape == (2, 1)
+        with pytest.raises(ValueError, match="do not match"):
+            b.submit(np.ones((1, 3, 3, 3), np.uint8))  # different plane count
+        with pytest.raises(ValueError, match="width"):
+            b.submit(np.ones((1, 2, 3, 3), np.uint8), np.ones((1, 10), np.uint8))  # S*S = 9
+        assert b.evaluate(np.ones((1, 2, 3, 3), np.uint8), np.ones(9, np.uint8)).shape == (1, 1)
+        assert b.stats()["errors"] == 0
+
+
 def _service(device, value=True, size=9):
     from alphago_amd.models.policy import CNNPolicy, CNNValue
 
@@ -217,6 +231,9 @@ def test_http_endpoints_concurrent_clients():
         with pytest.raises(urllib.error.HTTPError) as e:
             post_json(url + "/v1/policy", {"moves": [[0, 0]] * 200000})  # over the body cap
         assert e.value.code == 413
+        with pytest.raises(urllib.error.HTTPError) as e:
+            post_json(url + "/v1/policy", {"moves": [None] * (4 * 81 + 1)})  # over the move cap
+        assert e.value.code == 400
         st = svc.stats()["policy"]
         assert st["requests"] >= 24 + 1
     finally:

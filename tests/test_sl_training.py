@@ -101,3 +101,50 @@ def test_train_sl_fp8_forward_hip(tmp_path, cuda_device):
     meta = run_training([_model(tmp_path, "cuda"), _data(tmp_path), out, "--epochs", "2", "-B", "32",
                          "--backend", "hip", "--precision", "fp8", "-r", "0.05"])
     assert len(meta["epochs"]) == 2 and np.isfinite(meta["epochs"][1]["loss"])
+
+
+def test_chunk_cache_threaded_gather_matches_reads(tmp_path):
+    """the prefetch worker and validation share one _ChunkCache; concurrent gathers
+    from two threads must return exactly the rows a direct read returns."""
+    import threading
+    from alphago_amd.data.dataset import _ChunkCache
+    from alphago_amd.io.h5lite import H5File, H5Writer
+    p = str(tmp_path / "chunked.h5")
+    rng = np.random.default_rng(1)
+    states = rng.integers(0, 255, (900, 3, 5, 5), dtype=np.uint8)
+    with H5Writer(p) as f:
+        f.create_chunked("states", states, chunk_rows=16, compression="lzf")
+    ds = H5File(p)["states"]
+    assert ds.chunked
+    cache = _ChunkCache(ds, capacity=4, threads=2)  # small: constant eviction
+    errors = []
+
+    def worker(seed):
+        r = np.random.default_rng(seed)
+        out = np.empty((32, 3, 5, 5), np.uint8)
+        for _ in range(150):
+            rows = r.integers(0, 900, 32)
+            cache.gather(rows, out)
+            if not np.array_equal(out, states[rows]):
+                errors.append(seed)
+                return
+
+    ts = [threading.Thread(target=worker, args=(s,)) for s in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors
+
+
+def test_streamed_chunked_data_with_validation_cpu(tmp_path):
+    """--resident no on an LZF-chunked file with a validation split: the prefetch worker decodes
+    ahead while the epoch-end validation reads the same chunk cache."""
+    if not os.path.exists(FIXTURE):
+        pytest.skip("reference fixture not present")
+    out = str(tmp_path / "out")
+    meta = run_training([_model(tmp_path, "cpu"), FIXTURE, out, "--epochs", "2", "-l", "256", "-B", "16",
+                         "--backend", "torch", "--resident", "no"])
+    assert meta["data"]["resident"] is False and meta["data"]["chunked"] is True
+    assert len(meta["epochs"]) == 2
+    assert all(np.isfinite(e["val_loss"]) for e in meta["epochs"])
