@@ -138,6 +138,9 @@ def _dispatch(argv: List[str]):
     if cmd == "value-generate":
         from .train.value import generate_cli
         return generate_cli(rest)
+    if cmd == "selfplay-mcts":
+        from .search.selfplay_mcts import selfplay_cli
+        return selfplay_cli(rest)
     if cmd == "train-value":
         from .train.value import train_cli
         return train_cli(rest)

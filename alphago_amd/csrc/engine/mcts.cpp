@@ -57,6 +57,7 @@ Forest::Forest(int n_trees, double c_puct, double lmbda, int rollout_limit, int 
   for (auto& t : trees_) {
     t.nodes.clear();
     t.nodes.push_back(make_node(-1, PASS, 1.f));
+    t.rng.seed(rng_());
   }
 }
 
@@ -251,26 +252,59 @@ void Forest::leaf_masks(uint8_t* out) const {
   }
 }
 
-double Forest::rollout(GameState& s) {
-  const int p0 = s.current_player;
-  std::vector<int> cand;
-  for (int it = 0; it < rollout_limit_ && !s.is_end_of_game; ++it) {
-    int mv = PASS;
-    for (int tries = 0; tries < 24; ++tries) {
-      int p = (int)(rng_() % (uint64_t)s.np);
-      if (s.board[p] == EMPTY && s.is_legal(p) && !s.is_eye(p, s.current_player)) {
-        mv = p;
-        break;
+static inline bool sensible(const GameState& s, int p) {
+  return p >= 0 && s.board[p] == EMPTY && s.is_legal(p) && !s.is_eye(p, s.current_player);
+}
+
+int Forest::rollout_move(const GameState& s, std::mt19937_64& rng, std::vector<int>& cand) const {
+  const int me = s.current_player;
+  const int last = s.history.empty() ? PASS : s.history.back();
+  if (rollout_kind_ == ROLLOUT_HEURISTIC && last != PASS) {
+    // 1) capture the group just played (or an enemy neighbour of it) when it is in atari;
+    // 2) save an own group next to the last move that it put in atari, if the escape
+    //    point gives it more than one liberty
+    const Geometry& g = *s.g;
+    for (int k = 0; k < g.nnbr[last] + 1; ++k) {
+      const int q = k == 0 ? last : g.nbr[last][k - 1];
+      if (s.board[q] == -me && s.libc[s.head[q]] == 1) {
+        const int lib = s.libs[s.head[q]].first();
+        if (sensible(s, lib)) return lib;
       }
     }
-    if (mv == PASS) {
-      cand.clear();
-      for (int p = 0; p < s.np; ++p)
-        if (s.is_legal(p) && !s.is_eye(p, s.current_player)) cand.push_back(p);
-      if (!cand.empty()) mv = cand[rng_() % cand.size()];
+    for (int k = 0; k < g.nnbr[last]; ++k) {
+      const int q = g.nbr[last][k];
+      if (s.board[q] == me && s.libc[s.head[q]] == 1) {
+        const int lib = s.libs[s.head[q]].first();
+        if (!sensible(s, lib)) continue;
+        int gain = 0;  // liberties of the escape point beyond the group's old one
+        for (int j = 0; j < g.nnbr[lib]; ++j) gain += s.board[g.nbr[lib][j]] == EMPTY;
+        if (gain >= 2) return lib;
+      }
     }
-    s.try_move(mv, 0);
+    // 3) half of the remaining moves answer locally (8-neighbourhood of the last move)
+    if (rng() & 1ull) {
+      int loc[8], nl = 0;
+      for (int k = 0; k < g.nnbr[last]; ++k)
+        if (sensible(s, g.nbr[last][k])) loc[nl++] = g.nbr[last][k];
+      for (int k = 0; k < g.ndiag[last]; ++k)
+        if (sensible(s, g.diag[last][k])) loc[nl++] = g.diag[last][k];
+      if (nl) return loc[rng() % (uint64_t)nl];
+    }
   }
+  for (int tries = 0; tries < 24; ++tries) {
+    const int p = (int)(rng() % (uint64_t)s.np);
+    if (sensible(s, p)) return p;
+  }
+  cand.clear();
+  for (int p = 0; p < s.np; ++p)
+    if (sensible(s, p)) cand.push_back(p);
+  return cand.empty() ? PASS : cand[rng() % cand.size()];
+}
+
+double Forest::rollout(GameState& s, std::mt19937_64& rng) const {
+  const int p0 = s.current_player;
+  std::vector<int> cand;
+  for (int it = 0; it < rollout_limit_ && !s.is_end_of_game; ++it) s.try_move(rollout_move(s, rng, cand), 0);
   return (double)(s.get_winner() * p0);
 }
 
@@ -310,7 +344,7 @@ void Forest::apply_range(int i0, int i1, const float* priors, const float* value
     double v = values ? (double)values[i] : 0.0;
     if (lmbda_ > 0) {
       GameState s2 = st;
-      double z = rollout(s2);
+      double z = rollout(s2, tr.rng);
       v = (1.0 - lmbda_) * v + lmbda_ * z;
     }
     nd.v0 = (float)v;
@@ -320,8 +354,9 @@ void Forest::apply_range(int i0, int i1, const float* priors, const float* value
 
 void Forest::apply(const float* priors, const float* values, const uint8_t* mask) {
   const int L = (int)pending_.size();
-  // rollouts draw from the shared RNG: keep them serial (and reproducible)
-  const int T = lmbda_ > 0 ? 1 : std::max(1, std::min(threads_, L / 64));
+  // rollouts draw from their tree's own stream, so they run on every worker (results are
+  // independent of the worker count); without rollouts small batches stay on one thread
+  const int T = std::max(1, std::min(threads_, lmbda_ > 0 ? L : L / 64));
   if (T == 1) {
     apply_range(0, L, priors, values, mask);
   } else {
@@ -347,7 +382,7 @@ void Forest::add_root_noise(int t, double alpha, double eps) {
   std::vector<double> d(r.nchild);
   double s = 0;
   for (auto& x : d) {
-    x = gam(rng_);
+    x = gam(tr.rng);
     s += x;
   }
   for (int i = 0; i < r.nchild; ++i) {
@@ -387,7 +422,7 @@ int Forest::best_move(int t, double temperature) {
     s += w[i];
   }
   if (s <= 0) return tr.nodes[r.first_child].move;
-  double x = std::uniform_real_distribution<double>(0, s)(rng_);
+  double x = std::uniform_real_distribution<double>(0, s)(trees_[t].rng);
   for (int i = 0; i < r.nchild; ++i) {
     x -= w[i];
     if (x <= 0) return tr.nodes[r.first_child + i].move;

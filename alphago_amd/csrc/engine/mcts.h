@@ -9,8 +9,9 @@
 // Fixes over the reference: the root's visit count is
 // maintained and u = c·P·sqrt(ΣN)/(1+N) is evaluated at selection time (Q3);
 // values are backed up negamax-style from the side-to-move perspective (Q4);
-// rollouts are optional (λ = 0 is first class) and sample uniformly among
-// sensible moves instead of printing a warning at the limit (Q5).
+// rollouts are optional (λ = 0 is first class), sample from a cheap native
+// rollout policy instead of printing a warning at the limit (Q5), and run in
+// parallel over trees (one random stream per tree).
 #pragma once
 
 #include <cstdint>
@@ -79,7 +80,16 @@ struct SearchTree {
   NodeStore spare;  // scratch for advance()'s subtree copy (keeps its blocks)
   GameState root_state;
   int64_t sims = 0;
+  // per-tree stream (rollouts, root noise, temperature sampling): trees are
+  // searched by different workers, and the results do not depend on the count
+  std::mt19937_64 rng;
   SearchTree() : root_state(19) {}
+};
+
+// rollout move choice (reference: any rollout_fn callable, mcts.py:128-140)
+enum RolloutPolicy : int {
+  ROLLOUT_RANDOM = 0,     // uniform over sensible moves (legal, not an own true eye)
+  ROLLOUT_HEURISTIC = 1,  // capture / atari escape at the last move, else near it (p = 1/2), else uniform
 };
 
 class Forest {
@@ -119,6 +129,8 @@ class Forest {
       for (int p = 0; p < nparts; ++p) fn(p);
   }
   void add_root_noise(int t, double alpha, double eps);
+  void set_rollout_policy(int kind) { rollout_kind_ = kind; }
+  int rollout_policy() const { return rollout_kind_; }
   // Root statistics
   void root_stats(int t, std::vector<int>& moves, std::vector<int>& visits, std::vector<float>& q) const;
   int best_move(int t, double temperature);
@@ -130,7 +142,8 @@ class Forest {
 
  private:
   int select_child(const SearchTree& tr, int u) const;
-  double rollout(GameState& s);
+  double rollout(GameState& s, std::mt19937_64& rng) const;
+  int rollout_move(const GameState& s, std::mt19937_64& rng, std::vector<int>& cand) const;
   void backup(SearchTree& tr, int leaf, double v_leaf_to_move, bool remove_vl);
 
   std::vector<SearchTree> trees_;
@@ -143,7 +156,8 @@ class Forest {
   std::vector<std::vector<int>> leaf_paths_;
   double c_puct_, lmbda_;
   int rollout_limit_, playout_depth_, vloss_;
-  std::mt19937_64 rng_;
+  std::mt19937_64 rng_;  // seeds the per-tree streams
+  int rollout_kind_ = ROLLOUT_RANDOM;
   std::vector<int> fids_;
   int nplanes_ = 0;
   int64_t total_evals_ = 0;

@@ -132,6 +132,7 @@ void bind_mcts(py::module_& m) {
           },
           py::arg("priors"), py::arg("values") = py::none(), py::arg("mask") = py::none())
       .def("set_threads", &Forest::set_threads, py::arg("n"))
+      .def_property("rollout_policy", &Forest::rollout_policy, &Forest::set_rollout_policy)
       .def("add_root_noise", &Forest::add_root_noise, py::arg("tree"), py::arg("alpha") = 0.03,
            py::arg("eps") = 0.25)
       .def("root_stats",

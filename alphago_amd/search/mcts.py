@@ -83,10 +83,20 @@ class _ForestGroup(object):
 
 
 class BatchedMCTS(object):
+    ROLLOUT_POLICIES = {"random": 0, "heuristic": 1}
+
     def __init__(self, policy, value=None, n_trees: int = 1, c_puct: float = 5.0, lmbda: float = 0.0,
                  rollout_limit: int = 500, virtual_loss: int = 3, seed: int = 0, threads: Optional[int] = None,
-                 pipeline: Optional[bool] = None):
+                 pipeline: Optional[bool] = None, rollout_policy: str = "random", playout_depth: int = 1000):
+        """``rollout_policy`` (λ > 0): "random" = uniform over sensible moves, "heuristic" = capture /
+        atari escape at the last move, else a local answer half the time, else uniform (the native
+        stand-in for the reference's ``rollout_fn``, mcts.py:128-140).  Rollouts run in parallel
+        over trees (one random stream per tree)."""
+        if rollout_policy not in self.ROLLOUT_POLICIES:
+            raise ValueError("rollout_policy must be one of %s" % sorted(self.ROLLOUT_POLICIES))
         self.policy, self.value = policy, value
+        self.rollout_policy = rollout_policy
+        self.playout_depth = playout_depth
         self.pipeline = pipeline
         self.c_puct, self.lmbda, self.rollout_limit, self.vl, self.seed = c_puct, lmbda, rollout_limit, virtual_loss, seed
         # host worker threads (gather/apply/encode); a GPU box's process gets ~16 cores
@@ -111,8 +121,10 @@ class BatchedMCTS(object):
         sizes = [n_trees - n_trees // 2, n_trees // 2] if pipe and n_trees >= 2 else [n_trees]
         forests = []
         for k, n in enumerate(sizes):
-            f = _engine().Forest(n, self.c_puct, lm, self.rollout_limit, 1000, self.vl, self.seed + 7919 * k, pf)
+            f = _engine().Forest(n, self.c_puct, lm, self.rollout_limit, self.playout_depth, self.vl,
+                                 self.seed + 7919 * k, pf)
             f.set_threads(self.threads)
+            f.rollout_policy = self.ROLLOUT_POLICIES[self.rollout_policy]
             forests.append(f)
         self._forests = forests
         self.forest = forests[0] if len(forests) == 1 else _ForestGroup(forests)
@@ -213,39 +225,50 @@ class BatchedMCTS(object):
             values = self.value.engine.evaluate(vplanes).float().cpu().numpy()
         f.apply(probs, values)
 
-    def _sync_roots(self, states: Sequence) -> None:
-        for i, st in enumerate(states):
-            hist = st.history
+    def _sync_roots(self, states: Sequence, which: Optional[Sequence[int]] = None) -> None:
+        """Bring tree i's root to states[i]: advance through the moves played since (subtree reuse,
+        also across an opponent's reply), else a fresh tree."""
+        for i in (range(len(states)) if which is None else which):
+            st = states[i]
+            hist = list(st.history)
             prev = self._roots[i]
-            if prev is not None and len(hist) == len(prev) + 1 and hist[:-1] == prev:
+            if prev is not None and len(hist) > len(prev) and hist[:len(prev)] == prev:
                 try:
-                    self.forest.advance(i, hist[-1])
-                    self._roots[i] = list(hist)
+                    for mv in hist[len(prev):]:
+                        self.forest.advance(i, mv)
+                    self._roots[i] = hist
                     continue
                 except Exception:  # noqa: BLE001 - fall back to a fresh tree
                     pass
             if prev is None or hist != prev:
                 self.forest.set_root(i, st)
-                self._roots[i] = list(hist)
+                self._roots[i] = hist
 
     def search(self, states: Sequence, n_playout: int, leaves_per_tree: int = 16,
-               temperature: float = 0.0, noise: Optional[float] = None) -> List:
-        """Run ``n_playout`` simulations on every tree; return the chosen move per tree."""
+               temperature=0.0, noise: Optional[float] = None, active: Optional[Sequence[int]] = None) -> List:
+        """Run ``n_playout`` simulations on every tree (or only the trees in ``active``; the others
+        keep their roots and statistics); return the chosen move per tree (None for inactive trees).
+        ``temperature``: one value, or one per tree."""
         if len(states) != self._n:
             self.resize(len(states))
-        self._sync_roots(states)
+        act = list(range(self._n)) if active is None else sorted(set(int(i) for i in active))
+        self._sync_roots(states, act)
         fg = self.forest
-        # expand roots first (needed for root noise)
-        for k, f in enumerate(self._forests):
-            f.gather(1)
-            self._evaluate_pending(f, k)
-        if noise:
-            for i in range(self._n):
-                fg.add_root_noise(i, noise, 0.25)
         offs = [0]
         for f in self._forests:
             offs.append(offs[-1] + f.n_trees)
-        targets = [[fg.sims(offs[k] + j) + n_playout for j in range(f.n_trees)] for k, f in enumerate(self._forests)]
+        act_k = [[t - offs[k] for t in act if offs[k] <= t < offs[k + 1]] for k in range(len(self._forests))]
+        # expand roots first (needed for root noise)
+        for k, f in enumerate(self._forests):
+            if act_k[k]:
+                f.gather(1, act_k[k])
+                self._evaluate_pending(f, k)
+        if noise:
+            for i in act:
+                fg.add_root_noise(i, noise, 0.25)
+        on = set(act)
+        targets = [[fg.sims(offs[k] + j) + (n_playout if offs[k] + j in on else 0) for j in range(f.n_trees)]
+                   for k, f in enumerate(self._forests)]
 
         def gather(k):
             """Gather the next leaves of group k; False when its trees are done."""
@@ -290,7 +313,15 @@ class BatchedMCTS(object):
             for k in (0, 1):
                 if inflight[k] is not None:
                     self._finish(self._forests[k], inflight[k], pe, ve)
-        return [fg.best_move(i, temperature) for i in range(self._n)]
+        temps = list(temperature) if isinstance(temperature, (list, tuple, np.ndarray)) else [temperature] * self._n
+        return [fg.best_move(i, float(temps[i])) if i in on else None for i in range(self._n)]
+
+    def root_value(self, tree: int) -> float:
+        """Search value of the root for the player to move there: the visit-weighted mean child Q
+        (each child's Q is from the perspective of the player who moved into it)."""
+        _, visits, q = self.forest.root_stats(tree)
+        n = float(sum(visits))
+        return float(sum(v * x for v, x in zip(visits, q)) / n) if n > 0 else 0.0
 
     def visit_distribution(self, tree: int, size: int) -> np.ndarray:
         moves, visits, _ = self.forest.root_stats(tree)

@@ -1,0 +1,250 @@
+"""Does the search play well?  
+
+The reference tests only check MCTS selection order (/root/reference/tests/test_mcts.py:13-28).
+These tests would fail on a sign error in the negamax backup (csrc/engine/mcts.cpp backup) or a
+broken Q3/Q4 fix:
+
+* tactical: on random 5x5 / 7x7 positions with an exact-score value function (area score sign
+  for the player to move) and depth-2 playouts, the forest picks the unique move after which every
+  opponent reply still loses -- the depth-2 minimax answer, computed here by brute force;
+* strength: a lambda = 1 rollout MCTS (400 playouts) beats the raw random-init policy it searches
+  with (sampled directly) in > 70 % of 64 9x9 games;
+* determinism: with rollouts (lambda > 0) the forest gives identical trees for 1 and 8 worker
+  threads (one random stream per tree).
+"""
+import numpy as np
+import pytest
+
+from alphago_amd import go
+from alphago_amd._native import engine
+
+
+def _value(st):
+    """Exact area-score evaluation for the player to move (+1 win, -1 loss, 0 draw)."""
+    return float(st.get_winner() * st.current_player)
+
+
+def _sensible(st):
+    return [m for m in st.get_legal_moves() if not st.is_eye(m, st.current_player)]
+
+
+def _replies(st):
+    return _sensible(st) or [go.PASS_MOVE]
+
+
+def _after(st, m):
+    s = st.copy()
+    s.do_move(m)
+    return s
+
+
+def _unique_depth2_win(st):
+    """The one move after which every reply leaves the mover winning, or None."""
+    me = st.current_player
+    wins = []
+    for m in _replies(st):
+        s1 = _after(st, m)
+        if s1.is_end_of_game:
+            ok = s1.get_winner() == me
+        else:
+            ok = all(_after(s1, r).get_winner() == me for r in _replies(s1))
+        if ok:
+            wins.append(m)
+    return wins[0] if len(wins) == 1 and wins[0] is not go.PASS_MOVE else None
+
+
+def _random_position(size, rng, komi):
+    st = go.GameState(size, komi)
+    for _ in range(int(rng.integers(size * size // 3, size * size))):
+        ms = _sensible(st)
+        if not ms:
+            break
+        st.do_move(ms[int(rng.integers(len(ms)))])
+        if st.is_end_of_game:
+            break
+    return st
+
+
+def _search(st, playouts, seed=0):
+    """Depth-2 playouts, uniform priors, exact leaf values (lambda = 0)."""
+    f = engine().Forest(1, 1.5, 0.0, 0, 2, 1, seed, [])
+    f.set_root(0, st)
+    n2 = st.size * st.size
+    guard = 0
+    while f.sims(0) < playouts and guard < 4 * playouts:
+        guard += 1
+        L = f.gather(1)
+        if L == 0:
+            continue
+        leaf = f.leaf_state(0)
+        f.apply(np.ones((1, n2), np.float32), np.array([_value(leaf)], np.float32))
+    return f.best_move(0, 0.0)
+
+
+@pytest.mark.parametrize("size,komi", [(5, 0.5), (7, 0.5)])
+def test_forest_finds_the_unique_winning_move(size, komi):
+    rng = np.random.default_rng(11 + size)
+    found = 0
+    tries = 0
+    while found < 4 and tries < 3000:
+        tries += 1
+        st = _random_position(size, rng, komi)
+        if st.is_end_of_game:
+            continue
+        win = _unique_depth2_win(st)
+        if win is None:
+            continue
+        n_root = len(_replies(st))
+        assert _search(st, 60 * n_root * n_root // 4 + 400, seed=tries) == win, (size, tries, win)
+        found += 1
+    assert found >= 2, "no tactical positions found (generator too weak)"
+
+
+def test_rollouts_are_reproducible_across_thread_counts():
+    """lambda > 0: each tree draws from its own random stream, so apply() runs on every worker and
+    the trees are identical for any worker count."""
+    size = 7
+    rng = np.random.default_rng(3)
+    roots = [_random_position(size, rng, 7.5) for _ in range(12)]
+    out = []
+    for threads in (1, 8):
+        f = engine().Forest(len(roots), 5.0, 1.0, 200, 1000, 3, 5, [])
+        f.rollout_policy = 1
+        f.set_threads(threads)
+        for i, st in enumerate(roots):
+            f.set_root(i, st)
+        for _ in range(6):
+            L = f.gather(4)
+            if L:
+                f.apply(np.ones((L, size * size), np.float32), np.zeros(L, np.float32))
+        out.append([f.root_stats(i) for i in range(len(roots))])
+    assert out[0] == out[1]
+
+
+@pytest.mark.parametrize("policy_name", ["random", "heuristic"])
+def test_rollout_policies_finish_games(policy_name):
+    """Both native rollout policies play to the end of the game (two passes) within the limit."""
+    size = 9
+    f = engine().Forest(4, 5.0, 1.0, 400, 1000, 3, 2, [])
+    f.rollout_policy = {"random": 0, "heuristic": 1}[policy_name]
+    for i in range(4):
+        f.set_root(i, go.GameState(size, 7.5))
+    L = f.gather(1)
+    f.apply(np.ones((L, size * size), np.float32), np.zeros(L, np.float32))
+    _, visits, q = f.root_stats(0)
+    assert sum(visits) == 0 or all(-1.0 <= x <= 1.0 for x in q)
+    assert f.sims(0) == 1
+
+
+def test_rollout_mcts_beats_its_raw_policy():
+    """lambda = 1 (rollouts only, heuristic rollout policy) MCTS at 400 playouts vs the same
+    random-init policy network sampled directly: > 70 % of 64 9x9 games."""
+    import torch
+
+    from alphago_amd.models.policy import CNNPolicy
+    from alphago_amd.search.mcts import BatchedMCTS
+    from alphago_amd.search.selfplay import BatchedSampler
+    from alphago_amd.search.selfplay_mcts import mcts_vs_sampler
+
+    torch.manual_seed(0)
+    pol = CNNPolicy(["board", "ones", "turns_since", "sensibleness"], board=9, filters_per_layer=16, layers=3,
+                    device="cpu")
+    search = BatchedMCTS(pol, None, n_trees=64, lmbda=1.0, rollout_limit=200, seed=1, threads=8,
+                         rollout_policy="heuristic")
+    sampler = BatchedSampler(pol, temperature=1.0, seed=2)
+    res = mcts_vs_sampler(search, sampler, 64, 400, size=9, komi=7.5, leaves_per_tree=16)
+    assert res["mcts_win_rate"] > 0.70, res
+
+
+def _small_models(tmp_path, size=9):
+    import torch
+
+    from alphago_amd.models.policy import CNNPolicy, CNNValue
+    torch.manual_seed(0)
+    pol = CNNPolicy(["board", "ones", "turns_since", "sensibleness"], board=size, filters_per_layer=8, layers=2,
+                    device="cpu")
+    val = CNNValue(["board", "ones", "turns_since", "color"], board=size, filters_per_layer=8, layers=2, dense=8,
+                   device="cpu")
+    pj, vj = str(tmp_path / "pol.json"), str(tmp_path / "val.json")
+    pol.save_model(pj, str(tmp_path / "pol.h5"))
+    val.save_model(vj, str(tmp_path / "val.h5"))
+    return pol, val, pj, vj
+
+
+def test_selfplay_games_to_the_end_and_records(tmp_path):
+    """Full games (two passes, resignation or the move cap) with slots refilled, written as SGF +
+    (states, pi, outcomes, moves, game) HDF5 rows that replay the games exactly."""
+    from alphago_amd.io.h5lite import H5File
+    from alphago_amd.io.sgf import parse
+    from alphago_amd.search.selfplay_mcts import MCTSConfig, SelfPlayWriter, play_selfplay
+
+    pol, val, _, _ = _small_models(tmp_path)
+    cfg = MCTSConfig(n_playout=24, leaves_per_tree=4, lmbda=0.5, rollout_policy="heuristic", rollout_limit=120,
+                     temp_moves=6, resign=-0.9, resign_moves=2)
+    h5, sgf = str(tmp_path / "sp.h5"), str(tmp_path / "sgf")
+    w = SelfPlayWriter(h5, sgf, size=9)
+    recs = []
+
+    def keep(r):
+        recs.append(r)
+        w.add(r)
+
+    play_selfplay(pol, val, n_games=6, concurrent=4, cfg=cfg, size=9, max_moves=120, seed=3, threads=4, on_game=keep)
+    n = w.close()
+    assert len(recs) == 6 and sorted(r.game_id for r in recs) == list(range(6))
+    for r in recs:
+        st = r.final_state
+        assert st.is_end_of_game or len(st.history) >= 120 or r.resigned
+        assert r.winner in (-1, 0, 1) and (not r.resigned or r.winner == -r.resigned)
+    f = H5File(h5)
+    assert f["states"].shape[0] == n == sum(len(r.pi) for r in recs) == f["pi"].shape[0]
+    pi = np.asarray(f["pi"].read())
+    assert np.allclose(pi.sum(1), 1.0, atol=1e-5) and pi.shape[1] == 82
+    z = np.asarray(f["outcomes"].read())
+    assert set(np.unique(z)) <= {-1, 0, 1}
+    # the stored planes are the positions before each searched move: replay game 0 and compare
+    from alphago_amd.features import VALUE_FEATURES, Preprocess
+    r0 = recs[0]
+    st = go.GameState(9, 7.5)
+    rows = np.nonzero(np.asarray(f["game"].read()) == r0.game_id)[0]
+    planes = f["states"].read()[rows]
+    pre = Preprocess(VALUE_FEATURES)
+    for k, row in enumerate(planes[:10]):
+        assert np.array_equal(row, pre.state_to_uint8(st))
+        assert z[rows[k]] == r0.winner * st.current_player
+        mv = r0.moves[k]
+        st.do_move(None if mv < 0 else divmod(mv, 9))
+    for r in recs:
+        txt = open(str(tmp_path / "sgf" / ("game_%06d.sgf" % r.game_id))).read()
+        assert len(parse(txt)) == 1
+
+
+def test_selfplay_cli_two_ranks_merge(tmp_path):
+    """selfplay-mcts under torchrun (2 gloo ranks): per-rank files merged by rank 0, game ids unique."""
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    from alphago_amd.io.h5lite import H5File
+
+    _, _, pj, vj = _small_models(tmp_path)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "run")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "alphago_amd", "selfplay-mcts", pj, out,
+           "--value-json", vj, "--games", "3", "--concurrent", "2", "--playouts", "16", "--leaves-per-tree", "4",
+           "--max-moves", "40", "--rollout-limit", "60", "--lmbda", "0.5"]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2", PYTHONPATH=root)
+    p = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    f = H5File(os.path.join(out, "selfplay.h5"))
+    g = np.asarray(f["game"].read())
+    assert len(np.unique(g)) == 6 and f["states"].shape[0] == len(g) == f["pi"].shape[0]
+    assert not os.path.exists(os.path.join(out, "selfplay.h5.rank0"))
+    import json
+    summ = json.load(open(os.path.join(out, "selfplay_summary.json")))
+    assert summ["games"] == 6 and summ["leaf_evals"] > 0 and summ["phases_rank0"]
