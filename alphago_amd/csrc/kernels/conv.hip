@@ -70,7 +70,6 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   static_assert(BN % 32 == 0 && BN % 8 == 0 && A_ROWS_PW % 8 == 0, "tile geometry");
   static_assert(!(BDIST && M32), "round-robin weight staging: not in the 32x32 loop");
   static_assert(!(STR && M32), "straddled K-steps: not in the 32x32 loop");
-  static_assert(!(STR && CO), "straddled K-steps: tap-outer order only");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int lane = threadIdx.x & 63;
@@ -123,7 +122,14 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     xo1 = xo0;
     wo0 = st_w + st_c0;
     wo1 = wo0;
-    if constexpr (STR) {
+    if constexpr (STR && CO) {
+      // chunk outer: the 64-channel chunks run full steps tap by tap; the 32-channel tail chunk
+      // (Cin % 64 == 32) pairs taps t and t+1 in one step (t = K*K: the all-zero extra tap)
+      const bool part = st_c0 + 64 > a.Cin;
+      const int a_next = st_a + (st_kw + 1 == a.K ? (a.HPi - a.K + 1) * a.Cin : a.Cin);
+      xo1 = part ? (st_t + 1 < a.K * a.K ? a_next : st_a) + st_c0 : xo0 + 32;
+      wo1 = part ? st_w + wtap + st_c0 : wo0 + 32;
+    } else if constexpr (STR) {
       const int c1 = st_c0 + 32;
       const bool nx = c1 >= a.Cin;  // the second half opens the next tap
       const int a_next = st_a + (st_kw + 1 == a.K ? (a.HPi - a.K + 1) * a.Cin : a.Cin);
@@ -158,12 +164,14 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   // DMA with MFMAs inside one basic block
   auto st_advance = [&]() {
     if constexpr (CO) {
-      st_t += 1;
-      st_kw += 1;
-      st_w += wtap;
-      st_a += a.Cin;
-      const bool wrap2 = st_kw == a.K;
-      st_kw = wrap2 ? 0 : st_kw;
+      // one tap (two in the STR tail chunk, whose steps pair taps)
+      const int nt = (STR && st_c0 + 64 > a.Cin) ? 2 : 1;
+      st_t += nt;
+      st_kw += nt;
+      st_w += nt * wtap;
+      st_a += nt * a.Cin;
+      const bool wrap2 = st_kw >= a.K;
+      st_kw = wrap2 ? st_kw - a.K : st_kw;
       st_a += wrap2 ? (a.HPi - a.K) * a.Cin : 0;
       const bool wrapt = st_t == a.K * a.K;  // all taps of the chunk done: next chunk, tap 0
       st_t = wrapt ? 0 : st_t;
@@ -570,11 +578,8 @@ template <int MODE, bool STR>
 static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
   if (bm == 384) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR>(a, st);
   else if (bm == 385) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR>(a, st);
-  else if (bm == 386 || bm == 387) {  // chunk-outer order: not with straddled K-steps (they keep tap-outer)
-    if constexpr (STR) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR>(a, st);
-    else if (bm == 386) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, false, true>(a, st);
-    else launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, false, true>(a, st);
-  }
+  else if (bm == 386) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR, true>(a, st);
+  else if (bm == 387) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR, true>(a, st);
   else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
   else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
   else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 128 / 256 / 384-387");
@@ -594,8 +599,9 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // value (160-wide, straddled K-steps) 140.1k vs 136.7k bf16 (profiles/r2_dma_spread.md)
   // automatic (round 3): 386 = 385 with the chunk-outer K order.  10 s power-limited runs at
   // B = 2176 (profiles/r3_chunk_outer.md): 3x3 forward 515 -> 480 us, bitmask dgrad 497 -> 463 us;
-  // bench 120.8k -> 126.0k positions/s.  (The 160-wide straddled tiles keep the tap-outer order.)
-  if (bm == 0) bm = (a.M >= 384 * 512) ? (BN == 160 ? 385 : 386) : (a.M >= 256 * 512) ? 256 : 128;
+  // bench 120.8k -> 126.0k positions/s.  The 160-wide straddled tiles run the same order with the
+  // 32-channel tail chunk's steps pairing two taps.
+  if (bm == 0) bm = (a.M >= 384 * 512) ? 386 : (a.M >= 256 * 512) ? 256 : 128;
   if constexpr (BN == 160) {
     if (a.Cin % 64 == 32) launch_fwd_160<MODE, true>(a, bm, st);
     else launch_fwd_160<MODE, false>(a, bm, st);
@@ -652,52 +658,7 @@ void launch_conv_fwd(const ConvFwdArgs& a_in, int mode, hipStream_t st) {
 }
 
 // ----------------------------------------------------------------- wgrad
-template <int N>
-__device__ __forceinline__ void lgkm_fence(bf16x4 (&a)[N], bf16x4 (&b)[N]) {
-  static_assert(N >= 1 && N <= 15, "lgkm_fence supports 1..15 pairs (30 asm operands)");
-  if constexpr (N == 15)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]), "+v"(a[11]), "+v"(b[11]), "+v"(a[12]), "+v"(b[12]), "+v"(a[13]), "+v"(b[13]), "+v"(a[14]), "+v"(b[14]));
-  else if constexpr (N == 14)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]), "+v"(a[11]), "+v"(b[11]), "+v"(a[12]), "+v"(b[12]), "+v"(a[13]), "+v"(b[13]));
-  else if constexpr (N == 13)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]), "+v"(a[11]), "+v"(b[11]), "+v"(a[12]), "+v"(b[12]));
-  else if constexpr (N == 12)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]), "+v"(a[11]), "+v"(b[11]));
-  else if constexpr (N == 11)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]), "+v"(a[10]), "+v"(b[10]));
-  else if constexpr (N == 10)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]), "+v"(a[9]), "+v"(b[9]));
-  else if constexpr (N == 9)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]), "+v"(a[8]), "+v"(b[8]));
-  else if constexpr (N == 8)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]), "+v"(a[7]), "+v"(b[7]));
-  else if constexpr (N == 7)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]), "+v"(a[6]), "+v"(b[6]));
-  else if constexpr (N == 6)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]), "+v"(a[5]), "+v"(b[5]));
-  else if constexpr (N == 5)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]), "+v"(a[4]), "+v"(b[4]));
-  else if constexpr (N == 4)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]), "+v"(a[3]), "+v"(b[3]));
-  else if constexpr (N == 3)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]), "+v"(a[2]), "+v"(b[2]));
-  else if constexpr (N == 2)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]), "+v"(a[1]), "+v"(b[1]));
-  else if constexpr (N == 1)
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(b[0]));
-}
-
-// ds_read_b64_tr_b16 through inline asm.  The builtin form makes hipcc wait
-// vmcnt(0) before every such read while any LDS-DMA is outstanding (it cannot
-// tell the read from the DMA target), which would drain the ring; the caller
-// waits lgkmcnt itself (lgkm_fence below) before touching the results.
-__device__ __forceinline__ bf16x4 ds_read_tr16_asm(const char* p) {
-  bf16x4 v;
-  const uint32_t off = (uint32_t)(uintptr_t)(AG_LDS(p));
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(off));
-  return v;
-}
-
+// (lgkm_fence / ds_read_tr16_asm: conv_common.h)
 
 // 512 threads = 8 waves as 2 (n) x 4 (c).  One pipeline stage = KSUB sub-steps
 // of 32 pixels (one barrier per KSUB*32 pixels); each sub-step region is laid
@@ -1173,10 +1134,39 @@ unsigned debug_error_fetch_and_clear(hipStream_t st) {
 }
 #endif
 
+void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3]) {
+  const int code = variant == 5 ? wgrad_row_code(Cout, Cin, cin_real, K) : 0;
+  if (code) {  // one kernel row per workgroup, one workgroup per CU (~170 VGPRs, 8 or 6 waves)
+    out[0] = K;
+    out[1] = wgrad_row_wgs_per_split(code, Cout, Cin, cin_real, K);
+    out[2] = 1;
+    return;
+  }
+  // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
+  const int taps = wgrad_tap_group(Cout, Cin, K, variant == 5 ? 0 : variant);
+  const bool c48 = cin_real <= 48 && Cin == 64;
+  const int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
+  const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;
+  out[0] = taps;
+  out[1] = (K * K / taps) * (Cout / wn) * (c48 ? 1 : Cin / wc);
+  out[2] = 2;
+}
+
 void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
   ConvWgradArgs a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
+  if (a.variant == 5) {
+    // one-kernel-row wgrad (conv_wgrad_row.hip), opt-in: in the power-limited steady state it ran
+    // 607-694 us per 192 -> 192 layer against 548-583 us for the per-tap kernel
+    // (profiles/r3_wgrad_row.md); layers it does not cover run the per-tap kernel
+    const int code = wgrad_row_code(a.Cout, a.Cin, a.cin_real, a.K);
+    if (code) {
+      wgrad_row_launch(code, a, st);
+      return;
+    }
+    a.variant = 0;
+  }
   const bool n192 = a.Cout % 192 == 0, c192 = a.Cin % 192 == 0;
   const bool n128 = a.Cout % 128 == 0, c128 = a.Cin % 128 == 0;
   if (a.Cout == 160) {  // value net (152 filters padded to 160)

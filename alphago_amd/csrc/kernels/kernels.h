@@ -36,7 +36,8 @@ struct ConvWgradArgs {
   int ksteps_per_split, nsplit;
   int cin_real;        // real input channels (<= Cin); the zero padding above it is skipped when possible
   FastDiv divSS, divS; // filled by the launcher
-  int variant;         // 0 = production kernel; 1-4 kernel-lab build only
+  int variant;         // 0 = production per-tap kernel; 5 = one-kernel-row wgrad (conv_wgrad_row.hip);
+                       // 1-4 kernel-lab build only
   long long x_elems, dz_elems;  // tensor extents (debug-build bounds checks)
 };
 
@@ -155,6 +156,13 @@ void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 int wgrad_tap_group(int Cout, int Cin, int K, int variant);  // taps per wgrad workgroup (tap-merged 64-wide c tiles)
+// one-kernel-row wgrad (conv_wgrad_row.hip): geometry code (0 = not applicable), grid per split, launch
+int wgrad_row_code(int Cout, int Cin, int cin_real, int K);
+int wgrad_row_wgs_per_split(int code, int Cout, int Cin, int cin_real, int K);
+void wgrad_row_launch(int code, const ConvWgradArgs& a, hipStream_t st);
+// launch plan of the wgrad that launch_conv_wgrad runs for this variant:
+// {taps per workgroup, workgroups per split, resident workgroups per CU}
+void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3]);
 // a launch the runtime must reject (block of 2048 threads): tests the error path
 void launch_invalid_config_probe(hipStream_t st);
 #ifdef AGK_DEBUG
@@ -185,6 +193,8 @@ void launch_fp8_grad_scales(unsigned* amax, int* gscales8, float* gosc, int L, i
 void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st);
 void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st);
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
+// RCCL all-reduce stand-in (comm_proxy.hip): channels workgroups copy n floats and hold their CUs wire_us
+void launch_comm_proxy(const float* src, float* dst, long n, int channels, double wire_us, hipStream_t st);
 
 // fp32 dense layer GEMM (value head): C[M][N] = beta*C + A.B (+ bias[n]);
 // A is [M][K] (lda) or, transposed, [K][M]; B is [K][N] (ldb) or [N][K]

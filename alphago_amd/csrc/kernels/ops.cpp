@@ -22,9 +22,11 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
 
 // slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
-                int64_t Pin, int64_t Po, int64_t cin_real) {
+                int64_t Pin, int64_t Po, int64_t cin_real, int64_t variant) {
   check_dev("conv_wgrad", x, dz, slab, dbslab);
-  conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, 0);
+  // production kernels only: 0 = per-tap kernel (default), 5 = one-kernel-row wgrad where it applies
+  TORCH_CHECK(variant == 0 || variant == 5, "conv_wgrad variant ", variant, " is not a production kernel (0, 5)");
+  conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }
 
 void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
@@ -381,6 +383,24 @@ int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) {
   return agk::wgrad_tap_group((int)cout, (int)cin, (int)K, 0);
 }
 
+// {taps per workgroup, workgroups per split, resident workgroups per CU} of the production wgrad
+std::vector<int64_t> wgrad_plan(int64_t cout, int64_t cin, int64_t cin_real, int64_t K, int64_t variant) {
+  int o[3];
+  agk::wgrad_plan((int)cout, (int)cin, (int)(cin_real > 0 && cin_real < cin ? cin_real : cin), (int)K, (int)variant, o);
+  return {o[0], o[1], o[2]};
+}
+
+void comm_proxy(const Tensor& src, const Tensor& dst, int64_t channels, double wire_us) {
+  check_dev("comm_proxy", src, dst);
+  TORCH_CHECK(src.scalar_type() == at::kFloat && dst.scalar_type() == at::kFloat && src.is_contiguous() &&
+                  dst.is_contiguous() && dst.numel() >= src.numel() && src.numel() % 4 == 0,
+              "comm_proxy: contiguous f32, dst >= src, numel % 4 == 0");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+              "comm_proxy: 16-byte aligned buffers");
+  agk::launch_comm_proxy(src.data_ptr<float>(), dst.data_ptr<float>(), src.numel(), (int)channels, wire_us, cur_stream());
+  launch_check("comm_proxy");
+}
+
 void sgd_update(const Tensor& p, const Tensor& g, double lr, double gscale) {
   check_dev("sgd_update", p, g);
   CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
@@ -499,7 +519,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
       "Tensor(b!)? mbits=None, int tile=0) -> ()");
-  m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0) -> ()");
+  m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0, int variant=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def(
       "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor? weight, Tensor(a!)? dz, Tensor(b!)? loss, "
@@ -513,6 +533,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P) -> ()");
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
+  m.def("comm_proxy(Tensor src, Tensor(a!) dst, int channels, float wire_us) -> ()");
   m.def("sgd_update_sched(Tensor(a!) p, Tensor g, Tensor(b!) sched, float gscale) -> ()");
   m.def("dense_f32(Tensor A, Tensor B, Tensor? bias, Tensor(a!) C, bool transA, bool transB, float beta) -> ()");
   // budget: node visits per capture / escape read; 4096 = lb::kLadderVisits (ladder_bb.h)
@@ -532,6 +553,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("fp8_act_scales(Tensor(a!) amax, Tensor(b!) scales8, Tensor(c!) osc, int margin) -> ()");
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("wgrad_tap_group(int cout, int cin, int K) -> int", &wgrad_tap_group);
+  m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant=0) -> int[]", &wgrad_plan);
   m.def("selftest_bad_launch() -> ()", &selftest_bad_launch);
   m.def("is_debug_build() -> bool", []() -> bool {
 #ifdef AGK_DEBUG
@@ -556,6 +578,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("value_out", &value_out);
   m.impl("pack_weights", &pack_weights);
   m.impl("sgd_update", &sgd_update);
+  m.impl("comm_proxy", &comm_proxy);
   m.impl("sgd_update_sched", &sgd_update_sched);
   m.impl("dense_f32", &dense_f32);
   m.impl("ladder_planes", &ladder_planes);

@@ -43,6 +43,12 @@ int64_t wgrad_tap_group_lab(int64_t cout, int64_t cin, int64_t K, int64_t varian
   return agk::wgrad_tap_group((int)cout, (int)cin, (int)K, (int)variant);
 }
 
+std::vector<int64_t> wgrad_plan_lab(int64_t cout, int64_t cin, int64_t cin_real, int64_t K, int64_t variant) {
+  int o[3];
+  agk::wgrad_plan((int)cout, (int)cin, (int)(cin_real > 0 && cin_real < cin ? cin_real : cin), (int)K, (int)variant, o);
+  return {o[0], o[1], o[2]};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(alphago_amd_lab, m) {
@@ -55,6 +61,7 @@ TORCH_LIBRARY(alphago_amd_lab, m) {
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
       "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, int variant) -> ()");
   m.def("wgrad_tap_group(int cout, int cin, int K, int variant) -> int", &wgrad_tap_group_lab);
+  m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant) -> int[]", &wgrad_plan_lab);
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {

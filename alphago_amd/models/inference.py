@@ -70,6 +70,10 @@ class HipTrunkInference:
             self.osc8 = torch.ones(L, device=dev)
             self.amax8 = ops.fp8_amax_buffer(L, dev)
             self.calibrated = False
+        # encoded path: also write the uint8 planes of every board into the bucket (RL learner records
+        # stay on the device, search/selfplay.py); toggled before capture (set_encoded_planes)
+        self.encoded_planes = False
+        self._last_bk = None
         self.fz = None
         if feature_list is not None:
             from ..ops.gpu_features import GpuFeaturizer
@@ -140,11 +144,25 @@ class HipTrunkInference:
     def _alloc_outputs(self, bk):
         bk.probs = torch.zeros((bk.B, self.S * self.S), device=self.device)
 
+    def set_encoded_planes(self, on: bool) -> None:
+        """Make the encoded path also write uint8 planes (``encoded_planes_view``); re-captures graphs."""
+        if bool(on) != self.encoded_planes:
+            self.encoded_planes = bool(on)
+            for bk in self._b.values():
+                bk.graph_enc = None
+
+    def encoded_planes_view(self, n: int) -> torch.Tensor:
+        """(n, C, S, S) uint8 device planes of the last encoded submission (valid until the bucket is
+        submitted again); needs ``set_encoded_planes(True)``."""
+        if not self.encoded_planes or self._last_bk is None:
+            raise RuntimeError("encoded planes are off")
+        return self._last_bk.planes[:n]
+
     def _trunk(self, bk, encoded: bool = False) -> torch.Tensor:
         if encoded:
             bk.ovf.zero_()
             self.fz.run(bk.e_board, bk.e_ages, bk.e_meta, bk.e_ladder, nhwc=bk.X0, P=self.P0, sensible=bk.legal,
-                        overflow=bk.ovf)
+                        overflow=bk.ovf, planes=bk.planes if self.encoded_planes else None)
         else:
             ops.pack_input(bk.planes, bk.X0, self.P0)
         if self.precision == "fp8" and not getattr(self, "_calibrating", False):
@@ -254,6 +272,7 @@ class HipTrunkInference:
             bk.graph_enc.replay()
         else:
             self._run(bk, True)
+        self._last_bk = bk
         host = None
         if to_host:
             if not hasattr(bk, "h_out"):

@@ -136,10 +136,11 @@ def mbits_words(cout_p: int) -> int:
     return cout_p // conv_n_tile(cout_p) * 8
 
 
-def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1, cin_real: int = 0):
+def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1, cin_real: int = 0, variant: int = 0):
     """Split-K weight gradient into ``slab``; ``cin_real`` (< padded Cin) lets
-    the kernel skip zero-padded input channels (only slab columns < cin_real are written)."""
-    _ops().conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real)
+    the kernel skip zero-padded input channels (only slab columns < cin_real are written).
+    ``variant``: 0 = per-tap kernel (default), 5 = one-kernel-row wgrad where it applies (opt-in)."""
+    _ops().conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, variant)
 
 
 def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, beta: float = 0.0):
@@ -166,6 +167,11 @@ def pack_input(planes_u8, out, P: int, sym=None, target=None, target_out=None):
 
 def pack_weights(ws, wf, wd=()):
     _ops().pack_weights(list(ws), list(wf), list(wd))
+
+
+def comm_proxy(src, dst, channels: int, wire_us: float):
+    """RCCL all-reduce stand-in on the current stream (csrc/kernels/comm_proxy.hip)."""
+    _ops().comm_proxy(src, dst, channels, wire_us)
 
 
 def sgd_update(p, g, lr: float, gscale: float = 1.0):
@@ -213,6 +219,24 @@ def packed_weight_like(w_oihw: torch.Tensor, cin_p: int, cout_p: int, transposed
 def wgrad_tap_group(cout_p: int, cin_p: int, K: int) -> int:
     """Kernel taps one wgrad workgroup covers (K for tap-merged 64-wide c tiles, else 1)."""
     return int(_ops().wgrad_tap_group(cout_p, cin_p, K))
+
+
+def wgrad_plan(cout_p: int, cin_p: int, K: int, cin_real: int = 0, variant: int = 0):
+    """(taps per workgroup, workgroups per split, resident workgroups per CU) of the wgrad kernel the
+    production library runs for this layer (conv_wgrad_row.hip where it applies, else conv.hip)."""
+    t, w, c = _ops().wgrad_plan(cout_p, cin_p, cin_real, K, variant)
+    return int(t), int(w), int(c)
+
+
+def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, target_wgs: int = 0,
+                 cus: int = 256, variant: int = 0) -> int:
+    """Pixel splits of the production wgrad: one resident round of workgroups over ``cus`` CUs
+    (``target_wgs`` > 0 overrides the workgroup count).  A second, partial round of workgroups costs
+    30-70 % (profiles/r2_wgrad_variants.md), so the grid never exceeds one round."""
+    _, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, variant)
+    target = target_wgs if target_wgs > 0 else cus * per_cu
+    nks = (M + 31) // 32
+    return max(1, min(target // per_split, nks))
 
 
 def wgrad_splits(M: int, T: int, n_tiles: int = 1, target_wgs: int = 512) -> int:

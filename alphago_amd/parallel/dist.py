@@ -101,6 +101,19 @@ def shutdown() -> None:
     _ENV = None
 
 
+def live_backend() -> str:
+    """The initialised process group's backend as torch reports it ("nccl" = RCCL on ROCm), or "none"."""
+    if dist.is_available() and dist.is_initialized():
+        return str(dist.get_backend())
+    return "none"
+
+
+def live_world_size() -> int:
+    if dist.is_available() and dist.is_initialized():
+        return int(dist.get_world_size())
+    return 1
+
+
 def barrier() -> None:
     if dist.is_available() and dist.is_initialized():
         if env().backend == "nccl":
@@ -186,3 +199,55 @@ class BucketAllReducer:
         for h in self.handles:
             h.wait()
         self.handles = []
+
+
+class CommProxy:
+    """One-GPU stand-in for the bucketed all-reduce (same launch points, same waits): each bucket
+    launches ``ops.comm_proxy`` on a high-priority side stream -- ``channels`` workgroups that read
+    the bucket (the gradient is never modified) and hold their CUs for the modelled ring time
+    ``latency_us + bytes * 2 (W-1) / W / busbw`` -- so the CU contention of an overlapped all-reduce
+    can be measured without a second GPU (RCCL refuses two ranks on one device).
+
+    Configured by ``ALPHAGO_AMD_COMM_PROXY=channels,busbw_GBps,world[,latency_us]``."""
+
+    def __init__(self, flat: torch.Tensor, buckets, channels: int = 16, busbw_gbs: float = 300.0, world: int = 8,
+                 latency_us: float = 15.0):
+        from .. import ops
+        self.ops = ops
+        self.flat, self.buckets = flat, buckets
+        self.channels = int(channels)
+        self.factor = 2.0 * (world - 1) / world
+        self.busbw = float(busbw_gbs) * 1e9
+        self.latency_us = float(latency_us)
+        n = max(b[1] for b in buckets) + 8
+        self.scratch = torch.empty(n, dtype=torch.float32, device=flat.device)
+        self.stream = torch.cuda.Stream(device=flat.device, priority=-1)
+        self.launched = False
+
+    @staticmethod
+    def from_env(flat, buckets):
+        spec = os.environ.get("ALPHAGO_AMD_COMM_PROXY", "")
+        if not spec:
+            return None
+        v = [float(x) for x in spec.split(",")]
+        return CommProxy(flat, buckets, int(v[0]), v[1] if len(v) > 1 else 300.0, int(v[2]) if len(v) > 2 else 8,
+                         v[3] if len(v) > 3 else 15.0)
+
+    def wire_us(self, bucket_idx: int) -> float:
+        return self.latency_us + self.buckets[bucket_idx][1] * 4 * self.factor / self.busbw * 1e6
+
+    def launch(self, bucket_idx: int) -> None:
+        off, n, _ = self.buckets[bucket_idx]
+        lo = off - off % 4  # 16-byte aligned float4 view (reads a few neighbours: read-only)
+        hi = min(self.flat.numel(), (off + n + 3) // 4 * 4)
+        hi = lo + (hi - lo) // 4 * 4
+        ev = torch.cuda.current_stream(self.flat.device).record_event()
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(ev)
+            self.ops.comm_proxy(self.flat[lo:hi], self.scratch, self.channels, self.wire_us(bucket_idx))
+        self.launched = True
+
+    def wait(self) -> None:
+        if self.launched:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
+            self.launched = False

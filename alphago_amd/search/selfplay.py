@@ -29,6 +29,7 @@ class BatchedSampler(object):
         self.threads = threads
         self._names = [f.lower() for f in policy.preprocessor.feature_list]
         self.gen = torch.Generator(device=policy.device)
+        self._bad: List[int] = []
         self.gen.manual_seed(seed)
 
     def featurize(self, states) -> np.ndarray:
@@ -42,6 +43,7 @@ class BatchedSampler(object):
         E = _engine()
         b, a, m, l = E.encode_batch(list(states), eng.needs_ladder, self.threads)
         probs, sens, bad = eng.evaluate_encoded(b, a, m, l)
+        self._bad = list(bad)
         if bad:  # eye recursion too deep for the kernel: recompute those rows from CPU planes
             sub = [states[i] for i in bad]
             masks = self.masks(sub)
@@ -51,16 +53,34 @@ class BatchedSampler(object):
             sens[bad] = torch.from_numpy(masks).to(sens.device)
         return probs, (sens != 0).any(1)
 
-    def select(self, states: Sequence, planes: Optional[np.ndarray] = None, need_planes: bool = True):
-        """Returns (moves list, planes uint8 array or None, flat move indices (-1 = pass))."""
+    def device_planes_ok(self) -> bool:
+        """The engine featurises on the device and can hand its uint8 planes back (HIP engines)."""
+        eng = self.policy.engine
+        return getattr(eng, "supports_encoded", False) and hasattr(eng, "set_encoded_planes")
+
+    def select(self, states: Sequence, planes: Optional[np.ndarray] = None, need_planes: bool = True,
+               device_planes: bool = False):
+        """Returns (moves list, planes or None, flat move indices (-1 = pass)).  ``device_planes``
+        (HIP engines): the planes come back as a (n, C, S, S) uint8 DEVICE tensor written by the
+        GPU featurizer of the same forward -- no host featurisation, no host copy -- valid until
+        the next select."""
         n = len(states)
         if n == 0:
             return [], None, np.zeros(0, np.int64)
         size = states[0].size
         eng = self.policy.engine
-        if planes is None and not need_planes and getattr(eng, "supports_encoded", False):
+        dev_planes = None
+        if device_planes and planes is None and self.device_planes_ok():
+            eng.set_encoded_planes(True)
             probs, has = self._probs_encoded(states, eng)
-        else:
+            dev_planes = eng.encoded_planes_view(n)
+            if self._bad:  # overflowed eye recursion: those rows from the host featurizer
+                dev_planes[self._bad] = torch.from_numpy(self.featurize([states[i] for i in self._bad])).to(
+                    dev_planes.device)
+            planes = dev_planes
+        elif planes is None and not need_planes and getattr(eng, "supports_encoded", False):
+            probs, has = self._probs_encoded(states, eng)
+        elif dev_planes is None:
             if planes is None:
                 planes = self.featurize(states)
             masks = self.masks(states)
@@ -95,20 +115,50 @@ class GameRecords:
     states: List = field(default_factory=list)               # final states
 
 
+class _DeviceRecordBuffer(object):
+    """Learner planes kept on the device: rows appended by device-to-device copies from the GPU
+    featurizer's output, per-game row lists; grows by doubling."""
+
+    def __init__(self, row_shape, device, capacity: int = 4096):
+        self.buf = torch.empty((capacity,) + tuple(row_shape), dtype=torch.uint8, device=device)
+        self.n = 0
+
+    def append(self, rows: torch.Tensor) -> np.ndarray:
+        k = rows.shape[0]
+        if self.n + k > self.buf.shape[0]:
+            nb = torch.empty((max(2 * self.buf.shape[0], self.n + k),) + tuple(self.buf.shape[1:]),
+                             dtype=torch.uint8, device=self.buf.device)
+            nb[:self.n].copy_(self.buf[:self.n])
+            self.buf = nb
+        self.buf[self.n:self.n + k].copy_(rows)
+        self.n += k
+        return np.arange(self.n - k, self.n)
+
+
 def play_games(learner: BatchedSampler, opponent: BatchedSampler, n_games: int, size: int = 19,
                komi: float = 7.5, max_moves: int = 500, rng: Optional[np.random.Generator] = None,
                record: bool = True, learner_colors: Optional[Sequence[int]] = None,
-               standard_two_pass: bool = False) -> GameRecords:
+               standard_two_pass: bool = False, device_records: Optional[bool] = None) -> GameRecords:
     """Play n_games learner-vs-opponent games in lock-step (reference
     make_training_pairs, reinforcement_policy_trainer.py:16-76).  The learner's
     colour is drawn per game and its training pairs use the state
     *before* its own move (Q6).  ``standard_two_pass`` ends a game after any two
-    consecutive passes instead of the reference rule (Q9, go.py:345-348)."""
+    consecutive passes instead of the reference rule (Q9, go.py:345-348).
+
+    ``device_records`` (default: whenever the learner's engine featurises on the GPU): the
+    learner's planes are the GPU featurizer's own output of the sampling forward, copied into a
+    device buffer -- no host featurisation, numpy round trip or re-upload; ``GameRecords.planes``
+    then holds one device tensor per game."""
     rng = rng or np.random.default_rng()
     states = [go.GameState(size, komi, standard_two_pass) for _ in range(n_games)]
     colors = list(learner_colors) if learner_colors is not None else \
         [int(c) for c in rng.choice([go.BLACK, go.WHITE], size=n_games)]
-    rec_p: List[List[np.ndarray]] = [[] for _ in range(n_games)]
+    device_records = record and learner.device_planes_ok() and (device_records is None or device_records)
+    dbuf = None
+    if record and device_records:
+        C = learner.policy.preprocessor.output_dim
+        dbuf = _DeviceRecordBuffer((C, size, size), learner.policy.device, capacity=max(256, n_games * 64))
+    rec_p: List[List] = [[] for _ in range(n_games)]
     rec_m: List[List[int]] = [[] for _ in range(n_games)]
     for ply in range(max_moves):
         active = [i for i in range(n_games) if not states[i].is_end_of_game]
@@ -119,10 +169,18 @@ def play_games(learner: BatchedSampler, opponent: BatchedSampler, n_games: int, 
         for group, sampler, is_learner in ((lturn, learner, True), (oturn, opponent, False)):
             if not group:
                 continue
-            moves, planes, idx = sampler.select([states[i] for i in group], need_planes=record and is_learner)
+            want = record and is_learner
+            moves, planes, idx = sampler.select([states[i] for i in group], need_planes=want,
+                                                device_planes=want and dbuf is not None)
+            rows = None
+            if want and dbuf is not None:
+                keep = [k for k in range(len(group)) if moves[k] is not go.PASS_MOVE]
+                if keep:
+                    sel = planes if len(keep) == len(group) else planes[torch.as_tensor(keep, device=planes.device)]
+                    rows = dict(zip(keep, dbuf.append(sel)))
             for k, i in enumerate(group):
-                if record and is_learner and moves[k] is not go.PASS_MOVE:
-                    rec_p[i].append(planes[k])
+                if want and moves[k] is not go.PASS_MOVE:
+                    rec_p[i].append(rows[k] if rows is not None else planes[k])
                     rec_m[i].append(int(idx[k]))
                 try:
                     states[i].do_move(moves[k])
@@ -136,6 +194,9 @@ def play_games(learner: BatchedSampler, opponent: BatchedSampler, n_games: int, 
         out.states.append(states[i])
         if record:
             C = learner.policy.preprocessor.output_dim
-            out.planes.append(np.stack(rec_p[i]) if rec_p[i] else np.zeros((0, C, size, size), np.uint8))
+            if dbuf is not None:
+                out.planes.append(dbuf.buf[torch.as_tensor(np.asarray(rec_p[i], np.int64), device=dbuf.buf.device)])
+            else:
+                out.planes.append(np.stack(rec_p[i]) if rec_p[i] else np.zeros((0, C, size, size), np.uint8))
             out.moves.append(np.asarray(rec_m[i], dtype=np.int64))
     return out

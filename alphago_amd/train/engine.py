@@ -121,10 +121,13 @@ class HipConvTrainer:
     """MFMA conv-trunk training engine; subclasses provide the head."""
 
     def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
-                 overlap: bool = False, wgrad_target_wgs: int = 512, iterations: int = 0, precision: str = "bf16",
+                 overlap: bool = False, wgrad_target_wgs: int = 0, iterations: int = 0, precision: str = "bf16",
                  wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: bool = False,
-                 reduce_stream: Optional[bool] = None):
+                 reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None):
         ops.load()
+        # wgrad kernel: 0 = per-tap kernel (default), 5 = one-kernel-row wgrad (opt-in, slower so far)
+        self.wgrad_variant = int(os.environ.get("ALPHAGO_AMD_WGRAD_VARIANT", "0")) if wgrad_variant is None \
+            else int(wgrad_variant)
         self.conv_tile = conv_tile  # forward/dgrad tiling: 0 = automatic, or 128 / 256 / 384 / 385
         if precision not in ("bf16", "fp8"):
             raise ValueError("precision must be bf16 or fp8")
@@ -188,9 +191,9 @@ class HipConvTrainer:
         for l in range(self.L):
             cin_p = self.C0p if l == 0 else self.Fp
             T = self.K[l] ** 2
-            tiles = max(1, (self.Fp // ops.conv_n_tile(self.Fp)) * (cin_p // ops.conv_n_tile(cin_p)))
-            taps = ops.wgrad_tap_group(self.Fp, cin_p, self.K[l])  # taps share one workgroup
-            ns = ops.wgrad_splits(M, T // taps, tiles, wgrad_target_wgs)
+            # one resident round of wgrad workgroups (the kernel's own occupancy, ops.wgrad_plan)
+            ns = ops.wgrad_nsplit(M, self.Fp, cin_p, self.K[l], self.C0 if l == 0 else 0, wgrad_target_wgs,
+                                  self._num_cus(), self.wgrad_variant)
             self.nsplit.append(ns)
             slab_max = max(slab_max, ns * T * self.Fp * cin_p)
             db_max = max(db_max, ns * self.Fp)
@@ -228,6 +231,13 @@ class HipConvTrainer:
             last = ids[-1]
             self._bucket_after_layer[self._seg_layer[last] if self._seg_layer[last] is not None else -1] = bi
         self.reducer = agdist.BucketAllReducer(self.fp.grad, self.buckets)
+        # one-GPU contention proxy of the overlapped all-reduce (ALPHAGO_AMD_COMM_PROXY, world 1 only)
+        self._proxy = agdist.CommProxy.from_env(self.fp.grad, self.buckets) if not self.env.distributed else None
+        if self._proxy is not None:
+            self.reducer = self._proxy
+        # ALPHAGO_AMD_DEFER_ALLREDUCE=1: launch every bucket after the backward instead of at its bucket
+        # point (no overlap, no CU contention with the dgrad / wgrad kernels)
+        self.defer_allreduce = os.environ.get("ALPHAGO_AMD_DEFER_ALLREDUCE", "0") == "1"
         if precision == "fp8":
             # fp8 forward (block-scaled MFMA) with bf16 activations kept for the
             # backward; per-tensor power-of-two scales, all device-side:
@@ -352,6 +362,12 @@ class HipConvTrainer:
         ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)
         self._fp8_calibrated = True
 
+    def _num_cus(self) -> int:
+        try:
+            return int(torch.cuda.get_device_properties(self.device).multi_processor_count)
+        except Exception:  # noqa: BLE001 - a query failure keeps the MI355X default
+            return 256
+
     def _wgrad_layer(self, l: int, red: bool = False) -> None:
         """wgrad(l) into a split slab, then the deterministic reduce into the flat grad (and
         the async all-reduce of a completed bucket when ``red``).  With the reduce stream the
@@ -366,11 +382,12 @@ class HipConvTrainer:
         sr = self.s_r
         if sr is not None and self._slab_free[i] is not None:
             torch.cuda.current_stream(self.device).wait_event(self._slab_free[i])
-        ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0)
+        ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0,
+                       variant=self.wgrad_variant)
 
         def reduce():
             ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)
-            if red and l in self._bucket_after_layer:
+            if red and not self.defer_allreduce and l in self._bucket_after_layer:
                 self.reducer.launch(self._bucket_after_layer[l])
 
         if sr is None:
@@ -386,8 +403,8 @@ class HipConvTrainer:
         ``reduce=False`` leaves the local gradient (gradient accumulation: the
         caller all-reduces the sum once)."""
         main = torch.cuda.current_stream(self.device)
-        red = reduce and self.env.distributed
-        if red and -1 in self._bucket_after_layer:
+        red = reduce and (self.env.distributed or self._proxy is not None)
+        if red and not self.defer_allreduce and -1 in self._bucket_after_layer:
             self.reducer.launch(self._bucket_after_layer[-1])
         for l in reversed(range(self.L)):
             if self.s_w is not None:
@@ -417,6 +434,9 @@ class HipConvTrainer:
         if self.s_r is not None:
             main.wait_stream(self.s_r)
         if red:
+            if self.defer_allreduce:
+                for bi in range(len(self.buckets)):
+                    self.reducer.launch(bi)
             if self.comm_events is not None:  # exposed all-reduce time (utils.metrics.StepMetrics)
                 e0 = torch.cuda.Event(enable_timing=True)
                 e0.record(main)
@@ -482,7 +502,11 @@ class HipConvTrainer:
         gt.copy_(targets, non_blocking=True)
         if gs is not None:
             gs.copy_(sym, non_blocking=True)
-        dist = self.env.distributed
+        # ALPHAGO_AMD_GRAPH_ALLREDUCE=1: the bucketed async all-reduce is captured inside the graph
+        # (launched at its bucket points on RCCL's stream, joined before the update), so a graph step
+        # keeps the eager step's overlap; by default the all-reduce runs eagerly between two graphs
+        cap_ar = self.env.distributed and os.environ.get("ALPHAGO_AMD_GRAPH_ALLREDUCE", "0") == "1"
+        dist = self.env.distributed and not cap_ar
 
         def grads():
             self.compute_grads(gp, gt, gs, None, reduce=not dist)

@@ -64,7 +64,9 @@ def rl_update(trainer, records, B: int, device, loss: str = "reinforce") -> dict
     C = trainer.net.trunk.in_planes
     S = trainer.net.board
     if X:
-        X, T, Z = np.concatenate(X), np.concatenate(T).astype(np.int32), np.concatenate(Z)
+        # device records (play_games on a HIP learner) stay on the device
+        X = torch.cat(X) if isinstance(X[0], torch.Tensor) else np.concatenate(X)
+        T, Z = np.concatenate(T).astype(np.int32), np.concatenate(Z)
     else:
         X, T, Z = np.zeros((0, C, S, S), np.uint8), np.zeros(0, np.int32), np.zeros(0, np.float32)
     n = len(T)
@@ -82,15 +84,20 @@ def _accumulate_grads(trainer, X, T, W, B, device, n_chunks) -> None:
     C, S = trainer.net.trunk.in_planes, trainer.net.board
     n_chunks = max(1, n_chunks)
     acc = torch.zeros_like(trainer.fp.grad) if n_chunks > 1 else None
+    on_dev = isinstance(X, torch.Tensor)
     for c in range(n_chunks):
         sl = slice(c * B, (c + 1) * B)
         xb, tb, wb = X[sl], T[sl], W[sl]
         pad = B - len(tb)
         if pad:
-            xb = np.concatenate([xb, np.zeros((pad, C, S, S), np.uint8)])
+            if on_dev:
+                xb = torch.cat([xb, torch.zeros((pad, C, S, S), dtype=torch.uint8, device=xb.device)])
+            else:
+                xb = np.concatenate([xb, np.zeros((pad, C, S, S), np.uint8)])
             tb = np.concatenate([tb, np.full(pad, -1, np.int32)])
             wb = np.concatenate([wb, np.zeros(pad, np.float32)])
-        trainer.compute_grads(torch.from_numpy(xb).to(device), torch.from_numpy(tb).to(device), None,
+        xt = xb.to(device) if on_dev else torch.from_numpy(xb).to(device)
+        trainer.compute_grads(xt, torch.from_numpy(tb).to(device), None,
                               torch.from_numpy(wb.astype(np.float32)).to(device), reduce=False)
         if acc is not None:
             acc += trainer.fp.grad
@@ -123,6 +130,8 @@ def _reference_bce_update(trainer, records, B, device) -> dict:
                 X, T, z = games[k]
             else:  # this rank has run out of games: contribute a zero gradient
                 X, T, z = np.zeros((0, C, S, S), np.uint8), np.zeros(0, np.int32), 0.0
+            if isinstance(X, torch.Tensor) and len(T) == 0:
+                X = np.zeros((0, C, S, S), np.uint8)
             n = len(T)
             W = np.full(n, z * B / max(1, n), np.float32)
             n_chunks = int(agdist.all_reduce_max(float((n + B - 1) // B)))

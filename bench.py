@@ -31,6 +31,23 @@ from alphago_amd.train.engine import make_policy_trainer  # noqa: E402
 PAPER_SL_POS_PER_S = 3000.0  # paper SL throughput, 50 GPUs aggregate (derived)
 
 
+def teacher_pool_on_device(args, dev, rank):
+    """Teacher-labelled pool (alphago_amd/data/synthetic.py): the same fixed teacher on every rank,
+    a different position stream per rank; the teacher is freed before the student trains."""
+    from alphago_amd.data.synthetic import teacher_pool
+    from alphago_amd.features import DEFAULT_FEATURES
+    from alphago_amd.models.policy import CNNPolicy
+    cpu_rng = torch.get_rng_state()
+    torch.manual_seed(4242)  # one teacher for all ranks
+    teacher = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=args.filters, layers=args.layers, device=dev)
+    torch.set_rng_state(cpu_rng)
+    planes, tgt = teacher_pool(args.pool, teacher, seed=7000 + rank)
+    del teacher
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    return torch.from_numpy(planes).to(dev), torch.from_numpy(tgt).to(dev)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -47,9 +64,12 @@ def main():
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--planes", type=int, default=48)
-    ap.add_argument("--lr", type=float, default=0.003)
+    ap.add_argument("--lr", type=float, default=0.03, help="reference SL default (-r 0.03, supervised_policy_trainer.py)")
     ap.add_argument("--backend", default="hip", choices=["hip", "torch"])
-    ap.add_argument("--pool", type=int, default=16384, help="synthetic positions resident on device")
+    ap.add_argument("--pool", type=int, default=65536, help="synthetic positions resident on device")
+    ap.add_argument("--data", default="teacher", choices=["teacher", "random"],
+                    help="teacher: random-game positions labelled by a fixed random-init teacher of the same "
+                         "architecture (learnable: top1_acc measures learning); random: random planes/labels")
     ap.add_argument("--overlap", action="store_true",
                     help="run the wgrad on a second stream beside the dgrad (slower on MI355X; default serial)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
@@ -57,8 +77,8 @@ def main():
     ap.add_argument("--graph", action="store_true", help="run each training step as a HIP-graph replay")
     ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 128, 256, 384, 385, 386, 387],
                     help="forward/dgrad conv tiling (0 = automatic)")
-    ap.add_argument("--wgrad-wgs", type=int, default=512,
-                    help="target workgroups per wgrad launch (sets the split-K factor)")
+    ap.add_argument("--wgrad-wgs", type=int, default=0,
+                    help="target workgroups per wgrad launch (sets the split-K factor; 0 = one resident round)")
     ap.add_argument("--reduce-stream", type=int, default=None, choices=[0, 1],
                     help="1: split-K wgrad reduce on a side stream beside the dgrad (default: engine default)")
     ap.add_argument("--profile", default=None,
@@ -77,11 +97,20 @@ def main():
     if args.graph:
         trainer.enable_graphs()
 
-    # synthetic dataset, resident in HBM (uint8 one-hot planes + move targets)
+    # synthetic dataset, resident in HBM (uint8 one-hot planes + move targets), built before the clock
     g = torch.Generator(device=dev)
     g.manual_seed(99 + env.rank)
-    pool = torch.randint(0, 2, (args.pool, args.planes, 19, 19), device=dev, dtype=torch.uint8, generator=g)
-    pool_tgt = torch.randint(0, 361, (args.pool,), device=dev, dtype=torch.int32, generator=g)
+    t_pool = time.perf_counter()
+    if args.data == "teacher" and args.planes == 48:
+        pool, pool_tgt = teacher_pool_on_device(args, dev, env.rank)
+        data_desc = ("synthetic: %d random-game positions per rank (48 native-featurized planes) labelled by a "
+                     "fixed random-init %dx%d teacher (D4-averaged argmax); random-init student" %
+                     (args.pool, args.layers, args.filters))
+    else:
+        pool = torch.randint(0, 2, (args.pool, args.planes, 19, 19), device=dev, dtype=torch.uint8, generator=g)
+        pool_tgt = torch.randint(0, 361, (args.pool,), device=dev, dtype=torch.int32, generator=g)
+        data_desc = "synthetic (random uint8 planes/targets, random-init weights)"
+    pool_s = time.perf_counter() - t_pool
 
     def batch():
         idx = torch.randint(0, args.pool, (args.batch,), device=dev, generator=g)
@@ -116,6 +145,8 @@ def main():
         warm_steps += 10
     loss_sum.zero_()
     corr_sum.zero_()
+    if hasattr(trainer, "comm_events") and (env.distributed or getattr(trainer, "_proxy", None) is not None):
+        trainer.comm_events = []  # (start, end) events around the backward's all-reduce wait, per step
     if dev.type == "cuda":
         torch.cuda.synchronize()
     agdist.barrier()
@@ -129,8 +160,13 @@ def main():
     agdist.barrier()
     if dev.type == "cuda":
         torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    dt = agdist.all_reduce_max(dt)
+    dt_rank = time.perf_counter() - t0
+    rank_ms = [round(float(v) / args.steps * 1e3, 3) for v in agdist.all_gather_object(dt_rank)]
+    dt = agdist.all_reduce_max(dt_rank)
+    comm = None
+    ev = getattr(trainer, "comm_events", None)
+    if ev:  # exposed all-reduce per step, max over ranks
+        comm = agdist.all_reduce_max(sum(a.elapsed_time(b) for a, b in ev) / len(ev))
     n = env.world_size
     stats = torch.stack([loss_sum, corr_sum]).double()
     agdist.all_reduce_sum_(stats)
@@ -153,10 +189,15 @@ def main():
             "vs_baseline": round(value / PAPER_SL_POS_PER_S, 2),
             "dtype": (args.precision if args.precision == "bf16" else "fp8-fwd/bf16-bwd") if args.backend == "hip"
             else "fp32",
-            "data": "synthetic (random uint8 planes/targets, random-init weights)",
+            "data": data_desc,
             "top1_acc": round(float(stats[1]) / positions, 4),
             "mean_loss": round(float(stats[0]) / positions, 4),
             "tflops": round(net.flops_per_position() * 3 * value / 1e12, 1),
+            "dist_backend": agdist.live_backend(),
+            "world_size": agdist.live_world_size(),
+            "rank_ms_per_step": rank_ms,
+            "allreduce_exposed_ms_per_step": None if comm is None else round(comm, 3),
+            "pool_build_s": round(pool_s, 1),
             "config": {
                 "model": "SL policy net (%d-layer, %d filters, %d planes)" % (args.layers, args.filters, args.planes),
                 "global_batch": args.batch * n,

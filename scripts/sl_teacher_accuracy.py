@@ -1,12 +1,21 @@
 """Top-1 accuracy of the SL pipeline on a learnable synthetic task (no expert
 games are available offline): positions from random games, labelled with the
 greedy move of a fixed random-init "teacher" policy network (12 x 192, 48
-planes), written to the training-HDF5 schema, then learned by a fresh student
-network through the real SL trainer CLI (``train/sl.py run_training``).  The
-student's held-out top-1 agreement with the teacher is the accuracy figure.
+planes; alphago_amd/data/synthetic.py), written to the training-HDF5 schema,
+then learned by a fresh student network through the real SL trainer CLI
+(``train/sl.py run_training``).  The student's held-out top-1 agreement with
+the teacher is the accuracy figure (reference metric:
+supervised_policy_trainer.py:199-200).
+
+H6 parity: ``--arms hip-bf16,hip-fp8fwd,torch-fp32`` trains the
+same student initialisation on the same data and seeds with the HIP bf16
+engine, the HIP fp8-forward engine and the fp32 PyTorch trainer.
+``--real-epochs E`` adds a real-move check: each arm also trains on four of the
+reference's Lee Sedol games (tests/test_data/sgf) and is scored on the fifth.
 
 Usage: python scripts/sl_teacher_accuracy.py OUT_DIR [--positions N] [--epochs E] [--lr R] [--batch B]
-Prints one JSON line with the per-epoch acc / val_acc from metadata.json."""
+       [--arms A,B,..] [--real-epochs E]
+Prints one JSON line with the per-arm, per-epoch acc / val_acc."""
 import argparse
 import json
 import os
@@ -18,29 +27,43 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from alphago_amd import go  # noqa: E402
-from alphago_amd._native import engine  # noqa: E402
 from alphago_amd.features import DEFAULT_FEATURES  # noqa: E402
 from alphago_amd.io.h5lite import H5Writer  # noqa: E402
 from alphago_amd.models.policy import CNNPolicy  # noqa: E402
 from alphago_amd.train.sl import run_training  # noqa: E402
 
 
-def random_game_states(n_positions, rng):
-    """Positions from random games (uniform over non-eye legal moves, 1 % passes)."""
-    out = []
-    while len(out) < n_positions:
-        gs = go.GameState()
-        for _ in range(int(rng.integers(20, 300))):
-            moves = gs.get_legal_moves(include_eyes=False)
-            if not moves or rng.random() < 0.01:
-                gs.do_move(go.PASS_MOVE)
-            else:
-                gs.do_move(moves[int(rng.integers(len(moves)))])
-            if gs.is_end_of_game:
-                break
-            out.append(gs.copy())
-    return out[:n_positions]
+def _real_games(out, features):
+    """The reference's five Lee Sedol games (tests/test_data/sgf) as 48-plane HDF5: the first four
+    for training, the fifth held out (all of its positions: a game-level split)."""
+    from alphago_amd.data.convert import GameConverter
+    sgf_dir = "/root/reference/tests/test_data/sgf"
+    games = sorted(os.path.join(sgf_dir, f) for f in os.listdir(sgf_dir) if "Lee" in f) if os.path.isdir(sgf_dir) \
+        else []
+    if len(games) < 2:
+        return None
+    conv = GameConverter(features)
+    tr, ho = os.path.join(out, "real_train.h5"), os.path.join(out, "real_heldout.h5")
+    conv.sgfs_to_hdf5(games[:-1], tr, 19)
+    conv.sgfs_to_hdf5(games[-1:], ho, 19)
+    return tr, ho, os.path.basename(games[-1])
+
+
+def _heldout_top1(model_json, weights, h5, dev):
+    """Top-1 agreement of the trained student with the held-out file's moves (legal-masked argmax)."""
+    from alphago_amd.io.h5lite import H5File
+    f = H5File(h5)
+    planes = np.asarray(f["states"].read())
+    acts = np.asarray(f["actions"].read()).astype(np.int64)
+    tgt = acts[:, 0] * 19 + acts[:, 1]
+    pol = CNNPolicy.load_model(model_json, device=dev, weights_file=weights)
+    probs = np.concatenate([pol.engine.evaluate(planes[i:i + 512]).float().cpu().numpy().copy()
+                            for i in range(0, len(planes), 512)])
+    return float((probs.argmax(1) == tgt).mean()), int(len(tgt))
+
+
+ARMS = {"hip-bf16": ["--backend", "hip"], "hip-fp8fwd": ["--backend", "hip", "--precision", "fp8"],
+        "torch-fp32": ["--backend", "torch"]}
 
 
 def main():
@@ -51,6 +74,11 @@ def main():
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--arms", default="hip-bf16",
+                    help="comma list of %s: the same data, student init and seeds per arm" % ",".join(ARMS))
+    ap.add_argument("--real-epochs", type=int, default=0,
+                    help=">0: also train each arm on 4 reference Lee Sedol games and report held-out top-1 on the "
+                         "fifth (real moves)")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
@@ -61,50 +89,53 @@ def main():
     torch.manual_seed(1000 + a.seed)
     teacher = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
     h5 = os.path.join(a.out, "teacher.h5")
-    n_done = 0
     with H5Writer(h5) as f:
         f.attrs["features"] = np.array([x.encode() for x in DEFAULT_FEATURES])
         f.attrs["board_size"] = np.int64(19)
         states_ds = f.stream_dataset("states", (teacher.preprocessor.output_dim, 19, 19), np.uint8)
-        actions = []
-        chunk = 8192
-        while n_done < a.positions:
-            sts = random_game_states(min(chunk, a.positions - n_done), rng)
-            planes = teacher.preprocessor.states_to_uint8(sts)
-            masks = engine().featurize_batch(sts, ["sensibleness"], 16).reshape(len(sts), -1)
-            probs = []
-            for i in range(0, len(sts), 1024):
-                p = teacher.engine.evaluate(planes[i:i + 1024], masks[i:i + 1024]).float().cpu().numpy()
-                probs.append(p.copy())
-            probs = np.concatenate(probs) * (masks > 0)
-            has = masks.sum(1) > 0
-            idx = np.argmax(probs, axis=1)
-            keep = np.nonzero(has)[0]  # positions with no sensible move (teacher would pass) are dropped
-            states_ds.append(planes[keep])
-            actions.append(np.stack([idx[keep] // 19, idx[keep] % 19], axis=1).astype(np.uint8))
-            n_done += len(sts)
+        from alphago_amd.data.synthetic import teacher_pool
+        planes, idx = teacher_pool(a.positions, teacher, seed=a.seed, symmetrize=False)
+        states_ds.append(planes)
         states_ds.finish()
-        acts = np.concatenate(actions)
+        acts = np.stack([idx // 19, idx % 19], axis=1).astype(np.uint8)
         f.create_dataset("actions", data=acts)
         f.create_group("file_offsets")["synthetic"] = np.array([0, len(acts)], dtype=np.int64)
+    del teacher
     t_data = time.perf_counter() - t0
-    torch.manual_seed(2000 + a.seed)
-    student = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
-    model_json = os.path.join(a.out, "student.json")
-    student.save_model(model_json)
-    run_dir = os.path.join(a.out, "run")
-    t1 = time.perf_counter()
-    run_training([model_json, h5, run_dir, "--minibatch", str(a.batch), "--epochs", str(a.epochs),
-                  "--learning-rate", str(a.lr), "--decay", "0", "--no-symmetries", "--seed", str(a.seed)])
-    t_train = time.perf_counter() - t1
-    meta = json.load(open(os.path.join(run_dir, "metadata.json")))
-    ep = meta["epochs"]
+    real = _real_games(a.out, DEFAULT_FEATURES) if a.real_epochs > 0 else None
+    results = {}
+    for arm in [x for x in a.arms.split(",") if x]:
+        torch.manual_seed(2000 + a.seed)  # the same student initialisation in every arm
+        student = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
+        model_json = os.path.join(a.out, "student_%s.json" % arm)
+        student.save_model(model_json)
+        run_dir = os.path.join(a.out, "run_" + arm)
+        t1 = time.perf_counter()
+        run_training([model_json, h5, run_dir, "--minibatch", str(a.batch), "--epochs", str(a.epochs),
+                      "--learning-rate", str(a.lr), "--decay", "0", "--no-symmetries", "--seed", str(a.seed)]
+                     + ARMS[arm])
+        ep = json.load(open(os.path.join(run_dir, "metadata.json")))["epochs"]
+        res = {"acc": [round(e.get("acc", 0), 4) for e in ep], "val_acc": [round(e.get("val_acc", 0), 4) for e in ep],
+               "train_s": round(time.perf_counter() - t1, 1)}
+        if real is not None:
+            torch.manual_seed(3000 + a.seed)
+            stu = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
+            rj = os.path.join(a.out, "real_student_%s.json" % arm)
+            stu.save_model(rj)
+            rdir = os.path.join(a.out, "real_" + arm)
+            run_training([rj, real[0], rdir, "--minibatch", "32", "--epochs", str(a.real_epochs),
+                          "--learning-rate", str(a.lr), "--decay", "0", "--seed", str(a.seed),
+                          "--train-val-test", "1.0", "0.0", "0.0"] + ARMS[arm])
+            w = os.path.join(rdir, "weights.%05d.hdf5" % (a.real_epochs - 1))
+            top1, n = _heldout_top1(rj, w, real[1], dev)
+            res["real_heldout_top1"] = round(top1, 4)
+            res["real_heldout_positions"] = n
+            res["real_heldout_game"] = real[2]
+        results[arm] = res
     print(json.dumps({"metric": "SL top-1 agreement with a random-init teacher policy (held-out)",
-                      "positions": int(len(acts)), "epochs": len(ep), "minibatch": a.batch, "lr": a.lr,
-                      "acc": [round(e.get("acc", 0), 4) for e in ep],
-                      "val_acc": [round(e.get("val_acc", 0), 4) for e in ep],
-                      "chance": round(1.0 / 300, 4), "data_s": round(t_data, 1), "train_s": round(t_train, 1),
-                      "net": "%dx%d" % (L, F), "device": str(dev)}))
+                      "positions": int(len(acts)), "epochs": a.epochs, "minibatch": a.batch, "lr": a.lr,
+                      "chance": round(1.0 / 300, 4), "data_s": round(t_data, 1), "net": "%dx%d" % (L, F),
+                      "device": str(dev), "arms": results}))
 
 
 if __name__ == "__main__":

@@ -44,6 +44,11 @@ def test_bench_json_line_under_torchrun(nproc):
     assert out["config"]["global_batch"] == 2 * nproc
     assert out["config"]["parallelism"] == "dp%d" % nproc
     assert out["value"] > 0
+    # diagnostics of the multi-rank run: live process group, per-rank step times, exposed all-reduce
+    assert out["world_size"] == nproc and len(out["rank_ms_per_step"]) == nproc
+    assert out["dist_backend"] == ("gloo" if nproc > 1 else "none")
+    assert "allreduce_exposed_ms_per_step" in out
+    assert out["data"].startswith("synthetic: ")  # teacher-labelled pool (learnable labels)
     # at least --warmup steps and at least --min-warmup-s seconds, same count on every rank
     assert out["warmup_steps_run"] >= 1 and (out["warmup_steps_run"] - 1) % 10 == 0 and out["warmup_s"] >= 0.5
     # value is the whole-job rate: global positions over the (max-over-ranks) timed span

@@ -140,3 +140,89 @@ def test_rccl_path_world1_matches_local(cuda_device):
         tr.step(planes, tgt)
     torch.cuda.synchronize()
     assert torch.equal(torch.from_numpy(w), tr.fp.flat.cpu())
+
+
+def _rccl_graph_worker(port, q, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      ALPHAGO_AMD_FORCE_DIST="1")
+    os.environ.pop("ALPHAGO_AMD_DIST_BACKEND", None)
+    if mode == "graph_ar":
+        os.environ["ALPHAGO_AMD_GRAPH_ALLREDUCE"] = "1"
+    if mode == "defer":
+        os.environ["ALPHAGO_AMD_DEFER_ALLREDUCE"] = "1"
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.parallel import dist as agdist
+    from alphago_amd.train.engine import HipPolicyTrainer
+
+    env = agdist.init_from_env()
+    dev = env.device
+    torch.manual_seed(0)
+    net = PolicyNet(48, filters_per_layer=192, layers=12)
+    g = torch.Generator().manual_seed(5)
+    tr = HipPolicyTrainer(net, 32, lr=0.1, device=dev, bucket_mb=2.0)
+    if mode == "graph_ar":
+        tr.enable_graphs()
+    for _ in range(4):
+        planes = torch.randint(0, 2, (32, 48, 19, 19), dtype=torch.uint8, generator=g).to(dev)
+        tgt = torch.randint(0, 361, (32,), dtype=torch.int32, generator=g).to(dev)
+        tr.step(planes, tgt)
+    torch.cuda.synchronize()
+    q.put((tr.fp.flat.cpu().numpy().copy(), len(tr._graphs or []) if mode == "graph_ar" else -1))
+    agdist.shutdown()
+
+
+@pytest.mark.parametrize("mode", ["graph_ar", "defer"])
+def test_rccl_world1_graph_allreduce_and_defer(cuda_device, mode):
+    """ALPHAGO_AMD_GRAPH_ALLREDUCE=1: the bucketed RCCL all-reduce captured inside ONE HIP graph with
+    the whole step; ALPHAGO_AMD_DEFER_ALLREDUCE=1: every bucket launched after the backward.  Both
+    on a forced world-1 RCCL group, bitwise equal to local training."""
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.train.engine import HipPolicyTrainer
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_graph_worker, args=(_free_port(), q, mode))
+    p.start()
+    w, ngraphs = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    if mode == "graph_ar":
+        assert ngraphs == 1  # one graph: the all-reduce is inside it
+    torch.manual_seed(0)
+    net = PolicyNet(48, filters_per_layer=192, layers=12)
+    g = torch.Generator().manual_seed(5)
+    tr = HipPolicyTrainer(net, 32, lr=0.1, device=cuda_device, bucket_mb=2.0)
+    for _ in range(4):
+        planes = torch.randint(0, 2, (32, 48, 19, 19), dtype=torch.uint8, generator=g).to(cuda_device)
+        tgt = torch.randint(0, 361, (32,), dtype=torch.int32, generator=g).to(cuda_device)
+        tr.step(planes, tgt)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.from_numpy(w), tr.fp.flat.cpu())
+
+
+def test_comm_proxy_leaves_gradients_untouched(cuda_device, monkeypatch):
+    """ALPHAGO_AMD_COMM_PROXY (one-GPU stand-in for the overlapped all-reduce) only reads the
+    gradient: training with it, overlapped or deferred, equals training without it bit for bit."""
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.train.engine import HipPolicyTrainer
+
+    out = []
+    for env in ({}, {"ALPHAGO_AMD_COMM_PROXY": "16,300,8"},
+                {"ALPHAGO_AMD_COMM_PROXY": "16,300,8", "ALPHAGO_AMD_DEFER_ALLREDUCE": "1"}):
+        for k in ("ALPHAGO_AMD_COMM_PROXY", "ALPHAGO_AMD_DEFER_ALLREDUCE"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        torch.manual_seed(0)
+        tr = HipPolicyTrainer(PolicyNet(48, filters_per_layer=192, layers=12), 64, lr=0.1, device=cuda_device)
+        assert (tr._proxy is not None) == bool(env)
+        g = torch.Generator().manual_seed(9)
+        tr.comm_events = []
+        for _ in range(3):
+            planes = torch.randint(0, 2, (64, 48, 19, 19), dtype=torch.uint8, generator=g).to(cuda_device)
+            tgt = torch.randint(0, 361, (64,), dtype=torch.int32, generator=g).to(cuda_device)
+            tr.step(planes, tgt)
+        torch.cuda.synchronize()
+        assert len(tr.comm_events) == (3 if env else 0)
+        out.append(tr.fp.flat.cpu())
+    assert torch.equal(out[0], out[1]) and torch.equal(out[0], out[2])

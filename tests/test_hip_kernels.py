@@ -92,11 +92,14 @@ def test_conv_dgrad_with_relu_mask(ops, cuda_device, B, C, K):
     assert _rel_err(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 5, 1, 2, 3, 4])
 @pytest.mark.parametrize("B,Cin,Cout,K,Pin,nsplit", [(6, 192, 192, 3, 1, None), (5, 64, 192, 5, 2, None),
                                                     (3, 64, 64, 3, 1, None), (9, 128, 128, 3, 1, None),
-                                                    (7, 192, 192, 3, 1, 1), (4, 192, 192, 3, 1, 3)])
+                                                    (7, 192, 192, 3, 1, 1), (4, 192, 192, 3, 1, 3),
+                                                    (11, 192, 192, 3, 1, 40), (2, 128, 128, 3, 1, 5)])
 def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
+    """variant 0: production per-tap kernel; 5: the one-kernel-row wgrad (conv_wgrad_row.hip) for
+    192x192 and 128x128 3x3 layers; 1-4: kernel-lab variants."""
     torch.manual_seed(2)
     S = 19
     x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
@@ -114,6 +117,33 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     else:  # kernel-lab variants
         ops.lab().conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, 0, variant)
     gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
+    gb = torch.zeros(Cout, device=cuda_device)
+    ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert _rel_err(gw, ref_w) < 2e-3
+    assert _rel_err(gb, ref_b) < 2e-3
+
+
+@pytest.mark.parametrize("S,B,Cin,Cin_real,Cout,K,Pin", [(9, 13, 192, 192, 192, 3, 1), (13, 6, 192, 192, 192, 3, 1),
+                                                         (9, 7, 64, 48, 192, 5, 2), (13, 3, 64, 48, 128, 5, 2),
+                                                         (19, 1, 128, 128, 128, 3, 1)])
+def test_conv_wgrad_row_kernel_boards(ops, cuda_device, S, B, Cin, Cin_real, Cout, K, Pin):
+    """The one-kernel-row wgrad at other board sizes (windows of 32 compact pixels cross board rows
+    and boards at every alignment; taps leaving the board read the LDS zero rows), with the split
+    count of the training engine."""
+    torch.manual_seed(7)
+    assert ops.wgrad_plan(Cout, Cin, K, Cin_real, variant=5)[0] == K  # the row kernel applies
+    x = _bf(torch.randn(B, Cin_real, S, S, device=cuda_device))
+    dz = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
+    ref_w = torch.nn.grad.conv2d_weight(x, (Cout, Cin_real, K, K), dz, padding=K // 2)
+    ref_b = dz.sum(dim=(0, 2, 3))
+    xp = ops.to_padded(x, Pin, Cin)
+    dzp = ops.to_padded(dz, 1)
+    ns = ops.wgrad_nsplit(B * S * S, Cout, Cin, K, Cin_real, variant=5)
+    slab = torch.full((ns, K * K, Cout, Cin), float("nan"), device=cuda_device)
+    dbs = torch.zeros(ns, Cout, device=cuda_device)
+    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin_real if Cin_real < Cin else 0, variant=5)
+    gw = torch.zeros(Cout, Cin_real, K, K, device=cuda_device)
     gb = torch.zeros(Cout, device=cuda_device)
     ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
     torch.cuda.synchronize()
