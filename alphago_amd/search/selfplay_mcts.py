@@ -89,7 +89,7 @@ class RoundStats:
 def play_selfplay(policy, value, n_games: int, concurrent: int, cfg: MCTSConfig, size: int = 19,
                   komi: float = 7.5, max_moves: Optional[int] = None, seed: int = 0, threads: Optional[int] = None,
                   on_game: Optional[Callable[[GameRecord], None]] = None,
-                  stats: Optional[List[RoundStats]] = None) -> List[GameRecord]:
+                  stats: Optional[List[RoundStats]] = None, progress_every: int = 0) -> List[GameRecord]:
     """Play ``n_games`` self-play games, ``concurrent`` at a time, to the end.  ``on_game`` gets each
     finished game (then it is not kept in the returned list)."""
     max_moves = max_moves or 2 * size * size
@@ -143,6 +143,12 @@ def play_selfplay(policy, value, n_games: int, concurrent: int, cfg: MCTSConfig,
             stats.append(RoundStats(rnd, len(live), search.forest.total_evals - e0, time.perf_counter() - t0,
                                     min(lens), max(lens)))
         rnd += 1
+        if progress_every and stats is not None and rnd % progress_every == 0:
+            recent = stats[-progress_every:]
+            ev, sec = sum(r.evals for r in recent), sum(r.seconds for r in recent)
+            print("selfplay round %d: %d live games (moves %d-%d), %d finished, %.0f leaf evals/s" %
+                  (rnd, len(live), recent[-1].min_move, recent[-1].max_move, finished, ev / max(sec, 1e-9)),
+                  flush=True)
         for i in live:
             st, r = states[i], recs[i]
             me = st.current_player
@@ -400,6 +406,7 @@ def selfplay_cli(argv=None):
     p.add_argument("--positions-per-game", type=int, default=0)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-sgf", action="store_true")
+    p.add_argument("--progress-every", type=int, default=0, help="print a progress line every N search rounds")
     p.add_argument("--keep-shards", action="store_true")
     a = p.parse_args(argv)
     env = agdist.init_from_env()
@@ -418,7 +425,8 @@ def selfplay_cli(argv=None):
     stats: List[RoundStats] = []
     t0 = time.perf_counter()
     play_selfplay(policy, value, a.games, a.concurrent, cfg, size=S, komi=a.komi, max_moves=a.max_moves or None,
-                  seed=a.seed * 100003 + env.rank * 7919, on_game=writer.add, stats=stats)
+                  seed=a.seed * 100003 + env.rank * 7919, on_game=writer.add, stats=stats,
+                  progress_every=a.progress_every if env.is_main else 0)
     dt = time.perf_counter() - t0
     n = writer.close()
     evals = sum(s.evals for s in stats)
