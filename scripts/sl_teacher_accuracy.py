@@ -37,6 +37,10 @@ def _real_games(out, features):
     """The reference's five Lee Sedol games (tests/test_data/sgf) as 48-plane HDF5: the first four
     for training, the fifth held out (all of its positions: a game-level split)."""
     from alphago_amd.data.convert import GameConverter
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+    pre = (os.path.join(here, "lee_sedol_train.h5"), os.path.join(here, "lee_sedol_heldout.h5"))
+    if all(os.path.exists(p) for p in pre):  # converted in-tree (the reference checkout is not on the GPU box)
+        return pre[0], pre[1], "Lee-Sedol-vs-AlphaGo-20160315.sgf"
     sgf_dir = "/root/reference/tests/test_data/sgf"
     games = sorted(os.path.join(sgf_dir, f) for f in os.listdir(sgf_dir) if "Lee" in f) if os.path.isdir(sgf_dir) \
         else []
