@@ -215,8 +215,24 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_kernel(ConvFp8Args a) {
 // exact.  Waves own disjoint pixels (8 x 32 = 256 per workgroup) and all BN
 // channels.
 // DG: dgrad (e5m2 gradient operand, ReLU' mask from a.mask, no bias, max |dx|, e5m2 output)
-template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8, bool DG = false>
+// DGB: dgrad whose gradient operand is the bf16 dZ itself: each lane loads its 32 bf16 values
+// (64 B) per K-step and converts them to e5m2 in registers (v_cvt_scalef32_pk_bf8_bf16, two per
+// instruction, multiplier *a.in_scale) -- no quantisation pass, no e5m2 tensor; ReLU' mask from
+// the forward's bitmask; bf16 output and max |dx| only
+typedef __attribute__((ext_vector_type(2))) short s16x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+__device__ __forceinline__ int cvt4_bf16_bf8(unsigned lo2, unsigned hi2, float s) {
+  // two packed bf16 pairs -> four e5m2 bytes (low pair in bytes 0-1); the instruction DIVIDES by
+  // its scale operand (e5m2(x / s), measured by tests/test_fp8_inference.py::
+  // test_scalef32_bf8_conversion_semantics), so callers pass the reciprocal of the multiplier
+  s16x2_t r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16((s16x2_t){0, 0}, __builtin_bit_cast(bf16x2_t, lo2), s, false);
+  r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16(r, __builtin_bit_cast(bf16x2_t, hi2), s, true);
+  return __builtin_bit_cast(int, r);
+}
+
+template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8, bool DG = false, bool DGB = false>
 __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) {
+  static_assert(!(DG && DGB), "one dgrad form");
   // MB: 16-pixel blocks per wave; the BN/16 channel blocks are read from LDS in NPART parts
   constexpr int NB = BN / 16;   // 16-channel blocks per wave
   constexpr int NH = NB / NPART;
@@ -244,7 +260,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   const int sx = a.scales[0], sw = a.scales[1];
 
   const int nimg = a.M / SS;
-  const long long xbytes = (long long)nimg * a.HPi * a.HPi * a.Cin;
+  constexpr int XB = DGB ? 2 : 1;  // bytes per operand element in memory
+  const long long xbytes = (long long)nimg * a.HPi * a.HPi * a.Cin * XB;
   const long long wbytes = (long long)a.nch * a.Cout * 64;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.x, (short)0, (int)(xbytes < 0x7fffffffLL ? xbytes : 0x7fffffffLL), 0x00020000);
@@ -303,6 +320,29 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
       xf[j] = i32x8{(int)lo.x, (int)lo.y, (int)lo.z, (int)lo.w, (int)hi.x, (int)hi.y, (int)hi.z, (int)hi.w};
     }
   };
+  // DGB: the raw bf16 operand of a step (4 x 16 B per fragment), converted at the top of its step
+  u32x4 xraw[DGB ? MB : 1][4];
+  const float gin = DGB ? 1.f / *a.in_scale : 1.f;  // power of two: exact
+  auto load_xraw = [&](int ks) {
+    const int off0 = chunk_off(2 * ks), off1 = chunk_off(2 * ks + 1);
+    const int off = (g >= 2 ? off1 : off0) * 2;
+#pragma unroll
+    for (int j = 0; j < (DGB ? MB : 0); ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xraw[j][k] = __builtin_amdgcn_raw_buffer_load_b128(xr, xbase[j] * 2 + off + 16 * k, 0, 0);
+  };
+  auto convert_x = [&](i32x8 (&xf)[MB]) {
+#pragma unroll
+    for (int j = 0; j < (DGB ? MB : 0); ++j) {
+      // dword d of the fragment = e5m2 of channels 4d .. 4d+3 = bf16 pairs 2d, 2d+1 of the raw load
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        const u32x4& r = xraw[j][d >> 1];
+        const unsigned p0 = (d & 1) ? r.z : r.x, p1 = (d & 1) ? r.w : r.y;
+        xf[j][d] = cvt4_bf16_bf8(p0, p1, gin);
+      }
+    }
+  };
 
   f32x4 acc[NB][MB];
 #pragma unroll
@@ -317,14 +357,17 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   // issue order per step: W(next) then x(next); every consumer waits for exactly its own loads
   i32x8 xa[MB], xb[MB];
   load_w(0);
-  load_x(xa, 0);
+  if constexpr (DGB) load_xraw(0);
+  else load_x(xa, 0);
   store_w(0);
   __syncthreads();
   auto body = [&](int ks, i32x8 (&xc)[MB], i32x8 (&xn)[MB]) {
     const char* wb = smem + (ks & 1) * W_BYTES;
+    if constexpr (DGB) convert_x(xc);  // this step's raw loads -> e5m2 (waits for exactly them)
     load_w(ks + 1);
     __builtin_amdgcn_sched_barrier(0);
-    load_x(xn, ks + 1);
+    if constexpr (DGB) load_xraw(ks + 1);
+    else load_x(xn, ks + 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int h = 0; h < NPART; ++h) {
@@ -341,8 +384,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
       for (int i = 0; i < NH; ++i)
 #pragma unroll
         for (int j = 0; j < MB; ++j)
-          acc[h * NH + i][j] = DG ? mfma_fp8_bf8(wf[i], xc[j], acc[h * NH + i][j], sw, sx)
-                                  : mfma_fp8(wf[i], xc[j], acc[h * NH + i][j], sw, sx);
+          acc[h * NH + i][j] = (DG || DGB) ? mfma_fp8_bf8(wf[i], xc[j], acc[h * NH + i][j], sw, sx)
+                                           : mfma_fp8(wf[i], xc[j], acc[h * NH + i][j], sw, sx);
       __builtin_amdgcn_s_setprio(0);
     }
     store_w((ks + 1) & 1);
@@ -374,11 +417,21 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     const int ii = fdiv(rem, a.divS);
     const int jj = rem - ii * a.S;
     const size_t ooff = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout;
+    uint32_t mw[2] = {0u, 0u};
+    if constexpr (DGB) {  // ReLU' bits of the lane's channels (the forward epilogue's layout)
+      const size_t pw = (size_t)(ooff / a.Cout) * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
+      mw[0] = a.mbits_in[pw];
+      mw[1] = a.mbits_in[pw + 4];
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int n = nbase + i * 16;
       f32x4 v = acc[i][j];
-      if constexpr (DG) {
+      if constexpr (DGB) {
+        const uint32_t w = mw[i / (NB / 2)];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = ((w >> (4 * (i % (NB / 2)) + r)) & 1u) ? v[r] : 0.f;
+      } else if constexpr (DG) {
         const bf16x4 mk = *(const bf16x4*)(a.mask + ooff + n);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = (float)mk[r] > 0.f ? v[r] : 0.f;
@@ -390,7 +443,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
         v[3] = fmaxf(v[3] + bb[3], 0.f);
       }
       if (!ok) continue;
-      if constexpr (DG)
+      if constexpr (DG || DGB)
         vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
       else
         vmax = fmaxf(vmax, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
@@ -401,7 +454,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
         o[2] = (__bf16)v[2];
         o[3] = (__bf16)v[3];
         *(bf16x4*)(a.y_bf16 + ooff + n) = o;
-        if constexpr (!DG && NB % 2 == 0) {
+        if constexpr (!DG && !DGB && NB % 2 == 0) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) mb[i / (NB / 2)] |= ((float)o[r] > 0.f ? 1u : 0u) << (4 * (i % (NB / 2)) + r);
         }
@@ -423,7 +476,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
         }
       }
     }
-    if constexpr (!DG && OUT_BF16 && NB % 2 == 0) {
+    if constexpr (!DG && !DGB && OUT_BF16 && NB % 2 == 0) {
       if (a.mbits_out && ok) {
         const size_t pw = (size_t)(ooff / a.Cout) * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
         a.mbits_out[pw] = mb[0];
@@ -449,16 +502,27 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 // weights in 4 parts); kernel-lab build only: 1 / 3 / 4 = other L2-operand
 // tilings, 5 = LDS-staged conv_fwd_fp8_kernel
 
-template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false>
+template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false, bool DGB = false>
 static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
   constexpr int WROWS = (BN * 8) % 512 == 0 ? BN : ((BN * 8 + 511) / 512 * 512) / 8;  // as in the kernel
   constexpr int smem = 2 * WROWS * 128 + 64;
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   constexpr int BM = 128 * MB;
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG>), grid, dim3(512), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB>), grid, dim3(512), smem, st, a);
+}
+
+// fp8 dgrad from the bf16 gradient (in-register e5m2 conversion, bitmask ReLU', bf16 output)
+template <int BN>
+static void launch_fp8_dgrad_bf16(const ConvFp8Args& a, hipStream_t st) {
+  if (a.y_bf16 == nullptr || a.mbits_in == nullptr || a.in_scale == nullptr)
+    throw std::invalid_argument("conv_dgrad_fp8 (bf16 operand): needs y_bf16, mbits and the input scale");
+  if constexpr (BN == 160) launch_fp8_ga<160, 2, 5, true, false, false, true>(a, st);
+  else if constexpr (BN == 192) launch_fp8_ga<192, 2, 4, true, false, false, true>(a, st);
+  else launch_fp8_ga<BN, 2, 2, true, false, false, true>(a, st);
 }
 
 // fp8 dgrad: production tilings only, bf16 output always (the wgrad reads it)
@@ -534,6 +598,13 @@ void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
   ConvFp8Args a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
+  if (a.dgrad_bf16) {
+    if (a.Cout == 160) launch_fp8_dgrad_bf16<160>(a, st);
+    else if (a.Cout % 192 == 0) launch_fp8_dgrad_bf16<192>(a, st);
+    else if (a.Cout % 128 == 0) launch_fp8_dgrad_bf16<128>(a, st);
+    else launch_fp8_dgrad_bf16<64>(a, st);
+    return;
+  }
   if (a.dgrad) {
     if (a.Cout == 160) launch_fp8_dgrad_bn<160>(a, st);
     else if (a.Cout % 192 == 0) launch_fp8_dgrad_bn<192>(a, st);
@@ -585,6 +656,44 @@ void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Ci
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(pack_weights_fp8_kernel, dim3(blocks), dim3(256), 0, st, w, out, Cout_real, Cin_real, K, Cout_p,
                      Cin_p, nch, scale, scale_dev, transposed);
+}
+
+__global__ __launch_bounds__(256) void pack_weights_fp8_multi_kernel(Fp8PackArgs a) {
+  const Fp8PackJob& j = a.jobs[blockIdx.y];
+  const int CC = j.Cin_p >> 6;
+  const float scale = *j.scale;
+  const int rows_real = j.transposed ? j.Cin_real : j.Cout_real;
+  const int chans_real = j.transposed ? j.Cout_real : j.Cin_real;
+  const int K = j.K;
+  const long total = (long)j.nch * j.Cout_p * 16;  // 4 bytes per thread
+  for (long i4 = (long)blockIdx.x * blockDim.x + threadIdx.x; i4 < total; i4 += (long)gridDim.x * blockDim.x) {
+    const long idx = i4 * 4;
+    const int byte = (int)(idx & 63);
+    const long qn = idx >> 6;
+    const int n = (int)(qn % j.Cout_p);
+    const int q = (int)(qn / j.Cout_p);
+    const int t = q / CC;
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = (q - t * CC) * 64 + byte + r;
+      v[r] = 0.f;
+      if (t < K * K && n < rows_real && c < chans_real) {
+        const int kh = t / K, kw = t - (t / K) * K;
+        const size_t src = j.transposed ? (((size_t)c * j.Cin_real + n) * K + (K - 1 - kh)) * K + (K - 1 - kw)
+                                        : (((size_t)n * j.Cin_real + c) * K + kh) * K + kw;
+        v[r] = fminf(fmaxf(j.w[src] * scale, -448.f), 448.f);
+      }
+    }
+    int pk = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+    pk = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], pk, true);
+    *(int*)(j.out + idx) = pk;
+  }
+}
+
+void launch_pack_weights_fp8_multi(const Fp8PackArgs& a, hipStream_t st) {
+  if (a.n <= 0) return;
+  hipLaunchKernelGGL(pack_weights_fp8_multi_kernel, dim3(64, a.n), dim3(256), 0, st, a);
 }
 
 // Per-layer weight scales, one workgroup per layer: e = floor(log2(448 / amax|w|)),
@@ -670,9 +779,11 @@ __global__ __launch_bounds__(256) void quantize_bf8_dev_kernel(const __bf16* x, 
       m = fmaxf(m, fabsf(f[r]));
       f[r] = fminf(fmaxf(f[r] * sc, -57344.f), 57344.f);
     }
-    int pk = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], 0, false);
-    pk = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], pk, true);
-    *(int*)(y + 4 * i) = pk;
+    if (y) {  // null: max |x| only (the head's dZ entering the in-register fp8 dgrad chain)
+      int pk = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], 0, false);
+      pk = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], pk, true);
+      *(int*)(y + 4 * i) = pk;
+    }
   }
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(amax + (blockIdx.x & (kFp8AmaxSlots - 1)), __float_as_uint(m));
@@ -684,6 +795,33 @@ void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* s
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(quantize_bf8_dev_kernel, dim3(blocks), dim3(256), 0, st, x, y, n4, scale, amax);
 }
+
+#ifdef AGK_KERNEL_LAB
+// Probe of v_cvt_scalef32_pk_bf8_bf16 (2 bf16 -> 2 e5m2 with an f32 scale, one instruction):
+// mode 0 = f32 multiply + v_cvt_pk_bf8_f32 (the reference), 1 = scalef32 with `scale`,
+// 2 = scalef32 with 1 / scale.  tests/test_fp8_inference.py pins which scalef32 form equals x * scale.
+typedef __attribute__((ext_vector_type(2))) short agk_s16x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 agk_bf16x2;
+__global__ void bf8_convert_probe_kernel(const __bf16* x, uint8_t* y, long n2, float scale, int mode) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += (long)gridDim.x * blockDim.x) {
+    const agk_bf16x2 v = *(const agk_bf16x2*)(x + 2 * i);
+    unsigned short out;
+    if (mode == 0) {
+      const float f0 = fminf(fmaxf((float)v[0] * scale, -57344.f), 57344.f);
+      const float f1 = fminf(fmaxf((float)v[1] * scale, -57344.f), 57344.f);
+      out = (unsigned short)__builtin_amdgcn_cvt_pk_bf8_f32(f0, f1, 0, false);
+    } else {
+      const agk_s16x2 r = __builtin_amdgcn_cvt_scalef32_pk_bf8_bf16((agk_s16x2){0, 0}, v,
+                                                                     mode == 1 ? scale : 1.f / scale, false);
+      out = (unsigned short)r[0];
+    }
+    *(unsigned short*)(y + 2 * i) = out;
+  }
+}
+void launch_bf8_convert_probe(const __bf16* x, uint8_t* y, long n, float scale, int mode, hipStream_t st) {
+  hipLaunchKernelGGL(bf8_convert_probe_kernel, dim3(256), dim3(256), 0, st, x, y, n / 2, scale, mode);
+}
+#endif
 
 // e4m3 quantisation of a padded NHWC bf16 tensor (interior and borders alike: borders stay 0)
 __global__ void quantize_fp8_kernel(const __bf16* x, uint8_t* y, long n4, float scale) {

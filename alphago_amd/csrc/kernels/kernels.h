@@ -148,6 +148,12 @@ struct ConvFp8Args {
   // forward, production kernel: optional ReLU'(y) bitmask in conv_fwd_kernel's layout
   // (ConvEpilogue: (Cout/BN)*8 words per padded pixel) so the bf16 dgrad can run MODE_MASKBITS
   uint32_t* mbits_out;
+  // dgrad with a bf16 gradient operand (dgrad_bf16): x is the bf16 dZ (padded NHWC, Cin channels),
+  // converted to e5m2 in registers as it is loaded (multiplier *in_scale); the ReLU' mask comes from
+  // the forward's bitmask (mbits_in, conv_fwd_kernel's layout); bf16 output only
+  int dgrad_bf16;
+  const float* in_scale;
+  const uint32_t* mbits_in;
 };
 
 // Kernel choices are explicit launch arguments (ConvFwdArgs::tile,
@@ -188,10 +194,26 @@ struct Fp8WeightScalesArgs {
   int* scales8;   // [L][2]
 };
 void launch_fp8_weight_scales(const Fp8WeightScalesArgs& a, int L, hipStream_t st);
+// every fp8 weight pack of a repack (forward and transposed dgrad packs of all layers) in one launch
+constexpr int kMaxFp8PackJobs = 48;
+struct Fp8PackJob {
+  const float* w;         // OIHW fp32
+  uint8_t* out;           // [nch][rows_p][64] e4m3
+  const float* scale;     // device scale (one float)
+  int Cout_real, Cin_real, K, Cout_p, Cin_p, nch, transposed;
+};
+struct Fp8PackArgs {
+  Fp8PackJob jobs[kMaxFp8PackJobs];
+  int n;
+};
+void launch_pack_weights_fp8_multi(const Fp8PackArgs& a, hipStream_t st);
 void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st);
 void launch_fp8_grad_scales(unsigned* amax, int* gscales8, float* gosc, int L, int margin, hipStream_t st);
 void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st);
 void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st);
+#ifdef AGK_KERNEL_LAB
+void launch_bf8_convert_probe(const __bf16* x, uint8_t* y, long n, float scale, int mode, hipStream_t st);
+#endif
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
 // RCCL all-reduce stand-in (comm_proxy.hip): channels workgroups copy n floats and hold their CUs wire_us
 void launch_comm_proxy(const float* src, float* dst, long n, int channels, double wire_us, hipStream_t st);

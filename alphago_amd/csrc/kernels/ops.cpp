@@ -297,6 +297,62 @@ void conv_dgrad_fp8(const Tensor& dz8, const Tensor& w, const Tensor& mask, cons
   conv_fwd_fp8_impl(dz8, w, out_scale, scales, out_scale, amax, y_bf16, y_fp8, K, S, 1, 1, 0, mask);
 }
 
+void conv_dgrad_fp8_bf16(const Tensor& dz, const Tensor& w8t, const Tensor& mbits, const Tensor& scales,
+                         const Tensor& in_scale, const c10::optional<Tensor>& amax, const Tensor& dx, int64_t K,
+                         int64_t S) {
+  conv_dgrad_fp8_bf16_impl(dz, w8t, mbits, scales, in_scale, amax, dx, K, S);
+}
+
+// every fp8 weight pack of a repack in one launch: job i packs ws[i] into outs[i] with the device
+// scale scales[layer[i]] (forward layout, or transposed + flipped for the dgrad when transposed[i])
+void pack_weights_fp8_multi(at::TensorList ws, at::TensorList outs, const Tensor& scales, at::IntArrayRef layer,
+                            at::IntArrayRef transposed) {
+  check_dev("pack_weights_fp8_multi", ws, outs, scales);
+  const int n = (int)ws.size();
+  TORCH_CHECK(n == (int)outs.size() && n == (int)layer.size() && n == (int)transposed.size() &&
+                  n <= agk::kMaxFp8PackJobs, "pack_weights_fp8_multi: matching lists of at most 48 jobs");
+  TORCH_CHECK(scales.scalar_type() == at::kFloat && scales.is_contiguous(), "scales f32");
+  agk::Fp8PackArgs a{};
+  a.n = n;
+  for (int i = 0; i < n; ++i) {
+    const Tensor& w = ws[i];
+    const Tensor& o = outs[i];
+    CHECK_F32(w); CHECK_CONTIG(w); CHECK_CONTIG(o);
+    TORCH_CHECK(w.dim() == 4 && w.size(2) == w.size(3), "w OIHW");
+    TORCH_CHECK(o.scalar_type() == at::kByte && o.dim() == 3 && o.size(2) == 64, "out (nch, rows_p, 64) uint8");
+    TORCH_CHECK(layer[i] >= 0 && layer[i] < scales.numel(), "layer index");
+    const int K = (int)w.size(2);
+    const bool tr = transposed[i] != 0;
+    const int rows_p = (int)o.size(1), nch = (int)o.size(0);
+    agk::Fp8PackJob& j = a.jobs[i];
+    j.w = w.data_ptr<float>();
+    j.out = o.data_ptr<uint8_t>();
+    j.scale = scales.data_ptr<float>() + layer[i];
+    j.Cout_real = (int)w.size(0);
+    j.Cin_real = (int)w.size(1);
+    j.K = K;
+    j.Cout_p = rows_p;
+    // channel chunks per tap: the packed chunk count covers K*K taps (nch rounded up to even)
+    j.Cin_p = (int)(((int64_t)(tr ? w.size(0) : w.size(1)) + 63) / 64 * 64);
+    TORCH_CHECK(nch >= K * K * (j.Cin_p / 64), "out has too few chunks for the weights");
+    j.nch = nch;
+    j.transposed = tr ? 1 : 0;
+  }
+  agk::launch_pack_weights_fp8_multi(a, cur_stream());
+  launch_check("pack_weights_fp8_multi");
+}
+
+// max |x| of a bf16 tensor into the fp8 amax slots (float bits, atomicMax per slot)
+void absmax_bf16(const Tensor& x, const Tensor& amax, const Tensor& scale_any) {
+  check_dev("absmax_bf16", x, amax, scale_any);
+  CHECK_BF16(x); CHECK_CONTIG(x);
+  TORCH_CHECK(x.numel() % 4 == 0, "numel % 4");
+  TORCH_CHECK(amax.scalar_type() == at::kInt && amax.numel() >= agk::kFp8AmaxSlots, "amax int32[64]");
+  agk::launch_quantize_bf8_dev(bfp(x), nullptr, x.numel(), scale_any.data_ptr<float>(),
+                               reinterpret_cast<unsigned*>(amax.data_ptr<int>()), cur_stream());
+  launch_check("absmax_bf16");
+}
+
 void fp8_grad_scales(const Tensor& amax, const Tensor& gscales8, const Tensor& gosc, int64_t margin) {
   check_dev("fp8_grad_scales", amax, gscales8, gosc);
   TORCH_CHECK(amax.scalar_type() == at::kInt && gscales8.scalar_type() == at::kInt && gosc.scalar_type() == at::kFloat,
@@ -545,6 +601,10 @@ TORCH_LIBRARY(alphago_amd, m) {
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
       "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, Tensor(d!)? mbits=None) -> ()");
   m.def("pack_weights_fp8(Tensor w, Tensor(a!) out, float scale, Tensor? scale_dev, bool transposed=False) -> ()");
+  m.def("pack_weights_fp8_multi(Tensor[] ws, Tensor(a!)[] outs, Tensor scales, int[] layer, int[] transposed) -> ()");
+  m.def("absmax_bf16(Tensor x, Tensor(a!) amax, Tensor scale_any) -> ()");
+  m.def("conv_dgrad_fp8_bf16(Tensor dz, Tensor w8t, Tensor mbits, Tensor scales, Tensor in_scale, Tensor(a!)? amax, "
+        "Tensor(b!) dx, int K, int S) -> ()");
   m.def("conv_dgrad_fp8(Tensor dz8, Tensor w, Tensor mask, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
         "Tensor(b!) y_bf16, Tensor(c!)? y_fp8, int K, int S) -> ()");
   m.def("fp8_grad_scales(Tensor(a!) amax, Tensor(b!) gscales8, Tensor(c!) gosc, int margin) -> ()");
@@ -589,6 +649,9 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("conv_fwd_fp8", &conv_fwd_fp8);
   m.impl("pack_weights_fp8", &pack_weights_fp8);
   m.impl("conv_dgrad_fp8", &conv_dgrad_fp8);
+  m.impl("conv_dgrad_fp8_bf16", &conv_dgrad_fp8_bf16);
+  m.impl("pack_weights_fp8_multi", &pack_weights_fp8_multi);
+  m.impl("absmax_bf16", &absmax_bf16);
   m.impl("fp8_grad_scales", &fp8_grad_scales);
   m.impl("quantize_bf8", &quantize_bf8);
   m.impl("fp8_weight_scales", &fp8_weight_scales);

@@ -221,4 +221,45 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
   launch_check("conv_fwd_fp8");
 }
 
+// fp8 dgrad from the bf16 gradient: dz (B, HP, HP, Cg) bf16 padded NHWC is converted to e5m2 in
+// the kernel's registers (multiplier *in_scale, MFMA scale scales[0]); w8t: transposed flipped e4m3
+// weights (scales[1]); ReLU' from the forward's bitmask; dx bf16; amax accumulates max |dx|
+inline void conv_dgrad_fp8_bf16_impl(const Tensor& dz, const Tensor& w8t, const Tensor& mbits, const Tensor& scales,
+                                     const Tensor& in_scale, const c10::optional<Tensor>& amax, const Tensor& dx,
+                                     int64_t K, int64_t S) {
+  check_dev("conv_dgrad_fp8_bf16", dz, w8t, mbits, scales, in_scale, amax, dx);
+  CHECK_DEV(dz); CHECK_DEV(w8t); CHECK_DEV(mbits); CHECK_DEV(dx);
+  CHECK_BF16(dz); CHECK_CONTIG(dz); CHECK_BF16(dx); CHECK_CONTIG(dx); CHECK_CONTIG(w8t);
+  TORCH_CHECK(dz.dim() == 4 && dz.size(2) == dz.size(1) && dz.size(1) == S + 2, "dz (B, S+2, S+2, C) with pad 1");
+  TORCH_CHECK(w8t.scalar_type() == at::kByte && w8t.dim() == 3 && w8t.size(2) == 64, "w8t (nch, Cout, 64) e4m3");
+  TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2, "scales int32[2] (E8M0)");
+  TORCH_CHECK(in_scale.scalar_type() == at::kFloat && in_scale.numel() >= 1, "in_scale f32[1]");
+  TORCH_CHECK(mbits.scalar_type() == at::kInt && mbits.is_contiguous(), "mbits int32");
+  const int64_t B = dz.size(0), HP = dz.size(1), Cg = dz.size(3), nch = w8t.size(0), Cout = w8t.size(1);
+  TORCH_CHECK((Cg % 64 == 0 || Cg == 160) && (Cout % 64 == 0 || Cout == 160) && nch % 2 == 0 &&
+                  nch >= K * K * ((Cg + 63) / 64), "channel geometry (multiples of 64, or 160)");
+  TORCH_CHECK(dx.size(0) == B && dx.size(1) == HP && dx.size(2) == HP && dx.size(3) == Cout, "dx shape");
+  const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
+  TORCH_CHECK(mbits.numel() >= B * HP * HP * words, "mbits too small: need B*HPo*HPo*words");
+  TORCH_CHECK(dz.numel() < (1ll << 30) && dx.numel() < (1ll << 31), "tensor too large for int32 offsets");
+  agk::ConvFp8Args a{};
+  a.x = reinterpret_cast<const uint8_t*>(dz.data_ptr());
+  a.w = w8t.data_ptr<uint8_t>();
+  a.scales = scales.data_ptr<int>();
+  a.out_scale = in_scale.data_ptr<float>();  // unused by this form; a valid device pointer
+  a.in_scale = in_scale.data_ptr<float>();
+  a.y_bf16 = bfp_mut(dx);
+  a.mbits_in = reinterpret_cast<const uint32_t*>(mbits.data_ptr<int>());
+  if (amax.has_value()) {
+    TORCH_CHECK(amax->scalar_type() == at::kInt && amax->numel() >= agk::kFp8AmaxSlots, "amax int32[64]");
+    a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
+  }
+  a.dgrad_bf16 = 1;
+  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cg; a.Cout = (int)Cout; a.K = (int)K;
+  a.HPi = (int)HP; a.offi = 0; a.HPo = (int)HP; a.Po = 1; a.nch = (int)nch;
+  if (a.M == 0) return;
+  agk::launch_conv_fwd_fp8(a, cur_stream());
+  launch_check("conv_dgrad_fp8_bf16");
+}
+
 }  // namespace agk_ops

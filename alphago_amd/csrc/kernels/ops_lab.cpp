@@ -49,6 +49,15 @@ std::vector<int64_t> wgrad_plan_lab(int64_t cout, int64_t cin, int64_t cin_real,
   return {o[0], o[1], o[2]};
 }
 
+void bf8_convert_probe(const Tensor& x, const Tensor& y, double scale, int64_t mode) {
+  check_dev("bf8_convert_probe", x, y);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kByte && x.numel() == y.numel() &&
+                  x.numel() % 2 == 0 && x.is_contiguous() && y.is_contiguous(), "bf16 -> uint8, even size");
+  agk::launch_bf8_convert_probe(reinterpret_cast<const __bf16*>(x.data_ptr()), y.data_ptr<uint8_t>(), x.numel(),
+                                (float)scale, (int)mode, cur_stream());
+  launch_check("bf8_convert_probe");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(alphago_amd_lab, m) {
@@ -62,9 +71,11 @@ TORCH_LIBRARY(alphago_amd_lab, m) {
       "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, int variant) -> ()");
   m.def("wgrad_tap_group(int cout, int cin, int K, int variant) -> int", &wgrad_tap_group_lab);
   m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant) -> int[]", &wgrad_plan_lab);
+  m.def("bf8_convert_probe(Tensor x, Tensor(a!) y, float scale, int mode) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {
+  m.impl("bf8_convert_probe", &bf8_convert_probe);
   m.impl("conv_fwd", &conv_fwd_lab);
   m.impl("conv_wgrad", &conv_wgrad_lab);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8_lab);

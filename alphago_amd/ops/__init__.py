@@ -311,11 +311,32 @@ def pack_weights_fp8_into(w_oihw: torch.Tensor, out: torch.Tensor, scale_dev: to
     _ops().pack_weights_fp8(w_oihw, out, 1.0, scale_dev, transposed)
 
 
+def pack_weights_fp8_multi(ws, outs, scales_dev: torch.Tensor, layer, transposed):
+    """Every fp8 weight pack of a repack in ONE launch: job i packs ws[i] into outs[i] with the device
+    scale scales_dev[layer[i]]; transposed[i] selects the dgrad layout (rows = input channels,
+    taps flipped)."""
+    _ops().pack_weights_fp8_multi(list(ws), list(outs), scales_dev, [int(x) for x in layer],
+                                  [int(bool(x)) for x in transposed])
+
+
+def absmax_bf16(x, amax):
+    """max |x| of a bf16 tensor folded into fp8 amax slots (int32 float bits, per-slot atomicMax)."""
+    _ops().absmax_bf16(x, amax, amax.view(torch.float32))
+
+
 def conv_dgrad_fp8(dz8, w8t, mask, scales, out_scale, K: int, S: int, y_bf16, y_fp8=None, amax=None):
     """fp8 dgrad: dx = conv(dz8 (e5m2, E8M0 scale scales[0]), w8t (transposed e4m3, scales[1]))
     masked by mask > 0 (bf16 activation of the layer below); bf16 y_bf16 and optional e5m2
     y_fp8 (x out_scale); amax accumulates max |dx|."""
     _ops().conv_dgrad_fp8(dz8, w8t, mask, scales, out_scale, amax, y_bf16, y_fp8, K, S)
+
+
+def conv_dgrad_fp8_bf16(dz, w8t, mbits, scales, in_scale, K: int, S: int, dx, amax=None):
+    """fp8 dgrad straight from the bf16 gradient: dz (padded NHWC bf16) is converted to e5m2 in
+    registers as the kernel loads it (multiplier in_scale[0], MFMA E8M0 scale scales[0]), times the
+    transposed flipped e4m3 weights (scales[1]); ReLU' from the forward's bitmask ``mbits``; bf16 dx;
+    ``amax`` accumulates max |dx| (the next layer's gradient scale)."""
+    _ops().conv_dgrad_fp8_bf16(dz, w8t, mbits, scales, in_scale, amax, dx, K, S)
 
 
 def fp8_grad_scales(amax, gscales8, gosc, margin: int = 1):

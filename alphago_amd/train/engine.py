@@ -255,16 +255,15 @@ class HipConvTrainer:
             self._fp8_calibrated = False
             # fp8 dgrad (opt-in): e5m2 gradients x transposed e4m3 weights; per-layer delayed
             # gradient scales from the max |dZ| of the previous step (the first step runs bf16
-            # dgrads and calibrates them).  The kernel is barely faster than the bf16 dgrad (219
-            # vs 225 us per 3x3 layer at B=1024, serial) and the e5m2 quantisation pass and the
-            # transposed weight packs make it a net loss: value training 142.2k vs 143.5k
+            # dgrads and calibrates them).  Round 3: the kernel reads the bf16 dZ and converts it to
+            # e5m2 in registers (no quantisation pass, no e5m2 tensor), takes ReLU' from the
+            # forward's bitmask, and the transposed packs ride the one batched repack launch.
             self.fp8_dgrad = fp8_dgrad
             self.wd8 = [None] + [torch.zeros((ops.fp8_nchunks(self.K[l], self.Fp), self.Fp, 64), dtype=torch.uint8,
                                              device=dev) for l in range(1, L)]
             self.gscales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
             self.gosc8 = torch.ones(L, device=dev)
             self.gamax8 = ops.fp8_amax_buffer(L, dev)
-            self.DZ8 = [torch.zeros(self.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(2)]
             self._g8_calibrated = False
         # Keras-SGD schedule mirrored on the device (float64 {lr0, decay, iterations, lr}) so that
         # the SGD step reads its learning rate from memory: the whole step is graph-capturable
@@ -316,11 +315,13 @@ class HipConvTrainer:
         ops.pack_weights(ws, self.wf, self.wd)
         if self.precision == "fp8":
             ops.fp8_weight_scales(ws, self.wscale8, self.scales8)
-            for l in range(self.L):
-                ops.pack_weights_fp8_into(ws[l], self.w8[l], self.wscale8[l:l + 1])
+            # every e4m3 pack of the step (forward, and the transposed dgrad packs) in ONE launch
+            # (round 2: 12 + 11 launches of pack_weights_fp8 per step)
+            dg = list(range(1, self.L)) if self.fp8_dgrad else []
+            ops.pack_weights_fp8_multi([ws[l] for l in range(self.L)] + [ws[l] for l in dg],
+                                       self.w8 + [self.wd8[l] for l in dg], self.wscale8,
+                                       list(range(self.L)) + dg, [0] * self.L + [1] * len(dg))
             if self.fp8_dgrad:
-                for l in range(1, self.L):
-                    ops.pack_weights_fp8_into(ws[l], self.wd8[l], self.wscale8[l:l + 1], transposed=True)
                 self.gscales8[:, 1].copy_(self.scales8[:, 1])
 
     def _layer_in(self, l):
@@ -416,11 +417,14 @@ class HipConvTrainer:
                 self._wgrad_layer(l, red)
             if l > 0:
                 if self.precision == "fp8" and self.fp8_dgrad and self._g8_calibrated:
-                    if l == self.L - 1:  # the head's dZ enters the e5m2 chain
-                        ops.quantize_bf8(self.DZ[l], self.DZ8[l % 2], self.gosc8[l:l + 1], self.gamax8[l])
-                    ops.conv_dgrad_fp8(self.DZ8[l % 2], self.wd8[l], self.Y[l - 1], self.gscales8[l],
-                                       self.gosc8[l - 1:l], self.K[l], self.S, self.DZ[l - 1],
-                                       y_fp8=self.DZ8[(l - 1) % 2] if l > 1 else None, amax=self.gamax8[l - 1])
+                    # fp8 dgrad straight from the bf16 dZ: converted to e5m2 in the kernel's registers
+                    # (delayed per-layer scale gosc8[l]), ReLU' from the forward's bitmask, bf16 dx
+                    # whose max |dx| sets the next step's scale of layer l-1
+                    if l == self.L - 1:  # the head's dZ: its max |dZ| for the next step's scale
+                        ops.absmax_bf16(self.DZ[l], self.gamax8[l])
+                    ops.conv_dgrad_fp8_bf16(self.DZ[l], self.wd8[l], self.MBITS[l - 1], self.gscales8[l],
+                                            self.gosc8[l:l + 1], self.K[l], self.S, self.DZ[l - 1],
+                                            amax=self.gamax8[l - 1])
                 else:  # ReLU' bitmask from the forward epilogue (bf16 and fp8 forwards write it)
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=self.conv_tile)

@@ -196,3 +196,66 @@ def test_conv_dgrad_fp8(ops, cuda_device, C, Cp):
     assert out[:, C:].abs().sum() == 0
     assert _rel_err(ops.bf8_to_float(dx8, ey)[:, 1:S + 1, 1:S + 1, :C].permute(0, 3, 1, 2), ref) < 0.13
     assert abs(amax.view(torch.float32).max().item() - ref.abs().max().item()) <= 1e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("C,Cp,B", [(152, 160, 3), (192, 192, 3), (192, 192, 7)])
+def test_conv_dgrad_fp8_bf16_operand(ops, cuda_device, C, Cp, B):
+    """fp8 dgrad straight from the bf16 gradient (converted to e5m2 in the kernel's registers,
+    ReLU' from the forward's bitmask, bf16 output) vs fp32 conv2d_input of the dequantised
+    operands: e5m2(dZ * 2^eg) * 2^-eg and e4m3 weights."""
+    torch.manual_seed(6)
+    S, K = 19, 3
+    xin = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w0 = _bf(torch.randn(C, C, K, K, device=cuda_device) * 0.05)
+    b0 = torch.randn(C, device=cuda_device) * 0.1
+    wp0 = ops.packed_weight_like(w0, Cp, Cp)
+    ops.pack_weights([w0.contiguous()], [wp0])
+    yprev = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=cuda_device)
+    ops.conv_fwd(ops.to_padded(xin, 1, Cp), wp0, torch.nn.functional.pad(b0, (0, Cp - C)), yprev, K, S, 1, 1,
+                 mbits=mbits)
+    dz = _bf(torch.randn(B, C, S, S, device=cuda_device) * 1e-3)
+    w = torch.randn(C, C, K, K, device=cuda_device) * 0.05
+    eg = ops.fp8_exponent(float(dz.abs().max()), margin=0) + 7
+    ew = ops.fp8_exponent(float(w.abs().max()), margin=0)
+    w8t = torch.zeros((ops.fp8_nchunks(K, Cp), Cp, 64), dtype=torch.uint8, device=cuda_device)
+    ops.pack_weights_fp8_multi([w], [w8t], torch.tensor([2.0 ** ew], device=cuda_device), [0], [1])
+    dzq = (dz * 2.0 ** eg).clamp(-57344, 57344).to(torch.float8_e5m2).float() * 2.0 ** -eg
+    wq = (w * 2.0 ** ew).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** -ew
+    ymask = ops.from_padded(yprev, 1)[:, :C] > 0
+    ref = torch.nn.grad.conv2d_input((B, C, S, S), wq, dzq, padding=K // 2) * ymask
+    scales = torch.tensor([127 - eg, 127 - ew], dtype=torch.int32, device=cuda_device)
+    amax = ops.fp8_amax_buffer(1, cuda_device)[0]
+    dx = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    ops.conv_dgrad_fp8_bf16(ops.to_padded(dz, 1, Cp), w8t, mbits, scales,
+                            torch.tensor([2.0 ** eg], device=cuda_device), K, S, dx, amax=amax)
+    torch.cuda.synchronize()
+    out = ops.from_padded(dx, 1)
+    assert _rel_err(out[:, :C], ref) < 1e-2
+    assert out[:, C:].abs().sum() == 0
+    assert dx[:, 0].abs().sum() == 0  # borders untouched
+    assert abs(amax.view(torch.float32).max().item() - ref.abs().max().item()) <= 1e-2 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("Cin,Cout,K", [(152, 152, 3), (49, 152, 5), (192, 192, 3), (48, 192, 5)])
+def test_pack_weights_fp8_multi_matches_single(ops, cuda_device, Cin, Cout, K):
+    """The one-launch fp8 repack equals the per-layer packs, forward and transposed."""
+    torch.manual_seed(8)
+    w = torch.randn(Cout, Cin, K, K, device=cuda_device) * 0.05
+    cout_p, cin_p = ops.pad_filters(Cout), (ops.pad_filters(Cin) if Cin > 64 else 64)
+    sc = torch.tensor([4.0, 8.0], device=cuda_device)
+    a = torch.zeros((ops.fp8_nchunks(K, cin_p), cout_p, 64), dtype=torch.uint8, device=cuda_device)
+    b = torch.zeros_like(a)
+    ops.pack_weights_fp8_into(w, a, sc[1:2])
+    outs = [b]
+    tr = Cin == Cout
+    if tr:
+        at = torch.zeros((ops.fp8_nchunks(K, cout_p), cin_p, 64), dtype=torch.uint8, device=cuda_device)
+        bt = torch.zeros_like(at)
+        ops.pack_weights_fp8_into(w, at, sc[1:2], transposed=True)
+        outs.append(bt)
+    ops.pack_weights_fp8_multi([w] * len(outs), outs, sc, [1] * len(outs), [0, 1][:len(outs)])
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    if tr:
+        assert torch.equal(at, bt)

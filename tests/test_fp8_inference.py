@@ -91,3 +91,26 @@ def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad):
         t8.step(planes, z)
     assert t8.evaluate(planes, z)[0].item() < l0
     assert (t8.scales8[:, 0] != 127).any()  # activation exponents were set from the data
+
+
+@pytest.mark.gpu
+def test_scalef32_bf8_conversion_semantics(cuda_device):
+    """Pins the semantics of v_cvt_scalef32_pk_bf8_bf16 (2 bf16 -> 2 e5m2 with an f32 scale in one
+    instruction, the in-register gradient conversion of the fp8 dgrad): which scale argument
+    gives e5m2(x * s), against the f32-multiply + v_cvt_pk_bf8_f32 path and torch's e5m2 cast."""
+    from alphago_amd import ops
+    L = ops.lab()
+    torch.manual_seed(0)
+    x = (torch.randn(4096, device=cuda_device) * 3).to(torch.bfloat16)
+    s = 8.0
+    ref = (x.float() * s).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8)
+    out = {}
+    for mode in (0, 1, 2):
+        y = torch.zeros(4096, dtype=torch.uint8, device=cuda_device)
+        L.bf8_convert_probe(x, y, s, mode)
+        out[mode] = y
+    # the multiply path agrees with torch's e5m2 cast (round to nearest even) up to ties
+    assert (out[0] != ref).float().mean().item() < 1e-3
+    hits = [m for m in (1, 2) if torch.equal(out[m], out[0])]
+    print("scalef32 form equal to e5m2(x * s):", hits)
+    assert hits == [2]  # the instruction divides by its scale operand (conv_fp8.hip cvt4_bf16_bf8)
