@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <numeric>
 
 #include "common.h"
@@ -582,7 +583,8 @@ static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
   else if (bm == 387) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR, true>(a, st);
   else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
   else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
-  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 128 / 256 / 384-387");
+  else if (bm == 64) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR>(a, st);
+  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 64 / 128 / 256 / 384-387");
 }
 
 
@@ -601,7 +603,9 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // B = 2176 (profiles/r3_chunk_outer.md): 3x3 forward 515 -> 480 us, bitmask dgrad 497 -> 463 us;
   // bench 120.8k -> 126.0k positions/s.  The 160-wide straddled tiles run the same order with the
   // 32-channel tail chunk's steps pairing two taps.
-  if (bm == 0) bm = (a.M >= 384 * 512) ? 386 : (a.M >= 256 * 512) ? 256 : 128;
+  // Small batches (round 3): below 128 x 256 pixels (B < 91 at 19 x 19) a 64-pixel tile on 4 waves
+  // (32 x BN/2 per wave) -- B = 16 fills 91 workgroups instead of 46 (profiles/r3_small_batch.md)
+  if (bm == 0) bm = (a.M >= 384 * 512) ? 386 : (a.M >= 256 * 512) ? 256 : (a.M >= 128 * 256) ? 128 : 64;
   if constexpr (BN == 160) {
     if (a.Cin % 64 == 32) launch_fwd_160<MODE, true>(a, bm, st);
     else launch_fwd_160<MODE, false>(a, bm, st);
@@ -612,6 +616,7 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     if (bm == 384) launch_fwd_bm<BN, MODE, 384, 6, false, false>(a, st);
     else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
     else if (bm == 128) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
+    else if (bm == 64) launch_fwd_bm<BN, MODE, 64, 2>(a, st);
     // 385: the 384 tile with the next stage's LDS-DMA spread through the first
     // k-half's MFMAs instead of issued as one burst (kernel-lab tile 9)
     else if (bm == 385) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
@@ -688,11 +693,28 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
   const int lane = threadIdx.x & 63;
   const int wave = wave_id();
   const int wn = wave / NWC, wc = wave % NWC;
-  const int split = blockIdx.x;
-  const int t = blockIdx.y * TAPS;  // first tap of the group
+  // workgroup -> (split, tap group, channel block).  xcd_group (tap-merged rows): the hardware
+  // deals workgroups to the 8 XCDs round robin in launch order, which puts the K kernel-row
+  // workgroups of a split -- all reading the same dZ rows -- on K different L2s, so every dZ
+  // byte comes from the Infinity Cache K times (layer 0: 3 % L2 hits, profiles/r3_small_batch.md).
+  // Grouped, each XCD runs a contiguous range of split-major work and a split's rows share an L2.
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (TAPS > 1 && a.xcd_group) {
+    const int gyz = gridDim.y * gridDim.z;
+    const int nwg = gridDim.x * gyz;
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = lin & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int l = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (lin >> 3);
+    bx = l / gyz;
+    const int rem = l - bx * gyz;
+    by = rem / gridDim.z;
+    bz = rem - by * gridDim.z;
+  }
+  const int split = bx;
+  const int t = by * TAPS;  // first tap of the group
   const int ncb = a.Cin / WC;
-  const int n0 = (blockIdx.z / ncb) * WN;
-  const int c0 = (blockIdx.z % ncb) * WC;
+  const int n0 = (bz / ncb) * WN;
+  const int c0 = (bz % ncb) * WC;
   const int kh = t / a.K, kw = t - (t / a.K) * a.K;
   const int toff = (kh * a.HPi + kw) * a.Cin + c0;
   const int SS = a.S * a.S;
@@ -1152,10 +1174,19 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
   out[2] = 2;
 }
 
+static int wgrad_xcd_group() {
+  static const int on = [] {
+    const char* e = getenv("AGK_WGRAD_XCD");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return on;
+}
+
 void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
   ConvWgradArgs a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
+  a.xcd_group = wgrad_xcd_group();
   if (a.variant == 5) {
     // one-kernel-row wgrad (conv_wgrad_row.hip), opt-in: in the power-limited steady state it ran
     // 607-694 us per 192 -> 192 layer against 548-583 us for the per-tap kernel

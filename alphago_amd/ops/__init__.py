@@ -228,6 +228,9 @@ def wgrad_plan(cout_p: int, cin_p: int, K: int, cin_real: int = 0, variant: int 
     return int(t), int(w), int(c)
 
 
+WGRAD_MIN_STAGES = 8
+
+
 def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, target_wgs: int = 0,
                  cus: int = 256, variant: int = 0) -> int:
     """Pixel splits of the production wgrad: one resident round of workgroups over ``cus`` CUs
@@ -236,7 +239,10 @@ def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
     _, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, variant)
     target = target_wgs if target_wgs > 0 else cus * per_cu
     nks = (M + 31) // 32
-    return max(1, min(target // per_split, nks))
+    # at least WGRAD_MIN_STAGES 32-pixel stages per split: at small batches one resident round of
+    # 3-stage splits spends its time writing a 75-MB slab that the reduce then reads back
+    # (B = 16: 16.6 us wgrad + 16.3 us reduce per layer, profiles/r3_small_batch.md)
+    return max(1, min(target // per_split, nks // WGRAD_MIN_STAGES if target_wgs <= 0 else nks))
 
 
 def wgrad_splits(M: int, T: int, n_tiles: int = 1, target_wgs: int = 512) -> int:
