@@ -39,6 +39,7 @@ struct ConvWgradArgs {
   int variant;         // 0 = production per-tap kernel; 5 = one-kernel-row wgrad (conv_wgrad_row.hip);
                        // 1-4 kernel-lab build only
   long long x_elems, dz_elems;  // tensor extents (debug-build bounds checks)
+  int xcd_group;       // filled by the launcher: 1 = the kernel-row workgroups of a split share an XCD
 };
 
 struct WgradReduceArgs {
