@@ -56,9 +56,9 @@ def _hip_sources(flavor: str):
     kd = os.path.join(CSRC, "kernels")
     if flavor == "lab":
         return [os.path.join(kd, f) for f in ("conv.hip", "conv_wgrad_row.hip", "conv_fwd_variants.hip", "conv_fp8.hip",
-                                              "ops_lab.cpp")]
+                                              "winograd.hip", "ops_lab.cpp")]
     srcs = sorted(glob.glob(os.path.join(kd, "*.hip")) + glob.glob(os.path.join(kd, "*.cpp")))
-    return [f for f in srcs if os.path.basename(f) not in ("conv_fwd_variants.hip", "ops_lab.cpp")]
+    return [f for f in srcs if os.path.basename(f) not in ("conv_fwd_variants.hip", "winograd.hip", "ops_lab.cpp")]
 
 
 def _digest(paths, extra: str = "") -> str:

@@ -258,4 +258,14 @@ void launch_dense_f32(const DenseArgs& a, bool transA, bool transB, hipStream_t 
 // device-side schedule (graph-capturable): sched = {lr0, decay, iterations, lr_current} f64
 void launch_sgd_sched(float* p, const float* g, int64_t n, double* sched, float gscale, hipStream_t st);
 
+// ---- kernel lab: Winograd F(2x2, 3x3) forward (winograd.hip), bias + ReLU, padded NHWC bf16
+struct WinoArgs {
+  const __bf16* x;    // padded NHWC input (HP = S + 2), Cin channels
+  const __bf16* u;    // transformed weights, packed [16 xi][Cin/32][Cout/16][64 lanes][8]
+  const float* bias;  // [Cout] or null
+  __bf16* y;          // padded NHWC output (HP = S + 2), Cout channels
+  int S, Cin, Cout, ntiles, TS;  // TS = (S + 1) / 2 tiles per row; ntiles = B * TS * TS
+};
+void launch_wino_fwd(const WinoArgs& a, hipStream_t st);
+
 }  // namespace agk

@@ -58,6 +58,32 @@ void bf8_convert_probe(const Tensor& x, const Tensor& y, double scale, int64_t m
   launch_check("bf8_convert_probe");
 }
 
+void wino_fwd(const Tensor& x, const Tensor& u, const c10::optional<Tensor>& bias, const Tensor& y, int64_t S) {
+  check_dev("wino_fwd", x, u, bias, y);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && u.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16,
+              "wino_fwd: bf16 x, u, y");
+  TORCH_CHECK(x.dim() == 4 && y.dim() == 4 && x.size(1) == S + 2 && x.size(2) == S + 2 && y.size(1) == S + 2 &&
+                  y.size(2) == S + 2 && y.size(0) == x.size(0) && x.is_contiguous() && y.is_contiguous(),
+              "wino_fwd: padded NHWC x, y with one-pixel borders");
+  const int Cin = (int)x.size(3), Cout = (int)y.size(3);
+  TORCH_CHECK(u.is_contiguous() && u.numel() == 16LL * Cin * Cout, "wino_fwd: packed weights 16 x Cin x Cout");
+  TORCH_CHECK(x.numel() < (1LL << 31) && y.numel() < (1LL << 31), "wino_fwd: int32 offsets");
+  if (bias.has_value())
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() >= Cout, "wino_fwd: fp32 bias");
+  agk::WinoArgs a{};
+  a.x = reinterpret_cast<const __bf16*>(x.data_ptr());
+  a.u = reinterpret_cast<const __bf16*>(u.data_ptr());
+  a.bias = bias.has_value() ? bias->data_ptr<float>() : nullptr;
+  a.y = reinterpret_cast<__bf16*>(y.data_ptr());
+  a.S = (int)S;
+  a.Cin = Cin;
+  a.Cout = Cout;
+  a.TS = (int)((S + 1) / 2);
+  a.ntiles = (int)(x.size(0) * a.TS * a.TS);
+  agk::launch_wino_fwd(a, cur_stream());
+  launch_check("wino_fwd");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(alphago_amd_lab, m) {
@@ -72,10 +98,12 @@ TORCH_LIBRARY(alphago_amd_lab, m) {
   m.def("wgrad_tap_group(int cout, int cin, int K, int variant) -> int", &wgrad_tap_group_lab);
   m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant) -> int[]", &wgrad_plan_lab);
   m.def("bf8_convert_probe(Tensor x, Tensor(a!) y, float scale, int mode) -> ()");
+  m.def("wino_fwd(Tensor x, Tensor u, Tensor? bias, Tensor(a!) y, int S) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {
   m.impl("bf8_convert_probe", &bf8_convert_probe);
+  m.impl("wino_fwd", &wino_fwd);
   m.impl("conv_fwd", &conv_fwd_lab);
   m.impl("conv_wgrad", &conv_wgrad_lab);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8_lab);

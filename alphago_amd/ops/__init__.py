@@ -325,6 +325,18 @@ def pack_weights_fp8_multi(ws, outs, scales_dev: torch.Tensor, layer, transposed
                                   [int(bool(x)) for x in transposed])
 
 
+def wino_pack_weights(w_oihw: torch.Tensor) -> torch.Tensor:
+    """Kernel-lab Winograd F(2x2, 3x3) weights (winograd.hip): U = G g G^T per (cout, cin), bf16,
+    packed [16 xi][Cin/32][Cout/16][64 lanes][8] so that one MFMA B fragment is one 16-B load per
+    lane (lane -> cout 16 nb + lane % 16, cin 32 ks + 8 (lane // 16) + e)."""
+    w = w_oihw.detach().float()
+    cout, cin = w.shape[:2]
+    g = torch.tensor([[1.0, 0.0, 0.0], [0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [0.0, 0.0, 1.0]], device=w.device)
+    u = torch.einsum("ik,nckl,jl->ijnc", g, w, g).reshape(16, cout, cin)
+    u = u.reshape(16, cout // 16, 16, cin // 32, 4, 8).permute(0, 3, 1, 4, 2, 5)
+    return u.contiguous().to(torch.bfloat16)
+
+
 def absmax_bf16(x, amax):
     """max |x| of a bf16 tensor folded into fp8 amax slots (int32 float bits, per-slot atomicMax)."""
     _ops().absmax_bf16(x, amax, amax.view(torch.float32))

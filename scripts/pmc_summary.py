@@ -6,12 +6,12 @@ for k in sorted(glob.glob(root + "/*")):
     durs = []
     for f in glob.glob(k + "/*/runc/*_counter_collection.csv") + glob.glob(k + "/*/*/*_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
-            if "agk::" not in r.get("Kernel_Name", ""):
+            if "agk" not in r.get("Kernel_Name", ""):
                 continue
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
     for f in glob.glob(k + "/p1/*/*_kernel_trace.csv"):
         for r in csv.DictReader(open(f)):
-            if "agk::" in r["Kernel_Name"]:
+            if "agk" in r["Kernel_Name"]:
                 durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     print("==", k.split("/")[-1], "dur_us(median)=%.1f" % (sorted(durs)[len(durs)//2] if durs else 0))
     m = {c: sum(v) / len(v) for c, v in vals.items()}

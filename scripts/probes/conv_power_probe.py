@@ -1,7 +1,8 @@
 """One conv kernel of the SL step run back to back for ~10 s at B = 2176 (the power-limited steady
 state); the caller samples socket power.  Usage: conv_power_probe.py KIND:TILE [secs]
   KIND  fwd (3x3, 192 -> 192, bias + ReLU + bitmask), dgrad (3x3, bitmask ReLU'), fwd5 (5x5 layer 0,
-        48 planes padded to 64), wgrad (3x3 split-K + reduce)
+        48 planes padded to 64), wgrad (3x3 split-K + reduce), wino (kernel-lab Winograd forward,
+        bias + ReLU, PF counted as the direct conv's FLOPs)
   TILE  a production tile code (0, 384-387) or labN for a kernel-lab tiling"""
 import json
 import sys
@@ -50,6 +51,10 @@ if kind == "fwd":
     fn, flops = (lambda: fwd(x, wf, 3, 1, bits=mb)), 2.0 * M * F * F * 9
 elif kind == "dgrad":
     fn, flops = (lambda: fwd(y, wd, 3, 1, mode=ops.MODE_MASKBITS, bits=mb, out=dx, b=None)), 2.0 * M * F * F * 9
+elif kind == "wino":  # kernel-lab Winograd F(2x2,3x3) forward (bias + ReLU); direct-equivalent FLOPs
+    WL = ops.lab()
+    u = ops.wino_pack_weights(w)
+    fn, flops = (lambda: WL.wino_fwd(x, u, bias, y, S)), 2.0 * M * F * F * 9
 elif kind == "fwd5":
     fn, flops = (lambda: fwd(x0, wf1, 5, 2)), 2.0 * M * F * 48 * 25
 elif kind == "wgrad":

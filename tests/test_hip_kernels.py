@@ -518,3 +518,22 @@ def test_ops_refuse_host_tensors(cuda_device):
         ops.sgd_update(p, torch.zeros(1000), 0.1)
     torch.cuda.synchronize()  # the device is still healthy
     assert float(p.sum()) == 0.0
+
+
+@pytest.mark.parametrize("B,S", [(3, 19), (5, 9), (2, 13), (1, 8)])
+def test_winograd_lab_forward(ops, cuda_device, B, S):
+    """Kernel-lab Winograd F(2x2,3x3) forward (winograd.hip) vs fp32 F.conv2d: odd and even board
+    sizes (the last tile row/column of an odd board reads past the padded image: zero), tile counts
+    that do not fill the last 32-tile workgroup, bias + ReLU, borders untouched."""
+    torch.manual_seed(9)
+    C = 192
+    L = ops.lab()
+    x = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w = torch.randn(C, C, 3, 3, device=cuda_device) * 0.05
+    b = torch.randn(C, device=cuda_device) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    y = ops.padded_empty(B, S, 1, C, cuda_device)
+    L.wino_fwd(ops.to_padded(x, 1), ops.wino_pack_weights(w), b, y, S)
+    torch.cuda.synchronize()
+    assert _rel_err(ops.from_padded(y, 1), ref) < 1.5e-2
+    assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
