@@ -55,10 +55,11 @@ def hip_path(flavor: str = "prod") -> str:
 def _hip_sources(flavor: str):
     kd = os.path.join(CSRC, "kernels")
     if flavor == "lab":
-        return [os.path.join(kd, f) for f in ("conv.hip", "conv_wgrad_row.hip", "conv_fwd_variants.hip", "conv_fp8.hip",
-                                              "winograd.hip", "ops_lab.cpp")]
+        return [os.path.join(kd, f) for f in ("conv.hip", "conv_lab.hip", "conv_wgrad_row.hip", "conv_fwd_variants.hip",
+                                              "conv_fp8.hip", "winograd.hip", "lab_probes.hip", "ops_lab.cpp")]
     srcs = sorted(glob.glob(os.path.join(kd, "*.hip")) + glob.glob(os.path.join(kd, "*.cpp")))
-    return [f for f in srcs if os.path.basename(f) not in ("conv_fwd_variants.hip", "winograd.hip", "ops_lab.cpp")]
+    return [f for f in srcs if os.path.basename(f) not in ("conv_fwd_variants.hip", "conv_lab.hip", "winograd.hip", "lab_probes.hip",
+                                                                 "ops_lab.cpp")]
 
 
 def _digest(paths, extra: str = "") -> str:

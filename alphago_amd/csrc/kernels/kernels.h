@@ -268,4 +268,7 @@ struct WinoArgs {
 };
 void launch_wino_fwd(const WinoArgs& a, hipStream_t st);
 
+// kernel lab: ds_read_b64_tr_b8 lane-mapping probe (lab_probes.hip)
+void launch_tr8_probe(const uint8_t* lds_init, int nbytes, const int* addr, unsigned long long* out, hipStream_t st);
+
 }  // namespace agk

@@ -84,6 +84,20 @@ void wino_fwd(const Tensor& x, const Tensor& u, const c10::optional<Tensor>& bia
   launch_check("wino_fwd");
 }
 
+void tr8_probe(const Tensor& lds_init, const Tensor& addr, const Tensor& out) {
+  check_dev("tr8_probe", lds_init, addr, out);
+  TORCH_CHECK(lds_init.scalar_type() == at::kByte && lds_init.numel() <= 4096 && addr.scalar_type() == at::kInt &&
+                  addr.numel() == 64 && out.scalar_type() == at::kLong && out.numel() == 64,
+              "tr8_probe: <= 4096 LDS bytes, 64 int32 addresses, 64 int64 outputs");
+  auto ac = addr.cpu();
+  for (int i = 0; i < 64; ++i)
+    TORCH_CHECK(ac[i].item<int>() >= 0 && ac[i].item<int>() + 8 <= 4096 && ac[i].item<int>() % 8 == 0,
+                "tr8_probe: 8-byte aligned addresses inside the 4 KB LDS block");
+  agk::launch_tr8_probe(lds_init.data_ptr<uint8_t>(), (int)lds_init.numel(), addr.data_ptr<int>(),
+                        reinterpret_cast<unsigned long long*>(out.data_ptr<int64_t>()), cur_stream());
+  launch_check("tr8_probe");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(alphago_amd_lab, m) {
@@ -99,11 +113,13 @@ TORCH_LIBRARY(alphago_amd_lab, m) {
   m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant) -> int[]", &wgrad_plan_lab);
   m.def("bf8_convert_probe(Tensor x, Tensor(a!) y, float scale, int mode) -> ()");
   m.def("wino_fwd(Tensor x, Tensor u, Tensor? bias, Tensor(a!) y, int S) -> ()");
+  m.def("tr8_probe(Tensor lds_init, Tensor addr, Tensor(a!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {
   m.impl("bf8_convert_probe", &bf8_convert_probe);
   m.impl("wino_fwd", &wino_fwd);
+  m.impl("tr8_probe", &tr8_probe);
   m.impl("conv_fwd", &conv_fwd_lab);
   m.impl("conv_wgrad", &conv_wgrad_lab);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8_lab);

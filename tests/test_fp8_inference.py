@@ -114,3 +114,31 @@ def test_scalef32_bf8_conversion_semantics(cuda_device):
     hits = [m for m in (1, 2) if torch.equal(out[m], out[0])]
     print("scalef32 form equal to e5m2(x * s):", hits)
     assert hits == [2]  # the instruction divides by its scale operand (conv_fp8.hip cvt4_bf16_bf8)
+
+
+@pytest.mark.gpu
+def test_tr8_transpose_read_mapping(cuda_device):
+    """Pins ds_read_b64_tr_b8 (the 8-bit transpose read of the fp8 wgrad): per 16-lane group, lane
+    2q+p supplies the address of row q, bytes 8p..8p+7 of an 8-row x 16-byte block, and lane i of
+    the group receives column i of the 8 rows (row q in byte q) -- the 16-bit form's rule
+    (cdna_hip_programming.md T10) with 8 rows of bytes."""
+    from alphago_amd import ops
+    L = ops.lab()
+    stride = 64
+    init = (torch.arange(4096) % 251).to(torch.uint8).to(cuda_device)
+    addr = []
+    for lane in range(64):
+        g, i = divmod(lane, 16)
+        q, p = divmod(i, 2)
+        addr.append(g * 512 + q * stride + 8 * p)
+    out = torch.zeros(64, dtype=torch.int64, device=cuda_device)
+    L.tr8_probe(init, torch.tensor(addr, dtype=torch.int32, device=cuda_device), out)
+    got = out.cpu().numpy().view(np.uint8).reshape(64, 8)
+    host = (np.arange(4096) % 251).astype(np.uint8)
+    exp = np.zeros((64, 8), np.uint8)
+    for lane in range(64):
+        g, i = divmod(lane, 16)
+        for q in range(8):
+            exp[lane, q] = host[g * 512 + q * stride + i]
+    print("lane 0..3 got", got[:4].tolist())
+    assert np.array_equal(got, exp)
