@@ -155,6 +155,8 @@ struct ConvEpilogue {
   }
 
   __device__ __forceinline__ void store(const ConvFwdArgs& a, const f32x4 (&acc)[NB][MB], int mrow) const {
+    float gmax = 0.f;  // MODE_MASKBITS with an e5m2 copy: max |dx| of the lane
+    const float gsc = (MODE == MODE_MASKBITS && a.y_bf8) ? *a.bf8_scale : 0.f;
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
       if (mrow + j * 16 >= a.M) continue;
@@ -192,9 +194,28 @@ struct ConvEpilogue {
 #else
         *(bf16x4*)(a.y + ooff[j] + i * 16) = o;
 #endif
+        if constexpr (MODE == MODE_MASKBITS) {
+          if (a.y_bf8) {  // wave-uniform
+            float sv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              gmax = fmaxf(gmax, fabsf(v[r]));
+              sv[r] = fminf(fmaxf(v[r] * gsc, -57344.f), 57344.f);
+            }
+            int pk = __builtin_amdgcn_cvt_pk_bf8_f32(sv[0], sv[1], 0, false);
+            pk = __builtin_amdgcn_cvt_pk_bf8_f32(sv[2], sv[3], pk, true);
+            *(int*)(a.y_bf8 + ooff[j] + i * 16) = pk;
+          }
+        }
       }
       if constexpr (MODE == MODE_BIAS_RELU)
         if (a.mbits_out) a.mbits_out[(size_t)pix[j] * mwords + mslot] = bits;
+    }
+    if constexpr (MODE == MODE_MASKBITS) {
+      if (a.y_bf8 && a.bf8_amax) {
+        gmax = wave_max(gmax);
+        if ((threadIdx.x & 63) == 0 && gmax > 0.f) atomicMax(a.bf8_amax + (blockIdx.x & 63), __float_as_uint(gmax));
+      }
     }
   }
 };

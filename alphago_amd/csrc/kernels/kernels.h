@@ -24,6 +24,11 @@ struct ConvFwdArgs {
   int tile;            // 0 = automatic; 128/256/384 fixed tiles; other codes: kernel-lab build only
   unsigned long long* dbg;  // kernel lab: diagnostic segment-cycle stamps, else null
   long long x_elems, w_elems, y_elems;  // tensor extents (debug-build bounds checks)
+  // MODE_MASKBITS (dgrad) only, optional: an e5m2 copy of the output (y * *bf8_scale) for the fp8
+  // wgrad, and max |y| folded into 64 amax slots (the next step's delayed gradient scale)
+  uint8_t* y_bf8;
+  const float* bf8_scale;
+  unsigned* bf8_amax;
 };
 
 struct ConvWgradArgs {
@@ -41,6 +46,24 @@ struct ConvWgradArgs {
   long long x_elems, dz_elems;  // tensor extents (debug-build bounds checks)
   int xcd_group;       // filled by the launcher: 1 = the kernel-row workgroups of a split share an XCD
 };
+
+// fp8 wgrad (conv_wgrad_fp8.hip): e5m2 dZ x e4m3 X on the block-scaled MFMA, same slab as the bf16 wgrad
+struct ConvWgradFp8Args {
+  const uint8_t* x8;   // e4m3 layer input (padded NHWC, Cin), quantised with multiplier 2^ex
+  const uint8_t* dz8;  // e5m2 output gradient (padded NHWC, Cout, zero borders), multiplier 2^eg
+  float* slab;         // [nsplit][T][Cout][Cin]
+  float* dbias_slab;   // [nsplit][Cout]
+  const int* xscale;   // device E8M0 exponent 127 - ex
+  const int* gscale;   // device E8M0 exponent 127 - eg
+  const float* gmul;   // device 2^eg (the bias sums undo it)
+  int M, S, Cin, Cout, K, T;
+  int HPi, offi, HPo, Po;
+  int ksteps_per_split, nsplit;  // in 128-pixel steps
+  FastDiv divSS, divS;           // filled by the launcher
+};
+int wgrad_fp8_supported(int Cout, int Cin, int K);
+int wgrad_fp8_stage_pixels();
+void launch_conv_wgrad_fp8(const ConvWgradFp8Args& a, hipStream_t st);
 
 struct WgradReduceArgs {
   const float* slab;

@@ -30,6 +30,24 @@ void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Ten
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }
 
+// bitmask dgrad that also writes an e5m2 copy of dx (x *scale) and folds max |dx| into amax slots
+void conv_dgrad_bits_bf8(const Tensor& dz, const Tensor& wd, const Tensor& dx, const Tensor& mbits, const Tensor& dx8,
+                         const Tensor& scale, const c10::optional<Tensor>& amax, int64_t K, int64_t S, int64_t tile) {
+  check_dev("conv_dgrad_bits_bf8", dz, wd, dx, mbits, dx8, scale, amax);
+  TORCH_CHECK(tile == 0 || tile == 64 || tile == 128 || tile == 256 || (tile >= 384 && tile <= 387),
+              "conv_dgrad_bits_bf8: production tile codes only");
+  conv_fwd_impl(dz, wd, c10::nullopt, c10::nullopt, dx, K, S, 1, 1, agk::MODE_MASKBITS, mbits, (int)tile, nullptr, -1,
+                dx8, scale, amax);
+}
+
+void conv_wgrad_fp8(const Tensor& x8, const Tensor& dz8, const Tensor& slab, const Tensor& dbslab,
+                    const Tensor& xscale, const Tensor& gscale, const Tensor& gmul, int64_t K, int64_t S, int64_t Pin,
+                    int64_t Po) {
+  conv_wgrad_fp8_impl(x8, dz8, slab, dbslab, xscale, gscale, gmul, K, S, Pin, Po);
+}
+
+int64_t wgrad_fp8_stage_px() { return agk::wgrad_fp8_stage_pixels(); }
+
 void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
                        double scale, double beta) {
   check_dev("conv_wgrad_reduce", slab, dbslab, grad_w, grad_b);
@@ -578,6 +596,11 @@ TORCH_LIBRARY(alphago_amd, m) {
       "Tensor(b!)? mbits=None, int tile=0) -> ()");
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0, int variant=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
+  m.def("conv_dgrad_bits_bf8(Tensor dz, Tensor wd, Tensor(a!) dx, Tensor mbits, Tensor(b!) dx8, Tensor scale, "
+        "Tensor(c!)? amax, int K, int S, int tile=0) -> ()");
+  m.def("conv_wgrad_fp8(Tensor x8, Tensor dz8, Tensor(a!) slab, Tensor(b!) dbslab, Tensor xscale, Tensor gscale, "
+        "Tensor gmul, int K, int S, int Pin, int Po) -> ()");
+  m.def("wgrad_fp8_stage_px() -> int", &wgrad_fp8_stage_px);
   m.def(
       "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor? weight, Tensor(a!)? dz, Tensor(b!)? loss, "
       "Tensor(c!)? correct, Tensor(d!)? dhead, Tensor(e!)? probs, int S, float grad_scale, float temperature, "
@@ -632,6 +655,8 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("conv_fwd", &conv_fwd);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);
+  m.impl("conv_dgrad_bits_bf8", &conv_dgrad_bits_bf8);
+  m.impl("conv_wgrad_fp8", &conv_wgrad_fp8);
   m.impl("policy_head", &policy_head);
   m.impl("pack_input", &pack_input);
   m.impl("head_logits", &head_logits);

@@ -65,8 +65,11 @@ inline void launch_check(const char* op) {
 inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias,
                           const c10::optional<Tensor>& mask, const Tensor& y, int64_t K, int64_t S, int64_t Pin,
                           int64_t Po, int64_t mode, const c10::optional<Tensor>& mbits, int tile,
-                          unsigned long long* dbg = nullptr, long long x_elems_override = -1) {
-  check_dev("conv_fwd_impl", x, w, bias, mask, y, mbits);
+                          unsigned long long* dbg = nullptr, long long x_elems_override = -1,
+                          const c10::optional<Tensor>& y_bf8 = c10::nullopt,
+                          const c10::optional<Tensor>& bf8_scale = c10::nullopt,
+                          const c10::optional<Tensor>& bf8_amax = c10::nullopt) {
+  check_dev("conv_fwd_impl", x, w, bias, mask, y, mbits, y_bf8, bf8_scale, bf8_amax);
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
   CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
   CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y);
@@ -115,6 +118,21 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
     else a.mbits_in = reinterpret_cast<const uint32_t*>(mbits->data_ptr<int>());
   }
   TORCH_CHECK(mode != agk::MODE_MASKBITS || a.mbits_in, "mode 3 needs mbits");
+  if (y_bf8.has_value()) {  // dgrad's e5m2 copy (y * bf8_scale) and max |y|, for the fp8 wgrad
+    TORCH_CHECK(mode == agk::MODE_MASKBITS, "y_bf8: bitmask dgrad (mode 3) only");
+    CHECK_DEV(*y_bf8);
+    TORCH_CHECK(y_bf8->scalar_type() == at::kByte && y_bf8->is_contiguous() && y_bf8->sizes() == y.sizes(),
+                "y_bf8: uint8 with y's shape");
+    TORCH_CHECK(bf8_scale.has_value() && bf8_scale->scalar_type() == at::kFloat && bf8_scale->numel() >= 1,
+                "y_bf8 needs a device fp32 scale");
+    a.y_bf8 = y_bf8->data_ptr<uint8_t>();
+    a.bf8_scale = bf8_scale->data_ptr<float>();
+    if (bf8_amax.has_value()) {
+      TORCH_CHECK(bf8_amax->scalar_type() == at::kInt && bf8_amax->numel() >= agk::kFp8AmaxSlots &&
+                      bf8_amax->is_contiguous(), "bf8_amax: int32[64]");
+      a.bf8_amax = reinterpret_cast<unsigned*>(bf8_amax->data_ptr<int>());
+    }
+  }
   if (a.M == 0) return;
   agk::launch_conv_fwd(a, (int)mode, cur_stream());
   launch_check("conv_fwd");
@@ -154,6 +172,45 @@ inline void conv_wgrad_impl(const Tensor& x, const Tensor& dz, const Tensor& sla
   a.ksteps_per_split = (nks + a.nsplit - 1) / a.nsplit;
   agk::launch_conv_wgrad(a, cur_stream());
   launch_check("conv_wgrad");
+}
+
+// fp8 wgrad: x8 e4m3 (B, HPi, HPi, Cin) uint8, dz8 e5m2 (B, HPo, HPo, Cout) uint8, slabs as conv_wgrad_impl
+inline void conv_wgrad_fp8_impl(const Tensor& x8, const Tensor& dz8, const Tensor& slab, const Tensor& dbslab,
+                                const Tensor& xscale, const Tensor& gscale, const Tensor& gmul, int64_t K, int64_t S,
+                                int64_t Pin, int64_t Po) {
+  check_dev("conv_wgrad_fp8", x8, dz8, slab, dbslab, xscale, gscale, gmul);
+  TORCH_CHECK(x8.scalar_type() == at::kByte && dz8.scalar_type() == at::kByte, "x8 / dz8: uint8 (e4m3 / e5m2)");
+  CHECK_F32(slab); CHECK_F32(dbslab);
+  CHECK_CONTIG(x8); CHECK_CONTIG(dz8); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
+  TORCH_CHECK(xscale.scalar_type() == at::kInt && gscale.scalar_type() == at::kInt && gmul.scalar_type() == at::kFloat &&
+                  xscale.numel() >= 1 && gscale.numel() >= 1 && gmul.numel() >= 1,
+              "scales: int32 E8M0 exponents, fp32 gradient multiplier");
+  TORCH_CHECK(x8.dim() == 4 && dz8.dim() == 4 && dz8.size(0) == x8.size(0), "x8, dz8: (B, HP, HP, C) with the same B");
+  TORCH_CHECK(x8.numel() < (1ll << 31) && dz8.numel() < (1ll << 31), "tensor too large for int32 offsets");
+  const int64_t B = x8.size(0), HPi = x8.size(1), Cin = x8.size(3);
+  const int64_t HPo = dz8.size(1), Cout = dz8.size(3);
+  TORCH_CHECK(agk::wgrad_fp8_supported((int)Cout, (int)Cin, (int)K), "conv_wgrad_fp8: 160 -> 160 3x3 layers only");
+  TORCH_CHECK(HPi == S + 2 * Pin && HPo == S + 2 * Po && Po >= 1 && Pin >= K / 2, "geometry mismatch");
+  const int64_t nsplit = slab.size(0);
+  TORCH_CHECK(slab.dim() == 4 && slab.size(1) == K * K && slab.size(2) == Cout && slab.size(3) == Cin, "bad slab");
+  TORCH_CHECK(dbslab.size(0) == nsplit && dbslab.size(1) == Cout, "bad dbias slab");
+  agk::ConvWgradFp8Args a{};
+  a.x8 = x8.data_ptr<uint8_t>();
+  a.dz8 = dz8.data_ptr<uint8_t>();
+  a.slab = slab.data_ptr<float>();
+  a.dbias_slab = dbslab.data_ptr<float>();
+  a.xscale = xscale.data_ptr<int>();
+  a.gscale = gscale.data_ptr<int>();
+  a.gmul = gmul.data_ptr<float>();
+  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K; a.T = (int)(K * K);
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
+  const int sp = agk::wgrad_fp8_stage_pixels();
+  const int nks = (a.M + sp - 1) / sp;
+  a.nsplit = (int)nsplit;
+  a.ksteps_per_split = (nks + a.nsplit - 1) / a.nsplit;
+  if (a.M == 0) return;
+  agk::launch_conv_wgrad_fp8(a, cur_stream());
+  launch_check("conv_wgrad_fp8");
 }
 
 inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales,

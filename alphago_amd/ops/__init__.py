@@ -325,6 +325,31 @@ def pack_weights_fp8_multi(ws, outs, scales_dev: torch.Tensor, layer, transposed
                                   [int(bool(x)) for x in transposed])
 
 
+def conv_dgrad_bits_bf8(dz, wd, dx, mbits, dx8, scale, K: int, S: int, amax=None, tile: int = 0):
+    """Bitmask dgrad (conv_fwd mode 3) that also writes dx8 = e5m2(dx * scale[0]) for the fp8 wgrad
+    and folds max |dx| into ``amax`` (int32[64] float bits: the next step's delayed scale)."""
+    _ops().conv_dgrad_bits_bf8(dz, wd, dx, mbits, dx8, scale, amax, K, S, tile)
+
+
+def conv_wgrad_fp8(x8, dz8, slab, dbslab, xscale, gscale, gmul, K: int, S: int, Pin: int, Po: int = 1):
+    """fp8 weight gradient of a 160 -> 160 3x3 layer (conv_wgrad_fp8.hip): e4m3 x8 (E8M0 exponent
+    xscale[0]) x e5m2 dz8 (gscale[0]; gmul[0] = its 2^e multiplier, undone in the bias sums) into the
+    same split slab as conv_wgrad; reduce with conv_wgrad_reduce."""
+    _ops().conv_wgrad_fp8(x8, dz8, slab, dbslab, xscale, gscale, gmul, K, S, Pin, Po)
+
+
+def wgrad_fp8_supported(cout_p: int, cin_p: int, K: int) -> bool:
+    """Shapes the fp8 wgrad kernel covers (the value net's 160 -> 160 3x3 layers)."""
+    return cout_p == 160 and cin_p == 160 and K == 3
+
+
+def wgrad_fp8_nsplit(M: int, K: int = 3, target_wgs: int = 512) -> int:
+    """Pixel splits of the fp8 wgrad (128-pixel steps, one 160 x 160 tile per tap and split,
+    two workgroups per CU): one resident round."""
+    nks = (M + 127) // 128
+    return max(1, min(target_wgs // (K * K), nks))
+
+
 def wino_pack_weights(w_oihw: torch.Tensor) -> torch.Tensor:
     """Kernel-lab Winograd F(2x2, 3x3) weights (winograd.hip): U = G g G^T per (cout, cin), bf16,
     packed [16 xi][Cin/32][Cout/16][64 lanes][8] so that one MFMA B fragment is one 16-B load per

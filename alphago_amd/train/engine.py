@@ -123,7 +123,8 @@ class HipConvTrainer:
     def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
                  overlap: bool = False, wgrad_target_wgs: int = 0, iterations: int = 0, precision: str = "bf16",
                  wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: bool = False,
-                 reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None):
+                 reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None,
+                 fp8_wgrad: Optional[bool] = None):
         ops.load()
         # wgrad kernel: 0 = per-tap kernel (default), 5 = one-kernel-row wgrad (opt-in, slower so far)
         self.wgrad_variant = int(os.environ.get("ALPHAGO_AMD_WGRAD_VARIANT", "0")) if wgrad_variant is None \
@@ -265,6 +266,27 @@ class HipConvTrainer:
             self.gosc8 = torch.ones(L, device=dev)
             self.gamax8 = ops.fp8_amax_buffer(L, dev)
             self._g8_calibrated = False
+            # fp8 wgrad (160 -> 160 3x3 layers, conv_wgrad_fp8.hip): e4m3 inputs kept per layer (the
+            # forward's e4m3 outputs instead of a two-buffer ring), e5m2 output gradients written by
+            # the bitmask dgrad's epilogue (the head's by one quantise pass), delayed gradient scales
+            # as the fp8 dgrad's.  Layer 0 (49 planes) keeps the bf16 wgrad.
+            if fp8_wgrad is None:
+                fp8_wgrad = os.environ.get("ALPHAGO_AMD_FP8_WGRAD", "0") == "1"
+            self.fp8_wgrad = bool(fp8_wgrad) and all(
+                ops.wgrad_fp8_supported(self.Fp, self.Fp, self.K[l]) for l in range(1, L))
+            self._w8layers = set(range(1, L)) if self.fp8_wgrad else set()
+            if self.fp8_wgrad:
+                self.X8 = [None] + [torch.zeros(self.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(1, L)]
+                self.DZ8 = [None] + [torch.zeros(self.DZ[0].shape, dtype=torch.uint8, device=dev) for _ in range(1, L)]
+                self.nsplit8 = ops.wgrad_fp8_nsplit(M, 3)
+                need = self.nsplit8 * 9 * self.Fp * self.Fp
+                if need > self._slabs[0].numel():
+                    self._slabs = [torch.empty(need, device=dev) for _ in self._slabs]
+                if self.nsplit8 * self.Fp > self._dbslabs[0].numel():
+                    self._dbslabs = [torch.zeros(self.nsplit8 * self.Fp, device=dev) for _ in self._dbslabs]
+        else:
+            self.fp8_wgrad = False
+            self._w8layers = set()
         # Keras-SGD schedule mirrored on the device (float64 {lr0, decay, iterations, lr}) so that
         # the SGD step reads its learning rate from memory: the whole step is graph-capturable
         self._sched_dev = torch.zeros(4, dtype=torch.float64, device=dev)
@@ -344,10 +366,11 @@ class HipConvTrainer:
         x8, pin = self.X08, self.P0
         for l in range(self.L):
             last = l == self.L - 1
+            y8 = None if last else (self.X8[l + 1] if self.fp8_wgrad else self.Y8[l % 2])
             ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l], self.S,
-                             pin, 1, y_bf16=self.Y[l], y_fp8=None if last else self.Y8[l % 2],
-                             amax=self.amax8[l], mbits=None if last else self.MBITS[l])
-            x8, pin = self.Y8[l % 2], 1
+                             pin, 1, y_bf16=self.Y[l], y_fp8=y8, amax=self.amax8[l],
+                             mbits=None if last else self.MBITS[l])
+            x8, pin = y8, 1
         ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)  # next step's activation scales
 
     @torch.no_grad()
@@ -376,15 +399,20 @@ class HipConvTrainer:
         x, pin = self._layer_in(l)
         T = self.K[l] ** 2
         cin_p = x.shape[3]
-        ns = self.nsplit[l]
+        f8 = l in self._w8layers and self._g8_calibrated
+        ns = self.nsplit8 if f8 else self.nsplit[l]
         i = l % len(self._slabs)
         slab = self._slabs[i][:ns * T * self.Fp * cin_p].view(ns, T, self.Fp, cin_p)
         dbs = self._dbslabs[i][:ns * self.Fp].view(ns, self.Fp)
         sr = self.s_r
         if sr is not None and self._slab_free[i] is not None:
             torch.cuda.current_stream(self.device).wait_event(self._slab_free[i])
-        ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0,
-                       variant=self.wgrad_variant)
+        if f8:  # e5m2 dZ x e4m3 X, dequantised by the MFMA's block scales
+            ops.conv_wgrad_fp8(self.X8[l], self.DZ8[l], slab, dbs, self.scales8[l, 0:1], self.gscales8[l, 0:1],
+                               self.gosc8[l:l + 1], self.K[l], self.S, pin, 1)
+        else:
+            ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0,
+                           variant=self.wgrad_variant)
 
         def reduce():
             ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)
@@ -407,6 +435,10 @@ class HipConvTrainer:
         red = reduce and (self.env.distributed or self._proxy is not None)
         if red and not self.defer_allreduce and -1 in self._bucket_after_layer:
             self.reducer.launch(self._bucket_after_layer[-1])
+        w8 = self.fp8_wgrad and self._g8_calibrated
+        if w8:  # the head's dZ in e5m2 for wgrad(L-1), and its max |dZ| for the next step's scale
+            top = self.L - 1
+            ops.quantize_bf8(self.DZ[top], self.DZ8[top], self.gosc8[top:top + 1], self.gamax8[top])
         for l in reversed(range(self.L)):
             if self.s_w is not None:
                 ev = main.record_event()
@@ -416,7 +448,11 @@ class HipConvTrainer:
             else:
                 self._wgrad_layer(l, red)
             if l > 0:
-                if self.precision == "fp8" and self.fp8_dgrad and self._g8_calibrated:
+                if w8 and l - 1 in self._w8layers:  # bitmask dgrad + the e5m2 copy wgrad(l-1) reads
+                    ops.conv_dgrad_bits_bf8(self.DZ[l], self.wd[l], self.DZ[l - 1], self.MBITS[l - 1],
+                                            self.DZ8[l - 1], self.gosc8[l - 1:l], self.K[l], self.S,
+                                            amax=self.gamax8[l - 1], tile=self.conv_tile)
+                elif self.precision == "fp8" and self.fp8_dgrad and self._g8_calibrated:
                     # fp8 dgrad straight from the bf16 dZ: converted to e5m2 in the kernel's registers
                     # (delayed per-layer scale gosc8[l]), ReLU' from the forward's bitmask, bf16 dx
                     # whose max |dx| sets the next step's scale of layer l-1
@@ -428,7 +464,7 @@ class HipConvTrainer:
                 else:  # ReLU' bitmask from the forward epilogue (bf16 and fp8 forwards write it)
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=self.conv_tile)
-        if self.precision == "fp8" and self.fp8_dgrad:
+        if self.precision == "fp8" and (self.fp8_dgrad or self.fp8_wgrad):
             if self._g8_calibrated:
                 ops.fp8_grad_scales(self.gamax8, self.gscales8, self.gosc8, 1)  # next step's gradient scales
             else:

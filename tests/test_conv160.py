@@ -259,3 +259,68 @@ def test_pack_weights_fp8_multi_matches_single(ops, cuda_device, Cin, Cout, K):
     assert torch.equal(a, b)
     if tr:
         assert torch.equal(at, bt)
+
+
+@pytest.mark.parametrize("B", [3, 7])
+def test_conv_wgrad_fp8_160(ops, cuda_device, B):
+    """fp8 wgrad (e5m2 dZ x e4m3 X, 128-pixel steps through ds_read_b64_tr_b8) vs fp32
+    conv2d_weight of the dequantised operands; bias gradient from the e5m2 bytes."""
+    torch.manual_seed(11)
+    S, K, C, Cp = 19, 3, 152, 160
+    x = torch.relu(torch.randn(B, C, S, S, device=cuda_device)) * 2.0
+    dz = torch.randn(B, C, S, S, device=cuda_device) * 1e-3
+    ex = ops.fp8_exponent(float(x.abs().max()), margin=0)
+    eg = ops.fp8_exponent(float(dz.abs().max()), margin=0) + 7
+    xq = (x * 2.0 ** ex).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** -ex
+    dzq = (dz * 2.0 ** eg).clamp(-57344, 57344).to(torch.float8_e5m2).float() * 2.0 ** -eg
+    x8 = torch.zeros((B, S + 2, S + 2, Cp), dtype=torch.uint8, device=cuda_device)
+    x8[:, 1:S + 1, 1:S + 1, :C] = (x * 2.0 ** ex).clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8).permute(0, 2, 3, 1)
+    dz8 = torch.zeros_like(x8)
+    dz8[:, 1:S + 1, 1:S + 1, :C] = (dz * 2.0 ** eg).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8).permute(0, 2, 3, 1)
+    ref_w = torch.nn.grad.conv2d_weight(xq, (C, C, K, K), dzq, padding=1)
+    ref_b = dzq.sum(dim=(0, 2, 3))
+    ns = ops.wgrad_fp8_nsplit(B * S * S)
+    slab = torch.full((ns, K * K, Cp, Cp), float("nan"), device=cuda_device)
+    dbs = torch.zeros(ns, Cp, device=cuda_device)
+    xs = torch.tensor([127 - ex], dtype=torch.int32, device=cuda_device)
+    gs = torch.tensor([127 - eg], dtype=torch.int32, device=cuda_device)
+    gm = torch.tensor([2.0 ** eg], device=cuda_device)
+    ops.conv_wgrad_fp8(x8, dz8, slab, dbs, xs, gs, gm, K, S, 1, 1)
+    gw = torch.zeros(C, C, K, K, device=cuda_device)
+    gb = torch.zeros(C, device=cuda_device)
+    ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert _rel_err(gw, ref_w) < 2e-3
+    assert _rel_err(gb, ref_b) < 2e-3
+
+
+def test_dgrad_bits_bf8_copy(ops, cuda_device):
+    """The bitmask dgrad's e5m2 copy is e5m2(dx * scale) of the fp32 result (the bf16 output rounds
+    the same value: rare one-step differences), and the amax slots hold max |dx|."""
+    torch.manual_seed(12)
+    B, S, K, C, Cp = 4, 19, 3, 152, 160
+    xin = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w0 = _bf(torch.randn(C, C, K, K, device=cuda_device) * 0.05)
+    wp0 = ops.packed_weight_like(w0, Cp, Cp)
+    ops.pack_weights([w0], [wp0])
+    y = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=cuda_device)
+    ops.conv_fwd(ops.to_padded(xin, 1, Cp), wp0, torch.zeros(Cp, device=cuda_device), y, K, S, 1, 1, mbits=mbits)
+    w = _bf(torch.randn(C, C, K, K, device=cuda_device) * 0.05)
+    wf, wd = ops.packed_weight_like(w, Cp, Cp), ops.packed_weight_like(w, Cp, Cp, transposed=True)
+    ops.pack_weights([w], [wf], [wd])
+    dz = ops.to_padded(_bf(torch.randn(B, C, S, S, device=cuda_device) * 1e-3), 1, Cp)
+    dx = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    dx8 = torch.zeros(dx.shape, dtype=torch.uint8, device=cuda_device)
+    amax = ops.fp8_amax_buffer(1, cuda_device)[0]
+    sc = torch.tensor([2.0 ** 20], device=cuda_device)
+    ops.conv_dgrad_bits_bf8(dz, wd, dx, mbits, dx8, sc, K, S, amax=amax)
+    ref = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    ops.conv_fwd(dz, wd, None, ref, K, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mbits)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, ref)  # the bf16 output is unchanged by the extra copy
+    q = (dx.float() * 2.0 ** 20).clamp(-57344, 57344).to(torch.float8_e5m2).view(torch.uint8)
+    assert (q != dx8).float().mean().item() < 0.02  # fp32 vs bf16-rounded source: rare 1-ulp differences
+    deq = dx8.view(torch.float8_e5m2).float() * 2.0 ** -20
+    assert _rel_err(deq, dx.float()) < 0.13
+    assert abs(amax.view(torch.float32).max().item() - dx.float().abs().max().item()) <= 1e-2 * dx.float().abs().max().item()

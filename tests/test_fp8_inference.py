@@ -53,12 +53,14 @@ def test_fp8_value_engine_matches_bf16(cuda_device, F):
     assert (v8 - v16).abs().max().item() < 0.05 + 0.1 * v16.abs().max().item()
 
 
-@pytest.mark.parametrize("F,fp8_dgrad", [(192, False), (152, False), (152, True)])
-def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad):
+@pytest.mark.parametrize("F,fp8_dgrad,fp8_wgrad", [(192, False, False), (152, False, False), (152, True, False),
+                                                 (152, False, True)])
+def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad, fp8_wgrad):
     """Value-net training with the fp8 forward: gradients close to the bf16
     trainer's, loss goes down, activation scales are updated on the device
     (F = 152: 160-channel e4m3 activations, 160-wide tiles; fp8_dgrad: e5m2 x e4m3
-    dgrad from the second step on, after the first step calibrated its scales)."""
+    dgrad, fp8_wgrad: e5m2 x e4m3 wgrad, each from the second step on, after the first step
+    calibrated the gradient scales)."""
     import copy
 
     from alphago_amd.models.nets import ValueNet
@@ -70,7 +72,9 @@ def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad):
     net16 = copy.deepcopy(net)
     planes = _planes(B, 49, seed=5).to(cuda_device)
     z = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
-    t8 = HipValueTrainer(net, B, lr=0.05, device=cuda_device, precision="fp8", fp8_dgrad=fp8_dgrad)
+    t8 = HipValueTrainer(net, B, lr=0.05, device=cuda_device, precision="fp8", fp8_dgrad=fp8_dgrad,
+                         fp8_wgrad=fp8_wgrad)
+    assert t8.fp8_wgrad == fp8_wgrad
     t16 = HipValueTrainer(net16, B, lr=0.05, device=cuda_device)
     t8.compute_grads(planes, z)
     t16.compute_grads(planes, z)
@@ -78,7 +82,7 @@ def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad):
         a, b = t8.fp.grad_views[name], t16.fp.grad_views[name]
         cos = torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item()
         assert cos > 0.9, (name, cos)
-    if fp8_dgrad:  # second backward on the e5m2 path, same weights as the bf16 trainer
+    if fp8_dgrad or fp8_wgrad:  # second backward on the e5m2 path, same weights as the bf16 trainer
         t8.compute_grads(planes, z)
         t16.compute_grads(planes, z)
         for name in t8.fp.names:
