@@ -18,7 +18,9 @@
 // Scales: the MFMA's E8M0 block scales dequantise both operands (127 - e, from the device-resident
 // delayed scales), so the fp32 partials go to the same per-split slab as the bf16 wgrad and the same
 // deterministic conv_wgrad_reduce sums them.  Bias gradient: the tap-0 workgroups sum the e5m2
-// gradient bytes of their A fragments (e5m2 = the high byte of an fp16) and divide by the multiplier.
+// gradient bytes of their A fragments (e5m2 = the high byte of an fp16) and divide by the multiplier;
+// they also fold max |dZ| into the delayed-scale amax slots (a saturated e5m2 value reads 57344 / 2^eg,
+// so a scale that overflows shrinks by the margin every step until it fits).
 // Borders: pixels past the batch read padded-pixel 0 of dZ (always zero).
 #include <hip/hip_runtime.h>
 
@@ -121,6 +123,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
   float dbs[NBn];
 #pragma unroll
   for (int i = 0; i < NBn; ++i) dbs[i] = 0.f;
+  float vmax = 0.f;  // tap-0 workgroups: max |e5m2 dZ| (scaled)
   const bool do_bias = (t == 0) && (c0 == 0) && (wc == 0);
 
   // transposed-read address of read j (K rows 8 j .. 8 j + 7 of the lane group's 32) for 16-channel
@@ -173,8 +176,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
 #pragma unroll
         for (int d = 0; d < 8; ++d) {
           const unsigned w = (unsigned)af[i][d];
-          s += bf8_to_f32(w & 0xffu) + bf8_to_f32((w >> 8) & 0xffu) + bf8_to_f32((w >> 16) & 0xffu) +
-               bf8_to_f32(w >> 24);
+          const float v0 = bf8_to_f32(w & 0xffu), v1 = bf8_to_f32((w >> 8) & 0xffu);
+          const float v2 = bf8_to_f32((w >> 16) & 0xffu), v3 = bf8_to_f32(w >> 24);
+          s += (v0 + v1) + (v2 + v3);
+          vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v0), fabsf(v1)), fmaxf(fabsf(v2), fabsf(v3))));
         }
         dbs[i] += s;
       }
@@ -206,6 +211,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
       if (lane < 16) a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / 2) + i * 16 + lane] = s * inv;
+    }
+    if (a.amax) {  // the delayed scale of the next step: max |dZ| = max |e5m2| / 2^eg
+      vmax = wave_max(vmax) * inv;
+      if (lane == 0 && vmax > 0.f) atomicMax(a.amax + (split & (kFp8AmaxSlots - 1)), __float_as_uint(vmax));
     }
   }
 }

@@ -56,6 +56,7 @@ struct ConvWgradFp8Args {
   const int* xscale;   // device E8M0 exponent 127 - ex
   const int* gscale;   // device E8M0 exponent 127 - eg
   const float* gmul;   // device 2^eg (the bias sums undo it)
+  unsigned* amax;      // optional: max |dZ| (float bits, 64 slots) from the tap-0 workgroups' e5m2 bytes
   int M, S, Cin, Cout, K, T;
   int HPi, offi, HPo, Po;
   int ksteps_per_split, nsplit;  // in 128-pixel steps

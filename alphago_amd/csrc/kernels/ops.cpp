@@ -42,8 +42,8 @@ void conv_dgrad_bits_bf8(const Tensor& dz, const Tensor& wd, const Tensor& dx, c
 
 void conv_wgrad_fp8(const Tensor& x8, const Tensor& dz8, const Tensor& slab, const Tensor& dbslab,
                     const Tensor& xscale, const Tensor& gscale, const Tensor& gmul, int64_t K, int64_t S, int64_t Pin,
-                    int64_t Po) {
-  conv_wgrad_fp8_impl(x8, dz8, slab, dbslab, xscale, gscale, gmul, K, S, Pin, Po);
+                    int64_t Po, const c10::optional<Tensor>& amax) {
+  conv_wgrad_fp8_impl(x8, dz8, slab, dbslab, xscale, gscale, gmul, K, S, Pin, Po, amax);
 }
 
 int64_t wgrad_fp8_stage_px() { return agk::wgrad_fp8_stage_pixels(); }
@@ -599,7 +599,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("conv_dgrad_bits_bf8(Tensor dz, Tensor wd, Tensor(a!) dx, Tensor mbits, Tensor(b!) dx8, Tensor scale, "
         "Tensor(c!)? amax, int K, int S, int tile=0) -> ()");
   m.def("conv_wgrad_fp8(Tensor x8, Tensor dz8, Tensor(a!) slab, Tensor(b!) dbslab, Tensor xscale, Tensor gscale, "
-        "Tensor gmul, int K, int S, int Pin, int Po) -> ()");
+        "Tensor gmul, int K, int S, int Pin, int Po, Tensor(c!)? amax=None) -> ()");
   m.def("wgrad_fp8_stage_px() -> int", &wgrad_fp8_stage_px);
   m.def(
       "policy_head(Tensor y, Tensor w, Tensor b, Tensor? target, Tensor? legal, Tensor? weight, Tensor(a!)? dz, Tensor(b!)? loss, "

@@ -177,8 +177,8 @@ inline void conv_wgrad_impl(const Tensor& x, const Tensor& dz, const Tensor& sla
 // fp8 wgrad: x8 e4m3 (B, HPi, HPi, Cin) uint8, dz8 e5m2 (B, HPo, HPo, Cout) uint8, slabs as conv_wgrad_impl
 inline void conv_wgrad_fp8_impl(const Tensor& x8, const Tensor& dz8, const Tensor& slab, const Tensor& dbslab,
                                 const Tensor& xscale, const Tensor& gscale, const Tensor& gmul, int64_t K, int64_t S,
-                                int64_t Pin, int64_t Po) {
-  check_dev("conv_wgrad_fp8", x8, dz8, slab, dbslab, xscale, gscale, gmul);
+                                int64_t Pin, int64_t Po, const c10::optional<Tensor>& amax = c10::nullopt) {
+  check_dev("conv_wgrad_fp8", x8, dz8, slab, dbslab, xscale, gscale, gmul, amax);
   TORCH_CHECK(x8.scalar_type() == at::kByte && dz8.scalar_type() == at::kByte, "x8 / dz8: uint8 (e4m3 / e5m2)");
   CHECK_F32(slab); CHECK_F32(dbslab);
   CHECK_CONTIG(x8); CHECK_CONTIG(dz8); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
@@ -202,6 +202,11 @@ inline void conv_wgrad_fp8_impl(const Tensor& x8, const Tensor& dz8, const Tenso
   a.xscale = xscale.data_ptr<int>();
   a.gscale = gscale.data_ptr<int>();
   a.gmul = gmul.data_ptr<float>();
+  if (amax.has_value()) {
+    TORCH_CHECK(amax->scalar_type() == at::kInt && amax->numel() >= agk::kFp8AmaxSlots && amax->is_contiguous(),
+                "amax: int32[64]");
+    a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
+  }
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K; a.T = (int)(K * K);
   a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
   const int sp = agk::wgrad_fp8_stage_pixels();

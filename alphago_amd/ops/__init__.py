@@ -331,11 +331,12 @@ def conv_dgrad_bits_bf8(dz, wd, dx, mbits, dx8, scale, K: int, S: int, amax=None
     _ops().conv_dgrad_bits_bf8(dz, wd, dx, mbits, dx8, scale, amax, K, S, tile)
 
 
-def conv_wgrad_fp8(x8, dz8, slab, dbslab, xscale, gscale, gmul, K: int, S: int, Pin: int, Po: int = 1):
+def conv_wgrad_fp8(x8, dz8, slab, dbslab, xscale, gscale, gmul, K: int, S: int, Pin: int, Po: int = 1, amax=None):
     """fp8 weight gradient of a 160 -> 160 3x3 layer (conv_wgrad_fp8.hip): e4m3 x8 (E8M0 exponent
     xscale[0]) x e5m2 dz8 (gscale[0]; gmul[0] = its 2^e multiplier, undone in the bias sums) into the
-    same split slab as conv_wgrad; reduce with conv_wgrad_reduce."""
-    _ops().conv_wgrad_fp8(x8, dz8, slab, dbslab, xscale, gscale, gmul, K, S, Pin, Po)
+    same split slab as conv_wgrad; reduce with conv_wgrad_reduce.  ``amax`` (int32[64]): max |dZ|
+    from the e5m2 bytes (the next step's delayed scale)."""
+    _ops().conv_wgrad_fp8(x8, dz8, slab, dbslab, xscale, gscale, gmul, K, S, Pin, Po, amax)
 
 
 def wgrad_fp8_supported(cout_p: int, cin_p: int, K: int) -> bool:

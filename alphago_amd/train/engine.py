@@ -408,8 +408,10 @@ class HipConvTrainer:
         if sr is not None and self._slab_free[i] is not None:
             torch.cuda.current_stream(self.device).wait_event(self._slab_free[i])
         if f8:  # e5m2 dZ x e4m3 X, dequantised by the MFMA's block scales
+            # (its tap-0 workgroups also fold max |dZ| into the delayed-scale slots of layer l)
             ops.conv_wgrad_fp8(self.X8[l], self.DZ8[l], slab, dbs, self.scales8[l, 0:1], self.gscales8[l, 0:1],
-                               self.gosc8[l:l + 1], self.K[l], self.S, pin, 1)
+                               self.gosc8[l:l + 1], self.K[l], self.S, pin, 1,
+                               amax=self.gamax8[l] if l < self.L - 1 else None)
         else:
             ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0,
                            variant=self.wgrad_variant)
@@ -451,7 +453,7 @@ class HipConvTrainer:
                 if w8 and l - 1 in self._w8layers:  # bitmask dgrad + the e5m2 copy wgrad(l-1) reads
                     ops.conv_dgrad_bits_bf8(self.DZ[l], self.wd[l], self.DZ[l - 1], self.MBITS[l - 1],
                                             self.DZ8[l - 1], self.gosc8[l - 1:l], self.K[l], self.S,
-                                            amax=self.gamax8[l - 1], tile=self.conv_tile)
+                                            tile=self.conv_tile)
                 elif self.precision == "fp8" and self.fp8_dgrad and self._g8_calibrated:
                     # fp8 dgrad straight from the bf16 dZ: converted to e5m2 in the kernel's registers
                     # (delayed per-layer scale gosc8[l]), ReLU' from the forward's bitmask, bf16 dx
