@@ -186,6 +186,11 @@ static void launch_wgrad_160x160(const ConvWgradArgs& a, hipStream_t st) {
 
 int wgrad_stage_pixels() { return 32 * kWgradKsub; }
 
+// tap-pair / line-staged wgrads (variants 6-8): kernel lab (conv_lab.hip, profiles/r3_wgrad_pair.md)
+static bool wgrad_pair_applies(int Cout, int Cin, int cin_real, int K) {
+  return K == 3 && Cout == 192 && Cin == 192 && cin_real == Cin;
+}
+
 #ifdef AGK_DEBUG
 unsigned debug_error_fetch_and_clear(hipStream_t st) {
   hip_check(hipStreamSynchronize(st), "debug: stream synchronize");
@@ -197,6 +202,14 @@ unsigned debug_error_fetch_and_clear(hipStream_t st) {
 #endif
 
 void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3]) {
+  if ((variant == 6 || variant == 8) && wgrad_pair_applies(Cout, Cin, cin_real, K)) {
+    // tap pairs: 4.5 workgroups per split (9 per two splits), one per CU -- reported as 9 per
+    // split pair and 2 per CU so that nsplit = CUs * out[2] / out[1] stays an integer division
+    out[0] = 2;
+    out[1] = 9;
+    out[2] = 2;
+    return;
+  }
   const int code = variant == 5 ? wgrad_row_code(Cout, Cin, cin_real, K) : 0;
   if (code) {  // one kernel row per workgroup, one workgroup per CU (~170 VGPRs, 8 or 6 waves)
     out[0] = K;
@@ -205,7 +218,7 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
     return;
   }
   // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
-  const int taps = wgrad_tap_group(Cout, Cin, K, variant == 5 ? 0 : variant);
+  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 8) ? 0 : variant);
   const bool c48 = cin_real <= 48 && Cin == 64;
   const int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
   const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;
@@ -238,6 +251,12 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
     }
     a.variant = 0;
   }
+#ifdef AGK_KERNEL_LAB
+  if (a.variant >= 6 && a.variant <= 8) {  // tap pairs (8: DMA spread) / line-staged per-tap kernel
+    if (wgrad_pair_applies(a.Cout, a.Cin, a.cin_real, a.K) && launch_conv_wgrad_line_lab(a, st)) return;
+    a.variant = 0;
+  }
+#endif
   const bool n192 = a.Cout % 192 == 0, c192 = a.Cin % 192 == 0;
   const bool n128 = a.Cout % 128 == 0, c128 = a.Cin % 128 == 0;
   if (a.Cout == 160) {  // value net (152 filters padded to 160)

@@ -57,6 +57,13 @@ __device__ __forceinline__ void vmcnt_wait_dyn(int n) {
 }
 
 // ---- wgrad helpers (conv.hip, conv_wgrad_row.hip)
+// s_waitcnt lgkmcnt(CNT) tying one read pair: issued for each pair of a group whose reads are all
+// older than the CNT most recent ones (the first wait blocks, the rest are already satisfied)
+template <int CNT>
+__device__ __forceinline__ void lgkm_wait_pair(bf16x4& a, bf16x4& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(CNT));
+}
+
 // s_waitcnt lgkmcnt(0) with every listed read result as an in/out operand:
 // nothing that uses them can be scheduled above the wait.
 template <int N>

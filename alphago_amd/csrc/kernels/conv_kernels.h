@@ -375,8 +375,58 @@ static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
 // and reuses each staged dz tile for all of them; the x image of tap kw is the
 // tap-0 image shifted by kw columns (kw * Cin elements).  This triples (5x5:
 // quintuples) the MFMAs per staged dz byte, the limiter of the 64-wide tile.
-template <int WN, int WC, int KSUB, int NWC = 4, int TAPS = 1>
-__global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs a) {
+// the split's partial tile D[n][c] (lane owns n..n+3 at column c) and the bias partial
+template <int WN, int WC, int NWC, int TAPS>
+__device__ __forceinline__ void wgrad_store(const ConvWgradArgs& a, const f32x4 (&acc)[TAPS][WN / 32][WC / (16 * NWC)],
+                                            const float (&dbs)[WN / 32], bool do_bias, int split, int t, int n0, int c0,
+                                            int wn, int wc, int lane, int zero_split) {
+  constexpr int NBn = WN / 32, NBc = WC / (16 * NWC);
+  const int nb0 = n0 + wn * (WN / 2) + ((lane >> 4) << 2);
+  const int cbase = c0 + wc * (WC / NWC) + (lane & 15);
+#pragma unroll
+  for (int tp = 0; tp < TAPS; ++tp) {
+    float* out = a.slab + ((size_t)split * a.T + t + tp) * (size_t)a.Cout * a.Cin;
+#pragma unroll
+    for (int i = 0; i < NBn; ++i)
+#pragma unroll
+      for (int j = 0; j < NBc; ++j) {
+        const int n = nb0 + i * 16;
+        const int c = cbase + j * 16;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(size_t)(n + r) * a.Cin + c] = acc[tp][i][j][r];
+      }
+  }
+  if (zero_split >= 0) {  // PAIR's odd tap: the second split it covered contributes zeros
+    float* out = a.slab + ((size_t)zero_split * a.T + t) * (size_t)a.Cout * a.Cin;
+#pragma unroll
+    for (int i = 0; i < NBn; ++i)
+#pragma unroll
+      for (int j = 0; j < NBc; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(size_t)(nb0 + i * 16 + r) * a.Cin + cbase + j * 16] = 0.f;
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < NBn; ++i) {
+      float s = dbs[i];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (lane < 16) a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / 2) + i * 16 + lane] = s;
+    }
+  }
+}
+
+
+// PAIR (3x3 only, with TAPS == 2, KSUB == 2): a workgroup owns two consecutive taps t, t+1 of
+// any kernel rows (tstep = the element offset from tap t's x image to tap t+1's) and reuses each
+// staged dz tile for both; per 64-pixel stage it moves 72 KB for 4.7 M MACs -- the forward's
+// ratio and its one workgroup per CU -- instead of the per-tap kernel's 24 KB for 1.2 M.  The
+// odd last tap (K*K = 9) runs the one-tap body over two splits' pixels, so every workgroup of
+// the grid does the same MFMA work; it writes its sum into the first split's slab and zeros
+// into the second's.
+template <int WN, int WC, int KSUB, int NWC, int TAPS>
+__device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, int ks_begin, int ks_end, int t,
+                                           int tstep, int n0, int c0, int zero_split) {
   // 2 (n) x NWC (c) waves; NWC = 2 gives each wave a 96x96 tile at 192x192
   // (a third fewer LDS fragment reads per MFMA than NWC = 4)
   constexpr int NWAVES = 2 * NWC;
@@ -394,36 +444,9 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
   const int lane = threadIdx.x & 63;
   const int wave = wave_id();
   const int wn = wave / NWC, wc = wave % NWC;
-  // workgroup -> (split, tap group, channel block).  xcd_group (tap-merged rows): the hardware
-  // deals workgroups to the 8 XCDs round robin in launch order, which puts the K kernel-row
-  // workgroups of a split -- all reading the same dZ rows -- on K different L2s, so every dZ
-  // byte comes from the Infinity Cache K times (layer 0: 3 % L2 hits, profiles/r3_small_batch.md).
-  // Grouped, each XCD runs a contiguous range of split-major work and a split's rows share an L2.
-  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
-  if (TAPS > 1 && a.xcd_group) {
-    const int gyz = gridDim.y * gridDim.z;
-    const int nwg = gridDim.x * gyz;
-    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    const int xcd = lin & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int l = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (lin >> 3);
-    bx = l / gyz;
-    const int rem = l - bx * gyz;
-    by = rem / gridDim.z;
-    bz = rem - by * gridDim.z;
-  }
-  const int split = bx;
-  const int t = by * TAPS;  // first tap of the group
-  const int ncb = a.Cin / WC;
-  const int n0 = (bz / ncb) * WN;
-  const int c0 = (bz % ncb) * WC;
   const int kh = t / a.K, kw = t - (t / a.K) * a.K;
   const int toff = (kh * a.HPi + kw) * a.Cin + c0;
   const int SS = a.S * a.S;
-  // a.ksteps_per_split is in units of one stage (KSUB*32 pixels)
-  const int ks_begin = split * a.ksteps_per_split;
-  int ks_end = ks_begin + a.ksteps_per_split;
-  const int nks_total = (a.M + 32 * KSUB - 1) / (32 * KSUB);
-  if (ks_end > nks_total) ks_end = nks_total;
 
   auto stage = [&](int ks, int buf) {
     const int half = (lane & 1) * 8;
@@ -462,9 +485,9 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
         const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
         if (jj >= WN / 16 && jj < NINSTR / KSUB) {
           const int xj = jj - WN / 16;  // tap xj / XP, channel piece xj % XP
-          const long long o = (long long)xr[sub] + half + (xj / XP) * a.Cin + (xj % XP) * 16;
+          const long long o = (long long)xr[sub] + half + (xj / XP) * tstep + (xj % XP) * 16;
           const bool ok = AGK_DCHECK(o >= 0 && o + 8 <= a.x_elems, DBG_WG_X);
-          glds16(ok ? xsrc + (xj / XP) * a.Cin + (xj % XP) * 16 : a.x, base + sub * SUB + jj * 1024);
+          glds16(ok ? xsrc + (xj / XP) * tstep + (xj % XP) * 16 : a.x, base + sub * SUB + jj * 1024);
         }
       }
 #else
@@ -478,7 +501,7 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
         const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
         if (jj >= WN / 16 && jj < NINSTR / KSUB) {
           const int xj = jj - WN / 16;  // tap xj / XP, channel piece xj % XP
-          glds16(xsrc + (xj / XP) * a.Cin + (xj % XP) * 16, base + sub * SUB + jj * 1024);
+          glds16(xsrc + (xj / XP) * tstep + (xj % XP) * 16, base + sub * SUB + jj * 1024);
         }
       }
 #endif
@@ -561,31 +584,315 @@ __global__ __launch_bounds__(128 * NWC, 1) void conv_wgrad_kernel(ConvWgradArgs 
     __syncthreads();
   }
 
-  // --- write the split's partial tile: D[n][c], lane owns n..n+3 at column c
-  const int nb0 = n0 + wn * (WN / 2) + ((lane >> 4) << 2);
-  const int cbase = c0 + wc * (WC / NWC) + (lane & 15);
+  wgrad_store<WN, WC, NWC, TAPS>(a, acc, dbs, do_bias, split, t, n0, c0, wn, wc, lane, zero_split);
+}
+
+// LINE staging (wgrad variants 6 and 7): every DMA piece moves 8 whole 128-byte pixel lines (one
+// 64-channel chunk of 8 pixels; lanes 8r..8r+7 fill line r, their 16-byte chunks XOR-swizzled by
+// ((r >> 1) & 3) << 1) -- 8 cache lines per instruction instead of the 32 partial (32-byte) lines
+// of wgrad_tile's [16 ch][32 px] pieces.  The LDS image of a sub-step is [64-ch chunk][32 px][128 B]
+// and the transposed fragment reads address it directly (conflict-free: the 8 rows of a 32-lane
+// group land on 8 distinct 8-bank column groups).  Piece gi = wave + NWAVES * d always has row
+// group gi & 3 = wave & 3, so each lane stages one pixel per sub-step, as before.
+template <int WN, int WC, int KSUB, int NWC, int TAPS, bool ILVW = false>
+__device__ __forceinline__ void wgrad_tile_line(const ConvWgradArgs& a, int split, int ks_begin, int ks_end,
+                                                int t, int tstep, int n0, int c0, int zero_split) {
+  constexpr int NWAVES = 2 * NWC;
+  static_assert(NWAVES % 4 == 0 && WN % 64 == 0 && WC % 64 == 0 && KSUB <= 2, "line staging geometry");
+  constexpr int NBn = WN / 32;          // n blocks per wave (wave covers WN/2)
+  constexpr int NBc = WC / (16 * NWC);  // c blocks per wave (wave covers WC/NWC)
+  constexpr int NCN = WN / 64, NCC = WC / 64;  // 64-channel chunks of the two operands
+  constexpr int DZ_BYTES = WN * 64;
+  constexpr int X_BYTES = WC * 64 * TAPS;
+  constexpr int SUB = DZ_BYTES + X_BYTES;
+  constexpr int STAGE = SUB * KSUB;
+  constexpr int DZP = WN / 16 * KSUB, XPS = WC / 16 * TAPS * KSUB;  // 1 KB pieces per stage
+  static_assert((DZP + XPS) % NWAVES == 0, "pieces per wave");
+  constexpr int NPW = (DZP + XPS) / NWAVES;  // piece gi = wave + NWAVES * d: dz pieces first, then x
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wn = wave / NWC, wc = wave % NWC;
+  const int kh = t / a.K, kw = t - (t / a.K) * a.K;
+  const int toff = (kh * a.HPi + kw) * a.Cin + c0;
+  const int SS = a.S * a.S;
+  const int pp = wave & 3;                  // row group (8 pixels) of every piece this wave stages
+  const int r_st = pp * 8 + (lane >> 3);    // the pixel (LDS row) this lane stages in a sub-step
+  const int lchunk = ((lane & 7) ^ (((r_st >> 1) & 3) << 1)) * 8;  // its swizzled 16-B chunk (elements)
+
+  int dzr[KSUB], xr[KSUB];
+  auto stage_addr = [&](int ks) {
 #pragma unroll
-  for (int tp = 0; tp < TAPS; ++tp) {
-    float* out = a.slab + ((size_t)split * a.T + t + tp) * (size_t)a.Cout * a.Cin;
+    for (int sub = 0; sub < KSUB; ++sub) {
+      const int px = (ks * KSUB + sub) * 32 + r_st;
+      const int pm = px < a.M ? px : a.M - 1;
+      const int b = fdiv(pm, a.divSS);
+      const int rem = pm - b * SS;
+      const int ii = fdiv(rem, a.divS);
+      const int jx = rem - ii * a.S;
+      dzr[sub] = (px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po) * a.Cout : 0) + n0 + lchunk;
+      xr[sub] = ((b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi) * a.Cin + toff + lchunk;
+    }
+  };
+  // DMA pieces d0 <= d < d1 of the stage whose addresses stage_addr computed.  dz and x pieces in
+  // separate loops under wave-uniform conditions (see wgrad_tile: a per-piece select between the
+  // two tensors makes hipcc drain vmcnt before the LDS reads)
+  auto stage_pieces = [&](int buf, int d0, int d1) {
+    char* base = smem + buf * STAGE + pp * 1024;
+#pragma unroll
+    for (int d = 0; d < NPW; ++d) {
+      if (d < d0 || d >= d1) continue;
+      const int idx = (wave >> 2) + (NWAVES / 4) * d;  // (sub, chunk) of a dz piece
+      if (idx >= DZP / 4) continue;
+      const int sub = idx / NCN, cc = idx - sub * NCN;
+      const int o = (KSUB == 2 && sub ? dzr[KSUB - 1] : dzr[0]) + cc * 64;
+#ifdef AGK_DEBUG
+      const bool ok = AGK_DCHECK(o >= 0 && (long long)o + 8 <= a.dz_elems, DBG_WG_DZ);
+      glds16(ok ? a.dz + o : a.dz, base + sub * SUB + cc * 4096);
+#else
+      glds16(a.dz + o, base + sub * SUB + cc * 4096);
+#endif
+    }
+#pragma unroll
+    for (int d = 0; d < NPW; ++d) {
+      if (d < d0 || d >= d1) continue;
+      const int idx = (wave >> 2) + (NWAVES / 4) * d - DZP / 4;  // (sub, tap, chunk) of an x piece
+      if (idx < 0) continue;
+      const int sub = idx / (TAPS * NCC), rem = idx - sub * (TAPS * NCC);
+      const int tp = rem / NCC, cc = rem - tp * NCC;
+      const int o = (KSUB == 2 && sub ? xr[KSUB - 1] : xr[0]) + tp * tstep + cc * 64;
+#ifdef AGK_DEBUG
+      const bool ok = AGK_DCHECK(o >= 0 && (long long)o + 8 <= a.x_elems, DBG_WG_X);
+      glds16(ok ? a.x + o : a.x, base + sub * SUB + DZ_BYTES + (tp * NCC + cc) * 4096);
+#else
+      glds16(a.x + o, base + sub * SUB + DZ_BYTES + (tp * NCC + cc) * 4096);
+#endif
+    }
+  };
+  auto stage = [&](int ks, int buf) {
+    stage_addr(ks);
+    stage_pieces(buf, 0, NPW);
+  };
+
+  f32x4 acc[TAPS][NBn][NBc];
+#pragma unroll
+  for (int tp = 0; tp < TAPS; ++tp)
 #pragma unroll
     for (int i = 0; i < NBn; ++i)
 #pragma unroll
-      for (int j = 0; j < NBc; ++j) {
-        const int n = nb0 + i * 16;
-        const int c = cbase + j * 16;
+      for (int j = 0; j < NBc; ++j) acc[tp][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbs[NBn];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[(size_t)(n + r) * a.Cin + c] = acc[tp][i][j][r];
+  for (int i = 0; i < NBn; ++i) dbs[i] = 0.f;
+  const bool do_bias = (t == 0) && (c0 == 0) && (wc == 0);
+
+  // transposed reads: lane (g = lane>>4, q = (lane&15)>>2, p = lane&3) reads row 4g+q (16+4g+q),
+  // channels 4p..4p+3 of a 16-channel block: byte 32 (blk & 3) + 8p of the row, swizzled
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int rr = 4 * g + q;
+  const int swz = ((rr >> 1) & 3) << 1;
+  const int roff0 = rr * 128 + (p & 1) * 8;
+  const int roff1 = roff0 + 16 * 128;
+  auto blk_off = [&](int blk) { return (blk >> 2) * 4096 + (((((blk & 3) << 1) | (p >> 1)) ^ swz) << 4); };
+  int dzo[NBn], xo[NBc];
+#pragma unroll
+  for (int i = 0; i < NBn; ++i) dzo[i] = blk_off(wn * NBn + i);
+#pragma unroll
+  for (int j = 0; j < NBc; ++j) xo[j] = DZ_BYTES + blk_off(wc * NBc + j);
+  constexpr int NF = NBn + TAPS * NBc;  // fragments read per sub-step
+
+  if constexpr (TAPS == 2) {
+    // tap pairs: the second tap's x fragments are read while the first tap's MFMAs run (counted
+    // lgkmcnt); ILVW spreads the next stage's DMA pieces through the first sub-step's MFMAs (the
+    // last iteration re-stages clamped in-range rows into the idle buffer: no branch among them)
+    constexpr int N0 = NBn + NBc;  // dz + tap-0 fragments
+    constexpr int NMF = NBn * NBc;
+    if (ks_begin < ks_end) {
+      stage(ks_begin, 0);
+      wait_vmcnt0();
+      __syncthreads();
+    }
+    for (int ks = ks_begin; ks < ks_end; ++ks) {
+      const int cur = (ks - ks_begin) & 1;
+      if constexpr (ILVW) stage_addr(ks + 1);
+      else if (ks + 1 < ks_end) stage(ks + 1, cur ^ 1);
+#pragma unroll
+      for (int sub = 0; sub < KSUB; ++sub) {
+        const char* base = smem + cur * STAGE + sub * SUB;
+        bf16x4 tl[NF], th[NF];
+#pragma unroll
+        for (int i = 0; i < NBn; ++i) {
+          tl[i] = ds_read_tr16_asm(base + dzo[i] + roff0);
+          th[i] = ds_read_tr16_asm(base + dzo[i] + roff1);
+        }
+#pragma unroll
+        for (int tp = 0; tp < 2; ++tp)
+#pragma unroll
+          for (int j = 0; j < NBc; ++j) {
+            tl[NBn + tp * NBc + j] = ds_read_tr16_asm(base + tp * NCC * 4096 + xo[j] + roff0);
+            th[NBn + tp * NBc + j] = ds_read_tr16_asm(base + tp * NCC * 4096 + xo[j] + roff1);
+          }
+#pragma unroll
+        for (int f = 0; f < N0; ++f) lgkm_wait_pair<2 * NBc>(tl[f], th[f]);
+        bf16x8 af[NBn], bfm[2 * NBc];
+#pragma unroll
+        for (int i = 0; i < NBn; ++i)
+          af[i] = bf16x8{tl[i][0], tl[i][1], tl[i][2], tl[i][3], th[i][0], th[i][1], th[i][2], th[i][3]};
+#pragma unroll
+        for (int j = 0; j < NBc; ++j)
+          bfm[j] = bf16x8{tl[NBn + j][0], tl[NBn + j][1], tl[NBn + j][2], tl[NBn + j][3],
+                          th[NBn + j][0], th[NBn + j][1], th[NBn + j][2], th[NBn + j][3]};
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        constexpr int MPD = ILVW ? (NMF / NPW > 0 ? NMF / NPW : 1) : NMF + 1;
+#pragma unroll
+        for (int f = 0; f < NMF; ++f) {
+          acc[0][f / NBc][f % NBc] = mfma16x16x32(af[f / NBc], bfm[f % NBc], acc[0][f / NBc][f % NBc]);
+          if (ILVW && sub == 0 && f % MPD == MPD - 1 && f / MPD < NPW) {
+            __builtin_amdgcn_sched_barrier(0);
+            stage_pieces(cur ^ 1, f / MPD, f / MPD + 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        if (ILVW && sub == 0 && NMF / MPD < NPW) stage_pieces(cur ^ 1, NMF / MPD, NPW);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < NBc; ++j) lgkm_wait_pair<0>(tl[N0 + j], th[N0 + j]);
+#pragma unroll
+        for (int j = 0; j < NBc; ++j)
+          bfm[NBc + j] = bf16x8{tl[N0 + j][0], tl[N0 + j][1], tl[N0 + j][2], tl[N0 + j][3],
+                                th[N0 + j][0], th[N0 + j][1], th[N0 + j][2], th[N0 + j][3]};
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int f = 0; f < NMF; ++f)
+          acc[1][f / NBc][f % NBc] = mfma16x16x32(af[f / NBc], bfm[NBc + f % NBc], acc[1][f / NBc][f % NBc]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (do_bias) {
+#pragma unroll
+          for (int i = 0; i < NBn; ++i) {
+            float sm = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sm += (float)af[i][e];
+            dbs[i] += sm;
+          }
+        }
       }
+      wait_vmcnt0();
+      __syncthreads();
+    }
+    wgrad_store<WN, WC, NWC, TAPS>(a, acc, dbs, do_bias, split, t, n0, c0, wn, wc, lane, zero_split);
+    return;
   }
-  if (do_bias) {
+  if (ks_begin < ks_end) {
+    stage(ks_begin, 0);
+    wait_vmcnt0();
+    __syncthreads();
+  }
+  for (int ks = ks_begin; ks < ks_end; ++ks) {
+    const int cur = (ks - ks_begin) & 1;
+    if (ks + 1 < ks_end) stage(ks + 1, cur ^ 1);
 #pragma unroll
-    for (int i = 0; i < NBn; ++i) {
-      float s = dbs[i];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (lane < 16) a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / 2) + i * 16 + lane] = s;
+    for (int sub = 0; sub < KSUB; ++sub) {
+      const char* base = smem + cur * STAGE + sub * SUB;
+      bf16x4 tl[NF], th[NF];
+#pragma unroll
+      for (int i = 0; i < NBn; ++i) {
+        tl[i] = ds_read_tr16_asm(base + dzo[i] + roff0);
+        th[i] = ds_read_tr16_asm(base + dzo[i] + roff1);
+      }
+#pragma unroll
+      for (int tp = 0; tp < TAPS; ++tp)
+#pragma unroll
+        for (int j = 0; j < NBc; ++j) {
+          tl[NBn + tp * NBc + j] = ds_read_tr16_asm(base + tp * NCC * 4096 + xo[j] + roff0);
+          th[NBn + tp * NBc + j] = ds_read_tr16_asm(base + tp * NCC * 4096 + xo[j] + roff1);
+        }
+      lgkm_fence<NF>(tl, th);
+      bf16x8 af[NBn], bfm[TAPS * NBc];
+#pragma unroll
+      for (int i = 0; i < NBn; ++i)
+        af[i] = bf16x8{tl[i][0], tl[i][1], tl[i][2], tl[i][3], th[i][0], th[i][1], th[i][2], th[i][3]};
+#pragma unroll
+      for (int j = 0; j < TAPS * NBc; ++j)
+        bfm[j] = bf16x8{tl[NBn + j][0], tl[NBn + j][1], tl[NBn + j][2], tl[NBn + j][3],
+                        th[NBn + j][0], th[NBn + j][1], th[NBn + j][2], th[NBn + j][3]};
+#pragma unroll
+      for (int tp = 0; tp < TAPS; ++tp)
+#pragma unroll
+        for (int i = 0; i < NBn; ++i)
+#pragma unroll
+          for (int j = 0; j < NBc; ++j)
+            acc[tp][i][j] = mfma16x16x32(af[i], bfm[tp * NBc + j], acc[tp][i][j]);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < NBn; ++i) {
+          float sm = 0.f;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sm += (float)af[i][e];
+          dbs[i] += sm;
+        }
+      }
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+  wgrad_store<WN, WC, NWC, TAPS>(a, acc, dbs, do_bias, split, t, n0, c0, wn, wc, lane, zero_split);
+}
+
+// LINE && !PAIR: two 8-wave workgroups per CU like the production per-tap kernel (<= 128 VGPRs)
+template <int WN, int WC, int KSUB, int NWC = 4, int TAPS = 1, bool PAIR = false, bool LINE = false, bool ILVW = false>
+__global__ __launch_bounds__(128 * NWC, (LINE && !PAIR) ? 4 : 1) void conv_wgrad_kernel(ConvWgradArgs a) {
+  static_assert(!PAIR || TAPS == 2, "PAIR: two taps per workgroup");
+  // workgroup -> (split, tap group, channel block).  xcd_group (tap-merged rows): the hardware
+  // deals workgroups to the 8 XCDs round robin in launch order, which puts the K kernel-row
+  // workgroups of a split -- all reading the same dZ rows -- on K different L2s, so every dZ
+  // byte comes from the Infinity Cache K times (layer 0: 3 % L2 hits, profiles/r3_small_batch.md).
+  // Grouped, each XCD runs a contiguous range of split-major work and a split's rows share an L2.
+  int bx = blockIdx.x, by = blockIdx.y, bz = blockIdx.z;
+  if (TAPS > 1 && !PAIR && a.xcd_group) {
+    const int gyz = gridDim.y * gridDim.z;
+    const int nwg = gridDim.x * gyz;
+    const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = lin & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int l = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (lin >> 3);
+    bx = l / gyz;
+    const int rem = l - bx * gyz;
+    by = rem / gridDim.z;
+    bz = rem - by * gridDim.z;
+  }
+  const int split = bx;
+  const int ncb = a.Cin / WC;
+  const int n0 = (bz / ncb) * WN;
+  const int c0 = (bz % ncb) * WC;
+  // a.ksteps_per_split is in units of one stage (KSUB*32 pixels)
+  const int nks_total = (a.M + 32 * KSUB - 1) / (32 * KSUB);
+  const int t = by * TAPS;  // first tap of the group
+  if constexpr (PAIR) {
+    if (t + 1 >= a.T) {  // the odd last tap: one tap over the pixels of splits 2 bx and 2 bx + 1
+      const int s0 = 2 * split;
+      if (s0 >= a.nsplit) return;  // workgroup-uniform: no barrier reached yet
+      const int kb = s0 * a.ksteps_per_split;
+      int ke = kb + 2 * a.ksteps_per_split;
+      if (ke > nks_total) ke = nks_total;
+      if constexpr (LINE) wgrad_tile_line<WN, WC, KSUB, NWC, 1>(a, s0, kb, ke, t, 0, n0, c0, s0 + 1 < a.nsplit ? s0 + 1 : -1);
+      else wgrad_tile<WN, WC, KSUB, NWC, 1>(a, s0, kb, ke, t, 0, n0, c0, s0 + 1 < a.nsplit ? s0 + 1 : -1);
+      return;
     }
   }
+  const int ks_begin = split * a.ksteps_per_split;
+  int ks_end = ks_begin + a.ksteps_per_split;
+  if (ks_end > nks_total) ks_end = nks_total;
+  int tstep = a.Cin;  // kernel rows: tap t+1 is one column right
+  if constexpr (PAIR) {
+    const int t1 = t + 1;
+    tstep = ((t1 / a.K - t / a.K) * a.HPi + (t1 % a.K - t % a.K)) * a.Cin;
+  }
+  if constexpr (LINE) wgrad_tile_line<WN, WC, KSUB, NWC, TAPS, ILVW>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
+  else wgrad_tile<WN, WC, KSUB, NWC, TAPS>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
 }
 
 constexpr int kWgradKsub = 1;
@@ -597,6 +904,7 @@ constexpr int kWgradKsub = 1;
 // kernel-lab tile codes and wgrad variants (conv_lab.hip); true when the code was a lab code
 bool launch_conv_fwd_lab(int bm, const ConvFwdArgs& a, int bn, int mode, hipStream_t st);
 bool launch_conv_wgrad_lab(const ConvWgradArgs& a, int wn, int wc, dim3 grid, hipStream_t st);
+bool launch_conv_wgrad_line_lab(const ConvWgradArgs& a, hipStream_t st);  // wgrad variants 6-8
 #endif
 
 }  // namespace agk

@@ -428,4 +428,42 @@ bool launch_conv_wgrad_lab(const ConvWgradArgs& a, int wn, int wc, dim3 grid, hi
   return false;
 }
 
+// tap-pair wgrad (conv_wgrad_kernel PAIR): 192 x 192 x 2 taps per workgroup, 64-pixel stages,
+// one workgroup per CU; grid y = ceil(T / 2), the last y runs the odd tap over split pairs
+
+template <bool ILVW>
+static void launch_wgrad_pair(ConvWgradArgs a, hipStream_t st) {
+  constexpr int KS = 2;
+  constexpr int smem = 2 * (192 + 2 * 192) * 64 * KS;  // 144 KB
+  static const hipError_t attr = hipFuncSetAttribute(
+      (const void*)conv_wgrad_kernel<192, 192, KS, 4, 2, true, true, ILVW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      smem);
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+  const int nks = (a.M + 32 * KS - 1) / (32 * KS);  // the op computed ksteps in 32-pixel units
+  a.ksteps_per_split = (nks + a.nsplit - 1) / a.nsplit;
+  dim3 grid(a.nsplit, (a.T + 1) / 2, 1);
+  hipLaunchKernelGGL((conv_wgrad_kernel<192, 192, KS, 4, 2, true, true, ILVW>), grid, dim3(512), smem, st, a);
+}
+
+// per-tap kernel with line staging (variant 7): the production tile and grid, whole 128-byte
+// pixel lines per DMA piece
+static void launch_wgrad_line(const ConvWgradArgs& a, hipStream_t st) {
+  constexpr int KS = kWgradKsub;
+  constexpr int smem = 2 * (192 + 192) * 64 * KS;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<192, 192, KS, 4, 1, false, true>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+  dim3 grid(a.nsplit, a.T, 1);
+  hipLaunchKernelGGL((conv_wgrad_kernel<192, 192, KS, 4, 1, false, true>), grid, dim3(512), smem, st, a);
+}
+
+// variants 6 (tap pairs), 7 (per tap, line staging), 8 (tap pairs, DMA spread); 192 x 192 3x3 only
+bool launch_conv_wgrad_line_lab(const ConvWgradArgs& a, hipStream_t st) {
+  if (a.variant == 6) launch_wgrad_pair<false>(a, st);
+  else if (a.variant == 8) launch_wgrad_pair<true>(a, st);
+  else if (a.variant == 7) launch_wgrad_line(a, st);
+  else return false;
+  return true;
+}
+
 }  // namespace agk

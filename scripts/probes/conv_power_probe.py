@@ -59,7 +59,7 @@ elif kind == "fwd5":
     fn, flops = (lambda: fwd(x0, wf1, 5, 2)), 2.0 * M * F * 48 * 25
 elif kind == "wgrad":
     # one resident round of the chosen kernel (production: per-tap, 0; lab5 = the row kernel)
-    ns = ops.wgrad_nsplit(M, F, F, 3, variant=code if L is not None else 0)
+    ns = ops.wgrad_nsplit(M, F, F, 3, variant=code)
     slab = torch.empty(ns, 9, F, F, device=dev)
     dbs = torch.zeros(ns, F, device=dev)
     gw = torch.zeros(F, F, 3, 3, device=dev)
@@ -67,7 +67,7 @@ elif kind == "wgrad":
 
     def fn():
         if L is None:
-            ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1)
+            ops.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1, variant=code)  # 0 per-tap, 6 tap pairs, 5 rows
         else:
             L.conv_wgrad(x, y, slab, dbs, 3, S, 1, 1, 0, code)  # lab5: row kernel
         ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)

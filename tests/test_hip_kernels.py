@@ -92,14 +92,16 @@ def test_conv_dgrad_with_relu_mask(ops, cuda_device, B, C, K):
     assert _rel_err(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 5, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 5, 6, 7, 8, 1, 2, 3, 4])
 @pytest.mark.parametrize("B,Cin,Cout,K,Pin,nsplit", [(6, 192, 192, 3, 1, None), (5, 64, 192, 5, 2, None),
                                                     (3, 64, 64, 3, 1, None), (9, 128, 128, 3, 1, None),
                                                     (7, 192, 192, 3, 1, 1), (4, 192, 192, 3, 1, 3),
                                                     (11, 192, 192, 3, 1, 40), (2, 128, 128, 3, 1, 5)])
 def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     """variant 0: production per-tap kernel; 5: the one-kernel-row wgrad (conv_wgrad_row.hip) for
-    192x192 and 128x128 3x3 layers; 1-4: kernel-lab variants."""
+    192x192 and 128x128 3x3 layers; kernel-lab variants: 1-4, 6 tap-pair kernel for 192x192 3x3 (odd
+    tap over split pairs; the slab starts as NaN, so every split's every tap must be written), 7
+    per-tap kernel with whole-line staging, 8 tap pairs with the DMA spread through the MFMAs."""
     torch.manual_seed(2)
     S = 19
     x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
@@ -110,7 +112,7 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     dzp = ops.to_padded(dz, 1)
     M = B * S * S
     ns = nsplit or ops.wgrad_splits(M, K * K)
-    slab = torch.empty(ns, K * K, Cout, Cin, device=cuda_device)
+    slab = torch.full((ns, K * K, Cout, Cin), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, Cout, device=cuda_device)
     if variant == 0:
         ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1)
@@ -145,6 +147,33 @@ def test_conv_wgrad_row_kernel_boards(ops, cuda_device, S, B, Cin, Cin_real, Cou
     ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin_real if Cin_real < Cin else 0, variant=5)
     gw = torch.zeros(Cout, Cin_real, K, K, device=cuda_device)
     gb = torch.zeros(Cout, device=cuda_device)
+    ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert _rel_err(gw, ref_w) < 2e-3
+    assert _rel_err(gb, ref_b) < 2e-3
+
+
+@pytest.mark.parametrize("variant", [6, 7, 8])
+@pytest.mark.parametrize("S,B", [(9, 13), (13, 6), (19, 2176)])
+def test_conv_wgrad_line_lab_boards(ops, cuda_device, S, B, variant):
+    """The kernel-lab line-staged wgrads (6 / 8: tap pairs, 4.5 workgroups per split, one per CU;
+    7: per tap) at other board sizes and at the SL bench batch, with a one-round split count."""
+    torch.manual_seed(8)
+    C = 192
+    x = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    dz = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    ref_w = torch.nn.grad.conv2d_weight(x.float(), (C, C, 3, 3), dz.float(), padding=1)
+    ref_b = dz.float().sum(dim=(0, 2, 3))
+    xp = ops.to_padded(x, 1)
+    dzp = ops.to_padded(dz, 1)
+    L = ops.lab()
+    t_, per_split, per_cu = (int(v) for v in L.wgrad_plan(C, C, 0, 3, variant))
+    ns = max(1, min(256 * per_cu // per_split, (B * S * S + 31) // 32 // ops.WGRAD_MIN_STAGES))
+    slab = torch.full((ns, 9, C, C), float("nan"), device=cuda_device)
+    dbs = torch.zeros(ns, C, device=cuda_device)
+    L.conv_wgrad(xp, dzp, slab, dbs, 3, S, 1, 1, 0, variant)
+    gw = torch.zeros(C, C, 3, 3, device=cuda_device)
+    gb = torch.zeros(C, device=cuda_device)
     ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
     torch.cuda.synchronize()
     assert _rel_err(gw, ref_w) < 2e-3
