@@ -5,15 +5,17 @@
 //
 // The reduction runs over pixels, so both operands must reach the MFMA pixel-contiguous while they
 // are stored channel-contiguous (NHWC).  Each 128-pixel K-step is staged global -> LDS with
-// global_load_lds_dwordx4 as [32-channel block][128 rows][2 x 16 B] (a lane pair loads one pixel's
-// 32 bytes: 32 cache lines per 1-KB piece) and read back with the gfx950 8-bit transpose read
-// ds_read_b64_tr_b8 (per 16-lane group: lane 2q+p supplies row q, bytes 8p..8p+7 of an 8-row x
+// global_load_lds_dwordx4 as whole 160-byte pixel rows ([128 rows][160 B] per operand; a 1-KB piece
+// covers 6.4 consecutive rows, ~8 cache lines -- round 3's first build staged 32-byte row pieces,
+// 32 partial lines per piece, 171 vs 143 us per layer) and read back with the gfx950 8-bit transpose
+// read ds_read_b64_tr_b8 (per 16-lane group: lane 2q+p supplies row q, bytes 8p..8p+7 of an 8-row x
 // 16-byte block; lane i receives column i of the 8 rows -- pinned by
-// tests/test_fp8_inference.py::test_tr8_transpose_read_mapping).  Four reads give a lane the 32
-// K-bytes of its 16x16x128 fragment.  The pixel order inside a step is permuted identically for both
-// operands: K position k = 32 g + 8 j + q (g = lane group, j = read, q = row) lives in LDS row
-// 32 j + 8 g + q, and the two 16-byte halves of a row are swapped on rows with odd g, so the two
-// lane groups of a 32-lane half read disjoint banks.
+// tests/test_fp8_inference.py::test_tr8_transpose_read_mapping), with compile-time offsets from one
+// base register per operand.  Four reads give a lane the 32 K-bytes of its 16x16x128 fragment.  The
+// pixel order inside a step is permuted identically for both operands: K position k = 32 g + 8 j + q
+// (g = lane group, j = read, q = row) lives in LDS row 32 j + 8 g + q, and each row's ten 16-byte
+// chunks are rotated by (row >> 3) & 1, so the two lane groups of a 32-lane half (rows R and R + 8,
+// which share banks at a 160-byte pitch) read disjoint banks.
 //
 // Scales: the MFMA's E8M0 block scales dequantise both operands (127 - e, from the device-resident
 // delayed scales), so the fp32 partials go to the same per-split slab as the bf16 wgrad and the same
@@ -25,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdexcept>
+#include <utility>
 
 #include "common.h"
 #include "conv_common.h"
@@ -37,10 +40,23 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 
-__device__ __forceinline__ u32x2 ds_read_tr8_asm(const char* p) {
+// ds_read_b64_tr_b8 with a compile-time byte offset (the instruction's 16-bit offset field): one base
+// VGPR serves every fragment of a step instead of one address register per (block, read)
+template <int OFF>
+__device__ __forceinline__ u32x2 ds_read_tr8_off(uint32_t base) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
   u32x2 v;
-  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(v) : "v"((unsigned)(uintptr_t)p));
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:%2" : "=v"(v) : "v"(base), "n"(OFF));
   return v;
+}
+
+template <int... I, typename F>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 // e5m2 byte -> float (the byte is the high half of an IEEE half)
@@ -49,17 +65,16 @@ __device__ __forceinline__ float bf8_to_f32(unsigned byte) {
 }
 
 constexpr int kStepPx = 128;               // pixels per K-step (one 16x16x128 MFMA deep)
-constexpr int kBlockBytes = kStepPx * 32;  // one 32-channel block of a step: 4 KB
+constexpr int kImgBytes = kStepPx * 160;  // one operand image of a step: 128 pixel rows x 160 B
 
-// WN x WC tile of one tap per workgroup, 4 waves as 2 (n) x 2 (c)
+// WN x WC tile of one tap per workgroup, 4 waves as 2 (n) x 2 (c); each lane stages the same rows
+// of both operands, so one pixel decomposition serves a dz piece and an x piece.
 template <int WN, int WC>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args a) {
+  static_assert(WN == 160 && WC == 160, "line staging: whole 160-channel pixel rows");
   constexpr int NBn = WN / 32;  // 16-blocks per wave (a wave covers WN/2 x WC/2)
   constexpr int NBc = WC / 32;
-  constexpr int DZB = WN / 32, XB = WC / 32;  // 32-channel blocks per step
-  constexpr int STAGE = (DZB + XB) * kBlockBytes;
-  constexpr int NINSTR = 4 * (DZB + XB);  // 1-KB DMA pieces per step (four 32-row quarters per block)
-  constexpr int IPW = (NINSTR + 3) / 4;
+  constexpr int STAGE = 2 * kImgBytes;  // dz image, then x image
   static_assert(WN % 32 == 0 && WC % 32 == 0, "two waves per dimension, 32-channel blocks");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -80,39 +95,31 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
   if (ks_end > nks_total) ks_end = nks_total;
   const int sa = *a.gscale, sb = *a.xscale;  // E8M0 exponents (dZ, X)
 
-  // DMA piece (block, quarter jq): lane L fills row 32 jq + L/2 of the block, 16-byte unit L & 1,
-  // which holds source half (L & 1) ^ g of the pixel at K position k = 32 g + 8 jq + q,
-  // g = (L/2) / 8, q = (L/2) % 8
-  const int prow = lane >> 1;
-  const int pg = prow >> 3, pq = prow & 7;
-  const int phalf = ((lane & 1) ^ (pg & 1)) * 16;
+  constexpr int NPAIR = kStepPx * WC / 4096;  // 1-KB pieces per operand image per wave
   auto stage = [&](int ks, int buf) {
     char* base = smem + buf * STAGE;
-    int dzo[4], xo[4];
+    int dzo[NPAIR], xo[NPAIR];
 #pragma unroll
-    for (int jq = 0; jq < 4; ++jq) {
-      const int px = ks * kStepPx + 32 * pg + 8 * jq + pq;
+    for (int i = 0; i < NPAIR; ++i) {
+      const int P = wave * NPAIR + i;  // piece of the operand image
+      const int idx = P * 64 + lane;   // 16-byte unit of the image
+      const int R = idx / 10, pos = idx - R * 10;
+      int c = pos - ((R >> 3) & 1);
+      c = c < 0 ? c + 10 : c;  // source chunk (16 channels) of this LDS unit
+      const int k = 32 * ((R >> 3) & 3) + 8 * (R >> 5) + (R & 7);
+      const int px = ks * kStepPx + k;
       const int pm = px < a.M ? px : a.M - 1;
       const int b = fdiv(pm, a.divSS);
       const int rem = pm - b * SS;
       const int ii = fdiv(rem, a.divS);
       const int jx = rem - ii * a.S;
-      dzo[jq] = px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po) * a.Cout + n0 + phalf : phalf;  // pixel 0: zero border
-      xo[jq] = ((b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi) * a.Cin + toff + phalf;
-    }
-    // dz pieces, then x pieces, in wave-uniform loops (a per-piece select between the two source
-    // tensors makes hipcc drain vmcnt before the LDS reads that follow)
-#pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const int j = wave * IPW + i;
-      if (j < 4 * DZB) glds16(a.dz8 + dzo[j & 3] + (j >> 2) * 32, base + (j >> 2) * kBlockBytes + (j & 3) * 1024);
+      dzo[i] = (px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po) * a.Cout : 0) + c * 16;  // pixel 0: zero border
+      xo[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi) * a.Cin + toff + c * 16;
     }
 #pragma unroll
-    for (int i = 0; i < IPW; ++i) {
-      const int j = wave * IPW + i - 4 * DZB;
-      if (j >= 0 && j < 4 * XB)
-        glds16(a.x8 + xo[j & 3] + (j >> 2) * 32, base + (DZB + (j >> 2)) * kBlockBytes + (j & 3) * 1024);
-    }
+    for (int i = 0; i < NPAIR; ++i) glds16(a.dz8 + dzo[i], base + (wave * NPAIR + i) * 1024);
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) glds16(a.x8 + xo[i], base + kImgBytes + (wave * NPAIR + i) * 1024);
   };
 
   f32x4 acc[NBn][NBc];
@@ -126,13 +133,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
   float vmax = 0.f;  // tap-0 workgroups: max |e5m2 dZ| (scaled)
   const bool do_bias = (t == 0) && (c0 == 0) && (wc == 0);
 
-  // transposed-read address of read j (K rows 8 j .. 8 j + 7 of the lane group's 32) for 16-channel
-  // block nb (32-channel block nb / 2, half nb % 2, swapped on odd g)
+  // transposed reads: lane (g = lane >> 4, li = lane & 15) reads row 32 j + lrow, byte 8 (li & 1) of
+  // the rotated 16-byte chunk of its block
   const int g = lane >> 4, li = lane & 15;
-  const int troff = (8 * g + (li >> 1)) * 32 + 8 * (li & 1);
-  auto tr_addr = [&](const char* base, int nb, int j) {
-    return base + (nb >> 1) * kBlockBytes + 1024 * j + troff + (((nb & 1) ^ (g & 1)) << 4);
-  };
+  const int lrow = 8 * g + (li >> 1);
 
   if (ks_begin < ks_end) {
     stage(ks_begin, 0);
@@ -143,32 +147,51 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
     const int cur = (ks - ks_begin) & 1;
     if (ks + 1 < ks_end) stage(ks + 1, cur ^ 1);
     const char* base = smem + cur * STAGE;
-    u32x2 ra[NBn][4], rb[NBc][4];
+    i32x8 af[NBn];
+    {
+      // lane base (row lrow, the rotated chunk of block 0 of the wave's range) + immediate offsets;
+      // the range's last block (index 4 of 5) wraps to chunk 0 on rotated rows of the upper wave.
+      // All A fragments are read first; the B fragments of block C + 1 are read under block C's
+      // MFMAs (a 2-deep ring of 8 registers instead of all 40: the step otherwise spills).
+      const uint32_t b0 = (uint32_t)(uintptr_t)AG_LDS(base) + lrow * 160 + 8 * (li & 1) + (g & 1) * 16;
+      const uint32_t bn = b0 + wn * NBn * 16, bc = b0 + kImgBytes + wc * NBc * 16;
+      const uint32_t bn4 = bn - ((wn == 1 && (g & 1)) ? 160 : 0), bc4 = bc - ((wc == 1 && (g & 1)) ? 160 : 0);
+      u32x2 ra[NBn][4], rb[2][4];
+      static_for<4>([&](auto J) {
+        static_for<NBn>([&](auto I) { ra[I][J] = ds_read_tr8_off<J * 32 * 160 + I * 16>(I == NBn - 1 ? bn4 : bn); });
+      });
+      static_for<4>([&](auto J) { rb[0][J] = ds_read_tr8_off<J * 32 * 160>(bc); });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+      for (int i = 0; i < NBn; ++i)
+        af[i] = i32x8{(int)ra[i][0].x, (int)ra[i][0].y, (int)ra[i][1].x, (int)ra[i][1].y,
+                      (int)ra[i][2].x, (int)ra[i][2].y, (int)ra[i][3].x, (int)ra[i][3].y};
+      static_for<NBc>([&](auto C) {
+        constexpr int cb = C & 1, nb = (C + 1) & 1;
+        if constexpr (C + 1 < NBc)
+          static_for<4>([&](auto J) {
+            rb[nb][J] = ds_read_tr8_off<J * 32 * 160 + (C + 1) * 16>(C + 1 == NBc - 1 ? bc4 : bc);
+          });
+        const i32x8 bm = i32x8{(int)rb[cb][0].x, (int)rb[cb][0].y, (int)rb[cb][1].x, (int)rb[cb][1].y,
+                               (int)rb[cb][2].x, (int)rb[cb][2].y, (int)rb[cb][3].x, (int)rb[cb][3].y};
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < NBn; ++i) ra[i][j] = ds_read_tr8_asm(tr_addr(base, wn * NBn + i, j));
-#pragma unroll
-      for (int c = 0; c < NBc; ++c) rb[c][j] = ds_read_tr8_asm(tr_addr(base + DZB * kBlockBytes, wc * NBc + c, j));
+        for (int i = 0; i < NBn; ++i)
+          acc[i][C] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bm, acc[i][C], 1, 0, 0, sa, 0, sb);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (C + 1 < NBc)
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rb[nb][0]), "+v"(rb[nb][1]), "+v"(rb[nb][2]), "+v"(rb[nb][3]));
+      });
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    i32x8 af[NBn], bfm[NBc];
-#pragma unroll
-    for (int i = 0; i < NBn; ++i)
-      af[i] = i32x8{(int)ra[i][0].x, (int)ra[i][0].y, (int)ra[i][1].x, (int)ra[i][1].y,
-                    (int)ra[i][2].x, (int)ra[i][2].y, (int)ra[i][3].x, (int)ra[i][3].y};
-#pragma unroll
-    for (int c = 0; c < NBc; ++c)
-      bfm[c] = i32x8{(int)rb[c][0].x, (int)rb[c][0].y, (int)rb[c][1].x, (int)rb[c][1].y,
-                     (int)rb[c][2].x, (int)rb[c][2].y, (int)rb[c][3].x, (int)rb[c][3].y};
-    __builtin_amdgcn_s_setprio(1);
+    // pin the step's MFMAs above the barrier: without a use here, hipcc sinks them (pure builtins)
+    // past the barrier into the next iteration, keeping every fragment live across it (spills)
 #pragma unroll
     for (int i = 0; i < NBn; ++i)
 #pragma unroll
-      for (int c = 0; c < NBc; ++c)
-        acc[i][c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfm[c], acc[i][c], 1, 0, 0, sa, 0, sb);
-    __builtin_amdgcn_s_setprio(0);
+      for (int c = 0; c < NBc; ++c) asm volatile("" : "+v"(acc[i][c]));
     if (do_bias) {
 #pragma unroll
       for (int i = 0; i < NBn; ++i) {
@@ -230,7 +253,7 @@ void launch_conv_wgrad_fp8(const ConvWgradFp8Args& a_in, hipStream_t st) {
   if (!wgrad_fp8_supported(a.Cout, a.Cin, a.K))
     throw std::invalid_argument("conv_wgrad_fp8: 160 -> 160 3x3 layers only");
   constexpr int WN = 160, WC = 160;
-  constexpr int smem = 2 * (WN / 32 + WC / 32) * kBlockBytes;
+  constexpr int smem = 2 * 2 * kImgBytes;  // two stages of two images
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_fp8_kernel<WN, WC>,
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, smem);
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");

@@ -269,9 +269,11 @@ class HipConvTrainer:
             # fp8 wgrad (160 -> 160 3x3 layers, conv_wgrad_fp8.hip): e4m3 inputs kept per layer (the
             # forward's e4m3 outputs instead of a two-buffer ring), e5m2 output gradients written by
             # the bitmask dgrad's epilogue (the head's by one quantise pass), delayed gradient scales
-            # as the fp8 dgrad's.  Layer 0 (49 planes) keeps the bf16 wgrad.
+            # as the fp8 dgrad's.  Layer 0 (49 planes) keeps the bf16 wgrad.  On by default where it
+            # applies (value net: 143 vs 201 us per layer at B = 1024, profiles/r3_fp8_wgrad.md);
+            # ALPHAGO_AMD_FP8_WGRAD=0 keeps the bf16 wgrad.
             if fp8_wgrad is None:
-                fp8_wgrad = os.environ.get("ALPHAGO_AMD_FP8_WGRAD", "0") == "1"
+                fp8_wgrad = os.environ.get("ALPHAGO_AMD_FP8_WGRAD", "1") == "1"
             self.fp8_wgrad = bool(fp8_wgrad) and all(
                 ops.wgrad_fp8_supported(self.Fp, self.Fp, self.K[l]) for l in range(1, L))
             self._w8layers = set(range(1, L)) if self.fp8_wgrad else set()
