@@ -230,9 +230,15 @@ __device__ __forceinline__ int cvt4_bf16_bf8(unsigned lo2, unsigned hi2, float s
   return __builtin_bit_cast(int, r);
 }
 
-template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8, bool DG = false, bool DGB = false>
+// DGBITS (with DG): the e5m2 gradient operand is the copy the previous dgrad wrote for the fp8 wgrad,
+// ReLU' comes from the forward's bitmask (as DGB), outputs e5m2 (for the fp8 wgrad and the next
+// fp8 dgrad) and bf16 only where a bf16 consumer exists (the first layer's wgrad)
+template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8, bool DG = false, bool DGB = false,
+          bool DGBITS = false>
 __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) {
   static_assert(!(DG && DGB), "one dgrad form");
+  static_assert(!DGBITS || DG, "DGBITS: the e5m2-operand dgrad");
+  constexpr bool MASKBITS = DGB || DGBITS;  // ReLU' from the forward epilogue's bitmask
   // MB: 16-pixel blocks per wave; the BN/16 channel blocks are read from LDS in NPART parts
   constexpr int NB = BN / 16;   // 16-channel blocks per wave
   constexpr int NH = NB / NPART;
@@ -418,7 +424,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     const int jj = rem - ii * a.S;
     const size_t ooff = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout;
     uint32_t mw[2] = {0u, 0u};
-    if constexpr (DGB) {  // ReLU' bits of the lane's channels (the forward epilogue's layout)
+    if constexpr (MASKBITS) {  // ReLU' bits of the lane's channels (the forward epilogue's layout)
       const size_t pw = (size_t)(ooff / a.Cout) * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
       mw[0] = a.mbits_in[pw];
       mw[1] = a.mbits_in[pw + 4];
@@ -427,7 +433,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     for (int i = 0; i < NB; ++i) {
       const int n = nbase + i * 16;
       f32x4 v = acc[i][j];
-      if constexpr (DGB) {
+      if constexpr (MASKBITS) {
         const uint32_t w = mw[i / (NB / 2)];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = ((w >> (4 * (i % (NB / 2)) + r)) & 1u) ? v[r] : 0.f;
@@ -502,17 +508,24 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 // weights in 4 parts); kernel-lab build only: 1 / 3 / 4 = other L2-operand
 // tilings, 5 = LDS-staged conv_fwd_fp8_kernel
 
-template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false, bool DGB = false>
+template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false, bool DGB = false, bool DGBITS = false>
 static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
   constexpr int WROWS = (BN * 8) % 512 == 0 ? BN : ((BN * 8 + 511) / 512 * 512) / 8;  // as in the kernel
   constexpr int smem = 2 * WROWS * 128 + 64;
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB>, hipFuncAttributeMaxDynamicSharedMemorySize,
-      smem);  // once per instantiation (thread-safe static)
+      (const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS>,
+      hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   constexpr int BM = 128 * MB;
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB>), grid, dim3(512), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS>), grid, dim3(512), smem, st, a);
+}
+
+// fp8 dgrad of the fp8-wgrad value step: e5m2 operand (the previous dgrad's copy), bitmask ReLU',
+// e5m2 and/or bf16 outputs; the 160-wide value tile only
+template <bool OB, bool OF>
+static void launch_fp8_dgrad_bits_t(const ConvFp8Args& a, hipStream_t st) {
+  launch_fp8_ga<160, 3, 5, OB, OF, true, false, true>(a, st);
 }
 
 // fp8 dgrad from the bf16 gradient (in-register e5m2 conversion, bitmask ReLU', bf16 output)
@@ -603,6 +616,13 @@ void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
     else if (a.Cout % 192 == 0) launch_fp8_dgrad_bf16<192>(a, st);
     else if (a.Cout % 128 == 0) launch_fp8_dgrad_bf16<128>(a, st);
     else launch_fp8_dgrad_bf16<64>(a, st);
+    return;
+  }
+  if (a.dgrad && a.mbits_in) {
+    if (a.Cout != 160) throw std::invalid_argument("conv_dgrad_fp8_bits: 160-wide value layers only");
+    if (a.y_bf16 && a.y_fp8) launch_fp8_dgrad_bits_t<true, true>(a, st);
+    else if (a.y_bf16) launch_fp8_dgrad_bits_t<true, false>(a, st);
+    else launch_fp8_dgrad_bits_t<false, true>(a, st);
     return;
   }
   if (a.dgrad) {

@@ -316,6 +316,12 @@ void conv_dgrad_fp8(const Tensor& dz8, const Tensor& w, const Tensor& mask, cons
   conv_fwd_fp8_impl(dz8, w, out_scale, scales, out_scale, amax, y_bf16, y_fp8, K, S, 1, 1, 0, mask);
 }
 
+void conv_dgrad_fp8_bits(const Tensor& dz8, const Tensor& w8t, const Tensor& mbits, const Tensor& scales,
+                         const Tensor& out_scale, const c10::optional<Tensor>& amax, const c10::optional<Tensor>& y_bf16,
+                         const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S) {
+  conv_dgrad_fp8_bits_impl(dz8, w8t, mbits, scales, out_scale, amax, y_bf16, y_fp8, K, S);
+}
+
 void conv_dgrad_fp8_bf16(const Tensor& dz, const Tensor& w8t, const Tensor& mbits, const Tensor& scales,
                          const Tensor& in_scale, const c10::optional<Tensor>& amax, const Tensor& dx, int64_t K,
                          int64_t S) {
@@ -629,6 +635,8 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("absmax_bf16(Tensor x, Tensor(a!) amax, Tensor scale_any) -> ()");
   m.def("conv_dgrad_fp8_bf16(Tensor dz, Tensor w8t, Tensor mbits, Tensor scales, Tensor in_scale, Tensor(a!)? amax, "
         "Tensor(b!) dx, int K, int S) -> ()");
+  m.def("conv_dgrad_fp8_bits(Tensor dz8, Tensor w8t, Tensor mbits, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
+        "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S) -> ()");
   m.def("conv_dgrad_fp8(Tensor dz8, Tensor w, Tensor mask, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
         "Tensor(b!) y_bf16, Tensor(c!)? y_fp8, int K, int S) -> ()");
   m.def("fp8_grad_scales(Tensor(a!) amax, Tensor(b!) gscales8, Tensor(c!) gosc, int margin) -> ()");
@@ -676,6 +684,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("pack_weights_fp8", &pack_weights_fp8);
   m.impl("conv_dgrad_fp8", &conv_dgrad_fp8);
   m.impl("conv_dgrad_fp8_bf16", &conv_dgrad_fp8_bf16);
+  m.impl("conv_dgrad_fp8_bits", &conv_dgrad_fp8_bits);
   m.impl("pack_weights_fp8_multi", &pack_weights_fp8_multi);
   m.impl("absmax_bf16", &absmax_bf16);
   m.impl("fp8_grad_scales", &fp8_grad_scales);

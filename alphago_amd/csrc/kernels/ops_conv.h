@@ -283,6 +283,52 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
   launch_check("conv_fwd_fp8");
 }
 
+// fp8 dgrad of the fp8-wgrad value step: dz8 e5m2 (B, HP, HP, 160) (MFMA scale scales[0]), w8t the
+// transposed flipped e4m3 weights (scales[1]), ReLU' from the forward's bitmask; outputs y_fp8 (e5m2 of
+// dx * out_scale[0]) and/or y_bf16; amax (optional) accumulates max |dx|
+inline void conv_dgrad_fp8_bits_impl(const Tensor& dz8, const Tensor& w8t, const Tensor& mbits, const Tensor& scales,
+                                     const Tensor& out_scale, const c10::optional<Tensor>& amax,
+                                     const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8,
+                                     int64_t K, int64_t S) {
+  check_dev("conv_dgrad_fp8_bits", dz8, w8t, mbits, scales, out_scale, amax, y_bf16, y_fp8);
+  CHECK_DEV(dz8); CHECK_DEV(w8t); CHECK_DEV(mbits); CHECK_CONTIG(dz8); CHECK_CONTIG(w8t); CHECK_CONTIG(mbits);
+  TORCH_CHECK(dz8.scalar_type() == at::kByte && w8t.scalar_type() == at::kByte, "fp8 tensors are stored as uint8");
+  TORCH_CHECK(dz8.dim() == 4 && w8t.dim() == 3 && w8t.size(2) == 64 && dz8.size(3) == 160 && w8t.size(1) == 160,
+              "dz8 (B, HP, HP, 160), w8t (nch, 160, 64)");
+  TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2 && out_scale.scalar_type() == at::kFloat &&
+                  out_scale.numel() >= 1, "scales int32[2], out_scale f32[1]");
+  TORCH_CHECK(mbits.scalar_type() == at::kInt, "mbits int32");
+  TORCH_CHECK(y_bf16.has_value() || y_fp8.has_value(), "need an output");
+  const int64_t B = dz8.size(0), HP = dz8.size(1), nch = w8t.size(0);
+  TORCH_CHECK(HP == S + 2 && dz8.size(2) == HP && nch % 2 == 0 && nch >= K * K * 3, "geometry (pad 1, 160 channels)");
+  TORCH_CHECK(mbits.numel() >= B * HP * HP * 8, "mbits too small: need B*HP*HP*8 words");
+  agk::ConvFp8Args a{};
+  a.x = dz8.data_ptr<uint8_t>(); a.w = w8t.data_ptr<uint8_t>();
+  a.scales = scales.data_ptr<int>(); a.out_scale = out_scale.data_ptr<float>();
+  if (y_bf16.has_value()) {
+    CHECK_BF16(*y_bf16); CHECK_CONTIG(*y_bf16);
+    TORCH_CHECK(y_bf16->sizes() == dz8.sizes(), "y_bf16 shape");
+    a.y_bf16 = bfp_mut(*y_bf16);
+  }
+  if (y_fp8.has_value()) {
+    TORCH_CHECK(y_fp8->scalar_type() == at::kByte && y_fp8->is_contiguous() && y_fp8->sizes() == dz8.sizes(),
+                "y_fp8 uint8, shape of dz8");
+    a.y_fp8 = y_fp8->data_ptr<uint8_t>();
+  }
+  if (amax.has_value()) {
+    TORCH_CHECK(amax->scalar_type() == at::kInt && amax->numel() >= agk::kFp8AmaxSlots, "amax int32[64]");
+    a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
+  }
+  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = 160; a.Cout = 160; a.K = (int)K;
+  a.HPi = (int)HP; a.offi = (int)(1 - K / 2); a.HPo = (int)HP; a.Po = 1; a.nch = (int)nch;
+  a.dgrad = 1;
+  a.mbits_in = reinterpret_cast<const uint32_t*>(mbits.data_ptr<int>());
+  TORCH_CHECK(B * HP * HP * 160 < (1ll << 31), "tensor too large for int32 offsets");
+  if (a.M == 0) return;
+  agk::launch_conv_fwd_fp8(a, cur_stream());
+  launch_check("conv_dgrad_fp8_bits");
+}
+
 // fp8 dgrad from the bf16 gradient: dz (B, HP, HP, Cg) bf16 padded NHWC is converted to e5m2 in
 // the kernel's registers (multiplier *in_scale, MFMA scale scales[0]); w8t: transposed flipped e4m3
 // weights (scales[1]); ReLU' from the forward's bitmask; dx bf16; amax accumulates max |dx|

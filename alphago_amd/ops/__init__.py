@@ -375,6 +375,14 @@ def conv_dgrad_fp8(dz8, w8t, mask, scales, out_scale, K: int, S: int, y_bf16, y_
     _ops().conv_dgrad_fp8(dz8, w8t, mask, scales, out_scale, amax, y_bf16, y_fp8, K, S)
 
 
+def conv_dgrad_fp8_bits(dz8, w8t, mbits, scales, out_scale, K: int, S: int, y_bf16=None, y_fp8=None, amax=None):
+    """fp8 dgrad of the fp8-wgrad value step (160 channels): dz8 e5m2 (the copy the previous dgrad
+    wrote for the fp8 wgrad; MFMA scale scales[0]) x the transposed flipped e4m3 weights (scales[1]),
+    ReLU' from the forward's bitmask ``mbits``; writes y_fp8 = e5m2(dx * out_scale[0]) and/or bf16
+    y_bf16; ``amax`` accumulates max |dx|."""
+    _ops().conv_dgrad_fp8_bits(dz8, w8t, mbits, scales, out_scale, amax, y_bf16, y_fp8, K, S)
+
+
 def conv_dgrad_fp8_bf16(dz, w8t, mbits, scales, in_scale, K: int, S: int, dx, amax=None):
     """fp8 dgrad straight from the bf16 gradient: dz (padded NHWC bf16) is converted to e5m2 in
     registers as the kernel loads it (multiplier in_scale[0], MFMA E8M0 scale scales[0]), times the

@@ -122,7 +122,7 @@ class HipConvTrainer:
 
     def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
                  overlap: bool = False, wgrad_target_wgs: int = 0, iterations: int = 0, precision: str = "bf16",
-                 wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: bool = False,
+                 wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: Optional[bool] = None,
                  reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None,
                  fp8_wgrad: Optional[bool] = None):
         ops.load()
@@ -259,7 +259,7 @@ class HipConvTrainer:
             # dgrads and calibrates them).  Round 3: the kernel reads the bf16 dZ and converts it to
             # e5m2 in registers (no quantisation pass, no e5m2 tensor), takes ReLU' from the
             # forward's bitmask, and the transposed packs ride the one batched repack launch.
-            self.fp8_dgrad = fp8_dgrad
+            self.fp8_dgrad = bool(fp8_dgrad)  # resolved below once fp8_wgrad is known
             self.wd8 = [None] + [torch.zeros((ops.fp8_nchunks(self.K[l], self.Fp), self.Fp, 64), dtype=torch.uint8,
                                              device=dev) for l in range(1, L)]
             self.gscales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
@@ -277,6 +277,13 @@ class HipConvTrainer:
             self.fp8_wgrad = bool(fp8_wgrad) and all(
                 ops.wgrad_fp8_supported(self.Fp, self.Fp, self.K[l]) for l in range(1, L))
             self._w8layers = set(range(1, L)) if self.fp8_wgrad else set()
+            # With the fp8 wgrad the dgrad reads the same e5m2 dZ copy and writes e5m2 for the layer
+            # below (conv_dgrad_fp8_bits): the all-fp8 backward is the default there (value 12 x 152,
+            # B = 1024: 156.3k -> 179.9k positions/s, profiles/r3_fp8_wgrad.md);
+            # ALPHAGO_AMD_FP8_DGRAD=0 keeps the bf16 dgrad.  Elsewhere fp8 dgrad stays opt-in.
+            if fp8_dgrad is None:
+                fp8_dgrad = self.fp8_wgrad and os.environ.get("ALPHAGO_AMD_FP8_DGRAD", "1") == "1"
+            self.fp8_dgrad = bool(fp8_dgrad)
             if self.fp8_wgrad:
                 self.X8 = [None] + [torch.zeros(self.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(1, L)]
                 self.DZ8 = [None] + [torch.zeros(self.DZ[0].shape, dtype=torch.uint8, device=dev) for _ in range(1, L)]
@@ -452,7 +459,17 @@ class HipConvTrainer:
             else:
                 self._wgrad_layer(l, red)
             if l > 0:
-                if w8 and l - 1 in self._w8layers:  # bitmask dgrad + the e5m2 copy wgrad(l-1) reads
+                if w8 and self.fp8_dgrad:
+                    # all-fp8 backward: the e5m2 dZ copy wgrad(l) read is also this dgrad's operand;
+                    # the output goes out as e5m2 (wgrad(l-1) and dgrad(l-1) read it) and as bf16 only
+                    # for the first layer's bf16 wgrad; its max |dx| comes from wgrad(l-1)'s bytes
+                    f8out = l - 1 in self._w8layers
+                    ops.conv_dgrad_fp8_bits(self.DZ8[l], self.wd8[l], self.MBITS[l - 1], self.gscales8[l],
+                                            self.gosc8[l - 1:l], self.K[l], self.S,
+                                            y_bf16=None if f8out else self.DZ[l - 1],
+                                            y_fp8=self.DZ8[l - 1] if f8out else None,
+                                            amax=None if f8out else self.gamax8[l - 1])
+                elif w8 and l - 1 in self._w8layers:  # bitmask dgrad + the e5m2 copy wgrad(l-1) reads
                     ops.conv_dgrad_bits_bf8(self.DZ[l], self.wd[l], self.DZ[l - 1], self.MBITS[l - 1],
                                             self.DZ8[l - 1], self.gosc8[l - 1:l], self.K[l], self.S,
                                             tile=self.conv_tile)

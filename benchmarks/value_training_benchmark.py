@@ -37,7 +37,8 @@ def main():
     ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 64, 128, 256, 384, 385, 386, 387],
                     help="forward/dgrad conv tiling (0 = automatic)")
     ap.add_argument("--overlap", action="store_true", help="wgrad on a second stream beside the dgrad")
-    ap.add_argument("--fp8-dgrad", action="store_true", help="fp8 precision: e5m2 x e4m3 dgrad too")
+    ap.add_argument("--fp8-dgrad", action="store_true", help="(default with the fp8 wgrad) fp8 precision: e5m2 x e4m3 dgrad")
+    ap.add_argument("--no-fp8-dgrad", action="store_true", help="fp8 precision: keep the bf16 dgrad")
     ap.add_argument("--fp8-wgrad", action="store_true", help="(default) fp8 precision: e5m2 x e4m3 wgrad (160-wide layers)")
     ap.add_argument("--no-fp8-wgrad", action="store_true", help="fp8 precision: keep the bf16 wgrad")
     a = ap.parse_args()
@@ -46,7 +47,8 @@ def main():
     torch.manual_seed(7 + env.rank)
     net = ValueNet(49, filters_per_layer=a.filters, layers=a.layers)
     kw = ({"precision": a.precision, "conv_tile": a.conv_tile, "overlap": a.overlap,
-           "fp8_dgrad": a.fp8_dgrad, "fp8_wgrad": not a.no_fp8_wgrad} if dev.type == "cuda" else {})
+           "fp8_dgrad": False if a.no_fp8_dgrad else (True if a.fp8_dgrad else None),
+           "fp8_wgrad": not a.no_fp8_wgrad} if dev.type == "cuda" else {})
     tr = make_value_trainer(net, a.batch, lr=0.003, decay=8.664e-8, device=dev, **kw)
     g = torch.Generator(device=dev).manual_seed(11 + env.rank)
     pool = torch.randint(0, 2, (a.pool, 49, 19, 19), dtype=torch.uint8, device=dev, generator=g)

@@ -19,7 +19,8 @@ z = (torch.randint(0, 2, (B,), generator=g) * 2 - 1).float().to(dev)
 t16 = HipValueTrainer(copy.deepcopy(net), B, lr=0.0, device=dev)
 for _ in range(2):
     t16.compute_grads(planes, z)
-for name, kw in (("fp8_fwd", {}), ("fp8_fwd+dgrad", {"fp8_dgrad": True}), ("fp8_fwd+wgrad", {"fp8_wgrad": True})):
+for name, kw in (("fp8_fwd", {"fp8_wgrad": False}), ("fp8_fwd+dgrad", {"fp8_dgrad": True, "fp8_wgrad": False}),
+                 ("fp8_fwd+wgrad", {"fp8_wgrad": True}), ("fp8_fwd+dgrad+wgrad", {"fp8_dgrad": True, "fp8_wgrad": True})):
     t8 = HipValueTrainer(copy.deepcopy(net), B, lr=0.0, device=dev, precision="fp8", **kw)
     for _ in range(2):
         t8.compute_grads(planes, z)

@@ -237,6 +237,55 @@ def test_conv_dgrad_fp8_bf16_operand(ops, cuda_device, C, Cp, B):
     assert abs(amax.view(torch.float32).max().item() - ref.abs().max().item()) <= 1e-2 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("B,outs", [(3, "fp8"), (5, "bf16"), (2, "both")])
+def test_conv_dgrad_fp8_bits(ops, cuda_device, B, outs):
+    """All-fp8 value backward: dgrad from the e5m2 dZ copy (the one the fp8 wgrad reads), ReLU' from
+    the forward's bitmask, e5m2 and/or bf16 outputs vs fp32 conv2d_input of the dequantised operands."""
+    torch.manual_seed(16)
+    S, K, C, Cp = 19, 3, 152, 160
+    xin = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w0 = _bf(torch.randn(C, C, K, K, device=cuda_device) * 0.05)
+    wp0 = ops.packed_weight_like(w0, Cp, Cp)
+    ops.pack_weights([w0.contiguous()], [wp0])
+    yprev = ops.padded_empty(B, S, 1, Cp, cuda_device)
+    mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=cuda_device)
+    ops.conv_fwd(ops.to_padded(xin, 1, Cp), wp0, torch.randn(Cp, device=cuda_device) * 0.1, yprev, K, S, 1, 1,
+                 mbits=mbits)
+    dz = torch.randn(B, C, S, S, device=cuda_device) * 1e-3
+    w = torch.randn(C, C, K, K, device=cuda_device) * 0.05
+    eg = ops.fp8_exponent(float(dz.abs().max()), margin=0) + 7
+    ew = ops.fp8_exponent(float(w.abs().max()), margin=0)
+    w8t = torch.zeros((ops.fp8_nchunks(K, Cp), Cp, 64), dtype=torch.uint8, device=cuda_device)
+    ops.pack_weights_fp8_multi([w], [w8t], torch.tensor([2.0 ** ew], device=cuda_device), [0], [1])
+    dz8 = torch.zeros((B, S + 2, S + 2, Cp), dtype=torch.uint8, device=cuda_device)
+    dz8[:, 1:S + 1, 1:S + 1, :C] = (dz * 2.0 ** eg).clamp(-57344, 57344).to(torch.float8_e5m2).view(
+        torch.uint8).permute(0, 2, 3, 1)
+    dzq = (dz * 2.0 ** eg).clamp(-57344, 57344).to(torch.float8_e5m2).float() * 2.0 ** -eg
+    wq = (w * 2.0 ** ew).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** -ew
+    ymask = ops.from_padded(yprev, 1)[:, :C] > 0
+    ref = torch.nn.grad.conv2d_input((B, C, S, S), wq, dzq, padding=K // 2) * ymask
+    scales = torch.tensor([127 - eg, 127 - ew], dtype=torch.int32, device=cuda_device)
+    eo = ops.fp8_exponent(float(ref.abs().max()), margin=0) + 7
+    amax = ops.fp8_amax_buffer(1, cuda_device)[0]
+    dx = ops.padded_empty(B, S, 1, Cp, cuda_device) if outs in ("bf16", "both") else None
+    dx8 = torch.zeros_like(dz8) if outs in ("fp8", "both") else None
+    ops.conv_dgrad_fp8_bits(dz8, w8t, mbits, scales, torch.tensor([2.0 ** eo], device=cuda_device), K, S,
+                            y_bf16=dx, y_fp8=dx8, amax=amax)
+    torch.cuda.synchronize()
+    if dx is not None:
+        out = ops.from_padded(dx, 1)
+        assert _rel_err(out[:, :C], ref) < 1e-2
+        assert out[:, C:].abs().sum() == 0
+        assert dx[:, 0].abs().sum() == 0  # borders untouched
+    if dx8 is not None:
+        got = dx8[:, 1:S + 1, 1:S + 1, :C].view(torch.float8_e5m2).float().permute(0, 3, 1, 2) * 2.0 ** -eo
+        # e5m2 keeps 2 mantissa bits: at most half a step (12.5 % of the value) from the fp32 result
+        assert _rel_err(got, ref) < 0.13
+        assert (got - ref).abs().mean().item() < 0.1 * ref.abs().mean().item()
+        assert dx8[:, 0].sum() == 0 and dx8[:, 1:S + 1, 1:S + 1, C:].sum() == 0
+    assert abs(amax.view(torch.float32).max().item() - ref.abs().max().item()) <= 1e-2 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("Cin,Cout,K", [(152, 152, 3), (49, 152, 5), (192, 192, 3), (48, 192, 5)])
 def test_pack_weights_fp8_multi_matches_single(ops, cuda_device, Cin, Cout, K):
     """The one-launch fp8 repack equals the per-layer packs, forward and transposed."""

@@ -54,7 +54,7 @@ def test_fp8_value_engine_matches_bf16(cuda_device, F):
 
 
 @pytest.mark.parametrize("F,fp8_dgrad,fp8_wgrad", [(192, False, False), (152, False, False), (152, True, False),
-                                                 (152, False, True)])
+                                                 (152, False, True), (152, True, True)])
 def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad, fp8_wgrad):
     """Value-net training with the fp8 forward: gradients close to the bf16
     trainer's, loss goes down, activation scales are updated on the device
