@@ -464,6 +464,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 #pragma unroll
           for (int r = 0; r < 4; ++r) mb[i / (NB / 2)] |= ((float)o[r] > 0.f ? 1u : 0u) << (4 * (i % (NB / 2)) + r);
         }
+      } else if constexpr (!DG && !DGB && NB % 2 == 0) {
+        // e4m3-only forward (the all-fp8 value step: no bf16 consumer below the last layer): the
+        // ReLU' bits from the fp32 result (bf16 rounding keeps the sign and fp32's exponent range)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mb[i / (NB / 2)] |= (v[r] > 0.f ? 1u : 0u) << (4 * (i % (NB / 2)) + r);
       }
       if constexpr (OUT_FP8) {
         if constexpr (DG) {
@@ -482,7 +487,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
         }
       }
     }
-    if constexpr (!DG && !DGB && OUT_BF16 && NB % 2 == 0) {
+    if constexpr (!DG && !DGB && NB % 2 == 0) {
       if (a.mbits_out && ok) {
         const size_t pw = (size_t)(ooff / a.Cout) * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
         a.mbits_out[pw] = mb[0];
@@ -785,35 +790,47 @@ void launch_fp8_grad_scales(unsigned* amax, int* gscales8, float* gosc, int L, i
 }
 
 // e5m2 quantisation with a device-resident scale, tracking max |x| (the head's dZ, the first
-// input of the fp8 dgrad chain)
-__global__ __launch_bounds__(256) void quantize_bf8_dev_kernel(const __bf16* x, uint8_t* y, long n4, const float* scale,
+// input of the fp8 dgrad chain).  16-byte loads (8 bf16), 8-byte stores, one grid round of 4
+// workgroups per CU, and the max folded per workgroup before one atomic (round 3: 8-byte loads and
+// a per-wave atomic over 4096 workgroups took 99 us for the value head's 72 M elements)
+__global__ __launch_bounds__(256) void quantize_bf8_dev_kernel(const __bf16* x, uint8_t* y, long n8, const float* scale,
                                                                unsigned* amax) {
+  __shared__ float red[4];
   const float sc = *scale;
   float m = 0.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
-    const bf16x4 v = *(const bf16x4*)(x + 4 * i);
-    float f[4];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    const bf16x8 v = *(const bf16x8*)(x + 8 * i);
+    float f[8];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < 8; ++r) {
       f[r] = (float)v[r];
       m = fmaxf(m, fabsf(f[r]));
       f[r] = fminf(fmaxf(f[r] * sc, -57344.f), 57344.f);
     }
-    if (y) {  // null: max |x| only (the head's dZ entering the in-register fp8 dgrad chain)
-      int pk = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], 0, false);
-      pk = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], pk, true);
-      *(int*)(y + 4 * i) = pk;
+    if (y) {  // null: max |x| only
+      int lo = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], hi, true);
+      *(int2*)(y + 8 * i) = make_int2(lo, hi);
     }
   }
   m = wave_max(m);
-  if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(amax + (blockIdx.x & (kFp8AmaxSlots - 1)), __float_as_uint(m));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    if (m > 0.f) atomicMax(amax + (blockIdx.x & (kFp8AmaxSlots - 1)), __float_as_uint(m));
+  }
 }
 
 void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st) {
-  const long n4 = n / 4;
-  int blocks = (int)((n4 + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(quantize_bf8_dev_kernel, dim3(blocks), dim3(256), 0, st, x, y, n4, scale, amax);
+  if (n % 8 != 0) throw std::invalid_argument("quantize_bf8: element count must be a multiple of 8");
+  const long n8 = n / 8;
+  int blocks = (int)((n8 + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) return;
+  hipLaunchKernelGGL(quantize_bf8_dev_kernel, dim3(blocks), dim3(256), 0, st, x, y, n8, scale, amax);
 }
 
 #ifdef AGK_KERNEL_LAB

@@ -371,7 +371,8 @@ void pack_weights_fp8_multi(at::TensorList ws, at::TensorList outs, const Tensor
 void absmax_bf16(const Tensor& x, const Tensor& amax, const Tensor& scale_any) {
   check_dev("absmax_bf16", x, amax, scale_any);
   CHECK_BF16(x); CHECK_CONTIG(x);
-  TORCH_CHECK(x.numel() % 4 == 0, "numel % 4");
+  TORCH_CHECK(x.numel() % 8 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "absmax_bf16: numel % 8 == 0 and a 16-byte aligned tensor");
   TORCH_CHECK(amax.scalar_type() == at::kInt && amax.numel() >= agk::kFp8AmaxSlots, "amax int32[64]");
   agk::launch_quantize_bf8_dev(bfp(x), nullptr, x.numel(), scale_any.data_ptr<float>(),
                                reinterpret_cast<unsigned*>(amax.data_ptr<int>()), cur_stream());
@@ -394,7 +395,9 @@ void fp8_grad_scales(const Tensor& amax, const Tensor& gscales8, const Tensor& g
 void quantize_bf8(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor& amax) {
   check_dev("quantize_bf8", x, y, scale, amax);
   CHECK_BF16(x); CHECK_CONTIG(x); CHECK_DEV(x);
-  TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 4 == 0, "y");
+  TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0,
+              "quantize_bf8: y uint8 of x's size, numel % 8 == 0, 16-byte aligned x");
   TORCH_CHECK(scale.scalar_type() == at::kFloat && amax.scalar_type() == at::kInt &&
                   amax.numel() >= agk::kFp8AmaxSlots, "scale f32[1], amax int32[64]");
   agk::launch_quantize_bf8_dev(bfp(x), y.data_ptr<uint8_t>(), x.numel(), scale.data_ptr<float>(),
@@ -455,7 +458,9 @@ void fp8_act_scales(const Tensor& amax, const Tensor& scales8, const Tensor& osc
 void quantize_fp8(const Tensor& x, const Tensor& y, double scale) {
   check_dev("quantize_fp8", x, y);
   CHECK_BF16(x); CHECK_CONTIG(x);
-  TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 4 == 0, "y");
+  TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(y.data_ptr()) % 8 == 0,
+              "quantize_bf8: y uint8 of x's size, numel % 8 == 0, 16-byte aligned x");
   agk::launch_quantize_fp8(bfp(x), y.data_ptr<uint8_t>(), x.numel(), (float)scale, cur_stream());
   launch_check("quantize_fp8");
 }

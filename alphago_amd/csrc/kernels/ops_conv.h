@@ -269,8 +269,7 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
     a.mask = bfp(*dgrad_mask);
   }
   if (mbits.has_value()) {
-    TORCH_CHECK(!dgrad_mask.has_value() && variant == 0 && y_bf16.has_value(),
-                "mbits: production forward with a bf16 output only");
+    TORCH_CHECK(!dgrad_mask.has_value() && variant == 0, "mbits: production forward only");
     CHECK_DEV(*mbits);
     TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
     const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;

@@ -373,12 +373,16 @@ class HipConvTrainer:
     def _forward_fp8(self) -> None:
         ops.quantize_fp8(self.X0, self.X08, 0)  # binary planes: exact
         x8, pin = self.X08, self.P0
+        # all-fp8 backward (fp8 wgrad + dgrad): below the last layer nothing reads the bf16
+        # activations (wgrad reads the e4m3 copies, dgrad the ReLU' bits), so only e4m3 is written
+        # (the first, calibrating backward runs bf16 wgrads on these activations)
+        e4m3_only = self.fp8_wgrad and self.fp8_dgrad and self._g8_calibrated
         for l in range(self.L):
             last = l == self.L - 1
             y8 = None if last else (self.X8[l + 1] if self.fp8_wgrad else self.Y8[l % 2])
             ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l], self.S,
-                             pin, 1, y_bf16=self.Y[l], y_fp8=y8, amax=self.amax8[l],
-                             mbits=None if last else self.MBITS[l])
+                             pin, 1, y_bf16=None if (e4m3_only and not last) else self.Y[l], y_fp8=y8,
+                             amax=self.amax8[l], mbits=None if last else self.MBITS[l])
             x8, pin = y8, 1
         ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)  # next step's activation scales
 
