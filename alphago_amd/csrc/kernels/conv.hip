@@ -224,7 +224,10 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
   const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;
   out[0] = taps;
   out[1] = (K * K / taps) * (Cout / wn) * (c48 ? 1 : Cin / wc);
-  out[2] = 2;
+  // resident workgroups per CU: two, except the 5x5 tap-merged 160 x 64 kernel (value layer 0,
+  // 49 planes), whose 154 VGPRs leave room for one 8-wave workgroup -- a grid sized for two ran
+  // as two rounds (251 us per step, profiles/r3_fp8_wgrad.md)
+  out[2] = (taps == 5 && wn == 160 && !c48) ? 1 : 2;
 }
 
 static int wgrad_xcd_group() {
