@@ -206,6 +206,9 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   const int ep_nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
   ConvEpilogue<NB, MB, MODE> ep;
   const int ep_at = EPF ? (nK > 2 ? nK - 2 : 0) : nK - 1;
+  int xo00, xo01;  // step 0's source offsets (ILV: the re-staged operands when nK == 1)
+  size_t wo00, wo01;
+  st_offsets(xo00, xo01, wo00, wo01);
   stage(0);
   wait_vmcnt0();
   __syncthreads();
@@ -275,6 +278,11 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
       for (int f = 0; f < NMF; ++f)
         if (f >= f0 && f < f1) acc[f / MB][f % MB] = mfma16x16x32(wa[f / MB], xa[f % MB], acc[f / MB][f % MB]);
     };
+    // The last step re-stages its own (in-range) operands into the idle buffer instead of
+    // branching around each DMA piece: a uniform `if (more)` compiled to one s_cbranch per piece
+    // inside the MFMA stream.
+    int lxo0 = xo00, lxo1 = xo01;
+    size_t lwo0 = wo00, lwo1 = wo01;
     for (int ks = 0; ks < nK; ++ks) {
       const int cur = ks & 1;
       const char* base = smem + cur * STAGE;
@@ -284,6 +292,14 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
       int xo0, xo1;
       size_t wo0, wo1;
       st_offsets(xo0, xo1, wo0, wo1);
+      xo0 = more ? xo0 : lxo0;
+      xo1 = more ? xo1 : lxo1;
+      wo0 = more ? wo0 : lwo0;
+      wo1 = more ? wo1 : lwo1;
+      lxo0 = xo0;
+      lxo1 = xo1;
+      lwo0 = wo0;
+      lwo1 = wo1;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
       for (int d = 0; d < NDMA; ++d) {
         mfma_range(d * MPD, (d + 1) * MPD);
         __builtin_amdgcn_sched_barrier(0);
-        if (more) st_piece(d, nb, xo0, xo1, wo0, wo1);
+        st_piece(d, nb, xo0, xo1, wo0, wo1);
         __builtin_amdgcn_sched_barrier(0);
       }
       mfma_range(NDMA * MPD, NMF);
