@@ -507,6 +507,21 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
         }
       }
 #else
+      if constexpr (KSUB == 1 && (WN / 16) % IPW == 0 && NINSTR == NWAVES * IPW) {
+        // every wave stages only dz pieces or only x pieces: one scalar branch per stage instead of
+        // one per piece
+        if (wave < (WN / 16) / IPW) {
+#pragma unroll
+          for (int i = 0; i < IPW; ++i) glds16(dsrc + (wave * IPW + i) * 16, base + (wave * IPW + i) * 1024);
+        } else {
+#pragma unroll
+          for (int i = 0; i < IPW; ++i) {
+            const int xj = wave * IPW + i - WN / 16;  // tap xj / XP, channel piece xj % XP
+            glds16(xsrc + (xj / XP) * tstep + (xj % XP) * 16, base + (WN / 16 + xj) * 1024);
+          }
+        }
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < IPW; ++i) {
         const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
