@@ -343,6 +343,30 @@ __global__ __launch_bounds__(256) void value_out_kernel(ValueOutArgs a) {
   if (tid == 0) dp[a.D] = dv;
 }
 
+// Column sums of the per-board head partials (dhead [B][N]) into the flat gradient, plus the two
+// per-board metric vectors (loss, correct) into sums[0..1]: one launch instead of three library
+// reductions.  One workgroup per column; each thread sums rows tid, tid + 256, ... in order, then a
+// fixed tree (deterministic).
+__global__ __launch_bounds__(256) void head_grad_sums_kernel(const float* dhead, int B, int N, const float* loss,
+                                                            const float* correct, float* grad, float* sums) {
+  __shared__ float red[4];
+  const int col = blockIdx.x;
+  const float* src = col < N ? dhead + col : (col == N ? loss : correct);
+  const int stride = col < N ? N : 1;
+  float s = 0.f;
+  for (int r = threadIdx.x; r < B; r += 256) s += src[(size_t)r * stride];
+  s = block_reduce_sum(s, red);
+  if (threadIdx.x == 0) {
+    if (col < N) grad[col] = s;
+    else sums[col - N] = s;
+  }
+}
+
+void launch_head_grad_sums(const float* dhead, int B, int N, const float* loss, const float* correct, float* grad,
+                           float* sums, hipStream_t st) {
+  hipLaunchKernelGGL(head_grad_sums_kernel, dim3(N + 2), dim3(256), 0, st, dhead, B, N, loss, correct, grad, sums);
+}
+
 void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(head_logits_kernel, dim3(a.B), dim3(256), 0, st, a);
 }

@@ -206,6 +206,8 @@ void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
 void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st);
 void launch_head_backward(const PolicyHeadArgs& a, const float* dlogits, hipStream_t st);
 void launch_value_out(const ValueOutArgs& a, hipStream_t st);
+void launch_head_grad_sums(const float* dhead, int B, int N, const float* loss, const float* correct, float* grad,
+                           float* sums, hipStream_t st);
 void launch_pack_input(const PackInputArgs& a, hipStream_t st);
 void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st);
 void launch_featurize(const FeaturizeArgs& a, hipStream_t st);

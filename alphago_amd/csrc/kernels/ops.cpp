@@ -135,6 +135,21 @@ void head_logits(const Tensor& y, const Tensor& w, const Tensor& b, const Tensor
 }
 
 // dz (B, S+2, S+2, C) bf16 <- ReLU'(y) * dlogits x w;  dhead (B, C_real+1) partials
+// grad[n] = sum_b dhead[b][n]; sums = {sum_b loss[b], sum_b correct[b]} (fixed order, one launch)
+void head_grad_sums(const Tensor& dhead, const Tensor& loss, const Tensor& correct, const Tensor& grad,
+                    const Tensor& sums) {
+  check_dev("head_grad_sums", dhead, loss, correct, grad, sums);
+  CHECK_F32(dhead); CHECK_F32(loss); CHECK_F32(correct); CHECK_F32(grad); CHECK_F32(sums);
+  CHECK_CONTIG(dhead); CHECK_CONTIG(loss); CHECK_CONTIG(correct); CHECK_CONTIG(grad); CHECK_CONTIG(sums);
+  TORCH_CHECK(dhead.dim() == 2 && loss.numel() == dhead.size(0) && correct.numel() == dhead.size(0) &&
+                  grad.numel() == dhead.size(1) && sums.numel() >= 2,
+              "head_grad_sums: dhead (B, N), loss/correct (B), grad (N), sums (2)");
+  if (dhead.size(0) == 0) return;
+  agk::launch_head_grad_sums(dhead.data_ptr<float>(), (int)dhead.size(0), (int)dhead.size(1), loss.data_ptr<float>(),
+                             correct.data_ptr<float>(), grad.data_ptr<float>(), sums.data_ptr<float>(), cur_stream());
+  launch_check("head_grad_sums");
+}
+
 void head_backward(const Tensor& y, const Tensor& w, const Tensor& dlogits, const Tensor& dz, const Tensor& dhead,
                    int64_t S) {
   check_dev("head_backward", y, w, dlogits, dz, dhead);
@@ -618,6 +633,7 @@ TORCH_LIBRARY(alphago_amd, m) {
       "int loss_kind=0) -> ()");
   m.def("head_logits(Tensor y, Tensor w, Tensor b, Tensor(a!) z, int S) -> ()");
   m.def("head_backward(Tensor y, Tensor w, Tensor dlogits, Tensor(a!) dz, Tensor(b!) dhead, int S) -> ()");
+  m.def("head_grad_sums(Tensor dhead, Tensor loss, Tensor correct, Tensor(a!) grad, Tensor(b!) sums) -> ()");
   m.def(
       "value_out(Tensor h, Tensor w2, Tensor b2, Tensor? target, Tensor? weight, Tensor(a!) v, Tensor(b!)? loss, "
       "Tensor(c!)? correct, Tensor(d!)? dh, Tensor(e!)? dout, float grad_scale) -> ()");
@@ -694,6 +710,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("absmax_bf16", &absmax_bf16);
   m.impl("fp8_grad_scales", &fp8_grad_scales);
   m.impl("quantize_bf8", &quantize_bf8);
+  m.impl("head_grad_sums", &head_grad_sums);
   m.impl("fp8_weight_scales", &fp8_weight_scales);
   m.impl("fp8_act_scales", &fp8_act_scales);
   m.impl("quantize_fp8", &quantize_fp8);

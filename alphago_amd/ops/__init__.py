@@ -155,6 +155,11 @@ def policy_head_train(y, w, b, target, dz, loss, correct, dhead, S: int, grad_sc
                        1 if bce else 0)
 
 
+def head_grad_sums(dhead, loss, correct, grad, sums):
+    """grad = dhead.sum(0) and sums[:2] = (loss.sum(), correct.sum()) in one deterministic launch."""
+    _ops().head_grad_sums(dhead, loss, correct, grad, sums)
+
+
 def policy_head_probs(y, w, b, probs, S: int, legal=None, temperature: float = 1.0):
     _ops().policy_head(y, w, b, None, legal, None, None, None, None, None, probs, S, 0.0, temperature)
     return probs

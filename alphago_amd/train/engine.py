@@ -553,6 +553,9 @@ class HipConvTrainer:
             return self._graph_step(planes, targets, sym)
         self.compute_grads(planes, targets, sym, weight)
         self.apply_update()
+        return self._step_metrics()
+
+    def _step_metrics(self):
         return self.loss.sum(), self.correct.sum()
 
     def _graph_step(self, planes, targets, sym):
@@ -578,8 +581,9 @@ class HipConvTrainer:
 
         def update():
             self.apply_update(device_schedule=True)
-            torch.sum(self.loss, dim=0, out=self._g_out[0])
-            torch.sum(self.correct, dim=0, out=self._g_out[1])
+            l, c = self._step_metrics()  # the eager step's sums (same summation order: bitwise equal)
+            self._g_out[0].copy_(l)
+            self._g_out[1].copy_(c)
 
         if self._graphs is None:
             if not self._graph_warm:  # eager first step: code objects loaded, LDS attributes set
@@ -640,7 +644,13 @@ class HipPolicyTrainer(HipConvTrainer):
         ops.policy_head_train(self.Y[-1], hw, hb, self.tgt, self.DZ[-1], self.loss, self.correct, self.dhead,
                               self.S, gscale, weight=weight, bce=self.policy_loss == "bce")
         ho, hn = self.fp.segments["head_w"]
-        torch.sum(self.dhead, dim=0, out=self.fp.grad[ho:ho + hn + 1])
+        # head gradient and the step's two metric sums in one launch (a fresh 2-vector per step, so
+        # the returned scalars stay valid after the next step)
+        self._metric_sums = torch.empty(2, device=self.device)
+        ops.head_grad_sums(self.dhead, self.loss, self.correct, self.fp.grad[ho:ho + hn + 1], self._metric_sums)
+
+    def _step_metrics(self):
+        return self._metric_sums[0], self._metric_sums[1]
 
     @torch.no_grad()
     def evaluate(self, planes: torch.Tensor, targets: torch.Tensor):
