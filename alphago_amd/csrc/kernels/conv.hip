@@ -47,11 +47,10 @@ static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
   else if (bm == 385) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR>(a, st);
   else if (bm == 386) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR, true>(a, st);
   else if (bm == 387) launch_fwd_bm<160, MODE, 384, 6, false, false, false, false, STR, true>(a, st);
-  else if (bm == 388) launch_fwd_bm<160, MODE, 384, 6, false, false, false, true, STR, true, true>(a, st);
   else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
   else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
   else if (bm == 64) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR>(a, st);
-  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 64 / 128 / 256 / 384-388");
+  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 64 / 128 / 256 / 384-387");
 }
 
 
@@ -90,8 +89,6 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     // 386 / 387: 385 / 384 with the chunk-outer K order (CO above)
     else if (bm == 386) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true, false, true>(a, st);
     else if (bm == 387) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, false, false, true>(a, st);
-    // 388: 386 with the wave-group stagger (STG, profiles/r3_stagger.md)
-    else if (bm == 388) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true, false, true, true>(a, st);
 #ifdef AGK_KERNEL_LAB
     // kernel-lab tile codes (conv_lab.hip, profiles/r1_fwd_kernel_experiments.md)
     else if (launch_conv_fwd_lab(bm, a, BN, MODE, st)) return;

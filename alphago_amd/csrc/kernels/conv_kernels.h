@@ -4,8 +4,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <type_traits>
-
 #include "common.h"
 #include "conv_common.h"
 #include "kernels.h"
@@ -27,12 +25,8 @@ namespace agk {
 // by the 9 taps while they are hot in the XCD's L2, where the tap-outer order
 // cycles through every chunk of the tile (BM x Cin x 2 B per tile, ~5 MB for
 // the 32 tiles of an XCD at Cin 192 -- more than its 4 MB L2).
-// STG (with ILV): waves NW/2..NW-1 -- one per SIMD, each the partner of a wave 0..NW/2-1 --
-// defer the last STG_ND weight blocks of every step's second k-half to the top of the next step,
-// where they run under that step's fragment reads (the partners otherwise reach their reads, their
-// matrix work and the barrier together, profiles/r3_stagger.md)
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
-          bool STR = false, bool CO = false, bool STG = false>
+          bool STR = false, bool CO = false>
 __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
   constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
@@ -287,83 +281,46 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     // The last step re-stages its own (in-range) operands into the idle buffer instead of
     // branching around each DMA piece: a uniform `if (more)` compiled to one s_cbranch per piece
     // inside the MFMA stream.
-    constexpr int STG_ND = STG ? 2 : 0;
-    // the whole loop, versioned per wave group (STG: GB = the deferring group)
-    auto run = [&](auto gb_tag) {
-      constexpr bool GB = decltype(gb_tag)::value;
-      int lxo0 = xo00, lxo1 = xo01;
-      size_t lwo0 = wo00, lwo1 = wo01;
-      bf16x8 dw[GB ? STG_ND : 1], dx[GB ? MB : 1];
-      auto deferred = [&]() {
+    int lxo0 = xo00, lxo1 = xo01;
+    size_t lwo0 = wo00, lwo1 = wo01;
+    for (int ks = 0; ks < nK; ++ks) {
+      const int cur = ks & 1;
+      const char* base = smem + cur * STAGE;
+      const bool more = ks + 1 < nK;
+      read_frags(base, 0, xa, wa);
+      char* nb = smem + (cur ^ 1) * STAGE;
+      int xo0, xo1;
+      size_t wo0, wo1;
+      st_offsets(xo0, xo1, wo0, wo1);
+      xo0 = more ? xo0 : lxo0;
+      xo1 = more ? xo1 : lxo1;
+      wo0 = more ? wo0 : lwo0;
+      wo1 = more ? wo1 : lwo1;
+      lxo0 = xo0;
+      lxo1 = xo1;
+      lwo0 = wo0;
+      lwo1 = wo1;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < STG_ND; ++i)
-#pragma unroll
-          for (int j = 0; j < MB; ++j)
-            acc[NB - STG_ND + i][j] = mfma16x16x32(dw[i], dx[j], acc[NB - STG_ND + i][j]);
-      };
-      for (int ks = 0; ks < nK; ++ks) {
-        const int cur = ks & 1;
-        const char* base = smem + cur * STAGE;
-        const bool more = ks + 1 < nK;
-        read_frags(base, 0, xa, wa);
-        if constexpr (GB) {
-          if (ks > 0) {  // the previous step's deferred blocks, under this step's reads
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-            deferred();
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-        char* nb = smem + (cur ^ 1) * STAGE;
-        int xo0, xo1;
-        size_t wo0, wo1;
-        st_offsets(xo0, xo1, wo0, wo1);
-        xo0 = more ? xo0 : lxo0;
-        xo1 = more ? xo1 : lxo1;
-        wo0 = more ? wo0 : lwo0;
-        wo1 = more ? wo1 : lwo1;
-        lxo0 = xo0;
-        lxo1 = xo1;
-        lwo0 = wo0;
-        lwo1 = wo1;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int d = 0; d < NDMA; ++d) {
+        mfma_range(d * MPD, (d + 1) * MPD);
         __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int d = 0; d < NDMA; ++d) {
-          mfma_range(d * MPD, (d + 1) * MPD);
-          __builtin_amdgcn_sched_barrier(0);
-          st_piece(d, nb, xo0, xo1, wo0, wo1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        mfma_range(NDMA * MPD, NMF);
-        __builtin_amdgcn_s_setprio(0);
+        st_piece(d, nb, xo0, xo1, wo0, wo1);
         __builtin_amdgcn_sched_barrier(0);
-        st_advance();
-        read_frags(base, 1, xa, wa);
-        __builtin_amdgcn_s_setprio(1);
-        if constexpr (GB) {
-#pragma unroll
-          for (int f = 0; f < (NB - STG_ND) * MB; ++f)
-            acc[f / MB][f % MB] = mfma16x16x32(wa[f / MB], xa[f % MB], acc[f / MB][f % MB]);
-#pragma unroll
-          for (int i = 0; i < STG_ND; ++i) dw[i] = wa[NB - STG_ND + i];
-#pragma unroll
-          for (int j = 0; j < MB; ++j) dx[j] = xa[j];
-        } else {
-          mfmas(xa, wa);
-        }
-        __builtin_amdgcn_s_setprio(0);
-        wait_vmcnt0();
-        __syncthreads();
       }
-      if constexpr (GB) {
-        if (nK > 0) deferred();
-      }
-    };
-    if (STG && wave >= NW / 2) run(std::integral_constant<bool, STG>{});
-    else run(std::integral_constant<bool, false>{});
+      mfma_range(NDMA * MPD, NMF);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      st_advance();
+      read_frags(base, 1, xa, wa);
+      __builtin_amdgcn_s_setprio(1);
+      mfmas(xa, wa);
+      __builtin_amdgcn_s_setprio(0);
+      wait_vmcnt0();
+      __syncthreads();
+    }
     ep.load(a, ep_mrow, ep_nbase, wn);
     ep.store(a, acc, ep_mrow);
     return;
@@ -410,16 +367,16 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
 }
 
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
-          bool STR = false, bool CO = false, bool STG = false>
+          bool STR = false, bool CO = false>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (BM * 128 + BN * 128);
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO, STG>,
+      (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO, STG>), grid,
-                     dim3(BM / MBW * 8), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO>), grid, dim3(BM / MBW * 8),
+                     smem, st, a);
 }
 
 // ----------------------------------------------------------------- wgrad

@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--precision", default="fp8", choices=["bf16", "fp8"])
     ap.add_argument("--pool", type=int, default=8192)
-    ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 64, 128, 256, 384, 385, 386, 387, 388],
+    ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 64, 128, 256, 384, 385, 386, 387],
                     help="forward/dgrad conv tiling (0 = automatic)")
     ap.add_argument("--overlap", action="store_true", help="wgrad on a second stream beside the dgrad")
     ap.add_argument("--fp8-dgrad", action="store_true", help="(default with the fp8 wgrad) fp8 precision: e5m2 x e4m3 dgrad")
