@@ -558,17 +558,25 @@ class HipConvTrainer:
     def _step_metrics(self):
         return self.loss.sum(), self.correct.sum()
 
-    def _graph_step(self, planes, targets, sym):
+    def static_inputs(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None):
+        """Graph mode: the captured step's input buffers (allocated like the given tensors on first
+        use).  A data pipeline that writes a batch straight into them (``index_select(out=...)``, a
+        host copy) and passes them to ``step`` saves the step's three input copies."""
         if self._g_in is None:
             self._g_in = (torch.empty_like(planes), torch.empty_like(targets),
                           None if sym is None else torch.empty_like(sym))
             self._g_out = (torch.zeros((), device=self.device), torch.zeros((), device=self.device))
-        gp, gt, gs = self._g_in
+        return self._g_in
+
+    def _graph_step(self, planes, targets, sym):
+        gp, gt, gs = self.static_inputs(planes, targets, sym)
         if (sym is None) != (gs is None) or planes.shape != gp.shape:
             raise ValueError("graph mode: inputs must keep their shape and symmetry argument")
-        gp.copy_(planes, non_blocking=True)
-        gt.copy_(targets, non_blocking=True)
-        if gs is not None:
+        if planes.data_ptr() != gp.data_ptr():  # the caller's own buffers: copy into the static ones
+            gp.copy_(planes, non_blocking=True)
+        if targets.data_ptr() != gt.data_ptr():
+            gt.copy_(targets, non_blocking=True)
+        if gs is not None and sym.data_ptr() != gs.data_ptr():
             gs.copy_(sym, non_blocking=True)
         # ALPHAGO_AMD_GRAPH_ALLREDUCE=1: the bucketed async all-reduce is captured inside the graph
         # (launched at its bucket points on RCCL's stream, joined before the update), so a graph step

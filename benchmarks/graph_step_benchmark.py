@@ -39,17 +39,28 @@ def main():
             g.manual_seed(1)
             pool = torch.randint(0, 2, (max(B, 256) * 4, 48, 19, 19), dtype=torch.uint8, device=dev, generator=g)
             tg = torch.randint(0, 361, (pool.shape[0],), dtype=torch.int32, device=dev, generator=g)
-            batches = []
-            for k in range(4):
-                idx = torch.arange(k * B, (k + 1) * B, device=dev) % pool.shape[0]
-                batches.append((pool[idx].contiguous(), tg[idx].contiguous(),
-                                torch.randint(0, 8, (B,), dtype=torch.int32, device=dev, generator=g)))
+            syms = torch.randint(0, 8, (4, B), dtype=torch.int32, device=dev, generator=g)
+            idxs = [torch.arange(k * B, (k + 1) * B, device=dev) % pool.shape[0] for k in range(4)]
+            # every step gathers its batch from the device pool (the same data movement in both
+            # modes); graph mode gathers straight into the captured step's input buffers
+            static = tr.static_inputs(pool[:B], tg[:B], syms[0]) if graph else None
+
+            def step(k):
+                idx = idxs[k % 4]
+                if static is None:
+                    tr.step(pool.index_select(0, idx), tg.index_select(0, idx), syms[k % 4].clone())
+                else:
+                    torch.index_select(pool, 0, idx, out=static[0])
+                    torch.index_select(tg, 0, idx, out=static[1])
+                    static[2].copy_(syms[k % 4])
+                    tr.step(*static)
+
             for k in range(a.warmup):
-                tr.step(*batches[k % 4])
+                step(k)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for k in range(steps):
-                tr.step(*batches[k % 4])
+                step(k)
             th = time.perf_counter() - t0
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0

@@ -68,7 +68,7 @@ def test_graph_step_bitwise_equals_eager(cuda_device, B):
     from alphago_amd.models.nets import PolicyNet
     from alphago_amd.train.engine import HipPolicyTrainer
 
-    def run(graph):
+    def run(graph, static=False):
         torch.manual_seed(0)
         net = PolicyNet(48, filters_per_layer=192, layers=12)
         tr = HipPolicyTrainer(net, B, lr=0.003, decay=1e-3, device=cuda_device)
@@ -81,6 +81,12 @@ def test_graph_step_bitwise_equals_eager(cuda_device, B):
             planes = torch.randint(0, 2, (B, 48, 19, 19), dtype=torch.uint8, device=cuda_device, generator=g)
             tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device, generator=g)
             sym = torch.randint(0, 8, (B,), dtype=torch.int32, device=cuda_device, generator=g)
+            if static:  # the batch written straight into the captured step's input buffers
+                sp, st, ss = tr.static_inputs(planes, tgt, sym)
+                sp.copy_(planes)
+                st.copy_(tgt)
+                ss.copy_(sym)
+                planes, tgt, sym = sp, st, ss
             l, c = tr.step(planes, tgt, sym)
             losses.append((l.clone(), c.clone()))
         torch.cuda.synchronize()
@@ -88,8 +94,10 @@ def test_graph_step_bitwise_equals_eager(cuda_device, B):
 
     fe, le, ie, _ = run(False)
     fg, lg, ig, tr = run(True)
+    fs, ls_, is_, _ = run(True, static=True)
     assert tr._graphs is not None and len(tr._graphs) == 1
-    assert ie == ig == 5
-    assert torch.equal(fe, fg)
-    for (a, b), (c, d) in zip(le, lg):
+    assert ie == ig == is_ == 5
+    assert torch.equal(fe, fg) and torch.equal(fe, fs)
+    for (a, b), (c, d), (e, f) in zip(le, lg, ls_):
         assert torch.equal(a, c) and torch.equal(b, d)
+        assert torch.equal(a, e) and torch.equal(b, f)
