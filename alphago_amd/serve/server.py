@@ -31,6 +31,7 @@ from .batcher import BatcherPool, BatchingEvaluator, state_eval_fn
 
 
 MAX_BODY = 1 << 20  # a 19x19 move list is a few KB
+DRAIN_LIMIT = 16 * MAX_BODY  # oversized bodies up to this size are read and discarded before the 413
 
 
 class BadRequest(ValueError):
@@ -217,7 +218,17 @@ def _handler(service: GoService):
                     self._send(400, {"error": "negative Content-Length"})
                     return
                 if n > MAX_BODY:
-                    self.close_connection = True  # the unread body stays on the socket
+                    # drain a moderately oversized body (bounded, discarded in 64 KiB reads) so the
+                    # client, still sending, receives the 413 instead of a reset; beyond the drain
+                    # bound the connection is just closed
+                    self.close_connection = True
+                    if n <= DRAIN_LIMIT:
+                        left = n
+                        while left > 0:
+                            got = self.rfile.read(min(left, 1 << 16))
+                            if not got:
+                                break
+                            left -= len(got)
                     self._send(413, {"error": "request body over %d bytes" % MAX_BODY})
                     return
                 req = json.loads(self.rfile.read(n) or b"{}")
