@@ -326,8 +326,13 @@ def pack_weights_fp8_multi(ws, outs, scales_dev: torch.Tensor, layer, transposed
     """Every fp8 weight pack of a repack in ONE launch: job i packs ws[i] into outs[i] with the device
     scale scales_dev[layer[i]]; transposed[i] selects the dgrad layout (rows = input channels,
     taps flipped)."""
-    _ops().pack_weights_fp8_multi(list(ws), list(outs), scales_dev, [int(x) for x in layer],
-                                  [int(bool(x)) for x in transposed])
+    ws, outs, layer, transposed = list(ws), list(outs), [int(x) for x in layer], [int(bool(x)) for x in transposed]
+    for i in range(0, len(ws), FP8_PACK_MAX_JOBS):  # the kernel's job table holds 48 entries
+        j = i + FP8_PACK_MAX_JOBS
+        _ops().pack_weights_fp8_multi(ws[i:j], outs[i:j], scales_dev, layer[i:j], transposed[i:j])
+
+
+FP8_PACK_MAX_JOBS = 48  # kMaxFp8PackJobs (csrc/kernels/ops.cpp)
 
 
 def conv_dgrad_bits_bf8(dz, wd, dx, mbits, dx8, scale, K: int, S: int, amax=None, tile: int = 0):

@@ -39,11 +39,18 @@ class BatchedSampler(object):
         m = _engine().featurize_batch(list(states), ["sensibleness"], self.threads)
         return m.reshape(len(states), -1)
 
-    def _probs_encoded(self, states, eng):
+    def _probs_encoded(self, states, eng, want_planes: bool = False):
         E = _engine()
         b, a, m, l = E.encode_batch(list(states), eng.needs_ladder, self.threads)
         probs, sens, bad = eng.evaluate_encoded(b, a, m, l)
         self._bad = list(bad)
+        self._enc_planes = None
+        if want_planes:
+            # the featurizer's output rows; the fallback evaluation below may reuse the same bucket
+            # buffers, so they are copied out first when it runs
+            self._enc_planes = eng.encoded_planes_view(len(states))
+            if bad:
+                self._enc_planes = self._enc_planes.clone()
         if bad:  # eye recursion too deep for the kernel: recompute those rows from CPU planes
             sub = [states[i] for i in bad]
             masks = self.masks(sub)
@@ -72,8 +79,8 @@ class BatchedSampler(object):
         dev_planes = None
         if device_planes and planes is None and self.device_planes_ok():
             eng.set_encoded_planes(True)
-            probs, has = self._probs_encoded(states, eng)
-            dev_planes = eng.encoded_planes_view(n)
+            probs, has = self._probs_encoded(states, eng, want_planes=True)
+            dev_planes = self._enc_planes
             if self._bad:  # overflowed eye recursion: those rows from the host featurizer
                 dev_planes[self._bad] = torch.from_numpy(self.featurize([states[i] for i in self._bad])).to(
                     dev_planes.device)

@@ -249,6 +249,9 @@ class HipConvTrainer:
                                    dtype=torch.uint8, device=dev) for l in range(L)]
             self.wscale8 = torch.ones(L, device=dev)
             self.scales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
+            # this step's activation exponents, kept for the fp8 wgrad: X8[l] was quantised with
+            # them, while scales8[:, 0] already holds the next step's delayed exponents by then
+            self.xscale8 = torch.full((L, 1), 127, dtype=torch.int32, device=dev)
             self.osc8 = torch.ones(L, device=dev)
             self.amax8 = ops.fp8_amax_buffer(L, dev)
             self.X08 = torch.zeros(self.X0.shape, dtype=torch.uint8, device=dev)
@@ -384,6 +387,8 @@ class HipConvTrainer:
                              pin, 1, y_bf16=None if (e4m3_only and not last) else self.Y[l], y_fp8=y8,
                              amax=self.amax8[l], mbits=None if last else self.MBITS[l])
             x8, pin = y8, 1
+        if self.fp8_wgrad:
+            self.xscale8.copy_(self.scales8[:, 0:1])
         ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)  # next step's activation scales
 
     @torch.no_grad()
@@ -422,7 +427,7 @@ class HipConvTrainer:
             torch.cuda.current_stream(self.device).wait_event(self._slab_free[i])
         if f8:  # e5m2 dZ x e4m3 X, dequantised by the MFMA's block scales
             # (its tap-0 workgroups also fold max |dZ| into the delayed-scale slots of layer l)
-            ops.conv_wgrad_fp8(self.X8[l], self.DZ8[l], slab, dbs, self.scales8[l, 0:1], self.gscales8[l, 0:1],
+            ops.conv_wgrad_fp8(self.X8[l], self.DZ8[l], slab, dbs, self.xscale8[l], self.gscales8[l, 0:1],
                                self.gosc8[l:l + 1], self.K[l], self.S, pin, 1,
                                amax=self.gamax8[l] if l < self.L - 1 else None)
         else:
@@ -489,15 +494,17 @@ class HipConvTrainer:
                 else:  # ReLU' bitmask from the forward epilogue (bf16 and fp8 forwards write it)
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=self.conv_tile)
+        # join the side streams first: the fp8 wgrads still running there read gscales8 / gosc8
+        # and fold max |dZ| into gamax8, which the scale update below rewrites and clears
+        if self.s_w is not None:
+            main.wait_stream(self.s_w)
+        if self.s_r is not None:
+            main.wait_stream(self.s_r)
         if self.precision == "fp8" and (self.fp8_dgrad or self.fp8_wgrad):
             if self._g8_calibrated:
                 ops.fp8_grad_scales(self.gamax8, self.gscales8, self.gosc8, 1)  # next step's gradient scales
             else:
                 self._fp8_grad_calibrate()
-        if self.s_w is not None:
-            main.wait_stream(self.s_w)
-        if self.s_r is not None:
-            main.wait_stream(self.s_r)
         if red:
             if self.defer_allreduce:
                 for bi in range(len(self.buckets)):

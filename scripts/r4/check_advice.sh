@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 4: the ADVICE regression tests (fp8 wgrad exponents, fp8 overlap join, device records)
+# and a driver-shaped bench.  Output: gpurun_out/r4_advice/
+set -e
+O=gpurun_out/r4_advice
+mkdir -p $O
+export PYTHONPATH=$PWD
+timeout -k 10 240 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench1.json 2> $O/bench1.err
+tail -1 $O/bench1.json | cut -c1-260
+timeout -k 10 400 python3 -u -m pytest tests/test_fp8_inference.py tests/test_rl_value.py -x -v --timeout 150 --timeout-method thread > $O/tests.log 2>&1
+tail -3 $O/tests.log

@@ -99,6 +99,69 @@ def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad, fp8_wgrad):
     assert (t8.scales8[:, 0] != 127).any()  # activation exponents were set from the data
 
 
+def test_fp8_wgrad_uses_this_steps_activation_exponents(cuda_device):
+    """The fp8 wgrad dequantises X8[l] with the exponent it was quantised with, not the delayed
+    exponent the forward already computed for the next step: shrinking the first layer's weights 4x
+    between two steps moves every activation exponent by 2, and the fp8 weight gradients must still
+    match the bf16 trainer's in direction AND magnitude (a stale exponent scales a layer's gradient
+    by 4 or 1/4 while leaving its cosine at 1)."""
+    import copy
+
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import HipValueTrainer
+
+    torch.manual_seed(0)
+    B = 64
+    net = ValueNet(49, filters_per_layer=152, layers=4)
+    net16 = copy.deepcopy(net)
+    planes = _planes(B, 49, seed=7).to(cuda_device)
+    z = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
+    t8 = HipValueTrainer(net, B, lr=0.0, device=cuda_device, precision="fp8", fp8_dgrad=True, fp8_wgrad=True)
+    t16 = HipValueTrainer(net16, B, lr=0.0, device=cuda_device)
+    for _ in range(2):  # calibrating step, then one all-fp8 step whose forward sets the delayed scales
+        t8.compute_grads(planes, z)
+    before = t8.scales8[:, 0].clone()
+    for t in (t8, t16):
+        t.fp.views["w0"].mul_(0.25)
+        t.repack()
+    t8.compute_grads(planes, z)
+    t16.compute_grads(planes, z)
+    torch.cuda.synchronize()
+    assert (t8.scales8[1:, 0] != before[1:]).all(), "the activation exponents did not move"
+    for l in range(1, 4):
+        a, b = t8.fp.grad_views["w%d" % l].double(), t16.fp.grad_views["w%d" % l].double()
+        cos = torch.nn.functional.cosine_similarity(a.flatten(), b.flatten(), dim=0).item()
+        ratio = (a.norm() / b.norm()).item()
+        assert cos > 0.9 and 0.7 < ratio < 1.4, (l, cos, ratio)
+
+
+@pytest.mark.parametrize("F", [152])
+def test_fp8_overlap_backward_matches_serial(cuda_device, F):
+    """fp8 value training with the wgrad on its own stream (overlap=True) gives the serial
+    backward's gradients and scale state bit for bit: the gradient-scale update runs after the
+    side stream has joined (the fp8 wgrads there read and fold into the scale buffers)."""
+    import copy
+
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import HipValueTrainer
+
+    torch.manual_seed(2)
+    B = 64
+    net = ValueNet(49, filters_per_layer=F, layers=4)
+    nets = [net, copy.deepcopy(net)]
+    planes = _planes(B, 49, seed=9).to(cuda_device)
+    z = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
+    trs = [HipValueTrainer(n, B, lr=0.01, device=cuda_device, precision="fp8", overlap=ov) for n, ov in
+           zip(nets, (False, True))]
+    for _ in range(4):
+        for t in trs:
+            t.step(planes, z)
+    torch.cuda.synchronize()
+    a, b = trs
+    assert torch.equal(a.fp.flat, b.fp.flat)
+    assert torch.equal(a.gscales8, b.gscales8) and torch.equal(a.gamax8, b.gamax8)
+
+
 @pytest.mark.gpu
 def test_scalef32_bf8_conversion_semantics(cuda_device):
     """Pins the semantics of v_cvt_scalef32_pk_bf8_bf16 (2 bf16 -> 2 e5m2 with an f32 scale in one
