@@ -55,11 +55,17 @@ def hip_path(flavor: str = "prod") -> str:
 def _hip_sources(flavor: str):
     kd = os.path.join(CSRC, "kernels")
     if flavor == "lab":
-        return [os.path.join(kd, f) for f in ("conv.hip", "conv_lab.hip", "conv_wgrad_row.hip", "conv_fwd_variants.hip",
-                                              "conv_fp8.hip", "winograd.hip", "lab_probes.hip", "ops_lab.cpp")]
+        return [os.path.join(kd, f) for f in LAB_SOURCES + ("conv.hip", "conv_fp8.hip", "ops_lab.cpp")]
     srcs = sorted(glob.glob(os.path.join(kd, "*.hip")) + glob.glob(os.path.join(kd, "*.cpp")))
-    return [f for f in srcs if os.path.basename(f) not in ("conv_fwd_variants.hip", "conv_lab.hip", "winograd.hip", "lab_probes.hip",
-                                                                 "ops_lab.cpp")]
+    return [f for f in srcs if os.path.basename(f) not in LAB_SOURCES + ("ops_lab.cpp",)]
+
+
+# kernel-lab sources: measured and recorded slower or dead, kept buildable for experiments and out of
+# the production library -- forward-tile variants and the compact-halo kernels, wgrad variants 1-4 and
+# 6-8, the one-kernel-row wgrad (variant 5, profiles/r3_wgrad_row.md), Winograd (r3_winograd.md), the
+# GPU ladder reader (16x slower than the host reader, r2_gpu_ladders.md), hardware probes
+LAB_SOURCES = ("conv_fwd_variants.hip", "conv_lab.hip", "conv_wgrad_row.hip", "winograd.hip", "ladder.hip",
+               "lab_probes.hip")
 
 
 def _digest(paths, extra: str = "") -> str:
@@ -124,7 +130,7 @@ def build_selftest(sanitize: str = "", force: bool = False, verbose: bool = Fals
     """Standalone engine self-test (csrc/tools/engine_selftest.cpp), optionally
     with host sanitizers: ``address,undefined`` or ``thread``."""
     srcs = sorted(glob.glob(os.path.join(CSRC, "engine", "*.cpp")))
-    srcs = [s for s in srcs if not s.endswith(("bindings.cpp", "lzf.cpp"))]  # pybind11-only files
+    srcs = [s for s in srcs if not s.endswith(("bindings.cpp", "lzf.cpp", "lockstep.cpp"))]  # pybind11-only files
     hdrs = sorted(glob.glob(os.path.join(CSRC, "engine", "*.h")))
     main = os.path.join(CSRC, "tools", "engine_selftest.cpp")
     tag = sanitize.replace(",", "_") if sanitize else "plain"

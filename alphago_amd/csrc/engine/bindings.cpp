@@ -19,6 +19,7 @@ using namespace ag;
 namespace ag {
 void bind_mcts(pybind11::module_& m);
 void bind_lzf(py::module_& m);
+void bind_lockstep(py::module_& m);
 }
 
 static int to_idx(const GameState& s, const py::object& a) {
@@ -286,4 +287,5 @@ PYBIND11_MODULE(_engine, m) {
 
   bind_mcts(m);
   bind_lzf(m);
+  bind_lockstep(m);
 }

@@ -50,7 +50,9 @@ static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
   else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
   else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
   else if (bm == 64) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR>(a, st);
-  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 64 / 128 / 256 / 384-387");
+  else if (bm == 65) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR, false, 4>(a, st);
+  else if (bm == 130) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR, false, 3>(a, st);
+  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 64 / 65 / 128 / 130 / 256 / 384-387");
 }
 
 
@@ -83,6 +85,9 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
     else if (bm == 128) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
     else if (bm == 64) launch_fwd_bm<BN, MODE, 64, 2>(a, st);
+    // small batches: 65 / 130 = the 64 / 128-pixel tiles on a 4 / 3-slot LDS ring (NS above)
+    else if (bm == 65) launch_fwd_bm<BN, MODE, 64, 2, true, true, false, false, false, false, 4>(a, st);
+    else if (bm == 130) launch_fwd_bm<BN, MODE, 128, 4, true, true, false, false, false, false, 3>(a, st);
     // 385: the 384 tile with the next stage's LDS-DMA spread through the first
     // k-half's MFMAs instead of issued as one burst (kernel-lab tile 9)
     else if (bm == 385) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
@@ -116,6 +121,29 @@ void launch_conv_fwd(const ConvFwdArgs& a_in, int mode, hipStream_t st) {
   else launch_fwd_mode<MODE_NONE>(a, st);
 }
 
+// packed-tap first layer (conv_fwd_pk_kernel): 384-pixel tile, 96 x 96 (or 96 x 80) per wave
+template <int BN>
+static void launch_fwd_pk_t(const ConvFwdArgs& a, int cpt, hipStream_t st) {
+  constexpr int BM = 384, MBW = 6;
+  constexpr int smem = 2 * (BM * 128 + BN * 128);
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_fwd_pk_kernel<BN, BM, MBW>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+  dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
+  hipLaunchKernelGGL((conv_fwd_pk_kernel<BN, BM, MBW>), grid, dim3(BM / MBW * 8), smem, st, a, cpt);
+}
+
+void launch_conv_fwd_pk(const ConvFwdArgs& a_in, int cpt, hipStream_t st) {
+  ConvFwdArgs a = a_in;
+  a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
+  a.divS = make_fastdiv((uint32_t)a.S);
+  if (cpt < 4 || cpt > 8 || a.Cin != 64) throw std::invalid_argument("conv_fwd_pk: 32 < cin_real <= 64 in a 64-channel input");
+  if (a.Cout == 160) launch_fwd_pk_t<160>(a, cpt, st);
+  else if (a.Cout % 192 == 0) launch_fwd_pk_t<192>(a, cpt, st);
+  else if (a.Cout % 128 == 0) launch_fwd_pk_t<128>(a, cpt, st);
+  else launch_fwd_pk_t<64>(a, cpt, st);
+}
+
 // ----------------------------------------------------------------- wgrad launchers
 
 template <int WN, int TAPS>
@@ -147,16 +175,39 @@ int wgrad_tap_group(int Cout, int Cin, int K, int variant) {
   return (c64 && variant == 0 && (K == 3 || K == 5)) ? K : 1;
 }
 
+// variant 9 (small batches): the per-tap kernel on a 4-slot LDS ring, one workgroup per CU, for the
+// tile geometries whose waves stage equal piece counts (192 x 192, 128 x 128, 160 x 160)
+template <int WN, int WC, int NWC>
+static bool launch_wgrad_ring(const ConvWgradArgs& a, dim3 grid, hipStream_t st) {
+  constexpr int KS = kWgradKsub;
+  constexpr int NWAVES = 2 * NWC;
+  constexpr int NINSTR = WN / 16 + WC / 16;
+  constexpr int IPW = (NINSTR + NWAVES - 1) / NWAVES;
+  if constexpr ((WN / 16) % IPW == 0 && NINSTR == NWAVES * IPW) {
+    constexpr int NS = 4;
+    constexpr int smem = NS * (WN + WC) * 64 * KS;
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void*)conv_wgrad_kernel<WN, WC, KS, NWC, 1, false, false, false, NS>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+    hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS, NWC, 1, false, false, false, NS>), grid, dim3(64 * NWAVES),
+                       smem, st, a);
+    return true;
+  }
+  return false;
+}
+
 template <int WN, int WC>
 static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
   dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
   constexpr int KS = kWgradKsub;
   constexpr int smem = 2 * (WN + WC) * 64 * KS;
+  if (WC != 64 && a.variant == 9 && launch_wgrad_ring<WN, WC, 4>(a, grid, st)) return;
 #ifdef AGK_KERNEL_LAB
-  if (launch_conv_wgrad_lab(a, WN, WC, grid, st)) return;  // lab variants 2 / 3 / 4 (conv_lab.hip)
+  if (a.variant != 9 && launch_conv_wgrad_lab(a, WN, WC, grid, st)) return;  // lab variants 2 / 3 / 4 (conv_lab.hip)
 #else
-  if (a.variant != 0) throw std::invalid_argument("conv_wgrad: variant " + std::to_string(a.variant) +
-                                                  " is a kernel-lab variant");
+  if (a.variant != 0 && a.variant != 9)
+    throw std::invalid_argument("conv_wgrad: variant " + std::to_string(a.variant) + " is a kernel-lab variant");
 #endif
   if constexpr (WC == 64) {
     // tap-merged kernel rows (see conv_wgrad_kernel); lab variant 1 forces one tap per workgroup
@@ -174,7 +225,8 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
 // 160 x 160 tile on 4 waves (2 n x 2 c, 80 x 80 per wave): the value net's
 // padded width; 40 KB of LDS, so several workgroups share a CU
 static void launch_wgrad_160x160(const ConvWgradArgs& a, hipStream_t st) {
-  if (a.variant != 0) throw std::invalid_argument("conv_wgrad: 160-wide tiles have no lab variants");
+  if (a.variant == 9 && launch_wgrad_ring<160, 160, 2>(a, dim3(a.nsplit, a.T, 1), st)) return;
+  if (a.variant != 0 && a.variant != 9) throw std::invalid_argument("conv_wgrad: 160-wide tiles have no lab variants");
   constexpr int KS = kWgradKsub;
   constexpr int smem = 2 * (160 + 160) * 64 * KS;
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<160, 160, KS, 2>,
@@ -210,6 +262,7 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
     out[2] = 2;
     return;
   }
+#ifdef AGK_KERNEL_LAB
   const int code = variant == 5 ? wgrad_row_code(Cout, Cin, cin_real, K) : 0;
   if (code) {  // one kernel row per workgroup, one workgroup per CU (~170 VGPRs, 8 or 6 waves)
     out[0] = K;
@@ -217,8 +270,9 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
     out[2] = 1;
     return;
   }
+#endif
   // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
-  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 8) ? 0 : variant);
+  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 9) ? 0 : variant);
   const bool c48 = cin_real <= 48 && Cin == 64;
   const int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
   const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;
@@ -228,6 +282,7 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
   // 49 planes), whose 154 VGPRs leave room for one 8-wave workgroup -- a grid sized for two ran
   // as two rounds (251 us per step, profiles/r3_fp8_wgrad.md)
   out[2] = (taps == 5 && wn == 160 && !c48) ? 1 : 2;
+  if (variant == 9 && taps == 1) out[2] = 1;  // the 4-slot ring: one workgroup per CU
 }
 
 static int wgrad_xcd_group() {
@@ -243,8 +298,9 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
   a.xcd_group = wgrad_xcd_group();
+#ifdef AGK_KERNEL_LAB
   if (a.variant == 5) {
-    // one-kernel-row wgrad (conv_wgrad_row.hip), opt-in: in the power-limited steady state it ran
+    // one-kernel-row wgrad (conv_wgrad_row.hip), kernel lab: in the power-limited steady state it ran
     // 607-694 us per 192 -> 192 layer against 548-583 us for the per-tap kernel
     // (profiles/r3_wgrad_row.md); layers it does not cover run the per-tap kernel
     const int code = wgrad_row_code(a.Cout, a.Cin, a.cin_real, a.K);
@@ -254,6 +310,7 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
     }
     a.variant = 0;
   }
+#endif
 #ifdef AGK_KERNEL_LAB
   if (a.variant >= 6 && a.variant <= 8) {  // tap pairs (8: DMA spread) / line-staged per-tap kernel
     if (wgrad_pair_applies(a.Cout, a.Cin, a.cin_real, a.K) && launch_conv_wgrad_line_lab(a, st)) return;

@@ -25,8 +25,11 @@ namespace agk {
 // by the 9 taps while they are hot in the XCD's L2, where the tap-outer order
 // cycles through every chunk of the tile (BM x Cin x 2 B per tile, ~5 MB for
 // the 32 tiles of an XCD at Cin 192 -- more than its 4 MB L2).
+// NS > 2 (small batches): an NS-slot LDS ring, the DMA of step ks + NS - 1 issued while step ks
+// computes.  With few workgroups per CU nothing else hides the global->LDS latency of a 2-buffer
+// loop (~0.75 us per K-step at B = 16, 27 steps per 3x3 layer: profiles/r3_small_batch/).
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
-          bool STR = false, bool CO = false>
+          bool STR = false, bool CO = false, int NS = 2>
 __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
   constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
@@ -206,6 +209,32 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
   const int ep_nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
   ConvEpilogue<NB, MB, MODE> ep;
   const int ep_at = EPF ? (nK > 2 ? nK - 2 : 0) : nK - 1;
+  if constexpr (NS > 2) {
+    static_assert(PIPE && !M32 && !ILV && !BDIST, "ring: the pipelined 16x16 loop");
+    // DMA instructions per wave per stage (the vmcnt unit of one stage)
+    constexpr int PW = A_INSTR + B_INSTR;
+    static_assert(PW * (NS - 2) <= 63, "vmcnt range");
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nK) stage(s);  // workgroup-uniform
+    for (int ks = 0; ks < nK; ++ks) {
+      // step ks has landed once at most (stages issued after it) x PW DMAs are outstanding
+      const int later = (nK - 1 - ks) < (NS - 2) ? (nK - 1 - ks) : (NS - 2);
+      vmcnt_wait_dyn(later * PW);
+      __syncthreads();  // every wave's DMA of step ks is visible; slot (ks - 1) % NS is free
+      if (ks + NS - 1 < nK) stage((ks + NS - 1) % NS);
+      const char* base = smem + (ks % NS) * STAGE;
+      read_frags(base, 0, xa, wa);
+      read_frags(base, 1, xb, wb);
+      if (ks == ep_at) ep.load(a, ep_mrow, ep_nbase, wn);
+      __builtin_amdgcn_s_setprio(1);
+      mfmas(xa, wa);
+      mfmas(xb, wb);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    ep.store(a, acc, ep_mrow);
+    return;
+  }
   int xo00, xo01;  // step 0's source offsets (ILV: the re-staged operands when nK == 1)
   size_t wo00, wo01;
   st_offsets(xo00, xo01, wo00, wo01);
@@ -367,16 +396,167 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
 }
 
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
-          bool STR = false, bool CO = false>
+          bool STR = false, bool CO = false, int NS = 2>
 static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
-  constexpr int smem = 2 * (BM * 128 + BN * 128);
+  constexpr int smem = NS * (BM * 128 + BN * 128);
+  static_assert(smem <= 160 * 1024, "LDS");
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO>,
+      (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO, NS>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO>), grid, dim3(BM / MBW * 8),
-                     smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO, NS>), grid,
+                     dim3(BM / MBW * 8), smem, st, a);
+}
+
+// ----------------------------------------------------------------- packed-tap forward (thin first layer)
+// The first layer's input has cin_real <= 64 real planes in a 64-channel padded tensor (48 policy,
+// 49 value).  conv_fwd_kernel multiplies all 64 channels of every tap, so a quarter of the layer-0
+// MACs are zeros.  Here the K loop runs over (tap, 8-channel chunk) pairs of the real channels only:
+// cpt = ceil(cin_real / 8) chunks per tap, 8 chunks (one 64-wide K-step) per step, chunk j of step s
+// is q = 8 s + j = (tap q / cpt, channels 8 (q % cpt) ..).  48 planes: 25 x 6 = 150 chunks in 19 steps
+// instead of 25.  Weights packed [step][Cout][64] in the same chunk order (pack_weights_kernel with
+// PackLayer::pk_cpt), zero past the last chunk.  Each lane's DMA source is its own (tap, chunk): the
+// wave-uniform step state keeps the offsets of taps t0, t0 + 1, t0 + 2 (a step spans at most three
+// taps when cpt >= 4) and a piece selects one of them.  The MFMA loop, LDS layout and epilogue are
+// those of the 384-pixel tile (96 x 96 per wave, one DMA burst per step).
+template <int BN, int BM, int MBW>
+__global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_pk_kernel(ConvFwdArgs a, int cpt) {
+  constexpr int NW = BM / (16 * MBW) * 2;
+  constexpr int NB = BN / 32;
+  constexpr int MB = MBW;
+  constexpr int A_BYTES = BM * 128;
+  constexpr int B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int A_ROWS_PW = BM / NW;
+  constexpr int A_INSTR = A_ROWS_PW / 8;
+  constexpr bool BDIST = (BN / NW) % 8 != 0;
+  constexpr int B_ROWS_PW = BN / NW;
+  constexpr int B_INSTR = BDIST ? (BN / 8 + NW - 1) / NW : B_ROWS_PW / 8;
+  static_assert(BN % 32 == 0 && A_ROWS_PW % 8 == 0, "tile geometry");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_id();
+  const int wm = wave >> 1, wn = wave & 1;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int SS = a.S * a.S;
+  const int T = a.K * a.K;
+  const int nK = (T * cpt + 7) >> 3;
+
+  int arow[A_INSTR], alg[A_INSTR];
+#pragma unroll
+  for (int i = 0; i < A_INSTR; ++i) {
+    const int r = wave * A_ROWS_PW + i * 8 + (lane >> 3);
+    int m = m0 + r;
+    m = m < a.M ? m : a.M - 1;
+    const int b = fdiv(m, a.divSS);
+    const int rem = m - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jj = rem - ii * a.S;
+    alg[i] = (lane & 7) ^ ((r >> 1) & 7);
+    arow[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin;
+  }
+  int brow[B_INSTR], bldsrow[B_INSTR];
+#pragma unroll
+  for (int i = 0; i < B_INSTR; ++i) {
+    const int piece = BDIST ? wave + i * NW : wave * (B_ROWS_PW / 8) + i;
+    const int r = piece * 8 + (lane >> 3);
+    const int logical = (lane & 7) ^ ((r >> 1) & 7);
+    brow[i] = (n0 + (r < BN ? r : BN - 1)) * 64 + logical * 8;
+    bldsrow[i] = piece * 8;
+  }
+
+  // wave-uniform staging cursor: first chunk st_c of tap st_t = (st_kh, st_kw), weight step offset
+  int st_c = 0, st_t = 0, st_kh = 0, st_kw = 0;
+  size_t st_w = 0;
+  const size_t wstep = (size_t)a.Cout * 64;
+  auto stage = [&](int buf) {
+    char* base = smem + buf * STAGE;
+    // offsets of taps st_t, st_t + 1, st_t + 2 (past the last tap: the last tap's pixels, zero weights)
+    int kh1 = st_kh, kw1 = st_kw + 1;
+    if (kw1 == a.K) { kw1 = 0; ++kh1; }
+    int kh2 = kh1, kw2 = kw1 + 1;
+    if (kw2 == a.K) { kw2 = 0; ++kh2; }
+    const int o0 = (st_kh * a.HPi + st_kw) * a.Cin;
+    const int o1 = st_t + 1 < T ? (kh1 * a.HPi + kw1) * a.Cin : o0;
+    const int o2 = st_t + 2 < T ? (kh2 * a.HPi + kw2) * a.Cin : o1;
+#pragma unroll
+    for (int i = 0; i < A_INSTR; ++i) {
+      const int e = st_c + alg[i];
+      const int dt = (e >= cpt ? 1 : 0) + (e >= 2 * cpt ? 1 : 0);
+      const int off = (dt == 0 ? o0 : dt == 1 ? o1 : o2) + (e - dt * cpt) * 8;
+#ifdef AGK_DEBUG
+      const int xo = arow[i] + off;
+      const bool ok = AGK_DCHECK(xo >= 0 && (long long)xo + 8 <= a.x_elems, DBG_FWD_X);
+      glds16(a.x + (ok ? xo : 0), base + (wave * A_ROWS_PW + i * 8) * 128);
+#else
+      glds16(a.x + arow[i] + off, base + (wave * A_ROWS_PW + i * 8) * 128);
+#endif
+    }
+#pragma unroll
+    for (int i = 0; i < B_INSTR; ++i) {
+      if (BDIST && wave + i * NW >= BN / 8) continue;  // wave-uniform
+#ifdef AGK_DEBUG
+      const bool ok = AGK_DCHECK((long long)(st_w + brow[i]) + 8 <= a.w_elems, DBG_FWD_W);
+      glds16(ok ? a.w + st_w + brow[i] : a.w, base + A_BYTES + bldsrow[i] * 128);
+#else
+      glds16(a.w + st_w + brow[i], base + A_BYTES + bldsrow[i] * 128);
+#endif
+    }
+    // advance by 8 chunks (at most two tap boundaries when cpt >= 4)
+    st_w += wstep;
+    st_c += 8;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (st_c >= cpt) {
+        st_c -= cpt;
+        ++st_t;
+        if (++st_kw == a.K) { st_kw = 0; ++st_kh; }
+      }
+    }
+  };
+
+  f32x4 acc[NB][MB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+#pragma unroll
+    for (int j = 0; j < MB; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int swz = (lane & 15) >> 1;
+  const int xrow0 = (wm * 16 * MB + (lane & 15)) * 128;
+  const int wrow0 = A_BYTES + (wn * (BN / 2) + (lane & 15)) * 128;
+  bf16x8 xf[MB], wf[NB];
+  ConvEpilogue<NB, MB, MODE_BIAS_RELU> ep;
+  const int ep_mrow = m0 + wm * 16 * MB + (lane & 15);
+  const int ep_nbase = n0 + wn * (BN / 2) + ((lane >> 4) << 2);
+
+  stage(0);
+  wait_vmcnt0();
+  __syncthreads();
+  for (int ks = 0; ks < nK; ++ks) {
+    const int cur = ks & 1;
+    const char* base = smem + cur * STAGE;
+    if (ks + 1 < nK) stage(cur ^ 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int choff = (((kk << 2) + (lane >> 4)) ^ swz) << 4;
+#pragma unroll
+      for (int j = 0; j < MB; ++j) xf[j] = *(const bf16x8*)(base + xrow0 + j * 16 * 128 + choff);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) wf[i] = *(const bf16x8*)(base + wrow0 + i * 16 * 128 + choff);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < MB; ++j) acc[i][j] = mfma16x16x32(wf[i], xf[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    wait_vmcnt0();
+    __syncthreads();
+  }
+  ep.load(a, ep_mrow, ep_nbase, wn);
+  ep.store(a, acc, ep_mrow);
 }
 
 // ----------------------------------------------------------------- wgrad
@@ -440,7 +620,9 @@ __device__ __forceinline__ void wgrad_store(const ConvWgradArgs& a, const f32x4 
 // odd last tap (K*K = 9) runs the one-tap body over two splits' pixels, so every workgroup of
 // the grid does the same MFMA work; it writes its sum into the first split's slab and zeros
 // into the second's.
-template <int WN, int WC, int KSUB, int NWC, int TAPS>
+// NS > 2 (small batches): an NS-slot LDS ring instead of the double buffer (see conv_fwd_kernel);
+// only for geometries whose waves each stage exactly IPW pieces per stage (the vmcnt unit).
+template <int WN, int WC, int KSUB, int NWC, int TAPS, int NS = 2>
 __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, int ks_begin, int ks_end, int t,
                                            int tstep, int n0, int c0, int zero_split) {
   // 2 (n) x NWC (c) waves; NWC = 2 gives each wave a 96x96 tile at 192x192
@@ -559,14 +741,29 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
   const int tr1 = (16 + 4 * g + q) * 32 + p * 8;    // rows 16+4g..16+4g+3
   constexpr int NF = NBn + TAPS * NBc;  // fragments read per sub-step
 
-  if (ks_begin < ks_end) {
+  constexpr bool RING = NS > 2;
+  static_assert(!RING || (KSUB == 1 && (WN / 16) % IPW == 0 && NINSTR == NWAVES * IPW), "ring: uniform staging");
+  static_assert(!RING || IPW * (NS - 2) <= 63, "vmcnt range");
+  if constexpr (RING) {
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (ks_begin + s < ks_end) stage(ks_begin + s, s);
+  } else if (ks_begin < ks_end) {
     stage(ks_begin, 0);
     wait_vmcnt0();
     __syncthreads();
   }
   for (int ks = ks_begin; ks < ks_end; ++ks) {
-    const int cur = (ks - ks_begin) & 1;
-    if (ks + 1 < ks_end) stage(ks + 1, cur ^ 1);
+    int cur = (ks - ks_begin) & 1;
+    if constexpr (RING) {
+      const int later = (ks_end - 1 - ks) < (NS - 2) ? (ks_end - 1 - ks) : (NS - 2);
+      vmcnt_wait_dyn(later * IPW);
+      __syncthreads();  // stage ks visible to every wave; the slot read last step is free
+      cur = (ks - ks_begin) % NS;
+      if (ks + NS - 1 < ks_end) stage(ks + NS - 1, (ks - ks_begin + NS - 1) % NS);
+    } else if (ks + 1 < ks_end) {
+      stage(ks + 1, cur ^ 1);
+    }
 #pragma unroll
     for (int sub = 0; sub < KSUB; ++sub) {
       const char* base = smem + cur * STAGE + sub * SUB;
@@ -611,8 +808,10 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
         }
       }
     }
-    wait_vmcnt0();
-    __syncthreads();
+    if constexpr (!RING) {
+      wait_vmcnt0();
+      __syncthreads();
+    }
   }
 
   wgrad_store<WN, WC, NWC, TAPS>(a, acc, dbs, do_bias, split, t, n0, c0, wn, wc, lane, zero_split);
@@ -875,7 +1074,8 @@ __device__ __forceinline__ void wgrad_tile_line(const ConvWgradArgs& a, int spli
 }
 
 // LINE && !PAIR: two 8-wave workgroups per CU like the production per-tap kernel (<= 128 VGPRs)
-template <int WN, int WC, int KSUB, int NWC = 4, int TAPS = 1, bool PAIR = false, bool LINE = false, bool ILVW = false>
+template <int WN, int WC, int KSUB, int NWC = 4, int TAPS = 1, bool PAIR = false, bool LINE = false, bool ILVW = false,
+          int NS = 2>
 __global__ __launch_bounds__(128 * NWC, (LINE && !PAIR) ? 4 : 1) void conv_wgrad_kernel(ConvWgradArgs a) {
   static_assert(!PAIR || TAPS == 2, "PAIR: two taps per workgroup");
   // workgroup -> (split, tap group, channel block).  xcd_group (tap-merged rows): the hardware
@@ -923,7 +1123,7 @@ __global__ __launch_bounds__(128 * NWC, (LINE && !PAIR) ? 4 : 1) void conv_wgrad
     tstep = ((t1 / a.K - t / a.K) * a.HPi + (t1 % a.K - t % a.K)) * a.Cin;
   }
   if constexpr (LINE) wgrad_tile_line<WN, WC, KSUB, NWC, TAPS, ILVW>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
-  else wgrad_tile<WN, WC, KSUB, NWC, TAPS>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
+  else wgrad_tile<WN, WC, KSUB, NWC, TAPS, NS>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
 }
 
 constexpr int kWgradKsub = 1;

@@ -120,9 +120,10 @@ struct PackInputArgs {
 constexpr int kMaxPackLayers = 24;
 struct PackLayer {
   const float* w;  // OIHW fp32 [Cout_real][Cin_real][K][K]
-  __bf16* wf;      // [T][Cout_p][Cin_p]
+  __bf16* wf;      // [T][Cout_p][Cin_p]; pk_cpt > 0: [ceil(T * pk_cpt / 8)][Cout_p][64] (conv_fwd_pk_kernel)
   __bf16* wd;      // [T][Cin_p][Cout_p] flipped (dgrad) or null
   int Cout_real, Cin_real, Cout_p, Cin_p, K;
+  int pk_cpt;      // packed-tap first layer: 8-channel chunks per tap, else 0
 };
 struct PackWeightsArgs {
   PackLayer layers[kMaxPackLayers];
@@ -184,6 +185,8 @@ struct ConvFp8Args {
 // Kernel choices are explicit launch arguments (ConvFwdArgs::tile,
 // ConvWgradArgs::variant, ConvFp8Args::variant): no process-global state.
 void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
+// packed-tap first-layer forward (bias + ReLU, optional bitmask): cpt 8-channel chunks per tap
+void launch_conv_fwd_pk(const ConvFwdArgs& a, int cpt, hipStream_t st);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 int wgrad_tap_group(int Cout, int Cin, int K, int variant);  // taps per wgrad workgroup (tap-merged 64-wide c tiles)

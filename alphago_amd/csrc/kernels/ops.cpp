@@ -14,11 +14,21 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   check_dev("conv_fwd", x, w, bias, mask, y, mbits);
   // production tilings only: 0 = automatic, or a fixed 64 / 128 / 256 / 384-pixel tile (385: 384 with the
   // LDS-DMA issue spread through the MFMAs; 386 / 387: 385 / 384 with the chunk-outer K order)
-  TORCH_CHECK(tile == 0 || tile == 64 || tile == 128 || tile == 256 || tile == 384 || tile == 385 || tile == 386 ||
-                  tile == 387,
-              "conv_fwd tile ", tile, " is not a production tiling (0, 64, 128, 256, 384-387); kernel-lab variants are "
-              "in torch.ops.alphago_amd_lab (alphago_amd.ops.lab())");
+  TORCH_CHECK(tile == 0 || tile == 64 || tile == 65 || tile == 128 || tile == 130 || tile == 256 || tile == 384 ||
+                  tile == 385 || tile == 386 || tile == 387,
+              "conv_fwd tile ", tile, " is not a production tiling (0, 64, 65, 128, 130, 256, 384-387); kernel-lab "
+              "variants are in torch.ops.alphago_amd_lab (alphago_amd.ops.lab())");
   conv_fwd_impl(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, (int)tile);
+}
+
+// First layer on the packed-tap K loop (conv_fwd_pk_kernel): only the cin_real real input channels
+// of the 64-channel padded input are multiplied; w in the packed-tap layout (pack_weights detects it)
+void conv_fwd_pk(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& y, int64_t K, int64_t S,
+                 int64_t Pin, int64_t Po, int64_t cin_real, const c10::optional<Tensor>& mbits) {
+  check_dev("conv_fwd_pk", x, w, bias, y, mbits);
+  TORCH_CHECK(cin_real > 32 && cin_real <= 64, "conv_fwd_pk: 32 < cin_real <= 64");
+  conv_fwd_impl(x, w, bias, c10::nullopt, y, K, S, Pin, Po, agk::MODE_BIAS_RELU, mbits, 0, nullptr, -1, c10::nullopt,
+                c10::nullopt, c10::nullopt, (int)((cin_real + 7) / 8));
 }
 
 // slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
@@ -232,10 +242,15 @@ void pack_weights(at::TensorList ws, at::TensorList wf, at::TensorList wd) {
       L.Cout_real = (int)w.size(0); L.Cin_real = (int)w.size(1); L.K = (int)w.size(2);
       L.wf = bfp_mut(wf[i]);
       L.Cout_p = (int)wf[i].size(1); L.Cin_p = (int)wf[i].size(2);
-      // K*K taps, or K*K + 1 with a trailing all-zero tap (Cin % 64 == 32; never written here)
-      TORCH_CHECK((wf[i].size(0) == L.K * L.K || wf[i].size(0) == L.K * L.K + 1) && L.Cout_p >= L.Cout_real &&
+      // K*K taps, or K*K + 1 with a trailing all-zero tap (Cin % 64 == 32; never written here), or the
+      // packed-tap first-layer layout (conv_fwd_pk): ceil(K*K*cpt / 8) steps of 64, cpt = ceil(Cin / 8)
+      const int T = L.K * L.K, cpt = (L.Cin_real + 7) / 8;
+      L.pk_cpt = (wf[i].size(0) != T && wf[i].size(0) != T + 1 && L.Cin_p == 64 && L.Cin_real <= 64 &&
+                  wf[i].size(0) == (T * cpt + 7) / 8) ? cpt : 0;
+      TORCH_CHECK((wf[i].size(0) == T || wf[i].size(0) == T + 1 || L.pk_cpt > 0) && L.Cout_p >= L.Cout_real &&
                   L.Cin_p >= L.Cin_real, "bad wf");
       L.wd = nullptr;
+      TORCH_CHECK(L.pk_cpt == 0 || !(wd.size() && wd[i].numel() > 0), "packed-tap layout: no dgrad copy");
       if (wd.size() && wd[i].numel() > 0) {
         CHECK_BF16(wd[i]);
         TORCH_CHECK(wd[i].size(1) == L.Cin_p && wd[i].size(2) == L.Cout_p, "bad wd");
@@ -553,46 +568,6 @@ void dense_f32(const Tensor& A, const Tensor& B, const c10::optional<Tensor>& bi
   launch_check("dense_f32");
 }
 
-// Ladder planes from the compact board encoding: out (B, S*S) uint8, bit 0 =
-// ladder capture, bit 1 = ladder escape (the encoder's CPU ladder bits).
-void ladder_planes(const Tensor& board, const Tensor& meta, const Tensor& out, int64_t S, int64_t budget) {
-  check_dev("ladder_planes", board, meta, out);
-  CHECK_DEV(board); CHECK_DEV(meta); CHECK_DEV(out);
-  TORCH_CHECK(board.scalar_type() == at::kChar && board.dim() == 2 && board.size(1) == S * S && board.is_contiguous(),
-              "board int8 (B, S*S)");
-  TORCH_CHECK(meta.scalar_type() == at::kInt && meta.size(0) == board.size(0) && meta.is_contiguous(), "meta int32 (B, 2)");
-  TORCH_CHECK(out.scalar_type() == at::kByte && out.sizes() == board.sizes() && out.is_contiguous(), "out uint8 (B, S*S)");
-  TORCH_CHECK(S >= 2 && S <= 19, "board size 2..19");
-  const int64_t B = board.size(0);
-  if (B == 0) return;
-  auto i32 = board.options().dtype(at::kInt);
-  Tensor boards = at::empty({B, (int64_t)sizeof(agk::LadderBoard)}, board.options().dtype(at::kByte));
-  Tensor counts = at::empty({B + 1}, i32);  // [B] = search task counter
-  agk::LadderArgs a{};
-  a.board = board.data_ptr<int8_t>();
-  a.meta = meta.data_ptr<int32_t>();
-  a.boards = reinterpret_cast<agk::LadderBoard*>(boards.data_ptr<uint8_t>());
-  a.counts = counts.data_ptr<int32_t>();
-  a.out = out.data_ptr<uint8_t>();
-  a.B = (int)B;
-  a.S = (int)S;
-  TORCH_CHECK(budget > 0, "ladder budget must be positive");
-  a.budget = (int)budget;
-  a.counter = a.counts + B;
-  out.zero_();
-  counts.zero_();
-  agk::launch_ladder_prep(a, cur_stream());
-  launch_check("ladder_prep");
-  Tensor c = counts.narrow(0, 0, B);
-  Tensor offsets = (at::cumsum(c, 0, at::kInt) - c).contiguous();
-  a.offsets = offsets.data_ptr<int32_t>();
-  const int threads = (int)std::min<int64_t>(16384, B * 32);
-  Tensor frames = at::empty({(int64_t)threads * (int64_t)agk::ladder_frame_bytes()}, board.options().dtype(at::kByte));
-  a.frames = frames.data_ptr<uint8_t>();
-  agk::launch_ladder_search(a, threads, cur_stream());
-  launch_check("ladder_search");
-}
-
 // A deliberately invalid launch (2048 threads per block, above the 1024
 // limit): the runtime rejects it, launch_check turns that into a Python
 // RuntimeError -- the test of the error path every op shares.
@@ -617,6 +592,9 @@ void debug_conv_fwd_understated(const Tensor& x, const Tensor& w, const Tensor& 
 }  // namespace
 
 TORCH_LIBRARY(alphago_amd, m) {
+  m.def(
+      "conv_fwd_pk(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int K, int S, int Pin, int Po, int cin_real, "
+      "Tensor(b!)? mbits=None) -> ()");
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
       "Tensor(b!)? mbits=None, int tile=0) -> ()");
@@ -644,7 +622,6 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("sgd_update_sched(Tensor(a!) p, Tensor g, Tensor(b!) sched, float gscale) -> ()");
   m.def("dense_f32(Tensor A, Tensor B, Tensor? bias, Tensor(a!) C, bool transA, bool transB, float beta) -> ()");
   // budget: node visits per capture / escape read; 4096 = lb::kLadderVisits (ladder_bb.h)
-  m.def("ladder_planes(Tensor board, Tensor meta, Tensor(a!) out, int S, int budget=4096) -> ()");
   m.def(
       "featurize(Tensor board, Tensor ages, Tensor meta, Tensor? ladder, int[] fids, int[] fplanes, Tensor(a!)? planes, "
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
@@ -682,6 +659,7 @@ TORCH_LIBRARY(alphago_amd, m) {
 
 TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("conv_fwd", &conv_fwd);
+  m.impl("conv_fwd_pk", &conv_fwd_pk);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);
   m.impl("conv_dgrad_bits_bf8", &conv_dgrad_bits_bf8);
@@ -696,7 +674,6 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("comm_proxy", &comm_proxy);
   m.impl("sgd_update_sched", &sgd_update_sched);
   m.impl("dense_f32", &dense_f32);
-  m.impl("ladder_planes", &ladder_planes);
 #ifdef AGK_DEBUG
   m.impl("debug_conv_fwd_understated", &debug_conv_fwd_understated);
 #endif

@@ -68,7 +68,7 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
                           unsigned long long* dbg = nullptr, long long x_elems_override = -1,
                           const c10::optional<Tensor>& y_bf8 = c10::nullopt,
                           const c10::optional<Tensor>& bf8_scale = c10::nullopt,
-                          const c10::optional<Tensor>& bf8_amax = c10::nullopt) {
+                          const c10::optional<Tensor>& bf8_amax = c10::nullopt, int pk_cpt = 0) {
   check_dev("conv_fwd_impl", x, w, bias, mask, y, mbits, y_bf8, bf8_scale, bf8_amax);
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
   CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
@@ -78,9 +78,12 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
   const int64_t HPo = y.size(1), Cout = y.size(3);
   TORCH_CHECK(x.size(2) == HPi && y.size(2) == HPo && y.size(0) == B, "bad spatial dims");
   // Cin % 64 == 32 (straddled K-steps, 160-wide tile only): one extra all-zero weight tap
-  const int64_t taps = K * K + (Cin % 64 == 32 ? 1 : 0);
+  const int64_t taps = pk_cpt > 0 ? (K * K * pk_cpt + 7) / 8 : K * K + (Cin % 64 == 32 ? 1 : 0);
   TORCH_CHECK(w.size(0) == taps && w.size(1) == Cout && w.size(2) == Cin,
-              "w must be (K*K, Cout, Cin), or (K*K + 1, Cout, Cin) when Cin % 64 == 32");
+              "w must be (K*K, Cout, Cin), or (K*K + 1, Cout, Cin) when Cin % 64 == 32, or the packed-tap layout "
+              "(ceil(K*K*cpt/8), Cout, 64)");
+  TORCH_CHECK(pk_cpt == 0 || (Cin == 64 && mode == agk::MODE_BIAS_RELU && pk_cpt >= 4 && pk_cpt <= 8),
+              "packed-tap forward: 64-channel input, bias + ReLU, 32 < cin_real <= 64");
   TORCH_CHECK((Cout % 64 == 0 && Cin % 64 == 0) || (Cout == 160 && (Cin % 64 == 0 || Cin == 160)),
               "channels must be multiples of 64, or Cout 160 with Cin 160 / a multiple of 64");
   TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin && HPo == S + 2 * Po, "padding/geometry mismatch");
@@ -134,7 +137,8 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
     }
   }
   if (a.M == 0) return;
-  agk::launch_conv_fwd(a, (int)mode, cur_stream());
+  if (pk_cpt > 0) agk::launch_conv_fwd_pk(a, pk_cpt, cur_stream());
+  else agk::launch_conv_fwd(a, (int)mode, cur_stream());
   launch_check("conv_fwd");
 }
 

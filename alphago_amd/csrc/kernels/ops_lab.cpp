@@ -98,6 +98,47 @@ void tr8_probe(const Tensor& lds_init, const Tensor& addr, const Tensor& out) {
   launch_check("tr8_probe");
 }
 
+// GPU ladder reader (ladder.hip, kernel lab: 16x slower than the host reader, profiles/r2_gpu_ladders.md).
+// Ladder planes from the compact board encoding: out (B, S*S) uint8, bit 0 =
+// ladder capture, bit 1 = ladder escape (the encoder's CPU ladder bits).
+void ladder_planes(const Tensor& board, const Tensor& meta, const Tensor& out, int64_t S, int64_t budget) {
+  check_dev("ladder_planes", board, meta, out);
+  CHECK_DEV(board); CHECK_DEV(meta); CHECK_DEV(out);
+  TORCH_CHECK(board.scalar_type() == at::kChar && board.dim() == 2 && board.size(1) == S * S && board.is_contiguous(),
+              "board int8 (B, S*S)");
+  TORCH_CHECK(meta.scalar_type() == at::kInt && meta.size(0) == board.size(0) && meta.is_contiguous(), "meta int32 (B, 2)");
+  TORCH_CHECK(out.scalar_type() == at::kByte && out.sizes() == board.sizes() && out.is_contiguous(), "out uint8 (B, S*S)");
+  TORCH_CHECK(S >= 2 && S <= 19, "board size 2..19");
+  const int64_t B = board.size(0);
+  if (B == 0) return;
+  auto i32 = board.options().dtype(at::kInt);
+  Tensor boards = at::empty({B, (int64_t)sizeof(agk::LadderBoard)}, board.options().dtype(at::kByte));
+  Tensor counts = at::empty({B + 1}, i32);  // [B] = search task counter
+  agk::LadderArgs a{};
+  a.board = board.data_ptr<int8_t>();
+  a.meta = meta.data_ptr<int32_t>();
+  a.boards = reinterpret_cast<agk::LadderBoard*>(boards.data_ptr<uint8_t>());
+  a.counts = counts.data_ptr<int32_t>();
+  a.out = out.data_ptr<uint8_t>();
+  a.B = (int)B;
+  a.S = (int)S;
+  TORCH_CHECK(budget > 0, "ladder budget must be positive");
+  a.budget = (int)budget;
+  a.counter = a.counts + B;
+  out.zero_();
+  counts.zero_();
+  agk::launch_ladder_prep(a, cur_stream());
+  launch_check("ladder_prep");
+  Tensor c = counts.narrow(0, 0, B);
+  Tensor offsets = (at::cumsum(c, 0, at::kInt) - c).contiguous();
+  a.offsets = offsets.data_ptr<int32_t>();
+  const int threads = (int)std::min<int64_t>(16384, B * 32);
+  Tensor frames = at::empty({(int64_t)threads * (int64_t)agk::ladder_frame_bytes()}, board.options().dtype(at::kByte));
+  a.frames = frames.data_ptr<uint8_t>();
+  agk::launch_ladder_search(a, threads, cur_stream());
+  launch_check("ladder_search");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(alphago_amd_lab, m) {
@@ -114,6 +155,7 @@ TORCH_LIBRARY(alphago_amd_lab, m) {
   m.def("bf8_convert_probe(Tensor x, Tensor(a!) y, float scale, int mode) -> ()");
   m.def("wino_fwd(Tensor x, Tensor u, Tensor? bias, Tensor(a!) y, int S) -> ()");
   m.def("tr8_probe(Tensor lds_init, Tensor addr, Tensor(a!) out) -> ()");
+  m.def("ladder_planes(Tensor board, Tensor meta, Tensor(a!) out, int S, int budget=4096) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {
@@ -123,4 +165,5 @@ TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {
   m.impl("conv_fwd", &conv_fwd_lab);
   m.impl("conv_wgrad", &conv_wgrad_lab);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8_lab);
+  m.impl("ladder_planes", &ladder_planes);
 }

@@ -83,6 +83,22 @@ void launch_pack_input(const PackInputArgs& a, hipStream_t st) {
 __global__ void pack_weights_kernel(PackWeightsArgs a) {
   const PackLayer L = a.layers[blockIdx.y];
   const int T = L.K * L.K;
+  if (L.pk_cpt > 0) {  // packed-tap first layer: [step][Cout_p][64], chunk j of step s = q = 8 s + j
+    const int nst = (T * L.pk_cpt + 7) >> 3;
+    const int tot = nst * L.Cout_p * 64;
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += gridDim.x * blockDim.x) {
+      const int k = idx & 63;
+      const int rest = idx >> 6;
+      const int n = rest % L.Cout_p;
+      const int q = (rest / L.Cout_p) * 8 + (k >> 3);
+      const int t = q / L.pk_cpt;
+      const int c = (q - t * L.pk_cpt) * 8 + (k & 7);
+      float v = 0.f;
+      if (t < T && n < L.Cout_real && c < L.Cin_real) v = L.w[((size_t)n * L.Cin_real + c) * T + t];
+      L.wf[idx] = (__bf16)v;
+    }
+    return;
+  }
   const int total = T * L.Cout_p * L.Cin_p;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     const int c = idx % L.Cin_p;
@@ -106,7 +122,7 @@ void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st) {
   int maxtot = 0;
   for (int i = 0; i < a.nlayers; ++i) {
     const PackLayer& L = a.layers[i];
-    const int tot = L.K * L.K * L.Cout_p * L.Cin_p;
+    const int tot = L.pk_cpt > 0 ? ((L.K * L.K * L.pk_cpt + 7) / 8) * L.Cout_p * 64 : L.K * L.K * L.Cout_p * L.Cin_p;
     if (tot > maxtot) maxtot = tot;
   }
   int blocks = (maxtot + 255) / 256;

@@ -55,7 +55,10 @@ class HipTrunkInference:
         self.use_graphs = use_graphs
         dev = self.device
         # packed on the engine's device whatever device the module's parameters are on
-        self.wf = [ops.packed_weight_like(tr.weights[l], self.C0p if l == 0 else self.Fp, self.Fp, device=dev)
+        # first layer on the packed-tap forward when it applies (ops.conv_fwd_pk: real input planes only)
+        self.pk0 = ops.pk_applies(self.C0, self.C0p)
+        self.wf = [ops.packed_weight_pk(tr.weights[0], self.Fp, device=dev) if l == 0 and self.pk0 else
+                   ops.packed_weight_like(tr.weights[l], self.C0p if l == 0 else self.Fp, self.Fp, device=dev)
                    for l in range(self.L)]
         self.bias_p = [torch.zeros(self.Fp, device=dev) for _ in range(self.L)]
         self.head_w = torch.zeros(self.F, device=dev)
@@ -170,7 +173,10 @@ class HipTrunkInference:
         x, pin = bk.X0, self.P0
         for l in range(self.L):
             y = bk.Y[l % 2]
-            ops.conv_fwd(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1)
+            if l == 0 and self.pk0:
+                ops.conv_fwd_pk(x, self.wf[0], self.bias_p[0], y, self.K[0], self.S, pin, 1, self.C0)
+            else:
+                ops.conv_fwd(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1)
             if getattr(self, "_calibrating", False):
                 self._cal_amax[l] = max(self._cal_amax[l], float(y.amax()))
             x, pin = y, 1
@@ -299,6 +305,11 @@ class HipTrunkInference:
             return bk.h_out[:n].numpy(), bk.h_mask[:n].numpy(), bad
         bad = torch.nonzero(bk.ovf[:n]).flatten().tolist()
         return self._outputs(bk, n), bk.legal[:n], bad
+
+    def outputs(self, handle):
+        """Device views (outputs (n, ...), sensible mask (n, S*S) uint8) of a submission, no waiting."""
+        bk, n, _ = handle
+        return self._outputs(bk, n), bk.legal[:n]
 
     @torch.no_grad()
     def evaluate_encoded(self, board, ages, meta, ladder=None, slot: int = 0):

@@ -131,6 +131,28 @@ def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: 
     return y
 
 
+def pk_applies(cin_real: int, cin_p: int) -> bool:
+    """Whether a first layer runs on the packed-tap forward (conv_fwd_pk): 32 < cin_real < 64 real input
+    channels in a 64-channel padded input (48 policy / 49 value planes)."""
+    return cin_p == 64 and 32 < cin_real < 64 and os.environ.get("ALPHAGO_AMD_PK", "1") == "1"
+
+
+def packed_weight_pk(w_oihw: torch.Tensor, cout_p: int, device=None) -> torch.Tensor:
+    """Zeroed packed-tap weights (ceil(K*K*cpt/8), Cout, 64), cpt = ceil(cin_real/8); pack_weights fills
+    them (chunk j of step s = tap (8s + j) // cpt, channels 8 ((8s + j) % cpt) ..)."""
+    K, cin = w_oihw.shape[2], w_oihw.shape[1]
+    cpt = (cin + 7) // 8
+    return torch.zeros(((K * K * cpt + 7) // 8, cout_p, 64), device=w_oihw.device if device is None else device,
+                       dtype=torch.bfloat16)
+
+
+def conv_fwd_pk(x, w_pk, bias, y, K: int, S: int, Pin: int, Po: int, cin_real: int, mbits=None):
+    """First layer (bias + ReLU, optional ReLU' bitmask) on the packed-tap K loop: only the cin_real real
+    channels of the 64-channel padded input are multiplied (48 planes: 19 K-steps instead of 25)."""
+    _ops().conv_fwd_pk(x, w_pk, bias, y, K, S, Pin, Po, cin_real, mbits)
+    return y
+
+
 def mbits_words(cout_p: int) -> int:
     """32-bit ReLU'-bitmask words per padded pixel for a conv with cout_p output channels."""
     return cout_p // conv_n_tile(cout_p) * 8
@@ -199,7 +221,7 @@ def ladder_planes(board, meta, out, S: int, budget: int = 0):
         from .._native import engine
 
         budget = engine().ladder_budget()
-    _ops().ladder_planes(board, meta, out, S, budget)
+    lab().ladder_planes(board, meta, out, S, budget)  # kernel lab (ladder.hip: slower than the host reader)
     return out
 
 
@@ -248,6 +270,27 @@ def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
     # 3-stage splits spends its time writing a 75-MB slab that the reduce then reads back
     # (B = 16: 16.6 us wgrad + 16.3 us reduce per layer, profiles/r3_small_batch.md)
     return max(1, min(target // per_split, nks // WGRAD_MIN_STAGES if target_wgs <= 0 else nks))
+
+
+# small batches (round 4): where the min-stages rule leaves the grid short of one workgroup per CU,
+# the per-tap kernel runs on a 4-slot LDS ring (variant 9) with longer splits: the slab it writes
+# and the reduce reads shrink with the split count, and the ring hides the DMA latency that bounds
+# a short split
+WGRAD_RING_STAGES = int(os.environ.get("ALPHAGO_AMD_RING_STAGES", "16"))
+
+
+def wgrad_config(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, target_wgs: int = 0, cus: int = 256,
+                 variant: int = 0):
+    """(variant, nsplit) of a layer's wgrad: the requested variant and wgrad_nsplit, or at small
+    batches (variant 0, no explicit target) the ring variant 9 with WGRAD_RING_STAGES per split."""
+    ns = wgrad_nsplit(M, cout_p, cin_p, K, cin_real, target_wgs, cus, variant)
+    if variant != 0 or target_wgs > 0 or os.environ.get("ALPHAGO_AMD_WGRAD_RING", "1") == "0":
+        return variant, ns
+    taps, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, 0)
+    if taps != 1 or ns * per_split > cus:
+        return variant, ns
+    nks = (M + 31) // 32
+    return 9, max(1, min(cus // per_split, nks // WGRAD_RING_STAGES))
 
 
 def wgrad_splits(M: int, T: int, n_tiles: int = 1, target_wgs: int = 512) -> int:

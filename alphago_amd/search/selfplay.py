@@ -60,6 +60,18 @@ class BatchedSampler(object):
             sens[bad] = torch.from_numpy(masks).to(sens.device)
         return probs, (sens != 0).any(1)
 
+    def sample_device(self, probs: torch.Tensor, has: torch.Tensor) -> torch.Tensor:
+        """Flat move per board on the probs' device: argmax, or a sample of p**(1/T) (ai.py:37-49);
+        -1 (pass) where no sensible move exists.  No host synchronisation."""
+        if self.greedy:
+            idx = probs.argmax(1)
+        else:
+            p = probs.clamp_min(0) ** self.beta if self.beta != 1.0 else probs.clamp_min(0)
+            p = torch.where(has.unsqueeze(1), p, torch.ones_like(p))
+            p = p / p.sum(1, keepdim=True).clamp_min(1e-30)
+            idx = torch.multinomial(p, 1, generator=self.gen).squeeze(1)
+        return torch.where(has, idx, torch.full_like(idx, -1))
+
     def device_planes_ok(self) -> bool:
         """The engine featurises on the device and can hand its uint8 planes back (HIP engines)."""
         eng = self.policy.engine
@@ -93,14 +105,7 @@ class BatchedSampler(object):
             masks = self.masks(states)
             probs = eng.evaluate(planes, masks)
             has = torch.from_numpy(masks.any(axis=1)).to(probs.device)
-        if self.greedy:
-            idx = probs.argmax(1)
-        else:
-            p = probs.clamp_min(0) ** self.beta if self.beta != 1.0 else probs.clamp_min(0)
-            p = torch.where(has.unsqueeze(1), p, torch.ones_like(p))
-            p = p / p.sum(1, keepdim=True).clamp_min(1e-30)
-            idx = torch.multinomial(p, 1, generator=self.gen).squeeze(1)
-        idx = torch.where(has, idx, torch.full_like(idx, -1)).cpu().numpy()
+        idx = self.sample_device(probs, has).cpu().numpy()
         moves = [go.PASS_MOVE if i < 0 else (int(i) // size, int(i) % size) for i in idx]
         return moves, planes, idx
 
@@ -145,7 +150,8 @@ class _DeviceRecordBuffer(object):
 def play_games(learner: BatchedSampler, opponent: BatchedSampler, n_games: int, size: int = 19,
                komi: float = 7.5, max_moves: int = 500, rng: Optional[np.random.Generator] = None,
                record: bool = True, learner_colors: Optional[Sequence[int]] = None,
-               standard_two_pass: bool = False, device_records: Optional[bool] = None) -> GameRecords:
+               standard_two_pass: bool = False, device_records: Optional[bool] = None,
+               native: Optional[bool] = None) -> GameRecords:
     """Play n_games learner-vs-opponent games in lock-step (reference
     make_training_pairs, reinforcement_policy_trainer.py:16-76).  The learner's
     colour is drawn per game and its training pairs use the state
@@ -155,7 +161,16 @@ def play_games(learner: BatchedSampler, opponent: BatchedSampler, n_games: int, 
     ``device_records`` (default: whenever the learner's engine featurises on the GPU): the
     learner's planes are the GPU featurizer's own output of the sampling forward, copied into a
     device buffer -- no host featurisation, numpy round trip or re-upload; ``GameRecords.planes``
-    then holds one device tensor per game."""
+    then holds one device tensor per game.
+
+    ``native`` (default: whenever both engines featurise on the GPU): the pipelined native driver
+    (search/lockstep.py); False keeps this Python loop (CPU engines, and the equality tests)."""
+    from .lockstep import lockstep_ok, play_games_lockstep
+    if native is None:
+        native = lockstep_ok(learner, opponent)
+    if native:
+        return play_games_lockstep(learner, opponent, n_games, size, komi, max_moves, rng, record, learner_colors,
+                                   standard_two_pass, device_records)
     rng = rng or np.random.default_rng()
     states = [go.GameState(size, komi, standard_two_pass) for _ in range(n_games)]
     colors = list(learner_colors) if learner_colors is not None else \

@@ -170,10 +170,13 @@ class HipConvTrainer:
         self.bias_p = ([self.fp.views["b%d" % l] for l in range(self.L)] if self._bias_alias
                        else [torch.zeros(self.Fp, device=dev) for _ in range(self.L)])
         self.wf, self.wd = [], []
+        # first layer on the packed-tap forward: only the real input planes are multiplied (conv_fwd_pk)
+        self.pk0 = ops.pk_applies(self.C0, self.C0p)
         for l in range(self.L):
             cin_p = self.C0p if l == 0 else self.Fp
             w = self.fp.views["w%d" % l]
-            self.wf.append(ops.packed_weight_like(w, cin_p, self.Fp))
+            self.wf.append(ops.packed_weight_pk(w, self.Fp) if l == 0 and self.pk0 else
+                           ops.packed_weight_like(w, cin_p, self.Fp))
             self.wd.append(ops.packed_weight_like(w, cin_p, self.Fp, transposed=True) if l > 0
                            else torch.empty(0, device=dev, dtype=torch.bfloat16))
         # activations / gradients (zero borders are never written)
@@ -188,14 +191,17 @@ class HipConvTrainer:
         self.correct = torch.zeros(B, device=dev)
         M = B * S * S
         self.nsplit = []
+        self.wgrad_var = []
         slab_max, db_max = 0, 0
         for l in range(self.L):
             cin_p = self.C0p if l == 0 else self.Fp
             T = self.K[l] ** 2
-            # one resident round of wgrad workgroups (the kernel's own occupancy, ops.wgrad_plan)
-            ns = ops.wgrad_nsplit(M, self.Fp, cin_p, self.K[l], self.C0 if l == 0 else 0, wgrad_target_wgs,
-                                  self._num_cus(), self.wgrad_variant)
+            # one resident round of wgrad workgroups (the kernel's own occupancy, ops.wgrad_plan); small
+            # batches: the LDS-ring variant with longer splits (ops.wgrad_config)
+            var, ns = ops.wgrad_config(M, self.Fp, cin_p, self.K[l], self.C0 if l == 0 else 0, wgrad_target_wgs,
+                                       self._num_cus(), self.wgrad_variant)
             self.nsplit.append(ns)
+            self.wgrad_var.append(var)
             slab_max = max(slab_max, ns * T * self.Fp * cin_p)
             db_max = max(db_max, ns * self.Fp)
         # Split-K reduce on a side stream (serial backward only): the memory-bound reduce of
@@ -369,9 +375,16 @@ class HipConvTrainer:
             self._forward_fp8()
             return
         for l in range(self.L):
-            x, pin = self._layer_in(l)
-            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1,
-                         mbits=self.MBITS[l] if l < self.L - 1 else None, tile=self.conv_tile)
+            self._fwd_layer(l, self.MBITS[l] if l < self.L - 1 else None)
+
+    def _fwd_layer(self, l: int, mbits=None) -> None:
+        """bf16 forward of layer l into Y[l] (the first layer on the packed-tap kernel when it applies)."""
+        x, pin = self._layer_in(l)
+        if l == 0 and self.pk0:
+            ops.conv_fwd_pk(x, self.wf[0], self.bias_p[0], self.Y[0], self.K[0], self.S, pin, 1, self.C0, mbits)
+        else:
+            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1, mbits=mbits,
+                         tile=self.conv_tile)
 
     def _forward_fp8(self) -> None:
         ops.quantize_fp8(self.X0, self.X08, 0)  # binary planes: exact
@@ -396,8 +409,7 @@ class HipConvTrainer:
         """First step: activation scales from a bf16 forward of this batch."""
         amax = []
         for l in range(self.L):
-            x, pin = self._layer_in(l)
-            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1)
+            self._fwd_layer(l)
             amax.append(self.Y[l].amax().float())
         self.amax8.zero_()
         self.amax8[:, 0].copy_(torch.stack(amax).view(torch.int32))
@@ -432,7 +444,7 @@ class HipConvTrainer:
                                amax=self.gamax8[l] if l < self.L - 1 else None)
         else:
             ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0,
-                           variant=self.wgrad_variant)
+                           variant=self.wgrad_var[l])
 
         def reduce():
             ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)

@@ -49,13 +49,19 @@ DECAY = 8.664339379294006e-08
 
 def generate_positions(sl_policy: CNNPolicy, rl_policy: CNNPolicy, n_games: int, size: int = 19,
                        max_u: int = 450, max_moves: int = 600, temperature: float = 1.0, seed: int = 0,
-                       features: Optional[List[str]] = None):
-    """Returns (planes uint8 (N, F, S, S), outcomes int8 (N,)) with N <= n_games."""
+                       features: Optional[List[str]] = None, native: Optional[bool] = None):
+    """Returns (planes uint8 (N, F, S, S), outcomes int8 (N,)) with N <= n_games.  With GPU engines the
+    games run on the pipelined native driver (search/lockstep.py); ``native=False`` keeps this loop."""
     rng = np.random.default_rng(seed)
     feats = Preprocess(features or VALUE_FEATURES)
     sl = BatchedSampler(sl_policy, temperature, seed=seed)
     rl = BatchedSampler(rl_policy, temperature, seed=seed + 1)
     U = rng.integers(1, max_u + 1, size=n_games)
+    from ..search.lockstep import generate_value_positions_lockstep, lockstep_ok
+    if native is None:
+        native = lockstep_ok(sl, rl)
+    if native:
+        return generate_value_positions_lockstep(sl, rl, n_games, size, U, max_moves, feats.feature_list, seed)
     states = [go.GameState(size) for _ in range(n_games)]
     recorded = [None] * n_games
     rec_player = [0] * n_games

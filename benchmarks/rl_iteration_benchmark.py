@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--minibatch", type=int, default=256)
     ap.add_argument("--max-moves", type=int, default=500)
     ap.add_argument("--records", default="host,device")
+    ap.add_argument("--drivers", default="native,python",
+                    help="native: the pipelined native lock-step driver (search/lockstep.py); python: the round-3 loop")
     a = ap.parse_args()
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
     torch.manual_seed(0)
@@ -40,13 +42,16 @@ def main():
     opp = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=a.filters, layers=a.layers, device=dev)
     opp.model.load_state_dict(learner.model.state_dict())
     trainer = make_policy_trainer(learner.model, a.minibatch, 0.001, 0.0, device=dev)
+    arms = [(d, m) for d in a.drivers.split(",") for m in a.records.split(",")]
     for g in [int(x) for x in a.games.split(",")]:
-        for mode in a.records.split(","):
+        for driver, mode in arms:
+            nat = driver == "native"
             ls = BatchedSampler(learner, 1.0, seed=1)
             os_ = BatchedSampler(opp, 1.0, seed=2)
             rng = np.random.default_rng(3)
             # warm-up iteration (graph captures for the batch sizes, code objects)
-            rec = play_games(ls, os_, g, max_moves=a.max_moves, rng=rng, device_records=(mode == "device"))
+            rec = play_games(ls, os_, g, max_moves=a.max_moves, rng=rng, device_records=(mode == "device"),
+                             native=nat)
             rl_update(trainer, rec, a.minibatch, dev)
             learner.refresh()
             if dev.type == "cuda":
@@ -55,7 +60,8 @@ def main():
             games = positions = moves = 0
             for _ in range(a.iterations):
                 t0 = time.perf_counter()
-                rec = play_games(ls, os_, g, max_moves=a.max_moves, rng=rng, device_records=(mode == "device"))
+                rec = play_games(ls, os_, g, max_moves=a.max_moves, rng=rng, device_records=(mode == "device"),
+                                 native=nat)
                 if dev.type == "cuda":
                     torch.cuda.synchronize()
                 t1 = time.perf_counter()
@@ -70,7 +76,7 @@ def main():
                 positions += info["positions"]
                 moves += sum(rec.lengths)
             tot = t_play + t_upd
-            print(json.dumps({"games_per_iteration": g, "records": mode, "iterations": a.iterations,
+            print(json.dumps({"games_per_iteration": g, "driver": driver, "records": mode, "iterations": a.iterations,
                               "games_per_s": round(games / tot, 2), "learner_positions_per_s": round(positions / tot, 1),
                               "moves_per_s": round(moves / tot, 1), "play_s_per_it": round(t_play / a.iterations, 3),
                               "update_s_per_it": round(t_upd / a.iterations, 3),

@@ -66,6 +66,16 @@ def _heldout_top1(model_json, weights, h5, dev):
     return float((probs.argmax(1) == tgt).mean()), int(len(tgt))
 
 
+def _uniform_baseline(h5):
+    """Expected top-1 of a uniform pick over the sensible moves (the 'sensibleness' plane of
+    DEFAULT_FEATURES: legal and not filling an own eye) -- the floor a trained net must beat."""
+    from alphago_amd.io.h5lite import H5File
+    planes = np.asarray(H5File(h5)["states"].read())
+    sens = planes[:, 46].reshape(len(planes), -1)  # 48 planes: ..., sensibleness (46), zeros (47)
+    n = sens.sum(1).clip(min=1)
+    return float((1.0 / n).mean())
+
+
 ARMS = {"hip-bf16": ["--backend", "hip"], "hip-fp8fwd": ["--backend", "hip", "--precision", "fp8"],
         "torch-fp32": ["--backend", "torch"]}
 
@@ -80,6 +90,11 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--arms", default="hip-bf16",
                     help="comma list of %s: the same data, student init and seeds per arm" % ",".join(ARMS))
+    ap.add_argument("--real-seeds", type=int, default=1,
+                    help="student initialisations / data orders averaged in the real-move check")
+    ap.add_argument("--real-batch", type=int, default=32)
+    ap.add_argument("--real-lr", type=float, default=0.0, help="real-move lr (0: --lr)")
+    ap.add_argument("--real-only", action="store_true", help="skip the teacher task (real-move check only)")
     ap.add_argument("--real-epochs", type=int, default=0,
                     help=">0: also train each arm on 4 reference Lee Sedol games and report held-out top-1 on the "
                          "fifth (real moves)")
@@ -90,21 +105,23 @@ def main():
     F, L = (16, 3) if small else (192, 12)
     rng = np.random.default_rng(a.seed)
     t0 = time.perf_counter()
-    torch.manual_seed(1000 + a.seed)
-    teacher = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
     h5 = os.path.join(a.out, "teacher.h5")
-    with H5Writer(h5) as f:
-        f.attrs["features"] = np.array([x.encode() for x in DEFAULT_FEATURES])
-        f.attrs["board_size"] = np.int64(19)
-        states_ds = f.stream_dataset("states", (teacher.preprocessor.output_dim, 19, 19), np.uint8)
-        from alphago_amd.data.synthetic import teacher_pool
-        planes, idx = teacher_pool(a.positions, teacher, seed=a.seed, symmetrize=False)
-        states_ds.append(planes)
-        states_ds.finish()
-        acts = np.stack([idx // 19, idx % 19], axis=1).astype(np.uint8)
-        f.create_dataset("actions", data=acts)
-        f.create_group("file_offsets")["synthetic"] = np.array([0, len(acts)], dtype=np.int64)
-    del teacher
+    acts = np.zeros((0, 2))
+    if not a.real_only:
+        torch.manual_seed(1000 + a.seed)
+        teacher = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
+        with H5Writer(h5) as f:
+            f.attrs["features"] = np.array([x.encode() for x in DEFAULT_FEATURES])
+            f.attrs["board_size"] = np.int64(19)
+            states_ds = f.stream_dataset("states", (teacher.preprocessor.output_dim, 19, 19), np.uint8)
+            from alphago_amd.data.synthetic import teacher_pool
+            planes, idx = teacher_pool(a.positions, teacher, seed=a.seed, symmetrize=False)
+            states_ds.append(planes)
+            states_ds.finish()
+            acts = np.stack([idx // 19, idx % 19], axis=1).astype(np.uint8)
+            f.create_dataset("actions", data=acts)
+            f.create_group("file_offsets")["synthetic"] = np.array([0, len(acts)], dtype=np.int64)
+        del teacher
     t_data = time.perf_counter() - t0
     real = _real_games(a.out, DEFAULT_FEATURES) if a.real_epochs > 0 else None
     results = {}
@@ -115,26 +132,34 @@ def main():
         student.save_model(model_json)
         run_dir = os.path.join(a.out, "run_" + arm)
         t1 = time.perf_counter()
-        run_training([model_json, h5, run_dir, "--minibatch", str(a.batch), "--epochs", str(a.epochs),
-                      "--learning-rate", str(a.lr), "--decay", "0", "--no-symmetries", "--seed", str(a.seed)]
-                     + ARMS[arm])
-        ep = json.load(open(os.path.join(run_dir, "metadata.json")))["epochs"]
-        res = {"acc": [round(e.get("acc", 0), 4) for e in ep], "val_acc": [round(e.get("val_acc", 0), 4) for e in ep],
-               "train_s": round(time.perf_counter() - t1, 1)}
+        res = {}
+        if not a.real_only:
+            run_training([model_json, h5, run_dir, "--minibatch", str(a.batch), "--epochs", str(a.epochs),
+                          "--learning-rate", str(a.lr), "--decay", "0", "--no-symmetries", "--seed", str(a.seed)]
+                         + ARMS[arm])
+            ep = json.load(open(os.path.join(run_dir, "metadata.json")))["epochs"]
+            res = {"acc": [round(e.get("acc", 0), 4) for e in ep],
+                   "val_acc": [round(e.get("val_acc", 0), 4) for e in ep],
+                   "train_s": round(time.perf_counter() - t1, 1)}
         if real is not None:
-            torch.manual_seed(3000 + a.seed)
-            stu = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
-            rj = os.path.join(a.out, "real_student_%s.json" % arm)
-            stu.save_model(rj)
-            rdir = os.path.join(a.out, "real_" + arm)
-            run_training([rj, real[0], rdir, "--minibatch", "32", "--epochs", str(a.real_epochs),
-                          "--learning-rate", str(a.lr), "--decay", "0", "--seed", str(a.seed),
-                          "--train-val-test", "1.0", "0.0", "0.0"] + ARMS[arm])
-            w = os.path.join(rdir, "weights.%05d.hdf5" % (a.real_epochs - 1))
-            top1, n = _heldout_top1(rj, w, real[1], dev)
-            res["real_heldout_top1"] = round(top1, 4)
+            tops = []
+            for rs in range(a.real_seeds):
+                torch.manual_seed(3000 + a.seed + rs)  # the same initialisation per seed in every arm
+                stu = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=F, layers=L, device=dev)
+                rj = os.path.join(a.out, "real_student_%s_%d.json" % (arm, rs))
+                stu.save_model(rj)
+                rdir = os.path.join(a.out, "real_%s_%d" % (arm, rs))
+                run_training([rj, real[0], rdir, "--minibatch", str(a.real_batch), "--epochs", str(a.real_epochs),
+                              "--learning-rate", str(a.real_lr or a.lr), "--decay", "0", "--seed",
+                              str(a.seed + rs), "--train-val-test", "1.0", "0.0", "0.0"] + ARMS[arm])
+                w = os.path.join(rdir, "weights.%05d.hdf5" % (a.real_epochs - 1))
+                top1, n = _heldout_top1(rj, w, real[1], dev)
+                tops.append(round(top1, 4))
+            res["real_heldout_top1"] = round(float(np.mean(tops)), 4)
+            res["real_heldout_top1_per_seed"] = tops
             res["real_heldout_positions"] = n
             res["real_heldout_game"] = real[2]
+            res["real_uniform_sensible_baseline"] = round(_uniform_baseline(real[1]), 4)
         results[arm] = res
     print(json.dumps({"metric": "SL top-1 agreement with a random-init teacher policy (held-out)",
                       "positions": int(len(acts)), "epochs": a.epochs, "minibatch": a.batch, "lr": a.lr,

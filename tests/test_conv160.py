@@ -32,7 +32,7 @@ def test_padding_helpers(ops):
     assert ops.packed_weight_like(torch.zeros(152, 49, 5, 5), 64, 160).shape == (25, 160, 64)
 
 
-@pytest.mark.parametrize("tile", [0, 64, 128, 256, 384, 385, 386, 387])
+@pytest.mark.parametrize("tile", [0, 64, 65, 128, 130, 256, 384, 385, 386, 387])
 @pytest.mark.parametrize("B,Cin,Cin_p,K", [(5, 152, 160, 3), (3, 49, 64, 5), (1, 152, 160, 3)])
 def test_conv_fwd_160(ops, cuda_device, tile, B, Cin, Cin_p, K):
     torch.manual_seed(0)
@@ -56,7 +56,7 @@ def test_conv_fwd_160(ops, cuda_device, tile, B, Cin, Cin_p, K):
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", [0, 64, 128, 384, 385, 386, 387])
+@pytest.mark.parametrize("tile", [0, 64, 65, 130, 128, 384, 385, 386, 387])
 def test_conv_dgrad_160_bitmask(ops, cuda_device, tile):
     """dgrad with transposed 160-wide weights and the ReLU' bitmask written by
     the forward epilogue == conv2d_input * (y > 0)."""
@@ -88,7 +88,7 @@ def test_conv_dgrad_160_bitmask(ops, cuda_device, tile):
     assert out[:, C:].abs().sum() == 0
 
 
-@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("variant", [0, 9, pytest.param(5, marks=pytest.mark.lab)])
 @pytest.mark.parametrize("B,Cin,Cin_p,K,Pin", [(6, 152, 160, 3, 1), (5, 49, 64, 5, 2), (3, 152, 160, 3, 1)])
 def test_conv_wgrad_160(ops, cuda_device, B, Cin, Cin_p, K, Pin, variant):
     """variant 0: per-tap 160x160 / tap-merged 160x64 kernels; 5: the one-kernel-row wgrad."""
@@ -105,7 +105,10 @@ def test_conv_wgrad_160(ops, cuda_device, B, Cin, Cin_p, K, Pin, variant):
     ns = ops.wgrad_splits(B * S * S, K * K // taps)
     slab = torch.full((ns, K * K, Cp, Cin_p), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, Cp, device=cuda_device)
-    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin if Cin_p == 64 else 0, variant=variant)
+    if variant == 5:  # the one-kernel-row wgrad: kernel lab
+        ops.lab().conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, Cin if Cin_p == 64 else 0, variant)
+    else:
+        ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin if Cin_p == 64 else 0, variant=variant)
     gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
     gb = torch.zeros(Cout, device=cuda_device)
     ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)

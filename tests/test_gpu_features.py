@@ -287,6 +287,7 @@ def test_ladder_node_budget_same_in_both_readers():
 
 
 @pytest.mark.gpu
+@pytest.mark.lab
 def test_gpu_ladder_planes_match_cpu(cuda_device):
     """ladder_planes (csrc/kernels/ladder.hip) on >= 1000 random 19x19 positions
     and on 9x9 / 13x13 boards: bit-equal to the CPU ladder reader."""
@@ -312,6 +313,7 @@ def test_gpu_ladder_planes_match_cpu(cuda_device):
 
 
 @pytest.mark.gpu
+@pytest.mark.lab
 def test_gpu_featurizer_device_ladders(cuda_device):
     """GpuFeaturizer(gpu_ladders=True): ladder planes read on the device equal
     the CPU featurizer's, including the deep eye-chain positions."""

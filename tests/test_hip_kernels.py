@@ -4,6 +4,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from _marks import LAB, lab_params
+
 pytestmark = pytest.mark.gpu
 
 
@@ -19,7 +21,7 @@ def _bf(x):
     return x.to(torch.bfloat16).float()
 
 
-PROD_TILES = (0, 128, 256, 384, 385, 386, 387)
+PROD_TILES = (0, 64, 65, 128, 130, 256, 384, 385, 386, 387)
 
 
 def _conv_fwd(ops, tile, x, w, bias, y, K, S, Pin, Po=1, mode=0, mask=None, mbits=None):
@@ -92,7 +94,7 @@ def test_conv_dgrad_with_relu_mask(ops, cuda_device, B, C, K):
     assert _rel_err(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 5, 6, 7, 8, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", lab_params([0, 9, 5, 6, 7, 8, 1, 2, 3, 4], (0, 9)))
 @pytest.mark.parametrize("B,Cin,Cout,K,Pin,nsplit", [(6, 192, 192, 3, 1, None), (5, 64, 192, 5, 2, None),
                                                     (3, 64, 64, 3, 1, None), (9, 128, 128, 3, 1, None),
                                                     (7, 192, 192, 3, 1, 1), (4, 192, 192, 3, 1, 3),
@@ -114,8 +116,8 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     ns = nsplit or ops.wgrad_splits(M, K * K)
     slab = torch.full((ns, K * K, Cout, Cin), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, Cout, device=cuda_device)
-    if variant == 0:
-        ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1)
+    if variant in (0, 9):  # production: per-tap kernel, 9 = its small-batch LDS ring
+        ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, variant=variant)
     else:  # kernel-lab variants
         ops.lab().conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, 0, variant)
     gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
@@ -129,22 +131,24 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
 @pytest.mark.parametrize("S,B,Cin,Cin_real,Cout,K,Pin", [(9, 13, 192, 192, 192, 3, 1), (13, 6, 192, 192, 192, 3, 1),
                                                          (9, 7, 64, 48, 192, 5, 2), (13, 3, 64, 48, 128, 5, 2),
                                                          (19, 1, 128, 128, 128, 3, 1)])
+@LAB
 def test_conv_wgrad_row_kernel_boards(ops, cuda_device, S, B, Cin, Cin_real, Cout, K, Pin):
     """The one-kernel-row wgrad at other board sizes (windows of 32 compact pixels cross board rows
     and boards at every alignment; taps leaving the board read the LDS zero rows), with the split
     count of the training engine."""
     torch.manual_seed(7)
-    assert ops.wgrad_plan(Cout, Cin, K, Cin_real, variant=5)[0] == K  # the row kernel applies
+    L = ops.lab()
+    assert L.wgrad_plan(Cout, Cin, Cin_real, K, 5)[0] == K  # the row kernel applies
     x = _bf(torch.randn(B, Cin_real, S, S, device=cuda_device))
     dz = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
     ref_w = torch.nn.grad.conv2d_weight(x, (Cout, Cin_real, K, K), dz, padding=K // 2)
     ref_b = dz.sum(dim=(0, 2, 3))
     xp = ops.to_padded(x, Pin, Cin)
     dzp = ops.to_padded(dz, 1)
-    ns = ops.wgrad_nsplit(B * S * S, Cout, Cin, K, Cin_real, variant=5)
+    ns = ops.wgrad_splits(B * S * S, K * K // K)
     slab = torch.full((ns, K * K, Cout, Cin), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, Cout, device=cuda_device)
-    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin_real if Cin_real < Cin else 0, variant=5)
+    L.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, Cin_real if Cin_real < Cin else 0, 5)
     gw = torch.zeros(Cout, Cin_real, K, K, device=cuda_device)
     gb = torch.zeros(Cout, device=cuda_device)
     ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
@@ -155,6 +159,7 @@ def test_conv_wgrad_row_kernel_boards(ops, cuda_device, S, B, Cin, Cin_real, Cou
 
 @pytest.mark.parametrize("variant", [6, 7, 8])
 @pytest.mark.parametrize("S,B", [(9, 13), (13, 6), (19, 2176)])
+@LAB
 def test_conv_wgrad_line_lab_boards(ops, cuda_device, S, B, variant):
     """The kernel-lab line-staged wgrads (6 / 8: tap pairs, 4.5 workgroups per split, one per CU;
     7: per tap) at other board sizes and at the SL bench batch, with a one-round split count."""
@@ -279,7 +284,8 @@ def test_sgd_update(ops, cuda_device):
     assert torch.allclose(p, ref)
 
 
-@pytest.mark.parametrize("tile", [64, 128, 256, 2568, -1, 32, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("tile", lab_params([64, 65, 128, 130, 256, 2568, -1, 32, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9, 10,
+                                             11], PROD_TILES))
 def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     """Every forward tiling (gather 128/256, 128-pixel waves, halo) on a batch
     whose pixel count is not a multiple of any tile."""
@@ -299,7 +305,7 @@ def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", [64, 32, 256, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("tile", lab_params([64, 65, 130, 32, 256, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9, 10, 11], PROD_TILES))
 def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
     """Layer-1 geometry (Cin 64, 5x5, input pad 2) and the masked dgrad mode on each tiling."""
     torch.manual_seed(2)
@@ -327,7 +333,7 @@ def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
     assert _rel_err(ops.from_padded(dx, 1), ref_dx) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [0, 1, 3, 4, 5])
+@pytest.mark.parametrize("variant", lab_params([0, 1, 3, 4, 5], (0,)))
 @pytest.mark.parametrize("K,Cin,Cout,B", [(3, 192, 192, 5), (5, 64, 192, 3), (3, 128, 128, 4), (3, 192, 64, 2)])
 def test_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B, variant):
     """e4m3 conv on the block-scaled MFMA vs fp32 conv of the dequantised operands
@@ -369,7 +375,8 @@ def _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B, variant=0):
     assert y8[:, 0].sum() == 0 and yb[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", [0, 64, 128, 256, 384, 385, 386, 387, 32, 2, 4, 5, 6, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("tile", lab_params([0, 64, 65, 128, 130, 256, 384, 385, 386, 387, 32, 2, 4, 5, 6, 7, 8, 9, 10, 11],
+                                            PROD_TILES))
 @pytest.mark.parametrize("C", [192, 128])
 def test_relu_bitmask_dgrad_matches_mask(ops, cuda_device, tile, C):
     """Forward writes the ReLU' bitmask; dgrad mode 3 (bitmask) == mode 1 (bf16 activation mask)."""
@@ -550,6 +557,7 @@ def test_ops_refuse_host_tensors(cuda_device):
 
 
 @pytest.mark.parametrize("B,S", [(3, 19), (5, 9), (2, 13), (1, 8)])
+@LAB
 def test_winograd_lab_forward(ops, cuda_device, B, S):
     """Kernel-lab Winograd F(2x2,3x3) forward (winograd.hip) vs fp32 F.conv2d: odd and even board
     sizes (the last tile row/column of an odd board reads past the padded image: zero), tile counts
@@ -566,3 +574,77 @@ def test_winograd_lab_forward(ops, cuda_device, B, S):
     torch.cuda.synchronize()
     assert _rel_err(ops.from_padded(y, 1), ref) < 1.5e-2
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
+
+
+@pytest.mark.parametrize("B", [1, 4, 16])
+@pytest.mark.parametrize("tile", [0, 65, 130])
+def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, B, tile):
+    """Small batches (the reference's -B 16 training and batch-1 search calls): forward with the
+    bitmask, bitmask dgrad and the wgrad the trainer picks (ops.wgrad_config: the LDS-ring
+    variant with long splits) vs fp32 conv2d / conv2d_input / conv2d_weight."""
+    torch.manual_seed(12)
+    S, C = 19, 192
+    x = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    w = _bf(torch.randn(C, C, 3, 3, device=cuda_device) * 0.05)
+    b = torch.randn(C, device=cuda_device) * 0.1
+    wf = ops.packed_weight_like(w, C, C)
+    wd = ops.packed_weight_like(w, C, C, True)
+    ops.pack_weights([w.contiguous()], [wf], [wd])
+    xp = ops.to_padded(x, 1)
+    y = ops.padded_empty(B, S, 1, C, cuda_device)
+    mb = torch.full((B * (S + 2) ** 2 * ops.mbits_words(C),), -1, dtype=torch.int32, device=cuda_device)
+    ops.conv_fwd(xp, wf, b, y, 3, S, 1, 1, mbits=mb, tile=tile)
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    g = _bf(torch.randn(B, C, S, S, device=cuda_device))
+    dx = ops.padded_empty(B, S, 1, C, cuda_device)
+    ops.conv_fwd(ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb, tile=tile)
+    var, ns = ops.wgrad_config(B * S * S, C, C, 3)
+    assert var == 9 or B * S * S // 32 // ops.WGRAD_RING_STAGES == 0 or ns > 0
+    slab = torch.full((ns, 9, C, C), float("nan"), device=cuda_device)
+    dbs = torch.zeros(ns, C, device=cuda_device)
+    ops.conv_wgrad(xp, ops.to_padded(g, 1), slab, dbs, 3, S, 1, 1, variant=var)
+    gw = torch.zeros(C, C, 3, 3, device=cuda_device)
+    gb = torch.zeros(C, device=cuda_device)
+    ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
+    torch.cuda.synchronize()
+    assert _rel_err(ops.from_padded(y, 1), ref) < 1e-2
+    ref_dx = torch.nn.grad.conv2d_input((B, C, S, S), w, g, padding=1) * (ref > 0)
+    assert _rel_err(ops.from_padded(dx, 1), ref_dx) < 1e-2
+    assert _rel_err(gw, torch.nn.grad.conv2d_weight(x, (C, C, 3, 3), g, padding=1)) < 2e-3
+    assert _rel_err(gb, g.sum(dim=(0, 2, 3))) < 2e-3
+
+
+@pytest.mark.parametrize("S,B,Cin,Cout,Cout_p", [(19, 5, 48, 192, 192), (19, 3, 49, 152, 160), (9, 7, 48, 192, 192),
+                                                 (13, 2, 49, 152, 160), (19, 1, 40, 128, 128)])
+def test_conv_fwd_packed_taps_first_layer(ops, cuda_device, S, B, Cin, Cout, Cout_p):
+    """Packed-tap first layer (conv_fwd_pk: 8-channel chunks of the real planes only, up to three taps per
+    K-step) vs fp32 conv2d, and its ReLU' bitmask equal to the 64-channel kernel's."""
+    torch.manual_seed(13)
+    K, P = 5, 2
+    x = torch.randint(0, 2, (B, Cin, S, S), device=cuda_device).float()  # binary planes, as the featurizer's
+    w = _bf(torch.randn(Cout, Cin, K, K, device=cuda_device) * 0.05)
+    b = torch.randn(Cout, device=cuda_device) * 0.1
+    bp = torch.zeros(Cout_p, device=cuda_device)
+    bp[:Cout] = b
+    ref = F.relu(F.conv2d(x, w, b, padding=P))
+    xp = ops.to_padded(x, P)
+    assert ops.pk_applies(Cin, xp.shape[3])
+    wpk = ops.packed_weight_pk(w, Cout_p)
+    wfull = ops.packed_weight_like(w, 64, Cout_p)
+    ops.pack_weights([w.contiguous(), w.contiguous()], [wpk, wfull])
+    words = ops.mbits_words(Cout_p)
+    mb1 = torch.full((B * (S + 2) ** 2 * words,), -1, dtype=torch.int32, device=cuda_device)
+    mb2 = mb1.clone()
+    y = ops.padded_empty(B, S, 1, Cout_p, cuda_device)
+    y2 = ops.padded_empty(B, S, 1, Cout_p, cuda_device)
+    ops.conv_fwd_pk(xp, wpk, bp, y, K, S, P, 1, Cin, mbits=mb1)
+    ops.conv_fwd(xp, wfull, bp, y2, K, S, P, 1, mbits=mb2)
+    torch.cuda.synchronize()
+    out = ops.from_padded(y, 1)[:, :Cout]
+    assert _rel_err(out, ref) < 1e-2
+    assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
+    assert (ops.from_padded(y, 1)[:, Cout:] == 0).all()
+    # same products in a different summation order: bf16 outputs within rounding, same signs
+    assert _rel_err(ops.from_padded(y, 1), ops.from_padded(y2, 1)) < 1e-2
+    diff = (mb1 != mb2).float().mean().item()
+    assert diff < 1e-3, diff  # bits differ only where a pre-activation rounds across zero

@@ -79,7 +79,7 @@ def test_reference_bce_update_matches_keras_semantics():
     pol = _policy(torch.device("cpu"))
     net_ref = copy.deepcopy(pol.model)
     lr = 0.5
-    tr = TorchPolicyTrainer(pol.model, 4, lr=lr)
+    tr = TorchPolicyTrainer(pol.model, 4, lr=lr, device="cpu")  # CPU even where a GPU is present
     rng = np.random.default_rng(0)
     games = [(rng.integers(0, 2, (n, pol.preprocessor.output_dim, 9, 9), dtype=np.uint8),
               rng.integers(0, 81, n).astype(np.int32)) for n in (3, 6)]
