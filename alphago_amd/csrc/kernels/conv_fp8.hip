@@ -233,9 +233,15 @@ __device__ __forceinline__ int cvt4_bf16_bf8(unsigned lo2, unsigned hi2, float s
 // DGBITS (with DG): the e5m2 gradient operand is the copy the previous dgrad wrote for the fp8 wgrad,
 // ReLU' comes from the forward's bitmask (as DGB), outputs e5m2 (for the fp8 wgrad and the next
 // fp8 dgrad) and bf16 only where a bf16 consumer exists (the first layer's wgrad)
+// CW: bytes of one packed weight chunk = channels per K-chunk.  64 (default): a 128-K step is two
+// 64-channel chunks.  32 (the 160-channel value width, round 4): a step is four 32-channel chunks
+// and every MFMA K-block is one (tap, 32 channels) pair, so 160 channels are 5 chunks per tap instead
+// of 3 x 64 with a 32-channel zero half -- 45 chunks (12 steps) per 3x3 layer instead of 14 steps.
 template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8, bool DG = false, bool DGB = false,
-          bool DGBITS = false>
+          bool DGBITS = false, int CW = 64>
 __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) {
+  static_assert(CW == 64 || CW == 32, "chunk width");
+  constexpr int CPS = 128 / CW;  // chunks per K-step
   static_assert(!(DG && DGB), "one dgrad form");
   static_assert(!DGBITS || DG, "DGBITS: the e5m2-operand dgrad");
   constexpr bool MASKBITS = DGB || DGBITS;  // ReLU' from the forward epilogue's bitmask
@@ -260,8 +266,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   const int m0 = tile * BM;
   const int n0 = blockIdx.y * BN;
   const int SS = a.S * a.S;
-  const int CC = (a.Cin + 63) >> 6;  // Cin 160: the third chunk's upper half is the next pixel (zero weights)
-  const int nK = a.nch >> 1;
+  // CW 64, Cin 160: the third chunk's upper half is the next pixel (zero weights)
+  const int CC = (a.Cin + CW - 1) / CW;
+  const int nK = a.nch / CPS;
   const int qmax = a.K * a.K * CC - 1;
   const int sx = a.scales[0], sw = a.scales[1];
 
@@ -286,7 +293,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     const int rem = m - b * SS;
     const int ii = fdiv(rem, a.divS);
     const int jj = rem - ii * a.S;
-    xbase[j] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + (g & 1) * 32;
+    xbase[j] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + (CW == 64 ? (g & 1) * 32 : 0);
   }
   // A operand (weights) staging: piece p = tid + 512 i -> LDS row p/8, physical 16-B chunk p%8
   int wsrc[WP], wdst[WP];
@@ -295,7 +302,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     const int p = threadIdx.x + 512 * i;
     const int r = p >> 3, pc = p & 7;
     const int lc = pc ^ fp8_swz(r);
-    wsrc[i] = (((lc >> 2) * a.Cout) + n0 + (r < BN ? r : BN - 1)) * 64 + (lc & 3) * 16;
+    // logical 16-B chunk lc of the 128-B row: chunk lc / (CW / 16) of the step, bytes (lc % (CW / 16)) * 16
+    wsrc[i] = (((lc / (CW / 16)) * a.Cout) + n0 + (r < BN ? r : BN - 1)) * CW + (lc % (CW / 16)) * 16;
     wdst[i] = r * 128 + pc * 16;
   }
   auto chunk_off = [&](int q) {
@@ -304,21 +312,31 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     const int c = q - t * CC;
     const int kh = t / a.K;
     const int kw = t - kh * a.K;
-    return (kh * a.HPi + kw) * a.Cin + c * 64;
+    return (kh * a.HPi + kw) * a.Cin + c * CW;
+  };
+  // the lane's K-block (32 channels = 32 B of e4m3 / e5m2) of step ks: element offset from xbase
+  auto lane_off = [&](int ks) {
+    if constexpr (CW == 64) {
+      const int off0 = chunk_off(2 * ks), off1 = chunk_off(2 * ks + 1);
+      return g >= 2 ? off1 : off0;
+    } else {
+      const int o0 = chunk_off(4 * ks), o1 = chunk_off(4 * ks + 1);
+      const int o2 = chunk_off(4 * ks + 2), o3 = chunk_off(4 * ks + 3);
+      return g == 0 ? o0 : g == 1 ? o1 : g == 2 ? o2 : o3;
+    }
   };
   u32x4 wreg[WP];
   auto load_w = [&](int ks) {
-    const int q0 = 2 * ks < a.nch ? 2 * ks : a.nch - 2;
+    const int k0 = ks < nK ? ks : nK - 1;  // one step ahead of the last: any in-range step (unused)
 #pragma unroll
-    for (int i = 0; i < WP; ++i) wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, wsrc[i], q0 * a.Cout * 64, 0);
+    for (int i = 0; i < WP; ++i) wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, wsrc[i], k0 * a.Cout * 128, 0);
   };
   auto store_w = [&](int slot) {
 #pragma unroll
     for (int i = 0; i < WP; ++i) *(u32x4*)(smem + slot * W_BYTES + wdst[i]) = wreg[i];
   };
   auto load_x = [&](i32x8 (&xf)[MB], int ks) {
-    const int off0 = chunk_off(2 * ks), off1 = chunk_off(2 * ks + 1);
-    const int off = g >= 2 ? off1 : off0;
+    const int off = lane_off(ks);
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
       const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(xr, xbase[j] + off, 0, 0);
@@ -330,8 +348,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   u32x4 xraw[DGB ? MB : 1][4];
   const float gin = DGB ? 1.f / *a.in_scale : 1.f;  // power of two: exact
   auto load_xraw = [&](int ks) {
-    const int off0 = chunk_off(2 * ks), off1 = chunk_off(2 * ks + 1);
-    const int off = (g >= 2 ? off1 : off0) * 2;
+    const int off = lane_off(ks) * 2;
 #pragma unroll
     for (int j = 0; j < (DGB ? MB : 0); ++j)
 #pragma unroll
@@ -513,17 +530,26 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 // weights in 4 parts); kernel-lab build only: 1 / 3 / 4 = other L2-operand
 // tilings, 5 = LDS-staged conv_fwd_fp8_kernel
 
-template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false, bool DGB = false, bool DGBITS = false>
-static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
+template <int BN, int MB, int NPART, bool OB, bool OF, bool DG, bool DGB, bool DGBITS, int CW>
+static void launch_fp8_ga_cw(const ConvFp8Args& a, hipStream_t st) {
   constexpr int WROWS = (BN * 8) % 512 == 0 ? BN : ((BN * 8 + 511) / 512 * 512) / 8;  // as in the kernel
   constexpr int smem = 2 * WROWS * 128 + 64;
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS>,
+      (const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, CW>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   constexpr int BM = 128 * MB;
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS>), grid, dim3(512), smem, st, a);
+  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, CW>), grid, dim3(512), smem, st,
+                     a);
+}
+
+// a.cw: the packed weights' chunk width (32 for the 160-channel value layers packed in 32-channel
+// chunks, else 64)
+template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false, bool DGB = false, bool DGBITS = false>
+static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
+  if (a.cw == 32) launch_fp8_ga_cw<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, 32>(a, st);
+  else launch_fp8_ga_cw<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, 64>(a, st);
 }
 
 // fp8 dgrad of the fp8-wgrad value step: e5m2 operand (the previous dgrad's copy), bitmask ReLU',
@@ -561,6 +587,7 @@ static void launch_fp8_dgrad_bn(const ConvFp8Args& a, hipStream_t st) {
 
 template <int BN, bool OB, bool OF>
 static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
+  if (a.cw != 64 && a.variant != 0) throw std::invalid_argument("conv_fwd_fp8: 32-channel chunks: production kernel only");
 #ifndef AGK_KERNEL_LAB
   if (a.variant != 0) throw std::invalid_argument("conv_fwd_fp8: variant " + std::to_string(a.variant) +
                                                   " is a kernel-lab variant");
@@ -649,19 +676,20 @@ void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
 // channels, taps flipped -- w'[ci][co][kh][kw] = w[co][ci][K-1-kh][K-1-kw]; Cout_p / Cin_p are
 // then the padded row / chunked extents.
 __global__ void pack_weights_fp8_kernel(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p,
-                                        int Cin_p, int nch, float scale, const float* scale_dev, int transposed) {
-  const int CC = Cin_p >> 6;
+                                        int Cin_p, int nch, float scale, const float* scale_dev, int transposed,
+                                        int cw) {
+  const int CC = Cin_p / cw;
   if (scale_dev) scale = *scale_dev;
   const int rows_real = transposed ? Cin_real : Cout_real;
   const int chans_real = transposed ? Cout_real : Cin_real;
-  const long total = (long)nch * Cout_p * 64;
+  const long total = (long)nch * Cout_p * cw;
   for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += (long)gridDim.x * blockDim.x) {
-    const int byte = (int)(idx & 63);
-    const long qn = idx >> 6;
+    const int byte = (int)(idx % cw);
+    const long qn = idx / cw;
     const int n = (int)(qn % Cout_p);
     const int q = (int)(qn / Cout_p);
     const int t = q / CC;
-    const int c = (q - t * CC) * 64 + byte;
+    const int c = (q - t * CC) * cw + byte;
     float v = 0.f;
     if (t < K * K && n < rows_real && c < chans_real) {
       const int kh = t / K, kw = t - (t / K) * K;
@@ -675,33 +703,34 @@ __global__ void pack_weights_fp8_kernel(const float* w, uint8_t* out, int Cout_r
 }
 
 void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p, int Cin_p,
-                             int nch, float scale, const float* scale_dev, int transposed, hipStream_t st) {
-  const long total = (long)nch * Cout_p * 64;
+                             int nch, float scale, const float* scale_dev, int transposed, int cw, hipStream_t st) {
+  const long total = (long)nch * Cout_p * cw;
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(pack_weights_fp8_kernel, dim3(blocks), dim3(256), 0, st, w, out, Cout_real, Cin_real, K, Cout_p,
-                     Cin_p, nch, scale, scale_dev, transposed);
+                     Cin_p, nch, scale, scale_dev, transposed, cw);
 }
 
 __global__ __launch_bounds__(256) void pack_weights_fp8_multi_kernel(Fp8PackArgs a) {
   const Fp8PackJob& j = a.jobs[blockIdx.y];
-  const int CC = j.Cin_p >> 6;
+  const int cw = j.cw;
+  const int CC = j.Cin_p / cw;
   const float scale = *j.scale;
   const int rows_real = j.transposed ? j.Cin_real : j.Cout_real;
   const int chans_real = j.transposed ? j.Cout_real : j.Cin_real;
   const int K = j.K;
-  const long total = (long)j.nch * j.Cout_p * 16;  // 4 bytes per thread
+  const long total = (long)j.nch * j.Cout_p * (cw / 4);  // 4 bytes per thread
   for (long i4 = (long)blockIdx.x * blockDim.x + threadIdx.x; i4 < total; i4 += (long)gridDim.x * blockDim.x) {
     const long idx = i4 * 4;
-    const int byte = (int)(idx & 63);
-    const long qn = idx >> 6;
+    const int byte = (int)(idx % cw);
+    const long qn = idx / cw;
     const int n = (int)(qn % j.Cout_p);
     const int q = (int)(qn / j.Cout_p);
     const int t = q / CC;
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int c = (q - t * CC) * 64 + byte + r;
+      const int c = (q - t * CC) * cw + byte + r;
       v[r] = 0.f;
       if (t < K * K && n < rows_real && c < chans_real) {
         const int kh = t / K, kw = t - (t / K) * K;

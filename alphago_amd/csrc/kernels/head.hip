@@ -16,6 +16,9 @@
 
 namespace agk {
 
+// boards below which the per-board head kernels run 1024 threads per workgroup instead of 256
+constexpr int kHeadWideBelow = 256;
+
 __device__ __forceinline__ float block_reduce_max(float v, float* red) {
   v = wave_max(v);
   const int w = threadIdx.x >> 6;
@@ -83,6 +86,7 @@ __device__ __forceinline__ void head_dots(const __bf16* base, const float* w_s, 
 // Gradient of a 1x1 (F -> 1) head conv given dlogits g (in g_s, length S*S):
 // ReLU'-masked dY into the trunk's last activation and per-board partials of
 // dW_head (the dbias partial is written by the caller).
+template <int NT>
 __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int b, const __bf16* base,
                                                     const float* w_s, const float* g_s) {
   // One pass over the board's activations: thread (r, c8) walks positions
@@ -90,7 +94,7 @@ __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int
   // accumulating sum_p g[p] * y[p, c] in registers; the R partials per
   // channel are then reduced through LDS.  Consecutive threads cover
   // consecutive 16-B channel groups of one position (coalesced rows).
-  __shared__ float part[256 * 8];
+  __shared__ float part[NT * 8];
   const int tid = threadIdx.x;
   const int SS = a.S * a.S;
   const int HP = a.S + 2;
@@ -148,6 +152,7 @@ __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int
 //   L = -1/SS * sum_j [y_j log pc_j + (1 - y_j) log(1 - pc_j)],  pc = clip(p, 1e-7, 1 - 1e-7)
 // with y the one-hot move; clip has zero gradient outside its range (Theano
 // clip), and the softmax backward is dz_i = p_i (g_i - sum_j p_j g_j).
+template <int NT>
 __device__ void policy_bce_train(const PolicyHeadArgs& a, int b, int t, float wb, float zmax, float inv, int lidx,
                                  const __bf16* base, const float* w_s, float* z_s, float* red) {
   __shared__ float p_s[368];
@@ -155,7 +160,7 @@ __device__ void policy_bce_train(const PolicyHeadArgs& a, int b, int t, float wb
   const int SS = a.S * a.S;
   const float eps = 1e-7f;
   float ls = 0.f, pg = 0.f;
-  for (int p = tid; p < SS; p += 256) {
+  for (int p = tid; p < SS; p += NT) {
     const float pr = (z_s[p] == -INFINITY) ? 0.f : __expf(z_s[p] - zmax) * inv;
     const float pc = fminf(fmaxf(pr, eps), 1.f - eps);
     const bool y = p == t;
@@ -172,26 +177,28 @@ __device__ void policy_bce_train(const PolicyHeadArgs& a, int b, int t, float wb
     a.correct[b] = (t >= 0 && lidx == t) ? 1.f : 0.f;
   }
   const float sc = t >= 0 ? a.grad_scale * wb : 0.f;
-  for (int p = tid; p < SS; p += 256) z_s[p] = p_s[p] * (z_s[p] - pg) * sc;
+  for (int p = tid; p < SS; p += NT) z_s[p] = p_s[p] * (z_s[p] - pg) * sc;
   __syncthreads();
-  head_input_backward(a, b, base, w_s, z_s);
+  head_input_backward<NT>(a, b, base, w_s, z_s);
   float gs = 0.f;
-  for (int p = tid; p < SS; p += 256) gs += z_s[p];
+  for (int p = tid; p < SS; p += NT) gs += z_s[p];
   gs = block_reduce_sum(gs, red);
   if (tid == 0) a.dhead[(size_t)b * (a.C_real + 1) + a.C_real] = gs;
 }
 
-template <bool TRAIN>
-__global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
+// NT threads per board: 256 for large batches (occupancy), 1024 below (a board's latency-bound loops
+// get 4x the parallelism: B = 16 has only 16 workgroups)
+template <bool TRAIN, int NT>
+__global__ __launch_bounds__(NT) void policy_head_kernel(PolicyHeadArgs a) {
   __shared__ float w_s[256];
   __shared__ float z_s[368];
-  __shared__ float red[8];
-  __shared__ int redi[8];
+  __shared__ float red[16];
+  __shared__ int redi[16];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int SS = a.S * a.S;
   const int HP = a.S + 2;
-  for (int c = tid; c < a.C; c += 256) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
+  for (int c = tid; c < a.C; c += NT) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
   __syncthreads();
   const __bf16* base = a.y + (size_t)b * HP * HP * a.C;
   const float bias = a.b[0];
@@ -200,7 +207,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
   float lmax = -INFINITY;
   int lidx = 0x7fffffff;
   head_dots(base, w_s, z_s, a.S, a.C);
-  for (int p = tid; p < SS; p += 256) {
+  for (int p = tid; p < SS; p += NT) {
     float z = (z_s[p] + bias) * a.inv_temp;
     if (legal && !legal[p]) z = -INFINITY;
     z_s[p] = z;
@@ -227,7 +234,7 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
     __syncthreads();
     lmax = red[0];
     lidx = redi[0];
-    for (int w = 1; w < 4; ++w)
+    for (int w = 1; w < NT / 64; ++w)
       if (red[w] > lmax || (red[w] == lmax && redi[w] < lidx)) {
         lmax = red[w];
         lidx = redi[w];
@@ -235,18 +242,18 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
   }
   const float zmax = lmax;
   float ls = 0.f;
-  for (int p = tid; p < SS; p += 256) ls += (z_s[p] == -INFINITY) ? 0.f : __expf(z_s[p] - zmax);
+  for (int p = tid; p < SS; p += NT) ls += (z_s[p] == -INFINITY) ? 0.f : __expf(z_s[p] - zmax);
   const float sum = block_reduce_sum(ls, red);
   const float inv = 1.f / sum;
   if (a.probs) {
-    for (int p = tid; p < SS; p += 256)
+    for (int p = tid; p < SS; p += NT)
       a.probs[(size_t)b * SS + p] = (z_s[p] == -INFINITY) ? 0.f : __expf(z_s[p] - zmax) * inv;
   }
   if constexpr (TRAIN) {
     const int t = a.target[b];
     const float wb = a.weight ? a.weight[b] : 1.f;
     if (a.loss_kind == 1) {
-      policy_bce_train(a, b, t, wb, zmax, inv, lidx, base, w_s, z_s, red);
+      policy_bce_train<NT>(a, b, t, wb, zmax, inv, lidx, base, w_s, z_s, red);
       return;
     }
     if (tid == 0) {
@@ -261,15 +268,15 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
       }
     }
     __syncthreads();  // everyone has read z_s[t]
-    for (int p = tid; p < SS; p += 256) {
+    for (int p = tid; p < SS; p += NT) {
       float g = 0.f;
       if (t >= 0) g = (__expf(z_s[p] - zmax) * inv - (p == t ? 1.f : 0.f)) * a.grad_scale * wb;
       z_s[p] = g;
     }
     __syncthreads();
-    head_input_backward(a, b, base, w_s, z_s);
+    head_input_backward<NT>(a, b, base, w_s, z_s);
     float gs = 0.f;
-    for (int p = tid; p < SS; p += 256) gs += z_s[p];
+    for (int p = tid; p < SS; p += NT) gs += z_s[p];
     gs = block_reduce_sum(gs, red);
     if (tid == 0) a.dhead[(size_t)b * (a.C_real + 1) + a.C_real] = gs;
   }
@@ -277,39 +284,41 @@ __global__ __launch_bounds__(256) void policy_head_kernel(PolicyHeadArgs a) {
 
 // Head logits only: z[b][p] = y[b,p,:] . w + bias (value-net head input,
 // value.py:23-26); the board's activations are read once.
-__global__ __launch_bounds__(256) void head_logits_kernel(PolicyHeadArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void head_logits_kernel(PolicyHeadArgs a) {
   __shared__ float w_s[256];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int SS = a.S * a.S;
   const int HP = a.S + 2;
-  for (int c = tid; c < a.C; c += 256) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
+  for (int c = tid; c < a.C; c += NT) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
   __syncthreads();
   __shared__ float z_s[368];
   const __bf16* base = a.y + (size_t)b * HP * HP * a.C;
   const float bias = a.b[0];
   head_dots(base, w_s, z_s, a.S, a.C);
-  for (int p = tid; p < SS; p += 256) a.probs[(size_t)b * SS + p] = z_s[p] + bias;  // probs slot carries the logits
+  for (int p = tid; p < SS; p += NT) a.probs[(size_t)b * SS + p] = z_s[p] + bias;  // probs slot carries the logits
 }
 
 // Head backward from an externally computed dlogits (value net: dz = dh W1^T).
-__global__ __launch_bounds__(256) void head_backward_kernel(PolicyHeadArgs a, const float* dlogits) {
+template <int NT>
+__global__ __launch_bounds__(NT) void head_backward_kernel(PolicyHeadArgs a, const float* dlogits) {
   __shared__ float w_s[256];
   __shared__ float g_s[368];
-  __shared__ float red[8];
+  __shared__ float red[16];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const int SS = a.S * a.S;
   const int HP = a.S + 2;
-  for (int c = tid; c < a.C; c += 256) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
+  for (int c = tid; c < a.C; c += NT) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
   float gs = 0.f;
-  for (int p = tid; p < SS; p += 256) {
+  for (int p = tid; p < SS; p += NT) {
     const float g = dlogits[(size_t)b * SS + p];
     g_s[p] = g;
     gs += g;
   }
   __syncthreads();
-  head_input_backward(a, b, a.y + (size_t)b * HP * HP * a.C, w_s, g_s);
+  head_input_backward<NT>(a, b, a.y + (size_t)b * HP * HP * a.C, w_s, g_s);
   gs = block_reduce_sum(gs, red);
   if (tid == 0) a.dhead[(size_t)b * (a.C_real + 1) + a.C_real] = gs;
 }
@@ -368,18 +377,26 @@ void launch_head_grad_sums(const float* dhead, int B, int N, const float* loss, 
 }
 
 void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(head_logits_kernel, dim3(a.B), dim3(256), 0, st, a);
+  if (a.B < kHeadWideBelow) hipLaunchKernelGGL(head_logits_kernel<1024>, dim3(a.B), dim3(1024), 0, st, a);
+  else hipLaunchKernelGGL(head_logits_kernel<256>, dim3(a.B), dim3(256), 0, st, a);
 }
 void launch_head_backward(const PolicyHeadArgs& a, const float* dlogits, hipStream_t st) {
-  hipLaunchKernelGGL(head_backward_kernel, dim3(a.B), dim3(256), 0, st, a, dlogits);
+  if (a.B < kHeadWideBelow) hipLaunchKernelGGL(head_backward_kernel<1024>, dim3(a.B), dim3(1024), 0, st, a, dlogits);
+  else hipLaunchKernelGGL(head_backward_kernel<256>, dim3(a.B), dim3(256), 0, st, a, dlogits);
 }
 void launch_value_out(const ValueOutArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(value_out_kernel, dim3(a.B), dim3(256), 0, st, a);
 }
 
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st) {
-  if (train) hipLaunchKernelGGL(policy_head_kernel<true>, dim3(a.B), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(policy_head_kernel<false>, dim3(a.B), dim3(256), 0, st, a);
+  if (a.B < kHeadWideBelow) {
+    if (train) hipLaunchKernelGGL((policy_head_kernel<true, 1024>), dim3(a.B), dim3(1024), 0, st, a);
+    else hipLaunchKernelGGL((policy_head_kernel<false, 1024>), dim3(a.B), dim3(1024), 0, st, a);
+  } else if (train) {
+    hipLaunchKernelGGL((policy_head_kernel<true, 256>), dim3(a.B), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((policy_head_kernel<false, 256>), dim3(a.B), dim3(256), 0, st, a);
+  }
 }
 
 }  // namespace agk

@@ -162,7 +162,8 @@ struct ConvFp8Args {
   unsigned* amax;           // optional running max of the ReLU output (float bits), kFp8AmaxSlots slots
   int M, S, Cin, Cout, K;
   int HPi, offi, HPo, Po;
-  int nch;
+  int nch;                  // packed chunks (cw channels each; a K-step holds 128 / cw chunks)
+  int cw;                   // chunk width: 64, or 32 for 160-channel operands packed in 32-channel chunks
   FastDiv divSS, divS;      // filled by the launcher
   int variant;              // 0 = production (pixel operand from L2, 48 px/wave); lab: 1, 3, 4 other tilings,
                             // 5 = LDS-staged operands
@@ -216,7 +217,7 @@ void launch_pack_weights(const PackWeightsArgs& a, hipStream_t st);
 void launch_featurize(const FeaturizeArgs& a, hipStream_t st);
 void launch_conv_fwd_fp8(const ConvFp8Args& a, hipStream_t st);
 void launch_pack_weights_fp8(const float* w, uint8_t* out, int Cout_real, int Cin_real, int K, int Cout_p, int Cin_p,
-                             int nch, float scale, const float* scale_dev, int transposed, hipStream_t st);
+                             int nch, float scale, const float* scale_dev, int transposed, int cw, hipStream_t st);
 struct Fp8WeightScalesArgs {
   const float* w[kMaxPackLayers];
   int n[kMaxPackLayers];
@@ -231,6 +232,7 @@ struct Fp8PackJob {
   uint8_t* out;           // [nch][rows_p][64] e4m3
   const float* scale;     // device scale (one float)
   int Cout_real, Cin_real, K, Cout_p, Cin_p, nch, transposed;
+  int cw;                 // chunk width (channels per chunk): 64, or 32 for the 160-channel value layers
 };
 struct Fp8PackArgs {
   Fp8PackJob jobs[kMaxFp8PackJobs];
@@ -245,6 +247,28 @@ void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipSt
 void launch_bf8_convert_probe(const __bf16* x, uint8_t* y, long n, float scale, int mode, hipStream_t st);
 #endif
 void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hipStream_t st);
+
+// fused SGD + bf16 weight packs (pack.hip sgd_pack_kernel)
+constexpr int kSgdPackMaxTaps = 25;
+constexpr int kSgdPackMaxRanges = 64;
+struct SgdPackLayer {
+  int64_t off;     // OIHW fp32 weights at p + off (and their gradient at g + off)
+  __bf16* wf;      // forward pack [T][Cout_p][Cin_p], or the packed-tap layout when pk_cpt > 0
+  __bf16* wd;      // transposed dgrad pack [T][Cin_p][Cout_p] (taps flipped) or null
+  int Cout_real, Cin_real, Cout_p, Cin_p, K, pk_cpt;
+};
+struct SgdPackArgs {
+  float* p;
+  const float* g;
+  float lr, gscale;
+  double* sched;   // device Keras schedule {lr0, decay, iterations, lr} (advanced first) or null: lr
+  SgdPackLayer layers[kMaxPackLayers];
+  int nlayers;
+  int64_t range_off[kSgdPackMaxRanges];
+  int range_len[kSgdPackMaxRanges];
+  int nranges;
+};
+void launch_sgd_pack(const SgdPackArgs& a, hipStream_t st);
 // RCCL all-reduce stand-in (comm_proxy.hip): channels workgroups copy n floats and hold their CUs wire_us
 void launch_comm_proxy(const float* src, float* dst, long n, int channels, double wire_us, hipStream_t st);
 

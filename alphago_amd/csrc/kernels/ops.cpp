@@ -374,7 +374,8 @@ void pack_weights_fp8_multi(at::TensorList ws, at::TensorList outs, const Tensor
     const Tensor& o = outs[i];
     CHECK_F32(w); CHECK_CONTIG(w); CHECK_CONTIG(o);
     TORCH_CHECK(w.dim() == 4 && w.size(2) == w.size(3), "w OIHW");
-    TORCH_CHECK(o.scalar_type() == at::kByte && o.dim() == 3 && o.size(2) == 64, "out (nch, rows_p, 64) uint8");
+    TORCH_CHECK(o.scalar_type() == at::kByte && o.dim() == 3 && (o.size(2) == 64 || o.size(2) == 32),
+                "out (nch, rows_p, 64 or 32) uint8");
     TORCH_CHECK(layer[i] >= 0 && layer[i] < scales.numel(), "layer index");
     const int K = (int)w.size(2);
     const bool tr = transposed[i] != 0;
@@ -388,9 +389,12 @@ void pack_weights_fp8_multi(at::TensorList ws, at::TensorList outs, const Tensor
     j.K = K;
     j.Cout_p = rows_p;
     // channel chunks per tap: the packed chunk count covers K*K taps (nch rounded up to even)
-    j.Cin_p = (int)(((int64_t)(tr ? w.size(0) : w.size(1)) + 63) / 64 * 64);
-    TORCH_CHECK(nch >= K * K * (j.Cin_p / 64), "out has too few chunks for the weights");
+    const int cw = (int)o.size(2);
+    j.Cin_p = (int)(((int64_t)(tr ? w.size(0) : w.size(1)) + cw - 1) / cw * cw);
+    TORCH_CHECK(cw == 64 || j.Cin_p == 160, "32-channel chunks: 160-channel reductions only");
+    TORCH_CHECK(nch >= K * K * (j.Cin_p / cw) && nch % (128 / cw) == 0, "out has too few chunks for the weights");
     j.nch = nch;
+    j.cw = cw;
     j.transposed = tr ? 1 : 0;
   }
   agk::launch_pack_weights_fp8_multi(a, cur_stream());
@@ -439,19 +443,22 @@ void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c1
                       bool transposed) {
   check_dev("pack_weights_fp8", w, out, scale_dev);
   CHECK_F32(w); CHECK_CONTIG(w);
-  TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.dim() == 3 && out.size(2) == 64, "out");
+  TORCH_CHECK(out.scalar_type() == at::kByte && out.is_contiguous() && out.dim() == 3 &&
+                  (out.size(2) == 64 || out.size(2) == 32), "out (nch, rows_p, 64 or 32) uint8");
   const int K = (int)w.size(2);
-  const int nch = (int)out.size(0), Cout_p = (int)out.size(1);
+  const int nch = (int)out.size(0), Cout_p = (int)out.size(1), cw = (int)out.size(2);
   // chunked extent: input channels, or output channels for the transposed (dgrad) packing
-  const int Cin_p = ((int)w.size(transposed ? 0 : 1) + 63) / 64 * 64;
-  TORCH_CHECK(nch % 2 == 0 && nch >= K * K * (Cin_p / 64) && Cout_p >= w.size(transposed ? 1 : 0), "packed geometry");
+  const int Cin_p = ((int)w.size(transposed ? 0 : 1) + cw - 1) / cw * cw;
+  TORCH_CHECK(cw == 64 || Cin_p == 160, "32-channel chunks: 160-channel reductions only");
+  TORCH_CHECK(nch % (128 / cw) == 0 && nch >= K * K * (Cin_p / cw) && Cout_p >= w.size(transposed ? 1 : 0),
+              "packed geometry");
   const float* sd = nullptr;
   if (scale_dev.has_value()) {
     CHECK_F32(*scale_dev);
     sd = scale_dev->data_ptr<float>();
   }
   agk::launch_pack_weights_fp8(w.data_ptr<float>(), out.data_ptr<uint8_t>(), (int)w.size(0), (int)w.size(1), K, Cout_p,
-                               Cin_p, nch, (float)scale, sd, transposed ? 1 : 0, cur_stream());
+                               Cin_p, nch, (float)scale, sd, transposed ? 1 : 0, cw, cur_stream());
   launch_check("pack_weights_fp8");
 }
 
@@ -534,6 +541,61 @@ void sgd_update_sched(const Tensor& p, const Tensor& g, const Tensor& sched, dou
   agk::launch_sgd_sched(p.data_ptr<float>(), g.data_ptr<float>(), p.numel(), sched.data_ptr<double>(), (float)gscale,
                         cur_stream());
   launch_check("sgd_update_sched");
+}
+
+// Fused SGD + bf16 packs (pack.hip sgd_pack_kernel): conv layer i's OIHW weights live at flat offset
+// w_meta[4i] with (Cout_real, Cin_real, K) = w_meta[4i+1 .. 4i+3]; wf[i] / wd[i] (wd empty: none) as
+// pack_weights; plain SGD over (range_off, range_len); lr from ``sched`` (advanced) when given.
+void sgd_pack(const Tensor& p, const Tensor& g, double lr, const c10::optional<Tensor>& sched, double gscale,
+              at::IntArrayRef w_meta, at::TensorList wf, at::TensorList wd, at::IntArrayRef range_off,
+              at::IntArrayRef range_len) {
+  check_dev("sgd_pack", p, g, sched, wf, wd);
+  CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
+  TORCH_CHECK(p.numel() == g.numel(), "sgd_pack: p and g sizes differ");
+  const int nl = (int)wf.size();
+  TORCH_CHECK(nl <= agk::kMaxPackLayers && (int)w_meta.size() == 4 * nl && (wd.size() == 0 || (int)wd.size() == nl),
+              "sgd_pack: per-layer lists");
+  TORCH_CHECK(range_off.size() == range_len.size() && (int)range_off.size() <= agk::kSgdPackMaxRanges, "sgd_pack: ranges");
+  agk::SgdPackArgs a{};
+  a.p = p.data_ptr<float>();
+  a.g = g.data_ptr<float>();
+  a.lr = (float)lr;
+  a.gscale = (float)gscale;
+  if (sched.has_value()) {
+    TORCH_CHECK(sched->scalar_type() == at::kDouble && sched->numel() == 4 && sched->is_contiguous(),
+                "sched must be float64[4] {lr0, decay, iterations, lr}");
+    a.sched = sched->data_ptr<double>();
+  }
+  a.nlayers = nl;
+  for (int i = 0; i < nl; ++i) {
+    agk::SgdPackLayer& L = a.layers[i];
+    L.off = w_meta[4 * i];
+    L.Cout_real = (int)w_meta[4 * i + 1]; L.Cin_real = (int)w_meta[4 * i + 2]; L.K = (int)w_meta[4 * i + 3];
+    CHECK_BF16(wf[i]); CHECK_CONTIG(wf[i]);
+    L.wf = bfp_mut(wf[i]);
+    L.Cout_p = (int)wf[i].size(1); L.Cin_p = (int)wf[i].size(2);
+    const int T = L.K * L.K, cpt = (L.Cin_real + 7) / 8;
+    TORCH_CHECK(T <= agk::kSgdPackMaxTaps, "sgd_pack: at most 5x5 kernels");
+    TORCH_CHECK(L.off >= 0 && L.off + (int64_t)L.Cout_real * L.Cin_real * T <= p.numel(), "sgd_pack: weight range");
+    L.pk_cpt = (wf[i].size(0) != T && wf[i].size(0) != T + 1 && L.Cin_p == 64 && L.Cin_real <= 64 &&
+                wf[i].size(0) == (T * cpt + 7) / 8) ? cpt : 0;
+    TORCH_CHECK((wf[i].size(0) == T || wf[i].size(0) == T + 1 || L.pk_cpt > 0) && L.Cout_p >= L.Cout_real &&
+                L.Cin_p >= L.Cin_real, "sgd_pack: bad wf");
+    L.wd = nullptr;
+    if (wd.size() && wd[i].numel() > 0) {
+      CHECK_BF16(wd[i]); CHECK_CONTIG(wd[i]);
+      TORCH_CHECK(L.pk_cpt == 0 && wd[i].size(1) == L.Cin_p && wd[i].size(2) == L.Cout_p, "sgd_pack: bad wd");
+      L.wd = bfp_mut(wd[i]);
+    }
+  }
+  a.nranges = (int)range_off.size();
+  for (int r = 0; r < a.nranges; ++r) {
+    TORCH_CHECK(range_off[r] >= 0 && range_len[r] >= 0 && range_off[r] + range_len[r] <= p.numel(), "sgd_pack: range");
+    a.range_off[r] = range_off[r];
+    a.range_len[r] = (int)range_len[r];
+  }
+  agk::launch_sgd_pack(a, cur_stream());
+  launch_check("sgd_pack");
 }
 
 // C = beta*C + op(A) op(B) (+ bias); op(X) = X or X^T (no copies of transposed operands)
@@ -620,6 +682,8 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
   m.def("comm_proxy(Tensor src, Tensor(a!) dst, int channels, float wire_us) -> ()");
   m.def("sgd_update_sched(Tensor(a!) p, Tensor g, Tensor(b!) sched, float gscale) -> ()");
+  m.def("sgd_pack(Tensor(a!) p, Tensor g, float lr, Tensor(b!)? sched, float gscale, int[] w_meta, Tensor(c!)[] wf, "
+        "Tensor(d!)[] wd, int[] range_off, int[] range_len) -> ()");
   m.def("dense_f32(Tensor A, Tensor B, Tensor? bias, Tensor(a!) C, bool transA, bool transB, float beta) -> ()");
   // budget: node visits per capture / escape read; 4096 = lb::kLadderVisits (ladder_bb.h)
   m.def(
@@ -659,6 +723,7 @@ TORCH_LIBRARY(alphago_amd, m) {
 
 TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("conv_fwd", &conv_fwd);
+  m.impl("sgd_pack", &sgd_pack);
   m.impl("conv_fwd_pk", &conv_fwd_pk);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);

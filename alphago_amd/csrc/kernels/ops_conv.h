@@ -222,6 +222,16 @@ inline void conv_wgrad_fp8_impl(const Tensor& x8, const Tensor& dz8, const Tenso
   launch_check("conv_wgrad_fp8");
 }
 
+// packed fp8 weights (nch, rows, cw): cw = 64, or 32 for 160-channel reductions (32-channel chunks, no
+// zero half); nch covers K*K taps of ceil(C / cw) chunks and is a multiple of the chunks per 128-K step
+inline int fp8_check_chunks(const Tensor& w, int64_t K, int64_t C, const char* what) {
+  const int64_t cw = w.size(2);
+  TORCH_CHECK(cw == 64 || (cw == 32 && C == 160), what, ": packed chunk width 64, or 32 for 160 channels");
+  const int64_t nch = w.size(0);
+  TORCH_CHECK(nch % (128 / cw) == 0 && nch >= K * K * ((C + cw - 1) / cw), what, ": too few packed chunks");
+  return (int)cw;
+}
+
 inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales,
                               const Tensor& out_scale, const c10::optional<Tensor>& amax,
                               const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K,
@@ -233,13 +243,12 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
   // by dgrad_mask > 0, no bias, e5m2 y_fp8)
   CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
   TORCH_CHECK(x.scalar_type() == at::kByte && w.scalar_type() == at::kByte, "fp8 tensors are stored as uint8");
-  TORCH_CHECK(x.dim() == 4 && w.dim() == 3 && w.size(2) == 64, "x (B,HP,HP,C), w (nch, Cout, 64)");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 3, "x (B,HP,HP,C), w (nch, Cout, cw)");
   TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2 && out_scale.scalar_type() == at::kFloat, "scales");
   if (!dgrad_mask.has_value()) CHECK_F32(bias);
   const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3), nch = w.size(0), Cout = w.size(1);
-  TORCH_CHECK((Cin % 64 == 0 || Cin == 160) && (Cout % 64 == 0 || Cout == 160) && nch % 2 == 0 &&
-                  nch >= K * K * ((Cin + 63) / 64),
-              "channel geometry (multiples of 64, or 160)");
+  TORCH_CHECK((Cin % 64 == 0 || Cin == 160) && (Cout % 64 == 0 || Cout == 160), "channel geometry (multiples of 64, or 160)");
+  const int cw = fp8_check_chunks(w, K, Cin, "conv_fwd_fp8");
   TORCH_CHECK(Pin >= K / 2 && HPi == S + 2 * Pin, "padding/geometry mismatch");
   TORCH_CHECK(y_bf16.has_value() || y_fp8.has_value(), "need an output");
   agk::ConvFp8Args a{};
@@ -264,7 +273,7 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
     a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
   }
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K;
-  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po; a.nch = (int)nch;
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po; a.nch = (int)nch; a.cw = cw;
   if (dgrad_mask.has_value()) {
     CHECK_DEV(*dgrad_mask); CHECK_BF16(*dgrad_mask); CHECK_CONTIG(*dgrad_mask);
     TORCH_CHECK(y_bf16.has_value() && dgrad_mask->sizes() == y_bf16->sizes(), "dgrad: mask must match y_bf16");
@@ -296,14 +305,15 @@ inline void conv_dgrad_fp8_bits_impl(const Tensor& dz8, const Tensor& w8t, const
   check_dev("conv_dgrad_fp8_bits", dz8, w8t, mbits, scales, out_scale, amax, y_bf16, y_fp8);
   CHECK_DEV(dz8); CHECK_DEV(w8t); CHECK_DEV(mbits); CHECK_CONTIG(dz8); CHECK_CONTIG(w8t); CHECK_CONTIG(mbits);
   TORCH_CHECK(dz8.scalar_type() == at::kByte && w8t.scalar_type() == at::kByte, "fp8 tensors are stored as uint8");
-  TORCH_CHECK(dz8.dim() == 4 && w8t.dim() == 3 && w8t.size(2) == 64 && dz8.size(3) == 160 && w8t.size(1) == 160,
-              "dz8 (B, HP, HP, 160), w8t (nch, 160, 64)");
+  TORCH_CHECK(dz8.dim() == 4 && w8t.dim() == 3 && dz8.size(3) == 160 && w8t.size(1) == 160,
+              "dz8 (B, HP, HP, 160), w8t (nch, 160, cw)");
+  const int cw = fp8_check_chunks(w8t, K, 160, "conv_dgrad_fp8_bits");
   TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2 && out_scale.scalar_type() == at::kFloat &&
                   out_scale.numel() >= 1, "scales int32[2], out_scale f32[1]");
   TORCH_CHECK(mbits.scalar_type() == at::kInt, "mbits int32");
   TORCH_CHECK(y_bf16.has_value() || y_fp8.has_value(), "need an output");
   const int64_t B = dz8.size(0), HP = dz8.size(1), nch = w8t.size(0);
-  TORCH_CHECK(HP == S + 2 && dz8.size(2) == HP && nch % 2 == 0 && nch >= K * K * 3, "geometry (pad 1, 160 channels)");
+  TORCH_CHECK(HP == S + 2 && dz8.size(2) == HP, "geometry (pad 1, 160 channels)");
   TORCH_CHECK(mbits.numel() >= B * HP * HP * 8, "mbits too small: need B*HP*HP*8 words");
   agk::ConvFp8Args a{};
   a.x = dz8.data_ptr<uint8_t>(); a.w = w8t.data_ptr<uint8_t>();
@@ -323,7 +333,7 @@ inline void conv_dgrad_fp8_bits_impl(const Tensor& dz8, const Tensor& w8t, const
     a.amax = reinterpret_cast<unsigned*>(amax->data_ptr<int>());
   }
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = 160; a.Cout = 160; a.K = (int)K;
-  a.HPi = (int)HP; a.offi = (int)(1 - K / 2); a.HPo = (int)HP; a.Po = 1; a.nch = (int)nch;
+  a.HPi = (int)HP; a.offi = (int)(1 - K / 2); a.HPo = (int)HP; a.Po = 1; a.nch = (int)nch; a.cw = cw;
   a.dgrad = 1;
   a.mbits_in = reinterpret_cast<const uint32_t*>(mbits.data_ptr<int>());
   TORCH_CHECK(B * HP * HP * 160 < (1ll << 31), "tensor too large for int32 offsets");
@@ -342,13 +352,13 @@ inline void conv_dgrad_fp8_bf16_impl(const Tensor& dz, const Tensor& w8t, const 
   CHECK_DEV(dz); CHECK_DEV(w8t); CHECK_DEV(mbits); CHECK_DEV(dx);
   CHECK_BF16(dz); CHECK_CONTIG(dz); CHECK_BF16(dx); CHECK_CONTIG(dx); CHECK_CONTIG(w8t);
   TORCH_CHECK(dz.dim() == 4 && dz.size(2) == dz.size(1) && dz.size(1) == S + 2, "dz (B, S+2, S+2, C) with pad 1");
-  TORCH_CHECK(w8t.scalar_type() == at::kByte && w8t.dim() == 3 && w8t.size(2) == 64, "w8t (nch, Cout, 64) e4m3");
+  TORCH_CHECK(w8t.scalar_type() == at::kByte && w8t.dim() == 3, "w8t (nch, Cout, cw) e4m3");
   TORCH_CHECK(scales.scalar_type() == at::kInt && scales.numel() >= 2, "scales int32[2] (E8M0)");
   TORCH_CHECK(in_scale.scalar_type() == at::kFloat && in_scale.numel() >= 1, "in_scale f32[1]");
   TORCH_CHECK(mbits.scalar_type() == at::kInt && mbits.is_contiguous(), "mbits int32");
   const int64_t B = dz.size(0), HP = dz.size(1), Cg = dz.size(3), nch = w8t.size(0), Cout = w8t.size(1);
-  TORCH_CHECK((Cg % 64 == 0 || Cg == 160) && (Cout % 64 == 0 || Cout == 160) && nch % 2 == 0 &&
-                  nch >= K * K * ((Cg + 63) / 64), "channel geometry (multiples of 64, or 160)");
+  TORCH_CHECK((Cg % 64 == 0 || Cg == 160) && (Cout % 64 == 0 || Cout == 160), "channel geometry (multiples of 64, or 160)");
+  const int cw = fp8_check_chunks(w8t, K, Cg, "conv_dgrad_fp8_bf16");
   TORCH_CHECK(dx.size(0) == B && dx.size(1) == HP && dx.size(2) == HP && dx.size(3) == Cout, "dx shape");
   const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
   TORCH_CHECK(mbits.numel() >= B * HP * HP * words, "mbits too small: need B*HPo*HPo*words");
@@ -367,7 +377,7 @@ inline void conv_dgrad_fp8_bf16_impl(const Tensor& dz, const Tensor& w8t, const 
   }
   a.dgrad_bf16 = 1;
   a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cg; a.Cout = (int)Cout; a.K = (int)K;
-  a.HPi = (int)HP; a.offi = 0; a.HPo = (int)HP; a.Po = 1; a.nch = (int)nch;
+  a.HPi = (int)HP; a.offi = 0; a.HPo = (int)HP; a.Po = 1; a.nch = (int)nch; a.cw = cw;
   if (a.M == 0) return;
   agk::launch_conv_fwd_fp8(a, cur_stream());
   launch_check("conv_dgrad_fp8_bf16");

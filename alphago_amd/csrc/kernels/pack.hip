@@ -205,4 +205,89 @@ void launch_sgd(float* p, const float* g, int64_t n, float lr, float gscale, hip
   hipLaunchKernelGGL(sgd_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, g, n, lr * gscale);
 }
 
+
+// ----------------------------------------------------------------- fused SGD + bf16 weight packs
+// One launch per step for the whole update (round 4; was sgd_kernel over the flat buffer, then
+// pack_weights_kernel, whose strided OIHW reads and transposed writes took ~25 us at every batch
+// size).  Job y < nlayers: a 32 (c) x 32 (n) tile of conv layer y -- each thread updates the K*K
+// taps of one (n, c) (contiguous in OIHW), writes the forward pack wf[t][n][c] (or the first layer's
+// packed-tap layout) directly and stages the transposed dgrad pack through LDS so that wd[t'][c][n]
+// is written along n.  Job y == nlayers: plain SGD over the remaining ranges (biases, head).
+namespace {
+__device__ __forceinline__ size_t wf_index(const SgdPackLayer& L, int t, int n, int c) {
+  if (L.pk_cpt > 0) {  // packed-tap first layer (conv_fwd_pk_kernel)
+    const int q = t * L.pk_cpt + (c >> 3);
+    return ((size_t)(q >> 3) * L.Cout_p + n) * 64 + (q & 7) * 8 + (c & 7);
+  }
+  return ((size_t)t * L.Cout_p + n) * L.Cin_p + c;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
+  __shared__ __bf16 tile[kSgdPackMaxTaps * 32 * 33];  // [t][c][n] (n padded to 33: no bank conflicts)
+  float step = a.lr * a.gscale;
+  if (a.sched) step = (float)a.sched[3] * a.gscale;  // == the sgd_dev_kernel step
+  if ((int)blockIdx.y == a.nlayers) {  // plain ranges
+    for (int r = 0; r < a.nranges; ++r) {
+      float* p = a.p + a.range_off[r];
+      const float* g = a.g + a.range_off[r];
+      for (int i = blockIdx.x * 256 + threadIdx.x; i < a.range_len[r]; i += gridDim.x * 256) p[i] -= step * g[i];
+    }
+    return;
+  }
+  const SgdPackLayer& L = a.layers[blockIdx.y];
+  const int T = L.K * L.K;
+  const int ctiles = (L.Cin_p + 31) >> 5;
+  const int ntiles = (L.Cout_p + 31) >> 5;
+  if ((int)blockIdx.x >= ctiles * ntiles) return;  // block-uniform: before any barrier
+  const int c0 = (blockIdx.x % ctiles) * 32, n0 = (blockIdx.x / ctiles) * 32;
+  const int cl = threadIdx.x & 31, nq = threadIdx.x >> 5;  // 8 groups of 4 n
+  const int c = c0 + cl;
+  float* P = a.p + L.off;
+  const float* G = a.g + L.off;
+#pragma unroll 1
+  for (int k = 0; k < 4; ++k) {
+    const int nl = nq * 4 + k;
+    const int n = n0 + nl;
+    const bool real = n < L.Cout_real && c < L.Cin_real;
+    const size_t base = ((size_t)n * L.Cin_real + c) * T;
+    for (int t = 0; t < T; ++t) {
+      float v = 0.f;
+      if (real) {
+        v = P[base + t] - step * G[base + t];
+        P[base + t] = v;
+      }
+      const __bf16 bv = (__bf16)v;
+      if (n < L.Cout_p && c < L.Cin_p) L.wf[wf_index(L, t, n, c)] = bv;
+      if (L.wd) tile[(t * 32 + cl) * 33 + nl] = bv;
+    }
+  }
+  if (!L.wd) return;  // layer-uniform
+  __syncthreads();
+  const int nl = threadIdx.x & 31, cq = threadIdx.x >> 5;
+  const int n = n0 + nl;
+  for (int t = 0; t < T; ++t) {
+    const int kh = t / L.K, kw = t - kh * L.K;
+    const int tf = (L.K - 1 - kh) * L.K + (L.K - 1 - kw);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cc = cq * 4 + k;
+      if (c0 + cc < L.Cin_p && n < L.Cout_p)
+        L.wd[((size_t)tf * L.Cin_p + c0 + cc) * L.Cout_p + n] = tile[(t * 32 + cc) * 33 + nl];
+    }
+  }
+}
+
+void launch_sgd_pack(const SgdPackArgs& a, hipStream_t st) {
+  if (a.sched) hipLaunchKernelGGL(sgd_sched_kernel, dim3(1), dim3(64), 0, st, a.sched);
+  int tiles = 1;
+  for (int i = 0; i < a.nlayers; ++i) {
+    const SgdPackLayer& L = a.layers[i];
+    const int t = ((L.Cin_p + 31) / 32) * ((L.Cout_p + 31) / 32);
+    if (t > tiles) tiles = t;
+  }
+  if (tiles < 64) tiles = 64;  // the plain-range job's blocks
+  hipLaunchKernelGGL(sgd_pack_kernel, dim3(tiles, a.nlayers + 1), dim3(256), 0, st, a);
+}
+
 }  // namespace agk

@@ -100,3 +100,79 @@ def teacher_pool(n: int, teacher, seed: int, chunk: int = 8192, threads: int = 1
         tgt[done:done + len(keep)] = lab[keep]
         done += len(keep)
     return planes, tgt
+
+
+def value_teacher(planes_dim: int = 49, filters: int = 152, layers: int = 12, device=None, seed: int = 4343,
+                  probe: np.ndarray = None, target_std: float = 1.0):
+    """A fixed random-init value network (reference value.py:12-31 architecture) used as the value
+    teacher.  A random init's pre-tanh outputs are nearly constant, so its last layer is rescaled so that
+    the pre-tanh values on ``probe`` positions have mean 0 and std ``target_std``: the teacher's tanh
+    outputs then spread over (-1, 1) and are a learnable regression target."""
+    import torch
+
+    from ..models.inference import make_value_inference
+    from ..models.nets import ValueNet
+
+    g = torch.random.get_rng_state()
+    torch.manual_seed(seed)
+    net = ValueNet(planes_dim, filters_per_layer=filters, layers=layers)
+    torch.random.set_rng_state(g)
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    net = net.to(dev)
+    if probe is not None and len(probe):
+        eng = make_value_inference(net, dev)
+        with torch.no_grad():
+            h = _value_pre_tanh(net, eng, probe)
+            net.fc2_w.mul_(target_std / max(float(h.std()), 1e-12))
+            net.fc2_b.copy_(net.fc2_b * 0 - float(h.mean()) * target_std / max(float(h.std()), 1e-12))
+    return net
+
+
+def _value_pre_tanh(net, eng, planes: np.ndarray):
+    """Pre-tanh outputs (atanh of the engine's values, clipped) of ``planes``."""
+    import torch
+
+    v = []
+    for i in range(0, len(planes), 1024):
+        out = eng.evaluate(planes[i:i + 1024])
+        out = out.float().cpu() if hasattr(out, "cpu") else torch.as_tensor(np.asarray(out, np.float32))
+        v.append(out.clone())
+    v = torch.cat(v).double().clamp(-1 + 1e-12, 1 - 1e-12)
+    return torch.atanh(v)
+
+
+def value_teacher_pool(n: int, teacher, seed: int, chunk: int = 8192, threads: int = 16,
+                       symmetrize: bool = True) -> Tuple[np.ndarray, np.ndarray]:
+    """(planes (n, 49, S, S) uint8, targets (n,) float32 in (-1, 1)): random-game positions featurised
+    into the value net's 49 planes (AlphaGo/models/value.py:16; the 48 policy planes + colour), each
+    labelled with the value teacher's tanh output averaged over the 8 board symmetries (so the D4
+    augmentation of the training step keeps the labels consistent)."""
+    import torch
+
+    from ..features import VALUE_FEATURES, Preprocess
+    from ..models.inference import make_value_inference
+
+    rng = np.random.default_rng(seed)
+    dev = next(teacher.parameters()).device
+    eng = make_value_inference(teacher, dev)
+    pre = Preprocess(VALUE_FEATURES)
+    S = teacher.board
+    planes = np.empty((n, pre.output_dim, S, S), np.uint8)
+    tgt = np.empty((n,), np.float32)
+    done = 0
+    while done < n:
+        sts = random_game_states(min(chunk, n - done), rng, size=S)
+        pl = pre.states_to_uint8(sts, threads)
+        acc = np.zeros(len(pl), np.float64)
+        for k, t in (_D4 if symmetrize else _D4[:1]):
+            sp = np.ascontiguousarray(_fwd(pl, k, t))
+            for i in range(0, len(sp), 1024):
+                out = eng.evaluate(sp[i:i + 1024])
+                out = out.float().cpu().numpy() if hasattr(out, "cpu") else np.asarray(out, np.float32)
+                acc[i:i + len(out)] += out
+        acc /= 8 if symmetrize else 1
+        planes[done:done + len(pl)] = pl
+        tgt[done:done + len(pl)] = acc.astype(np.float32)
+        done += len(pl)
+    del torch
+    return planes, tgt

@@ -205,6 +205,15 @@ def sgd_update(p, g, lr: float, gscale: float = 1.0):
     _ops().sgd_update(p, g, lr, gscale)
 
 
+def sgd_pack(p, g, lr: float, w_meta, wf, wd, ranges, sched=None, gscale: float = 1.0):
+    """Fused SGD step + bf16 weight packs in one launch (pack.hip sgd_pack_kernel): conv layer i's weights
+    at flat offset w_meta[i][0] with shape (Cout, Cin, K, K) = w_meta[i][1:]; plain SGD over ``ranges``
+    ((offset, length) pairs: biases, head); ``sched`` (device Keras schedule) replaces ``lr``."""
+    meta = [int(v) for m in w_meta for v in m]
+    _ops().sgd_pack(p, g, float(lr), sched, float(gscale), meta, list(wf), list(wd), [int(o) for o, _ in ranges],
+                    [int(n) for _, n in ranges])
+
+
 def dense_f32(A, B, C, bias=None, trans_a: bool = False, trans_b: bool = False, beta: float = 0.0):
     """C = beta*C + op(A) @ op(B) (+ bias) in exact fp32 on the f32 MFMA (value-head dense layers);
     op(X) = X.T when trans_* (read in place, no copies)."""
@@ -349,12 +358,28 @@ def fp8_nchunks(K: int, cin_p: int) -> int:
     return n + (n & 1)
 
 
+def fp8_chunk_width(cin_p: int) -> int:
+    """Channels per packed fp8 weight chunk: 32 for 160-channel reductions (the value width: five
+    32-channel chunks per tap, no zero half; ALPHAGO_AMD_FP8_CW32=0 restores 64), else 64."""
+    return 32 if cin_p == 160 and os.environ.get("ALPHAGO_AMD_FP8_CW32", "1") == "1" else 64
+
+
+def fp8_weight_shape(K: int, cin_p: int, rows_p: int):
+    """Shape of packed e4m3 weights reducing over cin_p channels (forward: input channels; transposed
+    dgrad pack: output channels) with rows_p rows: (chunks, rows_p, chunk width); the chunk count
+    covers K*K taps and is a multiple of the chunks per 128-K step."""
+    cw = fp8_chunk_width(cin_p)
+    per = 128 // cw
+    n = K * K * ((cin_p + cw - 1) // cw)
+    return ((n + per - 1) // per * per, rows_p, cw)
+
+
 def pack_weights_fp8(w_oihw: torch.Tensor, cout_p: int, cin_p: int, exponent=None):
     """fp32 OIHW -> (uint8 e4m3 (nch, cout_p, 64) scaled by 2^e, e)."""
     w = w_oihw.detach().float().contiguous()
     if exponent is None:
         exponent = fp8_exponent(float(w.abs().max()), margin=0)
-    out = torch.empty((fp8_nchunks(w.shape[2], cin_p), cout_p, 64), dtype=torch.uint8, device=w.device)
+    out = torch.empty(fp8_weight_shape(w.shape[2], cin_p, cout_p), dtype=torch.uint8, device=w.device)
     _ops().pack_weights_fp8(w, out, float(2.0 ** exponent), None)
     return out, exponent
 

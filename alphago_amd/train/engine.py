@@ -251,7 +251,7 @@ class HipConvTrainer:
             # weights from their amax at every repack, activations delayed by
             # one step from the amax the fp8 kernels accumulate.
             L = self.L
-            self.w8 = [torch.zeros((ops.fp8_nchunks(self.K[l], self.C0p if l == 0 else self.Fp), self.Fp, 64),
+            self.w8 = [torch.zeros(ops.fp8_weight_shape(self.K[l], self.C0p if l == 0 else self.Fp, self.Fp),
                                    dtype=torch.uint8, device=dev) for l in range(L)]
             self.wscale8 = torch.ones(L, device=dev)
             self.scales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
@@ -269,7 +269,7 @@ class HipConvTrainer:
             # e5m2 in registers (no quantisation pass, no e5m2 tensor), takes ReLU' from the
             # forward's bitmask, and the transposed packs ride the one batched repack launch.
             self.fp8_dgrad = bool(fp8_dgrad)  # resolved below once fp8_wgrad is known
-            self.wd8 = [None] + [torch.zeros((ops.fp8_nchunks(self.K[l], self.Fp), self.Fp, 64), dtype=torch.uint8,
+            self.wd8 = [None] + [torch.zeros(ops.fp8_weight_shape(self.K[l], self.Fp, self.Fp), dtype=torch.uint8,
                                              device=dev) for l in range(1, L)]
             self.gscales8 = torch.full((L, 2), 127, dtype=torch.int32, device=dev)
             self.gosc8 = torch.ones(L, device=dev)
@@ -308,6 +308,9 @@ class HipConvTrainer:
         # Keras-SGD schedule mirrored on the device (float64 {lr0, decay, iterations, lr}) so that
         # the SGD step reads its learning rate from memory: the whole step is graph-capturable
         self._sched_dev = torch.zeros(4, dtype=torch.float64, device=dev)
+        # fused SGD + bf16 packs (ops.sgd_pack); ALPHAGO_AMD_FUSED_UPDATE=0: sgd_update + pack_weights
+        self._fused_update = os.environ.get("ALPHAGO_AMD_FUSED_UPDATE", "1") == "1"
+        self._pack_plan = None
         self.use_graph = False
         self._graphs = None
         self._g_in = None
@@ -348,11 +351,14 @@ class HipConvTrainer:
         raise NotImplementedError
 
     # ------------------------------------------------------------------ helpers
-    def repack(self) -> None:
+    def repack(self, bf16: bool = True) -> None:
+        """Device copies of the master weights the kernels read: padded biases, the bf16 packs (unless
+        the fused update already wrote them: ``bf16=False``) and the fp8 packs."""
         if not self._bias_alias:
             torch._foreach_copy_([b[:self.F] for b in self.bias_p], [self.fp.views["b%d" % l] for l in range(self.L)])
         ws = [self.fp.views["w%d" % l] for l in range(self.L)]
-        ops.pack_weights(ws, self.wf, self.wd)
+        if bf16:
+            ops.pack_weights(ws, self.wf, self.wd)
         if self.precision == "fp8":
             ops.fp8_weight_scales(ws, self.wscale8, self.scales8)
             # every e4m3 pack of the step (forward, and the transposed dgrad packs) in ONE launch
@@ -553,8 +559,37 @@ class HipConvTrainer:
         with trace_range("backward+allreduce"):
             self.backward_trunk(reduce)
 
+    def _sgd_pack_plan(self):
+        """(per-layer (flat offset, Cout, Cin, K, K), plain SGD ranges) of the fused update."""
+        meta, wsegs = [], set()
+        for l in range(self.L):
+            off, n = self.fp.segments["w%d" % l]
+            w = self.fp.views["w%d" % l]
+            meta.append((off, w.shape[0], w.shape[1], w.shape[2]))
+            wsegs.add(off)
+        ranges = []
+        for name in self.fp.names:
+            off, n = self.fp.segments[name]
+            if off in wsegs:
+                continue
+            if ranges and ranges[-1][0] + ranges[-1][1] == off:
+                ranges[-1] = (ranges[-1][0], ranges[-1][1] + n)
+            else:
+                ranges.append((off, n))
+        return meta, ranges
+
     def apply_update(self, device_schedule: bool = False) -> None:
         with trace_range("sgd+repack"):
+            if self._fused_update:
+                # one launch: SGD over the flat master weights + the bf16 forward / dgrad packs
+                if self._pack_plan is None:
+                    self._pack_plan = self._sgd_pack_plan()
+                meta, ranges = self._pack_plan
+                ops.sgd_pack(self.fp.flat, self.fp.grad, 0.0 if device_schedule else self.sched.current(), meta,
+                             self.wf, self.wd, ranges, sched=self._sched_dev if device_schedule else None)
+                self.sched.advance()
+                self.repack(bf16=False)
+                return
             if device_schedule:
                 # graph replays: lr = lr0 / (1 + decay * t) evaluated on the device (the same f64
                 # expression as KerasSGDSchedule.current()) from the copy synced at capture time

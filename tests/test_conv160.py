@@ -118,10 +118,12 @@ def test_conv_wgrad_160(ops, cuda_device, B, Cin, Cin_p, K, Pin, variant):
 
 
 @pytest.mark.parametrize("B,Cin,Cin_p,K", [(5, 152, 160, 3), (3, 49, 64, 5)])
-def test_conv_fwd_fp8_160(ops, cuda_device, B, Cin, Cin_p, K):
+@pytest.mark.parametrize("cw", [32, 64])
+def test_conv_fwd_fp8_160(ops, cuda_device, monkeypatch, cw, B, Cin, Cin_p, K):
     """e4m3 conv with 160-channel activations (three 64-channel chunks per tap,
     the third one's upper half reads the next pixel against zero weights) and a
     160-wide output tile vs fp32 conv of the dequantised operands."""
+    monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1" if cw == 32 else "0")  # 160-channel packs: 32 / 64-channel chunks
     torch.manual_seed(3)
     S, P, Cout, Cp = 19, K // 2, 152, 160
     x = F.relu(torch.randn(B, Cin, S, S, device=cuda_device)) * 3.0
@@ -134,7 +136,7 @@ def test_conv_fwd_fp8_160(ops, cuda_device, B, Cin, Cin_p, K):
     x8 = torch.empty(xp.shape, dtype=torch.uint8, device=cuda_device)
     ops.quantize_fp8(xp, x8, ex)
     w8, ew = ops.pack_weights_fp8(w, Cp, Cin_p)
-    assert w8.shape[0] == ops.fp8_nchunks(K, Cin_p)
+    assert tuple(w8.shape) == ops.fp8_weight_shape(K, Cin_p, Cp)
     xq = ops.fp8_to_float(x8, ex)[:, P:P + S, P:P + S, :Cin].permute(0, 3, 1, 2)
     wq = (w * 2.0 ** ew).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** -ew
     ref = F.relu(F.conv2d(xq, wq, b, padding=P))
@@ -166,9 +168,11 @@ def test_conv_fwd_fp8_160(ops, cuda_device, B, Cin, Cin_p, K):
 
 
 @pytest.mark.parametrize("C,Cp", [(152, 160), (192, 192)])
-def test_conv_dgrad_fp8(ops, cuda_device, C, Cp):
+@pytest.mark.parametrize("cw", [32, 64])
+def test_conv_dgrad_fp8(ops, cuda_device, monkeypatch, cw, C, Cp):
     """fp8 dgrad (e5m2 gradients x transposed e4m3 weights on the block-scaled MFMA)
     masked by the bf16 activation vs fp32 conv2d_input of the dequantised operands."""
+    monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1" if cw == 32 else "0")  # 160-channel packs: 32 / 64-channel chunks
     torch.manual_seed(4)
     B, S, K = 3, 19, 3
     dz = torch.randn(B, C, S, S, device=cuda_device) * 1e-3
@@ -181,7 +185,7 @@ def test_conv_dgrad_fp8(ops, cuda_device, C, Cp):
     ops.quantize_bf8(dzp, dz8, torch.tensor([2.0 ** eg], device=cuda_device), amax_in)
     assert abs(amax_in.view(torch.float32).max().item() - _bf(dz).abs().max().item()) < 1e-6
     ew = ops.fp8_exponent(float(w.abs().max()), margin=0)
-    w8t = torch.zeros((ops.fp8_nchunks(K, Cp), Cp, 64), dtype=torch.uint8, device=cuda_device)
+    w8t = torch.zeros(ops.fp8_weight_shape(K, Cp, Cp), dtype=torch.uint8, device=cuda_device)
     ops.pack_weights_fp8_into(w, w8t, torch.tensor([2.0 ** ew], device=cuda_device), transposed=True)
     dzq = ops.bf8_to_float(dz8, eg)[:, 1:S + 1, 1:S + 1, :C].permute(0, 3, 1, 2)
     wq = (w * 2.0 ** ew).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** -ew
@@ -202,10 +206,12 @@ def test_conv_dgrad_fp8(ops, cuda_device, C, Cp):
 
 
 @pytest.mark.parametrize("C,Cp,B", [(152, 160, 3), (192, 192, 3), (192, 192, 7)])
-def test_conv_dgrad_fp8_bf16_operand(ops, cuda_device, C, Cp, B):
+@pytest.mark.parametrize("cw", [32, 64])
+def test_conv_dgrad_fp8_bf16_operand(ops, cuda_device, monkeypatch, cw, C, Cp, B):
     """fp8 dgrad straight from the bf16 gradient (converted to e5m2 in the kernel's registers,
     ReLU' from the forward's bitmask, bf16 output) vs fp32 conv2d_input of the dequantised
     operands: e5m2(dZ * 2^eg) * 2^-eg and e4m3 weights."""
+    monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1" if cw == 32 else "0")  # 160-channel packs: 32 / 64-channel chunks
     torch.manual_seed(6)
     S, K = 19, 3
     xin = _bf(torch.randn(B, C, S, S, device=cuda_device))
@@ -221,7 +227,7 @@ def test_conv_dgrad_fp8_bf16_operand(ops, cuda_device, C, Cp, B):
     w = torch.randn(C, C, K, K, device=cuda_device) * 0.05
     eg = ops.fp8_exponent(float(dz.abs().max()), margin=0) + 7
     ew = ops.fp8_exponent(float(w.abs().max()), margin=0)
-    w8t = torch.zeros((ops.fp8_nchunks(K, Cp), Cp, 64), dtype=torch.uint8, device=cuda_device)
+    w8t = torch.zeros(ops.fp8_weight_shape(K, Cp, Cp), dtype=torch.uint8, device=cuda_device)
     ops.pack_weights_fp8_multi([w], [w8t], torch.tensor([2.0 ** ew], device=cuda_device), [0], [1])
     dzq = (dz * 2.0 ** eg).clamp(-57344, 57344).to(torch.float8_e5m2).float() * 2.0 ** -eg
     wq = (w * 2.0 ** ew).clamp(-448, 448).to(torch.float8_e4m3fn).float() * 2.0 ** -ew
@@ -241,9 +247,11 @@ def test_conv_dgrad_fp8_bf16_operand(ops, cuda_device, C, Cp, B):
 
 
 @pytest.mark.parametrize("B,outs", [(3, "fp8"), (5, "bf16"), (2, "both")])
-def test_conv_dgrad_fp8_bits(ops, cuda_device, B, outs):
+@pytest.mark.parametrize("cw", [32, 64])
+def test_conv_dgrad_fp8_bits(ops, cuda_device, monkeypatch, cw, B, outs):
     """All-fp8 value backward: dgrad from the e5m2 dZ copy (the one the fp8 wgrad reads), ReLU' from
     the forward's bitmask, e5m2 and/or bf16 outputs vs fp32 conv2d_input of the dequantised operands."""
+    monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1" if cw == 32 else "0")  # 160-channel packs: 32 / 64-channel chunks
     torch.manual_seed(16)
     S, K, C, Cp = 19, 3, 152, 160
     xin = _bf(torch.randn(B, C, S, S, device=cuda_device))
@@ -258,7 +266,7 @@ def test_conv_dgrad_fp8_bits(ops, cuda_device, B, outs):
     w = torch.randn(C, C, K, K, device=cuda_device) * 0.05
     eg = ops.fp8_exponent(float(dz.abs().max()), margin=0) + 7
     ew = ops.fp8_exponent(float(w.abs().max()), margin=0)
-    w8t = torch.zeros((ops.fp8_nchunks(K, Cp), Cp, 64), dtype=torch.uint8, device=cuda_device)
+    w8t = torch.zeros(ops.fp8_weight_shape(K, Cp, Cp), dtype=torch.uint8, device=cuda_device)
     ops.pack_weights_fp8_multi([w], [w8t], torch.tensor([2.0 ** ew], device=cuda_device), [0], [1])
     dz8 = torch.zeros((B, S + 2, S + 2, Cp), dtype=torch.uint8, device=cuda_device)
     dz8[:, 1:S + 1, 1:S + 1, :C] = (dz * 2.0 ** eg).clamp(-57344, 57344).to(torch.float8_e5m2).view(
@@ -290,19 +298,21 @@ def test_conv_dgrad_fp8_bits(ops, cuda_device, B, outs):
 
 
 @pytest.mark.parametrize("Cin,Cout,K", [(152, 152, 3), (49, 152, 5), (192, 192, 3), (48, 192, 5)])
-def test_pack_weights_fp8_multi_matches_single(ops, cuda_device, Cin, Cout, K):
+@pytest.mark.parametrize("cw", [32, 64])
+def test_pack_weights_fp8_multi_matches_single(ops, cuda_device, monkeypatch, cw, Cin, Cout, K):
     """The one-launch fp8 repack equals the per-layer packs, forward and transposed."""
+    monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1" if cw == 32 else "0")  # 160-channel packs: 32 / 64-channel chunks
     torch.manual_seed(8)
     w = torch.randn(Cout, Cin, K, K, device=cuda_device) * 0.05
     cout_p, cin_p = ops.pad_filters(Cout), (ops.pad_filters(Cin) if Cin > 64 else 64)
     sc = torch.tensor([4.0, 8.0], device=cuda_device)
-    a = torch.zeros((ops.fp8_nchunks(K, cin_p), cout_p, 64), dtype=torch.uint8, device=cuda_device)
+    a = torch.zeros(ops.fp8_weight_shape(K, cin_p, cout_p), dtype=torch.uint8, device=cuda_device)
     b = torch.zeros_like(a)
     ops.pack_weights_fp8_into(w, a, sc[1:2])
     outs = [b]
     tr = Cin == Cout
     if tr:
-        at = torch.zeros((ops.fp8_nchunks(K, cout_p), cin_p, 64), dtype=torch.uint8, device=cuda_device)
+        at = torch.zeros(ops.fp8_weight_shape(K, cout_p, cin_p), dtype=torch.uint8, device=cuda_device)
         bt = torch.zeros_like(at)
         ops.pack_weights_fp8_into(w, at, sc[1:2], transposed=True)
         outs.append(bt)

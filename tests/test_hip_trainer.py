@@ -227,3 +227,38 @@ def test_hip_trunk_small_boards_match_torch(cuda_device, S, F, L):
     probs = HipTrunkInference(net, cuda_device, buckets=(B,)).evaluate(planes.cpu().numpy())
     assert probs.shape == (B, S * S)
     assert torch.allclose(probs.float().sum(1), torch.ones(B, device=probs.device), atol=1e-3)
+
+
+@pytest.mark.parametrize("kind,F,C,B", [("policy", 192, 48, 6), ("value", 152, 49, 5), ("policy", 64, 12, 3)])
+def test_fused_sgd_pack_matches_separate_update(cuda_device, monkeypatch, kind, F, C, B):
+    """The fused update (ops.sgd_pack: SGD + bf16 forward / transposed / packed-tap packs in one launch)
+    leaves the same master weights and the same packed copies as sgd_update followed by pack_weights,
+    eager and with the device schedule (graph-mode path)."""
+    import copy
+
+    from alphago_amd.models.nets import PolicyNet, ValueNet
+    from alphago_amd.train.engine import HipPolicyTrainer, HipValueTrainer
+
+    torch.manual_seed(3)
+    net = PolicyNet(C, filters_per_layer=F, layers=3) if kind == "policy" else ValueNet(C, filters_per_layer=F, layers=3)
+    cls = HipPolicyTrainer if kind == "policy" else HipValueTrainer
+    trs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("ALPHAGO_AMD_FUSED_UPDATE", fused)
+        trs.append(cls(copy.deepcopy(net), B, lr=0.05, decay=0.01, device=cuda_device))
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    tgt = (torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device) if kind == "policy"
+           else torch.rand(B, device=cuda_device) * 2 - 1)
+    for t in trs:
+        t.step(planes, tgt)
+        t.sync_schedule()
+        t.compute_grads(planes, tgt)
+        t.apply_update(device_schedule=True)
+    torch.cuda.synchronize()
+    a, b = trs
+    assert a._fused_update and not b._fused_update
+    assert torch.allclose(a.fp.flat, b.fp.flat, rtol=0, atol=1e-7)
+    for l in range(3):
+        assert torch.equal(a.wf[l], b.wf[l]), l
+        assert torch.equal(a.wd[l], b.wd[l]), l
+    assert torch.equal(a._sched_dev, b._sched_dev)

@@ -107,7 +107,7 @@ def test_reinforce_sign():
 
     torch.manual_seed(0)
     pol = _policy(torch.device("cpu"))
-    tr = TorchPolicyTrainer(pol.model, 16, lr=1.0)
+    tr = TorchPolicyTrainer(pol.model, 16, lr=1.0, device="cpu")
     gs = go.GameState(9)
     planes = pol.preprocessor.states_to_uint8([gs])
     rec = GameRecords(planes=[planes, planes], moves=[np.array([40]), np.array([0])], winners=[1, 1],
