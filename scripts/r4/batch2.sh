@@ -21,3 +21,5 @@ step value_parity 600 python3 -u scripts/value_fp8_parity.py $O/value_parity.jso
 step genmove 300 python3 -u benchmarks/genmove_benchmark.py --playouts 1600 --leaves 8,16,32 --moves 4
 step value_fp8 200 python3 -u benchmarks/value_training_benchmark.py --precision fp8 --steps 30 --warmup 10
 step value_bf16 200 python3 -u benchmarks/value_training_benchmark.py --precision bf16 --steps 30 --warmup 10
+step prof 300 bash scripts/profile_step.sh $O/prof --steps 20 --warmup 5
+f=$(ls $O/prof/*/*kernel_trace.csv $O/prof/*kernel_trace.csv 2>/dev/null | head -1); [ -n "$f" ] && python3 scripts/timeline.py "$f" 5 > $O/timeline.txt 2>&1; cat $O/timeline.txt | head -30

@@ -4,7 +4,7 @@ f = sys.argv[1]; steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 rows = [r for r in csv.DictReader(open(f))]
 ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows), key=lambda t: t[0])
 # step boundary = sgd_kernel end
-ends = [i for i, k in enumerate(ks) if "sgd_kernel" in k[2]]
+ends = [i for i, k in enumerate(ks) if "sgd_kernel" in k[2] or "sgd_pack_kernel" in k[2]]
 if len(ends) < steps + 1:
     print("not enough steps"); sys.exit()
 lo, hi = ends[-steps - 1] + 1, ends[-1]

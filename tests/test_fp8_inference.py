@@ -211,3 +211,64 @@ def test_tr8_transpose_read_mapping(cuda_device):
             exp[lane, q] = host[g * 512 + q * stride + i]
     print("lane 0..3 got", got[:4].tolist())
     assert np.array_equal(got, exp)
+
+
+def _emulated_fp8_value_grads(net, planes, z, wscale, osc):
+    """fp32 autograd of the quantised value-net forward the fp8 trainer ran: e4m3 weights (per-layer
+    power-of-two wscale), e4m3 activations with this step's delayed multipliers osc (ReLU outputs,
+    saturating at 448), bf16 last activation, fp32 head; the quantisers pass gradients straight through
+    (as the HIP backward does)."""
+    import torch.nn.functional as F
+
+    def ste(x, q):
+        return x + (q - x).detach()
+
+    h = planes.float()
+    L = len(net.trunk.weights)
+    for l, (w, b, k) in enumerate(zip(net.trunk.weights, net.trunk.biases, net.trunk.widths)):
+        s = float(wscale[l])
+        wq = ste(w, (w.detach() * s).clamp(-448, 448).to(torch.float8_e4m3fn).float() / s)
+        y = F.relu(F.conv2d(h, wq, b, padding=k // 2))
+        if l < L - 1:
+            o = float(osc[l])
+            h = ste(y, (y.detach() * o).clamp(max=448).to(torch.float8_e4m3fn).float() / o)
+        else:
+            h = ste(y, y.detach().bfloat16().float())
+    zz = F.conv2d(h, net.head_w, net.head_b).flatten(1)
+    v = torch.tanh((zz @ net.fc1_w + net.fc1_b) @ net.fc2_w + net.fc2_b).squeeze(1)
+    loss = ((v - z) ** 2).sum() / len(z)
+    names = ["w%d" % l for l in range(L)]
+    g = torch.autograd.grad(loss, list(net.trunk.weights))
+    return dict(zip(names, g))
+
+
+def test_fp8_backward_12_layer_trunk_matches_exact_backward(cuda_device):
+    """The all-fp8 backward (e5m2 dZ x e4m3 weights dgrad, e5m2 dZ x e4m3 X wgrad) on the full 12 x 152
+    value trunk: every layer's weight gradient has cosine >= 0.95 with the exact fp32 gradient of the
+    same quantised forward (emulated in torch with the trainer's own scales).  The fp8-vs-bf16 gradient
+    gap at random init (~0.7) comes from the e4m3 FORWARD -- a different function -- not from the
+    backward kernels (profiles/r4/fp8_grad_sim.json: e5m2 gradients alone keep 0.98)."""
+    import copy
+
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import HipValueTrainer
+
+    torch.manual_seed(4)
+    B = 64
+    net = ValueNet(49, filters_per_layer=152, layers=12)
+    ref = copy.deepcopy(net).to(cuda_device)
+    planes = _planes(B, 49, seed=11).to(cuda_device)
+    z = torch.rand(B, device=cuda_device) * 2 - 1
+    t8 = HipValueTrainer(net, B, lr=0.0, device=cuda_device, precision="fp8")
+    assert t8.fp8_wgrad and t8.fp8_dgrad
+    t8.compute_grads(planes, z)  # calibrates the activation and gradient scales
+    osc = t8.osc8.clone()        # the delayed multipliers the next forward uses
+    wscale = t8.wscale8.clone()
+    t8.compute_grads(planes, z)  # all-fp8 step
+    torch.cuda.synchronize()
+    g_ref = _emulated_fp8_value_grads(ref, planes, z, wscale.cpu(), osc.cpu())
+    for l in range(12):
+        a, b = t8.fp.grad_views["w%d" % l].double().flatten(), g_ref["w%d" % l].double().flatten()
+        cos = torch.nn.functional.cosine_similarity(a, b, dim=0).item()
+        ratio = (a.norm() / b.norm()).item()
+        assert cos >= 0.95 and 0.8 < ratio < 1.25, (l, cos, ratio)
