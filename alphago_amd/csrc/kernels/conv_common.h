@@ -42,6 +42,24 @@ __device__ __forceinline__ void vmcnt_wait() {
   else static_assert(N < 0, "unsupported vmcnt");
 }
 
+// s_waitcnt vmcnt(N) for any immediate N (gfx950: 0..63)
+template <int N>
+__device__ __forceinline__ void vmcnt_n() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS-ring wait: at most `later` stages of PW DMA instructions each may still be outstanding
+// (later = 0 .. MAXL, wave-uniform); the exact count, not a clamped one, so the ring keeps its depth
+template <int PW, int MAXL>
+__device__ __forceinline__ void ring_wait(int later) {
+  static_assert(MAXL >= 0 && MAXL <= 3 && PW * MAXL <= 63, "ring depth");
+  if (MAXL >= 3 && later >= 3) vmcnt_n<PW * (MAXL >= 3 ? 3 : 0)>();
+  else if (MAXL >= 2 && later >= 2) vmcnt_n<PW * (MAXL >= 2 ? 2 : 0)>();
+  else if (MAXL >= 1 && later >= 1) vmcnt_n<PW * (MAXL >= 1 ? 1 : 0)>();
+  else vmcnt_n<0>();
+}
+
 __device__ __forceinline__ void vmcnt_wait_dyn(int n) {
   switch (n) {
     case 0: vmcnt_wait<0>(); break;

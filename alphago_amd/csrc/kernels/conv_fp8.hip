@@ -306,11 +306,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     wsrc[i] = (((lc / (CW / 16)) * a.Cout) + n0 + (r < BN ? r : BN - 1)) * CW + (lc % (CW / 16)) * 16;
     wdst[i] = r * 128 + pc * 16;
   }
-  auto chunk_off = [&](int q) {
+  auto chunk_off = [&](int q) {  // wave-uniform; divisions by the launcher's exact fast divisors
     q = q < qmax ? q : qmax;
-    const int t = q / CC;
+    const int t = (int)fdiv((uint32_t)q, a.divCC);
     const int c = q - t * CC;
-    const int kh = t / a.K;
+    const int kh = (int)fdiv((uint32_t)t, a.divK);
     const int kw = t - kh * a.K;
     return (kh * a.HPi + kw) * a.Cin + c * CW;
   };
@@ -643,6 +643,10 @@ void launch_conv_fwd_fp8(const ConvFp8Args& a_in, hipStream_t st) {
   ConvFp8Args a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
+  const int cw = a.cw ? a.cw : 64;
+  a.cw = cw;
+  a.divCC = make_fastdiv((uint32_t)((a.Cin + cw - 1) / cw));  // chunks per tap
+  a.divK = make_fastdiv((uint32_t)a.K);
   if (a.dgrad_bf16) {
     if (a.Cout == 160) launch_fp8_dgrad_bf16<160>(a, st);
     else if (a.Cout % 192 == 0) launch_fp8_dgrad_bf16<192>(a, st);

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     for (int ks = 0; ks < nK; ++ks) {
       // step ks has landed once at most (stages issued after it) x PW DMAs are outstanding
       const int later = (nK - 1 - ks) < (NS - 2) ? (nK - 1 - ks) : (NS - 2);
-      vmcnt_wait_dyn(later * PW);
+      ring_wait<PW, NS - 2>(later);
       __syncthreads();  // every wave's DMA of step ks is visible; slot (ks - 1) % NS is free
       if (ks + NS - 1 < nK) stage((ks + NS - 1) % NS);
       const char* base = smem + (ks % NS) * STAGE;
@@ -757,7 +757,7 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
     int cur = (ks - ks_begin) & 1;
     if constexpr (RING) {
       const int later = (ks_end - 1 - ks) < (NS - 2) ? (ks_end - 1 - ks) : (NS - 2);
-      vmcnt_wait_dyn(later * IPW);
+      ring_wait<IPW, (NS > 2 ? NS - 2 : 0)>(later);
       __syncthreads();  // stage ks visible to every wave; the slot read last step is free
       cur = (ks - ks_begin) % NS;
       if (ks + NS - 1 < ks_end) stage(ks + NS - 1, (ks - ks_begin + NS - 1) % NS);

@@ -165,6 +165,7 @@ struct ConvFp8Args {
   int nch;                  // packed chunks (cw channels each; a K-step holds 128 / cw chunks)
   int cw;                   // chunk width: 64, or 32 for 160-channel operands packed in 32-channel chunks
   FastDiv divSS, divS;      // filled by the launcher
+  FastDiv divCC, divK;      // chunks per tap, kernel width (launcher)
   int variant;              // 0 = production (pixel operand from L2, 48 px/wave); lab: 1, 3, 4 other tilings,
                             // 5 = LDS-staged operands
   // dgrad mode (production kernel only): x holds e5m2 gradients, w the transposed/flipped e4m3

@@ -243,6 +243,9 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
   const int c0 = (blockIdx.x % ctiles) * 32, n0 = (blockIdx.x / ctiles) * 32;
   const int cl = threadIdx.x & 31, nq = threadIdx.x >> 5;  // 8 groups of 4 n
   const int c = c0 + cl;
+  // packed-tap layout: channels past the last chunk of a tap have no slot (their index would alias the
+  // next tap's first chunk)
+  const int cslots = L.pk_cpt > 0 ? L.pk_cpt * 8 : L.Cin_p;
   float* P = a.p + L.off;
   const float* G = a.g + L.off;
 #pragma unroll 1
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
         P[base + t] = v;
       }
       const __bf16 bv = (__bf16)v;
-      if (n < L.Cout_p && c < L.Cin_p) L.wf[wf_index(L, t, n, c)] = bv;
+      if (n < L.Cout_p && c < cslots) L.wf[wf_index(L, t, n, c)] = bv;
       if (L.wd) tile[(t * 32 + cl) * 33 + nl] = bv;
     }
   }
