@@ -146,6 +146,26 @@ void launch_conv_fwd_pk(const ConvFwdArgs& a_in, int cpt, hipStream_t st) {
 
 // ----------------------------------------------------------------- wgrad launchers
 
+static int wgrad0_occ3() {
+  static const int on = [] {
+    const char* e = getenv("AGK_WGRAD0_OCC3");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return on;
+}
+
+template <int WN, int TAPS, int MW>
+static void launch_wgrad_taps48(const ConvWgradArgs& a, hipStream_t st) {
+  constexpr int smem = 2 * (WN + 48 * TAPS) * 64 * kWgradKsub;
+  static const hipError_t attr48 = hipFuncSetAttribute(
+      (const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, 2, MW>,
+      hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  hip_check(attr48, "hipFuncSetAttribute(max dynamic LDS)");
+  dim3 grid(a.nsplit, a.T / TAPS, a.Cout / WN);
+  hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, 2, MW>), grid, dim3(384),
+                     smem, st, a);
+}
+
 template <int WN, int TAPS>
 static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
   if (a.cin_real <= 48) {
@@ -153,12 +173,8 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
     // waves (2 n x 3 c) skips the zero channels -- 25% fewer MFMAs and x bytes
     // on the backward's serial tail; the slab columns 48..63 stay unwritten
     // (the reduce reads only cin_real of them)
-    constexpr int smem = 2 * (WN + 48 * TAPS) * 64 * kWgradKsub;
-    static const hipError_t attr48 = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
-  hip_check(attr48, "hipFuncSetAttribute(max dynamic LDS)");
-    dim3 grid(a.nsplit, a.T / TAPS, a.Cout / WN);
-    hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS>), grid, dim3(384), smem, st, a);
+    if (TAPS == 5 && wgrad0_occ3()) launch_wgrad_taps48<WN, TAPS, 3>(a, st);
+    else launch_wgrad_taps48<WN, TAPS, 0>(a, st);
     return;
   }
   constexpr int smem = 2 * (WN + 64 * TAPS) * 64 * kWgradKsub;

@@ -1074,9 +1074,14 @@ __device__ __forceinline__ void wgrad_tile_line(const ConvWgradArgs& a, int spli
 }
 
 // LINE && !PAIR: two 8-wave workgroups per CU like the production per-tap kernel (<= 128 VGPRs)
+// MW: minimum waves per SIMD the register allocation must allow (0: the default -- 4 for the line-staged
+// lab kernel, else 1).  The thin first layer's tap-merged rows (48-wide c tile, 6 waves) take 180 VGPRs,
+// which fits ONE workgroup per CU; MW = 3 caps them at 168 (11 dwords spilled) so that two share a CU
+// (AGK_WGRAD0_OCC3=1, round 4 A/B).
 template <int WN, int WC, int KSUB, int NWC = 4, int TAPS = 1, bool PAIR = false, bool LINE = false, bool ILVW = false,
-          int NS = 2>
-__global__ __launch_bounds__(128 * NWC, (LINE && !PAIR) ? 4 : 1) void conv_wgrad_kernel(ConvWgradArgs a) {
+          int NS = 2, int MW = 0>
+__global__ __launch_bounds__(128 * NWC, (MW > 0 ? MW : (LINE && !PAIR) ? 4 : 1)) void conv_wgrad_kernel(
+    ConvWgradArgs a) {
   static_assert(!PAIR || TAPS == 2, "PAIR: two taps per workgroup");
   // workgroup -> (split, tap group, channel block).  xcd_group (tap-merged rows): the hardware
   // deals workgroups to the 8 XCDs round robin in launch order, which puts the K kernel-row

@@ -7,6 +7,12 @@ export PYTHONPATH=$PWD
 source scripts/r4/lib.sh
 step kernels 600 python3 -u -m pytest tests/test_hip_kernels.py tests/test_conv160.py tests/test_hip_trainer.py tests/test_fp8_inference.py tests/test_lockstep.py -m gpu -x -q --timeout 120 --timeout-method thread
 step bench2176 240 python3 bench.py --gpus 1 --steps 20 --warmup 5
+# same-box A/Bs of this round's bench-path changes (each arm 100 steps)
+step ab_new 200 python3 bench.py --steps 100 --warmup 20
+step ab_pk0 200 env ALPHAGO_AMD_PK=0 python3 bench.py --steps 100 --warmup 20
+step ab_fused0 200 env ALPHAGO_AMD_FUSED_UPDATE=0 python3 bench.py --steps 100 --warmup 20
+step ab_occ3 200 env AGK_WGRAD0_OCC3=1 python3 bench.py --steps 100 --warmup 20
+step ab_new2 200 python3 bench.py --steps 100 --warmup 20
 step kbench 200 python3 -u scripts/r4/small_batch_kbench.py 1 4 16 64 256
 for B in 16 64 256; do
   for T in 0 65; do
