@@ -35,8 +35,13 @@ void conv_fwd_pk(const Tensor& x, const Tensor& w, const Tensor& bias, const Ten
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
                 int64_t Pin, int64_t Po, int64_t cin_real, int64_t variant) {
   check_dev("conv_wgrad", x, dz, slab, dbslab);
-  // production kernels only: 0 = per-tap kernel (default), 5 = one-kernel-row wgrad where it applies
-  TORCH_CHECK(variant == 0 || variant == 5, "conv_wgrad variant ", variant, " is not a production kernel (0, 5)");
+  // 0 = per-tap kernel (default), 9 = 4-slot LDS-ring kernel (small batches); the lab build also has
+  // 5 = one-kernel-row wgrad
+#ifdef AGK_KERNEL_LAB
+  TORCH_CHECK(variant == 0 || variant == 5 || variant == 9, "conv_wgrad variant ", variant, " unknown (0, 5, 9)");
+#else
+  TORCH_CHECK(variant == 0 || variant == 9, "conv_wgrad variant ", variant, " is not a production kernel (0, 9)");
+#endif
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }
 
@@ -575,7 +580,7 @@ void sgd_pack(const Tensor& p, const Tensor& g, double lr, const c10::optional<T
     L.wf = bfp_mut(wf[i]);
     L.Cout_p = (int)wf[i].size(1); L.Cin_p = (int)wf[i].size(2);
     const int T = L.K * L.K, cpt = (L.Cin_real + 7) / 8;
-    TORCH_CHECK(T <= agk::kSgdPackMaxTaps, "sgd_pack: at most 5x5 kernels");
+    TORCH_CHECK(L.K == 1 || L.K == 3 || L.K == 5, "sgd_pack: 1x1, 3x3 and 5x5 kernels only");
     TORCH_CHECK(L.off >= 0 && L.off + (int64_t)L.Cout_real * L.Cin_real * T <= p.numel(), "sgd_pack: weight range");
     L.pk_cpt = (wf[i].size(0) != T && wf[i].size(0) != T + 1 && L.Cin_p == 64 && L.Cin_real <= 64 &&
                 wf[i].size(0) == (T * cpt + 7) / 8) ? cpt : 0;

@@ -223,6 +223,75 @@ __device__ __forceinline__ size_t wf_index(const SgdPackLayer& L, int t, int n, 
 }
 }  // namespace
 
+// Phase 1 reads the tile's OIHW span along memory (for each of the 32 n, its 32 c x K*K taps are
+// contiguous), eight independent loads in flight per thread, and stages the bf16 result in LDS as
+// [t][c][n]; phase 2 writes wf along c and wd along n from LDS.  (The round-4 first cut had each thread
+// walk its (n, c)'s taps serially: strided, one load in flight, 79 us per step.)
+template <int K>
+__device__ __forceinline__ void sgd_pack_layer(const SgdPackLayer& L, float* P, const float* G, float step,
+                                               __bf16* tile) {
+  constexpr int KK = K;
+  constexpr int T = KK * KK;
+  constexpr int span = 32 * T;  // one n's slice of the tile, in floats
+  const int ctiles = (L.Cin_p + 31) >> 5;
+  const int c0 = (blockIdx.x % ctiles) * 32, n0 = (blockIdx.x / ctiles) * 32;
+  const int cw = min(32, L.Cin_real - c0), nw = min(32, L.Cout_real - n0);
+  const int lim = cw * T;  // real floats of one n's slice
+  const size_t rows = (size_t)L.Cin_real * T;
+  const size_t base0 = ((size_t)n0 * L.Cin_real + c0) * T;
+  constexpr int B = 8;
+#pragma unroll 1
+  for (int e0 = 0; e0 < 32 * span; e0 += 256 * B) {
+    float pv[B], gv[B];
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int e = e0 + j * 256 + (int)threadIdx.x;
+      const int nl = e / span, r = e - nl * span;
+      pv[j] = gv[j] = 0.f;
+      if (e < 32 * span && nl < nw && r < lim) {
+        pv[j] = P[base0 + nl * rows + r];
+        gv[j] = G[base0 + nl * rows + r];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B; ++j) {
+      const int e = e0 + j * 256 + (int)threadIdx.x;
+      if (e >= 32 * span) break;
+      const int nl = e / span, r = e - nl * span;
+      const int cl = r / T, t = r - cl * T;
+      float v = 0.f;
+      if (nl < nw && r < lim) {
+        v = pv[j] - step * gv[j];
+        P[base0 + nl * rows + r] = v;
+      }
+      tile[(t * 32 + cl) * 33 + nl] = (__bf16)v;
+    }
+  }
+  __syncthreads();
+  // forward pack wf[t][n][c] (or the packed-tap layout): along c.  Packed-tap layout: channels past the
+  // last chunk of a tap have no slot (their index would alias the next tap's first chunk).
+  const int cslots = L.pk_cpt > 0 ? L.pk_cpt * 8 : L.Cin_p;
+  {
+    const int cl = threadIdx.x & 31, c = c0 + cl;
+#pragma unroll 4
+    for (int row = threadIdx.x >> 5; row < T * 32; row += 8) {
+      const int t = row >> 5, nl = row & 31, n = n0 + nl;
+      if (n < L.Cout_p && c < cslots) L.wf[wf_index(L, t, n, c)] = tile[(t * 32 + cl) * 33 + nl];
+    }
+  }
+  if (!L.wd) return;
+  // dgrad pack wd[t'][c][n] (t' = the 180-degree-rotated tap): along n
+  const int nl = threadIdx.x & 31, n = n0 + nl;
+#pragma unroll 4
+  for (int row = threadIdx.x >> 5; row < T * 32; row += 8) {
+    const int t = row >> 5, cc = row & 31;
+    const int kh = t / KK, kw = t - kh * KK;
+    const int tf = (KK - 1 - kh) * KK + (KK - 1 - kw);
+    if (c0 + cc < L.Cin_p && n < L.Cout_p)
+      L.wd[((size_t)tf * L.Cin_p + c0 + cc) * L.Cout_p + n] = tile[(t * 32 + cc) * 33 + nl];
+  }
+}
+
 __global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
   __shared__ __bf16 tile[kSgdPackMaxTaps * 32 * 33];  // [t][c][n] (n padded to 33: no bank conflicts)
   float step = a.lr * a.gscale;
@@ -236,48 +305,16 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
     return;
   }
   const SgdPackLayer& L = a.layers[blockIdx.y];
-  const int T = L.K * L.K;
   const int ctiles = (L.Cin_p + 31) >> 5;
   const int ntiles = (L.Cout_p + 31) >> 5;
   if ((int)blockIdx.x >= ctiles * ntiles) return;  // block-uniform: before any barrier
-  const int c0 = (blockIdx.x % ctiles) * 32, n0 = (blockIdx.x / ctiles) * 32;
-  const int cl = threadIdx.x & 31, nq = threadIdx.x >> 5;  // 8 groups of 4 n
-  const int c = c0 + cl;
-  // packed-tap layout: channels past the last chunk of a tap have no slot (their index would alias the
-  // next tap's first chunk)
-  const int cslots = L.pk_cpt > 0 ? L.pk_cpt * 8 : L.Cin_p;
   float* P = a.p + L.off;
   const float* G = a.g + L.off;
-#pragma unroll 1
-  for (int k = 0; k < 4; ++k) {
-    const int nl = nq * 4 + k;
-    const int n = n0 + nl;
-    const bool real = n < L.Cout_real && c < L.Cin_real;
-    const size_t base = ((size_t)n * L.Cin_real + c) * T;
-    for (int t = 0; t < T; ++t) {
-      float v = 0.f;
-      if (real) {
-        v = P[base + t] - step * G[base + t];
-        P[base + t] = v;
-      }
-      const __bf16 bv = (__bf16)v;
-      if (n < L.Cout_p && c < cslots) L.wf[wf_index(L, t, n, c)] = bv;
-      if (L.wd) tile[(t * 32 + cl) * 33 + nl] = bv;
-    }
-  }
-  if (!L.wd) return;  // layer-uniform
-  __syncthreads();
-  const int nl = threadIdx.x & 31, cq = threadIdx.x >> 5;
-  const int n = n0 + nl;
-  for (int t = 0; t < T; ++t) {
-    const int kh = t / L.K, kw = t - kh * L.K;
-    const int tf = (L.K - 1 - kh) * L.K + (L.K - 1 - kw);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int cc = cq * 4 + k;
-      if (c0 + cc < L.Cin_p && n < L.Cout_p)
-        L.wd[((size_t)tf * L.Cin_p + c0 + cc) * L.Cout_p + n] = tile[(t * 32 + cc) * 33 + nl];
-    }
+  switch (L.K) {  // layer-uniform
+    case 1: sgd_pack_layer<1>(L, P, G, step, tile); break;
+    case 3: sgd_pack_layer<3>(L, P, G, step, tile); break;
+    case 5: sgd_pack_layer<5>(L, P, G, step, tile); break;
+    default: break;  // rejected on the host (kSgdPackMaxTaps)
   }
 }
 
