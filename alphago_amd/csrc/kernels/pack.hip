@@ -224,7 +224,7 @@ __device__ __forceinline__ size_t wf_index(const SgdPackLayer& L, int t, int n, 
 }  // namespace
 
 // Phase 1 reads the tile's OIHW span along memory (for each of the 32 n, its 32 c x K*K taps are
-// contiguous), eight independent loads in flight per thread, and stages the bf16 result in LDS as
+// contiguous), 18-20 independent loads in flight per thread, and stages the bf16 result in LDS as
 // [t][c][n]; phase 2 writes wf along c and wd along n from LDS.  (The round-4 first cut had each thread
 // walk its (n, c)'s taps serially: strided, one load in flight, 79 us per step.)
 template <int K>
@@ -239,7 +239,7 @@ __device__ __forceinline__ void sgd_pack_layer(const SgdPackLayer& L, float* P, 
   const int lim = cw * T;  // real floats of one n's slice
   const size_t rows = (size_t)L.Cin_real * T;
   const size_t base0 = ((size_t)n0 * L.Cin_real + c0) * T;
-  constexpr int B = 8;
+  constexpr int B = K == 1 ? 4 : K == 3 ? 18 : 20;  // loads in flight: 2 rounds (3x3), 5 (5x5)
 #pragma unroll 1
   for (int e0 = 0; e0 < 32 * span; e0 += 256 * B) {
     float pv[B], gv[B];

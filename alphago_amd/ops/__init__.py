@@ -131,10 +131,18 @@ def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: 
     return y
 
 
-def pk_applies(cin_real: int, cin_p: int) -> bool:
-    """Whether a first layer runs on the packed-tap forward (conv_fwd_pk): 32 < cin_real < 64 real input
+def pk_shape_ok(cin_real: int, cin_p: int) -> bool:
+    """Whether the packed-tap forward (conv_fwd_pk) can run a first layer: 32 < cin_real < 64 real input
     channels in a 64-channel padded input (48 policy / 49 value planes)."""
-    return cin_p == 64 and 32 < cin_real < 64 and os.environ.get("ALPHAGO_AMD_PK", "1") == "1"
+    return cin_p == 64 and 32 < cin_real < 64
+
+
+def pk_applies(cin_real: int, cin_p: int) -> bool:
+    """Whether the trainers / inference nets run their first layer on conv_fwd_pk.  Off by default
+    (ALPHAGO_AMD_PK=1 turns it on): it multiplies 24 % fewer MFMAs than the 64-channel 5x5 kernel but a
+    K-step's row then gathers from two or three pixels, and at B = 2176 it measured 399.5 us against the
+    64-channel kernel's ~381 us (profiles/r4/README.md)."""
+    return pk_shape_ok(cin_real, cin_p) and os.environ.get("ALPHAGO_AMD_PK", "0") == "1"
 
 
 def packed_weight_pk(w_oihw: torch.Tensor, cout_p: int, device=None) -> torch.Tensor:
@@ -282,18 +290,20 @@ def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
 
 
 # small batches (round 4): where the min-stages rule leaves the grid short of one workgroup per CU,
-# the per-tap kernel runs on a 4-slot LDS ring (variant 9) with longer splits: the slab it writes
+# the per-tap kernel can run on a 4-slot LDS ring (variant 9) with longer splits: the slab it writes
 # and the reduce reads shrink with the split count, and the ring hides the DMA latency that bounds
-# a short split
+# a short split.  Opt-in (ALPHAGO_AMD_WGRAD_RING=1): the SL step at B = 16 measured 0.901 ms with it
+# against 0.863 ms without (profiles/r4/README.md)
 WGRAD_RING_STAGES = int(os.environ.get("ALPHAGO_AMD_RING_STAGES", "16"))
 
 
 def wgrad_config(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, target_wgs: int = 0, cus: int = 256,
                  variant: int = 0):
     """(variant, nsplit) of a layer's wgrad: the requested variant and wgrad_nsplit, or at small
-    batches (variant 0, no explicit target) the ring variant 9 with WGRAD_RING_STAGES per split."""
+    batches with ALPHAGO_AMD_WGRAD_RING=1 (variant 0, no explicit target) the ring variant 9 with
+    WGRAD_RING_STAGES per split."""
     ns = wgrad_nsplit(M, cout_p, cin_p, K, cin_real, target_wgs, cus, variant)
-    if variant != 0 or target_wgs > 0 or os.environ.get("ALPHAGO_AMD_WGRAD_RING", "1") == "0":
+    if variant != 0 or target_wgs > 0 or os.environ.get("ALPHAGO_AMD_WGRAD_RING", "0") != "1":
         return variant, ns
     taps, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, 0)
     if taps != 1 or ns * per_split > cus:

@@ -577,11 +577,13 @@ def test_winograd_lab_forward(ops, cuda_device, B, S):
 
 
 @pytest.mark.parametrize("B", [1, 4, 16])
-@pytest.mark.parametrize("tile", [0, 65, 130])
-def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, B, tile):
+@pytest.mark.parametrize("tile,ring", [(0, "0"), (0, "1"), (65, "1"), (130, "0")])
+def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, monkeypatch, B, tile, ring):
     """Small batches (the reference's -B 16 training and batch-1 search calls): forward with the
-    bitmask, bitmask dgrad and the wgrad the trainer picks (ops.wgrad_config: the LDS-ring
-    variant with long splits) vs fp32 conv2d / conv2d_input / conv2d_weight."""
+    bitmask, bitmask dgrad and the wgrad the trainer picks (ops.wgrad_config: per-tap splits, or with
+    ALPHAGO_AMD_WGRAD_RING=1 the LDS-ring variant with long splits) vs fp32 conv2d / conv2d_input /
+    conv2d_weight."""
+    monkeypatch.setenv("ALPHAGO_AMD_WGRAD_RING", ring)
     torch.manual_seed(12)
     S, C = 19, 192
     x = _bf(torch.randn(B, C, S, S, device=cuda_device))
@@ -599,7 +601,7 @@ def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, B, tile):
     dx = ops.padded_empty(B, S, 1, C, cuda_device)
     ops.conv_fwd(ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb, tile=tile)
     var, ns = ops.wgrad_config(B * S * S, C, C, 3)
-    assert var == 9 or B * S * S // 32 // ops.WGRAD_RING_STAGES == 0 or ns > 0
+    assert var == (9 if ring == "1" else 0) and ns > 0
     slab = torch.full((ns, 9, C, C), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, C, device=cuda_device)
     ops.conv_wgrad(xp, ops.to_padded(g, 1), slab, dbs, 3, S, 1, 1, variant=var)
@@ -628,7 +630,7 @@ def test_conv_fwd_packed_taps_first_layer(ops, cuda_device, S, B, Cin, Cout, Cou
     bp[:Cout] = b
     ref = F.relu(F.conv2d(x, w, b, padding=P))
     xp = ops.to_padded(x, P)
-    assert ops.pk_applies(Cin, xp.shape[3])
+    assert ops.pk_shape_ok(Cin, xp.shape[3])
     wpk = ops.packed_weight_pk(w, Cout_p)
     wfull = ops.packed_weight_like(w, 64, Cout_p)
     ops.pack_weights([w.contiguous(), w.contiguous()], [wpk, wfull])
