@@ -154,16 +154,19 @@ static int wgrad0_occ3() {
   return on;
 }
 
-template <int WN, int TAPS, int MW>
+// variant 10: the thin first layer's tap-merged rows on 12 waves (4 n x 3 c, 48 x 48 per wave per tap:
+// 60 accumulator VGPRs instead of 120, 104 VGPRs in all) -- three waves per SIMD instead of 1.5 to hide
+// the LDS and DMA latency that bounds the 6-wave kernel (28.7 % MFMA busy, profiles/r3_final/pmc)
+template <int WN, int TAPS, int MW, int NWN = 2>
 static void launch_wgrad_taps48(const ConvWgradArgs& a, hipStream_t st) {
   constexpr int smem = 2 * (WN + 48 * TAPS) * 64 * kWgradKsub;
   static const hipError_t attr48 = hipFuncSetAttribute(
-      (const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, 2, MW>,
+      (const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, 2, MW, NWN>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr48, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid(a.nsplit, a.T / TAPS, a.Cout / WN);
-  hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, 2, MW>), grid, dim3(384),
-                     smem, st, a);
+  hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, 2, MW, NWN>), grid,
+                     dim3(64 * 3 * NWN), smem, st, a);
 }
 
 template <int WN, int TAPS>
@@ -173,8 +176,17 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
     // waves (2 n x 3 c) skips the zero channels -- 25% fewer MFMAs and x bytes
     // on the backward's serial tail; the slab columns 48..63 stay unwritten
     // (the reduce reads only cin_real of them)
-    if (TAPS == 5 && wgrad0_occ3()) launch_wgrad_taps48<WN, TAPS, 3>(a, st);
-    else launch_wgrad_taps48<WN, TAPS, 0>(a, st);
+    if (TAPS == 5 && wgrad0_occ3()) {
+      launch_wgrad_taps48<WN, TAPS, 3>(a, st);
+      return;
+    }
+    if constexpr (TAPS == 5 && (WN / 16) % 4 == 0) {
+      if (a.variant == 10) {
+        launch_wgrad_taps48<WN, TAPS, 0, 4>(a, st);
+        return;
+      }
+    }
+    launch_wgrad_taps48<WN, TAPS, 0>(a, st);
     return;
   }
   constexpr int smem = 2 * (WN + 64 * TAPS) * 64 * kWgradKsub;
@@ -222,7 +234,7 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
 #ifdef AGK_KERNEL_LAB
   if (a.variant != 9 && launch_conv_wgrad_lab(a, WN, WC, grid, st)) return;  // lab variants 2 / 3 / 4 (conv_lab.hip)
 #else
-  if (a.variant != 0 && a.variant != 9)
+  if (a.variant != 0 && a.variant != 9 && a.variant != 10)
     throw std::invalid_argument("conv_wgrad: variant " + std::to_string(a.variant) + " is a kernel-lab variant");
 #endif
   if constexpr (WC == 64) {
@@ -288,7 +300,7 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
   }
 #endif
   // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
-  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 9) ? 0 : variant);
+  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 10) ? 0 : variant);
   const bool c48 = cin_real <= 48 && Cin == 64;
   const int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
   const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;

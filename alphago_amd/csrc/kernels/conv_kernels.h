@@ -572,12 +572,13 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_pk_kernel(ConvFwdArg
 // tap-0 image shifted by kw columns (kw * Cin elements).  This triples (5x5:
 // quintuples) the MFMAs per staged dz byte, the limiter of the 64-wide tile.
 // the split's partial tile D[n][c] (lane owns n..n+3 at column c) and the bias partial
-template <int WN, int WC, int NWC, int TAPS>
-__device__ __forceinline__ void wgrad_store(const ConvWgradArgs& a, const f32x4 (&acc)[TAPS][WN / 32][WC / (16 * NWC)],
-                                            const float (&dbs)[WN / 32], bool do_bias, int split, int t, int n0, int c0,
-                                            int wn, int wc, int lane, int zero_split) {
-  constexpr int NBn = WN / 32, NBc = WC / (16 * NWC);
-  const int nb0 = n0 + wn * (WN / 2) + ((lane >> 4) << 2);
+template <int WN, int WC, int NWC, int TAPS, int NWN = 2>
+__device__ __forceinline__ void wgrad_store(const ConvWgradArgs& a,
+                                            const f32x4 (&acc)[TAPS][WN / (16 * NWN)][WC / (16 * NWC)],
+                                            const float (&dbs)[WN / (16 * NWN)], bool do_bias, int split, int t,
+                                            int n0, int c0, int wn, int wc, int lane, int zero_split) {
+  constexpr int NBn = WN / (16 * NWN), NBc = WC / (16 * NWC);
+  const int nb0 = n0 + wn * (WN / NWN) + ((lane >> 4) << 2);
   const int cbase = c0 + wc * (WC / NWC) + (lane & 15);
 #pragma unroll
   for (int tp = 0; tp < TAPS; ++tp) {
@@ -607,7 +608,7 @@ __device__ __forceinline__ void wgrad_store(const ConvWgradArgs& a, const f32x4 
       float s = dbs[i];
       s += __shfl_xor(s, 16, 64);
       s += __shfl_xor(s, 32, 64);
-      if (lane < 16) a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / 2) + i * 16 + lane] = s;
+      if (lane < 16) a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / NWN) + i * 16 + lane] = s;
     }
   }
 }
@@ -622,13 +623,14 @@ __device__ __forceinline__ void wgrad_store(const ConvWgradArgs& a, const f32x4 
 // into the second's.
 // NS > 2 (small batches): an NS-slot LDS ring instead of the double buffer (see conv_fwd_kernel);
 // only for geometries whose waves each stage exactly IPW pieces per stage (the vmcnt unit).
-template <int WN, int WC, int KSUB, int NWC, int TAPS, int NS = 2>
+// NWN: waves along n (2; the thin first layer's 12-wave variant has 4, see launch_wgrad_taps48).
+template <int WN, int WC, int KSUB, int NWC, int TAPS, int NS = 2, int NWN = 2>
 __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, int ks_begin, int ks_end, int t,
                                            int tstep, int n0, int c0, int zero_split) {
-  // 2 (n) x NWC (c) waves; NWC = 2 gives each wave a 96x96 tile at 192x192
+  // NWN (n) x NWC (c) waves; NWC = 2 gives each wave a 96x96 tile at 192x192
   // (a third fewer LDS fragment reads per MFMA than NWC = 4)
-  constexpr int NWAVES = 2 * NWC;
-  constexpr int NBn = WN / 32;          // n blocks per wave (wave covers WN/2)
+  constexpr int NWAVES = NWN * NWC;
+  constexpr int NBn = WN / (16 * NWN);  // n blocks per wave (wave covers WN/NWN)
   constexpr int NBc = WC / (16 * NWC);  // c blocks per wave (wave covers WC/NWC)
   constexpr int DZ_BYTES = WN * 64;  // [WN/16][32 px][16 ch] bf16
   constexpr int X_BYTES = WC * 64 * TAPS;  // [TAPS][WC/16][32 px][16 ch]
@@ -814,7 +816,7 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
     }
   }
 
-  wgrad_store<WN, WC, NWC, TAPS>(a, acc, dbs, do_bias, split, t, n0, c0, wn, wc, lane, zero_split);
+  wgrad_store<WN, WC, NWC, TAPS, NWN>(a, acc, dbs, do_bias, split, t, n0, c0, wn, wc, lane, zero_split);
 }
 
 // LINE staging (wgrad variants 6 and 7): every DMA piece moves 8 whole 128-byte pixel lines (one
@@ -1079,10 +1081,11 @@ __device__ __forceinline__ void wgrad_tile_line(const ConvWgradArgs& a, int spli
 // which fits ONE workgroup per CU; MW = 3 caps them at 168 (11 dwords spilled) so that two share a CU
 // (AGK_WGRAD0_OCC3=1, round 4 A/B).
 template <int WN, int WC, int KSUB, int NWC = 4, int TAPS = 1, bool PAIR = false, bool LINE = false, bool ILVW = false,
-          int NS = 2, int MW = 0>
-__global__ __launch_bounds__(128 * NWC, (MW > 0 ? MW : (LINE && !PAIR) ? 4 : 1)) void conv_wgrad_kernel(
+          int NS = 2, int MW = 0, int NWN = 2>
+__global__ __launch_bounds__(64 * NWN * NWC, (MW > 0 ? MW : (LINE && !PAIR) ? 4 : 1)) void conv_wgrad_kernel(
     ConvWgradArgs a) {
   static_assert(!PAIR || TAPS == 2, "PAIR: two taps per workgroup");
+  static_assert(NWN == 2 || (!PAIR && !LINE), "NWN != 2: the plain per-tap / tap-merged body only");
   // workgroup -> (split, tap group, channel block).  xcd_group (tap-merged rows): the hardware
   // deals workgroups to the 8 XCDs round robin in launch order, which puts the K kernel-row
   // workgroups of a split -- all reading the same dZ rows -- on K different L2s, so every dZ
@@ -1128,7 +1131,7 @@ __global__ __launch_bounds__(128 * NWC, (MW > 0 ? MW : (LINE && !PAIR) ? 4 : 1))
     tstep = ((t1 / a.K - t / a.K) * a.HPi + (t1 % a.K - t % a.K)) * a.Cin;
   }
   if constexpr (LINE) wgrad_tile_line<WN, WC, KSUB, NWC, TAPS, ILVW>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
-  else wgrad_tile<WN, WC, KSUB, NWC, TAPS, NS>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
+  else wgrad_tile<WN, WC, KSUB, NWC, TAPS, NS, NWN>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
 }
 
 constexpr int kWgradKsub = 1;

@@ -169,7 +169,8 @@ def mbits_words(cout_p: int) -> int:
 def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1, cin_real: int = 0, variant: int = 0):
     """Split-K weight gradient into ``slab``; ``cin_real`` (< padded Cin) lets
     the kernel skip zero-padded input channels (only slab columns < cin_real are written).
-    ``variant``: 0 = per-tap kernel (default), 5 = one-kernel-row wgrad where it applies (opt-in)."""
+    ``variant``: 0 = per-tap kernel (default), 9 = the per-tap kernel on a 4-slot LDS ring (small
+    batches), 10 = the thin first layer's kernel rows on 12 waves (ops.wgrad_config picks them)."""
     _ops().conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, variant)
 
 
@@ -303,6 +304,9 @@ def wgrad_config(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
     batches with ALPHAGO_AMD_WGRAD_RING=1 (variant 0, no explicit target) the ring variant 9 with
     WGRAD_RING_STAGES per split."""
     ns = wgrad_nsplit(M, cout_p, cin_p, K, cin_real, target_wgs, cus, variant)
+    if (variant == 0 and K == 5 and cin_p == 64 and 0 < cin_real <= 48 and cout_p % 64 == 0
+            and os.environ.get("ALPHAGO_AMD_WGRAD0_WAVES", "6") == "12"):
+        return 10, ns  # the thin first layer's kernel rows on 12 waves (conv.hip launch_wgrad_taps48)
     if variant != 0 or target_wgs > 0 or os.environ.get("ALPHAGO_AMD_WGRAD_RING", "0") != "1":
         return variant, ns
     taps, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, 0)

@@ -185,12 +185,15 @@ def test_conv_wgrad_line_lab_boards(ops, cuda_device, S, B, variant):
     assert _rel_err(gb, ref_b) < 2e-3
 
 
-@pytest.mark.parametrize("K,Pin", [(5, 2), (3, 1)])
-def test_conv_wgrad_thin_input(ops, cuda_device, K, Pin):
+@pytest.mark.parametrize("K,Pin,variant,S,B,Cout", [(5, 2, 0, 19, 5, 192), (3, 1, 0, 19, 5, 192),
+                                                    (5, 2, 10, 19, 5, 192), (5, 2, 10, 9, 13, 192),
+                                                    (5, 2, 10, 13, 3, 128), (5, 2, 10, 19, 1, 64)])
+def test_conv_wgrad_thin_input(ops, cuda_device, K, Pin, variant, S, B, Cout):
     """48 real input planes padded to 64 (the policy net's first layer): the
-    cin_real path computes only the real channels, matching the fp32 reference."""
+    cin_real path computes only the real channels, matching the fp32 reference (variant 10: the
+    kernel rows on 12 waves, 4 n x 3 c)."""
     torch.manual_seed(5)
-    B, Cin, Cout, S = 5, 48, 192, 19
+    Cin = 48
     x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
     dz = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
     ref_w = torch.nn.grad.conv2d_weight(x, (Cout, Cin, K, K), dz, padding=K // 2)
@@ -200,7 +203,7 @@ def test_conv_wgrad_thin_input(ops, cuda_device, K, Pin):
     ns = ops.wgrad_splits(B * S * S, K * K)
     slab = torch.full((ns, K * K, Cout, 64), float("nan"), device=cuda_device)  # unwritten columns must be ignored
     dbs = torch.zeros(ns, Cout, device=cuda_device)
-    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin)
+    ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin, variant=variant)
     gw = torch.zeros(Cout, Cin, K, K, device=cuda_device)
     gb = torch.zeros(Cout, device=cuda_device)
     ops.conv_wgrad_reduce(slab, dbs, gw, gb, 1.0, 0.0)
