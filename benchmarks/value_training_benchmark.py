@@ -2,9 +2,13 @@
 from self-play positions, DP=8, fp8 MFMA conv path").
 
 Paper/reference value net (AlphaGo/models/value.py:12-31): 49 planes, 5x5 +
-11x 3x3 convs of 152 filters (160-wide tiles in bf16, 192 in fp8), 1x1
-conv, Dense(256), Dense(1, tanh); MSE against +-1 outcomes.  Synthetic
-positions/outcomes, random init.  Runs under torchrun for DP (RCCL all-reduce).
+11x 3x3 convs of 152 filters (160-wide tiles), 1x1 conv, Dense(256),
+Dense(1, tanh); MSE.  Data (--data teacher, default): random-game positions
+labelled by a fixed random-init value teacher of the same architecture
+(data/synthetic.py value_teacher_pool: a learnable regression target), with a
+held-out MSE after the timed steps; --data random: random planes and +-1
+outcomes (speed only).  Random-init student.  Runs under torchrun for DP
+(RCCL all-reduce).
 
     python benchmarks/value_training_benchmark.py --precision fp8 --steps 20
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/value_training_benchmark.py
@@ -34,6 +38,8 @@ def main():
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--precision", default="fp8", choices=["bf16", "fp8"])
     ap.add_argument("--pool", type=int, default=8192)
+    ap.add_argument("--heldout", type=int, default=2048)
+    ap.add_argument("--data", default="teacher", choices=["teacher", "random"])
     ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 64, 128, 256, 384, 385, 386, 387],
                     help="forward/dgrad conv tiling (0 = automatic)")
     ap.add_argument("--overlap", action="store_true", help="wgrad on a second stream beside the dgrad")
@@ -51,8 +57,24 @@ def main():
            "fp8_wgrad": not a.no_fp8_wgrad} if dev.type == "cuda" else {})
     tr = make_value_trainer(net, a.batch, lr=0.003, decay=8.664e-8, device=dev, **kw)
     g = torch.Generator(device=dev).manual_seed(11 + env.rank)
-    pool = torch.randint(0, 2, (a.pool, 49, 19, 19), dtype=torch.uint8, device=dev, generator=g)
-    pz = (torch.randint(0, 2, (a.pool,), device=dev, generator=g) * 2 - 1).float()
+    t_data = time.perf_counter()
+    if a.data == "teacher":
+        import numpy as np
+
+        from alphago_amd.data.synthetic import random_game_states, value_teacher, value_teacher_pool
+        from alphago_amd.features import VALUE_FEATURES, Preprocess
+        probe = Preprocess(VALUE_FEATURES).states_to_uint8(random_game_states(1024, np.random.default_rng(0)))
+        teacher = value_teacher(49, a.filters, a.layers, device=dev, probe=probe)
+        planes, tz = value_teacher_pool(a.pool + a.heldout, teacher, seed=1 + env.rank)
+        del teacher
+        allp, allz = torch.from_numpy(planes).to(dev), torch.from_numpy(tz).to(dev)
+        pool, pz = allp[:a.pool], allz[:a.pool]
+        hp, hz = allp[a.pool:], allz[a.pool:]
+    else:
+        pool = torch.randint(0, 2, (a.pool, 49, 19, 19), dtype=torch.uint8, device=dev, generator=g)
+        pz = (torch.randint(0, 2, (a.pool,), device=dev, generator=g) * 2 - 1).float()
+        hp = hz = None
+    t_data = time.perf_counter() - t_data
 
     def batch():
         idx = torch.randint(0, a.pool, (a.batch,), device=dev, generator=g)
@@ -78,13 +100,25 @@ def main():
     agdist.all_reduce_sum_(ls)
     n = env.world_size
     pos = a.batch * n * a.steps
+    heldout = None
+    if hp is not None:  # after the clock: held-out MSE of the trained student (whole batches)
+        se = torch.zeros((), device=dev, dtype=torch.float64)
+        cnt = 0
+        for i in range(0, hp.shape[0] - a.batch + 1, a.batch):
+            se += tr.evaluate(hp[i:i + a.batch], hz[i:i + a.batch])[0].double()
+            cnt += a.batch
+        heldout = {"heldout_mse": round(float(se) / max(cnt, 1), 5), "heldout_var": round(float(hz.var()), 5),
+                   "heldout_n": cnt}
     if env.is_main:
         print(json.dumps({"metric": "value-net training positions/s (whole job)", "value": round(pos / dt, 1),
                           "unit": "positions/s", "n_gpus": n, "ms_per_step": round(dt / a.steps * 1e3, 3),
                           "precision": a.precision if dev.type == "cuda" else "fp32", "mse": round(float(ls) / pos, 4),
                           "config": {"model": "value net %d-layer %d filters 49 planes" % (a.layers, a.filters),
                                      "global_batch": a.batch * n, "parallelism": "dp%d" % n},
-                          "data": "synthetic positions/outcomes, random-init weights"}), flush=True)
+                          **(heldout or {}), "data_s": round(t_data, 1),
+                          "data": ("value-teacher-labelled random-game positions (synthetic), random-init student"
+                                   if a.data == "teacher" else "synthetic positions/outcomes, random-init weights")}),
+              flush=True)
     agdist.shutdown()
 
 

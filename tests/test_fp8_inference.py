@@ -242,36 +242,68 @@ def _emulated_fp8_value_grads(net, planes, z, wscale, osc):
     return dict(zip(names, g))
 
 
-def test_fp8_backward_12_layer_trunk_matches_exact_backward(cuda_device):
-    """The all-fp8 backward (e5m2 dZ x e4m3 weights dgrad, e5m2 dZ x e4m3 X wgrad) on the full 12 x 152
-    value trunk: every layer's weight gradient has cosine >= 0.95 with the exact fp32 gradient of the
-    same quantised forward (emulated in torch with the trainer's own scales).  The fp8-vs-bf16 gradient
-    gap at random init (~0.7) comes from the e4m3 FORWARD -- a different function -- not from the
-    backward kernels (profiles/r4/fp8_grad_sim.json: e5m2 gradients alone keep 0.98)."""
+def _fp8_trainers_grads(layers, B, arms, seed_planes=11):
+    """Per-arm trunk weight gradients of the fp8 value trainer on one batch (second backward: the first
+    calibrates the activation and gradient scales), plus the scales that forward used."""
     import copy
 
     from alphago_amd.models.nets import ValueNet
     from alphago_amd.train.engine import HipValueTrainer
 
     torch.manual_seed(4)
-    B = 64
-    net = ValueNet(49, filters_per_layer=152, layers=12)
-    ref = copy.deepcopy(net).to(cuda_device)
-    planes = _planes(B, 49, seed=11).to(cuda_device)
-    z = torch.rand(B, device=cuda_device) * 2 - 1
-    t8 = HipValueTrainer(net, B, lr=0.0, device=cuda_device, precision="fp8")
-    assert t8.fp8_wgrad and t8.fp8_dgrad
-    t8.compute_grads(planes, z)  # calibrates the activation and gradient scales
-    osc = t8.osc8.clone()        # the delayed multipliers the next forward uses
-    wscale = t8.wscale8.clone()
-    t8.compute_grads(planes, z)  # all-fp8 step
-    torch.cuda.synchronize()
-    g_ref = _emulated_fp8_value_grads(ref, planes, z, wscale.cpu(), osc.cpu())
-    res = []
-    for l in range(12):
-        a, b = t8.fp.grad_views["w%d" % l].double().flatten(), g_ref["w%d" % l].double().flatten()
-        res.append((l, round(torch.nn.functional.cosine_similarity(a, b, dim=0).item(), 4),
-                    round((a.norm() / b.norm()).item(), 4)))
-    print("per-layer (layer, cosine, norm ratio):", res)
-    for l, cos, ratio in res:
+    net = ValueNet(49, filters_per_layer=152, layers=layers)
+    dev = torch.device("cuda:0")
+    planes = _planes(B, 49, seed=seed_planes).to(dev)
+    z = torch.rand(B, device=dev) * 2 - 1
+    out = {}
+    for dg, wg in arms:
+        t = HipValueTrainer(copy.deepcopy(net), B, lr=0.0, device=dev, precision="fp8", fp8_dgrad=dg, fp8_wgrad=wg)
+        assert (t.fp8_dgrad, t.fp8_wgrad) == (dg, wg)
+        t.compute_grads(planes, z)
+        osc, wscale = t.osc8.clone(), t.wscale8.clone()
+        t.compute_grads(planes, z)
+        torch.cuda.synchronize()
+        out[(dg, wg)] = ({"w%d" % l: t.fp.grad_views["w%d" % l].double().flatten().clone() for l in range(layers)},
+                         osc.cpu(), wscale.cpu())
+    return net, planes, z, out
+
+
+def _cos_ratio(a, b):
+    return (round(torch.nn.functional.cosine_similarity(a, b, dim=0).item(), 4), round((a.norm() / b.norm()).item(), 4))
+
+
+def test_fp8_backward_4_layer_matches_exact_backward(cuda_device):
+    """Each fp8 backward arm (bf16 / e5m2 dgrad x bf16 / e5m2 wgrad) on the 4 x 152 value trunk vs the exact
+    fp32 autograd of the same quantised forward (emulated in torch with the trainer's own scales): every
+    layer's weight gradient within cosine 0.99 (measured >= 0.9946, scripts/r4/fp8_diag.py)."""
+    arms = [(False, False), (True, False), (False, True), (True, True)]
+    net, planes, z, got = _fp8_trainers_grads(4, 32, arms)
+    for arm in arms:
+        g, osc, wscale = got[arm]
+        g_ref = _emulated_fp8_value_grads(copy_net(net, cuda_device), planes, z, wscale, osc)
+        res = [_cos_ratio(g["w%d" % l], g_ref["w%d" % l].double().flatten()) for l in range(4)]
+        print(arm, res)
+        for l, (cos, ratio) in enumerate(res):
+            assert cos >= 0.99 and 0.95 < ratio < 1.05, (arm, l, cos, ratio)
+
+
+def copy_net(net, dev):
+    import copy
+
+    return copy.deepcopy(net).to(dev)
+
+
+def test_fp8_backward_12_layer_trunk_matches_bf16_backward(cuda_device):
+    """The all-fp8 backward (e5m2 dZ x e4m3 weights dgrad, e5m2 dZ x e4m3 X wgrad) on the full 12 x 152
+    value trunk vs the bf16 backward of the SAME fp8 forward (same kernels, same scales): every layer's
+    weight gradient within cosine 0.95 and norm ratio 0.8-1.25.  (Against a torch emulation of the
+    quantised forward the 12-layer cosines are 0.85-0.98 for the bf16 backward too: one-ulp e4m3
+    flips from a different fp32 summation order change a deep random-init value net's gradient
+    direction -- scripts/r4/fp8_diag.py, profiles/r4/README.md -- so the backward is pinned against
+    the backward.)"""
+    _, _, _, got = _fp8_trainers_grads(12, 64, [(False, False), (True, True)])
+    ref, g8 = got[(False, False)][0], got[(True, True)][0]
+    res = [_cos_ratio(g8["w%d" % l], ref["w%d" % l]) for l in range(12)]
+    print("per-layer (cosine, norm ratio):", res)
+    for l, (cos, ratio) in enumerate(res):
         assert cos >= 0.95 and 0.8 < ratio < 1.25, (l, cos, ratio)
