@@ -85,6 +85,10 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     else if (bm == 256) launch_fwd_bm<BN, MODE, 256, 4>(a, st);
     else if (bm == 128) launch_fwd_bm<BN, MODE, 128, 4>(a, st);
     else if (bm == 64) launch_fwd_bm<BN, MODE, 64, 2>(a, st);
+    // 32-pixel tiles (twice the workgroups of the 64 tile at small batches): 36 = 4 waves of 16 x BN/2,
+    // 37 = 2 waves of 32 x BN/2; same ReLU' bitmask layout
+    else if (bm == 36) launch_fwd_bm<BN, MODE, 32, 1>(a, st);
+    else if (bm == 37) launch_fwd_bm<BN, MODE, 32, 2>(a, st);
     // small batches: 65 / 130 = the 64 / 128-pixel tiles on a 4 / 3-slot LDS ring (NS above)
     else if (bm == 65) launch_fwd_bm<BN, MODE, 64, 2, true, true, false, false, false, false, 4>(a, st);
     else if (bm == 130) launch_fwd_bm<BN, MODE, 128, 4, true, true, false, false, false, false, 3>(a, st);
@@ -154,18 +158,22 @@ static int wgrad0_occ3() {
   return on;
 }
 
-// variant 10: the thin first layer's tap-merged rows on 12 waves (4 n x 3 c, 48 x 48 per wave per tap:
-// 60 accumulator VGPRs instead of 120, 104 VGPRs in all) -- three waves per SIMD instead of 1.5 to hide
-// the LDS and DMA latency that bounds the 6-wave kernel (28.7 % MFMA busy, profiles/r3_final/pmc)
-template <int WN, int TAPS, int MW, int NWN = 2>
+// The thin first layer's kernel rows run one workgroup per CU (180 VGPRs on 6 waves), so nothing hides
+// the global->LDS latency of the 2-buffer loop: ~1.16 us per 32-pixel stage, 26-29 % MFMA busy
+// (profiles/r3_final/pmc).  variant 11: the same 6 waves on a 4-slot LDS ring (three stages in
+// flight; 27 DMA pieces per stage on 6 waves, the three spare slots re-issue piece 0);
+// variant 10: 12 waves (4 n x 3 c, 48 x 48 per wave per tap, 104 VGPRs) on the 2-buffer loop --
+// measured equal to the 6-wave kernel (559 vs 556 us, profiles/r4/README.md); variant 12: 12 waves
+// on the ring.
+template <int WN, int TAPS, int MW, int NWN = 2, int NS = 2>
 static void launch_wgrad_taps48(const ConvWgradArgs& a, hipStream_t st) {
-  constexpr int smem = 2 * (WN + 48 * TAPS) * 64 * kWgradKsub;
+  constexpr int smem = NS * (WN + 48 * TAPS) * 64 * kWgradKsub;
   static const hipError_t attr48 = hipFuncSetAttribute(
-      (const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, 2, MW, NWN>,
+      (const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, NS, MW, NWN>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr48, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid(a.nsplit, a.T / TAPS, a.Cout / WN);
-  hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, 2, MW, NWN>), grid,
+  hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, NS, MW, NWN>), grid,
                      dim3(64 * 3 * NWN), smem, st, a);
 }
 
@@ -183,6 +191,16 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
     if constexpr (TAPS == 5 && (WN / 16) % 4 == 0) {
       if (a.variant == 10) {
         launch_wgrad_taps48<WN, TAPS, 0, 4>(a, st);
+        return;
+      }
+      if (a.variant == 12) {
+        launch_wgrad_taps48<WN, TAPS, 0, 4, 4>(a, st);
+        return;
+      }
+    }
+    if constexpr (TAPS == 5) {
+      if (a.variant == 11) {
+        launch_wgrad_taps48<WN, TAPS, 0, 2, 4>(a, st);
         return;
       }
     }
@@ -234,7 +252,7 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
 #ifdef AGK_KERNEL_LAB
   if (a.variant != 9 && launch_conv_wgrad_lab(a, WN, WC, grid, st)) return;  // lab variants 2 / 3 / 4 (conv_lab.hip)
 #else
-  if (a.variant != 0 && a.variant != 9 && a.variant != 10)
+  if (a.variant != 0 && !(a.variant >= 9 && a.variant <= 12))
     throw std::invalid_argument("conv_wgrad: variant " + std::to_string(a.variant) + " is a kernel-lab variant");
 #endif
   if constexpr (WC == 64) {
@@ -300,7 +318,7 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
   }
 #endif
   // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
-  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 10) ? 0 : variant);
+  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 12) ? 0 : variant);
   const bool c48 = cin_real <= 48 && Cin == 64;
   const int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
   const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;

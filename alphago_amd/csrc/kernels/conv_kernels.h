@@ -679,6 +679,9 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
           const bool ok = AGK_DCHECK(o >= 0 && o + 8 <= a.dz_elems, DBG_WG_DZ);
           glds16(ok ? dsrc + jj * 16 : a.dz, base + sub * SUB + jj * 1024);
         }
+        if constexpr (NS > 2) {  // see the release loop below
+          if (jj >= NINSTR / KSUB) glds16(dsrc, base + sub * SUB);
+        }
       }
 #pragma unroll
       for (int i = 0; i < IPW; ++i) {
@@ -710,6 +713,12 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
       for (int i = 0; i < IPW; ++i) {
         const int jj = wave * IPW + i - sub * (NINSTR / KSUB);
         if (jj >= 0 && jj < WN / 16) glds16(dsrc + jj * 16, base + sub * SUB + jj * 1024);
+        // LDS ring with unequal piece counts: a wave past the last piece re-issues dz piece 0 (same
+        // bytes to the same LDS address), so every wave has exactly IPW DMAs per stage -- the
+        // vmcnt unit ring_wait counts in
+        if constexpr (NS > 2) {
+          if (jj >= NINSTR / KSUB) glds16(dsrc, base + sub * SUB);
+        }
       }
 #pragma unroll
       for (int i = 0; i < IPW; ++i) {
@@ -744,7 +753,7 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
   constexpr int NF = NBn + TAPS * NBc;  // fragments read per sub-step
 
   constexpr bool RING = NS > 2;
-  static_assert(!RING || (KSUB == 1 && (WN / 16) % IPW == 0 && NINSTR == NWAVES * IPW), "ring: uniform staging");
+  static_assert(!RING || KSUB == 1, "ring: one sub-step per stage");
   static_assert(!RING || IPW * (NS - 2) <= 63, "vmcnt range");
   if constexpr (RING) {
 #pragma unroll

@@ -14,9 +14,9 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   check_dev("conv_fwd", x, w, bias, mask, y, mbits);
   // production tilings only: 0 = automatic, or a fixed 64 / 128 / 256 / 384-pixel tile (385: 384 with the
   // LDS-DMA issue spread through the MFMAs; 386 / 387: 385 / 384 with the chunk-outer K order)
-  TORCH_CHECK(tile == 0 || tile == 64 || tile == 65 || tile == 128 || tile == 130 || tile == 256 || tile == 384 ||
-                  tile == 385 || tile == 386 || tile == 387,
-              "conv_fwd tile ", tile, " is not a production tiling (0, 64, 65, 128, 130, 256, 384-387); kernel-lab "
+  TORCH_CHECK(tile == 0 || tile == 36 || tile == 37 || tile == 64 || tile == 65 || tile == 128 || tile == 130 ||
+                  tile == 256 || tile == 384 || tile == 385 || tile == 386 || tile == 387,
+              "conv_fwd tile ", tile, " is not a production tiling (0, 36, 37, 64, 65, 128, 130, 256, 384-387); kernel-lab "
               "variants are in torch.ops.alphago_amd_lab (alphago_amd.ops.lab())");
   conv_fwd_impl(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, (int)tile);
 }
@@ -35,14 +35,14 @@ void conv_fwd_pk(const Tensor& x, const Tensor& w, const Tensor& bias, const Ten
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
                 int64_t Pin, int64_t Po, int64_t cin_real, int64_t variant) {
   check_dev("conv_wgrad", x, dz, slab, dbslab);
-  // 0 = per-tap kernel (default), 9 = 4-slot LDS-ring kernel (small batches), 10 = the thin first layer's
-  // kernel rows on 12 waves; the lab build also has 5 = one-kernel-row wgrad
+  // 0 = per-tap kernel (default), 9 = 4-slot LDS-ring kernel (small batches), 10-12 = the thin first
+  // layer's kernel rows on 12 waves / a 4-slot ring / both; the lab build also has 5 = one-kernel-row wgrad
 #ifdef AGK_KERNEL_LAB
-  TORCH_CHECK(variant == 0 || variant == 5 || variant == 9 || variant == 10, "conv_wgrad variant ", variant,
-              " unknown (0, 5, 9, 10)");
+  TORCH_CHECK(variant == 0 || variant == 5 || (variant >= 9 && variant <= 12), "conv_wgrad variant ", variant,
+              " unknown (0, 5, 9-12)");
 #else
-  TORCH_CHECK(variant == 0 || variant == 9 || variant == 10, "conv_wgrad variant ", variant,
-              " is not a production kernel (0, 9, 10)");
+  TORCH_CHECK(variant == 0 || (variant >= 9 && variant <= 12), "conv_wgrad variant ", variant,
+              " is not a production kernel (0, 9-12)");
 #endif
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }

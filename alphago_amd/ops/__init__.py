@@ -304,9 +304,12 @@ def wgrad_config(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
     batches with ALPHAGO_AMD_WGRAD_RING=1 (variant 0, no explicit target) the ring variant 9 with
     WGRAD_RING_STAGES per split."""
     ns = wgrad_nsplit(M, cout_p, cin_p, K, cin_real, target_wgs, cus, variant)
-    if (variant == 0 and K == 5 and cin_p == 64 and 0 < cin_real <= 48 and cout_p % 64 == 0
-            and os.environ.get("ALPHAGO_AMD_WGRAD0_WAVES", "6") == "12"):
-        return 10, ns  # the thin first layer's kernel rows on 12 waves (conv.hip launch_wgrad_taps48)
+    v0 = os.environ.get("ALPHAGO_AMD_WGRAD0_VARIANT", "0")
+    if variant == 0 and K == 5 and cin_p == 64 and 0 < cin_real <= 48 and v0 in ("10", "11", "12") \
+            and (cout_p % 64 == 0 or v0 == "11"):
+        # the thin first layer's kernel rows: 10 = 12 waves, 11 = 4-slot LDS ring, 12 = both
+        # (conv.hip launch_wgrad_taps48)
+        return int(v0), ns
     if variant != 0 or target_wgs > 0 or os.environ.get("ALPHAGO_AMD_WGRAD_RING", "0") != "1":
         return variant, ns
     taps, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, 0)

@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                     help="conv forward precision (fp8 = e4m3 block-scaled MFMA forward, bf16 backward)")
     ap.add_argument("--graph", action="store_true", help="run each training step as a HIP-graph replay")
-    ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 64, 65, 128, 130, 256, 384, 385, 386, 387],
+    ap.add_argument("--conv-tile", type=int, default=0, choices=[0, 36, 37, 64, 65, 128, 130, 256, 384, 385, 386, 387],
                     help="forward/dgrad conv tiling (0 = automatic)")
     ap.add_argument("--wgrad-wgs", type=int, default=0,
                     help="target workgroups per wgrad launch (sets the split-K factor; 0 = one resident round)")

@@ -93,9 +93,11 @@ def test_fp8_value_training_tracks_bf16(cuda_device, F, fp8_dgrad, fp8_wgrad):
             assert cos > (0.85 if fp8_wgrad and name.startswith("b") else 0.9), (name, cos)
         assert (t8.gscales8[1:, 0] != 127).all()  # gradient exponents calibrated
     l0 = t8.evaluate(planes, z)[0].item()
-    for _ in range(15):
+    # 12 steps: at lr 0.05 the bf16 trainer itself overshoots on these 32 memorised boards at step 15
+    # (31.9 -> 20.3 -> 54.2; every fp8 arm tracks it step for step, scripts/r4/fp8_train_diag.py)
+    for _ in range(12):
         t8.step(planes, z)
-    assert t8.evaluate(planes, z)[0].item() < l0
+    assert t8.evaluate(planes, z)[0].item() < 0.9 * l0
     assert (t8.scales8[:, 0] != 127).any()  # activation exponents were set from the data
 
 

@@ -21,7 +21,7 @@ def _bf(x):
     return x.to(torch.bfloat16).float()
 
 
-PROD_TILES = (0, 64, 65, 128, 130, 256, 384, 385, 386, 387)
+PROD_TILES = (0, 36, 37, 64, 65, 128, 130, 256, 384, 385, 386, 387)
 
 
 def _conv_fwd(ops, tile, x, w, bias, y, K, S, Pin, Po=1, mode=0, mask=None, mbits=None):
@@ -185,13 +185,13 @@ def test_conv_wgrad_line_lab_boards(ops, cuda_device, S, B, variant):
     assert _rel_err(gb, ref_b) < 2e-3
 
 
-@pytest.mark.parametrize("K,Pin,variant,S,B,Cout", [(5, 2, 0, 19, 5, 192), (3, 1, 0, 19, 5, 192),
-                                                    (5, 2, 10, 19, 5, 192), (5, 2, 10, 9, 13, 192),
-                                                    (5, 2, 10, 13, 3, 128), (5, 2, 10, 19, 1, 64)])
+@pytest.mark.parametrize("K,Pin,variant,S,B,Cout", [(5, 2, 0, 19, 5, 192), (3, 1, 0, 19, 5, 192)] +
+                         [(5, 2, v, S, B, C) for v in (10, 11, 12)
+                          for S, B, C in ((19, 5, 192), (9, 13, 192), (13, 3, 128), (19, 1, 64))])
 def test_conv_wgrad_thin_input(ops, cuda_device, K, Pin, variant, S, B, Cout):
     """48 real input planes padded to 64 (the policy net's first layer): the
-    cin_real path computes only the real channels, matching the fp32 reference (variant 10: the
-    kernel rows on 12 waves, 4 n x 3 c)."""
+    cin_real path computes only the real channels, matching the fp32 reference (variants 10-12: the
+    kernel rows on 12 waves (4 n x 3 c) / a 4-slot LDS ring / both)."""
     torch.manual_seed(5)
     Cin = 48
     x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
@@ -287,8 +287,8 @@ def test_sgd_update(ops, cuda_device):
     assert torch.allclose(p, ref)
 
 
-@pytest.mark.parametrize("tile", lab_params([64, 65, 128, 130, 256, 2568, -1, 32, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9, 10,
-                                             11], PROD_TILES))
+@pytest.mark.parametrize("tile", lab_params([36, 37, 64, 65, 128, 130, 256, 2568, -1, 32, 2, 384, 385, 386, 387, 4, 5, 6, 7,
+                                             8, 9, 10, 11], PROD_TILES))
 def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     """Every forward tiling (gather 128/256, 128-pixel waves, halo) on a batch
     whose pixel count is not a multiple of any tile."""
@@ -308,7 +308,8 @@ def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", lab_params([64, 65, 130, 32, 256, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9, 10, 11], PROD_TILES))
+@pytest.mark.parametrize("tile", lab_params([36, 37, 64, 65, 130, 32, 256, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9, 10, 11],
+                                            PROD_TILES))
 def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
     """Layer-1 geometry (Cin 64, 5x5, input pad 2) and the masked dgrad mode on each tiling."""
     torch.manual_seed(2)
@@ -378,8 +379,8 @@ def _check_conv_fwd_fp8(ops, cuda_device, K, Cin, Cout, B, variant=0):
     assert y8[:, 0].sum() == 0 and yb[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", lab_params([0, 64, 65, 128, 130, 256, 384, 385, 386, 387, 32, 2, 4, 5, 6, 7, 8, 9, 10, 11],
-                                            PROD_TILES))
+@pytest.mark.parametrize("tile", lab_params([0, 36, 37, 64, 65, 128, 130, 256, 384, 385, 386, 387, 32, 2, 4, 5, 6, 7, 8, 9,
+                                             10, 11], PROD_TILES))
 @pytest.mark.parametrize("C", [192, 128])
 def test_relu_bitmask_dgrad_matches_mask(ops, cuda_device, tile, C):
     """Forward writes the ReLU' bitmask; dgrad mode 3 (bitmask) == mode 1 (bf16 activation mask)."""
@@ -580,7 +581,7 @@ def test_winograd_lab_forward(ops, cuda_device, B, S):
 
 
 @pytest.mark.parametrize("B", [1, 4, 16])
-@pytest.mark.parametrize("tile,ring", [(0, "0"), (0, "1"), (65, "1"), (130, "0")])
+@pytest.mark.parametrize("tile,ring", [(0, "0"), (0, "1"), (65, "1"), (130, "0"), (36, "0"), (37, "0")])
 def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, monkeypatch, B, tile, ring):
     """Small batches (the reference's -B 16 training and batch-1 search calls): forward with the
     bitmask, bitmask dgrad and the wgrad the trainer picks (ops.wgrad_config: per-tap splits, or with
