@@ -158,22 +158,24 @@ static int wgrad0_occ3() {
   return on;
 }
 
-// The thin first layer's kernel rows run one workgroup per CU (180 VGPRs on 6 waves), so nothing hides
-// the global->LDS latency of the 2-buffer loop: ~1.16 us per 32-pixel stage, 26-29 % MFMA busy
-// (profiles/r3_final/pmc).  variant 11: the same 6 waves on a 4-slot LDS ring (three stages in
-// flight; 27 DMA pieces per stage on 6 waves, the three spare slots re-issue piece 0);
-// variant 10: 12 waves (4 n x 3 c, 48 x 48 per wave per tap, 104 VGPRs) on the 2-buffer loop --
-// measured equal to the 6-wave kernel (559 vs 556 us, profiles/r4/README.md); variant 12: 12 waves
-// on the ring.
-template <int WN, int TAPS, int MW, int NWN = 2, int NS = 2>
+// The thin first layer's kernel rows run one workgroup per CU (180 VGPRs on 6 waves): ~1.16 us per
+// 32-pixel stage, 26-29 % MFMA busy (profiles/r3_final/pmc).  Round-4 variants (profiles/r4/README.md):
+//   10: 12 waves (4 n x 3 c, 48 x 48 per wave per tap, 104 VGPRs) -- 559 us vs 556 (equal);
+//   11: the 6 waves with unit pipelining (wgrad_tile UP: the next tap's x fragments are read under
+//       the current tap's MFMAs; after the barrier only the dz fragments and tap 0 are exposed);
+//   12: 12 waves with unit pipelining;
+//   15: 12 with at most 85 VGPRs (two 12-wave workgroups per CU);
+//   13: the 6 waves on a 4-slot LDS ring (three stages in flight; 27 DMA pieces per stage on 6
+//       waves, the spare slots re-issue piece 0) -- 601 us (slower: the stage is not DMA-bound).
+template <int WN, int TAPS, int MW, int NWN = 2, int NS = 2, bool UP = false>
 static void launch_wgrad_taps48(const ConvWgradArgs& a, hipStream_t st) {
   constexpr int smem = NS * (WN + 48 * TAPS) * 64 * kWgradKsub;
   static const hipError_t attr48 = hipFuncSetAttribute(
-      (const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, NS, MW, NWN>,
+      (const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, NS, MW, NWN, UP>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr48, "hipFuncSetAttribute(max dynamic LDS)");
   dim3 grid(a.nsplit, a.T / TAPS, a.Cout / WN);
-  hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, NS, MW, NWN>), grid,
+  hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, NS, MW, NWN, UP>), grid,
                      dim3(64 * 3 * NWN), smem, st, a);
 }
 
@@ -194,12 +196,20 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
         return;
       }
       if (a.variant == 12) {
-        launch_wgrad_taps48<WN, TAPS, 0, 4, 4>(a, st);
+        launch_wgrad_taps48<WN, TAPS, 0, 4, 2, true>(a, st);
+        return;
+      }
+      if (a.variant == 15) {  // 12 with the registers capped for two workgroups per CU (6 waves / SIMD)
+        launch_wgrad_taps48<WN, TAPS, 6, 4, 2, true>(a, st);
         return;
       }
     }
     if constexpr (TAPS == 5) {
       if (a.variant == 11) {
+        launch_wgrad_taps48<WN, TAPS, 0, 2, 2, true>(a, st);
+        return;
+      }
+      if (a.variant == 13) {
         launch_wgrad_taps48<WN, TAPS, 0, 2, 4>(a, st);
         return;
       }
@@ -252,7 +262,7 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
 #ifdef AGK_KERNEL_LAB
   if (a.variant != 9 && launch_conv_wgrad_lab(a, WN, WC, grid, st)) return;  // lab variants 2 / 3 / 4 (conv_lab.hip)
 #else
-  if (a.variant != 0 && !(a.variant >= 9 && a.variant <= 12))
+  if (a.variant != 0 && !(a.variant >= 9 && a.variant <= 15))
     throw std::invalid_argument("conv_wgrad: variant " + std::to_string(a.variant) + " is a kernel-lab variant");
 #endif
   if constexpr (WC == 64) {
@@ -262,6 +272,15 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
       else launch_wgrad_taps<WN, 5>(a, st);
       return;
     }
+  }
+  if (a.variant == 14) {  // unit pipelining (wgrad_tile UP): c block j + 1 read under c block j's MFMAs
+    static const hipError_t attr14 = hipFuncSetAttribute(
+        (const void*)conv_wgrad_kernel<WN, WC, KS, 4, 1, false, false, false, 2, 0, 2, true>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hip_check(attr14, "hipFuncSetAttribute(max dynamic LDS)");
+    hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS, 4, 1, false, false, false, 2, 0, 2, true>), grid, dim3(512),
+                       smem, st, a);
+    return;
   }
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
@@ -318,7 +337,7 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
   }
 #endif
   // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
-  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 12) ? 0 : variant);
+  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 15) ? 0 : variant);
   const bool c48 = cin_real <= 48 && Cin == 64;
   const int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
   const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;

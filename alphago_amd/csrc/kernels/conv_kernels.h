@@ -624,7 +624,10 @@ __device__ __forceinline__ void wgrad_store(const ConvWgradArgs& a,
 // NS > 2 (small batches): an NS-slot LDS ring instead of the double buffer (see conv_fwd_kernel);
 // only for geometries whose waves each stage exactly IPW pieces per stage (the vmcnt unit).
 // NWN: waves along n (2; the thin first layer's 12-wave variant has 4, see launch_wgrad_taps48).
-template <int WN, int WC, int KSUB, int NWC, int TAPS, int NS = 2, int NWN = 2>
+// UP: unit pipelining inside a sub-step -- the x fragments of column unit u + 1 (a (tap, c block)
+// pair) are read while the MFMAs of unit u run, instead of every fragment before the first MFMA;
+// only the dz fragments and unit 0 stay exposed after the barrier.
+template <int WN, int WC, int KSUB, int NWC, int TAPS, int NS = 2, int NWN = 2, bool UP = false>
 __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, int ks_begin, int ks_end, int t,
                                            int tstep, int n0, int c0, int zero_split) {
   // NWN (n) x NWC (c) waves; NWC = 2 gives each wave a 96x96 tile at 192x192
@@ -784,6 +787,45 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
         const char* cb = base + (wn * NBn + i) * 1024;
         tl[i] = ds_read_tr16_asm(cb + tr0);
         th[i] = ds_read_tr16_asm(cb + tr1);
+      }
+      if constexpr (UP) {
+        constexpr int NU = TAPS * NBc;  // column units u = tp * NBc + j
+        auto read_unit = [&](int u) {
+          const char* cb = base + DZ_BYTES + ((u / NBc) * XP + wc * NBc + (u % NBc)) * 1024;
+          tl[NBn + u] = ds_read_tr16_asm(cb + tr0);
+          th[NBn + u] = ds_read_tr16_asm(cb + tr1);
+        };
+        read_unit(0);
+        bf16x8 af[NBn];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          if (u + 1 < NU) read_unit(u + 1);
+          // all but the two reads of unit u + 1 have returned (LDS reads complete in order)
+          if (u == 0) {
+#pragma unroll
+            for (int i = 0; i < NBn; ++i) {
+              if (NU > 1) lgkm_wait_pair<2>(tl[i], th[i]);
+              else lgkm_wait_pair<0>(tl[i], th[i]);
+              af[i] = bf16x8{tl[i][0], tl[i][1], tl[i][2], tl[i][3], th[i][0], th[i][1], th[i][2], th[i][3]};
+            }
+          }
+          if (u + 1 < NU) lgkm_wait_pair<2>(tl[NBn + u], th[NBn + u]);
+          else lgkm_wait_pair<0>(tl[NBn + u], th[NBn + u]);
+          const bf16x8 bu = bf16x8{tl[NBn + u][0], tl[NBn + u][1], tl[NBn + u][2], tl[NBn + u][3],
+                                   th[NBn + u][0], th[NBn + u][1], th[NBn + u][2], th[NBn + u][3]};
+#pragma unroll
+          for (int i = 0; i < NBn; ++i) acc[u / NBc][i][u % NBc] = mfma16x16x32(af[i], bu, acc[u / NBc][i][u % NBc]);
+        }
+        if (do_bias) {
+#pragma unroll
+          for (int i = 0; i < NBn; ++i) {
+            float sb = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sb += (float)af[i][e];
+            dbs[i] += sb;
+          }
+        }
+        continue;
       }
 #pragma unroll
       for (int tp = 0; tp < TAPS; ++tp)
@@ -1090,7 +1132,7 @@ __device__ __forceinline__ void wgrad_tile_line(const ConvWgradArgs& a, int spli
 // which fits ONE workgroup per CU; MW = 3 caps them at 168 (11 dwords spilled) so that two share a CU
 // (AGK_WGRAD0_OCC3=1, round 4 A/B).
 template <int WN, int WC, int KSUB, int NWC = 4, int TAPS = 1, bool PAIR = false, bool LINE = false, bool ILVW = false,
-          int NS = 2, int MW = 0, int NWN = 2>
+          int NS = 2, int MW = 0, int NWN = 2, bool UP = false>
 __global__ __launch_bounds__(64 * NWN * NWC, (MW > 0 ? MW : (LINE && !PAIR) ? 4 : 1)) void conv_wgrad_kernel(
     ConvWgradArgs a) {
   static_assert(!PAIR || TAPS == 2, "PAIR: two taps per workgroup");
@@ -1140,7 +1182,7 @@ __global__ __launch_bounds__(64 * NWN * NWC, (MW > 0 ? MW : (LINE && !PAIR) ? 4 
     tstep = ((t1 / a.K - t / a.K) * a.HPi + (t1 % a.K - t % a.K)) * a.Cin;
   }
   if constexpr (LINE) wgrad_tile_line<WN, WC, KSUB, NWC, TAPS, ILVW>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
-  else wgrad_tile<WN, WC, KSUB, NWC, TAPS, NS, NWN>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
+  else wgrad_tile<WN, WC, KSUB, NWC, TAPS, NS, NWN, UP>(a, split, ks_begin, ks_end, t, tstep, n0, c0, -1);
 }
 
 constexpr int kWgradKsub = 1;
