@@ -74,6 +74,9 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // Small batches (round 3): below 128 x 256 pixels (B < 91 at 19 x 19) a 64-pixel tile on 4 waves
   // (32 x BN/2 per wave) -- B = 16 fills 91 workgroups instead of 46 (profiles/r3_small_batch.md)
   if (bm == 0) bm = (a.M >= 384 * 512) ? 386 : (a.M >= 256 * 512) ? 256 : (a.M >= 128 * 256) ? 128 : 64;
+  // round 4: below 64 x 256 pixels (B <= 45 at 19 x 19) the 32-pixel tile on 4 waves (tile 36) -- twice
+  // the workgroups of the 64 tile; SL step at B = 16: 18.6k -> 19.7k positions/s (profiles/r4/README.md)
+  if (BN != 160 && a.tile == 0 && a.M < 64 * 256) bm = 36;
   if constexpr (BN == 160) {
     if (a.Cin % 64 == 32) launch_fwd_160<MODE, true>(a, bm, st);
     else launch_fwd_160<MODE, false>(a, bm, st);
@@ -159,14 +162,14 @@ static int wgrad0_occ3() {
 }
 
 // The thin first layer's kernel rows run one workgroup per CU (180 VGPRs on 6 waves): ~1.16 us per
-// 32-pixel stage, 26-29 % MFMA busy (profiles/r3_final/pmc).  Round-4 variants (profiles/r4/README.md):
-//   10: 12 waves (4 n x 3 c, 48 x 48 per wave per tap, 104 VGPRs) -- 559 us vs 556 (equal);
+// 32-pixel stage, 26-29 % MFMA busy (profiles/r3_final/pmc).  Round-4 variants, opt-in
+// (ALPHAGO_AMD_WGRAD0_VARIANT; in-step times at B = 2176, profiles/r4/README.md):
+//   10: 12 waves (4 n x 3 c, 48 x 48 per wave per tap, 104 VGPRs): 559 us vs 556 us;
 //   11: the 6 waves with unit pipelining (wgrad_tile UP: the next tap's x fragments are read under
-//       the current tap's MFMAs; after the barrier only the dz fragments and tap 0 are exposed);
-//   12: 12 waves with unit pipelining;
-//   15: 12 with at most 85 VGPRs (two 12-wave workgroups per CU);
-//   13: the 6 waves on a 4-slot LDS ring (three stages in flight; 27 DMA pieces per stage on 6
-//       waves, the spare slots re-issue piece 0) -- 601 us (slower: the stage is not DMA-bound).
+//       the current tap's MFMAs; after the barrier only the dz fragments and tap 0 are exposed): 557 us;
+//   12: 12 waves with unit pipelining: 556 us.
+// Measured and removed: the 6 waves on a 4-slot LDS ring (601 us), 12 waves + UP capped at 85 VGPRs
+// for two workgroups per CU (56 B spilled, bench -4.5 %), UP on the 3x3 per-tap kernel (517 vs 500 us).
 template <int WN, int TAPS, int MW, int NWN = 2, int NS = 2, bool UP = false>
 static void launch_wgrad_taps48(const ConvWgradArgs& a, hipStream_t st) {
   constexpr int smem = NS * (WN + 48 * TAPS) * 64 * kWgradKsub;
@@ -199,20 +202,14 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
         launch_wgrad_taps48<WN, TAPS, 0, 4, 2, true>(a, st);
         return;
       }
-      if (a.variant == 15) {  // 12 with the registers capped for two workgroups per CU (6 waves / SIMD)
-        launch_wgrad_taps48<WN, TAPS, 6, 4, 2, true>(a, st);
-        return;
-      }
+
     }
     if constexpr (TAPS == 5) {
       if (a.variant == 11) {
         launch_wgrad_taps48<WN, TAPS, 0, 2, 2, true>(a, st);
         return;
       }
-      if (a.variant == 13) {
-        launch_wgrad_taps48<WN, TAPS, 0, 2, 4>(a, st);
-        return;
-      }
+
     }
     launch_wgrad_taps48<WN, TAPS, 0>(a, st);
     return;
@@ -262,7 +259,7 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
 #ifdef AGK_KERNEL_LAB
   if (a.variant != 9 && launch_conv_wgrad_lab(a, WN, WC, grid, st)) return;  // lab variants 2 / 3 / 4 (conv_lab.hip)
 #else
-  if (a.variant != 0 && !(a.variant >= 9 && a.variant <= 15))
+  if (a.variant != 0 && !(a.variant >= 9 && a.variant <= 12))
     throw std::invalid_argument("conv_wgrad: variant " + std::to_string(a.variant) + " is a kernel-lab variant");
 #endif
   if constexpr (WC == 64) {
@@ -272,15 +269,6 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
       else launch_wgrad_taps<WN, 5>(a, st);
       return;
     }
-  }
-  if (a.variant == 14) {  // unit pipelining (wgrad_tile UP): c block j + 1 read under c block j's MFMAs
-    static const hipError_t attr14 = hipFuncSetAttribute(
-        (const void*)conv_wgrad_kernel<WN, WC, KS, 4, 1, false, false, false, 2, 0, 2, true>,
-        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    hip_check(attr14, "hipFuncSetAttribute(max dynamic LDS)");
-    hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS, 4, 1, false, false, false, 2, 0, 2, true>), grid, dim3(512),
-                       smem, st, a);
-    return;
   }
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
@@ -337,7 +325,7 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
   }
 #endif
   // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
-  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 15) ? 0 : variant);
+  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 12) ? 0 : variant);
   const bool c48 = cin_real <= 48 && Cin == 64;
   const int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
   const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;

@@ -35,15 +35,15 @@ void conv_fwd_pk(const Tensor& x, const Tensor& w, const Tensor& bias, const Ten
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
                 int64_t Pin, int64_t Po, int64_t cin_real, int64_t variant) {
   check_dev("conv_wgrad", x, dz, slab, dbslab);
-  // 0 = per-tap kernel (default), 9 = 4-slot LDS-ring kernel (small batches), 10-13 = the thin first
-  // layer's kernel rows (conv.hip launch_wgrad_taps48, and 15), 14 = per-tap kernel with unit pipelining; the lab
-  // build also has 5 = one-kernel-row wgrad
+  // 0 = per-tap kernel (default), 9 = 4-slot LDS-ring kernel (small batches), 10-12 = the thin first
+  // layer's kernel rows on 12 waves / with unit pipelining / both; the lab build also has 5 = one-kernel-row
+  // wgrad
 #ifdef AGK_KERNEL_LAB
-  TORCH_CHECK(variant == 0 || variant == 5 || (variant >= 9 && variant <= 15), "conv_wgrad variant ", variant,
-              " unknown (0, 5, 9-15)");
+  TORCH_CHECK(variant == 0 || variant == 5 || (variant >= 9 && variant <= 12), "conv_wgrad variant ", variant,
+              " unknown (0, 5, 9-12)");
 #else
-  TORCH_CHECK(variant == 0 || (variant >= 9 && variant <= 15), "conv_wgrad variant ", variant,
-              " is not a production kernel (0, 9-15)");
+  TORCH_CHECK(variant == 0 || (variant >= 9 && variant <= 12), "conv_wgrad variant ", variant,
+              " is not a production kernel (0, 9-12)");
 #endif
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }

@@ -305,14 +305,11 @@ def wgrad_config(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
     WGRAD_RING_STAGES per split."""
     ns = wgrad_nsplit(M, cout_p, cin_p, K, cin_real, target_wgs, cus, variant)
     v0 = os.environ.get("ALPHAGO_AMD_WGRAD0_VARIANT", "0")
-    if variant == 0 and K == 5 and cin_p == 64 and 0 < cin_real <= 48 and v0 in ("10", "11", "12", "13", "15") \
-            and (cout_p % 64 == 0 or v0 in ("11", "13")):
-        # the thin first layer's kernel rows: 10 = 12 waves, 11 = unit pipelining, 12 = both, 15 = 12
-        # with two workgroups per CU, 13 = 4-slot LDS ring (conv.hip launch_wgrad_taps48)
+    if variant == 0 and K == 5 and cin_p == 64 and 0 < cin_real <= 48 and v0 in ("10", "11", "12") \
+            and (cout_p % 64 == 0 or v0 == "11"):
+        # the thin first layer's kernel rows: 10 = 12 waves, 11 = unit pipelining, 12 = both
+        # (conv.hip launch_wgrad_taps48; measured equal to the default, opt-in)
         return int(v0), ns
-    if variant == 0 and os.environ.get("ALPHAGO_AMD_WGRAD_UP", "0") == "1" and not (K == 5 and cin_p == 64) \
-            and cin_p != 160 and cin_p % 64 == 0:
-        return 14, ns  # per-tap kernel with unit pipelining
     if variant != 0 or target_wgs > 0 or os.environ.get("ALPHAGO_AMD_WGRAD_RING", "0") != "1":
         return variant, ns
     taps, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, 0)

@@ -13,3 +13,19 @@ step() {
   fi
   return 0
 }
+
+# prof NAME SECONDS OUTDIR_STEPS [bench args]: rocprofv3 kernel trace of bench.py, the per-step timeline
+# (scripts/timeline.py) kept, the raw trace deleted (gpurun copies back at most 64 MiB)
+prof() {
+  local name=$1 secs=$2 steps=$3
+  shift 3
+  step $name $secs bash scripts/profile_step.sh $O/$name "$@"
+  local f
+  f=$(ls $O/$name/*/*kernel_trace.csv 2>/dev/null | head -1)
+  if [ -n "$f" ]; then
+    python3 scripts/timeline.py "$f" $steps > $O/$name.timeline.txt 2>&1
+    head -12 $O/$name.timeline.txt
+    tail -2 $O/$name.timeline.txt
+    rm -f "$f"
+  fi
+}
