@@ -130,6 +130,9 @@ class HipConvTrainer:
         self.wgrad_variant = int(os.environ.get("ALPHAGO_AMD_WGRAD_VARIANT", "0")) if wgrad_variant is None \
             else int(wgrad_variant)
         self.conv_tile = conv_tile  # forward/dgrad tiling: 0 = automatic, or 128 / 256 / 384 / 385
+        # kernel-lab A/B only: the 3x3 forwards and dgrads on a lab tiling of the lab library
+        # (torch.ops.alphago_amd_lab), e.g. 5 = compact halo + ping-pong (profiles/r3_chunk_outer.md)
+        self.lab_tile = int(os.environ.get("ALPHAGO_AMD_LAB_TILE", "0"))
         if precision not in ("bf16", "fp8"):
             raise ValueError("precision must be bf16 or fp8")
         self.precision = precision
@@ -388,6 +391,9 @@ class HipConvTrainer:
         x, pin = self._layer_in(l)
         if l == 0 and self.pk0:
             ops.conv_fwd_pk(x, self.wf[0], self.bias_p[0], self.Y[0], self.K[0], self.S, pin, 1, self.C0, mbits)
+        elif self.lab_tile and self.K[l] == 3:
+            ops.lab().conv_fwd(x, self.wf[l], self.bias_p[l], None, self.Y[l], 3, self.S, pin, 1, 0, mbits,
+                               self.lab_tile)
         else:
             ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1, mbits=mbits,
                          tile=self.conv_tile)
@@ -509,6 +515,9 @@ class HipConvTrainer:
                     ops.conv_dgrad_fp8_bf16(self.DZ[l], self.wd8[l], self.MBITS[l - 1], self.gscales8[l],
                                             self.gosc8[l:l + 1], self.K[l], self.S, self.DZ[l - 1],
                                             amax=self.gamax8[l - 1])
+                elif self.lab_tile and self.K[l] == 3:  # kernel-lab A/B (see __init__)
+                    ops.lab().conv_fwd(self.DZ[l], self.wd[l], None, None, self.DZ[l - 1], 3, self.S, 1, 1,
+                                       ops.MODE_MASKBITS, self.MBITS[l - 1], self.lab_tile)
                 else:  # ReLU' bitmask from the forward epilogue (bf16 and fp8 forwards write it)
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=self.conv_tile)
