@@ -30,7 +30,9 @@ def main():
     ap.add_argument("--iterations", type=int, default=2)
     ap.add_argument("--filters", type=int, default=192)
     ap.add_argument("--layers", type=int, default=12)
-    ap.add_argument("--minibatch", type=int, default=256)
+    ap.add_argument("--minibatch", type=int, default=0,
+                    help="REINFORCE chunk (gradients accumulate over chunks, ONE update per iteration, so the "
+                         "chunk size does not change the step); 0 = 2048 at >= 128 games/iteration, else 512")
     ap.add_argument("--max-moves", type=int, default=500)
     ap.add_argument("--records", default="host,device")
     ap.add_argument("--drivers", default="native,python",
@@ -41,9 +43,13 @@ def main():
     learner = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=a.filters, layers=a.layers, device=dev)
     opp = CNNPolicy(DEFAULT_FEATURES, filters_per_layer=a.filters, layers=a.layers, device=dev)
     opp.model.load_state_dict(learner.model.state_dict())
-    trainer = make_policy_trainer(learner.model, a.minibatch, 0.001, 0.0, device=dev)
     arms = [(d, m) for d in a.drivers.split(",") for m in a.records.split(",")]
+    trainers = {}
     for g in [int(x) for x in a.games.split(",")]:
+        mb = a.minibatch or (2048 if g >= 128 else 512)
+        if mb not in trainers:
+            trainers[mb] = make_policy_trainer(learner.model, mb, 0.001, 0.0, device=dev)
+        trainer = trainers[mb]
         for driver, mode in arms:
             nat = driver == "native"
             ls = BatchedSampler(learner, 1.0, seed=1)
@@ -52,7 +58,7 @@ def main():
             # warm-up iteration (graph captures for the batch sizes, code objects)
             rec = play_games(ls, os_, g, max_moves=a.max_moves, rng=rng, device_records=(mode == "device"),
                              native=nat)
-            rl_update(trainer, rec, a.minibatch, dev)
+            rl_update(trainer, rec, mb, dev)
             learner.refresh()
             if dev.type == "cuda":
                 torch.cuda.synchronize()
@@ -65,7 +71,7 @@ def main():
                 if dev.type == "cuda":
                     torch.cuda.synchronize()
                 t1 = time.perf_counter()
-                info = rl_update(trainer, rec, a.minibatch, dev)
+                info = rl_update(trainer, rec, mb, dev)
                 learner.refresh()
                 if dev.type == "cuda":
                     torch.cuda.synchronize()
@@ -80,7 +86,7 @@ def main():
                               "games_per_s": round(games / tot, 2), "learner_positions_per_s": round(positions / tot, 1),
                               "moves_per_s": round(moves / tot, 1), "play_s_per_it": round(t_play / a.iterations, 3),
                               "update_s_per_it": round(t_upd / a.iterations, 3),
-                              "positions_per_it": positions // a.iterations,
+                              "positions_per_it": positions // a.iterations, "reinforce_chunk": mb,
                               "net": "%dx%d" % (a.layers, a.filters)}), flush=True)
 
 
