@@ -91,6 +91,7 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     // 32-pixel tiles (twice the workgroups of the 64 tile at small batches): 36 = 4 waves of 16 x BN/2,
     // 37 = 2 waves of 32 x BN/2; same ReLU' bitmask layout
     else if (bm == 36) launch_fwd_bm<BN, MODE, 32, 1>(a, st);
+    else if (bm == 38) launch_fwd_splitk<BN, MODE>(a, st);  // 36 with split-K (conv_fwd_splitk op)
     else if (bm == 37) launch_fwd_bm<BN, MODE, 32, 2>(a, st);
     // small batches: 65 / 130 = the 64 / 128-pixel tiles on a 4 / 3-slot LDS ring (NS above)
     else if (bm == 65) launch_fwd_bm<BN, MODE, 64, 2, true, true, false, false, false, false, 4>(a, st);

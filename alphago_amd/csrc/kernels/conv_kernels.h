@@ -4,6 +4,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <stdexcept>
+
 #include "common.h"
 #include "conv_common.h"
 #include "kernels.h"
@@ -28,8 +30,13 @@ namespace agk {
 // NS > 2 (small batches): an NS-slot LDS ring, the DMA of step ks + NS - 1 issued while step ks
 // computes.  With few workgroups per CU nothing else hides the global->LDS latency of a 2-buffer
 // loop (~0.75 us per K-step at B = 16, 27 steps per 3x3 layer: profiles/r3_small_batch/).
+// SK (split-K, small batches): blockIdx.z = split z of gridDim.z; the workgroup runs K-steps
+// [nK z / nz, nK (z+1) / nz) and writes its raw fp32 partial tile to a.sk_ws[z][m][n];
+// conv_splitk_finish_kernel sums the splits and applies the epilogue.  At B = 16 a 3x3 layer is 181
+// 32-pixel tiles of 27 serial K-steps (~0.7 us each, whatever the DMA scheme): splitting K shortens
+// that chain and fills the CUs.
 template <int BN, int MODE, int BM, int MBW, bool EPF = true, bool PIPE = true, bool M32 = false, bool ILV = false,
-          bool STR = false, bool CO = false, int NS = 2>
+          bool STR = false, bool CO = false, int NS = 2, bool SK = false>
 __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a) {
   // (BM / (16 MBW)) x 2 waves; each wave owns a 16*MBW (m) x BN/2 (n) output tile
   constexpr int NW = BM / (16 * MBW) * 2;  // waves per workgroup
@@ -235,6 +242,43 @@ __global__ __launch_bounds__(BM / MBW * 8, 1) void conv_fwd_kernel(ConvFwdArgs a
     ep.store(a, acc, ep_mrow);
     return;
   }
+  if constexpr (SK) {
+    static_assert(PIPE && !M32 && !ILV && !CO, "split-K: the pipelined 2-buffer loop, tap-outer order");
+    const int z = blockIdx.z, nz = gridDim.z;
+    const int kb = (int)((long)nK * z / nz), ke = (int)((long)nK * (z + 1) / nz);
+    for (int i = 0; i < kb; ++i) st_advance();  // scalar cursor to step kb
+    if (kb < ke) {  // workgroup-uniform
+      stage(0);
+      wait_vmcnt0();
+      __syncthreads();
+      read_frags(smem, 0, xa, wa);
+      for (int ks = kb; ks < ke; ++ks) {
+        const int cur = (ks - kb) & 1;
+        const char* base = smem + cur * STAGE;
+        if (ks + 1 < ke) stage(cur ^ 1);
+        read_frags(base, 1, xb, wb);
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+        mfmas(xa, wa);
+        mfmas(xb, wb);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        wait_vmcnt0();
+        __syncthreads();
+        if (ks + 1 < ke) read_frags(smem + (cur ^ 1) * STAGE, 0, xa, wa);
+      }
+    }
+    // raw partial sums: lane owns channels ep_nbase + 16 i + [0, 4) of pixel ep_mrow + 16 j
+    float* ws = a.sk_ws + (size_t)z * a.M * a.Cout;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+      const int m = ep_mrow + j * 16;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) *(f32x4*)(ws + (size_t)m * a.Cout + ep_nbase + i * 16) = acc[i][j];
+    }
+    return;
+  }
   int xo00, xo01;  // step 0's source offsets (ILV: the re-staged operands when nK == 1)
   size_t wo00, wo01;
   st_offsets(xo00, xo01, wo00, wo01);
@@ -407,6 +451,78 @@ static void launch_fwd_bm(const ConvFwdArgs& a, hipStream_t st) {
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
   hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, EPF, PIPE, M32, ILV, STR, CO, NS>), grid,
                      dim3(BM / MBW * 8), smem, st, a);
+}
+
+// Split-K finish: one thread per (pixel, bitmask word); word w of a pixel covers the channels
+// tn * BN + wn * BN/2 + 4 q + 16 i + r (tn = w / 8, wn = (w / 4) % 2, q = w % 4; i < NB = BN / 32,
+// r < 4) -- the channels one lane of the conv epilogue owns, so the bitmask layout is the tile's.
+template <int MODE, int NB>
+__global__ __launch_bounds__(256) void conv_splitk_finish_kernel(ConvFwdArgs a) {
+  constexpr int BN = 32 * NB;
+  const int WPP = (a.Cout / BN) * 8;
+  const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (long)a.M * WPP) return;
+  const int m = (int)(gid / WPP), w = (int)(gid - (long)m * WPP);
+  const int base = (w >> 3) * BN + ((w >> 2) & 1) * (BN / 2) + 4 * (w & 3);
+  f32x4 v[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < a.sk_nsplit; ++z) {
+    const float* src = a.sk_ws + ((size_t)z * a.M + m) * a.Cout + base;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) v[i] += *(const f32x4*)(src + 16 * i);
+  }
+  const int SS = a.S * a.S;
+  const int b = fdiv(m, a.divSS);
+  const int rem = m - b * SS;
+  const int ii = fdiv(rem, a.divS);
+  const int jj = rem - ii * a.S;
+  const size_t pix = (size_t)(b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po;
+  uint32_t mw = 0u, bits = 0u;
+  if constexpr (MODE == MODE_MASKBITS) mw = a.mbits_in[pix * WPP + w];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    float o4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = v[i][r];
+      if constexpr (MODE == MODE_BIAS_RELU) x = fmaxf(x + a.bias[base + 16 * i + r], 0.f);
+      if constexpr (MODE == MODE_MASKBITS) x = ((mw >> (4 * i + r)) & 1u) ? x : 0.f;
+      o4[r] = x;
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o[r] = (__bf16)o4[r];
+      if constexpr (MODE == MODE_BIAS_RELU) bits |= ((float)o[r] > 0.f ? 1u : 0u) << (4 * i + r);
+    }
+    *(bf16x4*)(a.y + pix * a.Cout + base + 16 * i) = o;
+  }
+  if constexpr (MODE == MODE_BIAS_RELU)
+    if (a.mbits_out) a.mbits_out[pix * WPP + w] = bits;
+}
+
+// tile code 38: the 32-pixel tile (36) with split-K over a.sk_nsplit workgroups per tile, then the finish
+template <int BN, int MODE>
+static void launch_fwd_splitk(const ConvFwdArgs& a, hipStream_t st) {
+  if constexpr (MODE == MODE_MASK) {
+    throw std::invalid_argument("conv_fwd split-K: modes 0 (bias + ReLU), 2 (none) and 3 (bitmask dgrad)");
+  } else {
+    if (!a.sk_ws || a.sk_nsplit < 1 || a.y_bf8)
+      throw std::invalid_argument("conv_fwd split-K (tile 38): needs a workspace and nsplit >= 1, no e5m2 copy");
+    constexpr int BM = 32, MBW = 1;
+    constexpr int smem = 2 * (BM * 128 + BN * 128);
+    static const hipError_t attr = hipFuncSetAttribute(
+        (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, true, true, false, false, false, false, 2, true>,
+        hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+    dim3 grid((a.M + BM - 1) / BM, a.Cout / BN, a.sk_nsplit);
+    hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, true, true, false, false, false, false, 2, true>), grid,
+                       dim3(BM / MBW * 8), smem, st, a);
+    const long threads = (long)a.M * (a.Cout / BN) * 8;
+    hipLaunchKernelGGL((conv_splitk_finish_kernel<MODE, BN / 32>), dim3((unsigned)((threads + 255) / 256)), dim3(256),
+                       0, st, a);
+  }
 }
 
 // ----------------------------------------------------------------- packed-tap forward (thin first layer)

@@ -29,6 +29,10 @@ struct ConvFwdArgs {
   uint8_t* y_bf8;
   const float* bf8_scale;
   unsigned* bf8_amax;
+  // split-K (tile code 38, small batches): fp32 partial sums [sk_nsplit][M][Cout], finished by
+  // conv_splitk_finish_kernel (bias + ReLU + bitmask, or the bitmask of dgrad)
+  float* sk_ws;
+  int sk_nsplit;
 };
 
 struct ConvWgradArgs {

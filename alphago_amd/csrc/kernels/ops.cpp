@@ -31,6 +31,16 @@ void conv_fwd_pk(const Tensor& x, const Tensor& w, const Tensor& bias, const Ten
                 c10::nullopt, c10::nullopt, (int)((cin_real + 7) / 8));
 }
 
+// Small batches: the 32-pixel tile with the K loop split over nsplit workgroups per tile (tile 38) into
+// ws (>= nsplit * M * Cout fp32), then one finishing pass (bias + ReLU + bitmask, or the bitmask dgrad)
+void conv_fwd_splitk(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const Tensor& y, int64_t K,
+                     int64_t S, int64_t Pin, int64_t Po, int64_t mode, const c10::optional<Tensor>& mbits,
+                     const Tensor& ws, int64_t nsplit) {
+  check_dev("conv_fwd_splitk", x, w, bias, y, mbits, ws);
+  conv_fwd_impl(x, w, bias, c10::nullopt, y, K, S, Pin, Po, mode, mbits, 38, nullptr, -1, c10::nullopt, c10::nullopt,
+                c10::nullopt, 0, ws, (int)nsplit);
+}
+
 // slab: (nsplit, T, Cout, Cin) f32; dbslab: (nsplit, Cout) f32
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
                 int64_t Pin, int64_t Po, int64_t cin_real, int64_t variant) {
@@ -668,6 +678,9 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
       "Tensor(b!)? mbits=None, int tile=0) -> ()");
+  m.def(
+      "conv_fwd_splitk(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
+      "Tensor(b!)? mbits, Tensor(c!) ws, int nsplit) -> ()");
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0, int variant=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def("conv_dgrad_bits_bf8(Tensor dz, Tensor wd, Tensor(a!) dx, Tensor mbits, Tensor(b!) dx8, Tensor scale, "
@@ -733,6 +746,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("conv_fwd", &conv_fwd);
   m.impl("sgd_pack", &sgd_pack);
   m.impl("conv_fwd_pk", &conv_fwd_pk);
+  m.impl("conv_fwd_splitk", &conv_fwd_splitk);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);
   m.impl("conv_dgrad_bits_bf8", &conv_dgrad_bits_bf8);

@@ -68,8 +68,9 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
                           unsigned long long* dbg = nullptr, long long x_elems_override = -1,
                           const c10::optional<Tensor>& y_bf8 = c10::nullopt,
                           const c10::optional<Tensor>& bf8_scale = c10::nullopt,
-                          const c10::optional<Tensor>& bf8_amax = c10::nullopt, int pk_cpt = 0) {
-  check_dev("conv_fwd_impl", x, w, bias, mask, y, mbits, y_bf8, bf8_scale, bf8_amax);
+                          const c10::optional<Tensor>& bf8_amax = c10::nullopt, int pk_cpt = 0,
+                          const c10::optional<Tensor>& sk_ws = c10::nullopt, int sk_nsplit = 0) {
+  check_dev("conv_fwd_impl", x, w, bias, mask, y, mbits, y_bf8, bf8_scale, bf8_amax, sk_ws);
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(y);
   CHECK_CONTIG(x); CHECK_CONTIG(w); CHECK_CONTIG(y);
   CHECK_BF16(x); CHECK_BF16(w); CHECK_BF16(y);
@@ -135,6 +136,17 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
                       bf8_amax->is_contiguous(), "bf8_amax: int32[64]");
       a.bf8_amax = reinterpret_cast<unsigned*>(bf8_amax->data_ptr<int>());
     }
+  }
+  if (sk_ws.has_value()) {  // split-K (tile 38): fp32 partials [nsplit][M][Cout]
+    CHECK_F32(*sk_ws); CHECK_CONTIG(*sk_ws);
+    TORCH_CHECK(tile == 38 && sk_nsplit >= 1 && sk_nsplit <= 64, "split-K: tile 38, 1 <= nsplit <= 64");
+    TORCH_CHECK(Cout != 160 && Cin % 64 == 0, "split-K: 64 / 128 / 192-wide tiles");
+    TORCH_CHECK(mode != agk::MODE_MASK && !y_bf8.has_value(), "split-K: modes 0, 2, 3 without an e5m2 copy");
+    TORCH_CHECK(sk_ws->numel() >= (int64_t)sk_nsplit * a.M * Cout, "split-K workspace too small: nsplit*M*Cout");
+    a.sk_ws = sk_ws->data_ptr<float>();
+    a.sk_nsplit = sk_nsplit;
+  } else {
+    TORCH_CHECK(tile != 38, "tile 38 (split-K) needs a workspace: conv_fwd_splitk");
   }
   if (a.M == 0) return;
   if (pk_cpt > 0) agk::launch_conv_fwd_pk(a, pk_cpt, cur_stream());

@@ -176,3 +176,19 @@ def value_teacher_pool(n: int, teacher, seed: int, chunk: int = 8192, threads: i
         done += len(pl)
     del torch
     return planes, tgt
+
+
+def value_material_pool(n: int, seed: int, size: int = 19, threads: int = 16) -> Tuple[np.ndarray, np.ndarray]:
+    """(planes (n, 49, S, S) uint8, targets (n,) float32 in (-1, 1)): random-game positions in the value
+    net's 49 planes labelled tanh((d + 2 a) / s): d = own minus opponent stones (board planes 0 / 1), a =
+    opponent minus own stones in atari (the one-liberty plane, 12, masked by colour), s = their standard
+    deviation over the pool.  Symmetric under D4, so the augmentation keeps the labels; a learnable
+    regression target (counts and a local product) for the value-net precision parity run."""
+    from ..features import VALUE_FEATURES, Preprocess
+
+    rng = np.random.default_rng(seed)
+    pre = Preprocess(VALUE_FEATURES)
+    planes = pre.states_to_uint8(random_game_states(n, rng, size=size), threads)[:n]
+    own, opp, atari = (planes[:, i].astype(np.float32) for i in (0, 1, 12))
+    raw = own.sum((1, 2)) - opp.sum((1, 2)) + 2.0 * ((opp * atari).sum((1, 2)) - (own * atari).sum((1, 2)))
+    return planes, np.tanh(raw / max(float(raw.std()), 1e-6)).astype(np.float32)

@@ -129,6 +129,11 @@ class HipTrunkInference:
         bk.legal = torch.ones((B, S * S), dtype=torch.uint8, device=dev)
         bk.X0 = ops.padded_empty(B, S, self.P0, self.C0p, dev)
         bk.Y = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(2)]
+        # small buckets: the split-K 32-pixel conv (ops.conv_fwd_splitk), fp32 partials in bk.ws
+        M = B * S * S
+        bk.sk = [1 if (l == 0 and self.pk0) or self.precision != "bf16" else
+                 ops.splitk_nsplit(M, self.Fp, self.C0p if l == 0 else self.Fp, self.K[l]) for l in range(self.L)]
+        bk.ws = torch.empty(max(bk.sk) * M * self.Fp, device=dev) if max(bk.sk) > 1 else None
         if self.precision == "fp8":
             bk.X08 = torch.zeros(bk.X0.shape, dtype=torch.uint8, device=dev)
             bk.Y8 = [torch.zeros(bk.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -175,6 +180,9 @@ class HipTrunkInference:
             y = bk.Y[l % 2]
             if l == 0 and self.pk0:
                 ops.conv_fwd_pk(x, self.wf[0], self.bias_p[0], y, self.K[0], self.S, pin, 1, self.C0)
+            elif bk.sk[l] > 1:
+                ops.conv_fwd_splitk(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1, ops.MODE_BIAS_RELU,
+                                    None, bk.ws, bk.sk[l])
             else:
                 ops.conv_fwd(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1)
             if getattr(self, "_calibrating", False):

@@ -131,6 +131,31 @@ def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: 
     return y
 
 
+# split-K forward / dgrad (tile 38) below this many output pixels (B <= 45 at 19 x 19); ALPHAGO_AMD_SPLITK=0
+# turns it off
+SPLITK_MAX_M = 64 * 256
+SPLITK_TARGET_WGS = 512
+
+
+def splitk_nsplit(M: int, cout_p: int, cin_p: int, K: int, target_wgs: int = SPLITK_TARGET_WGS) -> int:
+    """Split count of the small-batch split-K conv (conv_fwd_splitk): enough 32-pixel workgroups for
+    ``target_wgs``, at least three K-steps (64-channel chunks of a tap) per split; 1 = no split
+    (large M, the 160-wide value tiles, ALPHAGO_AMD_SPLITK=0)."""
+    if M >= SPLITK_MAX_M or cout_p == 160 or cin_p % 64 or os.environ.get("ALPHAGO_AMD_SPLITK", "1") == "0":
+        return 1
+    tiles = (M + 31) // 32 * (cout_p // conv_n_tile(cout_p))
+    nk = K * K * (cin_p // 64)
+    return max(1, min(nk // 3, -(-target_wgs // tiles), 64))
+
+
+def conv_fwd_splitk(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int, mode: int, mbits, ws, nsplit: int):
+    """conv_fwd on the 32-pixel tile with its K loop split over ``nsplit`` workgroups per tile (fp32
+    partials in ``ws``, >= nsplit * M * Cout floats) and one finishing pass: modes 0 (bias + ReLU,
+    optional bitmask), 2 (none), 3 (bitmask dgrad)."""
+    _ops().conv_fwd_splitk(x, w_packed, bias, y, K, S, Pin, Po, mode, mbits, ws, nsplit)
+    return y
+
+
 def pk_shape_ok(cin_real: int, cin_p: int) -> bool:
     """Whether the packed-tap forward (conv_fwd_pk) can run a first layer: 32 < cin_real < 64 real input
     channels in a 64-channel padded input (48 policy / 49 value planes)."""

@@ -207,6 +207,19 @@ class HipConvTrainer:
             self.wgrad_var.append(var)
             slab_max = max(slab_max, ns * T * self.Fp * cin_p)
             db_max = max(db_max, ns * self.Fp)
+        # small batches (B <= 45): forward and bitmask dgrad on the split-K 32-pixel tile
+        # (ops.conv_fwd_splitk: the K loop of a tile over several workgroups, one finishing pass);
+        # bf16 path with the automatic tiling only
+        self.sk_fwd = [1] * self.L
+        self.sk_dg = [1] * self.L
+        if conv_tile == 0 and self.precision == "bf16" and not self.lab_tile:
+            for l in range(self.L):
+                cin_p = self.C0p if l == 0 else self.Fp
+                self.sk_fwd[l] = 1 if (l == 0 and self.pk0) else ops.splitk_nsplit(M, self.Fp, cin_p, self.K[l])
+                if l > 0:
+                    self.sk_dg[l] = ops.splitk_nsplit(M, self.Fp, self.Fp, self.K[l])
+        sk_max = max(self.sk_fwd + self.sk_dg)
+        self._sk_ws = torch.empty(sk_max * M * self.Fp, device=dev) if sk_max > 1 else None
         # Split-K reduce on a side stream (serial backward only): the memory-bound reduce of
         # layer l runs beside dgrad(l) instead of between the two big conv kernels.  The
         # slabs are double-buffered by layer parity, so wgrad(l-1) never waits for
@@ -394,6 +407,9 @@ class HipConvTrainer:
         elif self.lab_tile and self.K[l] == 3:
             ops.lab().conv_fwd(x, self.wf[l], self.bias_p[l], None, self.Y[l], 3, self.S, pin, 1, 0, mbits,
                                self.lab_tile)
+        elif self.sk_fwd[l] > 1:
+            ops.conv_fwd_splitk(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1,
+                                ops.MODE_BIAS_RELU, mbits, self._sk_ws, self.sk_fwd[l])
         else:
             ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1, mbits=mbits,
                          tile=self.conv_tile)
@@ -518,6 +534,9 @@ class HipConvTrainer:
                 elif self.lab_tile and self.K[l] == 3:  # kernel-lab A/B (see __init__)
                     ops.lab().conv_fwd(self.DZ[l], self.wd[l], None, None, self.DZ[l - 1], 3, self.S, 1, 1,
                                        ops.MODE_MASKBITS, self.MBITS[l - 1], self.lab_tile)
+                elif self.sk_dg[l] > 1:  # small batches: split-K bitmask dgrad
+                    ops.conv_fwd_splitk(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
+                                        ops.MODE_MASKBITS, self.MBITS[l - 1], self._sk_ws, self.sk_dg[l])
                 else:  # ReLU' bitmask from the forward epilogue (bf16 and fp8 forwards write it)
                     ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=self.conv_tile)

@@ -16,6 +16,7 @@ After the first epoch the script also compares one batch's gradients of the fp8 
 at the bf16 arm's weights (per-layer cosine), on the 12-layer trunk.
 
 Usage: python scripts/value_fp8_parity.py OUT_JSON [--positions N] [--epochs E] [--arms a,b,c]
+       [--task teacher|material] [--init keras|he] [--lr R]
 Prints one JSON line and writes it to OUT_JSON."""
 import argparse
 import copy
@@ -78,14 +79,24 @@ def main():
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--arms", default="torch-fp32,hip-bf16,hip-fp8")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--task", default="teacher", choices=["teacher", "material"],
+                    help="teacher: a random-init value teacher's outputs; material: tanh of the stone and atari "
+                         "balance (data/synthetic.py value_material_pool)")
+    ap.add_argument("--init", default="keras", choices=["keras", "he"],
+                    help="student init: keras = the reference's uniform(-0.05, 0.05); he = uniform He bounds "
+                         "(the reference init shrinks a 12-layer trunk's signal ~30x)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     t0 = time.perf_counter()
     rng = np.random.default_rng(a.seed)
-    probe = Preprocess(VALUE_FEATURES).states_to_uint8(random_game_states(2048, rng))
-    teacher = value_teacher(49, a.filters, a.layers, device=dev, probe=probe)
-    planes, z = value_teacher_pool(a.positions + a.heldout, teacher, seed=a.seed + 1)
-    del teacher
+    if a.task == "teacher":
+        probe = Preprocess(VALUE_FEATURES).states_to_uint8(random_game_states(2048, rng))
+        teacher = value_teacher(49, a.filters, a.layers, device=dev, probe=probe)
+        planes, z = value_teacher_pool(a.positions + a.heldout, teacher, seed=a.seed + 1)
+        del teacher
+    else:
+        from alphago_amd.data.synthetic import value_material_pool
+        planes, z = value_material_pool(a.positions + a.heldout, seed=a.seed + 1)
     torch.cuda.empty_cache()
     t_data = time.perf_counter() - t0
     print("data: %d positions in %.1f s, target std %.3f" % (len(z), t_data, float(np.std(z))), flush=True)
@@ -101,6 +112,14 @@ def main():
     syms = [torch.randint(0, 8, (a.positions,), dtype=torch.int32, generator=g) for _ in range(a.epochs)]
     torch.manual_seed(a.seed + 100)
     student0 = ValueNet(49, filters_per_layer=a.filters, layers=a.layers)
+    if a.init == "he":
+        with torch.no_grad():
+            for w in list(student0.trunk.weights) + [student0.head_w]:
+                bound = (6.0 / (w.shape[1] * w.shape[2] * w.shape[3])) ** 0.5
+                w.uniform_(-bound, bound)
+            for w in (student0.fc1_w, student0.fc2_w):  # Keras (in, out) layout: fan_in = rows
+                bound = (3.0 / w.shape[0]) ** 0.5
+                w.uniform_(-bound, bound)
     res = {"teacher_target_std": round(float(Z.std()), 4), "heldout_var": round(float(Zho.var()), 5)}
     arms = {}
     mid_net = None
@@ -138,7 +157,8 @@ def main():
         res["grad_cosine_bf16_vs_fp32_after_epoch1"] = grad_cosines("hip-bf16", "torch-fp32", mid_net,
                                                                     Ptr.index_select(0, idx), Ztr.index_select(0, idx),
                                                                     B, a.lr, dev)
-    out = {"metric": "value-net held-out MSE on a value-teacher task (12x152, 49 planes)", "positions": a.positions,
+    out = {"metric": "value-net held-out MSE on a learnable value task (%dx%d, 49 planes)" % (a.layers, a.filters),
+           "task": a.task, "init": a.init, "positions": a.positions,
            "heldout": a.heldout, "epochs": a.epochs, "batch": B, "lr": a.lr, "data_s": round(t_data, 1),
            "net": "%dx%d" % (a.layers, a.filters), **res}
     print(json.dumps(out), flush=True)

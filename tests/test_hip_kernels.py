@@ -620,6 +620,50 @@ def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, monkeypatch, B, tile
     assert _rel_err(gb, g.sum(dim=(0, 2, 3))) < 2e-3
 
 
+@pytest.mark.parametrize("B,S,Cin,Cout,K,ns", [(1, 19, 192, 192, 3, 9), (4, 19, 192, 192, 3, 3), (16, 19, 192, 192, 3, 3),
+                                            (3, 19, 64, 192, 5, 8), (5, 13, 128, 128, 3, 4), (7, 9, 64, 64, 3, 2),
+                                            (2, 19, 192, 192, 3, 1)])
+def test_conv_fwd_splitk(ops, cuda_device, B, S, Cin, Cout, K, ns):
+    """Split-K 32-pixel conv (tile 38: the K loop over ns workgroups per tile, fp32 partials, one
+    finishing pass): forward with bias + ReLU + bitmask and the bitmask dgrad vs fp32 conv2d /
+    conv2d_input, and its bitmask equal to the one-pass tile-36 kernel's (up to pre-activations that
+    round across zero)."""
+    torch.manual_seed(21)
+    P = K // 2
+    x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
+    w = _bf(torch.randn(Cout, Cin, K, K, device=cuda_device) * 0.05)
+    b = torch.randn(Cout, device=cuda_device) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=P))
+    wf = ops.packed_weight_like(w, Cin, Cout)
+    ops.pack_weights([w.contiguous()], [wf])
+    xp = ops.to_padded(x, P)
+    M = B * S * S
+    ws = torch.full((ns * M * Cout,), float("nan"), device=cuda_device)
+    words = ops.mbits_words(Cout)
+    mb = torch.full((B * (S + 2) ** 2 * words,), -1, dtype=torch.int32, device=cuda_device)
+    mb36 = mb.clone()
+    y = ops.padded_empty(B, S, 1, Cout, cuda_device)
+    y36 = ops.padded_empty(B, S, 1, Cout, cuda_device)
+    ops.conv_fwd_splitk(xp, wf, b, y, K, S, P, 1, ops.MODE_BIAS_RELU, mb, ws, ns)
+    ops.conv_fwd(xp, wf, b, y36, K, S, P, 1, mbits=mb36, tile=36)
+    torch.cuda.synchronize()
+    assert _rel_err(ops.from_padded(y, 1), ref) < 1e-2
+    assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
+    assert (mb != mb36).float().mean().item() < 1e-3
+    if Cin != Cout or K != 3:
+        return
+    # bitmask dgrad through the same workspace (Cin == Cout: the transposed 3x3 pack)
+    wd = ops.packed_weight_like(w, Cin, Cout, True)
+    ops.pack_weights([w.contiguous()], [wf], [wd])
+    g = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
+    dx = ops.padded_empty(B, S, 1, Cin, cuda_device)
+    ops.conv_fwd_splitk(ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, ops.MODE_MASKBITS, mb36, ws, ns)
+    torch.cuda.synchronize()
+    y36f = ops.from_padded(y36, 1)
+    ref_dx = torch.nn.grad.conv2d_input((B, Cin, S, S), w, g, padding=1) * (y36f > 0)
+    assert _rel_err(ops.from_padded(dx, 1), ref_dx) < 1e-2
+
+
 @pytest.mark.parametrize("S,B,Cin,Cout,Cout_p", [(19, 5, 48, 192, 192), (19, 3, 49, 152, 160), (9, 7, 48, 192, 192),
                                                  (13, 2, 49, 152, 160), (19, 1, 40, 128, 128)])
 def test_conv_fwd_packed_taps_first_layer(ops, cuda_device, S, B, Cin, Cout, Cout_p):

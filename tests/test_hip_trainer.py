@@ -294,3 +294,33 @@ def test_packed_tap_first_layer_trainer_matches(cuda_device, monkeypatch, kind, 
         if gb.norm() < 1e-6 * b.fp.grad.norm():  # the policy head's scalar bias: softmax rows sum to 1
             continue
         assert torch.nn.functional.cosine_similarity(ga, gb, dim=0) > 0.995, name
+
+
+@pytest.mark.parametrize("B", [16, 3])
+def test_splitk_small_batch_trainer_matches(cuda_device, monkeypatch, B):
+    """Small batches run the forward and the bitmask dgrad on the split-K 32-pixel tile
+    (ops.conv_fwd_splitk); same loss and gradients as ALPHAGO_AMD_SPLITK=0 up to summation order."""
+    import copy
+
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.train.engine import HipPolicyTrainer
+
+    torch.manual_seed(6)
+    net = PolicyNet(48, filters_per_layer=192, layers=4)
+    trs = []
+    for sk in ("1", "0"):
+        monkeypatch.setenv("ALPHAGO_AMD_SPLITK", sk)
+        trs.append(HipPolicyTrainer(copy.deepcopy(net), B, lr=0.05, device=cuda_device))
+    assert max(trs[0].sk_fwd) > 1 and max(trs[0].sk_dg) > 1 and max(trs[1].sk_fwd + trs[1].sk_dg) == 1
+    planes = torch.randint(0, 2, (B, 48, 19, 19), dtype=torch.uint8, device=cuda_device)
+    tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    for t in trs:
+        t.compute_grads(planes, tgt)
+    torch.cuda.synchronize()
+    a, b = trs
+    assert abs(a.loss.sum().item() - b.loss.sum().item()) < 1e-2 * abs(b.loss.sum().item())
+    for name in a.fp.names:
+        ga, gb = a.fp.grad_views[name].double().flatten(), b.fp.grad_views[name].double().flatten()
+        if gb.norm() < 1e-6 * b.fp.grad.norm():
+            continue
+        assert torch.nn.functional.cosine_similarity(ga, gb, dim=0) > 0.999, name
