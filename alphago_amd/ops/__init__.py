@@ -131,10 +131,11 @@ def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: 
     return y
 
 
-# split-K forward / dgrad (tile 38) below this many output pixels (B <= 9 at 19 x 19); ALPHAGO_AMD_SPLITK=0
-# turns it off.  SL step (profiles/r4/README.md): B = 4 5.3k -> 5.9k positions/s, but B = 16 19.5k -> 16.9k
-# (the split conv kernels are no faster there and the finishing passes add 110 us per step)
-SPLITK_MAX_M = 3300
+# split-K forward / dgrad (tile 38) below this many output pixels (B <= 4 at 19 x 19); ALPHAGO_AMD_SPLITK=0
+# turns it off.  SL step (profiles/r4/README.md): B = 1 1.33k -> 1.74k positions/s, B = 4 5.3k -> 5.9k, but
+# B = 8 10.5k -> 10.1k and B = 16 19.5k -> 16.9k (the split conv kernels are no faster there and the
+# finishing passes add ~5 us per layer)
+SPLITK_MAX_M = 1500
 SPLITK_TARGET_WGS = 512
 
 

@@ -296,7 +296,7 @@ def test_packed_tap_first_layer_trainer_matches(cuda_device, monkeypatch, kind, 
         assert torch.nn.functional.cosine_similarity(ga, gb, dim=0) > 0.995, name
 
 
-@pytest.mark.parametrize("B", [8, 3])
+@pytest.mark.parametrize("B", [4, 1])
 def test_splitk_small_batch_trainer_matches(cuda_device, monkeypatch, B):
     """Small batches run the forward and the bitmask dgrad on the split-K 32-pixel tile
     (ops.conv_fwd_splitk); same loss and gradients as ALPHAGO_AMD_SPLITK=0 up to summation order."""

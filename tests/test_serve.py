@@ -257,8 +257,10 @@ def test_batcher_on_hip_engine_matches_direct(cuda_device):
     reqs = [rng.integers(0, 2, (int(rng.integers(1, 3)), 48, 19, 19), dtype=np.uint8) for _ in range(40)]
     ref = [eng.evaluate(r).float().cpu().numpy() for r in reqs]
     out = [None] * len(reqs)
-    with BatchingEvaluator(engine_eval_fn(eng), max_batch=64, max_wait_ms=5) as b:
+    go = threading.Barrier(8)
+    with BatchingEvaluator(engine_eval_fn(eng), max_batch=64, max_wait_ms=20) as b:
         def worker(k):
+            go.wait()  # all clients submit together: the first rounds must batch
             for i in range(k, len(reqs), 8):
                 out[i] = b.evaluate(reqs[i])
         ts = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
