@@ -23,6 +23,31 @@
 
 namespace agk {
 
+// e4m3 pack of four ReLU outputs (already scaled and clamped to 448): round to nearest even, or with
+// sr (training forward, ConvFp8Args::sr_seed) stochastic rounding with per-element random bits from a
+// hash of (output element index, seed) -- unbiased activations for the fp8 training step
+__device__ __forceinline__ uint32_t fp8_sr_bits(uint32_t idx, uint32_t seed) {
+  uint32_t h = idx * 0x9E3779B1u ^ (seed + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ int fp8_pack4(float s0, float s1, float s2, float s3, bool sr, uint32_t idx,
+                                         uint32_t seed) {
+  if (sr) {
+    int pk = __builtin_amdgcn_cvt_sr_fp8_f32(s0, (int)fp8_sr_bits(idx, seed), 0, 0);
+    pk = __builtin_amdgcn_cvt_sr_fp8_f32(s1, (int)fp8_sr_bits(idx + 1, seed), pk, 1);
+    pk = __builtin_amdgcn_cvt_sr_fp8_f32(s2, (int)fp8_sr_bits(idx + 2, seed), pk, 2);
+    return __builtin_amdgcn_cvt_sr_fp8_f32(s3, (int)fp8_sr_bits(idx + 3, seed), pk, 3);
+  }
+  int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
+}
+
+
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 __device__ __forceinline__ int fp8_swz(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 2); }
@@ -181,9 +206,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_kernel(ConvFp8Args a) {
       if constexpr (OUT_FP8) {
         const float s0 = fminf(v[0] * osc, 448.f), s1 = fminf(v[1] * osc, 448.f);
         const float s2 = fminf(v[2] * osc, 448.f), s3 = fminf(v[3] * osc, 448.f);
-        int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
-        pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
-        *(int*)(a.y_fp8 + ooff + n) = pk;
+        const bool sr = a.sr_seed != nullptr;  // uniform
+        *(int*)(a.y_fp8 + ooff + n) = fp8_pack4(s0, s1, s2, s3, sr, (uint32_t)(ooff + n), sr ? (uint32_t)*a.sr_seed : 0u);
       }
     }
   }
@@ -425,6 +449,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   // --- epilogue: bias + ReLU, amax, bf16 and/or e4m3 stores (lane: 4 channels of one pixel per block)
   const int nbase = n0 + ((lane >> 4) << 2);
   const float osc = a.out_scale[0];
+  const bool sr = a.sr_seed != nullptr;  // uniform
+  const uint32_t seed = sr ? (uint32_t)*a.sr_seed : 0u;
   float vmax = 0.f;
   // ReLU' bitmask in conv_fwd_kernel's layout: channel block i belongs to its wave half
   // wn = i / (NB/2), bit 4*(i % (NB/2)) + r of word blockIdx.y*8 + wn*4 + lane/16
@@ -498,9 +524,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
         } else {
           const float s0 = fminf(v[0] * osc, 448.f), s1 = fminf(v[1] * osc, 448.f);
           const float s2 = fminf(v[2] * osc, 448.f), s3 = fminf(v[3] * osc, 448.f);
-          int pk = __builtin_amdgcn_cvt_pk_fp8_f32(s0, s1, 0, false);
-          pk = __builtin_amdgcn_cvt_pk_fp8_f32(s2, s3, pk, true);
-          *(int*)(a.y_fp8 + ooff + n) = pk;
+          *(int*)(a.y_fp8 + ooff + n) = fp8_pack4(s0, s1, s2, s3, sr, (uint32_t)(ooff + n), seed);
         }
       }
     }

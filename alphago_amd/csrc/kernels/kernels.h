@@ -186,6 +186,9 @@ struct ConvFp8Args {
   int dgrad_bf16;
   const float* in_scale;
   const uint32_t* mbits_in;
+  // forward, optional: stochastic rounding of the e4m3 output (v_cvt_sr_fp8_f32), random bits hashed
+  // from (pixel, channel, *sr_seed); the trainer advances the device seed every step
+  const int* sr_seed;
 };
 
 // Kernel choices are explicit launch arguments (ConvFwdArgs::tile,

@@ -350,9 +350,10 @@ void featurize(const Tensor& board, const Tensor& ages, const Tensor& meta, cons
 void conv_fwd_fp8(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales, const Tensor& out_scale,
                   const c10::optional<Tensor>& amax, const c10::optional<Tensor>& y_bf16,
                   const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S, int64_t Pin, int64_t Po,
-                  const c10::optional<Tensor>& mbits) {
-  check_dev("conv_fwd_fp8", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, mbits);
-  conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, 0, c10::nullopt, mbits);
+                  const c10::optional<Tensor>& mbits, const c10::optional<Tensor>& sr_seed) {
+  check_dev("conv_fwd_fp8", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, mbits, sr_seed);
+  conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, 0, c10::nullopt, mbits,
+                    sr_seed);
 }
 
 // fp8 dgrad: dx = conv(dz (e5m2, scales[0]), flipped/transposed e4m3 weights (scales[1])) masked
@@ -712,7 +713,8 @@ TORCH_LIBRARY(alphago_amd, m) {
       "Tensor(b!)? nhwc, Tensor(c!)? sensible, Tensor(d!)? legal, Tensor(e!)? overflow, int S, int P) -> ()");
   m.def(
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
-      "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, Tensor(d!)? mbits=None) -> ()");
+      "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, Tensor(d!)? mbits=None, "
+      "Tensor? sr_seed=None) -> ()");
   m.def("pack_weights_fp8(Tensor w, Tensor(a!) out, float scale, Tensor? scale_dev, bool transposed=False) -> ()");
   m.def("pack_weights_fp8_multi(Tensor[] ws, Tensor(a!)[] outs, Tensor scales, int[] layer, int[] transposed) -> ()");
   m.def("absmax_bf16(Tensor x, Tensor(a!) amax, Tensor scale_any) -> ()");

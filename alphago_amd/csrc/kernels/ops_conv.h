@@ -249,8 +249,9 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
                               const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K,
                               int64_t S, int64_t Pin, int64_t Po, int variant,
                               const c10::optional<Tensor>& dgrad_mask = c10::nullopt,
-                              const c10::optional<Tensor>& mbits = c10::nullopt) {
-  check_dev("conv_fwd_fp8_impl", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, dgrad_mask, mbits);
+                              const c10::optional<Tensor>& mbits = c10::nullopt,
+                              const c10::optional<Tensor>& sr_seed = c10::nullopt) {
+  check_dev("conv_fwd_fp8_impl", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, dgrad_mask, mbits, sr_seed);
   // dgrad_mask given: fp8 dgrad (x = e5m2 gradients, w = transposed e4m3 weights, output masked
   // by dgrad_mask > 0, no bias, e5m2 y_fp8)
   CHECK_DEV(x); CHECK_DEV(w); CHECK_CONTIG(x); CHECK_CONTIG(w);
@@ -292,6 +293,11 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
     TORCH_CHECK(variant == 0, "dgrad: production kernel only");
     a.dgrad = 1;
     a.mask = bfp(*dgrad_mask);
+  }
+  if (sr_seed.has_value()) {
+    TORCH_CHECK(!dgrad_mask.has_value() && variant == 0 && sr_seed->scalar_type() == at::kInt &&
+                    sr_seed->numel() >= 1, "sr_seed: int32 device scalar, production forward only");
+    a.sr_seed = sr_seed->data_ptr<int>();
   }
   if (mbits.has_value()) {
     TORCH_CHECK(!dgrad_mask.has_value() && variant == 0, "mbits: production forward only");

@@ -545,10 +545,11 @@ def quantize_fp8(x_bf16: torch.Tensor, out: torch.Tensor, exponent: int):
 
 
 def conv_fwd_fp8(x8, w8, bias, scales, out_scale, K: int, S: int, Pin: int, Po: int = 1, y_bf16=None, y_fp8=None,
-                 amax=None, mbits=None):
+                 amax=None, mbits=None, sr_seed=None):
     """fp8 conv + bias + ReLU.  scales: int32 device tensor {127 - e_x, 127 - e_w} (MFMA E8M0);
-    out_scale: f32 device tensor [2^e_y] for the e4m3 output; amax: int32[64] running max slots (float bits)."""
-    _ops().conv_fwd_fp8(x8, w8, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, mbits)
+    out_scale: f32 device tensor [2^e_y] for the e4m3 output; amax: int32[64] running max slots (float bits);
+    sr_seed: int32 device scalar -> the e4m3 output is stochastically rounded (training forward)."""
+    _ops().conv_fwd_fp8(x8, w8, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, mbits, sr_seed)
 
 
 def fp8_to_float(t_u8: torch.Tensor, exponent: int = 0) -> torch.Tensor:

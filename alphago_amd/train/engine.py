@@ -276,6 +276,11 @@ class HipConvTrainer:
             self.xscale8 = torch.full((L, 1), 127, dtype=torch.int32, device=dev)
             self.osc8 = torch.ones(L, device=dev)
             self.amax8 = ops.fp8_amax_buffer(L, dev)
+            # ALPHAGO_AMD_FP8_SR=1: the training forward rounds its e4m3 activations stochastically
+            # (v_cvt_sr_fp8_f32; a device seed advanced every step); evaluation keeps round-to-nearest
+            self.fp8_sr = os.environ.get("ALPHAGO_AMD_FP8_SR", "0") == "1"
+            self._sr_seed = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._train_fwd = False
             self.X08 = torch.zeros(self.X0.shape, dtype=torch.uint8, device=dev)
             self.Y8 = [torch.zeros(self.Y[0].shape, dtype=torch.uint8, device=dev) for _ in range(2)]
             self._fp8_calibrated = False
@@ -421,13 +426,16 @@ class HipConvTrainer:
         # activations (wgrad reads the e4m3 copies, dgrad the ReLU' bits), so only e4m3 is written
         # (the first, calibrating backward runs bf16 wgrads on these activations)
         e4m3_only = self.fp8_wgrad and self.fp8_dgrad and self._g8_calibrated
+        sr = self._sr_seed if (self.fp8_sr and self._train_fwd) else None
         for l in range(self.L):
             last = l == self.L - 1
             y8 = None if last else (self.X8[l + 1] if self.fp8_wgrad else self.Y8[l % 2])
             ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l], self.S,
                              pin, 1, y_bf16=None if (e4m3_only and not last) else self.Y[l], y_fp8=y8,
-                             amax=self.amax8[l], mbits=None if last else self.MBITS[l])
+                             amax=self.amax8[l], mbits=None if last else self.MBITS[l], sr_seed=sr)
             x8, pin = y8, 1
+        if sr is not None:
+            self._sr_seed.add_(1)
         if self.fp8_wgrad:
             self.xscale8.copy_(self.scales8[:, 0:1])
         ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)  # next step's activation scales
@@ -581,7 +589,11 @@ class HipConvTrainer:
         if B != self.batch:
             raise ValueError("batch %d != configured %d" % (B, self.batch))
         with trace_range("forward"):
-            self._forward_for_head(planes, targets, sym)
+            self._train_fwd = True
+            try:
+                self._forward_for_head(planes, targets, sym)
+            finally:
+                self._train_fwd = False
         with trace_range("head"):
             self._head_train(targets, 1.0 / (B * self.env.world_size), weight)
         with trace_range("backward+allreduce"):

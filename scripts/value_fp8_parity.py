@@ -12,6 +12,7 @@ Arms (same data, same student initialisation, same batch order and symmetries):
   hip-bf16    the HIP trainer, bf16 convs
   hip-fp8     the HIP trainer, fp8 conv path (e4m3 forward, e5m2 x e4m3 dgrad / wgrad: the default)
   hip-fp8fwd  the HIP trainer, e4m3 forward and bf16 backward (where the fp8 loss comes from)
+  hip-fp8sr   hip-fp8 with stochastic rounding of the forward's e4m3 activations (ALPHAGO_AMD_FP8_SR)
 After the first epoch the script also compares one batch's gradients of the fp8 and the fp32 trainer
 at the bf16 arm's weights (per-layer cosine), on the 12-layer trunk.
 
@@ -41,6 +42,10 @@ def make_trainer(arm, net, B, lr, dev):
         return TorchValueTrainer(net, B, lr=lr, device=dev)
     if arm == "hip-fp8fwd":  # e4m3 forward, bf16 backward
         return HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8", fp8_dgrad=False, fp8_wgrad=False)
+    if arm == "hip-fp8sr":  # all-fp8 step with stochastically rounded e4m3 activations in the forward
+        tr = HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8")
+        tr.fp8_sr = True
+        return tr
     return HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8" if arm == "hip-fp8" else "bf16")
 
 

@@ -309,3 +309,41 @@ def test_fp8_backward_12_layer_trunk_matches_bf16_backward(cuda_device):
     print("per-layer (cosine, norm ratio):", res)
     for l, (cos, ratio) in enumerate(res):
         assert cos >= 0.95 and 0.8 < ratio < 1.25, (l, cos, ratio)
+
+
+def test_fp8_forward_stochastic_rounding(cuda_device):
+    """sr_seed: the e4m3 output is stochastically rounded -- every element is one of the two e4m3
+    neighbours of the exact scaled value, the choice changes with the seed, and the rounding is
+    unbiased (mean error far below round-to-nearest's worst case)."""
+    import torch.nn.functional as F
+
+    from alphago_amd import ops
+    torch.manual_seed(9)
+    B, C, S = 8, 192, 19
+    x = F.relu(torch.randn(B, C, S, S, device=cuda_device))
+    w = torch.randn(C, C, 3, 3, device=cuda_device) * 0.05
+    b = torch.randn(C, device=cuda_device) * 0.1
+    xp = ops.to_padded(x, 1)
+    ex = ops.fp8_exponent(float(x.abs().max()), margin=0)
+    x8 = torch.empty(xp.shape, dtype=torch.uint8, device=cuda_device)
+    ops.quantize_fp8(xp, x8, ex)
+    w8, ew = ops.pack_weights_fp8(w, C, C)
+    scales = torch.tensor([127 - ex, 127 - ew], dtype=torch.int32, device=cuda_device)
+    yb = ops.padded_empty(B, S, 1, C, cuda_device)
+    ops.conv_fwd_fp8(x8, w8, b, scales, torch.ones(1, device=cuda_device), 3, S, 1, 1, y_bf16=yb)
+    ref = ops.from_padded(yb, 1).float()  # the exact (bf16-rounded) pre-quantisation output
+    ey = ops.fp8_exponent(float(ref.max()), margin=0)
+    osc = torch.tensor([2.0 ** ey], device=cuda_device)
+    outs = []
+    for seed in (0, 0, 1):
+        y8 = torch.zeros((B, S + 2, S + 2, C), dtype=torch.uint8, device=cuda_device)
+        ops.conv_fwd_fp8(x8, w8, b, scales, osc, 3, S, 1, 1, y_fp8=y8,
+                         sr_seed=torch.tensor([seed], dtype=torch.int32, device=cuda_device))
+        outs.append(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1].permute(0, 3, 1, 2))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])  # deterministic for a seed
+    nz = ref > 2.0 ** (-ey - 6)  # e4m3 normal range
+    err = (outs[0] - ref)[nz]
+    assert (err.abs() <= 0.126 * ref[nz] + 1e-6).all()  # one of the two neighbours
+    assert (outs[0] != outs[2])[nz].float().mean().item() > 0.05  # the seed changes the rounding
+    assert abs(err.mean().item()) < 0.01 * ref[nz].mean().item()  # unbiased
