@@ -785,8 +785,19 @@ __global__ __launch_bounds__(1024) void fp8_weight_scales_kernel(Fp8WeightScales
   const int l = blockIdx.x;
   const float* w = a.w[l];
   const int n = a.n[l];
+  // eight independent loads in flight per thread (a one-load loop was latency-bound: 39.6 us per
+  // value-net repack, profiles/r4/raw/timeline_value_fp8_b1024.txt)
   float m = 0.f;
-  for (int i = threadIdx.x; i < n; i += 1024) m = fmaxf(m, fabsf(w[i]));
+  for (int i0 = threadIdx.x; i0 < n; i0 += 8 * 1024) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + k * 1024;
+      v[k] = i < n ? fabsf(w[i]) : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m = fmaxf(m, v[k]);
+  }
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
