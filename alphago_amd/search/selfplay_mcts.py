@@ -203,11 +203,19 @@ class SelfPlayWriter(object):
         self.games = self.positions = 0
         self.winners = {go.BLACK: 0, go.WHITE: 0, 0: 0}
         self.lengths: List[int] = []
+        # how the games ended: two passes (then scored), resignation, or the move cap
+        self.endings = {"two_passes": 0, "resignation": 0, "move_cap": 0}
         if sgf_dir:
             os.makedirs(sgf_dir, exist_ok=True)
 
     def add(self, r: GameRecord) -> None:
         n = len(r.pi)
+        if r.resigned:
+            self.endings["resignation"] += 1
+        elif len(r.moves) >= 2 and r.moves[-1] == -1 and r.moves[-2] == -1:
+            self.endings["two_passes"] += 1
+        else:
+            self.endings["move_cap"] += 1
         keep = np.arange(n)
         if self.ppg > 0 and n > self.ppg:
             keep = np.sort(self.rng.choice(n, self.ppg, replace=False))
@@ -433,7 +441,8 @@ def selfplay_cli(argv=None):
     local = {"rank": env.rank, "games": writer.games, "positions": n, "seconds": round(dt, 2),
              "leaf_evals": evals, "winners": {"B": writer.winners.get(go.BLACK, 0), "W": writer.winners.get(go.WHITE, 0),
                                                "draw": writer.winners.get(0, 0)},
-             "mean_length": round(float(np.mean(writer.lengths)), 1) if writer.lengths else 0.0}
+             "mean_length": round(float(np.mean(writer.lengths)), 1) if writer.lengths else 0.0,
+             "endings": dict(writer.endings)}
     every = agdist.all_gather_object(local)
     if env.world_size > 1:
         agdist.barrier()
@@ -446,7 +455,8 @@ def selfplay_cli(argv=None):
         agdist.barrier()
     summary = {"games": sum(e["games"] for e in every), "positions": sum(e["positions"] for e in every),
                "leaf_evals": sum(e["leaf_evals"] for e in every), "seconds": max(e["seconds"] for e in every),
-               "ranks": every, "phases_rank0": phase_table(stats)}
+               "ranks": every, "phases_rank0": phase_table(stats),
+               "endings": {k: sum(e["endings"][k] for e in every) for k in every[0]["endings"]}}
     summary["leaf_evals_per_s"] = round(summary["leaf_evals"] / max(summary["seconds"], 1e-9), 1)
     if env.is_main:
         with open(os.path.join(a.out_directory, "selfplay_summary.json"), "w") as f:

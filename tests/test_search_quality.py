@@ -248,3 +248,4 @@ def test_selfplay_cli_two_ranks_merge(tmp_path):
     import json
     summ = json.load(open(os.path.join(out, "selfplay_summary.json")))
     assert summ["games"] == 6 and summ["leaf_evals"] > 0 and summ["phases_rank0"]
+    assert sum(summ["endings"].values()) == 6  # every game counted under one way of ending
