@@ -218,6 +218,17 @@ void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
 void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st);
 void launch_head_backward(const PolicyHeadArgs& a, const float* dlogits, hipStream_t st);
 void launch_value_out(const ValueOutArgs& a, hipStream_t st);
+
+// fused move sampling (sample.hip): out[b] = a draw from probs[b]**beta, -1 where has[b] == 0
+struct SampleArgs {
+  const float* probs;    // [B][NP]
+  const uint8_t* has;    // [B] any sensible move
+  int64_t* out;          // [B]
+  int B, NP;
+  float beta;
+  uint64_t seed;
+};
+void launch_sample_moves(const SampleArgs& a, hipStream_t st);
 void launch_head_grad_sums(const float* dhead, int B, int N, const float* loss, const float* correct, float* grad,
                            float* sums, hipStream_t st);
 void launch_pack_input(const PackInputArgs& a, hipStream_t st);

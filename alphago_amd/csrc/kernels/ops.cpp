@@ -31,6 +31,25 @@ void conv_fwd_pk(const Tensor& x, const Tensor& w, const Tensor& bias, const Ten
                 c10::nullopt, c10::nullopt, (int)((cin_real + 7) / 8));
 }
 
+// one draw per board from probs ** beta (probs: (B, NP) f32, has: (B,) bool / uint8, out: (B,) int64)
+void sample_moves(const Tensor& probs, const Tensor& has, const Tensor& out, double beta, int64_t seed) {
+  check_dev("sample_moves", probs, has, out);
+  CHECK_F32(probs); CHECK_CONTIG(probs); CHECK_CONTIG(has); CHECK_CONTIG(out);
+  TORCH_CHECK(probs.dim() == 2 && probs.size(1) <= 512, "probs (B, NP <= 512)");
+  TORCH_CHECK((has.scalar_type() == at::kBool || has.scalar_type() == at::kByte) && has.numel() == probs.size(0),
+              "has: (B,) bool or uint8");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == probs.size(0), "out: (B,) int64");
+  agk::SampleArgs a{};
+  a.probs = probs.data_ptr<float>();
+  a.has = reinterpret_cast<const uint8_t*>(has.data_ptr());
+  a.out = out.data_ptr<int64_t>();
+  a.B = (int)probs.size(0); a.NP = (int)probs.size(1);
+  a.beta = (float)beta;
+  a.seed = (uint64_t)seed;
+  agk::launch_sample_moves(a, cur_stream());
+  launch_check("sample_moves");
+}
+
 // Small batches: the 32-pixel tile with the K loop split over nsplit workgroups per tile (tile 38) into
 // ws (>= nsplit * M * Cout fp32), then one finishing pass (bias + ReLU + bitmask, or the bitmask dgrad)
 void conv_fwd_splitk(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bias, const Tensor& y, int64_t K,
@@ -682,6 +701,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "conv_fwd_splitk(Tensor x, Tensor w, Tensor? bias, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
       "Tensor(b!)? mbits, Tensor(c!) ws, int nsplit) -> ()");
+  m.def("sample_moves(Tensor probs, Tensor has, Tensor(a!) out, float beta, int seed) -> ()");
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0, int variant=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def("conv_dgrad_bits_bf8(Tensor dz, Tensor wd, Tensor(a!) dx, Tensor mbits, Tensor(b!) dx8, Tensor scale, "
@@ -749,6 +769,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("sgd_pack", &sgd_pack);
   m.impl("conv_fwd_pk", &conv_fwd_pk);
   m.impl("conv_fwd_splitk", &conv_fwd_splitk);
+  m.impl("sample_moves", &sample_moves);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);
   m.impl("conv_dgrad_bits_bf8", &conv_dgrad_bits_bf8);

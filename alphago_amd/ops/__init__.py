@@ -158,6 +158,14 @@ def conv_fwd_splitk(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int, mod
     return y
 
 
+def sample_moves(probs: torch.Tensor, has: torch.Tensor, beta: float, seed: int) -> torch.Tensor:
+    """(B,) int64 device moves: one draw per board from probs ** beta (a counter-based hash of
+    (seed, board) supplies the uniform), -1 where ``has`` is false (sample.hip)."""
+    out = torch.empty(probs.shape[0], dtype=torch.int64, device=probs.device)
+    _ops().sample_moves(probs.contiguous(), has.contiguous(), out, float(beta), int(seed) & ((1 << 63) - 1))
+    return out
+
+
 def pk_shape_ok(cin_real: int, cin_p: int) -> bool:
     """Whether the packed-tap forward (conv_fwd_pk) can run a first layer: 32 < cin_real < 64 real input
     channels in a 64-channel padded input (48 policy / 49 value planes)."""

@@ -31,6 +31,10 @@ class BatchedSampler(object):
         self.gen = torch.Generator(device=policy.device)
         self._bad: List[int] = []
         self.gen.manual_seed(seed)
+        # HIP engines: one fused sampling kernel per call (ops.sample_moves), its uniforms from a
+        # counter-based hash of (seed, call, board)
+        self._fused = None  # resolved at the first sample (the engine is built lazily)
+        self._calls = int(seed) * 1000003
 
     def featurize(self, states) -> np.ndarray:
         return _engine().featurize_batch(list(states), self._names, self.threads)
@@ -63,8 +67,14 @@ class BatchedSampler(object):
     def sample_device(self, probs: torch.Tensor, has: torch.Tensor) -> torch.Tensor:
         """Flat move per board on the probs' device: argmax, or a sample of p**(1/T) (ai.py:37-49);
         -1 (pass) where no sensible move exists.  No host synchronisation."""
+        if self._fused is None:
+            self._fused = bool(getattr(self.policy.engine, "supports_encoded", False)) and probs.is_cuda
         if self.greedy:
             idx = probs.argmax(1)
+        elif self._fused and probs.dtype == torch.float32 and probs.shape[1] <= 512:
+            from .. import ops
+            self._calls += 1
+            return ops.sample_moves(probs, has, self.beta, self._calls)
         else:
             p = probs.clamp_min(0) ** self.beta if self.beta != 1.0 else probs.clamp_min(0)
             p = torch.where(has.unsqueeze(1), p, torch.ones_like(p))

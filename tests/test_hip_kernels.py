@@ -698,3 +698,30 @@ def test_conv_fwd_packed_taps_first_layer(ops, cuda_device, S, B, Cin, Cout, Cou
     assert _rel_err(ops.from_padded(y, 1), ops.from_padded(y2, 1)) < 1e-2
     diff = (mb1 != mb2).float().mean().item()
     assert diff < 1e-3, diff  # bits differ only where a pre-activation rounds across zero
+
+
+@pytest.mark.parametrize("beta", [1.0, 2.0])
+def test_sample_moves_distribution(ops, cuda_device, beta):
+    """Fused sampler: draws follow probs ** beta (normalised), rows without a sensible move give -1,
+    one-hot rows give their index, and a seed reproduces its draws."""
+    torch.manual_seed(3)
+    B, NP = 8192, 361
+    base = torch.zeros(NP, device=cuda_device)
+    base[[3, 50, 77, 200, 360]] = torch.tensor([0.1, 0.2, 0.3, 0.15, 0.25], device=cuda_device)
+    probs = base.repeat(B, 1).contiguous()
+    probs[0] = 0.0
+    probs[0, 123] = 1.0
+    has = torch.ones(B, dtype=torch.bool, device=cuda_device)
+    has[1] = False
+    out = ops.sample_moves(probs, has, beta, 11)
+    again = ops.sample_moves(probs, has, beta, 11)
+    other = ops.sample_moves(probs, has, beta, 12)
+    torch.cuda.synchronize()
+    assert torch.equal(out, again) and not torch.equal(out, other)
+    assert out[0].item() == 123 and out[1].item() == -1
+    rest = out[2:]
+    assert set(rest.unique().tolist()) <= {3, 50, 77, 200, 360}
+    w = base[[3, 50, 77, 200, 360]] ** beta
+    expect = (w / w.sum()).cpu()
+    got = torch.stack([(rest == i).float().mean() for i in (3, 50, 77, 200, 360)]).cpu()
+    assert (got - expect).abs().max().item() < 0.02, (got, expect)
