@@ -6,6 +6,8 @@ Commands
   train-sl       supervised policy training          (reference supervised_policy_trainer CLI)
   train-rl       RL policy training by self-play     (reference reinforcement_policy_trainer CLI)
   value-generate self-play positions for the value net
+  selfplay-mcts  batched MCTS self-play games (SGF + states / pi / outcomes HDF5)
+  selfplay-to-sl MCTS self-play records -> SL training data (most-visited or played move targets)
   train-value    value-network regression
   gtp            run a GTP v2 engine on stdin/stdout (reference interface/gtp_wrapper)
   match          play games between two players (policy / mcts / random / external GTP)
@@ -141,6 +143,9 @@ def _dispatch(argv: List[str]):
     if cmd == "selfplay-mcts":
         from .search.selfplay_mcts import selfplay_cli
         return selfplay_cli(rest)
+    if cmd == "selfplay-to-sl":
+        from .data.selfplay_to_sl import selfplay_to_sl_cli
+        return selfplay_to_sl_cli(rest)
     if cmd == "train-value":
         from .train.value import train_cli
         return train_cli(rest)

@@ -249,3 +249,43 @@ def test_selfplay_cli_two_ranks_merge(tmp_path):
     summ = json.load(open(os.path.join(out, "selfplay_summary.json")))
     assert summ["games"] == 6 and summ["leaf_evals"] > 0 and summ["phases_rank0"]
     assert sum(summ["endings"].values()) == 6  # every game counted under one way of ending
+
+
+def test_selfplay_records_feed_sl_and_value_training(tmp_path):
+    """The MCTS self-play file is consumed: selfplay-to-sl turns its visit distributions (pi) into the
+    SL schema (48 policy planes + (x, y) actions of the most-visited move) that train-sl reads, and
+    train-value reads its states + outcomes directly."""
+    import json
+
+    from alphago_amd.data.dataset import PositionDataset  # the SL / value trainers' reader
+    from alphago_amd.data.selfplay_to_sl import selfplay_to_sl
+    from alphago_amd.io.h5lite import H5File
+    from alphago_amd.search.selfplay_mcts import selfplay_cli
+
+    import os
+
+    pol = os.path.join(str(tmp_path), "p.json")
+    val = os.path.join(str(tmp_path), "v.json")
+    from alphago_amd.cli import main as cli_main
+    assert cli_main(["init-model", "policy", pol, "--filters", "8", "--layers", "2", "--board", "7"]) == 0
+    assert cli_main(["init-model", "value", val, "--filters", "8", "--layers", "2", "--board", "7"]) == 0
+    out = os.path.join(str(tmp_path), "run")
+    selfplay_cli([pol, out, "--value-json", val, "--games", "3", "--concurrent", "3", "--playouts", "8",
+                  "--max-moves", "30", "--rollout-limit", "20", "--lmbda", "0.5"])
+    sp = os.path.join(out, "selfplay.h5")
+    with H5File(sp) as f:
+        n = f["states"].shape[0]
+        pi = np.asarray(f["pi"].read())
+    dst = os.path.join(str(tmp_path), "sl.h5")
+    res = selfplay_to_sl(sp, dst, "pi")
+    assert res["positions"] == n and res["written"] + res["dropped_pass"] == n
+    with H5File(dst) as f:
+        st, acts = f["states"], np.asarray(f["actions"].read())
+        assert st.shape[1:] == (48, 7, 7) and len(acts) == res["written"]
+        keep = np.flatnonzero(pi.argmax(1) < 49)
+        assert np.array_equal(acts[:, 0].astype(int) * 7 + acts[:, 1], pi.argmax(1)[keep])
+    sl = PositionDataset(dst, targets="actions")
+    assert sl.planes == 48 and np.array_equal(sl.targets_np, pi.argmax(1)[keep].astype(np.int32))
+    vd = PositionDataset(sp, targets="outcomes")
+    assert vd.planes == 49 and vd.n == n and set(np.unique(vd.targets_np)) <= {-1.0, 0.0, 1.0}
+    del json
