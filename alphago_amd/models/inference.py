@@ -53,6 +53,10 @@ class HipTrunkInference:
         self.P0 = self.K[0] // 2
         self.buckets = sorted(buckets)
         self.use_graphs = use_graphs
+        # fp8 engines run buckets below this many boards on the bf16 trunk: the fp8 forward's 384-pixel
+        # tiles leave a small batch with a handful of workgroups (~480 us per policy forward at B <= 64 vs
+        # 185-325 us bf16, profiles/r4/README.md); ALPHAGO_AMD_FP8_MIN_BATCH overrides
+        self.fp8_min_batch = int(os.environ.get("ALPHAGO_AMD_FP8_MIN_BATCH", "128"))
         dev = self.device
         # packed on the engine's device whatever device the module's parameters are on
         # first layer on the packed-tap forward when it applies (ops.conv_fwd_pk: real input planes only)
@@ -131,7 +135,7 @@ class HipTrunkInference:
         bk.Y = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(2)]
         # small buckets: the split-K 32-pixel conv (ops.conv_fwd_splitk), fp32 partials in bk.ws
         M = B * S * S
-        bk.sk = [1 if (l == 0 and self.pk0) or self.precision != "bf16" else
+        bk.sk = [1 if (l == 0 and self.pk0) or (self.precision == "fp8" and B >= self.fp8_min_batch) else
                  ops.splitk_nsplit(M, self.Fp, self.C0p if l == 0 else self.Fp, self.K[l]) for l in range(self.L)]
         bk.ws = torch.empty(max(bk.sk) * M * self.Fp, device=dev) if max(bk.sk) > 1 else None
         if self.precision == "fp8":
@@ -173,7 +177,7 @@ class HipTrunkInference:
                         overflow=bk.ovf, planes=bk.planes if self.encoded_planes else None)
         else:
             ops.pack_input(bk.planes, bk.X0, self.P0)
-        if self.precision == "fp8" and not getattr(self, "_calibrating", False):
+        if self.precision == "fp8" and not getattr(self, "_calibrating", False) and bk.B >= self.fp8_min_batch:
             return self._trunk_fp8(bk)
         x, pin = bk.X0, self.P0
         for l in range(self.L):
