@@ -55,8 +55,10 @@ class HipTrunkInference:
         self.use_graphs = use_graphs
         # fp8 engines run buckets below this many boards on the bf16 trunk: the fp8 forward's 384-pixel
         # tiles leave a small batch with a handful of workgroups (~480 us per policy forward at B <= 64 vs
-        # 185-325 us bf16, profiles/r4/README.md); ALPHAGO_AMD_FP8_MIN_BATCH overrides
-        self.fp8_min_batch = int(os.environ.get("ALPHAGO_AMD_FP8_MIN_BATCH", "128"))
+        # 185-325 us bf16; even at B = 128, 520 / 451 us vs 515 / 427 bf16 for policy / value; fp8 wins
+        # from B = 256 on, 578 / 488 us vs 817 / 702; profiles/r4/README.md); ALPHAGO_AMD_FP8_MIN_BATCH
+        # overrides
+        self.fp8_min_batch = int(os.environ.get("ALPHAGO_AMD_FP8_MIN_BATCH", "256"))
         dev = self.device
         # packed on the engine's device whatever device the module's parameters are on
         # first layer on the packed-tap forward when it applies (ops.conv_fwd_pk: real input planes only)

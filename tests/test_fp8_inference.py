@@ -22,7 +22,7 @@ def test_fp8_policy_engine_matches_bf16(cuda_device):
         net.head_w.mul_(20.0)
     e16 = HipTrunkInference(net, cuda_device, precision="bf16")
     e8 = HipTrunkInference(net, cuda_device, precision="fp8")
-    e8.fp8_min_batch = 0  # the fp8 trunk at this batch too (by default buckets below 128 run bf16)
+    e8.fp8_min_batch = 0  # the fp8 trunk at this batch too (by default buckets below 256 run bf16)
     x = _planes(64, 48)
     p16 = e16.evaluate(x).float().cpu()
     p8 = e8.evaluate(x).float().cpu()
@@ -352,7 +352,7 @@ def test_fp8_forward_stochastic_rounding(cuda_device):
 
 
 def test_fp8_engine_small_buckets_run_bf16(cuda_device):
-    """fp8 inference engines run buckets below fp8_min_batch (default 128) on the bf16 trunk -- the fp8
+    """fp8 inference engines run buckets below fp8_min_batch (default 256) on the bf16 trunk -- the fp8
     forward's 384-pixel tiles are latency-bound there -- and their results equal the bf16 engine's."""
     from alphago_amd.models.inference import HipTrunkInference
     from alphago_amd.models.nets import PolicyNet
@@ -361,6 +361,6 @@ def test_fp8_engine_small_buckets_run_bf16(cuda_device):
     net = PolicyNet(48, filters_per_layer=192, layers=4).to(cuda_device)
     e16 = HipTrunkInference(net, cuda_device, precision="bf16")
     e8 = HipTrunkInference(net, cuda_device, precision="fp8")
-    assert e8.fp8_min_batch == 128
+    assert e8.fp8_min_batch == 256
     x = _planes(8, 48, seed=4)
     assert torch.equal(e8.evaluate(x).cpu(), e16.evaluate(x).cpu())
