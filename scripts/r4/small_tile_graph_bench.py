@@ -26,7 +26,7 @@ def main():
         xs = [ops.padded_empty(B, S, 1, F, dev) for _ in range(2)]
         xs[0][:, 1:S + 1, 1:S + 1].normal_()
         for tile in (64, 36, 38, 39, 42):
-            ns = max(2, ops.splitk_nsplit(0, F, F, 3)) if tile == 38 else 0
+            ns = 0
             if tile == 38:
                 tiles = (M + 31) // 32 * (F // 192)
                 ns = max(1, min(9, -(-512 // tiles)))
