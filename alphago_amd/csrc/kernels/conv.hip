@@ -113,16 +113,6 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
 
 template <int MODE>
 static void launch_fwd_mode(const ConvFwdArgs& a, hipStream_t st) {
-  // narrow-N small-batch tiles (round 4, inference): a 128-pixel tile over 64 (39) or 96 (42) output
-  // channels, so each workgroup re-reads a third / half of the layer's weights; their ReLU' bitmask
-  // (if any) has (Cout / BN) * 8 words per pixel
-  if (a.tile == 39 || a.tile == 42) {
-    if (a.Cin % 64 != 0 || a.Cout % (a.tile == 39 ? 64 : 96) != 0)
-      throw std::invalid_argument("conv_fwd tiles 39 / 42: Cin % 64 == 0 and Cout % 64 (39) / 96 (42) == 0");
-    if (a.tile == 39) launch_fwd_bm<64, MODE, 128, 4>(a, st);
-    else launch_fwd_bm<96, MODE, 128, 4>(a, st);
-    return;
-  }
   if (a.Cout == 160) launch_fwd_t<160, MODE>(a, st);
   else if (a.Cout % 192 == 0) launch_fwd_t<192, MODE>(a, st);
   else if (a.Cout % 128 == 0) launch_fwd_t<128, MODE>(a, st);

@@ -14,10 +14,9 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   check_dev("conv_fwd", x, w, bias, mask, y, mbits);
   // production tilings only: 0 = automatic, or a fixed 64 / 128 / 256 / 384-pixel tile (385: 384 with the
   // LDS-DMA issue spread through the MFMAs; 386 / 387: 385 / 384 with the chunk-outer K order)
-  TORCH_CHECK(tile == 0 || tile == 36 || tile == 37 || tile == 39 || tile == 42 || tile == 64 || tile == 65 ||
-                  tile == 128 || tile == 130 || tile == 256 || tile == 384 || tile == 385 || tile == 386 || tile == 387,
-              "conv_fwd tile ", tile, " is not a production tiling (0, 36, 37, 39, 42, 64, 65, 128, 130, 256, 384-387); "
-              "kernel-lab "
+  TORCH_CHECK(tile == 0 || tile == 36 || tile == 37 || tile == 64 || tile == 65 || tile == 128 || tile == 130 ||
+                  tile == 256 || tile == 384 || tile == 385 || tile == 386 || tile == 387,
+              "conv_fwd tile ", tile, " is not a production tiling (0, 36, 37, 64, 65, 128, 130, 256, 384-387); kernel-lab "
               "variants are in torch.ops.alphago_amd_lab (alphago_amd.ops.lab())");
   conv_fwd_impl(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, (int)tile);
 }

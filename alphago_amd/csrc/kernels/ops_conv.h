@@ -115,7 +115,6 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
   if (mbits.has_value()) {
     CHECK_DEV(*mbits);
     TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
-    TORCH_CHECK(tile != 39 && tile != 42, "tiles 39 / 42 (inference) write no ReLU' bitmask");
     const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;
     TORCH_CHECK(mbits->numel() >= B * HPo * HPo * words, "mbits too small: need B*HPo*HPo*words");
     TORCH_CHECK(mode == agk::MODE_BIAS_RELU || mode == agk::MODE_MASKBITS, "mbits with modes 0 (write) / 3 (read)");

@@ -1,7 +1,7 @@
 """Per-layer GPU time of the 192 -> 192 3x3 forward at small batches on each small tile, measured as
 HIP-graph replays of 12 back-to-back convs (no host dispatch in the timing, unlike the eager
-small_batch_kbench.py).  Tiles: 64, 36 (32 pixels), 38 (36 + split-K), 39 / 42 (128 pixels x 64 / 96
-output channels).  One JSON line per (B, tile).  Usage: python scripts/r4/small_tile_graph_bench.py [B ...]"""
+small_batch_kbench.py); TILES=a,b,... picks the tiles (0 = the automatic choice; default 64, 36 =
+32 pixels, 38 = 36 + split-K; the narrow-N tiles 39 / 42 measured here were removed, profiles/r4/README.md).  One JSON line per (B, tile).  Usage: python scripts/r4/small_tile_graph_bench.py [B ...]"""
 import json
 import os
 import sys
@@ -25,7 +25,7 @@ def main():
         M = B * S * S
         xs = [ops.padded_empty(B, S, 1, F, dev) for _ in range(2)]
         xs[0][:, 1:S + 1, 1:S + 1].normal_()
-        for tile in (64, 36, 38, 39, 42):
+        for tile in [int(t) for t in os.environ.get("TILES", "64,36,38").split(",")]:
             ns = 0
             if tile == 38:
                 tiles = (M + 31) // 32 * (F // 192)

@@ -21,7 +21,7 @@ def _bf(x):
     return x.to(torch.bfloat16).float()
 
 
-PROD_TILES = (0, 36, 37, 39, 42, 64, 65, 128, 130, 256, 384, 385, 386, 387)
+PROD_TILES = (0, 36, 37, 64, 65, 128, 130, 256, 384, 385, 386, 387)
 
 
 def _conv_fwd(ops, tile, x, w, bias, y, K, S, Pin, Po=1, mode=0, mask=None, mbits=None):
@@ -287,8 +287,8 @@ def test_sgd_update(ops, cuda_device):
     assert torch.allclose(p, ref)
 
 
-@pytest.mark.parametrize("tile", lab_params([36, 37, 39, 42, 64, 65, 128, 130, 256, 2568, -1, 32, 2, 384, 385, 386, 387, 4,
-                                             5, 6, 7, 8, 9, 10, 11], PROD_TILES))
+@pytest.mark.parametrize("tile", lab_params([36, 37, 64, 65, 128, 130, 256, 2568, -1, 32, 2, 384, 385, 386, 387, 4, 5, 6, 7,
+                                             8, 9, 10, 11], PROD_TILES))
 def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     """Every forward tiling (gather 128/256, 128-pixel waves, halo) on a batch
     whose pixel count is not a multiple of any tile."""
@@ -308,8 +308,8 @@ def test_conv_fwd_tile_variants(ops, cuda_device, tile):
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", lab_params([36, 37, 39, 42, 64, 65, 130, 32, 256, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9,
-                                             10, 11], PROD_TILES))
+@pytest.mark.parametrize("tile", lab_params([36, 37, 64, 65, 130, 32, 256, 2, 384, 385, 386, 387, 4, 5, 6, 7, 8, 9, 10, 11],
+                                            PROD_TILES))
 def test_conv_ring_5x5_and_dgrad(ops, cuda_device, tile):
     """Layer-1 geometry (Cin 64, 5x5, input pad 2) and the masked dgrad mode on each tiling."""
     torch.manual_seed(2)
