@@ -52,7 +52,8 @@ static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
   else if (bm == 64) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR>(a, st);
   else if (bm == 65) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR, false, 4>(a, st);
   else if (bm == 130) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR, false, 3>(a, st);
-  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 64 / 65 / 128 / 130 / 256 / 384-387");
+  else if (bm == 38) launch_fwd_splitk<160, MODE, STR>(a, st);  // split-K (small value-net batches)
+  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 38 / 64 / 65 / 128 / 130 / 256 / 384-387");
 }
 
 

@@ -503,7 +503,8 @@ __global__ __launch_bounds__(256) void conv_splitk_finish_kernel(ConvFwdArgs a) 
 }
 
 // tile code 38: the 32-pixel tile (36) with split-K over a.sk_nsplit workgroups per tile, then the finish
-template <int BN, int MODE>
+// (BN = 160, the value width: STR straddled K-steps when Cin % 64 == 32, weight pieces dealt round-robin)
+template <int BN, int MODE, bool STR = false>
 static void launch_fwd_splitk(const ConvFwdArgs& a, hipStream_t st) {
   if constexpr (MODE == MODE_MASK) {
     throw std::invalid_argument("conv_fwd split-K: modes 0 (bias + ReLU), 2 (none) and 3 (bitmask dgrad)");
@@ -513,11 +514,11 @@ static void launch_fwd_splitk(const ConvFwdArgs& a, hipStream_t st) {
     constexpr int BM = 32, MBW = 1;
     constexpr int smem = 2 * (BM * 128 + BN * 128);
     static const hipError_t attr = hipFuncSetAttribute(
-        (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, true, true, false, false, false, false, 2, true>,
+        (const void*)conv_fwd_kernel<BN, MODE, BM, MBW, true, true, false, false, STR, false, 2, true>,
         hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
     dim3 grid((a.M + BM - 1) / BM, a.Cout / BN, a.sk_nsplit);
-    hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, true, true, false, false, false, false, 2, true>), grid,
+    hipLaunchKernelGGL((conv_fwd_kernel<BN, MODE, BM, MBW, true, true, false, false, STR, false, 2, true>), grid,
                        dim3(BM / MBW * 8), smem, st, a);
     const long threads = (long)a.M * (a.Cout / BN) * 8;
     hipLaunchKernelGGL((conv_splitk_finish_kernel<MODE, BN / 32>), dim3((unsigned)((threads + 255) / 256)), dim3(256),

@@ -140,7 +140,7 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
   if (sk_ws.has_value()) {  // split-K (tile 38): fp32 partials [nsplit][M][Cout]
     CHECK_F32(*sk_ws); CHECK_CONTIG(*sk_ws);
     TORCH_CHECK(tile == 38 && sk_nsplit >= 1 && sk_nsplit <= 64, "split-K: tile 38, 1 <= nsplit <= 64");
-    TORCH_CHECK(Cout != 160 && Cin % 64 == 0, "split-K: 64 / 128 / 192-wide tiles");
+    // any width the conv takes (line 88): 64 / 128 / 192-wide tiles, or the 160-wide value tile
     TORCH_CHECK(mode != agk::MODE_MASK && !y_bf8.has_value(), "split-K: modes 0, 2, 3 without an e5m2 copy");
     TORCH_CHECK(sk_ws->numel() >= (int64_t)sk_nsplit * a.M * Cout, "split-K workspace too small: nsplit*M*Cout");
     a.sk_ws = sk_ws->data_ptr<float>();

@@ -143,12 +143,12 @@ SPLITK_TARGET_WGS = int(os.environ.get("ALPHAGO_AMD_SPLITK_WGS", "144"))
 
 def splitk_nsplit(M: int, cout_p: int, cin_p: int, K: int, target_wgs: int = SPLITK_TARGET_WGS) -> int:
     """Split count of the small-batch split-K conv (conv_fwd_splitk): enough 32-pixel workgroups for
-    ``target_wgs``, at least three K-steps (64-channel chunks of a tap) per split; 1 = no split
-    (large M, the 160-wide value tiles, ALPHAGO_AMD_SPLITK=0)."""
-    if M >= SPLITK_MAX_M or cout_p == 160 or cin_p % 64 or os.environ.get("ALPHAGO_AMD_SPLITK", "1") == "0":
+    ``target_wgs``, at least three K-steps (64-channel chunks of a tap; 160-channel inputs run
+    straddled steps) per split; 1 = no split (large M, ALPHAGO_AMD_SPLITK=0)."""
+    if M >= SPLITK_MAX_M or os.environ.get("ALPHAGO_AMD_SPLITK", "1") == "0":
         return 1
     tiles = (M + 31) // 32 * (cout_p // conv_n_tile(cout_p))
-    nk = K * K * (cin_p // 64)
+    nk = -(-K * K * cin_p // 64)
     return max(1, min(nk // 3, -(-target_wgs // tiles), 64))
 
 

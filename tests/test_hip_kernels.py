@@ -622,12 +622,14 @@ def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, monkeypatch, B, tile
 
 @pytest.mark.parametrize("B,S,Cin,Cout,K,ns", [(1, 19, 192, 192, 3, 9), (4, 19, 192, 192, 3, 3), (16, 19, 192, 192, 3, 3),
                                             (3, 19, 64, 192, 5, 8), (5, 13, 128, 128, 3, 4), (7, 9, 64, 64, 3, 2),
-                                            (2, 19, 192, 192, 3, 1)])
+                                            (2, 19, 192, 192, 3, 1), (1, 19, 160, 160, 3, 7), (4, 19, 160, 160, 3, 3),
+                                            (2, 19, 64, 160, 5, 8)])
 def test_conv_fwd_splitk(ops, cuda_device, B, S, Cin, Cout, K, ns):
     """Split-K 32-pixel conv (tile 38: the K loop over ns workgroups per tile, fp32 partials, one
     finishing pass): forward with bias + ReLU + bitmask and the bitmask dgrad vs fp32 conv2d /
-    conv2d_input, and its bitmask equal to the one-pass tile-36 kernel's (up to pre-activations that
-    round across zero)."""
+    conv2d_input, and its bitmask equal to the one-pass tile-36 kernel's (tile 64 at the 160 value
+    width, whose 160 -> 160 layers run straddled K-steps) up to pre-activations that round across
+    zero."""
     torch.manual_seed(21)
     P = K // 2
     x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
@@ -645,7 +647,7 @@ def test_conv_fwd_splitk(ops, cuda_device, B, S, Cin, Cout, K, ns):
     y = ops.padded_empty(B, S, 1, Cout, cuda_device)
     y36 = ops.padded_empty(B, S, 1, Cout, cuda_device)
     ops.conv_fwd_splitk(xp, wf, b, y, K, S, P, 1, ops.MODE_BIAS_RELU, mb, ws, ns)
-    ops.conv_fwd(xp, wf, b, y36, K, S, P, 1, mbits=mb36, tile=36)
+    ops.conv_fwd(xp, wf, b, y36, K, S, P, 1, mbits=mb36, tile=64 if Cout == 160 else 36)
     torch.cuda.synchronize()
     assert _rel_err(ops.from_padded(y, 1), ref) < 1e-2
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0

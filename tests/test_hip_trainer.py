@@ -296,24 +296,31 @@ def test_packed_tap_first_layer_trainer_matches(cuda_device, monkeypatch, kind, 
         assert torch.nn.functional.cosine_similarity(ga, gb, dim=0) > 0.995, name
 
 
-@pytest.mark.parametrize("B", [4, 1])
-def test_splitk_small_batch_trainer_matches(cuda_device, monkeypatch, B):
+@pytest.mark.parametrize("B,kind", [(4, "policy"), (1, "policy"), (2, "value")])
+def test_splitk_small_batch_trainer_matches(cuda_device, monkeypatch, B, kind):
     """Small batches run the forward and the bitmask dgrad on the split-K 32-pixel tile
-    (ops.conv_fwd_splitk); same loss and gradients as ALPHAGO_AMD_SPLITK=0 up to summation order."""
+    (ops.conv_fwd_splitk; the value net's 152 filters on the 160-wide tile with straddled K-steps);
+    same loss and gradients as ALPHAGO_AMD_SPLITK=0 up to summation order."""
     import copy
 
-    from alphago_amd.models.nets import PolicyNet
-    from alphago_amd.train.engine import HipPolicyTrainer
+    from alphago_amd.models.nets import PolicyNet, ValueNet
+    from alphago_amd.train.engine import HipPolicyTrainer, HipValueTrainer
 
     torch.manual_seed(6)
-    net = PolicyNet(48, filters_per_layer=192, layers=4)
+    if kind == "policy":
+        net, C, cls = PolicyNet(48, filters_per_layer=192, layers=4), 48, HipPolicyTrainer
+    else:
+        net, C, cls = ValueNet(49, filters_per_layer=152, layers=4), 49, HipValueTrainer
     trs = []
     for sk in ("1", "0"):
         monkeypatch.setenv("ALPHAGO_AMD_SPLITK", sk)
-        trs.append(HipPolicyTrainer(copy.deepcopy(net), B, lr=0.05, device=cuda_device))
+        trs.append(cls(copy.deepcopy(net), B, lr=0.05, device=cuda_device))
     assert max(trs[0].sk_fwd) > 1 and max(trs[0].sk_dg) > 1 and max(trs[1].sk_fwd + trs[1].sk_dg) == 1
-    planes = torch.randint(0, 2, (B, 48, 19, 19), dtype=torch.uint8, device=cuda_device)
-    tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    if kind == "policy":
+        tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    else:
+        tgt = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
     for t in trs:
         t.compute_grads(planes, tgt)
     torch.cuda.synchronize()
