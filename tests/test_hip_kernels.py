@@ -638,7 +638,7 @@ def test_conv_fwd_splitk(ops, cuda_device, B, S, Cin, Cout, K, ns):
     ref = F.relu(F.conv2d(x, w, b, padding=P))
     wf = ops.packed_weight_like(w, Cin, Cout)
     ops.pack_weights([w.contiguous()], [wf])
-    xp = ops.to_padded(x, P)
+    xp = ops.to_padded(x, P, Cin)
     M = B * S * S
     ws = torch.full((ns * M * Cout,), float("nan"), device=cuda_device)
     words = ops.mbits_words(Cout)
@@ -659,7 +659,7 @@ def test_conv_fwd_splitk(ops, cuda_device, B, S, Cin, Cout, K, ns):
     ops.pack_weights([w.contiguous()], [wf], [wd])
     g = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
     dx = ops.padded_empty(B, S, 1, Cin, cuda_device)
-    ops.conv_fwd_splitk(ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, ops.MODE_MASKBITS, mb36, ws, ns)
+    ops.conv_fwd_splitk(ops.to_padded(g, 1, Cout), wd, None, dx, 3, S, 1, 1, ops.MODE_MASKBITS, mb36, ws, ns)
     torch.cuda.synchronize()
     y36f = ops.from_padded(y36, 1)
     ref_dx = torch.nn.grad.conv2d_input((B, Cin, S, S), w, g, padding=1) * (y36f > 0)
