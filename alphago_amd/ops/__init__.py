@@ -131,13 +131,13 @@ def conv_fwd(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int = 1, mode: 
     return y
 
 
-# split-K forward / dgrad (tile 38) below this many output pixels (B <= 4 at 19 x 19); ALPHAGO_AMD_SPLITK=0
-# turns it off.  SL step (profiles/r4/README.md): B = 1 1.33k -> 1.74k positions/s, B = 4 5.3k -> 5.9k, but
-# B = 8 10.5k -> 10.1k and B = 16 19.5k -> 16.9k (the split conv kernels are no faster there and the
-# finishing passes add ~5 us per layer).  Split count: ~144 workgroups per layer -- graph-timed 192 -> 192
-# 3x3 forwards (scripts/r4/launch_floor.py) are fastest at 9 splits for B = 1 (11.4 us vs 16.8 unsplit),
-# 6 for B = 2 and 3 for B = 4 (14.7 us; 9 splits 16.3): more splits cost more in partials than they hide
-SPLITK_MAX_M = 1500
+# split-K forward / dgrad (tile 38) below this many output pixels (B <= 8 at 19 x 19); ALPHAGO_AMD_SPLITK=0
+# turns it off.  SL step (profiles/r4/README.md): B = 1 1.33k -> 1.74k positions/s, B = 4 5.3k -> 6.27k,
+# B = 8 10.54k -> 11.09k; at B = 16 the count below is 1 (181 tiles already fill ~144 workgroups).
+# Split count: ~144 workgroups per layer -- graph-timed 192 -> 192 3x3 forwards
+# (scripts/r4/launch_floor.py) are fastest at 9 splits for B = 1 (11.4 us vs 16.8 unsplit), 6 for
+# B = 2 and 3 for B = 4 (14.7 us; 9 splits 16.3): more splits cost more in partials than they hide
+SPLITK_MAX_M = int(os.environ.get("ALPHAGO_AMD_SPLITK_MAX_M", "3000"))
 SPLITK_TARGET_WGS = int(os.environ.get("ALPHAGO_AMD_SPLITK_WGS", "144"))
 
 

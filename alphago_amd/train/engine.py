@@ -207,7 +207,7 @@ class HipConvTrainer:
             self.wgrad_var.append(var)
             slab_max = max(slab_max, ns * T * self.Fp * cin_p)
             db_max = max(db_max, ns * self.Fp)
-        # small batches (B <= 45): forward and bitmask dgrad on the split-K 32-pixel tile
+        # small batches (B <= 8, ops.SPLITK_MAX_M): forward and bitmask dgrad on the split-K 32-pixel tile
         # (ops.conv_fwd_splitk: the K loop of a tile over several workgroups, one finishing pass);
         # bf16 path with the automatic tiling only
         self.sk_fwd = [1] * self.L
