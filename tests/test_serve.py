@@ -269,8 +269,10 @@ def test_batcher_on_hip_engine_matches_direct(cuda_device):
         for t in ts:
             t.join()
         assert b.stats()["rounds"] < len(reqs)
+    # direct calls of 1-2 boards run the 8-board bucket on the split-K convs, batched rounds the 32 / 64
+    # buckets unsplit: the fp32 sums run in another order (bf16 activations round differently at ~1e-3)
     for o, r in zip(out, ref):
-        np.testing.assert_allclose(o, r, rtol=0, atol=2e-6)
+        np.testing.assert_allclose(o, r, rtol=5e-3, atol=1e-6)
 
 
 @pytest.mark.gpu
