@@ -455,6 +455,15 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   // ReLU' bitmask in conv_fwd_kernel's layout: channel block i belongs to its wave half
   // wn = i / (NB/2), bit 4*(i % (NB/2)) + r of word blockIdx.y*8 + wn*4 + lane/16
   const int mwords = gridDim.y * 8;
+  // the lane's bias quads, loaded once for all MB pixel blocks and issued back to back: inside the
+  // block loop the compiler sank each load under the pixel-range branch and waited on it there, 30
+  // serialised L2 round trips per wave at MB 3 x NB 10 (ISA of the 160-wide value forward)
+  constexpr bool BIAS = !DG && !MASKBITS;
+  f32x4 bias4[BIAS ? NB : 1];
+  if constexpr (BIAS) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) bias4[i] = *(const f32x4*)(a.bias + nbase + i * 16);
+  }
 #pragma unroll
   for (int j = 0; j < MB; ++j) {
     uint32_t mb[2] = {0u, 0u};
@@ -472,6 +481,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
       mw[0] = a.mbits_in[pw];
       mw[1] = a.mbits_in[pw + 4];
     }
+    bf16x4 mk[DG ? NB : 1];  // DG: the block's ReLU' mask quads, issued together (m is clamped in range)
+    if constexpr (DG) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) mk[i] = *(const bf16x4*)(a.mask + ooff + nbase + i * 16);
+    }
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       const int n = nbase + i * 16;
@@ -481,11 +495,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = ((w >> (4 * (i % (NB / 2)) + r)) & 1u) ? v[r] : 0.f;
       } else if constexpr (DG) {
-        const bf16x4 mk = *(const bf16x4*)(a.mask + ooff + n);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (float)mk[r] > 0.f ? v[r] : 0.f;
+        for (int r = 0; r < 4; ++r) v[r] = (float)mk[i][r] > 0.f ? v[r] : 0.f;
       } else {
-        const f32x4 bb = *(const f32x4*)(a.bias + n);
+        const f32x4 bb = bias4[i];
         v[0] = fmaxf(v[0] + bb[0], 0.f);
         v[1] = fmaxf(v[1] + bb[1], 0.f);
         v[2] = fmaxf(v[2] + bb[2], 0.f);
