@@ -464,22 +464,35 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 #pragma unroll
     for (int i = 0; i < NB; ++i) bias4[i] = *(const f32x4*)(a.bias + nbase + i * 16);
   }
+  // pixel of each block and (MASKBITS) its ReLU' words, all issued before the first use
+  int pixo[MB];
+  bool okj[MB];
+  uint32_t mwj[MASKBITS ? MB : 1][2];
 #pragma unroll
   for (int j = 0; j < MB; ++j) {
-    uint32_t mb[2] = {0u, 0u};
     int m = m0 + wave * 16 * MB + j * 16 + (lane & 15);
-    const bool ok = m < a.M;
-    m = ok ? m : a.M - 1;
+    okj[j] = m < a.M;
+    m = okj[j] ? m : a.M - 1;
     const int b = fdiv(m, a.divSS);
     const int rem = m - b * SS;
     const int ii = fdiv(rem, a.divS);
     const int jj = rem - ii * a.S;
-    const size_t ooff = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po) * a.Cout;
-    uint32_t mw[2] = {0u, 0u};
+    pixo[j] = (b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po;
     if constexpr (MASKBITS) {  // ReLU' bits of the lane's channels (the forward epilogue's layout)
-      const size_t pw = (size_t)(ooff / a.Cout) * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
-      mw[0] = a.mbits_in[pw];
-      mw[1] = a.mbits_in[pw + 4];
+      const size_t pw = (size_t)pixo[j] * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
+      mwj[j][0] = a.mbits_in[pw];
+      mwj[j][1] = a.mbits_in[pw + 4];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MB; ++j) {
+    uint32_t mb[2] = {0u, 0u};
+    const bool ok = okj[j];
+    const size_t ooff = (size_t)pixo[j] * a.Cout;
+    uint32_t mw[2] = {0u, 0u};
+    if constexpr (MASKBITS) {
+      mw[0] = mwj[j][0];
+      mw[1] = mwj[j][1];
     }
     bf16x4 mk[DG ? NB : 1];  // DG: the block's ReLU' mask quads, issued together (m is clamped in range)
     if constexpr (DG) {
@@ -543,7 +556,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     }
     if constexpr (!DG && !DGB && NB % 2 == 0) {
       if (a.mbits_out && ok) {
-        const size_t pw = (size_t)(ooff / a.Cout) * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
+        const size_t pw = (size_t)pixo[j] * mwords + blockIdx.y * 8 + ((lane >> 4) & 3);
         a.mbits_out[pw] = mb[0];
         a.mbits_out[pw + 4] = mb[1];
       }

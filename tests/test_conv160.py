@@ -323,12 +323,13 @@ def test_pack_weights_fp8_multi_matches_single(ops, cuda_device, monkeypatch, cw
         assert torch.equal(at, bt)
 
 
-@pytest.mark.parametrize("B", [3, 7])
-def test_conv_wgrad_fp8_160(ops, cuda_device, B):
+@pytest.mark.parametrize("B,S", [(3, 19), (7, 19), (24, 19), (5, 9)])
+def test_conv_wgrad_fp8_160(ops, cuda_device, B, S):
     """fp8 wgrad (e5m2 dZ x e4m3 X, 128-pixel steps through ds_read_b64_tr_b8) vs fp32
-    conv2d_weight of the dequantised operands; bias gradient from the e5m2 bytes."""
+    conv2d_weight of the dequantised operands; bias gradient from the e5m2 bytes (B = 24: the
+    production 56 splits; S = 9: boards smaller than one 128-pixel step)."""
     torch.manual_seed(11)
-    S, K, C, Cp = 19, 3, 152, 160
+    K, C, Cp = 3, 152, 160
     x = torch.relu(torch.randn(B, C, S, S, device=cuda_device)) * 2.0
     dz = torch.randn(B, C, S, S, device=cuda_device) * 1e-3
     ex = ops.fp8_exponent(float(x.abs().max()), margin=0)
