@@ -170,8 +170,32 @@ class BatchedMCTS(object):
                            self.threads)
         lad = l[:L] if ladder else None
         hp = pe.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot, to_host=True)
-        hv = ve.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot, to_host=True) if ve is not None else None
+        hv = None
+        if ve is not None:
+            side = self._value_stream(L, pe)
+            if side is not None:
+                # small leaf batches leave most CUs idle in each net's forward: the value net runs
+                # beside the policy net on a second stream (both read only the pinned encodings, and
+                # collect() waits on each one's own event)
+                with torch.cuda.stream(side):
+                    hv = ve.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot, to_host=True)
+            else:
+                hv = ve.submit_encoded(b[:L], a[:L], m[:L], lad, slot=slot, to_host=True)
         return hp, hv
+
+    # leaf batches up to this many boards run the value forward on a side stream (ALPHAGO_AMD_MCTS_VALUE_STREAM=0:
+    # never); above it one net's forward fills the GPU and a second stream only interleaves them
+    VALUE_STREAM_MAX = 64
+
+    def _value_stream(self, L: int, pe):
+        if L > self.VALUE_STREAM_MAX or os.environ.get("ALPHAGO_AMD_MCTS_VALUE_STREAM", "1") == "0":
+            return None
+        dev = getattr(pe, "device", None)
+        if dev is None or torch.device(dev).type != "cuda":
+            return None
+        if getattr(self, "_vstream", None) is None:
+            self._vstream = torch.cuda.Stream(device=dev)
+        return self._vstream
 
     def _finish(self, f, handles, pe, ve) -> None:
         """Collect a submitted evaluation and apply it to f."""

@@ -222,6 +222,26 @@ def test_batched_mcts_encoded_path(cuda_device):
 
 
 @pytest.mark.gpu
+def test_mcts_value_side_stream_matches_serial(cuda_device, monkeypatch):
+    """Small leaf batches run the value forward on a side stream beside the policy forward: the
+    search statistics equal the one-stream search's."""
+    from alphago_amd.models.policy import CNNPolicy, CNNValue
+    from alphago_amd.search.mcts import BatchedMCTS
+
+    pol = CNNPolicy(DEFAULT_FEATURES, device=cuda_device, filters_per_layer=32, layers=2)
+    val = CNNValue(VALUE_FEATURES, device=cuda_device, filters_per_layer=32, layers=2)
+    states = random_positions(1, seed=5, max_len=40)
+    dists = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("ALPHAGO_AMD_MCTS_VALUE_STREAM", flag)
+        m = BatchedMCTS(pol, val, n_trees=1)
+        m.search(states, n_playout=96, leaves_per_tree=8)
+        assert (getattr(m, "_vstream", None) is not None) == (flag == "1")
+        dists.append(m.visit_distribution(0, 19))
+    np.testing.assert_array_equal(dists[0], dists[1])
+
+
+@pytest.mark.gpu
 def test_gpu_planes_match_cpu_1000_positions(cuda_device):
     """>= 1,000 random 19x19 positions (every game length 0..330): every plane of
     the GPU featurizer (46 reference planes + ladders from the encoder + colour
