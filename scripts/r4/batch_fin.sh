@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 4 final validation: the full GPU suite, smoke, the driver-shaped bench, genmove latency and the
 # RL / value-generate drivers on the final tree.  Output: gpurun_out/r4_fin/
-O=gpurun_out/r4_fin
+O=gpurun_out/r4_fin${FINTAG:-}
 mkdir -p $O
 export PYTHONPATH=$PWD
 source scripts/r4/lib.sh
