@@ -53,7 +53,8 @@ static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
   else if (bm == 65) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR, false, 4>(a, st);
   else if (bm == 130) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR, false, 3>(a, st);
   else if (bm == 38) launch_fwd_splitk<160, MODE, STR>(a, st);  // split-K (small value-net batches)
-  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 38 / 64 / 65 / 128 / 130 / 256 / 384-387");
+  else if (bm == 36) launch_fwd_bm<160, MODE, 32, 1, true, true, false, false, STR>(a, st);  // 32 pixels, 4 waves
+  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 36 / 38 / 64 / 65 / 128 / 130 / 256 / 384-387");
 }
 
 
@@ -78,6 +79,10 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
   // round 4: below 64 x 256 pixels (B <= 45 at 19 x 19) the 32-pixel tile on 4 waves (tile 36) -- twice
   // the workgroups of the 64 tile; SL step at B = 16: 18.6k -> 19.7k positions/s (profiles/r4/README.md)
   if (BN != 160 && a.tile == 0 && a.M < 64 * 256) bm = 36;
+  // the 160-wide value layers: 32-pixel tile below 8192 pixels (B <= 22); graph-timed per layer at
+  // B = 1 / 16 15.0 / 16.1 us vs 16.4 / 17.0 (tile 64), but 18.9 vs 17.7 at B = 32
+  // (profiles/r4/raw/tiles_160_graph.txt)
+  if (BN == 160 && a.tile == 0 && a.M < 8192) bm = 36;
   if constexpr (BN == 160) {
     if (a.Cin % 64 == 32) launch_fwd_160<MODE, true>(a, bm, st);
     else launch_fwd_160<MODE, false>(a, bm, st);

@@ -15,7 +15,7 @@ from alphago_amd import ops  # noqa: E402
 def main():
     ops.load()
     dev = torch.device("cuda")
-    S, F, L = 19, 192, 12
+    S, F, L = 19, int(os.environ.get("WIDTH", "192")), 12  # WIDTH=160: the value net's padded width
     bs = [int(b) for b in sys.argv[1:]] or [1, 4, 16, 64]
     w = torch.randn(F, F, 3, 3, device=dev) * 0.05
     wf = ops.packed_weight_like(w, F, F)
@@ -28,7 +28,7 @@ def main():
         for tile in [int(t) for t in os.environ.get("TILES", "64,36,38").split(",")]:
             ns = 0
             if tile == 38:
-                tiles = (M + 31) // 32 * (F // 192)
+                tiles = (M + 31) // 32 * (F // ops.conv_n_tile(F))
                 ns = max(1, min(9, -(-512 // tiles)))
                 ws = torch.empty(ns * M * F, device=dev)
 

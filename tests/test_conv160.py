@@ -32,7 +32,7 @@ def test_padding_helpers(ops):
     assert ops.packed_weight_like(torch.zeros(152, 49, 5, 5), 64, 160).shape == (25, 160, 64)
 
 
-@pytest.mark.parametrize("tile", [0, 64, 65, 128, 130, 256, 384, 385, 386, 387])
+@pytest.mark.parametrize("tile", [0, 36, 64, 65, 128, 130, 256, 384, 385, 386, 387])
 @pytest.mark.parametrize("B,Cin,Cin_p,K", [(5, 152, 160, 3), (3, 49, 64, 5), (1, 152, 160, 3)])
 def test_conv_fwd_160(ops, cuda_device, tile, B, Cin, Cin_p, K):
     torch.manual_seed(0)
@@ -56,7 +56,7 @@ def test_conv_fwd_160(ops, cuda_device, tile, B, Cin, Cin_p, K):
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", [0, 64, 65, 130, 128, 384, 385, 386, 387])
+@pytest.mark.parametrize("tile", [0, 36, 64, 65, 130, 128, 384, 385, 386, 387])
 def test_conv_dgrad_160_bitmask(ops, cuda_device, tile):
     """dgrad with transposed 160-wide weights and the ReLU' bitmask written by
     the forward epilogue == conv2d_input * (y > 0)."""
