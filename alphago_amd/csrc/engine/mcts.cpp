@@ -230,8 +230,11 @@ void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* l
   if (L == 0) return;
   const int np = leaf_state(0).np;
   ensure_pool(threads);  // the forest's persistent pool (set_threads) runs the parts
-  // small chunks claimed dynamically: ladder reads make a few boards far costlier than the rest
-  constexpr int kChunk = 4;
+  // small chunks claimed dynamically: ladder reads make a few boards far costlier than the rest.  A
+  // single tree's leaf batch (tens of boards) goes one board per part so that every pool thread gets
+  // work: with 4-board parts a 32-leaf batch kept 8 of 16 threads busy, and on positions with long
+  // edge ladders the encode was 0.6 ms of each 1 ms search round (scripts/r4/genmove_diag.py)
+  const int kChunk = L <= 256 ? 1 : 4;
   auto work = [&](int c) {
     for (int i = c * kChunk; i < std::min(L, (c + 1) * kChunk); ++i)
       encode_state(leaf_state(i), board + (size_t)i * np, ages + (size_t)i * np, meta + 2 * i,
