@@ -310,7 +310,7 @@ def wgrad_plan(cout_p: int, cin_p: int, K: int, cin_real: int = 0, variant: int 
     return int(t), int(w), int(c)
 
 
-WGRAD_MIN_STAGES = 8
+WGRAD_MIN_STAGES = int(os.environ.get("ALPHAGO_AMD_WGRAD_MIN_STAGES", "8"))
 
 
 def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, target_wgs: int = 0,
