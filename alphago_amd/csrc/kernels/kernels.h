@@ -222,7 +222,8 @@ void launch_value_out(const ValueOutArgs& a, hipStream_t st);
 // fused move sampling (sample.hip): out[b] = a draw from probs[b]**beta, -1 where has[b] == 0
 struct SampleArgs {
   const float* probs;    // [B][NP]
-  const uint8_t* has;    // [B] any sensible move
+  const uint8_t* has;    // [B] any sensible move, or null: then
+  const uint8_t* legal;  // [B][NP] sensible-move mask, "has" = any nonzero entry of the row
   int64_t* out;          // [B]
   int B, NP;
   float beta;

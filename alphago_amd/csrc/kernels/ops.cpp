@@ -36,12 +36,16 @@ void sample_moves(const Tensor& probs, const Tensor& has, const Tensor& out, dou
   check_dev("sample_moves", probs, has, out);
   CHECK_F32(probs); CHECK_CONTIG(probs); CHECK_CONTIG(has); CHECK_CONTIG(out);
   TORCH_CHECK(probs.dim() == 2 && probs.size(1) <= 512, "probs (B, NP <= 512)");
-  TORCH_CHECK((has.scalar_type() == at::kBool || has.scalar_type() == at::kByte) && has.numel() == probs.size(0),
-              "has: (B,) bool or uint8");
+  // has: (B,) any-sensible flags, or the (B, NP) uint8 sensible-move mask (the kernel takes the row's any)
+  const bool mask2d = has.dim() == 2;
+  TORCH_CHECK((has.scalar_type() == at::kBool || has.scalar_type() == at::kByte) &&
+                  (mask2d ? (has.size(0) == probs.size(0) && has.size(1) == probs.size(1)) : has.numel() == probs.size(0)),
+              "has: (B,) bool / uint8, or the (B, NP) uint8 mask");
   TORCH_CHECK(out.scalar_type() == at::kLong && out.numel() == probs.size(0), "out: (B,) int64");
   agk::SampleArgs a{};
   a.probs = probs.data_ptr<float>();
-  a.has = reinterpret_cast<const uint8_t*>(has.data_ptr());
+  a.has = mask2d ? nullptr : reinterpret_cast<const uint8_t*>(has.data_ptr());
+  a.legal = mask2d ? reinterpret_cast<const uint8_t*>(has.data_ptr()) : nullptr;
   a.out = out.data_ptr<int64_t>();
   a.B = (int)probs.size(0); a.NP = (int)probs.size(1);
   a.beta = (float)beta;

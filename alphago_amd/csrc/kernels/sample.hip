@@ -51,7 +51,11 @@ __global__ __launch_bounds__(256) void sample_moves_kernel(SampleArgs a) {
     total += wsum[k];
   }
   const float hi = before + incl, lo = hi - s;  // this thread's cumulative range [lo, hi)
-  const bool has = a.has[b] != 0;
+  // any sensible move: the caller's flag, or (legal mask) any nonzero entry of the row -- every
+  // thread reaches this barrier
+  const bool has = a.has ? a.has[b] != 0
+                         : __syncthreads_or((i0 < a.NP && a.legal[(size_t)b * a.NP + i0]) ||
+                                            (i1 < a.NP && a.legal[(size_t)b * a.NP + i1])) != 0;
   // u in [0, total): 24 random bits from (seed, board)
   const float u = (float)(mix64(a.seed * 0x100000001B3ull + (uint64_t)b) >> 40) * (1.f / 16777216.f) * total;
   // the thread whose range holds u picks; rounding at the top end falls back to the last positive entry

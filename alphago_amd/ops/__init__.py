@@ -160,10 +160,13 @@ def conv_fwd_splitk(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int, mod
     return y
 
 
-def sample_moves(probs: torch.Tensor, has: torch.Tensor, beta: float, seed: int) -> torch.Tensor:
+def sample_moves(probs: torch.Tensor, has: torch.Tensor, beta: float, seed: int,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """(B,) int64 device moves: one draw per board from probs ** beta (a counter-based hash of
-    (seed, board) supplies the uniform), -1 where ``has`` is false (sample.hip)."""
-    out = torch.empty(probs.shape[0], dtype=torch.int64, device=probs.device)
+    (seed, board) supplies the uniform), -1 where ``has`` is false (sample.hip).  ``has``: (B,) flags,
+    or the (B, NP) uint8 sensible-move mask (the kernel reduces each row)."""
+    if out is None:
+        out = torch.empty(probs.shape[0], dtype=torch.int64, device=probs.device)
     _ops().sample_moves(probs.contiguous(), has.contiguous(), out, float(beta), int(seed) & ((1 << 63) - 1))
     return out
 

@@ -35,6 +35,11 @@ class _HostBufs(object):
         self.ladder = torch.empty((n, np_), dtype=torch.uint8, pin_memory=True) if ladder else None
         self.moves = torch.empty(n, dtype=torch.int64, pin_memory=True)
         self.ovf = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        # numpy views for the native encoder and the completion event, made once (per-ply
+        # conversions and event objects were a visible part of the host time per submission)
+        self.np_views = (self.board.numpy(), self.ages.numpy(), self.meta.numpy(),
+                         self.ladder.numpy() if ladder else None)
+        self.ev = torch.cuda.Event() if torch.cuda.is_available() else None
 
 
 def lockstep_ok(*samplers) -> bool:
@@ -73,20 +78,20 @@ class LockstepPlayer(object):
         k = len(idx)
         lad = eng.needs_ladder
         b = self._buf((id(eng), set_id), self.games.n, lad)
-        self.games.encode(idx, b.board.numpy(), b.ages.numpy(), b.meta.numpy(), b.ladder.numpy() if lad else None)
+        nb, na, nm, nl = b.np_views
+        self.games.encode(idx, nb, na, nm, nl if lad else None)
         if want_planes:
             eng.set_encoded_planes(True)
         handle = eng.submit_encoded(b.board[:k], b.ages[:k], b.meta[:k], b.ladder[:k] if lad else None, slot=set_id)
         bk = handle[0]
         probs, legal = eng.outputs(handle)
-        has = (legal != 0).any(1)
-        mv = sampler.sample_device(probs, has)
+        mv = sampler.sample_device_mask(probs, legal)
         f = _Inflight()
         f.idx, f.sampler, f.bufs, f.k = idx, sampler, b, k
         f.rows = eng.encoded_planes_view(k) if want_planes else None
         b.moves[:k].copy_(mv, non_blocking=True)
         b.ovf[:k].copy_(bk.ovf[:k], non_blocking=True)
-        f.ev = torch.cuda.Event()
+        f.ev = b.ev if b.ev is not None else torch.cuda.Event()
         f.ev.record()
         return f
 

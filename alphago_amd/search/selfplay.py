@@ -82,6 +82,18 @@ class BatchedSampler(object):
             idx = torch.multinomial(p, 1, generator=self.gen).squeeze(1)
         return torch.where(has, idx, torch.full_like(idx, -1))
 
+    def sample_device_mask(self, probs: torch.Tensor, legal: torch.Tensor) -> torch.Tensor:
+        """sample_device from the (n, S*S) sensible-move mask: on the fused kernel the mask goes in as
+        it is (each workgroup reduces its row), saving the two tensor kernels of ``legal.any(1)``."""
+        if self._fused is None:
+            self._fused = bool(getattr(self.policy.engine, "supports_encoded", False)) and probs.is_cuda
+        if (not self.greedy and self._fused and probs.dtype == torch.float32 and probs.shape[1] <= 512
+                and legal.dtype == torch.uint8 and legal.shape == probs.shape):
+            from .. import ops
+            self._calls += 1
+            return ops.sample_moves(probs, legal, self.beta, self._calls)
+        return self.sample_device(probs, (legal != 0).any(1))
+
     def device_planes_ok(self) -> bool:
         """The engine featurises on the device and can hand its uint8 planes back (HIP engines)."""
         eng = self.policy.engine

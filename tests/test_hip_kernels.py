@@ -727,3 +727,10 @@ def test_sample_moves_distribution(ops, cuda_device, beta):
     expect = (w / w.sum()).cpu()
     got = torch.stack([(rest == i).float().mean() for i in (3, 50, 77, 200, 360)]).cpu()
     assert (got - expect).abs().max().item() < 0.02, (got, expect)
+    # mask mode: the (B, NP) sensible-move mask instead of the flags -- same draws (row 1 all-zero)
+    legal = (probs > 0).to(torch.uint8)
+    legal[1] = 0
+    legal[5, 0] = 1  # a sensible entry with zero probability does not change the draw
+    via_mask = ops.sample_moves(probs, legal, beta, 11)
+    torch.cuda.synchronize()
+    assert torch.equal(via_mask, out)
