@@ -62,7 +62,7 @@ Forest::Forest(int n_trees, double c_puct, double lmbda, int rollout_limit, int 
 }
 
 void Forest::set_root(int t, const GameState& s) {
-  if (!pending_.empty()) throw std::runtime_error("set_root with pending evaluations");
+  if (!pending_.empty() || !held_.empty()) throw std::runtime_error("set_root with pending evaluations");
   auto& tr = trees_.at(t);
   tr.root_state = s;
   tr.nodes.clear();
@@ -434,7 +434,7 @@ int Forest::best_move(int t, double temperature) {
 }
 
 void Forest::advance(int t, int move) {
-  if (!pending_.empty()) throw std::runtime_error("advance with pending evaluations");
+  if (!pending_.empty() || !held_.empty()) throw std::runtime_error("advance with pending evaluations");
   SearchTree& tr = trees_.at(t);
   int found = -1;
   const Node& r = tr.nodes[0];

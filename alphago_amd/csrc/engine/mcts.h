@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <memory>
 #include <random>
+#include <stdexcept>
 #include <vector>
 
 #include "go.h"
@@ -103,6 +104,24 @@ class Forest {
   // Descend all (or the listed) trees; returns number of leaves queued for evaluation.
   int gather(int leaves_per_tree, const std::vector<int>* which = nullptr);
   int n_pending() const { return (int)pending_.size(); }
+  // Two batches of one forest in flight (single-tree search, round 4): hold() parks the pending batch
+  // -- its leaves keep their virtual losses and queued status, its leaf states keep their slot bank --
+  // so gather() can queue the next batch while the parked one is evaluated; swap_held() exchanges the
+  // pending and the parked batch (apply() backs up whichever is pending).
+  void hold() {
+    if (!held_.empty()) throw std::runtime_error("hold: a batch is already held");
+    held_.swap(pending_);
+    held_slot_.swap(leaf_slot_);
+    held_slots_.swap(slots_);
+    pending_.clear();
+    leaf_slot_.clear();
+  }
+  void swap_held() {
+    held_.swap(pending_);
+    held_slot_.swap(leaf_slot_);
+    held_slots_.swap(slots_);
+  }
+  int n_held() const { return (int)held_.size(); }
   const GameState& leaf_state(int i) const { return slots_[leaf_slot_[i]]; }
   int feature_planes() const { return nplanes_; }
   // uint8 features (L, F, n, n) and sensible-move masks (L, n*n); threaded.
@@ -148,6 +167,9 @@ class Forest {
 
   std::vector<SearchTree> trees_;
   std::vector<Leaf> pending_;
+  std::vector<Leaf> held_;                // hold() / swap_held(): the parked batch,
+  std::vector<int> held_slot_;            // its slot ids
+  std::vector<GameState> held_slots_;     // and its slot bank
   // Leaf states live in a persistent slot pool (a GameState is ~20 KB of
   // inline arrays): each gather copies the root into a reused slot and plays
   // the path there, so a leaf costs one copy and no allocation.

@@ -80,6 +80,9 @@ void bind_mcts(py::module_& m) {
             return L;
           },
           py::arg("ptr"), py::arg("capacity"), py::arg("threads") = 8)
+      .def("hold", &Forest::hold)
+      .def("swap_held", &Forest::swap_held)
+      .def_property_readonly("n_held", &Forest::n_held)
       .def(
           "leaf_encode_into",
           [](const Forest& f, uintptr_t board, uintptr_t ages, uintptr_t meta, uintptr_t ladder, size_t capacity,

@@ -305,8 +305,17 @@ class BatchedMCTS(object):
                     return True
                 # only terminal/collided paths this round: they still count as sims
 
+        def gather_once(k):
+            """One gather attempt (no retry): False when the trees are done or every path ended on a
+            queued leaf (a held batch's) or a terminal."""
+            f = self._forests[k]
+            todo = [j for j in range(f.n_trees) if f.sims(j) < targets[k][j]]
+            return bool(todo) and f.gather(leaves_per_tree, todo) > 0
+
         enc = self._encoded_engines()
-        if len(self._forests) == 1 or enc is None:
+        if len(self._forests) == 1 and enc is not None and self._pipeline_single():
+            self._search_pipelined(self._forests[0], gather, gather_once, enc)
+        elif len(self._forests) == 1 or enc is None:
             for k, f in enumerate(self._forests):
                 while gather(k):
                     self._evaluate_pending(f, k)
@@ -339,6 +348,33 @@ class BatchedMCTS(object):
                     self._finish(self._forests[k], inflight[k], pe, ve)
         temps = list(temperature) if isinstance(temperature, (list, tuple, np.ndarray)) else [temperature] * self._n
         return [fg.best_move(i, float(temps[i])) if i in on else None for i in range(self._n)]
+
+    @staticmethod
+    def _pipeline_single() -> bool:
+        return os.environ.get("ALPHAGO_AMD_MCTS_PIPELINE", "1") != "0"
+
+    def _search_pipelined(self, f, gather, gather_once, enc) -> None:
+        """One forest (e.g. the single tree of a GTP genmove), two batches in flight: while batch A is
+        evaluated on the device, the next batch B is gathered (A's leaves keep their virtual losses and
+        count as collisions) and encoded and launched; then A is backed up.  The host work of each
+        round overlaps the previous round's forwards instead of following them."""
+        pe, ve = enc
+        if not gather(0):
+            return
+        slot = 0
+        cur = self._submit(f, slot, pe, ve)
+        while cur is not None:
+            f.hold()  # A parked with its virtual losses; pending is empty
+            nxt = None
+            if gather_once(0):
+                nxt = self._submit(f, slot ^ 1, pe, ve)
+            f.swap_held()  # pending = A, held = B (or nothing)
+            self._finish(f, cur, pe, ve)  # backs up A
+            f.swap_held()  # pending = B
+            if nxt is None and gather(0):  # every path met A's queued leaves (a young tree): after A
+                nxt = self._submit(f, slot ^ 1, pe, ve)
+            cur = nxt
+            slot ^= 1
 
     def root_value(self, tree: int) -> float:
         """Search value of the root for the player to move there: the visit-weighted mean child Q

@@ -242,6 +242,33 @@ def test_mcts_value_side_stream_matches_serial(cuda_device, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("leaves", [8, 32])
+def test_mcts_single_tree_two_batches_in_flight(cuda_device, monkeypatch, leaves):
+    """The single-tree search keeps two leaf batches in flight (Forest.hold / swap_held): it spends
+    the playout budget (at most one batch over), leaves nothing pending or held, picks a legal move,
+    and on a position with one winning capture finds it like the one-batch search."""
+    from alphago_amd.models.policy import CNNPolicy, CNNValue
+    from alphago_amd.search.mcts import BatchedMCTS
+
+    pol = CNNPolicy(DEFAULT_FEATURES, device=cuda_device, filters_per_layer=32, layers=2)
+    val = CNNValue(VALUE_FEATURES, device=cuda_device, filters_per_layer=32, layers=2)
+    states = random_positions(3, seed=7, max_len=80)
+    for st in states:
+        for flag in ("1", "0"):
+            monkeypatch.setenv("ALPHAGO_AMD_MCTS_PIPELINE", flag)
+            m = BatchedMCTS(pol, val, n_trees=1)
+            mv = m.search([st], n_playout=200, leaves_per_tree=leaves)[0]
+            f = m._forests[0]
+            assert f.n_pending == 0 and f.n_held == 0
+            visits = sum(m.forest.root_stats(0)[1])
+            assert 200 <= visits <= 200 + 2 * leaves + 1, (flag, visits)
+            assert mv is None or st.is_legal(mv)
+            # a second search on the same tree (subtree reuse path) also drains
+            m.search([st], n_playout=64, leaves_per_tree=leaves)
+            assert f.n_pending == 0 and f.n_held == 0
+
+
+@pytest.mark.gpu
 def test_gpu_planes_match_cpu_1000_positions(cuda_device):
     """>= 1,000 random 19x19 positions (every game length 0..330): every plane of
     the GPU featurizer (46 reference planes + ladders from the encoder + colour
