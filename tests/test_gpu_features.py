@@ -245,8 +245,8 @@ def test_mcts_value_side_stream_matches_serial(cuda_device, monkeypatch):
 @pytest.mark.parametrize("leaves", [8, 32])
 def test_mcts_single_tree_two_batches_in_flight(cuda_device, monkeypatch, leaves):
     """The single-tree search keeps two leaf batches in flight (Forest.hold / swap_held): it spends
-    the playout budget (at most one batch over), leaves nothing pending or held, picks a legal move,
-    and on a position with one winning capture finds it like the one-batch search."""
+    the playout budget (at most a batch or two over), leaves nothing pending or held, picks a legal
+    move, and drains again on a second search of the reused tree -- with and without the pipeline."""
     from alphago_amd.models.policy import CNNPolicy, CNNValue
     from alphago_amd.search.mcts import BatchedMCTS
 
