@@ -261,7 +261,7 @@ def test_mcts_single_tree_two_batches_in_flight(cuda_device, monkeypatch, leaves
             f = m._forests[0]
             assert f.n_pending == 0 and f.n_held == 0
             visits = sum(m.forest.root_stats(0)[1])
-            assert 200 <= visits <= 200 + 2 * leaves + 1, (flag, visits)
+            assert 199 <= visits <= 200 + 2 * leaves + 1, (flag, visits)  # the root expansion is a sim, not a child visit
             assert mv is None or st.is_legal(mv)
             # a second search on the same tree (subtree reuse path) also drains
             m.search([st], n_playout=64, leaves_per_tree=leaves)
