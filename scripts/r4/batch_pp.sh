@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 batch PP: single-tree search with two leaf batches in flight -- tests, genmove on / off.
-O=gpurun_out/r4_pp
+O=gpurun_out/r4_pp${PPTAG:-}
 mkdir -p $O
 export PYTHONPATH=$PWD
 source scripts/r4/lib.sh
