@@ -17,7 +17,9 @@ The gradient all-reduce of a bucket overlaps the remaining backward.  dgrad
 and wgrad of a layer are independent; ``overlap=True`` runs the wgrad on a
 second HIP stream, but on MI355X the two big-LDS kernels then split the CUs
 and the step is slower (alternating A/B, scripts/overlap_ab.sh: SL 118.7k vs
-120.3k, value 131.2k vs 136.8k positions/s), so the default is serial.  Every
+120.3k, value 131.2k vs 136.8k positions/s), so large batches run serial.  Up to
+B = 256 (``overlap=None``, the default) the kernels leave CUs idle and the overlap wins
+(SL B = 16 19.6k -> 22.3k positions/s, round 4).  Every
 activation and gradient has its own buffer (HBM is plentiful: ~2 GB at
 batch 512), so there are no cross-stream reuse hazards.
 
@@ -117,11 +119,15 @@ class KerasSGDSchedule:
         self.iterations += 1
 
 
+# automatic wgrad / dgrad stream overlap up to this many pixels per step (B = 256 at 19 x 19)
+OVERLAP_AUTO_MAX_PIXELS = 256 * 361
+
+
 class HipConvTrainer:
     """MFMA conv-trunk training engine; subclasses provide the head."""
 
     def __init__(self, net, batch: int, lr: float = 0.003, decay: float = 0.0, device=None, bucket_mb: float = 4.0,
-                 overlap: bool = False, wgrad_target_wgs: int = 0, iterations: int = 0, precision: str = "bf16",
+                 overlap: Optional[bool] = None, wgrad_target_wgs: int = 0, iterations: int = 0, precision: str = "bf16",
                  wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: Optional[bool] = None,
                  reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None,
                  fp8_wgrad: Optional[bool] = None):
@@ -143,6 +149,13 @@ class HipConvTrainer:
         self.net = net.to(self.device)
         self.batch = batch
         self.sched = KerasSGDSchedule(lr, decay, iterations)
+        if overlap is None:
+            # automatic: the wgrad on a side stream beside the dgrad at small batches, where both
+            # kernels leave CUs idle -- SL B = 16 19.6k -> 22.3k, B = 256 95.3k -> 99.4k positions/s --
+            # and serial from B = 512 on (108.8k vs 107.0k) and at the bench batch
+            # (profiles/r4/raw/overlap_small_batch_ab.txt); ALPHAGO_AMD_OVERLAP=0 keeps it serial
+            overlap = (precision == "bf16" and batch * net.board * net.board <= OVERLAP_AUTO_MAX_PIXELS
+                       and os.environ.get("ALPHAGO_AMD_OVERLAP", "auto") != "0")
         self.overlap = overlap
         self.comm_events = None  # list: record the all-reduce wait of each backward as (start, end) events
         tr = net.trunk

@@ -71,7 +71,8 @@ def main():
                     help="teacher: random-game positions labelled by a fixed random-init teacher of the same "
                          "architecture (learnable: top1_acc measures learning); random: random planes/labels")
     ap.add_argument("--overlap", action="store_true",
-                    help="run the wgrad on a second stream beside the dgrad (slower on MI355X; default serial)")
+                    help="run the wgrad on a second stream beside the dgrad at any batch (default: automatic, on up to "
+                         "B = 256 where it wins, serial above -- slower at the bench batch)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                     help="conv forward precision (fp8 = e4m3 block-scaled MFMA forward, bf16 backward)")
     ap.add_argument("--graph", action="store_true", help="run each training step as a HIP-graph replay")
@@ -89,7 +90,7 @@ def main():
     dev = env.device
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
-    kw = {} if args.backend == "torch" else {"overlap": args.overlap, "precision": args.precision,
+    kw = {} if args.backend == "torch" else {"overlap": True if args.overlap else None, "precision": args.precision,
                                              "wgrad_target_wgs": args.wgrad_wgs, "conv_tile": args.conv_tile,
                                              "reduce_stream": None if args.reduce_stream is None
                                              else bool(args.reduce_stream)}

@@ -52,7 +52,7 @@ def main():
     dev = env.device
     torch.manual_seed(7 + env.rank)
     net = ValueNet(49, filters_per_layer=a.filters, layers=a.layers)
-    kw = ({"precision": a.precision, "conv_tile": a.conv_tile, "overlap": a.overlap,
+    kw = ({"precision": a.precision, "conv_tile": a.conv_tile, "overlap": True if a.overlap else None,
            "fp8_dgrad": False if a.no_fp8_dgrad else (True if a.fp8_dgrad else None),
            "fp8_wgrad": not a.no_fp8_wgrad} if dev.type == "cuda" else {})
     tr = make_value_trainer(net, a.batch, lr=0.003, decay=8.664e-8, device=dev, **kw)
