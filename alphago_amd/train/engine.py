@@ -17,8 +17,8 @@ The gradient all-reduce of a bucket overlaps the remaining backward.  dgrad
 and wgrad of a layer are independent; ``overlap=True`` runs the wgrad on a
 second HIP stream, but on MI355X the two big-LDS kernels then split the CUs
 and the step is slower (alternating A/B, scripts/overlap_ab.sh: SL 118.7k vs
-120.3k, value 131.2k vs 136.8k positions/s), so large batches run serial.  Up to
-B = 256 (``overlap=None``, the default) the kernels leave CUs idle and the overlap wins
+120.3k, value 131.2k vs 136.8k positions/s), so large batches run serial.  For
+B = 8 .. 256 (``overlap=None``, the default) the kernels leave CUs idle and the overlap wins
 (SL B = 16 19.6k -> 22.3k positions/s, round 4).  Every
 activation and gradient has its own buffer (HBM is plentiful: ~2 GB at
 batch 512), so there are no cross-stream reuse hazards.
@@ -119,8 +119,8 @@ class KerasSGDSchedule:
         self.iterations += 1
 
 
-# automatic wgrad / dgrad stream overlap up to this many pixels per step (B = 256 at 19 x 19)
-OVERLAP_AUTO_MAX_PIXELS = 256 * 361
+# automatic wgrad / dgrad stream overlap between these pixel counts per step (B = 8 .. 256 at 19 x 19)
+OVERLAP_AUTO_MIN_PIXELS, OVERLAP_AUTO_MAX_PIXELS = 8 * 361, 256 * 361
 
 
 class HipConvTrainer:
@@ -154,7 +154,10 @@ class HipConvTrainer:
             # kernels leave CUs idle -- SL B = 16 19.6k -> 22.3k, B = 256 95.3k -> 99.4k positions/s --
             # and serial from B = 512 on (108.8k vs 107.0k) and at the bench batch
             # (profiles/r4/raw/overlap_small_batch_ab.txt); ALPHAGO_AMD_OVERLAP=0 keeps it serial
-            overlap = (precision == "bf16" and batch * net.board * net.board <= OVERLAP_AUTO_MAX_PIXELS
+            # Below B = 8 the steps are ~0.6 ms and the two-stream step measured mixed (B = 1 +8 %,
+            # B = 2 -9 %, B = 4 -13..+2 %; raw/auto_overlap_splitk_batches.txt): serial there
+            px = batch * net.board * net.board
+            overlap = (precision == "bf16" and OVERLAP_AUTO_MIN_PIXELS <= px <= OVERLAP_AUTO_MAX_PIXELS
                        and os.environ.get("ALPHAGO_AMD_OVERLAP", "auto") != "0")
         self.overlap = overlap
         self.comm_events = None  # list: record the all-reduce wait of each backward as (start, end) events

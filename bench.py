@@ -71,8 +71,8 @@ def main():
                     help="teacher: random-game positions labelled by a fixed random-init teacher of the same "
                          "architecture (learnable: top1_acc measures learning); random: random planes/labels")
     ap.add_argument("--overlap", action="store_true",
-                    help="run the wgrad on a second stream beside the dgrad at any batch (default: automatic, on up to "
-                         "B = 256 where it wins, serial above -- slower at the bench batch)")
+                    help="run the wgrad on a second stream beside the dgrad at any batch (default: automatic, on for "
+                         "B = 8 .. 256 where it wins, serial outside -- slower at the bench batch)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                     help="conv forward precision (fp8 = e4m3 block-scaled MFMA forward, bf16 backward)")
     ap.add_argument("--graph", action="store_true", help="run each training step as a HIP-graph replay")
