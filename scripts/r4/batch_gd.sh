@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 batch GD: per-genmove diagnosis (evaluations, overflow fallbacks, host time split).
-O=gpurun_out/r4_gd
+O=gpurun_out/r4_gd${GDTAG:-}
 mkdir -p $O
 export PYTHONPATH=$PWD
 source scripts/r4/lib.sh

@@ -56,7 +56,7 @@ def main():
     for c in ("boardsize 19", "clear_board", "genmove b", "clear_board"):
         eng.send(c)
     color = "b"
-    for _ in range(6):
+    for _ in range(int(os.environ.get("DIAG_MOVES", "6"))):
         for k in st:
             st[k] = 0 if isinstance(st[k], int) else 0.0
         t0 = time.perf_counter()
