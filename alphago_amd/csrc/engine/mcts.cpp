@@ -179,6 +179,20 @@ void Forest::gather_trees(const int* trees, int ntrees, int leaves_per_tree, std
   }
 }
 
+void Forest::discard() {
+  for (const std::vector<Leaf>* batch : {&pending_, &held_}) {
+    for (const Leaf& lf : *batch) {
+      SearchTree& tr = trees_.at(lf.tree);
+      if (tr.nodes[lf.node].status == 1) tr.nodes[lf.node].status = 0;
+      for (int x = lf.node; x >= 0; x = tr.nodes[x].parent) tr.nodes[x].vl -= 1;
+    }
+  }
+  pending_.clear();
+  held_.clear();
+  leaf_slot_.clear();
+  held_slot_.clear();
+}
+
 int Forest::gather(int leaves_per_tree, const std::vector<int>* which) {
   if (!pending_.empty()) throw std::runtime_error("gather called with pending evaluations; call apply first");
   leaf_slot_.clear();

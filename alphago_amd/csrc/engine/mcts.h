@@ -122,6 +122,15 @@ class Forest {
     held_slots_.swap(slots_);
   }
   int n_held() const { return (int)held_.size(); }
+  int n_held_tree(int t) const {
+    int n = 0;
+    for (const Leaf& lf : held_) n += lf.tree == t;
+    return n;
+  }
+  // Unwind an interrupted search: the pending and the held batch lose their virtual losses and
+  // queued status (their leaves become unexpanded again) and both lists are cleared, so set_root /
+  // advance work afterwards.
+  void discard();
   const GameState& leaf_state(int i) const { return slots_[leaf_slot_[i]]; }
   int feature_planes() const { return nplanes_; }
   // uint8 features (L, F, n, n) and sensible-move masks (L, n*n); threaded.

@@ -82,6 +82,8 @@ void bind_mcts(py::module_& m) {
           py::arg("ptr"), py::arg("capacity"), py::arg("threads") = 8)
       .def("hold", &Forest::hold)
       .def("swap_held", &Forest::swap_held)
+      .def("discard", &Forest::discard)
+      .def("n_held_tree", &Forest::n_held_tree)
       .def_property_readonly("n_held", &Forest::n_held)
       .def(
           "leaf_encode_into",

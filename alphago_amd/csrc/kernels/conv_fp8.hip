@@ -887,9 +887,13 @@ void launch_fp8_grad_scales(unsigned* amax, int* gscales8, float* gosc, int L, i
 // input of the fp8 dgrad chain).  16-byte loads (8 bf16), 8-byte stores, one grid round of 4
 // workgroups per CU, and the max folded per workgroup before one atomic (round 3: 8-byte loads and
 // a per-wave atomic over 4096 workgroups took 99 us for the value head's 72 M elements)
+// E4M3 = true: the e4m3 variant (activations: a bf16-precision layer of the mixed-precision fp8 step
+// feeding an fp8 layer, with the delayed activation scale and amax of the fp8 kernels)
+template <bool E4M3>
 __global__ __launch_bounds__(256) void quantize_bf8_dev_kernel(const __bf16* x, uint8_t* y, long n8, const float* scale,
                                                                unsigned* amax) {
   __shared__ float red[4];
+  constexpr float kMax = E4M3 ? 448.f : 57344.f;
   const float sc = *scale;
   float m = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
@@ -899,13 +903,21 @@ __global__ __launch_bounds__(256) void quantize_bf8_dev_kernel(const __bf16* x, 
     for (int r = 0; r < 8; ++r) {
       f[r] = (float)v[r];
       m = fmaxf(m, fabsf(f[r]));
-      f[r] = fminf(fmaxf(f[r] * sc, -57344.f), 57344.f);
+      f[r] = fminf(fmaxf(f[r] * sc, -kMax), kMax);
     }
     if (y) {  // null: max |x| only
-      int lo = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], 0, false);
-      lo = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], lo, true);
-      int hi = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], 0, false);
-      hi = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], hi, true);
+      int lo, hi;
+      if constexpr (E4M3) {
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+      } else {
+        lo = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], 0, false);
+        lo = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], lo, true);
+        hi = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], 0, false);
+        hi = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], hi, true);
+      }
       *(int2*)(y + 8 * i) = make_int2(lo, hi);
     }
   }
@@ -918,13 +930,15 @@ __global__ __launch_bounds__(256) void quantize_bf8_dev_kernel(const __bf16* x, 
   }
 }
 
-void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st) {
+void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st,
+                             bool e4m3) {
   if (n % 8 != 0) throw std::invalid_argument("quantize_bf8: element count must be a multiple of 8");
   const long n8 = n / 8;
   int blocks = (int)((n8 + 255) / 256);
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) return;
-  hipLaunchKernelGGL(quantize_bf8_dev_kernel, dim3(blocks), dim3(256), 0, st, x, y, n8, scale, amax);
+  if (e4m3) hipLaunchKernelGGL(quantize_bf8_dev_kernel<true>, dim3(blocks), dim3(256), 0, st, x, y, n8, scale, amax);
+  else hipLaunchKernelGGL(quantize_bf8_dev_kernel<false>, dim3(blocks), dim3(256), 0, st, x, y, n8, scale, amax);
 }
 
 #ifdef AGK_KERNEL_LAB

@@ -261,7 +261,8 @@ struct Fp8PackArgs {
 void launch_pack_weights_fp8_multi(const Fp8PackArgs& a, hipStream_t st);
 void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st);
 void launch_fp8_grad_scales(unsigned* amax, int* gscales8, float* gosc, int L, int margin, hipStream_t st);
-void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st);
+void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st,
+                             bool e4m3 = false);
 void launch_quantize_fp8(const __bf16* x, uint8_t* y, long n, float scale, hipStream_t st);
 #ifdef AGK_KERNEL_LAB
 void launch_bf8_convert_probe(const __bf16* x, uint8_t* y, long n, float scale, int mode, hipStream_t st);
@@ -287,6 +288,15 @@ struct SgdPackArgs {
   int64_t range_off[kSgdPackMaxRanges];
   int range_len[kSgdPackMaxRanges];
   int nranges;
+  // optimizer (Keras 1.0 SGD / Adam semantics): 0 = SGD (p -= lr g), 1 = SGD with momentum
+  // (v = mom v - lr g; p += v, or p += mom v - lr g with nesterov), 2 = Adam (m1, m2 = first and second
+  // moments; the bias-corrected step lr_t comes from the device schedule or the host).  m1 / m2 are flat
+  // fp32 buffers parallel to p.
+  int opt;
+  float* m1;
+  float* m2;
+  float mom, b1, b2, eps;
+  int nesterov;
 };
 void launch_sgd_pack(const SgdPackArgs& a, hipStream_t st);
 // RCCL all-reduce stand-in (comm_proxy.hip): channels workgroups copy n floats and hold their CUs wire_us

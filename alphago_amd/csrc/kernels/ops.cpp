@@ -467,8 +467,16 @@ void fp8_grad_scales(const Tensor& amax, const Tensor& gscales8, const Tensor& g
   launch_check("fp8_grad_scales");
 }
 
-// e5m2 quantisation with a device scale; amax (int32[64], float bits) accumulates max |x|
+// e5m2 (or, e4m3 = true, e4m3) quantisation with a device scale; amax (int32[64], float bits)
+// accumulates max |x|
+static void quantize_dev(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor& amax, bool e4m3);
 void quantize_bf8(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor& amax) {
+  quantize_dev(x, y, scale, amax, false);
+}
+void quantize_fp8_dev(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor& amax) {
+  quantize_dev(x, y, scale, amax, true);
+}
+static void quantize_dev(const Tensor& x, const Tensor& y, const Tensor& scale, const Tensor& amax, bool e4m3) {
   check_dev("quantize_bf8", x, y, scale, amax);
   CHECK_BF16(x); CHECK_CONTIG(x); CHECK_DEV(x);
   TORCH_CHECK(y.scalar_type() == at::kByte && y.is_contiguous() && y.numel() == x.numel() && x.numel() % 8 == 0 &&
@@ -477,8 +485,8 @@ void quantize_bf8(const Tensor& x, const Tensor& y, const Tensor& scale, const T
   TORCH_CHECK(scale.scalar_type() == at::kFloat && amax.scalar_type() == at::kInt &&
                   amax.numel() >= agk::kFp8AmaxSlots, "scale f32[1], amax int32[64]");
   agk::launch_quantize_bf8_dev(bfp(x), y.data_ptr<uint8_t>(), x.numel(), scale.data_ptr<float>(),
-                               reinterpret_cast<unsigned*>(amax.data_ptr<int>()), cur_stream());
-  launch_check("quantize_bf8");
+                               reinterpret_cast<unsigned*>(amax.data_ptr<int>()), cur_stream(), e4m3);
+  launch_check(e4m3 ? "quantize_fp8_dev" : "quantize_bf8");
 }
 
 void pack_weights_fp8(const Tensor& w, const Tensor& out, double scale, const c10::optional<Tensor>& scale_dev,
@@ -588,10 +596,24 @@ void sgd_update_sched(const Tensor& p, const Tensor& g, const Tensor& sched, dou
 // Fused SGD + bf16 packs (pack.hip sgd_pack_kernel): conv layer i's OIHW weights live at flat offset
 // w_meta[4i] with (Cout_real, Cin_real, K) = w_meta[4i+1 .. 4i+3]; wf[i] / wd[i] (wd empty: none) as
 // pack_weights; plain SGD over (range_off, range_len); lr from ``sched`` (advanced) when given.
+// opt: 0 SGD, 1 SGD + momentum (m1 = velocity), 2 Adam (m1, m2 = moments; an 8-entry sched carries its
+// bias correction); hyper = {momentum, beta_1, beta_2, epsilon, nesterov}.
 void sgd_pack(const Tensor& p, const Tensor& g, double lr, const c10::optional<Tensor>& sched, double gscale,
               at::IntArrayRef w_meta, at::TensorList wf, at::TensorList wd, at::IntArrayRef range_off,
-              at::IntArrayRef range_len) {
+              at::IntArrayRef range_len, int64_t opt, const c10::optional<Tensor>& m1,
+              const c10::optional<Tensor>& m2, at::ArrayRef<double> hyper) {
   check_dev("sgd_pack", p, g, sched, wf, wd);
+  check_dev("sgd_pack", p, m1, m2);
+  TORCH_CHECK(opt >= 0 && opt <= 2, "sgd_pack: opt 0 (SGD), 1 (momentum) or 2 (Adam)");
+  TORCH_CHECK(hyper.size() == 5, "sgd_pack: hyper = {momentum, beta_1, beta_2, epsilon, nesterov}");
+  if (opt >= 1) {
+    TORCH_CHECK(m1.has_value() && m1->scalar_type() == at::kFloat && m1->is_contiguous() &&
+                m1->numel() == p.numel(), "sgd_pack: m1 must be a contiguous fp32 buffer like p");
+  }
+  if (opt == 2) {
+    TORCH_CHECK(m2.has_value() && m2->scalar_type() == at::kFloat && m2->is_contiguous() &&
+                m2->numel() == p.numel(), "sgd_pack: m2 must be a contiguous fp32 buffer like p");
+  }
   CHECK_F32(p); CHECK_F32(g); CHECK_CONTIG(p); CHECK_CONTIG(g);
   TORCH_CHECK(p.numel() == g.numel(), "sgd_pack: p and g sizes differ");
   const int nl = (int)wf.size();
@@ -604,10 +626,20 @@ void sgd_pack(const Tensor& p, const Tensor& g, double lr, const c10::optional<T
   a.lr = (float)lr;
   a.gscale = (float)gscale;
   if (sched.has_value()) {
-    TORCH_CHECK(sched->scalar_type() == at::kDouble && sched->numel() == 4 && sched->is_contiguous(),
-                "sched must be float64[4] {lr0, decay, iterations, lr}");
+    TORCH_CHECK(sched->scalar_type() == at::kDouble && sched->is_contiguous() &&
+                (sched->numel() == 4 || sched->numel() == 8),
+                "sched must be float64[4] {lr0, decay, iterations, lr} or [8] (+ {beta_1, beta_2, opt, 0})");
+    TORCH_CHECK(opt != 2 || sched->numel() == 8, "sgd_pack: Adam needs the 8-entry schedule");
     a.sched = sched->data_ptr<double>();
   }
+  a.opt = (int)opt;
+  a.m1 = opt >= 1 ? m1->data_ptr<float>() : nullptr;
+  a.m2 = opt == 2 ? m2->data_ptr<float>() : nullptr;
+  a.mom = (float)hyper[0];
+  a.b1 = (float)hyper[1];
+  a.b2 = (float)hyper[2];
+  a.eps = (float)hyper[3];
+  a.nesterov = hyper[4] != 0.0;
   a.nlayers = nl;
   for (int i = 0; i < nl; ++i) {
     agk::SgdPackLayer& L = a.layers[i];
@@ -729,7 +761,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("comm_proxy(Tensor src, Tensor(a!) dst, int channels, float wire_us) -> ()");
   m.def("sgd_update_sched(Tensor(a!) p, Tensor g, Tensor(b!) sched, float gscale) -> ()");
   m.def("sgd_pack(Tensor(a!) p, Tensor g, float lr, Tensor(b!)? sched, float gscale, int[] w_meta, Tensor(c!)[] wf, "
-        "Tensor(d!)[] wd, int[] range_off, int[] range_len) -> ()");
+        "Tensor(d!)[] wd, int[] range_off, int[] range_len, int opt, Tensor(e!)? m1, Tensor(f!)? m2, float[] hyper) -> ()");
   m.def("dense_f32(Tensor A, Tensor B, Tensor? bias, Tensor(a!) C, bool transA, bool transB, float beta) -> ()");
   // budget: node visits per capture / escape read; 4096 = lb::kLadderVisits (ladder_bb.h)
   m.def(
@@ -750,6 +782,7 @@ TORCH_LIBRARY(alphago_amd, m) {
         "Tensor(b!) y_bf16, Tensor(c!)? y_fp8, int K, int S) -> ()");
   m.def("fp8_grad_scales(Tensor(a!) amax, Tensor(b!) gscales8, Tensor(c!) gosc, int margin) -> ()");
   m.def("quantize_bf8(Tensor x, Tensor(a!) y, Tensor scale, Tensor(b!) amax) -> ()");
+  m.def("quantize_fp8_dev(Tensor x, Tensor(a!) y, Tensor scale, Tensor(b!) amax) -> ()");
   m.def("fp8_weight_scales(Tensor[] ws, Tensor(a!) wscale, Tensor(b!) scales8) -> ()");
   m.def("fp8_act_scales(Tensor(a!) amax, Tensor(b!) scales8, Tensor(c!) osc, int margin) -> ()");
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
@@ -801,6 +834,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("absmax_bf16", &absmax_bf16);
   m.impl("fp8_grad_scales", &fp8_grad_scales);
   m.impl("quantize_bf8", &quantize_bf8);
+  m.impl("quantize_fp8_dev", &quantize_fp8_dev);
   m.impl("head_grad_sums", &head_grad_sums);
   m.impl("fp8_weight_scales", &fp8_weight_scales);
   m.impl("fp8_act_scales", &fp8_act_scales);

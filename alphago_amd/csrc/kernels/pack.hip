@@ -152,9 +152,15 @@ __global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ g, i
 // captured in a HIP graph: sched = {lr0, decay, iterations, lr_current} (f64).
 // One thread computes lr = lr0 / (1 + decay * iterations) -- the same double
 // expression as KerasSGDSchedule.current() -- and advances the counter.
-__global__ void sgd_sched_kernel(double* sched) {
+// An 8-entry schedule {lr0, decay, iterations, lr, beta_1, beta_2, opt, 0} adds Keras 1.0 Adam's
+// bias correction lr_t = lr sqrt(1 - beta_2^t) / (1 - beta_1^t), t = iterations + 1, when opt == 2.
+__global__ void sgd_sched_kernel(double* sched, int n) {
   if (threadIdx.x == 0) {
-    const double lr = sched[0] / (1.0 + sched[1] * sched[2]);
+    double lr = sched[0] / (1.0 + sched[1] * sched[2]);
+    if (n >= 8 && sched[6] == 2.0) {
+      const double t = sched[2] + 1.0;
+      lr = lr * sqrt(1.0 - pow(sched[5], t)) / (1.0 - pow(sched[4], t));
+    }
     sched[3] = lr;
     sched[2] = sched[2] + 1.0;
   }
@@ -181,7 +187,7 @@ __global__ void sgd_dev_kernel(float* __restrict__ p, const float* __restrict__ 
 }
 
 void launch_sgd_sched(float* p, const float* g, int64_t n, double* sched, float gscale, hipStream_t st) {
-  hipLaunchKernelGGL(sgd_sched_kernel, dim3(1), dim3(64), 0, st, sched);
+  hipLaunchKernelGGL(sgd_sched_kernel, dim3(1), dim3(64), 0, st, sched, 4);
   int64_t blocks = ((n >> 2) + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
@@ -227,9 +233,30 @@ __device__ __forceinline__ size_t wf_index(const SgdPackLayer& L, int t, int n, 
 // contiguous), 18-20 independent loads in flight per thread, and stages the bf16 result in LDS as
 // [t][c][n]; phase 2 writes wf along c and wd along n from LDS.  (The round-4 first cut had each thread
 // walk its (n, c)'s taps serially: strided, one load in flight, 79 us per step.)
-template <int K>
-__device__ __forceinline__ void sgd_pack_layer(const SgdPackLayer& L, float* P, const float* G, float step,
-                                               __bf16* tile) {
+// One parameter's update under the optimizer OPT (SgdPackArgs::opt); i = its flat index.  OPT 0 is the
+// round-4 expression (p - step g, step = lr * gscale), so plain SGD stays bitwise unchanged.
+template <int OPT>
+__device__ __forceinline__ float opt_update(const SgdPackArgs& a, size_t i, float p, float g, float step, float m1v,
+                                            float m2v) {
+  if constexpr (OPT == 0) {
+    return p - step * g;
+  } else if constexpr (OPT == 1) {
+    const float v = a.mom * m1v - step * g;
+    a.m1[i] = v;
+    return a.nesterov ? p + a.mom * v - step * g : p + v;
+  } else {
+    const float ge = g * a.gscale;
+    const float m = a.b1 * m1v + (1.f - a.b1) * ge;
+    const float v = a.b2 * m2v + (1.f - a.b2) * ge * ge;
+    a.m1[i] = m;
+    a.m2[i] = v;
+    return p - step * m / (sqrtf(v) + a.eps);
+  }
+}
+
+template <int K, int OPT>
+__device__ __forceinline__ void sgd_pack_layer(const SgdPackArgs& a, const SgdPackLayer& L, float* P, const float* G,
+                                               float step, __bf16* tile) {
   constexpr int KK = K;
   constexpr int T = KK * KK;
   constexpr int span = 32 * T;  // one n's slice of the tile, in floats
@@ -242,15 +269,19 @@ __device__ __forceinline__ void sgd_pack_layer(const SgdPackLayer& L, float* P, 
   constexpr int B = K == 1 ? 4 : K == 3 ? 18 : 20;  // loads in flight: 2 rounds (3x3), 5 (5x5)
 #pragma unroll 1
   for (int e0 = 0; e0 < 32 * span; e0 += 256 * B) {
-    float pv[B], gv[B];
+    float pv[B], gv[B], m1v[OPT ? B : 1], m2v[OPT == 2 ? B : 1];
 #pragma unroll
     for (int j = 0; j < B; ++j) {
       const int e = e0 + j * 256 + (int)threadIdx.x;
       const int nl = e / span, r = e - nl * span;
       pv[j] = gv[j] = 0.f;
+      if constexpr (OPT != 0) m1v[j] = 0.f;
+      if constexpr (OPT == 2) m2v[j] = 0.f;
       if (e < 32 * span && nl < nw && r < lim) {
         pv[j] = P[base0 + nl * rows + r];
         gv[j] = G[base0 + nl * rows + r];
+        if constexpr (OPT != 0) m1v[j] = a.m1[L.off + base0 + nl * rows + r];
+        if constexpr (OPT == 2) m2v[j] = a.m2[L.off + base0 + nl * rows + r];
       }
     }
 #pragma unroll
@@ -261,7 +292,8 @@ __device__ __forceinline__ void sgd_pack_layer(const SgdPackLayer& L, float* P, 
       const int cl = r / T, t = r - cl * T;
       float v = 0.f;
       if (nl < nw && r < lim) {
-        v = pv[j] - step * gv[j];
+        v = opt_update<OPT>(a, L.off + base0 + nl * rows + r, pv[j], gv[j], step, m1v[OPT ? j : 0],
+                            m2v[OPT == 2 ? j : 0]);
         P[base0 + nl * rows + r] = v;
       }
       tile[(t * 32 + cl) * 33 + nl] = (__bf16)v;
@@ -292,15 +324,25 @@ __device__ __forceinline__ void sgd_pack_layer(const SgdPackLayer& L, float* P, 
   }
 }
 
-__global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
-  __shared__ __bf16 tile[kSgdPackMaxTaps * 32 * 33];  // [t][c][n] (n padded to 33: no bank conflicts)
-  float step = a.lr * a.gscale;
-  if (a.sched) step = (float)a.sched[3] * a.gscale;  // == the sgd_dev_kernel step
+template <int OPT>
+__device__ __forceinline__ void sgd_pack_job(const SgdPackArgs& a, __bf16* tile) {
+  // SGD: step = lr * gscale (the sgd_dev_kernel step); momentum / Adam: step = lr (Adam: lr_t), and
+  // Adam scales the gradient itself (its step is invariant to a gradient scale only up to eps)
+  float step = OPT == 2 ? a.lr : a.lr * a.gscale;
+  if (a.sched) step = OPT == 2 ? (float)a.sched[3] : (float)a.sched[3] * a.gscale;
   if ((int)blockIdx.y == a.nlayers) {  // plain ranges
     for (int r = 0; r < a.nranges; ++r) {
-      float* p = a.p + a.range_off[r];
-      const float* g = a.g + a.range_off[r];
-      for (int i = blockIdx.x * 256 + threadIdx.x; i < a.range_len[r]; i += gridDim.x * 256) p[i] -= step * g[i];
+      const int64_t o = a.range_off[r];
+      float* p = a.p + o;
+      const float* g = a.g + o;
+      for (int i = blockIdx.x * 256 + threadIdx.x; i < a.range_len[r]; i += gridDim.x * 256) {
+        if constexpr (OPT == 0) {
+          p[i] -= step * g[i];
+        } else {
+          const float m2v = OPT == 2 ? a.m2[o + i] : 0.f;
+          p[i] = opt_update<OPT>(a, o + i, p[i], g[i], step, a.m1[o + i], m2v);
+        }
+      }
     }
     return;
   }
@@ -311,15 +353,22 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
   float* P = a.p + L.off;
   const float* G = a.g + L.off;
   switch (L.K) {  // layer-uniform
-    case 1: sgd_pack_layer<1>(L, P, G, step, tile); break;
-    case 3: sgd_pack_layer<3>(L, P, G, step, tile); break;
-    case 5: sgd_pack_layer<5>(L, P, G, step, tile); break;
+    case 1: sgd_pack_layer<1, OPT>(a, L, P, G, step, tile); break;
+    case 3: sgd_pack_layer<3, OPT>(a, L, P, G, step, tile); break;
+    case 5: sgd_pack_layer<5, OPT>(a, L, P, G, step, tile); break;
     default: break;  // rejected on the host (kSgdPackMaxTaps)
   }
 }
 
+__global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
+  __shared__ __bf16 tile[kSgdPackMaxTaps * 32 * 33];  // [t][c][n] (n padded to 33: no bank conflicts)
+  if (a.opt == 1) sgd_pack_job<1>(a, tile);  // launch-uniform
+  else if (a.opt == 2) sgd_pack_job<2>(a, tile);
+  else sgd_pack_job<0>(a, tile);
+}
+
 void launch_sgd_pack(const SgdPackArgs& a, hipStream_t st) {
-  if (a.sched) hipLaunchKernelGGL(sgd_sched_kernel, dim3(1), dim3(64), 0, st, a.sched);
+  if (a.sched) hipLaunchKernelGGL(sgd_sched_kernel, dim3(1), dim3(64), 0, st, a.sched, a.opt == 2 ? 8 : 4);
   int tiles = 1;
   for (int i = 0; i < a.nlayers; ++i) {
     const SgdPackLayer& L = a.layers[i];

@@ -335,11 +335,13 @@ class HipTrunkInference:
         return self.collect(self.submit_encoded(board, ages, meta, ladder, slot))
 
     @torch.no_grad()
-    def evaluate(self, planes, legal=None):
+    def evaluate(self, planes, legal=None, slot: int = 0):
         """planes: (n, C, S, S) uint8 (numpy or tensor); legal: (n, S*S) uint8 or None.
-        Returns the bucket's output tensors (views of the first n rows)."""
+        Returns the bucket's output tensors (views of the first n rows).  ``slot`` selects the
+        bucket buffers as in submit_encoded (a caller with encoded batches in flight uses a slot
+        none of them holds)."""
         n = planes.shape[0]
-        bk = self._get(n, encoded=False)
+        bk = self._get(n, encoded=False, slot=slot)
         src = torch.as_tensor(planes)
         bk.planes[:n].copy_(src, non_blocking=True)
         if n < bk.B:
@@ -403,7 +405,7 @@ class TorchPolicyInference:
         pass
 
     @torch.no_grad()
-    def evaluate(self, planes, legal=None):
+    def evaluate(self, planes, legal=None, slot: int = 0):
         x = torch.as_tensor(planes).to(self.device)
         logits = self.net.logits_torch(x.float())
         if legal is not None:
@@ -423,7 +425,7 @@ class TorchValueInference:
         pass
 
     @torch.no_grad()
-    def evaluate(self, planes, legal=None):
+    def evaluate(self, planes, legal=None, slot: int = 0):
         return self.net.forward_torch(torch.as_tensor(planes).to(self.device).float())
 
 

@@ -35,6 +35,22 @@ def keras_uniform_(t: torch.Tensor, scale: float = KERAS_UNIFORM_SCALE, generato
         return t.uniform_(-scale, scale, generator=generator)
 
 
+def he_uniform_(net: nn.Module, generator=None) -> nn.Module:
+    """Fan-in scaled uniform init (He for the ReLU trunk and the 1x1 head conv, LeCun for the dense
+    layers) of a PolicyNet / ValueNet, biases zero: the reference's ``uniform(-0.05, 0.05)`` shrinks a
+    12-layer trunk's signal ~30x (value.py:17,21), which plain SGD does not recover from."""
+    with torch.no_grad():
+        for w in list(net.trunk.weights) + [net.head_w]:
+            bound = (6.0 / (w.shape[1] * w.shape[2] * w.shape[3])) ** 0.5
+            w.uniform_(-bound, bound, generator=generator)
+        for name in ("fc1_w", "fc2_w"):  # Keras (in, out) layout: fan_in = rows
+            w = getattr(net, name, None)
+            if w is not None:
+                bound = (3.0 / w.shape[0]) ** 0.5
+                w.uniform_(-bound, bound, generator=generator)
+    return net
+
+
 class ConvStack(nn.Module):
     """Shared trunk: conv(k_1) + (L-1) conv(k_i), all ReLU, 'same' padding."""
 

@@ -254,13 +254,21 @@ def sgd_update(p, g, lr: float, gscale: float = 1.0):
     _ops().sgd_update(p, g, lr, gscale)
 
 
-def sgd_pack(p, g, lr: float, w_meta, wf, wd, ranges, sched=None, gscale: float = 1.0):
-    """Fused SGD step + bf16 weight packs in one launch (pack.hip sgd_pack_kernel): conv layer i's weights
-    at flat offset w_meta[i][0] with shape (Cout, Cin, K, K) = w_meta[i][1:]; plain SGD over ``ranges``
-    ((offset, length) pairs: biases, head); ``sched`` (device Keras schedule) replaces ``lr``."""
+OPT_SGD, OPT_MOMENTUM, OPT_ADAM = 0, 1, 2
+
+
+def sgd_pack(p, g, lr: float, w_meta, wf, wd, ranges, sched=None, gscale: float = 1.0, opt: int = OPT_SGD,
+             m1=None, m2=None, momentum: float = 0.0, beta_1: float = 0.9, beta_2: float = 0.999,
+             epsilon: float = 1e-8, nesterov: bool = False):
+    """Fused optimizer step + bf16 weight packs in one launch (pack.hip sgd_pack_kernel): conv layer i's
+    weights at flat offset w_meta[i][0] with shape (Cout, Cin, K, K) = w_meta[i][1:]; the same update over
+    ``ranges`` ((offset, length) pairs: biases, head); ``sched`` (device Keras schedule) replaces ``lr``.
+    ``opt``: OPT_SGD, OPT_MOMENTUM (velocity ``m1``) or OPT_ADAM (moments ``m1``, ``m2``; ``lr`` is then the
+    bias-corrected lr_t, or ``sched`` an 8-entry schedule that computes it) -- Keras 1.0 semantics."""
     meta = [int(v) for m in w_meta for v in m]
     _ops().sgd_pack(p, g, float(lr), sched, float(gscale), meta, list(wf), list(wd), [int(o) for o, _ in ranges],
-                    [int(n) for _, n in ranges])
+                    [int(n) for _, n in ranges], int(opt), m1, m2,
+                    [float(momentum), float(beta_1), float(beta_2), float(epsilon), 1.0 if nesterov else 0.0])
 
 
 def dense_f32(A, B, C, bias=None, trans_a: bool = False, trans_b: bool = False, beta: float = 0.0):
@@ -534,6 +542,13 @@ def fp8_grad_scales(amax, gscales8, gosc, margin: int = 1):
 def quantize_bf8(x_bf16: torch.Tensor, out: torch.Tensor, scale_dev: torch.Tensor, amax: torch.Tensor):
     """e5m2 quantisation (x * scale_dev[0]) with max |x| accumulated into amax (int32[64])."""
     _ops().quantize_bf8(x_bf16, out, scale_dev, amax)
+    return out
+
+
+def quantize_fp8_dev(x_bf16: torch.Tensor, out: torch.Tensor, scale_dev: torch.Tensor, amax: torch.Tensor):
+    """e4m3 quantisation (x * scale_dev[0]) with max |x| accumulated into amax (int32[64]): a bf16 layer's
+    output as the next fp8 layer's input in the mixed-precision fp8 step."""
+    _ops().quantize_fp8_dev(x_bf16, out, scale_dev, amax)
     return out
 
 

@@ -34,6 +34,14 @@ from .._native import engine as _engine
 from ..utils.gorecords import flatten_idx
 
 
+# bucket slot of the overflow fallback (slots 0 / 1 hold the pipelined search's in-flight batches)
+FALLBACK_SLOT = 2
+
+
+def _fallback_eval(engine, planes, masks=None) -> np.ndarray:
+    return engine.evaluate(planes, masks, slot=FALLBACK_SLOT).float().cpu().numpy()
+
+
 class _ForestGroup(object):
     """Several native Forests presented as one (tree t -> (forest, local index))."""
 
@@ -213,10 +221,15 @@ class BatchedMCTS(object):
             states = [f.leaf_state(i) for i in bad]
             planes = self.policy.preprocessor.states_to_uint8(states)
             masks = _engine().featurize_batch(states, ["sensibleness"], self.threads).reshape(len(bad), -1)
-            probs[bad] = pe.evaluate(planes, masks).float().cpu().numpy()
+            # another batch may still be in flight (pipelined search: its value forward on the side
+            # stream): the fallback runs on bucket buffers of its own slot, after the side stream
+            vs = getattr(self, "_vstream", None)
+            if vs is not None:
+                torch.cuda.current_stream(vs.device).wait_stream(vs)
+            probs[bad] = _fallback_eval(pe, planes, masks)
             mask[bad] = masks
             if ve is not None:
-                values[bad] = ve.evaluate(self.value.preprocessor.states_to_uint8(states)).float().cpu().numpy()
+                values[bad] = _fallback_eval(ve, self.value.preprocessor.states_to_uint8(states))
         f.apply(probs, values, mask)
 
     def _evaluate_encoded(self, pe, ve, f=None, slot: int = 0) -> None:
@@ -307,9 +320,10 @@ class BatchedMCTS(object):
 
         def gather_once(k):
             """One gather attempt (no retry): False when the trees are done or every path ended on a
-            queued leaf (a held batch's) or a terminal."""
+            queued leaf (a held batch's) or a terminal.  The held batch's leaves count toward the
+            playout budget, so the pipelined search does the serial search's number of playouts."""
             f = self._forests[k]
-            todo = [j for j in range(f.n_trees) if f.sims(j) < targets[k][j]]
+            todo = [j for j in range(f.n_trees) if f.sims(j) + f.n_held_tree(j) < targets[k][j]]
             return bool(todo) and f.gather(leaves_per_tree, todo) > 0
 
         enc = self._encoded_engines()
@@ -359,6 +373,15 @@ class BatchedMCTS(object):
         count as collisions) and encoded and launched; then A is backed up.  The host work of each
         round overlaps the previous round's forwards instead of following them."""
         pe, ve = enc
+        try:
+            self._pipeline_loop(f, gather, gather_once, pe, ve)
+        except BaseException:
+            # a HIP error or an interrupt (e.g. a GTP session's Ctrl-C) mid-search: drop both
+            # in-flight batches with their virtual losses so the forest stays usable
+            f.discard()
+            raise
+
+    def _pipeline_loop(self, f, gather, gather_once, pe, ve) -> None:
         if not gather(0):
             return
         slot = 0

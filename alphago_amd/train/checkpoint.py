@@ -6,7 +6,8 @@ and data position on resume.  A native checkpoint holds everything needed to
 continue *bit-identically* (in a deterministic configuration):
 
 * the flat fp32 master parameters (``trainer.fp.flat``);
-* the Keras-SGD iteration count (drives ``lr/(1+decay*t)``);
+* the Keras-SGD iteration count (drives ``lr/(1+decay*t)``) and the optimizer state (momentum
+  velocity / Adam moments) when the optimizer keeps one;
 * the data cursor, epoch and step-within-epoch, partial epoch sums;
 * the augmentation RNG state;
 * the run configuration (argparse namespace as a dict) for provenance.
@@ -26,9 +27,14 @@ FORMAT = "alphago_amd.ckpt.v1"
 
 
 def trainer_state(trainer) -> Dict[str, Any]:
-    return {"flat": trainer.fp.flat.detach().to("cpu", copy=True),
-            "names": list(trainer.fp.names),
-            "iterations": int(trainer.sched.iterations)}
+    st = {"flat": trainer.fp.flat.detach().to("cpu", copy=True),
+          "names": list(trainer.fp.names),
+          "iterations": int(trainer.sched.iterations)}
+    opt = getattr(trainer, "opt_state", None)
+    if opt:  # momentum velocity / Adam moments
+        st["optimizer"] = trainer.sched.optimizer
+        st["opt_state"] = [t.detach().to("cpu", copy=True) for t in opt]
+    return st
 
 
 def load_trainer_state(trainer, st: Dict[str, Any]) -> None:
@@ -38,6 +44,13 @@ def load_trainer_state(trainer, st: Dict[str, Any]) -> None:
     with torch.no_grad():
         trainer.fp.flat.copy_(flat.to(trainer.fp.flat.device))
     trainer.sched.iterations = int(st["iterations"])
+    opt = getattr(trainer, "opt_state", None)
+    if opt:
+        if st.get("optimizer") != trainer.sched.optimizer or len(st.get("opt_state", [])) != len(opt):
+            raise ValueError("checkpoint optimizer state does not match this trainer's optimizer")
+        with torch.no_grad():
+            for dst, src in zip(opt, st["opt_state"]):
+                dst.copy_(src.to(dst.device))
     if hasattr(trainer, "sync_schedule"):
         trainer.sync_schedule()  # graph replays read the schedule from the device
     if hasattr(trainer, "repack"):

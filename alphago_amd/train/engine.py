@@ -106,17 +106,70 @@ class FlatParams:
         self.numel = off
 
 
-class KerasSGDSchedule:
-    """Keras 1.0 SGD learning rate: lr / (1 + decay * iterations), momentum 0."""
+OPTIMIZERS = ("sgd", "momentum", "adam")
 
-    def __init__(self, lr: float, decay: float = 0.0, iterations: int = 0):
+
+class KerasSGDSchedule:
+    """Keras 1.0 optimizer step size: lr / (1 + decay * iterations) (``SGD(lr, decay)``, the reference's
+    optimizer, supervised_policy_trainer.py:199).  ``optimizer="momentum"`` is Keras ``SGD(lr, momentum,
+    decay, nesterov)``; ``"adam"`` is Keras ``Adam(lr, beta_1, beta_2, epsilon)``, whose step is the
+    bias-corrected lr_t = lr sqrt(1 - beta_2^t) / (1 - beta_1^t), t = iterations + 1 (the decay factor
+    applies to it as well; Keras 1.0 Adam has none, so keep decay 0 for parity)."""
+
+    def __init__(self, lr: float, decay: float = 0.0, iterations: int = 0, optimizer: str = "sgd",
+                 momentum: float = 0.0, nesterov: bool = False, beta_1: float = 0.9, beta_2: float = 0.999,
+                 epsilon: float = 1e-8):
+        if optimizer not in OPTIMIZERS:
+            raise ValueError("optimizer must be one of %s" % (OPTIMIZERS,))
+        if optimizer == "momentum" and not 0.0 <= momentum < 1.0:
+            raise ValueError("momentum must be in [0, 1)")
         self.lr, self.decay, self.iterations = lr, decay, iterations
+        self.optimizer, self.momentum, self.nesterov = optimizer, momentum, nesterov
+        self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
+
+    @property
+    def opt_code(self) -> int:
+        return OPTIMIZERS.index(self.optimizer)
+
+    @property
+    def n_moments(self) -> int:
+        """Flat fp32 state buffers the optimizer keeps (velocity; Adam's two moments)."""
+        return {"sgd": 0, "momentum": 1, "adam": 2}[self.optimizer]
 
     def current(self) -> float:
-        return self.lr / (1.0 + self.decay * self.iterations)
+        lr = self.lr / (1.0 + self.decay * self.iterations)
+        if self.optimizer == "adam":
+            t = self.iterations + 1.0
+            lr = lr * math.sqrt(1.0 - math.pow(self.beta_2, t)) / (1.0 - math.pow(self.beta_1, t))
+        return lr
 
     def advance(self) -> None:
         self.iterations += 1
+
+    def kernel_kwargs(self) -> dict:
+        """Optimizer arguments of ops.sgd_pack."""
+        return dict(opt=self.opt_code, momentum=self.momentum, beta_1=self.beta_1, beta_2=self.beta_2,
+                    epsilon=self.epsilon, nesterov=self.nesterov)
+
+
+def optimizer_update_(p: torch.Tensor, g: torch.Tensor, state: List[torch.Tensor], sched: KerasSGDSchedule,
+                      step: float) -> None:
+    """The fused kernel's update (pack.hip opt_update) in torch fp32 ops, same operation order."""
+    with torch.no_grad():
+        if sched.optimizer == "sgd":
+            p.sub_(g * step)
+        elif sched.optimizer == "momentum":
+            v = state[0]
+            v.mul_(sched.momentum).sub_(g * step)
+            if sched.nesterov:
+                p.add_(v * sched.momentum - g * step)
+            else:
+                p.add_(v)
+        else:
+            m, v = state
+            m.mul_(sched.beta_1).add_(g * (1.0 - sched.beta_1))
+            v.mul_(sched.beta_2).add_(g * g * (1.0 - sched.beta_2))
+            p.sub_(step * m / (v.sqrt() + sched.epsilon))
 
 
 # automatic wgrad / dgrad stream overlap between these pixel counts per step (B = 8 .. 256 at 19 x 19)
@@ -130,7 +183,8 @@ class HipConvTrainer:
                  overlap: Optional[bool] = None, wgrad_target_wgs: int = 0, iterations: int = 0, precision: str = "bf16",
                  wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: Optional[bool] = None,
                  reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None,
-                 fp8_wgrad: Optional[bool] = None):
+                 fp8_wgrad: Optional[bool] = None, optimizer: str = "sgd", momentum: float = 0.0,
+                 nesterov: bool = False, fp8_bf16_layers: Optional[Sequence[int]] = None):
         ops.load()
         # wgrad kernel: 0 = per-tap kernel (default), 5 = one-kernel-row wgrad (opt-in, slower so far)
         self.wgrad_variant = int(os.environ.get("ALPHAGO_AMD_WGRAD_VARIANT", "0")) if wgrad_variant is None \
@@ -148,7 +202,13 @@ class HipConvTrainer:
             raise RuntimeError("%s needs a GPU device" % type(self).__name__)
         self.net = net.to(self.device)
         self.batch = batch
-        self.sched = KerasSGDSchedule(lr, decay, iterations)
+        self.sched = KerasSGDSchedule(lr, decay, iterations, optimizer=optimizer, momentum=momentum,
+                                      nesterov=nesterov)
+        self.fp8_bf16_layers = frozenset(int(l) for l in (fp8_bf16_layers or ()))
+        if reduce_stream is None:
+            reduce_stream = os.environ.get("ALPHAGO_AMD_REDUCE_STREAM", "0") == "1"
+        if overlap is None and reduce_stream:
+            overlap = False  # an explicit reduce stream is a serial-backward mode: it wins over the auto overlap
         if overlap is None:
             # automatic: the wgrad on a side stream beside the dgrad at small batches, where both
             # kernels leave CUs idle -- SL B = 16 19.6k -> 22.3k, B = 256 95.3k -> 99.4k positions/s --
@@ -182,6 +242,8 @@ class HipConvTrainer:
         self.fp = FlatParams(named + head, self.device)
         if self.env.distributed:
             agdist.broadcast_(self.fp.flat, 0)
+        # optimizer state (momentum velocity / Adam moments), flat fp32 like the master weights
+        self.opt_state = [torch.zeros_like(self.fp.flat) for _ in range(self.sched.n_moments)]
         dev, B, S = self.device, batch, self.S
         # unpadded filters: the kernels read the biases straight from the flat
         # master parameters (no per-step copies); padded: zero-tailed copies
@@ -240,8 +302,6 @@ class HipConvTrainer:
         # layer l runs beside dgrad(l) instead of between the two big conv kernels.  The
         # slabs are double-buffered by layer parity, so wgrad(l-1) never waits for
         # reduce(l); wgrad(l-2) waits for reduce(l) through an event.
-        if reduce_stream is None:
-            reduce_stream = os.environ.get("ALPHAGO_AMD_REDUCE_STREAM", "0") == "1"
         self.s_r = (torch.cuda.Stream(device=dev, priority=-1) if reduce_stream and not overlap else None)
         nslab = 2 if self.s_r is not None else 1
         self._slabs = [torch.empty(slab_max, device=dev) for _ in range(nslab)]
@@ -322,7 +382,9 @@ class HipConvTrainer:
                 fp8_wgrad = os.environ.get("ALPHAGO_AMD_FP8_WGRAD", "1") == "1"
             self.fp8_wgrad = bool(fp8_wgrad) and all(
                 ops.wgrad_fp8_supported(self.Fp, self.Fp, self.K[l]) for l in range(1, L))
-            self._w8layers = set(range(1, L)) if self.fp8_wgrad else set()
+            # per-layer precision: the layers in fp8_bf16_layers run their forward, dgrad and wgrad in bf16
+            # (their weights are never quantised); the others stay on the fp8 kernels
+            self._w8layers = (set(range(1, L)) - self.fp8_bf16_layers) if self.fp8_wgrad else set()
             # With the fp8 wgrad the dgrad reads the same e5m2 dZ copy and writes e5m2 for the layer
             # below (conv_dgrad_fp8_bits): the all-fp8 backward is the default there (value 12 x 152,
             # B = 1024: 156.3k -> 179.9k positions/s, profiles/r3_fp8_wgrad.md);
@@ -344,7 +406,7 @@ class HipConvTrainer:
             self._w8layers = set()
         # Keras-SGD schedule mirrored on the device (float64 {lr0, decay, iterations, lr}) so that
         # the SGD step reads its learning rate from memory: the whole step is graph-capturable
-        self._sched_dev = torch.zeros(4, dtype=torch.float64, device=dev)
+        self._sched_dev = torch.zeros(8, dtype=torch.float64, device=dev)
         # fused SGD + bf16 packs (ops.sgd_pack); ALPHAGO_AMD_FUSED_UPDATE=0: sgd_update + pack_weights
         self._fused_update = os.environ.get("ALPHAGO_AMD_FUSED_UPDATE", "1") == "1"
         self._pack_plan = None
@@ -357,8 +419,9 @@ class HipConvTrainer:
     # ------------------------------------------------------------------ schedule / graphs
     def sync_schedule(self) -> None:
         """Copy the host schedule (lr, decay, iterations) to the device copy used by graph replays."""
-        self._sched_dev.copy_(torch.tensor([self.sched.lr, self.sched.decay, float(self.sched.iterations), 0.0],
-                                           dtype=torch.float64))
+        sc = self.sched
+        self._sched_dev.copy_(torch.tensor([sc.lr, sc.decay, float(sc.iterations), 0.0, sc.beta_1, sc.beta_2,
+                                            float(sc.opt_code), 0.0], dtype=torch.float64))
 
     def enable_graphs(self, on: bool = True) -> None:
         """Run ``step`` as HIP-graph replays (bf16, per-board weights not supported): the first
@@ -443,12 +506,20 @@ class HipConvTrainer:
         # (the first, calibrating backward runs bf16 wgrads on these activations)
         e4m3_only = self.fp8_wgrad and self.fp8_dgrad and self._g8_calibrated
         sr = self._sr_seed if (self.fp8_sr and self._train_fwd) else None
+        bfl = self.fp8_bf16_layers
         for l in range(self.L):
             last = l == self.L - 1
-            y8 = None if last else (self.X8[l + 1] if self.fp8_wgrad else self.Y8[l % 2])
-            ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l], self.S,
-                             pin, 1, y_bf16=None if (e4m3_only and not last) else self.Y[l], y_fp8=y8,
-                             amax=self.amax8[l], mbits=None if last else self.MBITS[l], sr_seed=sr)
+            nxt_bf = l + 1 in bfl  # the next layer reads this output in bf16
+            y8 = None if (last or nxt_bf) else (self.X8[l + 1] if self.fp8_wgrad else self.Y8[l % 2])
+            if l in bfl:  # bf16 layer: bf16 conv, then the e4m3 copy the next (fp8) layer reads
+                self._fwd_layer(l, None if last else self.MBITS[l])
+                if y8 is not None:
+                    ops.quantize_fp8_dev(self.Y[l], y8, self.osc8[l:l + 1], self.amax8[l])
+            else:
+                keep_bf16 = last or nxt_bf or not e4m3_only
+                ops.conv_fwd_fp8(x8, self.w8[l], self.bias_p[l], self.scales8[l], self.osc8[l:l + 1], self.K[l],
+                                 self.S, pin, 1, y_bf16=self.Y[l] if keep_bf16 else None, y_fp8=y8,
+                                 amax=self.amax8[l], mbits=None if last else self.MBITS[l], sr_seed=sr)
             x8, pin = y8, 1
         if sr is not None:
             self._sr_seed.add_(1)
@@ -520,7 +591,7 @@ class HipConvTrainer:
         if red and not self.defer_allreduce and -1 in self._bucket_after_layer:
             self.reducer.launch(self._bucket_after_layer[-1])
         w8 = self.fp8_wgrad and self._g8_calibrated
-        if w8:  # the head's dZ in e5m2 for wgrad(L-1), and its max |dZ| for the next step's scale
+        if w8 and self.L - 1 in self._w8layers:  # the head's dZ in e5m2 for wgrad(L-1), and its max |dZ|
             top = self.L - 1
             ops.quantize_bf8(self.DZ[top], self.DZ8[top], self.gosc8[top:top + 1], self.gamax8[top])
         for l in reversed(range(self.L)):
@@ -532,7 +603,7 @@ class HipConvTrainer:
             else:
                 self._wgrad_layer(l, red)
             if l > 0:
-                if w8 and self.fp8_dgrad:
+                if w8 and self.fp8_dgrad and l in self._w8layers:
                     # all-fp8 backward: the e5m2 dZ copy wgrad(l) read is also this dgrad's operand;
                     # the output goes out as e5m2 (wgrad(l-1) and dgrad(l-1) read it) and as bf16 only
                     # for the first layer's bf16 wgrad; its max |dx| comes from wgrad(l-1)'s bytes
@@ -546,7 +617,8 @@ class HipConvTrainer:
                     ops.conv_dgrad_bits_bf8(self.DZ[l], self.wd[l], self.DZ[l - 1], self.MBITS[l - 1],
                                             self.DZ8[l - 1], self.gosc8[l - 1:l], self.K[l], self.S,
                                             tile=self.conv_tile)
-                elif self.precision == "fp8" and self.fp8_dgrad and self._g8_calibrated:
+                elif (self.precision == "fp8" and self.fp8_dgrad and self._g8_calibrated
+                      and l not in self.fp8_bf16_layers):
                     # fp8 dgrad straight from the bf16 dZ: converted to e5m2 in the kernel's registers
                     # (delayed per-layer scale gosc8[l]), ReLU' from the forward's bitmask, bf16 dx
                     # whose max |dx| sets the next step's scale of layer l-1
@@ -641,15 +713,22 @@ class HipConvTrainer:
                 if self._pack_plan is None:
                     self._pack_plan = self._sgd_pack_plan()
                 meta, ranges = self._pack_plan
+                sched = None
+                if device_schedule:  # the SGD kernels read the 4-entry prefix, Adam all 8
+                    sched = self._sched_dev if self.sched.optimizer == "adam" else self._sched_dev[:4]
+                st = self.opt_state
                 ops.sgd_pack(self.fp.flat, self.fp.grad, 0.0 if device_schedule else self.sched.current(), meta,
-                             self.wf, self.wd, ranges, sched=self._sched_dev if device_schedule else None)
+                             self.wf, self.wd, ranges, sched=sched, m1=st[0] if st else None,
+                             m2=st[1] if len(st) > 1 else None, **self.sched.kernel_kwargs())
                 self.sched.advance()
                 self.repack(bf16=False)
                 return
+            if self.sched.optimizer != "sgd":
+                raise ValueError("momentum / Adam run in the fused update only (ALPHAGO_AMD_FUSED_UPDATE=1)")
             if device_schedule:
                 # graph replays: lr = lr0 / (1 + decay * t) evaluated on the device (the same f64
                 # expression as KerasSGDSchedule.current()) from the copy synced at capture time
-                ops.sgd_update_sched(self.fp.flat, self.fp.grad, self._sched_dev, 1.0)
+                ops.sgd_update_sched(self.fp.flat, self.fp.grad, self._sched_dev[:4], 1.0)
             else:
                 ops.sgd_update(self.fp.flat, self.fp.grad, self.sched.current(), 1.0)
             self.sched.advance()
@@ -851,17 +930,20 @@ class HipValueTrainer(HipConvTrainer):
 
 
 class _TorchTrainerBase:
-    def _setup(self, net, batch, lr, decay, device, dtype, iterations, named):
+    def _setup(self, net, batch, lr, decay, device, dtype, iterations, named, optimizer="sgd", momentum=0.0,
+               nesterov=False):
         self.env = agdist.env()
         self.device = torch.device(device) if device is not None else self.env.device
         self.net = net.to(self.device)
         self.batch = batch
         self.dtype = dtype
-        self.sched = KerasSGDSchedule(lr, decay, iterations)
+        self.sched = KerasSGDSchedule(lr, decay, iterations, optimizer=optimizer, momentum=momentum,
+                                      nesterov=nesterov)
         self.params = [p for _, p in named]
         self.fp = FlatParams(named, self.device)
         if self.env.distributed:
             agdist.broadcast_(self.fp.flat, 0)
+        self.opt_state = [torch.zeros_like(self.fp.flat) for _ in range(self.sched.n_moments)]
         self.table = symmetry_tables(net.board, self.device)
 
     def compute_grads(self, planes, targets, sym=None, weight=None, reduce: bool = True):
@@ -880,7 +962,10 @@ class _TorchTrainerBase:
 
     def apply_update(self):
         with torch.no_grad():
-            self.fp.flat.add_(self.fp.grad, alpha=-self.sched.current())
+            if self.sched.optimizer == "sgd":
+                self.fp.flat.add_(self.fp.grad, alpha=-self.sched.current())
+            else:
+                optimizer_update_(self.fp.flat, self.fp.grad, self.opt_state, self.sched, self.sched.current())
         self.sched.advance()
 
     def step(self, planes, targets, sym=None, weight=None):
@@ -901,14 +986,15 @@ class TorchPolicyTrainer(_TorchTrainerBase):
     policy_loss = "ce"  # or "bce" (reference RL loss), as HipPolicyTrainer
 
     def __init__(self, net: PolicyNet, batch: int, lr: float = 0.003, decay: float = 0.0, device=None,
-                 dtype=torch.float32, iterations: int = 0):
+                 dtype=torch.float32, iterations: int = 0, optimizer: str = "sgd", momentum: float = 0.0,
+                 nesterov: bool = False):
         named = []
         tr = net.trunk
         for l in range(tr.layers):
             named.append(("w%d" % l, tr.weights[l]))
             named.append(("b%d" % l, tr.biases[l]))
         named += [("head_w", net.head_w), ("head_b", net.head_b)]
-        self._setup(net, batch, lr, decay, device, dtype, iterations, named)
+        self._setup(net, batch, lr, decay, device, dtype, iterations, named, optimizer, momentum, nesterov)
 
     def _loss(self, planes, targets, sym, weight):
         if sym is not None:
@@ -937,7 +1023,8 @@ class TorchPolicyTrainer(_TorchTrainerBase):
 
 class TorchValueTrainer(_TorchTrainerBase):
     def __init__(self, net: ValueNet, batch: int, lr: float = 0.003, decay: float = 0.0, device=None,
-                 dtype=torch.float32, iterations: int = 0):
+                 dtype=torch.float32, iterations: int = 0, optimizer: str = "sgd", momentum: float = 0.0,
+                 nesterov: bool = False):
         named = []
         tr = net.trunk
         for l in range(tr.layers):
@@ -945,7 +1032,7 @@ class TorchValueTrainer(_TorchTrainerBase):
             named.append(("b%d" % l, tr.biases[l]))
         named += [("head_w", net.head_w), ("head_b", net.head_b), ("fc1_w", net.fc1_w), ("fc1_b", net.fc1_b),
                   ("fc2_w", net.fc2_w), ("fc2_b", net.fc2_b)]
-        self._setup(net, batch, lr, decay, device, dtype, iterations, named)
+        self._setup(net, batch, lr, decay, device, dtype, iterations, named, optimizer, momentum, nesterov)
 
     def _loss(self, planes, targets, sym, weight):
         if sym is not None:
@@ -965,7 +1052,7 @@ def make_value_trainer(net: ValueNet, batch: int, lr: float, decay: float = 0.0,
         backend = "hip" if dev.type == "cuda" else "torch"
     if backend == "hip":
         return HipValueTrainer(net, batch, lr, decay, device=dev, **kw)
-    return TorchValueTrainer(net, batch, lr, decay, device=dev, iterations=kw.get("iterations", 0))
+    return TorchValueTrainer(net, batch, lr, decay, device=dev, **_torch_kw(kw))
 
 
 def make_policy_trainer(net: PolicyNet, batch: int, lr: float, decay: float = 0.0, backend: str = "auto",
@@ -975,4 +1062,9 @@ def make_policy_trainer(net: PolicyNet, batch: int, lr: float, decay: float = 0.
         backend = "hip" if dev.type == "cuda" else "torch"
     if backend == "hip":
         return HipPolicyTrainer(net, batch, lr, decay, device=dev, **kw)
-    return TorchPolicyTrainer(net, batch, lr, decay, device=dev, iterations=kw.get("iterations", 0))
+    return TorchPolicyTrainer(net, batch, lr, decay, device=dev, **_torch_kw(kw))
+
+
+def _torch_kw(kw: dict) -> dict:
+    """The HIP-trainer keywords the autograd trainers share (the rest are kernel options)."""
+    return {k: kw[k] for k in ("iterations", "optimizer", "momentum", "nesterov") if k in kw}

@@ -45,6 +45,13 @@ from .engine import make_value_trainer
 
 LEARNING_RATE = .003
 DECAY = 8.664339379294006e-08
+# Defaults of train-value (round 5): the reference's SGD(0.003) on its uniform(+-0.05) init does not learn
+# a 12-layer value trunk (profiles/r4/raw/value_parity_keras_init_4ep.json: every arm at the constant
+# predictor; profiles/r5/README.md: the material task).  Keras 1.0 Adam at 3e-4 learns it in fp32 and on
+# the HIP path; --optimizer sgd --learning-rate 0.003 --init keras restores the reference configuration.
+DEFAULT_OPTIMIZER = "adam"
+DEFAULT_LR = {"sgd": LEARNING_RATE, "momentum": LEARNING_RATE, "adam": 3e-4}
+DEFAULT_INIT = "keras"
 
 
 def generate_positions(sl_policy: CNNPolicy, rl_policy: CNNPolicy, n_games: int, size: int = 19,
@@ -195,8 +202,19 @@ def train_cli(argv=None):
     p.add_argument("out_directory")
     p.add_argument("--minibatch", "-B", type=int, default=32, help="per-GPU minibatch")
     p.add_argument("--epochs", "-E", type=int, default=10)
-    p.add_argument("--learning-rate", "-r", type=float, default=LEARNING_RATE)
-    p.add_argument("--decay", "-d", type=float, default=DECAY)
+    p.add_argument("--learning-rate", "-r", type=float, default=None,
+                   help="default: %s" % ", ".join("%s %g" % kv for kv in DEFAULT_LR.items()))
+    p.add_argument("--decay", "-d", type=float, default=None,
+                   help="Keras lr decay; default: the paper's %g for SGD, 0 for Adam (Keras 1.0 Adam has none)" % DECAY)
+    p.add_argument("--optimizer", default=DEFAULT_OPTIMIZER, choices=["sgd", "momentum", "adam"],
+                   help="Keras 1.0 SGD(lr, decay) / SGD(lr, momentum, decay, nesterov) / Adam(lr) (default %(default)s)")
+    p.add_argument("--momentum", type=float, default=0.9, help="with --optimizer momentum")
+    p.add_argument("--nesterov", action="store_true")
+    p.add_argument("--init", default=DEFAULT_INIT, choices=["keras", "he"],
+                   help="weights of a model JSON without a weights file: keras = uniform(+-0.05) (value.py:17,21), "
+                        "he = fan-in scaled uniform (models/nets.py he_uniform_)")
+    p.add_argument("--fp8-bf16-layers", default="0,11",
+                   help="--precision fp8: trunk layers kept in bf16 (per-layer precision; '' = all fp8)")
     p.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
@@ -217,6 +235,16 @@ def train_cli(argv=None):
     dev = env.device
     world, rank = env.world_size, env.rank
     val = CNNValue.load_model(a.model, device=dev)
+    with open(a.model) as f:
+        has_weights = bool(json.load(f).get("weights_file"))
+    if a.init == "he" and not has_weights:
+        from ..models.nets import he_uniform_
+        g = torch.Generator(device="cpu").manual_seed(a.seed)
+        net_cpu = val.model.to("cpu")
+        he_uniform_(net_cpu, generator=g)
+        val.model = net_cpu.to(dev)
+    lr = a.learning_rate if a.learning_rate is not None else DEFAULT_LR[a.optimizer]
+    decay = a.decay if a.decay is not None else (0.0 if a.optimizer == "adam" else DECAY)
     with H5File(a.train_data) as f:
         n = f["states"].shape[0]
     perm = np.random.default_rng(a.seed).permutation(n)
@@ -227,8 +255,16 @@ def train_cli(argv=None):
     data = ValueDataset(a.train_data, dev, rows=np.concatenate([my_tr, my_va]), resident=a.resident)
     n_my_tr = len(my_tr)
     B = a.minibatch
-    kw = {"precision": a.precision} if a.precision != "bf16" else {}
-    trainer = make_value_trainer(val.model, B, a.learning_rate, a.decay, backend=a.backend, device=dev, **kw)
+    kw = {"optimizer": a.optimizer, "momentum": a.momentum if a.optimizer == "momentum" else 0.0,
+          "nesterov": a.nesterov}
+    if a.precision != "bf16":
+        kw["precision"] = a.precision
+        kw["fp8_bf16_layers"] = [int(x) for x in a.fp8_bf16_layers.split(",") if x.strip() != ""]
+    backend = a.backend if a.backend != "auto" else ("hip" if dev.type == "cuda" else "torch")
+    if backend == "torch":
+        kw.pop("precision", None)
+        kw.pop("fp8_bf16_layers", None)
+    trainer = make_value_trainer(val.model, B, lr, decay, backend=backend, device=dev, **kw)
     gen = torch.Generator(device=dev)
     gen.manual_seed(a.seed + rank)
     if env.is_main:

@@ -13,11 +13,13 @@ Arms (same data, same student initialisation, same batch order and symmetries):
   hip-fp8     the HIP trainer, fp8 conv path (e4m3 forward, e5m2 x e4m3 dgrad / wgrad: the default)
   hip-fp8fwd  the HIP trainer, e4m3 forward and bf16 backward (where the fp8 loss comes from)
   hip-fp8sr   hip-fp8 with stochastic rounding of the forward's e4m3 activations (ALPHAGO_AMD_FP8_SR)
+  hip-fp8mix  per-layer precision: the --bf16-layers (default the first and last trunk layers) in bf16,
+              the rest all-fp8; hip-fp8mixsr adds the stochastic rounding
 After the first epoch the script also compares one batch's gradients of the fp8 and the fp32 trainer
 at the bf16 arm's weights (per-layer cosine), on the 12-layer trunk.
 
 Usage: python scripts/value_fp8_parity.py OUT_JSON [--positions N] [--epochs E] [--arms a,b,c]
-       [--task teacher|material] [--init keras|he] [--lr R]
+       [--task teacher|material] [--init keras|he] [--lr R] [--optimizer sgd|momentum|adam] [--seeds N]
 Prints one JSON line and writes it to OUT_JSON."""
 import argparse
 import copy
@@ -37,16 +39,23 @@ from alphago_amd.models.nets import ValueNet  # noqa: E402
 from alphago_amd.train.engine import HipValueTrainer, TorchValueTrainer  # noqa: E402
 
 
+OPT = {}  # optimizer keywords of every arm (--optimizer / --momentum)
+BF16_LAYERS = ()  # --bf16-layers: the layers the hip-fp8mix arms keep in bf16
+
+
 def make_trainer(arm, net, B, lr, dev):
     if arm == "torch-fp32":
-        return TorchValueTrainer(net, B, lr=lr, device=dev)
+        return TorchValueTrainer(net, B, lr=lr, device=dev, **OPT)
     if arm == "hip-fp8fwd":  # e4m3 forward, bf16 backward
-        return HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8", fp8_dgrad=False, fp8_wgrad=False)
-    if arm == "hip-fp8sr":  # all-fp8 step with stochastically rounded e4m3 activations in the forward
-        tr = HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8")
+        return HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8", fp8_dgrad=False, fp8_wgrad=False, **OPT)
+    if arm in ("hip-fp8sr", "hip-fp8mixsr"):  # stochastically rounded e4m3 activations in the forward
+        tr = HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8",
+                             fp8_bf16_layers=BF16_LAYERS if arm == "hip-fp8mixsr" else None, **OPT)
         tr.fp8_sr = True
         return tr
-    return HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8" if arm == "hip-fp8" else "bf16")
+    if arm == "hip-fp8mix":  # per-layer precision: BF16_LAYERS in bf16, the rest all-fp8
+        return HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8", fp8_bf16_layers=BF16_LAYERS, **OPT)
+    return HipValueTrainer(net, B, lr=lr, device=dev, precision="fp8" if arm == "hip-fp8" else "bf16", **OPT)
 
 
 def heldout_mse(tr, planes, z, B):
@@ -90,7 +99,15 @@ def main():
     ap.add_argument("--init", default="keras", choices=["keras", "he"],
                     help="student init: keras = the reference's uniform(-0.05, 0.05); he = uniform He bounds "
                          "(the reference init shrinks a 12-layer trunk's signal ~30x)")
+    ap.add_argument("--optimizer", default="sgd", choices=["sgd", "momentum", "adam"])
+    ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--bf16-layers", default="0,11", help="hip-fp8mix arms: layers kept in bf16")
+    ap.add_argument("--seeds", type=int, default=1,
+                    help="repeat every arm with this many student inits / batch orders (same data)")
     a = ap.parse_args()
+    global BF16_LAYERS
+    BF16_LAYERS = tuple(int(x) for x in a.bf16_layers.split(",") if x != "")
+    OPT.update(optimizer=a.optimizer, momentum=a.momentum if a.optimizer == "momentum" else 0.0)
     dev = torch.device("cuda")
     t0 = time.perf_counter()
     rng = np.random.default_rng(a.seed)
@@ -111,44 +128,48 @@ def main():
     Pho, Zho = P[a.positions:], Z[a.positions:]
     B = a.batch
     steps = a.positions // B
-    # the batch order and symmetries of every epoch, shared by all arms
-    g = torch.Generator(device="cpu").manual_seed(a.seed + 7)
-    orders = [torch.randperm(a.positions, generator=g) for _ in range(a.epochs)]
-    syms = [torch.randint(0, 8, (a.positions,), dtype=torch.int32, generator=g) for _ in range(a.epochs)]
-    torch.manual_seed(a.seed + 100)
-    student0 = ValueNet(49, filters_per_layer=a.filters, layers=a.layers)
-    if a.init == "he":
-        with torch.no_grad():
-            for w in list(student0.trunk.weights) + [student0.head_w]:
-                bound = (6.0 / (w.shape[1] * w.shape[2] * w.shape[3])) ** 0.5
-                w.uniform_(-bound, bound)
-            for w in (student0.fc1_w, student0.fc2_w):  # Keras (in, out) layout: fan_in = rows
-                bound = (3.0 / w.shape[0]) ** 0.5
-                w.uniform_(-bound, bound)
     res = {"teacher_target_std": round(float(Z.std()), 4), "heldout_var": round(float(Zho.var()), 5)}
     arms = {}
     mid_net = None
-    for arm in [x for x in a.arms.split(",") if x]:
-        net = copy.deepcopy(student0)
-        tr = make_trainer(arm, net, B, a.lr, dev)
-        mses, losses = [], []
-        t1 = time.perf_counter()
-        for e in range(a.epochs):
-            ep_loss = 0.0
-            order, sym = orders[e].to(dev), syms[e].to(dev)
-            for s in range(steps):
-                idx = order[s * B:(s + 1) * B]
-                loss, _ = tr.step(Ptr.index_select(0, idx), Ztr.index_select(0, idx), sym[s * B:(s + 1) * B])
-                ep_loss += float(loss) if s % 16 == 0 else 0.0
-            torch.cuda.synchronize()
-            losses.append(round(ep_loss / max(1, (steps + 15) // 16) / B, 5))
-            mses.append(round(heldout_mse(tr, Pho, Zho, B), 5))
-            print("[%s] epoch %d heldout_mse %.5f train_mse %.5f" % (arm, e + 1, mses[-1], losses[-1]), flush=True)
-            if arm == "hip-bf16" and e == 0:
-                mid_net = copy.deepcopy(net)
-        arms[arm] = {"heldout_mse": mses, "train_mse": losses, "train_s": round(time.perf_counter() - t1, 1)}
-        del tr
-        torch.cuda.empty_cache()
+    from alphago_amd.models.nets import he_uniform_
+    for k in range(a.seeds):
+        # the batch order and symmetries of every epoch, shared by all arms of this seed
+        g = torch.Generator(device="cpu").manual_seed(a.seed + 7 + 1000 * k)
+        orders = [torch.randperm(a.positions, generator=g) for _ in range(a.epochs)]
+        syms = [torch.randint(0, 8, (a.positions,), dtype=torch.int32, generator=g) for _ in range(a.epochs)]
+        torch.manual_seed(a.seed + 100 + 1000 * k)
+        student0 = ValueNet(49, filters_per_layer=a.filters, layers=a.layers)
+        if a.init == "he":
+            he_uniform_(student0)
+        for arm in [x for x in a.arms.split(",") if x]:
+            net = copy.deepcopy(student0)
+            tr = make_trainer(arm, net, B, a.lr, dev)
+            mses, losses = [], []
+            t1 = time.perf_counter()
+            for e in range(a.epochs):
+                ep_loss = 0.0
+                order, sym = orders[e].to(dev), syms[e].to(dev)
+                for s in range(steps):
+                    idx = order[s * B:(s + 1) * B]
+                    loss, _ = tr.step(Ptr.index_select(0, idx), Ztr.index_select(0, idx), sym[s * B:(s + 1) * B])
+                    ep_loss += float(loss) if s % 16 == 0 else 0.0
+                torch.cuda.synchronize()
+                losses.append(round(ep_loss / max(1, (steps + 15) // 16) / B, 5))
+                mses.append(round(heldout_mse(tr, Pho, Zho, B), 5))
+                print("[%s seed %d] epoch %d heldout_mse %.5f train_mse %.5f" % (arm, k, e + 1, mses[-1], losses[-1]),
+                      flush=True)
+                if arm == "hip-bf16" and e == 0 and k == 0:
+                    mid_net = copy.deepcopy(net)
+            r = arms.setdefault(arm, {"heldout_mse_seeds": [], "train_mse_seeds": [], "train_s": []})
+            r["heldout_mse_seeds"].append(mses)
+            r["train_mse_seeds"].append(losses)
+            r["train_s"].append(round(time.perf_counter() - t1, 1))
+            del tr
+            torch.cuda.empty_cache()
+    for r in arms.values():
+        r["heldout_mse"] = [round(float(np.mean(c)), 5) for c in zip(*r["heldout_mse_seeds"])]
+        r["train_mse"] = [round(float(np.mean(c)), 5) for c in zip(*r["train_mse_seeds"])]
+        r["heldout_mse_over_var"] = [round(m / float(Zho.var()), 4) for m in r["heldout_mse"]]
     if "torch-fp32" in arms:
         ref = arms["torch-fp32"]["heldout_mse"]
         for arm, r in arms.items():
@@ -163,7 +184,8 @@ def main():
                                                                     Ptr.index_select(0, idx), Ztr.index_select(0, idx),
                                                                     B, a.lr, dev)
     out = {"metric": "value-net held-out MSE on a learnable value task (%dx%d, 49 planes)" % (a.layers, a.filters),
-           "task": a.task, "init": a.init, "positions": a.positions,
+           "task": a.task, "init": a.init, "optimizer": a.optimizer, "seeds": a.seeds,
+           "bf16_layers": list(BF16_LAYERS), "positions": a.positions,
            "heldout": a.heldout, "epochs": a.epochs, "batch": B, "lr": a.lr, "data_s": round(t_data, 1),
            "net": "%dx%d" % (a.layers, a.filters), **res}
     print(json.dumps(out), flush=True)

@@ -331,3 +331,52 @@ def test_splitk_small_batch_trainer_matches(cuda_device, monkeypatch, B, kind):
         if gb.norm() < 1e-6 * b.fp.grad.norm():
             continue
         assert torch.nn.functional.cosine_similarity(ga, gb, dim=0) > 0.999, name
+
+
+@pytest.mark.parametrize("optimizer,nesterov", [("momentum", False), ("momentum", True), ("adam", False)])
+def test_fused_optimizer_matches_torch_update(cuda_device, optimizer, nesterov):
+    """Momentum SGD and Adam in the fused update (pack.hip opt_update) vs the same Keras 1.0 update in
+    torch fp32 ops (engine.optimizer_update_) over three steps -- two eager, one with the device
+    schedule (graph-mode path: the 8-entry schedule computes Adam's bias correction) -- and the bf16
+    packs equal a fresh pack of the updated master weights."""
+    from alphago_amd import ops
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import HipValueTrainer, optimizer_update_
+
+    torch.manual_seed(9)
+    B, C = 5, 49
+    net = ValueNet(C, filters_per_layer=152, layers=3)
+    tr = HipValueTrainer(net, B, lr=0.01, decay=0.01, device=cuda_device, optimizer=optimizer, momentum=0.9,
+                         nesterov=nesterov)
+    assert len(tr.opt_state) == (2 if optimizer == "adam" else 1)
+    p_ref = tr.fp.flat.clone()
+    st_ref = [torch.zeros_like(p_ref) for _ in tr.opt_state]
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    z = torch.rand(B, device=cuda_device) * 2 - 1
+    for k in range(3):
+        tr.compute_grads(planes, z)
+        torch.cuda.synchronize()
+        g = tr.fp.grad.clone()
+        step = tr.sched.current()
+        if k == 2:
+            tr.sync_schedule()
+        tr.apply_update(device_schedule=(k == 2))
+        optimizer_update_(p_ref, g, st_ref, tr.sched, step)
+        torch.cuda.synchronize()
+        torch.testing.assert_close(tr.fp.flat, p_ref, rtol=1e-5, atol=1e-7)
+        for a, b in zip(tr.opt_state, st_ref):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-9)
+        tr.fp.flat.copy_(p_ref)  # keep the two paths on the same weights
+    assert int(tr._sched_dev[2].item()) == tr.sched.iterations == 3
+    wf = [torch.zeros_like(w) for w in tr.wf]
+    wd = [torch.zeros_like(w) for w in tr.wd]
+    tr.fp.flat.copy_(p_ref)
+    ops.pack_weights([tr.fp.views["w%d" % l] for l in range(3)], wf, wd)
+    tr.compute_grads(planes, z)
+    tr.fp.grad.zero_()
+    tr.opt_state[0].zero_()  # zero gradient and zero velocity / first moment: the master stays put
+    tr.apply_update()
+    torch.cuda.synchronize()
+    for l in range(3):
+        assert torch.equal(tr.wf[l], wf[l]) and torch.equal(tr.wd[l], wd[l]), l
+

@@ -320,3 +320,29 @@ def test_device_records_equal_host_records(cuda_device):
     for ph, pd in zip(h.planes, d.planes):
         assert np.array_equal(ph, pd.cpu().numpy())
     assert torch.equal(grads[0], grads[1])
+
+
+def test_torch_adam_matches_keras_formula():
+    """CPU: the autograd trainer's Adam is Keras 1.0 Adam (lr_t bias correction, eps on sqrt(v))."""
+    import numpy as np
+
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import TorchValueTrainer
+
+    torch.manual_seed(2)
+    net = ValueNet(49, board=9, filters_per_layer=8, layers=2, dense=16)
+    tr = TorchValueTrainer(net, 4, lr=0.002, device="cpu", optimizer="adam")
+    p = tr.fp.flat.detach().double().numpy().copy()
+    m = np.zeros_like(p)
+    v = np.zeros_like(p)
+    planes = torch.randint(0, 2, (4, 49, 9, 9), dtype=torch.uint8)
+    z = torch.tensor([0.5, -0.2, 0.9, -1.0])
+    for t in range(1, 4):
+        tr.compute_grads(planes, z)
+        g = tr.fp.grad.double().numpy().copy()
+        tr.apply_update()
+        m = 0.9 * m + 0.1 * g
+        v = 0.999 * v + 0.001 * g * g
+        lr_t = 0.002 * np.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
+        p = p - lr_t * m / (np.sqrt(v) + 1e-8)
+        np.testing.assert_allclose(tr.fp.flat.double().numpy(), p, rtol=1e-4, atol=1e-6)

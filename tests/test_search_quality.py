@@ -289,3 +289,35 @@ def test_selfplay_records_feed_sl_and_value_training(tmp_path):
     vd = PositionDataset(sp, targets="outcomes")
     assert vd.planes == 49 and vd.n == n and set(np.unique(vd.targets_np)) <= {-1.0, 0.0, 1.0}
     del json
+
+
+def test_forest_discard_unwinds_in_flight_batches():
+    """an interrupted pipelined search (pending + held batch) is unwound by discard():
+    the virtual losses and queued marks go, set_root / advance work again, and the search continues
+    exactly as a forest that never gathered the dropped batches."""
+    size = 7
+    st = _random_position(size, np.random.default_rng(5), 7.5)
+    n2 = size * size
+
+    def run(interrupt):
+        f = engine().Forest(1, 1.5, 0.0, 0, 1000, 3, 9, [])
+        f.set_root(0, st)
+        f.gather(1)
+        f.apply(np.ones((1, n2), np.float32), np.zeros(1, np.float32))
+        if interrupt:
+            assert f.gather(4) > 0
+            f.hold()
+            f.gather(4)
+            assert f.n_held > 0
+            f.discard()
+            assert f.n_pending == 0 and f.n_held == 0
+        for _ in range(10):
+            L = f.gather(4)
+            if L:
+                v = np.linspace(-0.5, 0.5, L).astype(np.float32)
+                f.apply(np.ones((L, n2), np.float32), v)
+        stats = f.root_stats(0)
+        f.set_root(0, st)  # raised 'with pending evaluations' before discard() existed
+        return stats
+
+    assert run(True) == run(False)
