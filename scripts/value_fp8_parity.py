@@ -101,13 +101,14 @@ def main():
                          "(the reference init shrinks a 12-layer trunk's signal ~30x)")
     ap.add_argument("--optimizer", default="sgd", choices=["sgd", "momentum", "adam"])
     ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--decay", type=float, default=0.0, help="Keras lr decay: lr / (1 + decay * step)")
     ap.add_argument("--bf16-layers", default="0,11", help="hip-fp8mix arms: layers kept in bf16")
     ap.add_argument("--seeds", type=int, default=1,
                     help="repeat every arm with this many student inits / batch orders (same data)")
     a = ap.parse_args()
     global BF16_LAYERS
     BF16_LAYERS = tuple(int(x) for x in a.bf16_layers.split(",") if x != "")
-    OPT.update(optimizer=a.optimizer, momentum=a.momentum if a.optimizer == "momentum" else 0.0)
+    OPT.update(optimizer=a.optimizer, momentum=a.momentum if a.optimizer == "momentum" else 0.0, decay=a.decay)
     dev = torch.device("cuda")
     t0 = time.perf_counter()
     rng = np.random.default_rng(a.seed)
@@ -184,7 +185,7 @@ def main():
                                                                     Ptr.index_select(0, idx), Ztr.index_select(0, idx),
                                                                     B, a.lr, dev)
     out = {"metric": "value-net held-out MSE on a learnable value task (%dx%d, 49 planes)" % (a.layers, a.filters),
-           "task": a.task, "init": a.init, "optimizer": a.optimizer, "seeds": a.seeds,
+           "task": a.task, "init": a.init, "optimizer": a.optimizer, "decay": a.decay, "seeds": a.seeds,
            "bf16_layers": list(BF16_LAYERS), "positions": a.positions,
            "heldout": a.heldout, "epochs": a.epochs, "batch": B, "lr": a.lr, "data_s": round(t_data, 1),
            "net": "%dx%d" % (a.layers, a.filters), **res}

@@ -1,4 +1,5 @@
-"""bench.py driver contract on CPU: torch.distributed.run with 1 and 4 gloo ranks.
+"""bench.py driver contract on CPU: torch.distributed.run with 1, 4 and 8 gloo ranks (8 = the
+driver's scaling run on a full MI355X node, here on gloo).
 
 The driver runs ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``
 on one node; this rehearses the same launch (gloo instead of RCCL, tiny net, torch
@@ -22,7 +23,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("nproc", [1, 4])
+@pytest.mark.parametrize("nproc", [1, 4, 8])
 def test_bench_json_line_under_torchrun(nproc):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
@@ -31,7 +32,7 @@ def test_bench_json_line_under_torchrun(nproc):
            "--min-warmup-s", "0.5"]
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
                PYTHONPATH=ROOT)
-    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout  # rank 0 only

@@ -17,7 +17,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, opt="sgd"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     from alphago_amd.models.nets import PolicyNet
@@ -30,11 +30,12 @@ def _worker(rank, world, port, q):
     planes = torch.randint(0, 2, (8, 12, 19, 19), dtype=torch.uint8, generator=g)
     tgt = torch.randint(0, 361, (8,), dtype=torch.int32, generator=g)
     B = 8 // world
-    tr = TorchPolicyTrainer(net, B, lr=0.1)
+    tr = TorchPolicyTrainer(net, B, lr=0.1 if opt == "sgd" else 0.01, optimizer=opt, momentum=0.9)
     sl = slice(rank * B, (rank + 1) * B)
     tr.compute_grads(planes[sl], tgt[sl])
     grad = tr.fp.grad.clone()
     tr.step(planes[sl], tgt[sl])
+    tr.step(planes[sl], tgt[sl])  # a second step: the optimizer state (momentum / Adam moments) is used
     # numpy copies travel by value (a torch tensor is shared through a file descriptor that dies with
     # the worker if the parent has not unpickled it yet)
     q.put((rank, grad.numpy().copy(), tr.fp.flat.numpy().copy()))
@@ -42,14 +43,18 @@ def _worker(rank, world, port, q):
     agdist.shutdown()
 
 
-def test_dp_gradients_equal_single_process():
+@pytest.mark.parametrize("world,opt", [(2, "sgd"), (4, "sgd"), (2, "adam"), (4, "momentum")])
+def test_dp_gradients_equal_single_process(world, opt):
+    """world 2 / 4 DP (gloo all-reduce of the flat gradient) == one process on the union batch, with
+    SGD and with the optimizers that keep state (Keras momentum / Adam: the state sees the reduced
+    gradient, so it stays identical on every replica)."""
     from alphago_amd.models.nets import PolicyNet
     from alphago_amd.train.engine import TorchPolicyTrainer
 
-    world, port = 2, _free_port()
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, opt)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
@@ -63,14 +68,16 @@ def test_dp_gradients_equal_single_process():
     g = torch.Generator().manual_seed(5)
     planes = torch.randint(0, 2, (8, 12, 19, 19), dtype=torch.uint8, generator=g)
     tgt = torch.randint(0, 361, (8,), dtype=torch.int32, generator=g)
-    tr = TorchPolicyTrainer(net, 8, lr=0.1)
+    tr = TorchPolicyTrainer(net, 8, lr=0.1 if opt == "sgd" else 0.01, optimizer=opt, momentum=0.9)
     tr.compute_grads(planes, tgt)
     ref_grad = tr.fp.grad.clone()
+    tr.step(planes, tgt)
     tr.step(planes, tgt)
     for rank, grad, flat in res:
         assert torch.allclose(grad, ref_grad, atol=1e-6, rtol=1e-4)
         assert torch.allclose(flat, tr.fp.flat, atol=1e-6, rtol=1e-4)
-    assert torch.equal(res[0][2], res[1][2])  # replicas identical
+    for r in res[1:]:
+        assert torch.equal(res[0][2], r[2])  # replicas identical
 
 
 def test_buckets_cover_flat_buffer():

@@ -346,3 +346,22 @@ def test_torch_adam_matches_keras_formula():
         lr_t = 0.002 * np.sqrt(1 - 0.999 ** t) / (1 - 0.9 ** t)
         p = p - lr_t * m / (np.sqrt(v) + 1e-8)
         np.testing.assert_allclose(tr.fp.flat.double().numpy(), p, rtol=1e-4, atol=1e-6)
+
+
+def test_rl_two_ranks_cli(tmp_path):
+    """train-rl under torchrun on 2 gloo ranks: every rank plays its own games, the REINFORCE gradient
+    is all-reduced, rank 0 writes the snapshots / opponent pool, and the learner replicas stay equal."""
+    import json
+
+    j, w = _save_policy(tmp_path, "cpu")
+    folder = str(tmp_path / "pool")
+    metrics = str(tmp_path / "rl.jsonl")
+    r = _torchrun_cli(["train-rl", w, j, "--model_folder", folder, "--game_batch_size", "2", "--iterations", "2",
+                       "--save_every", "1", "--minibatch", "32", "--max-moves", "40", "--backend", "torch",
+                       "--metrics", metrics])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert os.path.exists(os.path.join(folder, "weights.00001.hdf5"))
+    recs = [json.loads(x) for x in open(metrics)]
+    its = [x for x in recs if "games" in x]
+    assert len(its) == 2 and all(x["games"] == 4 for x in its)  # both ranks' games counted
+
