@@ -50,11 +50,13 @@ static void launch_fwd_160(const ConvFwdArgs& a, int bm, hipStream_t st) {
   else if (bm == 256) launch_fwd_bm<160, MODE, 256, 4, true, true, false, false, STR>(a, st);
   else if (bm == 128) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR>(a, st);
   else if (bm == 64) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR>(a, st);
+#ifdef AGK_KERNEL_LAB  // LDS-ring tiles (round 4: slower or equal at small batches, kernel lab)
   else if (bm == 65) launch_fwd_bm<160, MODE, 64, 2, true, true, false, false, STR, false, 4>(a, st);
   else if (bm == 130) launch_fwd_bm<160, MODE, 128, 4, true, true, false, false, STR, false, 3>(a, st);
+#endif
   else if (bm == 38) launch_fwd_splitk<160, MODE, STR>(a, st);  // split-K (small value-net batches)
   else if (bm == 36) launch_fwd_bm<160, MODE, 32, 1, true, true, false, false, STR>(a, st);  // 32 pixels, 4 waves
-  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 36 / 38 / 64 / 65 / 128 / 130 / 256 / 384-387");
+  else throw std::invalid_argument("conv_fwd: 160-wide tiles support tile codes 36 / 38 / 64 / 128 / 256 / 384-387");
 }
 
 
@@ -99,9 +101,12 @@ static void launch_fwd_t(const ConvFwdArgs& a, hipStream_t st) {
     else if (bm == 36) launch_fwd_bm<BN, MODE, 32, 1>(a, st);
     else if (bm == 38) launch_fwd_splitk<BN, MODE>(a, st);  // 36 with split-K (conv_fwd_splitk op)
     else if (bm == 37) launch_fwd_bm<BN, MODE, 32, 2>(a, st);
-    // small batches: 65 / 130 = the 64 / 128-pixel tiles on a 4 / 3-slot LDS ring (NS above)
+#ifdef AGK_KERNEL_LAB
+    // small batches: 65 / 130 = the 64 / 128-pixel tiles on a 4 / 3-slot LDS ring (NS above); measured
+    // slower or equal (round 4), kernel lab only
     else if (bm == 65) launch_fwd_bm<BN, MODE, 64, 2, true, true, false, false, false, false, 4>(a, st);
     else if (bm == 130) launch_fwd_bm<BN, MODE, 128, 4, true, true, false, false, false, false, 3>(a, st);
+#endif
     // 385: the 384 tile with the next stage's LDS-DMA spread through the first
     // k-half's MFMAs instead of issued as one burst (kernel-lab tile 9)
     else if (bm == 385) launch_fwd_bm<BN, MODE, 384, 6, false, false, false, true>(a, st);
@@ -135,7 +140,9 @@ void launch_conv_fwd(const ConvFwdArgs& a_in, int mode, hipStream_t st) {
   else launch_fwd_mode<MODE_NONE>(a, st);
 }
 
-// packed-tap first layer (conv_fwd_pk_kernel): 384-pixel tile, 96 x 96 (or 96 x 80) per wave
+#ifdef AGK_KERNEL_LAB
+// packed-tap first layer (conv_fwd_pk_kernel): 384-pixel tile, 96 x 96 (or 96 x 80) per wave; equal to the
+// 64-channel kernel in the step (399.5 vs 398.1 us, round 4), kernel lab only
 template <int BN>
 static void launch_fwd_pk_t(const ConvFwdArgs& a, int cpt, hipStream_t st) {
   constexpr int BM = 384, MBW = 6;
@@ -157,20 +164,16 @@ void launch_conv_fwd_pk(const ConvFwdArgs& a_in, int cpt, hipStream_t st) {
   else if (a.Cout % 128 == 0) launch_fwd_pk_t<128>(a, cpt, st);
   else launch_fwd_pk_t<64>(a, cpt, st);
 }
+#endif  // AGK_KERNEL_LAB
 
 // ----------------------------------------------------------------- wgrad launchers
 
-static int wgrad0_occ3() {
-  static const int on = [] {
-    const char* e = getenv("AGK_WGRAD0_OCC3");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return on;
-}
+
 
 // The thin first layer's kernel rows run one workgroup per CU (180 VGPRs on 6 waves): ~1.16 us per
-// 32-pixel stage, 26-29 % MFMA busy (profiles/r3_final/pmc).  Round-4 variants, opt-in
-// (ALPHAGO_AMD_WGRAD0_VARIANT; in-step times at B = 2176, profiles/r4/README.md):
+// 32-pixel stage, 26-29 % MFMA busy (profiles/r3_final/pmc).  Round-4 variants, kernel lab only since
+// round 5 (torch.ops.alphago_amd_lab.conv_wgrad variant argument; in-step times at B = 2176,
+// profiles/r4/README.md):
 //   10: 12 waves (4 n x 3 c, 48 x 48 per wave per tap, 104 VGPRs): 559 us vs 556 us;
 //   11: the 6 waves with unit pipelining (wgrad_tile UP: the next tap's x fragments are read under
 //       the current tap's MFMAs; after the barrier only the dz fragments and tap 0 are exposed): 557 us;
@@ -178,15 +181,17 @@ static int wgrad0_occ3() {
 // Measured and removed: the 6 waves on a 4-slot LDS ring (601 us), 12 waves + UP capped at 85 VGPRs
 // for two workgroups per CU (56 B spilled, bench -4.5 %), UP on the 3x3 per-tap kernel (517 vs 500 us).
 template <int WN, int TAPS, int MW, int NWN = 2, int NS = 2, bool UP = false>
-static void launch_wgrad_taps48(const ConvWgradArgs& a, hipStream_t st) {
+static void launch_wgrad_taps48(const ConvWgradArgs& a_in, hipStream_t st) {
   constexpr int smem = NS * (WN + 48 * TAPS) * 64 * kWgradKsub;
+  constexpr int threads = 64 * 3 * NWN;
   static const hipError_t attr48 = hipFuncSetAttribute(
       (const void*)conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, NS, MW, NWN, UP>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr48, "hipFuncSetAttribute(max dynamic LDS)");
+  const ConvWgradArgs& a = a_in;
   dim3 grid(a.nsplit, a.T / TAPS, a.Cout / WN);
   hipLaunchKernelGGL((conv_wgrad_kernel<WN, 48, kWgradKsub, 3, TAPS, false, false, false, NS, MW, NWN, UP>), grid,
-                     dim3(64 * 3 * NWN), smem, st, a);
+                     dim3(threads), smem, st, a);
 }
 
 template <int WN, int TAPS>
@@ -196,7 +201,8 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
     // waves (2 n x 3 c) skips the zero channels -- 25% fewer MFMAs and x bytes
     // on the backward's serial tail; the slab columns 48..63 stay unwritten
     // (the reduce reads only cin_real of them)
-    if (TAPS == 5 && wgrad0_occ3()) {
+#ifdef AGK_KERNEL_LAB  // round-4 re-cuts of this kernel (equal or slower): variants 10-12, 13 = two per CU
+    if (TAPS == 5 && a.variant == 13) {
       launch_wgrad_taps48<WN, TAPS, 3>(a, st);
       return;
     }
@@ -216,7 +222,15 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
         launch_wgrad_taps48<WN, TAPS, 0, 2, 2, true>(a, st);
         return;
       }
-
+    }
+#endif
+    if constexpr (TAPS == 5 && WN == 192) {
+      // round 5: the 5x5 first layer as 96-channel halves of the output rows -- half the accumulators
+      // per wave (104 VGPRs instead of 180), so two workgroups share a CU and one resident round covers
+      // the grid (51 splits instead of two rounds of 102): 552.9 -> 489.8 us in the B = 2176 step, its
+      // split-K slab halved (reduce 205.5 -> 188.3 us per step), bench +0.6 % (profiles/r5/README.md)
+      launch_wgrad_taps48<96, TAPS, 0>(a, st);
+      return;
     }
     launch_wgrad_taps48<WN, TAPS, 0>(a, st);
     return;
@@ -235,8 +249,10 @@ int wgrad_tap_group(int Cout, int Cin, int K, int variant) {
   return (c64 && variant == 0 && (K == 3 || K == 5)) ? K : 1;
 }
 
+#ifdef AGK_KERNEL_LAB
 // variant 9 (small batches): the per-tap kernel on a 4-slot LDS ring, one workgroup per CU, for the
-// tile geometries whose waves stage equal piece counts (192 x 192, 128 x 128, 160 x 160)
+// tile geometries whose waves stage equal piece counts (192 x 192, 128 x 128, 160 x 160); the SL step at
+// B = 16 measured 0.901 ms with it against 0.863 ms without (round 4): kernel lab only
 template <int WN, int WC, int NWC>
 static bool launch_wgrad_ring(const ConvWgradArgs& a, dim3 grid, hipStream_t st) {
   constexpr int KS = kWgradKsub;
@@ -256,17 +272,18 @@ static bool launch_wgrad_ring(const ConvWgradArgs& a, dim3 grid, hipStream_t st)
   }
   return false;
 }
+#endif  // AGK_KERNEL_LAB
 
 template <int WN, int WC>
 static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
   dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
   constexpr int KS = kWgradKsub;
   constexpr int smem = 2 * (WN + WC) * 64 * KS;
-  if (WC != 64 && a.variant == 9 && launch_wgrad_ring<WN, WC, 4>(a, grid, st)) return;
 #ifdef AGK_KERNEL_LAB
+  if (WC != 64 && a.variant == 9 && launch_wgrad_ring<WN, WC, 4>(a, grid, st)) return;
   if (a.variant != 9 && launch_conv_wgrad_lab(a, WN, WC, grid, st)) return;  // lab variants 2 / 3 / 4 (conv_lab.hip)
 #else
-  if (a.variant != 0 && !(a.variant >= 9 && a.variant <= 12))
+  if (a.variant != 0)
     throw std::invalid_argument("conv_wgrad: variant " + std::to_string(a.variant) + " is a kernel-lab variant");
 #endif
   if constexpr (WC == 64) {
@@ -277,7 +294,9 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
       return;
     }
   }
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
   hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS>), grid, dim3(512), smem, st, a);
 }
@@ -285,8 +304,10 @@ static void launch_wgrad_t(const ConvWgradArgs& a, hipStream_t st) {
 // 160 x 160 tile on 4 waves (2 n x 2 c, 80 x 80 per wave): the value net's
 // padded width; 40 KB of LDS, so several workgroups share a CU
 static void launch_wgrad_160x160(const ConvWgradArgs& a, hipStream_t st) {
+#ifdef AGK_KERNEL_LAB
   if (a.variant == 9 && launch_wgrad_ring<160, 160, 2>(a, dim3(a.nsplit, a.T, 1), st)) return;
-  if (a.variant != 0 && a.variant != 9) throw std::invalid_argument("conv_wgrad: 160-wide tiles have no lab variants");
+#endif
+  if (a.variant != 0) throw std::invalid_argument("conv_wgrad: 160-wide tiles have no production variants");
   constexpr int KS = kWgradKsub;
   constexpr int smem = 2 * (160 + 160) * 64 * KS;
   static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<160, 160, KS, 2>,
@@ -313,13 +334,14 @@ unsigned debug_error_fetch_and_clear(hipStream_t st) {
 }
 #endif
 
-void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3]) {
+void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[4]) {
   if ((variant == 6 || variant == 8) && wgrad_pair_applies(Cout, Cin, cin_real, K)) {
     // tap pairs: 4.5 workgroups per split (9 per two splits), one per CU -- reported as 9 per
     // split pair and 2 per CU so that nsplit = CUs * out[2] / out[1] stays an integer division
     out[0] = 2;
     out[1] = 9;
     out[2] = 2;
+    out[3] = 512;
     return;
   }
 #ifdef AGK_KERNEL_LAB
@@ -328,13 +350,15 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
     out[0] = K;
     out[1] = wgrad_row_wgs_per_split(code, Cout, Cin, cin_real, K);
     out[2] = 1;
+    out[3] = 256;
     return;
   }
 #endif
   // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
-  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 12) ? 0 : variant);
+  const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 13) ? 0 : variant);
   const bool c48 = cin_real <= 48 && Cin == 64;
-  const int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
+  int wn = Cout == 160 ? 160 : Cout % 192 == 0 ? 192 : Cout % 128 == 0 ? 128 : 64;
+  if (c48 && taps == 5 && wn == 192) wn = 96;  // the first layer's 96-wide halves (launch_wgrad_taps)
   const int wc = Cout == 160 && Cin == 160 ? 160 : Cin % 192 == 0 ? 192 : Cin % 128 == 0 ? 128 : 64;
   out[0] = taps;
   out[1] = (K * K / taps) * (Cout / wn) * (c48 ? 1 : Cin / wc);
@@ -343,6 +367,8 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3])
   // as two rounds (251 us per step, profiles/r3_fp8_wgrad.md)
   out[2] = (taps == 5 && wn == 160 && !c48) ? 1 : 2;
   if (variant == 9 && taps == 1) out[2] = 1;  // the 4-slot ring: one workgroup per CU
+  // threads per workgroup
+  out[3] = c48 ? 384 : (wn == 160 && wc == 160) ? 256 : 512;
 }
 
 static int wgrad_xcd_group() {
@@ -402,7 +428,7 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
 // in increasing order, the leftover splits added to s_0, then
 // (s0 + s1) + (s2 + s3).  Wave k of a 256-thread block computes s_k for 64
 // float4 elements (4 consecutive input channels of one tap and output
-// channel), 4 16-B loads in flight; the four partials meet in LDS.  The OIHW
+// channel), up to 8 16-B loads in flight; the four partials meet in LDS.  The OIHW
 // write is strided but touches the (small) gradient once.
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(WgradReduceArgs a) {
   __shared__ f32x4 part[4][64];
@@ -422,20 +448,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(WgradReduceArgs 
     const float* s = a.slab + (size_t)t * tile + (size_t)n * a.Cin + c;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (c < a.Cin_real) {
-      int sp = k;
-      for (; sp + 12 < n4; sp += 16) {
-        const f32x4 v0 = *(const f32x4*)(s + (size_t)sp * sstride);
-        const f32x4 v1 = *(const f32x4*)(s + (size_t)(sp + 4) * sstride);
-        const f32x4 v2 = *(const f32x4*)(s + (size_t)(sp + 8) * sstride);
-        const f32x4 v3 = *(const f32x4*)(s + (size_t)(sp + 12) * sstride);
-        acc += v0;
-        acc += v1;
-        acc += v2;
-        acc += v3;
+      // up to 8 of this wave's splits loaded before they are added (round 5: 4 loads in flight left
+      // the reduce latency-bound, ~4.4 TB/s); same order of additions as one split at a time
+      for (int sp0 = k; sp0 < n4; sp0 += 32) {
+        const int cnt = (n4 - sp0 + 3) >> 2;
+        const float* p = s + (size_t)sp0 * sstride;
+        f32x4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (i < cnt) v[i] = *(const f32x4*)(p + (size_t)(4 * i) * sstride);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (i < cnt) acc += v[i];
       }
-      for (; sp < n4; sp += 4) acc += *(const f32x4*)(s + (size_t)sp * sstride);
       if (k == 0)
-        for (sp = n4; sp < a.nsplit; ++sp) acc += *(const f32x4*)(s + (size_t)sp * sstride);
+        for (int sp = n4; sp < a.nsplit; ++sp) acc += *(const f32x4*)(s + (size_t)sp * sstride);
     }
     part[k][lane] = acc;
     __syncthreads();

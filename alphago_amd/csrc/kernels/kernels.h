@@ -205,7 +205,7 @@ int wgrad_row_wgs_per_split(int code, int Cout, int Cin, int cin_real, int K);
 void wgrad_row_launch(int code, const ConvWgradArgs& a, hipStream_t st);
 // launch plan of the wgrad that launch_conv_wgrad runs for this variant:
 // {taps per workgroup, workgroups per split, resident workgroups per CU}
-void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[3]);
+void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[4]);
 // a launch the runtime must reject (block of 2048 threads): tests the error path
 void launch_invalid_config_probe(hipStream_t st);
 #ifdef AGK_DEBUG

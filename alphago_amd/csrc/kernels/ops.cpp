@@ -14,21 +14,11 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   check_dev("conv_fwd", x, w, bias, mask, y, mbits);
   // production tilings only: 0 = automatic, or a fixed 64 / 128 / 256 / 384-pixel tile (385: 384 with the
   // LDS-DMA issue spread through the MFMAs; 386 / 387: 385 / 384 with the chunk-outer K order)
-  TORCH_CHECK(tile == 0 || tile == 36 || tile == 37 || tile == 64 || tile == 65 || tile == 128 || tile == 130 ||
-                  tile == 256 || tile == 384 || tile == 385 || tile == 386 || tile == 387,
-              "conv_fwd tile ", tile, " is not a production tiling (0, 36, 37, 64, 65, 128, 130, 256, 384-387); kernel-lab "
+  TORCH_CHECK(tile == 0 || tile == 36 || tile == 37 || tile == 64 || tile == 128 || tile == 256 || tile == 384 ||
+                  tile == 385 || tile == 386 || tile == 387,
+              "conv_fwd tile ", tile, " is not a production tiling (0, 36, 37, 64, 128, 256, 384-387); kernel-lab "
               "variants are in torch.ops.alphago_amd_lab (alphago_amd.ops.lab())");
   conv_fwd_impl(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, (int)tile);
-}
-
-// First layer on the packed-tap K loop (conv_fwd_pk_kernel): only the cin_real real input channels
-// of the 64-channel padded input are multiplied; w in the packed-tap layout (pack_weights detects it)
-void conv_fwd_pk(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& y, int64_t K, int64_t S,
-                 int64_t Pin, int64_t Po, int64_t cin_real, const c10::optional<Tensor>& mbits) {
-  check_dev("conv_fwd_pk", x, w, bias, y, mbits);
-  TORCH_CHECK(cin_real > 32 && cin_real <= 64, "conv_fwd_pk: 32 < cin_real <= 64");
-  conv_fwd_impl(x, w, bias, c10::nullopt, y, K, S, Pin, Po, agk::MODE_BIAS_RELU, mbits, 0, nullptr, -1, c10::nullopt,
-                c10::nullopt, c10::nullopt, (int)((cin_real + 7) / 8));
 }
 
 // one draw per board from probs ** beta (probs: (B, NP) f32, has: (B,) bool / uint8, out: (B,) int64)
@@ -68,16 +58,9 @@ void conv_fwd_splitk(const Tensor& x, const Tensor& w, const c10::optional<Tenso
 void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Tensor& dbslab, int64_t K, int64_t S,
                 int64_t Pin, int64_t Po, int64_t cin_real, int64_t variant) {
   check_dev("conv_wgrad", x, dz, slab, dbslab);
-  // 0 = per-tap kernel (default), 9 = 4-slot LDS-ring kernel (small batches), 10-12 = the thin first
-  // layer's kernel rows on 12 waves / with unit pipelining / both; the lab build also has 5 = one-kernel-row
-  // wgrad
-#ifdef AGK_KERNEL_LAB
-  TORCH_CHECK(variant == 0 || variant == 5 || (variant >= 9 && variant <= 12), "conv_wgrad variant ", variant,
-              " unknown (0, 5, 9-12)");
-#else
-  TORCH_CHECK(variant == 0 || (variant >= 9 && variant <= 12), "conv_wgrad variant ", variant,
-              " is not a production kernel (0, 9-12)");
-#endif
+  // the per-tap / tap-merged kernel only; the round-4 variants (9 LDS ring, 10-13 first-layer re-cuts) and
+  // the older lab variants run from torch.ops.alphago_amd_lab
+  TORCH_CHECK(variant == 0, "conv_wgrad variant ", variant, " is a kernel-lab variant (alphago_amd.ops.lab())");
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }
 
@@ -556,11 +539,12 @@ int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) {
   return agk::wgrad_tap_group((int)cout, (int)cin, (int)K, 0);
 }
 
-// {taps per workgroup, workgroups per split, resident workgroups per CU} of the production wgrad
+// {taps per workgroup, workgroups per split, resident workgroups per CU, threads per workgroup} of the
+// production wgrad
 std::vector<int64_t> wgrad_plan(int64_t cout, int64_t cin, int64_t cin_real, int64_t K, int64_t variant) {
-  int o[3];
+  int o[4];
   agk::wgrad_plan((int)cout, (int)cin, (int)(cin_real > 0 && cin_real < cin ? cin_real : cin), (int)K, (int)variant, o);
-  return {o[0], o[1], o[2]};
+  return {o[0], o[1], o[2], o[3]};
 }
 
 void comm_proxy(const Tensor& src, const Tensor& dst, int64_t channels, double wire_us) {
@@ -729,9 +713,6 @@ void debug_conv_fwd_understated(const Tensor& x, const Tensor& w, const Tensor& 
 
 TORCH_LIBRARY(alphago_amd, m) {
   m.def(
-      "conv_fwd_pk(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int K, int S, int Pin, int Po, int cin_real, "
-      "Tensor(b!)? mbits=None) -> ()");
-  m.def(
       "conv_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? mask, Tensor(a!) y, int K, int S, int Pin, int Po, int mode, "
       "Tensor(b!)? mbits=None, int tile=0) -> ()");
   m.def(
@@ -804,7 +785,6 @@ TORCH_LIBRARY(alphago_amd, m) {
 TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("conv_fwd", &conv_fwd);
   m.impl("sgd_pack", &sgd_pack);
-  m.impl("conv_fwd_pk", &conv_fwd_pk);
   m.impl("conv_fwd_splitk", &conv_fwd_splitk);
   m.impl("sample_moves", &sample_moves);
   m.impl("conv_wgrad", &conv_wgrad);

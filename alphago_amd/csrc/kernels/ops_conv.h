@@ -149,8 +149,13 @@ inline void conv_fwd_impl(const Tensor& x, const Tensor& w, const c10::optional<
     TORCH_CHECK(tile != 38, "tile 38 (split-K) needs a workspace: conv_fwd_splitk");
   }
   if (a.M == 0) return;
+#ifdef AGK_KERNEL_LAB
   if (pk_cpt > 0) agk::launch_conv_fwd_pk(a, pk_cpt, cur_stream());
   else agk::launch_conv_fwd(a, (int)mode, cur_stream());
+#else
+  TORCH_CHECK(pk_cpt <= 0, "conv_fwd: the packed-tap first layer is a kernel-lab variant");
+  agk::launch_conv_fwd(a, (int)mode, cur_stream());
+#endif
   launch_check("conv_fwd");
 }
 

@@ -31,6 +31,17 @@ void conv_wgrad_lab(const Tensor& x, const Tensor& dz, const Tensor& slab, const
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }
 
+// First layer on the packed-tap K loop (conv_fwd_pk_kernel; production until round 4, measured equal):
+// only the cin_real real input channels of the 64-channel padded input are multiplied; w in the
+// packed-tap layout (pack_weights detects it)
+void conv_fwd_pk_lab(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& y, int64_t K, int64_t S,
+                     int64_t Pin, int64_t Po, int64_t cin_real, const c10::optional<Tensor>& mbits) {
+  check_dev("conv_fwd_pk", x, w, bias, y, mbits);
+  TORCH_CHECK(cin_real > 32 && cin_real <= 64, "conv_fwd_pk: 32 < cin_real <= 64");
+  conv_fwd_impl(x, w, bias, c10::nullopt, y, K, S, Pin, Po, agk::MODE_BIAS_RELU, mbits, 0, nullptr, -1, c10::nullopt,
+                c10::nullopt, c10::nullopt, (int)((cin_real + 7) / 8));
+}
+
 void conv_fwd_fp8_lab(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales,
                       const Tensor& out_scale, const c10::optional<Tensor>& amax,
                       const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S,
@@ -44,9 +55,9 @@ int64_t wgrad_tap_group_lab(int64_t cout, int64_t cin, int64_t K, int64_t varian
 }
 
 std::vector<int64_t> wgrad_plan_lab(int64_t cout, int64_t cin, int64_t cin_real, int64_t K, int64_t variant) {
-  int o[3];
+  int o[4];
   agk::wgrad_plan((int)cout, (int)cin, (int)(cin_real > 0 && cin_real < cin ? cin_real : cin), (int)K, (int)variant, o);
-  return {o[0], o[1], o[2]};
+  return {o[0], o[1], o[2], o[3]};
 }
 
 void bf8_convert_probe(const Tensor& x, const Tensor& y, double scale, int64_t mode) {
@@ -150,6 +161,9 @@ TORCH_LIBRARY(alphago_amd_lab, m) {
   m.def(
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
       "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, int variant) -> ()");
+  m.def(
+      "conv_fwd_pk(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int K, int S, int Pin, int Po, int cin_real, "
+      "Tensor(b!)? mbits=None) -> ()");
   m.def("wgrad_tap_group(int cout, int cin, int K, int variant) -> int", &wgrad_tap_group_lab);
   m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant) -> int[]", &wgrad_plan_lab);
   m.def("bf8_convert_probe(Tensor x, Tensor(a!) y, float scale, int mode) -> ()");
@@ -165,5 +179,6 @@ TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {
   m.impl("conv_fwd", &conv_fwd_lab);
   m.impl("conv_wgrad", &conv_wgrad_lab);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8_lab);
+  m.impl("conv_fwd_pk", &conv_fwd_pk_lab);
   m.impl("ladder_planes", &ladder_planes);
 }

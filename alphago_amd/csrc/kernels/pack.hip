@@ -360,11 +360,12 @@ __device__ __forceinline__ void sgd_pack_job(const SgdPackArgs& a, __bf16* tile)
   }
 }
 
+// one kernel per optimizer: the Adam body's extra moment registers must not lower the SGD kernel's
+// occupancy (one kernel with a runtime switch took 56 us per step instead of 35, round 5)
+template <int OPT>
 __global__ __launch_bounds__(256) void sgd_pack_kernel(SgdPackArgs a) {
   __shared__ __bf16 tile[kSgdPackMaxTaps * 32 * 33];  // [t][c][n] (n padded to 33: no bank conflicts)
-  if (a.opt == 1) sgd_pack_job<1>(a, tile);  // launch-uniform
-  else if (a.opt == 2) sgd_pack_job<2>(a, tile);
-  else sgd_pack_job<0>(a, tile);
+  sgd_pack_job<OPT>(a, tile);
 }
 
 void launch_sgd_pack(const SgdPackArgs& a, hipStream_t st) {
@@ -376,7 +377,9 @@ void launch_sgd_pack(const SgdPackArgs& a, hipStream_t st) {
     if (t > tiles) tiles = t;
   }
   if (tiles < 64) tiles = 64;  // the plain-range job's blocks
-  hipLaunchKernelGGL(sgd_pack_kernel, dim3(tiles, a.nlayers + 1), dim3(256), 0, st, a);
+  if (a.opt == 1) hipLaunchKernelGGL(sgd_pack_kernel<1>, dim3(tiles, a.nlayers + 1), dim3(256), 0, st, a);
+  else if (a.opt == 2) hipLaunchKernelGGL(sgd_pack_kernel<2>, dim3(tiles, a.nlayers + 1), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(sgd_pack_kernel<0>, dim3(tiles, a.nlayers + 1), dim3(256), 0, st, a);
 }
 
 }  // namespace agk

@@ -61,10 +61,7 @@ class HipTrunkInference:
         self.fp8_min_batch = int(os.environ.get("ALPHAGO_AMD_FP8_MIN_BATCH", "256"))
         dev = self.device
         # packed on the engine's device whatever device the module's parameters are on
-        # first layer on the packed-tap forward when it applies (ops.conv_fwd_pk: real input planes only)
-        self.pk0 = ops.pk_applies(self.C0, self.C0p)
-        self.wf = [ops.packed_weight_pk(tr.weights[0], self.Fp, device=dev) if l == 0 and self.pk0 else
-                   ops.packed_weight_like(tr.weights[l], self.C0p if l == 0 else self.Fp, self.Fp, device=dev)
+        self.wf = [ops.packed_weight_like(tr.weights[l], self.C0p if l == 0 else self.Fp, self.Fp, device=dev)
                    for l in range(self.L)]
         self.bias_p = [torch.zeros(self.Fp, device=dev) for _ in range(self.L)]
         self.head_w = torch.zeros(self.F, device=dev)
@@ -137,7 +134,7 @@ class HipTrunkInference:
         bk.Y = [ops.padded_empty(B, S, 1, self.Fp, dev) for _ in range(2)]
         # small buckets: the split-K 32-pixel conv (ops.conv_fwd_splitk), fp32 partials in bk.ws
         M = B * S * S
-        bk.sk = [1 if (l == 0 and self.pk0) or (self.precision == "fp8" and B >= self.fp8_min_batch) else
+        bk.sk = [1 if (self.precision == "fp8" and B >= self.fp8_min_batch) else
                  ops.splitk_nsplit(M, self.Fp, self.C0p if l == 0 else self.Fp, self.K[l]) for l in range(self.L)]
         bk.ws = torch.empty(max(bk.sk) * M * self.Fp, device=dev) if max(bk.sk) > 1 else None
         if self.precision == "fp8":
@@ -184,9 +181,7 @@ class HipTrunkInference:
         x, pin = bk.X0, self.P0
         for l in range(self.L):
             y = bk.Y[l % 2]
-            if l == 0 and self.pk0:
-                ops.conv_fwd_pk(x, self.wf[0], self.bias_p[0], y, self.K[0], self.S, pin, 1, self.C0)
-            elif bk.sk[l] > 1:
+            if bk.sk[l] > 1:
                 ops.conv_fwd_splitk(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1, ops.MODE_BIAS_RELU,
                                     None, bk.ws, bk.sk[l])
             else:

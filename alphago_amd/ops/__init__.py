@@ -177,12 +177,6 @@ def pk_shape_ok(cin_real: int, cin_p: int) -> bool:
     return cin_p == 64 and 32 < cin_real < 64
 
 
-def pk_applies(cin_real: int, cin_p: int) -> bool:
-    """Whether the trainers / inference nets run their first layer on conv_fwd_pk.  Off by default
-    (ALPHAGO_AMD_PK=1 turns it on): it multiplies 24 % fewer MFMAs than the 64-channel 5x5 kernel but a
-    K-step's row then gathers from two or three pixels, and at B = 2176 it measured 399.5 us against the
-    64-channel kernel's ~381 us (profiles/r4/README.md)."""
-    return pk_shape_ok(cin_real, cin_p) and os.environ.get("ALPHAGO_AMD_PK", "0") == "1"
 
 
 def packed_weight_pk(w_oihw: torch.Tensor, cout_p: int, device=None) -> torch.Tensor:
@@ -195,9 +189,12 @@ def packed_weight_pk(w_oihw: torch.Tensor, cout_p: int, device=None) -> torch.Te
 
 
 def conv_fwd_pk(x, w_pk, bias, y, K: int, S: int, Pin: int, Po: int, cin_real: int, mbits=None):
-    """First layer (bias + ReLU, optional ReLU' bitmask) on the packed-tap K loop: only the cin_real real
-    channels of the 64-channel padded input are multiplied (48 planes: 19 K-steps instead of 25)."""
-    _ops().conv_fwd_pk(x, w_pk, bias, y, K, S, Pin, Po, cin_real, mbits)
+    """Kernel lab: the first layer (bias + ReLU, optional ReLU' bitmask) on the packed-tap K loop -- only
+    the cin_real real channels of the 64-channel padded input are multiplied (48 planes: 19 K-steps
+    instead of 25).  It multiplies 24 % fewer MFMAs but a K-step's row gathers from two or three pixels,
+    and at B = 2176 it measured 399.5 us against the 64-channel kernel's ~381-398 us (round 4), so the
+    trainers no longer use it."""
+    lab().conv_fwd_pk(x, w_pk, bias, y, K, S, Pin, Po, cin_real, mbits)
     return y
 
 
@@ -209,9 +206,9 @@ def mbits_words(cout_p: int) -> int:
 def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1, cin_real: int = 0, variant: int = 0):
     """Split-K weight gradient into ``slab``; ``cin_real`` (< padded Cin) lets
     the kernel skip zero-padded input channels (only slab columns < cin_real are written).
-    ``variant``: 0 = per-tap kernel (default), 9 = the per-tap kernel on a 4-slot LDS ring (small
-    batches), 10 = the thin first layer's kernel rows on 12 waves (ops.wgrad_config picks them)."""
-    _ops().conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, variant)
+    ``variant`` 0 = the production per-tap kernel; any other variant is a kernel-lab kernel
+    (torch.ops.alphago_amd_lab: 9 = LDS ring, 10-13 = first-layer re-cuts, ...)."""
+    (_ops() if variant == 0 else lab()).conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, variant)
 
 
 def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, beta: float = 0.0):
@@ -315,10 +312,10 @@ def wgrad_tap_group(cout_p: int, cin_p: int, K: int) -> int:
 
 
 def wgrad_plan(cout_p: int, cin_p: int, K: int, cin_real: int = 0, variant: int = 0):
-    """(taps per workgroup, workgroups per split, resident workgroups per CU) of the wgrad kernel the
-    production library runs for this layer (conv_wgrad_row.hip where it applies, else conv.hip)."""
-    t, w, c = _ops().wgrad_plan(cout_p, cin_p, cin_real, K, variant)
-    return int(t), int(w), int(c)
+    """(taps per workgroup, workgroups per split, resident workgroups per CU, threads per workgroup) of
+    the wgrad kernel the production library runs for this layer."""
+    t, w, c, th = _ops().wgrad_plan(cout_p, cin_p, cin_real, K, variant)
+    return int(t), int(w), int(c), int(th)
 
 
 WGRAD_MIN_STAGES = int(os.environ.get("ALPHAGO_AMD_WGRAD_MIN_STAGES", "8"))
@@ -329,7 +326,7 @@ def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
     """Pixel splits of the production wgrad: one resident round of workgroups over ``cus`` CUs
     (``target_wgs`` > 0 overrides the workgroup count).  A second, partial round of workgroups costs
     30-70 % (profiles/r2_wgrad_variants.md), so the grid never exceeds one round."""
-    _, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, variant)
+    _, per_split, per_cu, _ = wgrad_plan(cout_p, cin_p, K, cin_real, variant)
     target = target_wgs if target_wgs > 0 else cus * per_cu
     nks = (M + 31) // 32
     # at least WGRAD_MIN_STAGES 32-pixel stages per split: at small batches one resident round of
@@ -338,33 +335,12 @@ def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
     return max(1, min(target // per_split, nks // WGRAD_MIN_STAGES if target_wgs <= 0 else nks))
 
 
-# small batches (round 4): where the min-stages rule leaves the grid short of one workgroup per CU,
-# the per-tap kernel can run on a 4-slot LDS ring (variant 9) with longer splits: the slab it writes
-# and the reduce reads shrink with the split count, and the ring hides the DMA latency that bounds
-# a short split.  Opt-in (ALPHAGO_AMD_WGRAD_RING=1): the SL step at B = 16 measured 0.901 ms with it
-# against 0.863 ms without (profiles/r4/README.md)
-WGRAD_RING_STAGES = int(os.environ.get("ALPHAGO_AMD_RING_STAGES", "16"))
-
-
 def wgrad_config(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, target_wgs: int = 0, cus: int = 256,
                  variant: int = 0):
-    """(variant, nsplit) of a layer's wgrad: the requested variant and wgrad_nsplit, or at small
-    batches with ALPHAGO_AMD_WGRAD_RING=1 (variant 0, no explicit target) the ring variant 9 with
-    WGRAD_RING_STAGES per split."""
-    ns = wgrad_nsplit(M, cout_p, cin_p, K, cin_real, target_wgs, cus, variant)
-    v0 = os.environ.get("ALPHAGO_AMD_WGRAD0_VARIANT", "0")
-    if variant == 0 and K == 5 and cin_p == 64 and 0 < cin_real <= 48 and v0 in ("10", "11", "12") \
-            and (cout_p % 64 == 0 or v0 == "11"):
-        # the thin first layer's kernel rows: 10 = 12 waves, 11 = unit pipelining, 12 = both
-        # (conv.hip launch_wgrad_taps48; measured equal to the default, opt-in)
-        return int(v0), ns
-    if variant != 0 or target_wgs > 0 or os.environ.get("ALPHAGO_AMD_WGRAD_RING", "0") != "1":
-        return variant, ns
-    taps, per_split, per_cu = wgrad_plan(cout_p, cin_p, K, cin_real, 0)
-    if taps != 1 or ns * per_split > cus:
-        return variant, ns
-    nks = (M + 31) // 32
-    return 9, max(1, min(cus // per_split, nks // WGRAD_RING_STAGES))
+    """(variant, nsplit) of a layer's wgrad: the requested variant and wgrad_nsplit.  (Round 4's
+    small-batch LDS-ring variant 9 and the first-layer variants 10-12 are kernel-lab kernels since
+    round 5: measured slower or equal.)"""
+    return variant, wgrad_nsplit(M, cout_p, cin_p, K, cin_real, target_wgs, cus, variant)
 
 
 def wgrad_splits(M: int, T: int, n_tiles: int = 1, target_wgs: int = 512) -> int:

@@ -251,13 +251,10 @@ class HipConvTrainer:
         self.bias_p = ([self.fp.views["b%d" % l] for l in range(self.L)] if self._bias_alias
                        else [torch.zeros(self.Fp, device=dev) for _ in range(self.L)])
         self.wf, self.wd = [], []
-        # first layer on the packed-tap forward: only the real input planes are multiplied (conv_fwd_pk)
-        self.pk0 = ops.pk_applies(self.C0, self.C0p)
         for l in range(self.L):
             cin_p = self.C0p if l == 0 else self.Fp
             w = self.fp.views["w%d" % l]
-            self.wf.append(ops.packed_weight_pk(w, self.Fp) if l == 0 and self.pk0 else
-                           ops.packed_weight_like(w, cin_p, self.Fp))
+            self.wf.append(ops.packed_weight_like(w, cin_p, self.Fp))
             self.wd.append(ops.packed_weight_like(w, cin_p, self.Fp, transposed=True) if l > 0
                            else torch.empty(0, device=dev, dtype=torch.bfloat16))
         # activations / gradients (zero borders are never written)
@@ -293,7 +290,7 @@ class HipConvTrainer:
         if conv_tile == 0 and self.precision == "bf16" and not self.lab_tile:
             for l in range(self.L):
                 cin_p = self.C0p if l == 0 else self.Fp
-                self.sk_fwd[l] = 1 if (l == 0 and self.pk0) else ops.splitk_nsplit(M, self.Fp, cin_p, self.K[l])
+                self.sk_fwd[l] = ops.splitk_nsplit(M, self.Fp, cin_p, self.K[l])
                 if l > 0:
                     self.sk_dg[l] = ops.splitk_nsplit(M, self.Fp, self.Fp, self.K[l])
         sk_max = max(self.sk_fwd + self.sk_dg)
@@ -484,11 +481,9 @@ class HipConvTrainer:
             self._fwd_layer(l, self.MBITS[l] if l < self.L - 1 else None)
 
     def _fwd_layer(self, l: int, mbits=None) -> None:
-        """bf16 forward of layer l into Y[l] (the first layer on the packed-tap kernel when it applies)."""
+        """bf16 forward of layer l into Y[l]."""
         x, pin = self._layer_in(l)
-        if l == 0 and self.pk0:
-            ops.conv_fwd_pk(x, self.wf[0], self.bias_p[0], self.Y[0], self.K[0], self.S, pin, 1, self.C0, mbits)
-        elif self.lab_tile and self.K[l] == 3:
+        if self.lab_tile and self.K[l] == 3:
             ops.lab().conv_fwd(x, self.wf[l], self.bias_p[l], None, self.Y[l], 3, self.S, pin, 1, 0, mbits,
                                self.lab_tile)
         elif self.sk_fwd[l] > 1:

@@ -4,8 +4,20 @@ ReLU'-bitmask dgrad, and the 160x160 / tap-merged 160x64 wgrad tiles."""
 import pytest
 import torch
 import torch.nn.functional as F
+from _marks import lab_params
 
 pytestmark = pytest.mark.gpu
+
+PROD_160 = (0, 36, 64, 128, 256, 384, 385, 386, 387)
+
+
+def _conv_fwd(ops, tile, x, w, bias, y, K, S, Pin, Po=1, mode=0, mbits=None):
+    """Production tiles through torch.ops.alphago_amd, the LDS-ring tiles 65 / 130 (kernel lab since
+    round 5) through torch.ops.alphago_amd_lab."""
+    if tile in PROD_160:
+        return ops.conv_fwd(x, w, bias, y, K, S, Pin, Po, mode=mode, mbits=mbits, tile=tile)
+    ops.lab().conv_fwd(x, w, bias, None, y, K, S, Pin, Po, mode, mbits, tile)
+    return y
 
 
 @pytest.fixture(scope="module")
@@ -32,7 +44,7 @@ def test_padding_helpers(ops):
     assert ops.packed_weight_like(torch.zeros(152, 49, 5, 5), 64, 160).shape == (25, 160, 64)
 
 
-@pytest.mark.parametrize("tile", [0, 36, 64, 65, 128, 130, 256, 384, 385, 386, 387])
+@pytest.mark.parametrize("tile", lab_params([0, 36, 64, 65, 128, 130, 256, 384, 385, 386, 387], PROD_160))
 @pytest.mark.parametrize("B,Cin,Cin_p,K", [(5, 152, 160, 3), (3, 49, 64, 5), (1, 152, 160, 3)])
 def test_conv_fwd_160(ops, cuda_device, tile, B, Cin, Cin_p, K):
     torch.manual_seed(0)
@@ -48,7 +60,7 @@ def test_conv_fwd_160(ops, cuda_device, tile, B, Cin, Cin_p, K):
     bp[:Cout] = b
     y = ops.padded_empty(B, S, 1, Cp, cuda_device)
     mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=cuda_device)
-    ops.conv_fwd(xp, wp, bp, y, K, S, P, 1, mbits=mbits, tile=tile)
+    _conv_fwd(ops, tile, xp, wp, bp, y, K, S, P, 1, mbits=mbits)
     torch.cuda.synchronize()
     out = ops.from_padded(y, 1)
     assert _rel_err(out[:, :Cout], ref) < 1e-2
@@ -56,7 +68,7 @@ def test_conv_fwd_160(ops, cuda_device, tile, B, Cin, Cin_p, K):
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("tile", [0, 36, 64, 65, 130, 128, 384, 385, 386, 387])
+@pytest.mark.parametrize("tile", lab_params([0, 36, 64, 65, 130, 128, 384, 385, 386, 387], PROD_160))
 def test_conv_dgrad_160_bitmask(ops, cuda_device, tile):
     """dgrad with transposed 160-wide weights and the ReLU' bitmask written by
     the forward epilogue == conv2d_input * (y > 0)."""
@@ -74,21 +86,21 @@ def test_conv_dgrad_160_bitmask(ops, cuda_device, tile):
     bp0[:C] = b0
     y = ops.padded_empty(B, S, 1, Cp, cuda_device)
     mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=cuda_device)
-    ops.conv_fwd(ops.to_padded(xin, 1, Cp), wp0, bp0, y, K, S, 1, 1, mbits=mbits, tile=tile)
+    _conv_fwd(ops, tile, ops.to_padded(xin, 1, Cp), wp0, bp0, y, K, S, 1, 1, mbits=mbits)
     yv = ops.from_padded(y, 1)[:, :C]
     ref = torch.nn.grad.conv2d_input((B, C, S, S), w, dz, padding=K // 2) * (yv > 0)
     wf = ops.packed_weight_like(w, Cp, Cp)
     wd = ops.packed_weight_like(w, Cp, Cp, transposed=True)
     ops.pack_weights([w], [wf], [wd])
     dx = ops.padded_empty(B, S, 1, Cp, cuda_device)
-    ops.conv_fwd(ops.to_padded(dz, 1, Cp), wd, None, dx, K, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mbits, tile=tile)
+    _conv_fwd(ops, tile, ops.to_padded(dz, 1, Cp), wd, None, dx, K, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mbits)
     torch.cuda.synchronize()
     out = ops.from_padded(dx, 1)
     assert _rel_err(out[:, :C], ref) < 1e-2
     assert out[:, C:].abs().sum() == 0
 
 
-@pytest.mark.parametrize("variant", [0, 9, pytest.param(5, marks=pytest.mark.lab)])
+@pytest.mark.parametrize("variant", [0, pytest.param(9, marks=pytest.mark.lab), pytest.param(5, marks=pytest.mark.lab)])
 @pytest.mark.parametrize("B,Cin,Cin_p,K,Pin", [(6, 152, 160, 3, 1), (5, 49, 64, 5, 2), (3, 152, 160, 3, 1)])
 def test_conv_wgrad_160(ops, cuda_device, B, Cin, Cin_p, K, Pin, variant):
     """variant 0: per-tap 160x160 / tap-merged 160x64 kernels; 5: the one-kernel-row wgrad."""
@@ -105,7 +117,7 @@ def test_conv_wgrad_160(ops, cuda_device, B, Cin, Cin_p, K, Pin, variant):
     ns = ops.wgrad_splits(B * S * S, K * K // taps)
     slab = torch.full((ns, K * K, Cp, Cin_p), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, Cp, device=cuda_device)
-    if variant == 5:  # the one-kernel-row wgrad: kernel lab
+    if variant != 0:  # 5: the one-kernel-row wgrad, 9: the LDS-ring wgrad (kernel lab)
         ops.lab().conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, Cin if Cin_p == 64 else 0, variant)
     else:
         ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, cin_real=Cin if Cin_p == 64 else 0, variant=variant)

@@ -21,7 +21,7 @@ def _bf(x):
     return x.to(torch.bfloat16).float()
 
 
-PROD_TILES = (0, 36, 37, 64, 65, 128, 130, 256, 384, 385, 386, 387)
+PROD_TILES = (0, 36, 37, 64, 128, 256, 384, 385, 386, 387)
 
 
 def _conv_fwd(ops, tile, x, w, bias, y, K, S, Pin, Po=1, mode=0, mask=None, mbits=None):
@@ -172,7 +172,7 @@ def test_conv_wgrad_line_lab_boards(ops, cuda_device, S, B, variant):
     xp = ops.to_padded(x, 1)
     dzp = ops.to_padded(dz, 1)
     L = ops.lab()
-    t_, per_split, per_cu = (int(v) for v in L.wgrad_plan(C, C, 0, 3, variant))
+    t_, per_split, per_cu = (int(v) for v in L.wgrad_plan(C, C, 0, 3, variant)[:3])
     ns = max(1, min(256 * per_cu // per_split, (B * S * S + 31) // 32 // ops.WGRAD_MIN_STAGES))
     slab = torch.full((ns, 9, C, C), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, C, device=cuda_device)
@@ -460,9 +460,27 @@ def test_production_library_has_no_lab_variants(ops, cuda_device):
     x = ops.padded_empty(1, 19, 1, 64, cuda_device)
     w = torch.zeros(9, 64, 64, dtype=torch.bfloat16, device=cuda_device)
     y = ops.padded_empty(1, 19, 1, 64, cuda_device)
-    with pytest.raises(RuntimeError, match="not a production tiling"):
-        ops.conv_fwd(x, w, torch.zeros(64, device=cuda_device), y, 3, 19, 1, 1, tile=11)
+    for tile in (11, 65, 130):  # 65 / 130: the LDS-ring tiles, retired in round 5
+        with pytest.raises(RuntimeError, match="not a production tiling"):
+            ops.conv_fwd(x, w, torch.zeros(64, device=cuda_device), y, 3, 19, 1, 1, tile=tile)
     assert not hasattr(torch.ops.alphago_amd, "set_conv_tile")
+    # round 5: the packed-tap first layer, the ring wgrad (9) and the first-layer wgrad re-cuts (10-13)
+    # are lab-only; the production op refuses the variants, and the library has no conv_fwd_pk op
+    assert not hasattr(torch.ops.alphago_amd, "conv_fwd_pk")
+    x64 = ops.padded_empty(2, 19, 2, 64, cuda_device)
+    dz = ops.padded_empty(2, 19, 1, 192, cuda_device)
+    slab = torch.zeros(1, 25, 192, 64, device=cuda_device)
+    dbs = torch.zeros(1, 192, device=cuda_device)
+    for variant in (9, 10, 11, 12, 13):
+        with pytest.raises((RuntimeError, ValueError), match="kernel-lab"):
+            torch.ops.alphago_amd.conv_wgrad(x64, dz, slab, dbs, 5, 19, 2, 1, 48, variant)
+    import subprocess
+
+    from alphago_amd import _build
+
+    # the retired packed-tap launcher is not in the production library
+    syms = subprocess.run(["nm", "-D", "-C", _build.hip_path("prod")], capture_output=True, text=True).stdout
+    assert "launch_conv_fwd_pk" not in syms
 
 
 _DEBUG_CHILD = r"""
@@ -581,13 +599,14 @@ def test_winograd_lab_forward(ops, cuda_device, B, S):
 
 
 @pytest.mark.parametrize("B", [1, 4, 16])
-@pytest.mark.parametrize("tile,ring", [(0, "0"), (0, "1"), (65, "1"), (130, "0"), (36, "0"), (37, "0")])
-def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, monkeypatch, B, tile, ring):
+@pytest.mark.parametrize("tile,ring", [(0, "0"), (36, "0"), (37, "0"),
+                                       pytest.param(0, "1", marks=LAB), pytest.param(65, "1", marks=LAB),
+                                       pytest.param(130, "0", marks=LAB)])
+def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, B, tile, ring):
     """Small batches (the reference's -B 16 training and batch-1 search calls): forward with the
-    bitmask, bitmask dgrad and the wgrad the trainer picks (ops.wgrad_config: per-tap splits, or with
-    ALPHAGO_AMD_WGRAD_RING=1 the LDS-ring variant with long splits) vs fp32 conv2d / conv2d_input /
-    conv2d_weight."""
-    monkeypatch.setenv("ALPHAGO_AMD_WGRAD_RING", ring)
+    bitmask, bitmask dgrad and the wgrad the trainer picks (ops.wgrad_config: per-tap splits) vs fp32
+    conv2d / conv2d_input / conv2d_weight.  Lab cases: the LDS-ring tiles 65 / 130 and the ring wgrad
+    (variant 9 with 16-stage splits), retired from the production library in round 5."""
     torch.manual_seed(12)
     S, C = 19, 192
     x = _bf(torch.randn(B, C, S, S, device=cuda_device))
@@ -599,13 +618,16 @@ def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, monkeypatch, B, tile
     xp = ops.to_padded(x, 1)
     y = ops.padded_empty(B, S, 1, C, cuda_device)
     mb = torch.full((B * (S + 2) ** 2 * ops.mbits_words(C),), -1, dtype=torch.int32, device=cuda_device)
-    ops.conv_fwd(xp, wf, b, y, 3, S, 1, 1, mbits=mb, tile=tile)
+    _conv_fwd(ops, tile, xp, wf, b, y, 3, S, 1, 1, mbits=mb)
     ref = F.relu(F.conv2d(x, w, b, padding=1))
     g = _bf(torch.randn(B, C, S, S, device=cuda_device))
     dx = ops.padded_empty(B, S, 1, C, cuda_device)
-    ops.conv_fwd(ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb, tile=tile)
+    _conv_fwd(ops, tile, ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb)
     var, ns = ops.wgrad_config(B * S * S, C, C, 3)
-    assert var == (9 if ring == "1" else 0) and ns > 0
+    if ring == "1":  # the lab's ring wgrad: one workgroup per CU, 16 32-pixel stages per split
+        taps, per_split, _, _ = ops.wgrad_plan(C, C, 3)
+        var, ns = 9, max(1, min(256 // per_split, (B * S * S + 31) // 32 // 16))
+    assert ns > 0
     slab = torch.full((ns, 9, C, C), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, C, device=cuda_device)
     ops.conv_wgrad(xp, ops.to_padded(g, 1), slab, dbs, 3, S, 1, 1, variant=var)
@@ -666,6 +688,7 @@ def test_conv_fwd_splitk(ops, cuda_device, B, S, Cin, Cout, K, ns):
     assert _rel_err(ops.from_padded(dx, 1), ref_dx) < 1e-2
 
 
+@pytest.mark.lab
 @pytest.mark.parametrize("S,B,Cin,Cout,Cout_p", [(19, 5, 48, 192, 192), (19, 3, 49, 152, 160), (9, 7, 48, 192, 192),
                                                  (13, 2, 49, 152, 160), (19, 1, 40, 128, 128)])
 def test_conv_fwd_packed_taps_first_layer(ops, cuda_device, S, B, Cin, Cout, Cout_p):
@@ -734,3 +757,4 @@ def test_sample_moves_distribution(ops, cuda_device, beta):
     via_mask = ops.sample_moves(probs, legal, beta, 11)
     torch.cuda.synchronize()
     assert torch.equal(via_mask, out)
+

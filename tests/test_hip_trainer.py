@@ -231,7 +231,7 @@ def test_hip_trunk_small_boards_match_torch(cuda_device, S, F, L):
 
 @pytest.mark.parametrize("kind,F,C,B", [("policy", 192, 48, 6), ("value", 152, 49, 5), ("policy", 64, 12, 3)])
 def test_fused_sgd_pack_matches_separate_update(cuda_device, monkeypatch, kind, F, C, B):
-    """The fused update (ops.sgd_pack: SGD + bf16 forward / transposed / packed-tap packs in one launch)
+    """The fused update (ops.sgd_pack: SGD + bf16 forward / transposed packs in one launch)
     leaves the same master weights and the same packed copies as sgd_update followed by pack_weights,
     eager and with the device schedule (graph-mode path)."""
     import copy
@@ -243,7 +243,6 @@ def test_fused_sgd_pack_matches_separate_update(cuda_device, monkeypatch, kind, 
     net = PolicyNet(C, filters_per_layer=F, layers=3) if kind == "policy" else ValueNet(C, filters_per_layer=F, layers=3)
     cls = HipPolicyTrainer if kind == "policy" else HipValueTrainer
     trs = []
-    monkeypatch.setenv("ALPHAGO_AMD_PK", "1")  # the packed-tap first-layer pack too
     for fused in ("1", "0"):
         monkeypatch.setenv("ALPHAGO_AMD_FUSED_UPDATE", fused)
         trs.append(cls(copy.deepcopy(net), B, lr=0.05, decay=0.01, device=cuda_device))
@@ -263,37 +262,6 @@ def test_fused_sgd_pack_matches_separate_update(cuda_device, monkeypatch, kind, 
         assert torch.equal(a.wf[l], b.wf[l]), l
         assert torch.equal(a.wd[l], b.wd[l]), l
     assert torch.equal(a._sched_dev, b._sched_dev)
-
-
-@pytest.mark.parametrize("kind,F,C,B", [("policy", 192, 48, 6), ("value", 152, 49, 5)])
-def test_packed_tap_first_layer_trainer_matches(cuda_device, monkeypatch, kind, F, C, B):
-    """ALPHAGO_AMD_PK=1 (first layer on conv_fwd_pk) vs the 64-channel kernel: same loss and gradients
-    up to bf16 summation order."""
-    import copy
-
-    from alphago_amd.models.nets import PolicyNet, ValueNet
-    from alphago_amd.train.engine import HipPolicyTrainer, HipValueTrainer
-
-    torch.manual_seed(4)
-    net = PolicyNet(C, filters_per_layer=F, layers=3) if kind == "policy" else ValueNet(C, filters_per_layer=F, layers=3)
-    cls = HipPolicyTrainer if kind == "policy" else HipValueTrainer
-    trs = []
-    for pk in ("1", "0"):
-        monkeypatch.setenv("ALPHAGO_AMD_PK", pk)
-        trs.append(cls(copy.deepcopy(net), B, lr=0.05, device=cuda_device))
-    assert trs[0].pk0 and not trs[1].pk0
-    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
-    tgt = (torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device) if kind == "policy"
-           else torch.rand(B, device=cuda_device) * 2 - 1)
-    for t in trs:
-        t.compute_grads(planes, tgt)
-    torch.cuda.synchronize()
-    a, b = trs
-    for name in a.fp.names:
-        ga, gb = a.fp.grad_views[name].double().flatten(), b.fp.grad_views[name].double().flatten()
-        if gb.norm() < 1e-6 * b.fp.grad.norm():  # the policy head's scalar bias: softmax rows sum to 1
-            continue
-        assert torch.nn.functional.cosine_similarity(ga, gb, dim=0) > 0.995, name
 
 
 @pytest.mark.parametrize("B,kind", [(4, "policy"), (1, "policy"), (2, "value")])
