@@ -43,7 +43,7 @@ def main():
     ap.add_argument("--data", default="material", choices=["material", "teacher", "random"],
                     help="material (default): tanh of the stone / atari balance, learnable in a few hundred steps; "
                          "teacher: a random-init value teacher's outputs; random: +-1 outcomes (speed only)")
-    ap.add_argument("--quality-steps", type=int, default=600,
+    ap.add_argument("--quality-steps", type=int, default=1600,
                     help="after the clock: this many more steps before the held-out MSE (0: none)")
     ap.add_argument("--optimizer", default=None, choices=["sgd", "momentum", "adam"],
                     help="default: train-value's (train/value.py DEFAULT_OPTIMIZER)")
