@@ -157,7 +157,8 @@ bool ladder_escape_at(const GameState& s, int m) {
 }
 
 // ---------------------------------------------------------------- GPU encoding
-void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder) {
+void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder,
+                  const LadderRecord* ref, LadderRecord* rec) {
   const int np = s.np;
   for (int p = 0; p < np; ++p) board[p] = (int8_t)s.board[p];
   std::memset(ages, 255, np);
@@ -202,11 +203,50 @@ void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* met
     }
     ls.ko = s.ko;
     const int budget = ladder_budget();
+    if (rec) {
+      rec->black = ls.black;
+      rec->white = ls.white;
+      rec->budget = budget;
+      rec->e.clear();
+      rec->reused = rec->read = 0;
+    }
+    // the points where this board and the reference's differ
+    const bool use_ref = ref && ref->budget == budget && !ref->e.empty();
+    lb::BB diff;
+    if (use_ref)
+      for (int i = 0; i < lb::W; ++i)
+        diff.w[i] = (ref->black.w[i] ^ ls.black.w[i]) | (ref->white.w[i] ^ ls.white.w[i]);
+    size_t ri = 0;
     for (int i = 0; i < BW; ++i)
       for (uint64_t w = cand.w[i]; w; w &= w - 1) {
         const int p = i * 64 + __builtin_ctzll(w);
         if (p >= np || s.board[p] != EMPTY || !s.is_legal(p)) continue;
-        ladder[p] = (uint8_t)(lb::ladder_bits_at(ls, p, me, stack, g, budget) & 3);
+        int bits = -1;
+        lb::BB reads;
+        if (use_ref) {  // candidates ascend, so does the reference's list
+          while (ri < ref->e.size() && ref->e[ri].p < p) ++ri;
+          if (ri < ref->e.size() && ref->e[ri].p == p) {
+            const LadderEntry& en = ref->e[ri];
+            uint64_t hit = 0;
+            for (int k = 0; k < lb::W; ++k) hit |= en.reads.w[k] & diff.w[k];
+            if (!hit) {
+              bits = en.bits;
+              reads = en.reads;
+              if (rec) ++rec->reused;
+            }
+          }
+        }
+        if (bits < 0) {
+          if (rec) {
+            lb::bzero(reads);
+            lb::trace_slot() = &reads;
+          }
+          bits = lb::ladder_bits_at(ls, p, me, stack, g, budget);
+          lb::trace_slot() = nullptr;
+          if (rec) ++rec->read;
+        }
+        ladder[p] = (uint8_t)(bits & 3);
+        if (rec) rec->e.push_back({(int16_t)p, (uint8_t)bits, reads});
       }
   }
 }

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "go.h"
+#include "ladder_bb.h"
 
 namespace ag {
 
@@ -42,7 +43,27 @@ int featurize(const GameState& s, const int* fids, int nf, uint8_t* out);
 // board[p] in {-1,0,1}; ages[p] = turns_since plane (0..7) or 255; meta =
 // {ko or -1, player to move}; ladder (optional) bit0 = ladder capture,
 // bit1 = ladder escape (only computed when requested: it is the expensive part).
-void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder);
+//
+// Ladder cache (the MCTS encoder, Forest::leaf_encode): with `rec`, every candidate point's read is
+// recorded with its read set (ladder_bb.h trace_slot) next to the board; with `ref` -- the record of a
+// state with the same player to move, e.g. the leaf's grandparent or an already encoded sibling -- a
+// candidate whose recorded read set holds none of the points where the two boards differ takes the
+// recorded result instead of reading again.  The reuse is exact: the read is a function of the board on
+// its read set (the ko point only decides the root move's legality, which encode_state checks on the
+// state itself first).
+struct LadderEntry {
+  int16_t p;
+  uint8_t bits;  // lb::ladder_bits_at
+  lb::BB reads;  // the board points the read looked at
+};
+struct LadderRecord {
+  lb::BB black, white;
+  int budget = -1;  // the node budget the reads ran with (ladder_budget())
+  std::vector<LadderEntry> e;  // ascending p
+  int reused = 0, read = 0;    // entries taken from the reference / read here
+};
+void encode_state(const GameState& s, int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder,
+                  const LadderRecord* ref = nullptr, LadderRecord* rec = nullptr);
 
 // Ladder reading (paper features; NotImplementedError in the reference
 // preprocessing.py:147-152).  Exposed for tests.

@@ -56,6 +56,37 @@ struct BB {
   uint64_t w[W];
 };
 
+// Read-set tracing (host only; the ladder cache of the MCTS encoder, featurize.cpp): while
+// trace_slot() points at a set, every board point whose content a search reads is added to it --
+// the points color_at tests, the dilation of every chain group_of fills or libs_of counts, and the
+// neighbourhood of the hunter stones frame_init screens.  A search is a deterministic function of
+// those points (plus the root's ko point, which only decides the root move's legality), so a board
+// that differs from the traced one only outside the set gives the same result, bit for bit.
+#if !defined(__HIP_DEVICE_COMPILE__)
+inline BB*& trace_slot() {
+  static thread_local BB* t = nullptr;
+  return t;
+}
+#define LB_TRACE_PT(p)                                           \
+  do {                                                           \
+    if (::lb::BB* t_ = ::lb::trace_slot()) t_->w[(p) >> 6] |= 1ull << ((p) & 63); \
+  } while (0)
+#define LB_TRACE_SET(b)                                          \
+  do {                                                           \
+    if (::lb::BB* t_ = ::lb::trace_slot()) {                     \
+      const ::lb::BB b_ = (b);                                   \
+      for (int i_ = 0; i_ < ::lb::W; ++i_) t_->w[i_] |= b_.w[i_]; \
+    }                                                            \
+  } while (0)
+#else
+#define LB_TRACE_PT(p) \
+  do {                 \
+  } while (0)
+#define LB_TRACE_SET(b) \
+  do {                  \
+  } while (0)
+#endif
+
 LB_HD int popc(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __popcll(x);
@@ -164,7 +195,10 @@ struct LState {
   int ko;  // -1 = none
 };
 
-LB_HD int color_at(const LState& s, int p) { return btest(s.black, p) ? 1 : (btest(s.white, p) ? -1 : 0); }
+LB_HD int color_at(const LState& s, int p) {
+  LB_TRACE_PT(p);
+  return btest(s.black, p) ? 1 : (btest(s.white, p) ? -1 : 0);
+}
 // per-word selects (no reference to one of two register aggregates, which the
 // GPU compiler would materialise in scratch)
 LB_HD BB stones_copy(const LState& s, int c) {
@@ -186,6 +220,7 @@ LB_HD BB group_of(const LState& s, int p, const Geo& g) {
     if (beq(d, grp)) break;
     grp = d;
   }
+  LB_TRACE_SET(dilate(grp, g));
   return grp;
 }
 
@@ -216,6 +251,7 @@ LB_HD BB two_empty_nbrs(const BB& e, const Geo& g) {
 
 LB_HD BB libs_of(const LState& s, const BB& grp, const Geo& g) {
   BB d = dilate(grp, g);
+  LB_TRACE_SET(d);
   for (int i = 0; i < W; ++i) d.w[i] &= ~(s.black.w[i] | s.white.w[i]);
   return d;
 }
@@ -353,6 +389,7 @@ LB_HD int frame_init(Frame& f, const LState& st, const Geo& g, int& visits, int 
   // prey: its liberty, then liberties of adjacent hunter groups in atari
   f.cand[f.nc++] = (int16_t)bfirst(lb);
   BB around = dilate(grp, g);
+  LB_TRACE_SET(dilate(around, g));  // the hunter stones next to the chain and their neighbours
   BB hunters = stones_copy(st, -pc);
   for (int i = 0; i < W; ++i) hunters.w[i] &= around.w[i];
   // A chain holding a stone with two empty neighbours has two liberties: it is

@@ -68,6 +68,9 @@ void Forest::set_root(int t, const GameState& s) {
   tr.nodes.clear();
   tr.nodes.push_back(make_node(-1, PASS, 1.f));
   tr.sims = 0;
+  lad_records_ -= (int64_t)tr.lad.size();
+  tr.lad.clear();
+  tr.lad_rep.clear();
 }
 
 int Forest::select_child(const SearchTree& tr, int u) const {
@@ -239,11 +242,51 @@ void Forest::leaf_features(uint8_t* out, int threads) const {
   });
 }
 
-void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) const {
+void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) {
   int L = (int)pending_.size();
   if (L == 0) return;
   const int np = leaf_state(0).np;
   ensure_pool(threads);  // the forest's persistent pool (set_threads) runs the parts
+  // ladder cache: each leaf's candidate references (grandparent, encoded sibling), looked up before the
+  // parallel encode (which only reads the maps) and the new records committed after it
+  const bool cache = ladder && ladder_cache_;
+  std::vector<const LadderRecord*> ref_gp, ref_sib;
+  if (cache) {
+    if ((int)lad_fresh_.size() < L) lad_fresh_.resize(L);
+    ref_gp.assign(L, nullptr);
+    ref_sib.assign(L, nullptr);
+    for (int i = 0; i < L; ++i) {
+      const SearchTree& tr = trees_[pending_[i].tree];
+      const int pu = tr.nodes[pending_[i].node].parent;
+      if (pu < 0) continue;
+      const int gp = tr.nodes[pu].parent;
+      if (gp >= 0) {
+        auto it = tr.lad.find(gp);
+        if (it != tr.lad.end()) ref_gp[i] = &it->second;
+      }
+      auto rs = tr.lad_rep.find(pu);
+      if (rs != tr.lad_rep.end()) {
+        auto it = tr.lad.find(rs->second);
+        if (it != tr.lad.end()) ref_sib[i] = &it->second;
+      }
+    }
+  }
+  auto pick_ref = [&](int i) -> const LadderRecord* {
+    const LadderRecord* a = ref_gp[i];
+    const LadderRecord* b = ref_sib[i];
+    if (!a || !b) return a ? a : b;
+    // the reference whose board differs from the leaf's in fewer points
+    const GameState& s = leaf_state(i);
+    auto ndiff = [&](const LadderRecord* r) {
+      int d = 0;
+      for (int p = 0; p < s.np; ++p) {
+        const int c = lb::btest(r->black, p) ? BLACK : lb::btest(r->white, p) ? WHITE : EMPTY;
+        d += c != s.board[p];
+      }
+      return d;
+    };
+    return ndiff(b) < ndiff(a) ? b : a;
+  };
   // small chunks claimed dynamically: ladder reads make a few boards far costlier than the rest.  A
   // single tree's leaf batch (tens of boards) goes one board per part so that every pool thread gets
   // work: with 4-board parts a 32-leaf batch kept 8 of 16 threads busy, and on positions with long
@@ -252,7 +295,8 @@ void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* l
   auto work = [&](int c) {
     for (int i = c * kChunk; i < std::min(L, (c + 1) * kChunk); ++i)
       encode_state(leaf_state(i), board + (size_t)i * np, ages + (size_t)i * np, meta + 2 * i,
-                   ladder ? ladder + (size_t)i * np : nullptr);
+                   ladder ? ladder + (size_t)i * np : nullptr, cache ? pick_ref(i) : nullptr,
+                   cache ? &lad_fresh_[i] : nullptr);
   };
   const int nchunks = (L + kChunk - 1) / kChunk;
   if (!ladder) {  // without ladders this is a memcpy-class walk
@@ -260,6 +304,19 @@ void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* l
     return;
   }
   run_parts(nchunks, work);
+  if (!cache) return;
+  for (int i = 0; i < L; ++i) {
+    SearchTree& tr = trees_[pending_[i].tree];
+    const int u = pending_[i].node;
+    lad_reused_ += lad_fresh_[i].reused;
+    lad_read_ += lad_fresh_[i].read;
+    if (lad_records_ >= kLadderRecordCap) continue;
+    auto ins = tr.lad.emplace(u, LadderRecord());
+    if (ins.second) ++lad_records_;
+    std::swap(ins.first->second, lad_fresh_[i]);  // (the fresh slot keeps a vector for the next batch)
+    const int pu = tr.nodes[u].parent;
+    if (pu >= 0) tr.lad_rep.emplace(pu, u);
+  }
 }
 
 void Forest::leaf_masks(uint8_t* out) const {
@@ -458,6 +515,9 @@ void Forest::advance(int t, int move) {
   if (found < 0 || tr.nodes[found].status == 1) {
     tr.nodes.clear();
     tr.nodes.push_back(make_node(-1, PASS, 1.f));
+    lad_records_ -= (int64_t)tr.lad.size();
+    tr.lad.clear();
+    tr.lad_rep.clear();
     return;
   }
   // BFS copy of the reused subtree (children stay contiguous)
@@ -483,6 +543,28 @@ void Forest::advance(int t, int move) {
     }
   }
   tr.nodes.swap(nn);
+  // the ladder cache follows the kept subtree's renumbering; the rest is dropped
+  if (!tr.lad.empty()) {
+    std::unordered_map<int, LadderRecord> lad;
+    std::unordered_map<int, int> rep;
+    std::vector<int> new_of;  // old index -> new (-1: dropped)
+    for (int k = 0; k < (int)old_of.size(); ++k) {
+      if ((int)new_of.size() <= old_of[k]) new_of.resize(old_of[k] + 1, -1);
+      new_of[old_of[k]] = k;
+    }
+    auto nw = [&](int o) { return o >= 0 && o < (int)new_of.size() ? new_of[o] : -1; };
+    for (auto& kv : tr.lad) {
+      const int k = nw(kv.first);
+      if (k >= 0) lad.emplace(k, std::move(kv.second));
+    }
+    for (auto& kv : tr.lad_rep) {
+      const int a = nw(kv.first), b = nw(kv.second);
+      if (a >= 0 && b >= 0) rep.emplace(a, b);
+    }
+    lad_records_ += (int64_t)lad.size() - (int64_t)tr.lad.size();
+    tr.lad.swap(lad);
+    tr.lad_rep.swap(rep);
+  }
 }
 
 // ------------------------------------------------------------------ bindings

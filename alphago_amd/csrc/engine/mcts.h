@@ -18,8 +18,10 @@
 #include <memory>
 #include <random>
 #include <stdexcept>
+#include <unordered_map>
 #include <vector>
 
+#include "featurize.h"
 #include "go.h"
 #include "workpool.h"
 
@@ -84,6 +86,10 @@ struct SearchTree {
   // per-tree stream (rollouts, root noise, temperature sampling): trees are
   // searched by different workers, and the results do not depend on the count
   std::mt19937_64 rng;
+  // ladder cache (leaf_encode): each encoded node's ladder reads, and per expanded node the first of its
+  // children that was encoded (the reference of its siblings)
+  std::unordered_map<int, LadderRecord> lad;
+  std::unordered_map<int, int> lad_rep;
   SearchTree() : root_state(19) {}
 };
 
@@ -136,8 +142,29 @@ class Forest {
   // uint8 features (L, F, n, n) and sensible-move masks (L, n*n); threaded.
   void leaf_features(uint8_t* out, int threads) const;
   void leaf_masks(uint8_t* out) const;
-  // compact GPU-featurizer encoding of the pending leaves (see encode_state)
-  void leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) const;
+  // compact GPU-featurizer encoding of the pending leaves (see encode_state).  With ladders and the
+  // ladder cache on, a leaf's reads are checked against its grandparent's or an encoded sibling's
+  // (whichever board differs in fewer points; same player to move) and only the reads whose read set
+  // the difference touches run again -- bit-exact (featurize.h LadderRecord).
+  void leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads);
+  void set_ladder_cache(bool on) {
+    ladder_cache_ = on;
+    if (!on) clear_ladder_cache();
+  }
+  bool ladder_cache() const { return ladder_cache_; }
+  void clear_ladder_cache() {
+    for (SearchTree& tr : trees_) {
+      tr.lad.clear();
+      tr.lad_rep.clear();
+    }
+    lad_records_ = 0;
+  }
+  // records held, reads taken from a reference, reads run
+  void ladder_cache_stats(int64_t& records, int64_t& reused, int64_t& read) const {
+    records = lad_records_;
+    reused = lad_reused_;
+    read = lad_read_;
+  }
   // priors (L, n*n) float32 (any non-negative scores; renormalised over sensible moves), values (L,);
   // mask (L, n*n) optional sensible-move mask (e.g. from the GPU featurizer) — skips the legality/eye scan
   void apply(const float* priors, const float* values, const uint8_t* mask = nullptr);
@@ -192,6 +219,10 @@ class Forest {
   std::vector<int> fids_;
   int nplanes_ = 0;
   int64_t total_evals_ = 0;
+  bool ladder_cache_ = true;
+  int64_t lad_records_ = 0, lad_reused_ = 0, lad_read_ = 0;
+  static constexpr int64_t kLadderRecordCap = 1 << 18;  // forest-wide (~0.3-1 KB each)
+  std::vector<LadderRecord> lad_fresh_;
   int threads_ = 1;
   mutable std::unique_ptr<WorkPool> pool_;  // threads_ - 1 persistent workers (set_threads)
   void gather_trees(const int* trees, int ntrees, int lpt, std::vector<Leaf>& pend, std::vector<int>& slot_ids,

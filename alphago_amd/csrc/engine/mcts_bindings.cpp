@@ -87,7 +87,7 @@ void bind_mcts(py::module_& m) {
       .def_property_readonly("n_held", &Forest::n_held)
       .def(
           "leaf_encode_into",
-          [](const Forest& f, uintptr_t board, uintptr_t ages, uintptr_t meta, uintptr_t ladder, size_t capacity,
+          [](Forest& f, uintptr_t board, uintptr_t ages, uintptr_t meta, uintptr_t ladder, size_t capacity,
              int threads) {
             int L = f.n_pending();
             if (L == 0) return 0;
@@ -137,6 +137,18 @@ void bind_mcts(py::module_& m) {
           },
           py::arg("priors"), py::arg("values") = py::none(), py::arg("mask") = py::none())
       .def("set_threads", &Forest::set_threads, py::arg("n"))
+      .def_property("ladder_cache", &Forest::ladder_cache, &Forest::set_ladder_cache)
+      .def("clear_ladder_cache", &Forest::clear_ladder_cache)
+      .def("ladder_cache_stats",
+           [](const Forest& f) {
+             int64_t n, reused, read;
+             f.ladder_cache_stats(n, reused, read);
+             py::dict d;
+             d["records"] = n;
+             d["reused"] = reused;
+             d["read"] = read;
+             return d;
+           })
       .def_property("rollout_policy", &Forest::rollout_policy, &Forest::set_rollout_policy)
       .def("add_root_noise", &Forest::add_root_noise, py::arg("tree"), py::arg("alpha") = 0.03,
            py::arg("eps") = 0.25)

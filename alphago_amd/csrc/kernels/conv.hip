@@ -134,6 +134,16 @@ void launch_conv_fwd(const ConvFwdArgs& a_in, int mode, hipStream_t st) {
   ConvFwdArgs a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
+  if (a.tile == 40) {  // weight-stationary small-batch kernel (conv_ws.hip)
+    launch_conv_ws(a, mode, 0, st);
+    return;
+  }
+#ifdef AGK_KERNEL_LAB
+  if (a.tile > 40 && a.tile < 48) {  // its probes (which part sets the per-chunk time)
+    launch_conv_ws(a, mode, 0, st, a.tile - 40);
+    return;
+  }
+#endif
   if (mode == MODE_BIAS_RELU) launch_fwd_mode<MODE_BIAS_RELU>(a, st);
   else if (mode == MODE_MASK) launch_fwd_mode<MODE_MASK>(a, st);
   else if (mode == MODE_MASKBITS) launch_fwd_mode<MODE_MASKBITS>(a, st);

@@ -197,6 +197,9 @@ void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 // packed-tap first-layer forward (bias + ReLU, optional bitmask): cpt 8-channel chunks per tap
 void launch_conv_fwd_pk(const ConvFwdArgs& a, int cpt, hipStream_t st);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
+// weight-stationary small-batch conv (conv_ws.hip, tile code 40): modes 0 / 2 / 3; target_wgs <= 0: 256
+void launch_conv_ws(const ConvFwdArgs& a, int mode, int target_wgs, hipStream_t st, int probe = 0);
+bool conv_ws_supported(int Cout, int Cin, int K);
 int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 int wgrad_tap_group(int Cout, int Cin, int K, int variant);  // taps per wgrad workgroup (tap-merged 64-wide c tiles)
 // one-kernel-row wgrad (conv_wgrad_row.hip): geometry code (0 = not applicable), grid per split, launch

@@ -14,9 +14,9 @@ void conv_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>& bia
   check_dev("conv_fwd", x, w, bias, mask, y, mbits);
   // production tilings only: 0 = automatic, or a fixed 64 / 128 / 256 / 384-pixel tile (385: 384 with the
   // LDS-DMA issue spread through the MFMAs; 386 / 387: 385 / 384 with the chunk-outer K order)
-  TORCH_CHECK(tile == 0 || tile == 36 || tile == 37 || tile == 64 || tile == 128 || tile == 256 || tile == 384 ||
-                  tile == 385 || tile == 386 || tile == 387,
-              "conv_fwd tile ", tile, " is not a production tiling (0, 36, 37, 64, 128, 256, 384-387); kernel-lab "
+  TORCH_CHECK(tile == 0 || tile == 36 || tile == 37 || tile == 40 || tile == 64 || tile == 128 || tile == 256 ||
+                  tile == 384 || tile == 385 || tile == 386 || tile == 387,
+              "conv_fwd tile ", tile, " is not a production tiling (0, 36, 37, 40, 64, 128, 256, 384-387); kernel-lab "
               "variants are in torch.ops.alphago_amd_lab (alphago_amd.ops.lab())");
   conv_fwd_impl(x, w, bias, mask, y, K, S, Pin, Po, mode, mbits, (int)tile);
 }
@@ -541,6 +541,10 @@ int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) {
 
 // {taps per workgroup, workgroups per split, resident workgroups per CU, threads per workgroup} of the
 // production wgrad
+bool conv_ws_supported(int64_t cout, int64_t cin, int64_t K) {
+  return agk::conv_ws_supported((int)cout, (int)cin, (int)K);
+}
+
 std::vector<int64_t> wgrad_plan(int64_t cout, int64_t cin, int64_t cin_real, int64_t K, int64_t variant) {
   int o[4];
   agk::wgrad_plan((int)cout, (int)cin, (int)(cin_real > 0 && cin_real < cin ? cin_real : cin), (int)K, (int)variant, o);
@@ -769,6 +773,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("wgrad_tap_group(int cout, int cin, int K) -> int", &wgrad_tap_group);
   m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant=0) -> int[]", &wgrad_plan);
+  m.def("conv_ws_supported(int cout, int cin, int K) -> bool", &conv_ws_supported);
   m.def("selftest_bad_launch() -> ()", &selftest_bad_launch);
   m.def("is_debug_build() -> bool", []() -> bool {
 #ifdef AGK_DEBUG

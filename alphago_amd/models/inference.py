@@ -136,6 +136,11 @@ class HipTrunkInference:
         M = B * S * S
         bk.sk = [1 if (self.precision == "fp8" and B >= self.fp8_min_batch) else
                  ops.splitk_nsplit(M, self.Fp, self.C0p if l == 0 else self.Fp, self.K[l]) for l in range(self.L)]
+        # ... or the weight-stationary kernel (tile 40) where it applies (it replaces split-K there)
+        bk.wst = [self.precision != "fp8" or B < self.fp8_min_batch for _ in range(self.L)]
+        bk.wst = [bk.wst[l] and ops.ws_applies(M, self.Fp, self.C0p if l == 0 else self.Fp, self.K[l])
+                  for l in range(self.L)]
+        bk.sk = [1 if bk.wst[l] else bk.sk[l] for l in range(self.L)]
         bk.ws = torch.empty(max(bk.sk) * M * self.Fp, device=dev) if max(bk.sk) > 1 else None
         if self.precision == "fp8":
             bk.X08 = torch.zeros(bk.X0.shape, dtype=torch.uint8, device=dev)
@@ -181,7 +186,9 @@ class HipTrunkInference:
         x, pin = bk.X0, self.P0
         for l in range(self.L):
             y = bk.Y[l % 2]
-            if bk.sk[l] > 1:
+            if bk.wst[l]:
+                ops.conv_fwd(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1, tile=40)
+            elif bk.sk[l] > 1:
                 ops.conv_fwd_splitk(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1, ops.MODE_BIAS_RELU,
                                     None, bk.ws, bk.sk[l])
             else:

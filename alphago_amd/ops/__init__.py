@@ -152,6 +152,22 @@ def splitk_nsplit(M: int, cout_p: int, cin_p: int, K: int, target_wgs: int = SPL
     return max(1, min(nk // 3, -(-target_wgs // tiles), 64))
 
 
+# Weight-stationary small-batch conv (tile 40, conv_ws.hip): the output-channel slice's weights stay in
+# the workgroup's VGPRs while 16-pixel chunks stream past.  Automatic up to these output-pixel counts
+# (graph-timed chains of 11 layers with distinct weights, scripts/r5/ws_bench.py, profiles/r5/README.md):
+# 192-wide layers up to B = 8 (10.7 / 11.5 / 15.4 us per layer at B = 1 / 4 / 8 vs 20.3 / 19.5 / 19.4 on
+# the automatic tile; equal at B = 16), 160-wide up to B = 32 (9.4 .. 18.5 us vs 20.2 .. 20.6).
+# ALPHAGO_AMD_WS=0: off.
+WS_MAX_M = {192: 8 * 361, 160: 32 * 361}
+
+
+def ws_applies(M: int, cout_p: int, cin_p: int, K: int) -> bool:
+    """Whether a conv of M output pixels runs on the weight-stationary kernel (tile 40)."""
+    if os.environ.get("ALPHAGO_AMD_WS", "1") == "0" or M > WS_MAX_M.get(conv_n_tile(cout_p), 0):
+        return False
+    return bool(_ops().conv_ws_supported(cout_p, cin_p, K))
+
+
 def conv_fwd_splitk(x, w_packed, bias, y, K: int, S: int, Pin: int, Po: int, mode: int, mbits, ws, nsplit: int):
     """conv_fwd on the 32-pixel tile with its K loop split over ``nsplit`` workgroups per tile (fp32
     partials in ``ws``, >= nsplit * M * Cout floats) and one finishing pass: modes 0 (bias + ReLU,

@@ -293,6 +293,16 @@ class HipConvTrainer:
                 self.sk_fwd[l] = ops.splitk_nsplit(M, self.Fp, cin_p, self.K[l])
                 if l > 0:
                     self.sk_dg[l] = ops.splitk_nsplit(M, self.Fp, self.Fp, self.K[l])
+        # small batches: the weight-stationary kernel (tile 40) where it applies, instead of split-K
+        self.ws_fwd = [False] * self.L
+        self.ws_dg = [False] * self.L
+        if conv_tile == 0 and self.precision == "bf16" and not self.lab_tile:
+            for l in range(self.L):
+                cin_p = self.C0p if l == 0 else self.Fp
+                if ops.ws_applies(M, self.Fp, cin_p, self.K[l]):
+                    self.ws_fwd[l], self.sk_fwd[l] = True, 1
+                if l > 0 and ops.ws_applies(M, self.Fp, self.Fp, self.K[l]):
+                    self.ws_dg[l], self.sk_dg[l] = True, 1
         sk_max = max(self.sk_fwd + self.sk_dg)
         self._sk_ws = torch.empty(sk_max * M * self.Fp, device=dev) if sk_max > 1 else None
         # Split-K reduce on a side stream (serial backward only): the memory-bound reduce of
@@ -486,6 +496,8 @@ class HipConvTrainer:
         if self.lab_tile and self.K[l] == 3:
             ops.lab().conv_fwd(x, self.wf[l], self.bias_p[l], None, self.Y[l], 3, self.S, pin, 1, 0, mbits,
                                self.lab_tile)
+        elif self.ws_fwd[l]:
+            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1, mbits=mbits, tile=40)
         elif self.sk_fwd[l] > 1:
             ops.conv_fwd_splitk(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1,
                                 ops.MODE_BIAS_RELU, mbits, self._sk_ws, self.sk_fwd[l])
@@ -625,6 +637,9 @@ class HipConvTrainer:
                 elif self.lab_tile and self.K[l] == 3:  # kernel-lab A/B (see __init__)
                     ops.lab().conv_fwd(self.DZ[l], self.wd[l], None, None, self.DZ[l - 1], 3, self.S, 1, 1,
                                        ops.MODE_MASKBITS, self.MBITS[l - 1], self.lab_tile)
+                elif self.ws_dg[l]:  # small batches: weight-stationary bitmask dgrad
+                    ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
+                                 mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=40)
                 elif self.sk_dg[l] > 1:  # small batches: split-K bitmask dgrad
                     ops.conv_fwd_splitk(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                         ops.MODE_MASKBITS, self.MBITS[l - 1], self._sk_ws, self.sk_dg[l])

@@ -213,8 +213,8 @@ def train_cli(argv=None):
     p.add_argument("--init", default=DEFAULT_INIT, choices=["keras", "he"],
                    help="weights of a model JSON without a weights file: keras = uniform(+-0.05) (value.py:17,21), "
                         "he = fan-in scaled uniform (models/nets.py he_uniform_)")
-    p.add_argument("--fp8-bf16-layers", default="0,11",
-                   help="--precision fp8: trunk layers kept in bf16 (per-layer precision; '' = all fp8)")
+    p.add_argument("--fp8-bf16-layers", default="",
+                   help="--precision fp8: trunk layers kept in bf16, e.g. 0,11 (per-layer precision; default: all fp8, at parity with fp32 under Adam, profiles/r5)")
     p.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])

@@ -758,3 +758,54 @@ def test_sample_moves_distribution(ops, cuda_device, beta):
     torch.cuda.synchronize()
     assert torch.equal(via_mask, out)
 
+
+
+@pytest.mark.parametrize("B,S,Cin,Cout,K", [(1, 19, 192, 192, 3), (4, 19, 192, 192, 3), (16, 19, 192, 192, 3),
+                                            (33, 19, 192, 192, 3), (16, 19, 64, 192, 5), (3, 19, 64, 192, 5),
+                                            (16, 19, 160, 160, 3), (2, 19, 160, 160, 3), (5, 9, 128, 128, 3),
+                                            (7, 13, 64, 64, 3)])
+def test_conv_weight_stationary(ops, cuda_device, B, S, Cin, Cout, K):
+    """Weight-stationary small-batch conv (tile 40, conv_ws.hip: a workgroup's output-channel slice held
+    in VGPRs across its waves' K ranges, 16-pixel chunks streamed past): bias + ReLU forward vs fp32
+    conv2d with its ReLU' bitmask equal to the 32-pixel tile's (up to pre-activations that round across
+    zero), the bitmask dgrad vs conv2d_input, and no write outside the interior."""
+    torch.manual_seed(40 + B)
+    P = K // 2
+    real = 48 if (Cin == 64 and K == 5) else (152 if Cin == 160 else Cin)
+    oreal = 152 if Cout == 160 else Cout
+    x = _bf(torch.randn(B, real, S, S, device=cuda_device))
+    w = _bf(torch.randn(oreal, real, K, K, device=cuda_device) * 0.05)
+    b = torch.randn(oreal, device=cuda_device) * 0.1
+    bp = torch.zeros(Cout, device=cuda_device)
+    bp[:oreal] = b
+    ref = F.relu(F.conv2d(x, w, b, padding=P))
+    wf = ops.packed_weight_like(w, Cin, Cout)
+    ops.pack_weights([w.contiguous()], [wf])
+    xp = ops.to_padded(x, P, Cin)
+    words = ops.mbits_words(Cout)
+    mb = torch.full((B * (S + 2) ** 2 * words,), -1, dtype=torch.int32, device=cuda_device)
+    mb_ref = mb.clone()
+    y = ops.padded_empty(B, S, 1, Cout, cuda_device)
+    yr = ops.padded_empty(B, S, 1, Cout, cuda_device)
+    ops.conv_fwd(xp, wf, bp, y, K, S, P, 1, mbits=mb, tile=40)
+    ops.conv_fwd(xp, wf, bp, yr, K, S, P, 1, mbits=mb_ref, tile=64 if Cout == 160 else 36)
+    torch.cuda.synchronize()
+    out = ops.from_padded(y, 1)
+    assert _rel_err(out[:, :oreal], ref) < 1e-2
+    assert (out[:, oreal:] == 0).all()
+    assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
+    assert (mb != mb_ref).float().mean().item() < 1e-3
+    if Cin != Cout or K != 3:
+        return
+    # bitmask dgrad (mode 3) with the transposed pack
+    wd = ops.packed_weight_like(w, Cin, Cout, True)
+    ops.pack_weights([w.contiguous()], [wf], [wd])
+    g = _bf(torch.randn(B, oreal, S, S, device=cuda_device))
+    dx = ops.padded_empty(B, S, 1, Cin, cuda_device)
+    ops.conv_fwd(ops.to_padded(g, 1, Cout), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb_ref, tile=40)
+    torch.cuda.synchronize()
+    yrf = ops.from_padded(yr, 1)[:, :real]
+    ref_dx = torch.nn.grad.conv2d_input((B, real, S, S), w, g, padding=1) * (yrf > 0)
+    dxo = ops.from_padded(dx, 1)
+    assert _rel_err(dxo[:, :real], ref_dx) < 1e-2
+    assert (dxo[:, real:] == 0).all()

@@ -280,6 +280,7 @@ def test_splitk_small_batch_trainer_matches(cuda_device, monkeypatch, B, kind):
     else:
         net, C, cls = ValueNet(49, filters_per_layer=152, layers=4), 49, HipValueTrainer
     trs = []
+    monkeypatch.setenv("ALPHAGO_AMD_WS", "0")  # the weight-stationary tile would take these batches
     for sk in ("1", "0"):
         monkeypatch.setenv("ALPHAGO_AMD_SPLITK", sk)
         trs.append(cls(copy.deepcopy(net), B, lr=0.05, device=cuda_device))
@@ -348,3 +349,44 @@ def test_fused_optimizer_matches_torch_update(cuda_device, optimizer, nesterov):
     for l in range(3):
         assert torch.equal(tr.wf[l], wf[l]) and torch.equal(tr.wd[l], wd[l]), l
 
+
+@pytest.mark.parametrize("B,kind", [(1, "policy"), (8, "policy"), (2, "value"), (16, "value")])
+def test_weight_stationary_trainer_matches(cuda_device, monkeypatch, B, kind):
+    """Small batches run the forward and the bitmask dgrad on the weight-stationary tile (tile 40,
+    conv_ws.hip): same loss and gradients as the 32-pixel tiles (ALPHAGO_AMD_WS=0, no split-K) up to
+    summation order, and the weights after a step."""
+    import copy
+
+    from alphago_amd.models.nets import PolicyNet, ValueNet
+    from alphago_amd.train.engine import HipPolicyTrainer, HipValueTrainer
+
+    torch.manual_seed(8)
+    if kind == "policy":
+        net, C, cls = PolicyNet(48, filters_per_layer=192, layers=4), 48, HipPolicyTrainer
+    else:
+        net, C, cls = ValueNet(49, filters_per_layer=152, layers=4), 49, HipValueTrainer
+    trs = []
+    for ws in ("1", "0"):
+        monkeypatch.setenv("ALPHAGO_AMD_WS", ws)
+        monkeypatch.setenv("ALPHAGO_AMD_SPLITK", ws)
+        trs.append(cls(copy.deepcopy(net), B, lr=0.05, device=cuda_device))
+    assert all(trs[0].ws_fwd[1:]) and all(trs[0].ws_dg[1:]) and not any(trs[1].ws_fwd + trs[1].ws_dg)
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    if kind == "policy":
+        tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    else:
+        tgt = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
+    for t in trs:
+        t.compute_grads(planes, tgt)
+    torch.cuda.synchronize()
+    a, b = trs
+    assert abs(a.loss.sum().item() - b.loss.sum().item()) < 1e-2 * abs(b.loss.sum().item())
+    for name in a.fp.names:
+        ga, gb = a.fp.grad_views[name].double().flatten(), b.fp.grad_views[name].double().flatten()
+        if gb.norm() < 1e-6 * b.fp.grad.norm():
+            continue
+        assert torch.nn.functional.cosine_similarity(ga, gb, dim=0) > 0.995, name
+    for t in trs:
+        t.apply_update()
+    torch.cuda.synchronize()
+    assert (a.fp.flat - b.fp.flat).abs().max().item() < 5e-3
