@@ -139,8 +139,8 @@ void launch_conv_fwd(const ConvFwdArgs& a_in, int mode, hipStream_t st) {
     return;
   }
 #ifdef AGK_KERNEL_LAB
-  if (a.tile > 40 && a.tile < 48) {  // its probes (which part sets the per-chunk time)
-    launch_conv_ws(a, mode, 0, st, a.tile - 40);
+  if (a.tile > 1000 && a.tile < 1064) {  // its probes (which part sets the layer's time)
+    launch_conv_ws(a, mode, 0, st, a.tile - 1000);
     return;
   }
 #endif

@@ -21,8 +21,10 @@
 // l % 16.
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
+
+#include <algorithm>
 #include <stdexcept>
+#include <vector>
 #include <string>
 
 #include "conv_common.h"
@@ -44,6 +46,10 @@ struct WsParams {
   int k;       // slices per XCD (a divisor of slices); P = 8 k / slices XCDs share a slice set
   int P;
   int gper;    // chunk groups per XCD = ceil(ngrp / P); grid = 8 * k * gper
+  int NR;      // RING: input-row slots (the rows of two consecutive chunks fit)
+  int RS;      // RING: bytes per slot = HPi * PST
+  int PST;     // RING: bytes per pixel in a slot = Cin * 2 + 16 (the pad spreads a fragment read over
+               // all LDS banks)
 };
 
 typedef __attribute__((ext_vector_type(4))) unsigned ws_u32x4;
@@ -66,13 +72,15 @@ constexpr unsigned WS_OOB = 0x80000000u;  // a byte offset past every buffer's e
 }  // namespace
 
 // NWV MFMA waves split the K-steps (KW each) and NE epilogue waves finish the chunks (1 workgroup per CU).
-// The roles are wave-uniform and run separate loops that meet at one barrier per chunk, so the MFMA
-// waves' vector-memory queue holds only their activation loads -- never the epilogue's output stores --
-// and their two-chunks-ahead prefetch is waited on with an exact count.
-// PROBE (kernel lab only, tiles 41..47): bit 0 = no activation loads after the first chunks, bit 1 = no
-// MFMA, bit 2 = no epilogue work -- which part sets the per-chunk time
-template <int NBLK, int KW, int NWV, int NE, int MODE, int PROBE = 0>
+// The roles are wave-uniform and run separate loops that meet at one barrier per chunk (plus one after
+// the prologue and one at the end), so the MFMA waves' vector-memory queue never holds the epilogue's
+// output stores.  RING: activations through an LDS ring of input rows (RM: most new rows per chunk,
+// IPR: 16-byte row units per lane); else straight from global memory, two chunks ahead.
+// PROBE (kernel lab only, tiles 1000 + PROBE): bit 1 = no MFMA, bit 2 = no epilogue work, bit 3 = no
+// weight loads -- which part sets the layer's time (round-5 probes: profiles/r5/README.md)
+template <int NBLK, int KW, int NWV, int NE, int MODE, bool RING, int PROBE = 0>
 __global__ __launch_bounds__(64 * (NWV + NE), 1) void conv_ws_kernel(ConvFwdArgs a, WsParams p) {
+  constexpr int RM = 6, IPR = 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63;
   const int wave = wave_id();
@@ -99,48 +107,21 @@ __global__ __launch_bounds__(64 * (NWV + NE), 1) void conv_ws_kernel(ConvFwdArgs
     // ---------------- MFMA waves
     const int row = lane & 15, kq = lane >> 4;
     const int s0 = wave * KW;  // first K-step of this wave
-    // the slice's weights, resident for the workgroup's life (A operands)
+    // the slice's weights, resident for the workgroup's life (A operands): in the weight-stationary
+    // order (ws_pack_kernel) each fragment is one contiguous KB, 16 bytes per lane -- from the standard
+    // [tap][Cout][Cin] pack each load instruction touched 16 half-used cache lines (round-5 probe: 4.6 us
+    // of a 15 us layer at B = 16)
     bf16x8 wa[NBLK][KW];
+    const __bf16* wsl = a.w + (size_t)(slice * NWV + wave) * NBLK * KW * 512 + lane * 8;
 #pragma unroll
-    for (int b = 0; b < NBLK; ++b) {
-      const int gi = 4 * b + (row >> 2);  // group of 4 channels within the slice
-      const int w = slice * p.WS + gi / p.NB;
-      const int n = ws_word_base(w, p.BN) + 16 * (gi % p.NB) + (row & 3);
+    for (int b = 0; b < NBLK; ++b)
 #pragma unroll
       for (int kk = 0; kk < KW; ++kk) {
-        const int s = s0 + kk;
-        const int t = s / p.CS, c0 = (s - t * p.CS) * 32;
-        wa[b][kk] = *(const bf16x8*)(a.w + ((size_t)t * a.Cout + n) * a.Cin + c0 + 8 * kq);
+        if constexpr (PROBE & 8) wa[b][kk] = bf16x8{};
+        else wa[b][kk] = *(const bf16x8*)(wsl + (b * KW + kk) * 512);
       }
-    }
-    // per-K-step byte offsets of this wave (tap shift + channel chunk): wave-uniform, scalar operands
-    int koff[KW];
-#pragma unroll
-    for (int kk = 0; kk < KW; ++kk) {
-      const int s = s0 + kk;
-      const int t = s / p.CS, c0 = (s - t * p.CS) * 32;
-      const int kh = t / a.K, kw = t - kh * a.K;
-      koff[kk] = __builtin_amdgcn_readfirstlane(((kh * a.HPi + kw) * a.Cin + c0) * 2);
-    }
-    const __amdgpu_buffer_rsrc_t xr =
-        ws_rsrc(a.x, (long long)(a.M / SS) * a.HPi * a.HPi * a.Cin * 2);
-    // chunk c's B fragments (past the last chunk / pixel: any valid pixel -- the epilogue drops it)
-    auto load_chunk = [&](int c, bf16x8 (&xb)[KW]) {
-      int m = c * 16 + row;
-      m = m < a.M ? m : a.M - 1;
-      const int bb = fdiv(m, a.divSS);
-      const int rem = m - bb * SS;
-      const int ii = fdiv(rem, a.divS);
-      const int jj = rem - ii * a.S;
-      const int base = (((bb * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + 8 * kq) * 2;
-#pragma unroll
-      for (int kk = 0; kk < KW; ++kk)
-        xb[kk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, base, koff[kk], 0));
-    };
-    // one chunk: prefetch chunk j + 2 (always issued, clamped, so the wait count is static), MFMA, partials
-    auto body = [&](int j, bf16x8 (&cur)[KW], bf16x8 (&fill)[KW]) {
-      if constexpr (!(PROBE & 1)) load_chunk(c_begin + j + 2, fill);
-      __builtin_amdgcn_sched_barrier(0);  // the prefetch leaves before this chunk's MFMAs, not after
+    const __amdgpu_buffer_rsrc_t xr = ws_rsrc(a.x, (long long)(a.M / SS) * a.HPi * a.HPi * a.Cin * 2);
+    auto mfma_chunk = [&](int j, const bf16x8 (&cur)[KW]) {
       f32x4 acc[NBLK];
 #pragma unroll
       for (int b = 0; b < NBLK; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -158,17 +139,138 @@ __global__ __launch_bounds__(64 * (NWV + NE), 1) void conv_ws_kernel(ConvFwdArgs
       for (int b = 0; b < NBLK; ++b) pb[(wave * NBLK + b) * 64 + lane] = acc[b];
       __syncthreads();  // chunk j's partials complete (the epilogue waves read them next)
     };
-    bf16x8 x0[KW], x1[KW], x2[KW];  // three chunk buffers in rotation: chunk j lives in x[j % 3]
-    load_chunk(c_begin, x0);
-    load_chunk(c_begin + 1, x1);
-    int j = 0;
-    for (; j + 3 <= nc; j += 3) {
-      body(j, x0, x2);
-      body(j + 1, x1, x0);
-      body(j + 2, x2, x1);
+
+    if constexpr (RING) {
+      // Activations through an LDS ring of padded input rows: the waves copy each row the chunks need
+      // once, as whole 16-byte runs of the row (a row of the padded NHWC input is contiguous), and every
+      // wave then reads its B fragments (16 pixels x 64 bytes per K-step) from LDS.  Reading them from
+      // global memory directly, each load instruction touched 16 half-used cache lines.
+      uint8_t* ring = (uint8_t*)(bitw + 2 * 16 * p.WS);
+      const int rowbytes = a.HPi * a.Cin * 2, upp = a.Cin / 8, U = a.HPi * upp;
+      int u_src[IPR], u_dst[IPR];
+#pragma unroll
+      for (int i = 0; i < IPR; ++i) {  // this lane's 16-byte units of a row load
+        const int u = wave * 64 + lane + 64 * NWV * i;
+        const int uc = u < U ? u : U - 1;
+        u_src[i] = uc * 16;
+        u_dst[i] = u < U ? (uc / upp) * p.PST + (uc - (uc / upp) * upp) * 16 : -1;
+      }
+      // per-K-step tap row and in-row byte offset (tap column, channel chunk): wave-uniform
+      int kh_[KW], kofs[KW];
+#pragma unroll
+      for (int kk = 0; kk < KW; ++kk) {
+        const int s = s0 + kk;
+        const int t = s / p.CS, c0 = (s - t * p.CS) * 32;
+        const int kh = t / a.K, kw = t - kh * a.K;
+        kh_[kk] = __builtin_amdgcn_readfirstlane(kh);
+        kofs[kk] = __builtin_amdgcn_readfirstlane(kw * p.PST + c0 * 2);
+      }
+      auto row_of = [&](int m) -> int {  // padded input row of pixel m's first tap row
+        const int bb = fdiv(m, a.divSS);
+        const int ii = fdiv(m - bb * SS, a.divS);
+        return bb * a.HPi + ii + a.offi;
+      };
+      auto g0 = [&](int c) { return __builtin_amdgcn_readfirstlane(row_of(c * 16)); };
+      auto g1 = [&](int c) {
+        const int m = c * 16 + 15 < a.M ? c * 16 + 15 : a.M - 1;
+        return __builtin_amdgcn_readfirstlane(row_of(m) + a.K - 1);
+      };
+      auto load_row = [&](int G, ws_u32x4 (&v)[IPR]) {
+#pragma unroll
+        for (int i = 0; i < IPR; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, u_src[i], G * rowbytes, 0);
+      };
+      auto write_row = [&](int G, const ws_u32x4 (&v)[IPR]) {
+        uint8_t* d = ring + (G % p.NR) * p.RS;
+#pragma unroll
+        for (int i = 0; i < IPR; ++i)
+          if (u_dst[i] >= 0) *(ws_u32x4*)(d + u_dst[i]) = v[i];
+      };
+      // prologue: the rows of the first two chunks
+      int loaded = g1(c_begin + (nc > 1 ? 1 : 0));
+      for (int G = g0(c_begin); G <= loaded; ++G) {
+        ws_u32x4 v[IPR];
+        load_row(G, v);
+        write_row(G, v);
+      }
+      __syncthreads();
+      ws_u32x4 stage[RM][IPR];
+      int npend = 0, pend_lo = 0;
+      for (int j = 0; j < nc; ++j) {
+        const int c = c_begin + j;
+        // a. the rows loaded during the previous chunk (chunk j + 1's new rows) into their slots: no wave
+        // still reads those slots (the ring holds chunk j's and j + 1's rows at once; launch_conv_ws)
+#pragma unroll
+        for (int r = 0; r < RM; ++r)
+          if (r < npend) write_row(pend_lo + r, stage[r]);
+        // b. chunk j + 2's new rows into registers: written at the next chunk, read two chunks on
+        npend = 0;
+        if (j + 2 < nc) {
+          const int h = g1(c + 2);
+          pend_lo = loaded + 1;
+          npend = h - loaded;
+          loaded = h;
+#pragma unroll
+          for (int r = 0; r < RM; ++r)
+            if (r < npend) load_row(pend_lo + r, stage[r]);
+        }
+        // c. this chunk's B fragments from the ring (past the last pixel: any valid pixel)
+        const int m = c * 16 + row < a.M ? c * 16 + row : a.M - 1;
+        const int bb = fdiv(m, a.divSS);
+        const int rem = m - bb * SS;
+        const int ii = fdiv(rem, a.divS);
+        const int jj = rem - ii * a.S;
+        const int gs = (bb * a.HPi + ii + a.offi) % p.NR;
+        const uint8_t* cb = ring + (jj + a.offi) * p.PST + kq * 16;
+        bf16x8 xb[KW];
+#pragma unroll
+        for (int kk = 0; kk < KW; ++kk) {
+          const int sl = gs + kh_[kk] < p.NR ? gs + kh_[kk] : gs + kh_[kk] - p.NR;
+          xb[kk] = *(const bf16x8*)(cb + sl * p.RS + kofs[kk]);
+        }
+        mfma_chunk(j, xb);
+      }
+    } else {
+      // Activations straight from global memory, two chunks ahead (the 160-wide shape: its partials leave
+      // no LDS for a ring)
+      int koff[KW];  // per-K-step byte offsets (tap shift + channel chunk): wave-uniform, scalar operands
+#pragma unroll
+      for (int kk = 0; kk < KW; ++kk) {
+        const int s = s0 + kk;
+        const int t = s / p.CS, c0 = (s - t * p.CS) * 32;
+        const int kh = t / a.K, kw = t - kh * a.K;
+        koff[kk] = __builtin_amdgcn_readfirstlane(((kh * a.HPi + kw) * a.Cin + c0) * 2);
+      }
+      auto load_chunk = [&](int c, bf16x8 (&xb)[KW]) {  // (past the last pixel: any valid pixel)
+        int m = c * 16 + row;
+        m = m < a.M ? m : a.M - 1;
+        const int bb = fdiv(m, a.divSS);
+        const int rem = m - bb * SS;
+        const int ii = fdiv(rem, a.divS);
+        const int jj = rem - ii * a.S;
+        const int base = (((bb * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + 8 * kq) * 2;
+#pragma unroll
+        for (int kk = 0; kk < KW; ++kk)
+          xb[kk] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, base, koff[kk], 0));
+      };
+      // one chunk: prefetch chunk j + 2 (always issued, clamped, so the wait count is static), MFMA
+      auto body = [&](int j, bf16x8 (&cur)[KW], bf16x8 (&fill)[KW]) {
+        load_chunk(c_begin + j + 2, fill);
+        __builtin_amdgcn_sched_barrier(0);  // the prefetch leaves before this chunk's MFMAs, not after
+        mfma_chunk(j, cur);
+      };
+      bf16x8 x0[KW], x1[KW], x2[KW];  // three chunk buffers in rotation: chunk j lives in x[j % 3]
+      load_chunk(c_begin, x0);
+      load_chunk(c_begin + 1, x1);
+      __syncthreads();  // (the ring variant's prologue barrier: the epilogue waves count it)
+      int j = 0;
+      for (; j + 3 <= nc; j += 3) {
+        body(j, x0, x2);
+        body(j + 1, x1, x0);
+        body(j + 2, x2, x1);
+      }
+      if (j < nc) body(j, x0, x2);
+      if (j + 1 < nc) body(j + 1, x1, x0);
     }
-    if (j < nc) body(j, x0, x2);
-    if (j + 1 < nc) body(j + 1, x1, x0);
     __syncthreads();  // the epilogue waves' last-chunk barrier
   } else {
     // ---------------- epilogue waves: item (pixel it % 16, group it / 16) of every chunk, IPT per thread
@@ -212,6 +314,7 @@ __global__ __launch_bounds__(64 * (NWV + NE), 1) void conv_ws_kernel(ConvFwdArgs
     if constexpr (MODE == MODE_MASKBITS) load_mw(c_begin, mw_cur);
     if constexpr (MODE == MODE_BIAS_RELU)
       for (int k = et; k < 32 * p.WS; k += 64 * NE) bitw[k] = 0u;
+    __syncthreads();  // the MFMA waves' prologue
     // write chunk c's assembled bitmask words (lanes < 16 * WS; others and c < c_begin: dropped), clear them
     auto flush_bits = [&](int c, int buf) {
       const int k = et < 16 * p.WS ? et : 16 * p.WS - 1;
@@ -299,10 +402,90 @@ bool conv_ws_supported(int Cout, int Cin, int K) {
   return ws_shape(Cout, Cin, K, nblk, kw, bn);
 }
 
-template <int NBLK, int KW, int NWV, int NE, int PROBE = 0>
-static void launch_ws_t(const ConvFwdArgs& a, int mode, const WsParams& p, hipStream_t st) {
-  // partials of two chunks + the bitmask words being assembled
-  const int smem = 2 * NWV * NBLK * 64 * 16 + 2 * 16 * p.WS * 4;
+// Weight-stationary order of a standard (tap, Cout, Cin) bf16 pack: fragment (slice, wave, n-block, K-step)
+// is one KB, lane l's 16 bytes at l * 16 -- rows / K of v_mfma_f32_16x16x32_bf16's A operand as
+// conv_ws_kernel's MFMA waves hold it (row channel from the bitmask word geometry, see the kernel).
+__global__ __launch_bounds__(256) void ws_pack_kernel(WsPackArgs args) {
+  const WsPackJob& j = args.job[blockIdx.y];
+  const int nb = j.bn / 32;
+  const long units = (long)j.slices * j.nwv * j.nblk * j.kw * 64;
+  for (long u = (long)blockIdx.x * 256 + threadIdx.x; u < units; u += (long)gridDim.x * 256) {
+    const int lane = (int)(u & 63);
+    long blk = u >> 6;
+    const int kk = (int)(blk % j.kw);
+    blk /= j.kw;
+    const int b = (int)(blk % j.nblk);
+    blk /= j.nblk;
+    const int wave = (int)(blk % j.nwv);
+    const int slice = (int)(blk / j.nwv);
+    const int row = lane & 15, kq = lane >> 4;
+    const int gi = 4 * b + (row >> 2);
+    const int w = slice * j.ws + gi / nb;
+    const int n = ws_word_base(w, j.bn) + 16 * (gi % nb) + (row & 3);
+    const int s = wave * j.kw + kk, cs = j.Cin / 32;
+    const int t = s / cs, c0 = (s - t * cs) * 32;
+    *(bf16x8*)(j.dst + u * 8) = *(const bf16x8*)(j.src + ((size_t)t * j.Cout + n) * j.Cin + c0 + 8 * kq);
+  }
+}
+
+void launch_ws_pack(const std::vector<WsPackJob>& jobs_in, hipStream_t st) {
+  for (size_t i0 = 0; i0 < jobs_in.size(); i0 += kMaxWsPackJobs) {
+    WsPackArgs args{};
+    args.n = (int)std::min(jobs_in.size() - i0, (size_t)kMaxWsPackJobs);
+    long most = 0;
+    for (int i = 0; i < args.n; ++i) {
+      WsPackJob j = jobs_in[i0 + i];
+      if (!ws_shape(j.Cout, j.Cin, j.K, j.nblk, j.kw, j.bn))
+        throw std::invalid_argument("ws_pack: no weight-stationary shape for Cout " + std::to_string(j.Cout) +
+                                    " Cin " + std::to_string(j.Cin) + " K " + std::to_string(j.K));
+      j.nwv = j.K * j.K * (j.Cin / 32) / j.kw;
+      j.ws = 4 * j.nblk / (j.bn / 32);
+      j.slices = (j.Cout / j.bn) * 8 / j.ws;
+      args.job[i] = j;
+      most = std::max(most, (long)j.slices * j.nwv * j.nblk * j.kw * 64);
+    }
+    const dim3 grid((unsigned)std::min((most + 255) / 256, 1024L), args.n);
+    hipLaunchKernelGGL(ws_pack_kernel, grid, dim3(256), 0, st, args);
+  }
+}
+
+// The input-row window of the ring: slots for the rows two consecutive chunks read (NR) and the most
+// new rows one chunk adds (RM), from a scan of one period of the chunk / image pattern (16 c mod S^2)
+struct RingGeo {
+  int nr, rm;
+};
+static RingGeo ring_geometry(int S, int HPi, int offi, int K) {
+  const int SS = S * S;
+  auto row_of = [&](long m) { return (int)((m / SS) * HPi + (m % SS) / S + offi); };
+  auto g0 = [&](long c) { return row_of(16 * c); };
+  auto g1 = [&](long c) { return row_of(16 * c + 15) + K - 1; };
+  RingGeo r{0, 0};
+  for (long c = 0; c <= SS + 1; ++c) {
+    r.nr = std::max(r.nr, g1(c + 1) - g0(c) + 1);
+    r.rm = std::max(r.rm, g1(c + 1) - g1(c));
+  }
+  return r;
+}
+
+template <int NBLK, int KW, int NWV, int NE, bool RING, int PROBE = 0>
+static void launch_ws_t(const ConvFwdArgs& a, int mode, WsParams p, hipStream_t st) {
+  // partials of two chunks + the bitmask words being assembled (+ the input-row ring)
+  int smem = 2 * NWV * NBLK * 64 * 16 + 2 * 16 * p.WS * 4;
+  if constexpr (RING) {
+    static thread_local int key[4] = {-1, -1, -1, -1};
+    static thread_local RingGeo geo;
+    if (key[0] != a.S || key[1] != a.HPi || key[2] != a.offi || key[3] != a.K) {
+      geo = ring_geometry(a.S, a.HPi, a.offi, a.K);
+      key[0] = a.S, key[1] = a.HPi, key[2] = a.offi, key[3] = a.K;
+    }
+    p.PST = a.Cin * 2 + 16;
+    p.RS = a.HPi * p.PST;
+    p.NR = geo.nr;
+    smem += p.NR * p.RS;
+    if (geo.rm > 6 || a.HPi * a.Cin / 8 > 64 * NWV || smem > 160 * 1024)
+      throw std::invalid_argument("conv_fwd tile 40: the input-row ring does not fit this geometry (S " +
+                                  std::to_string(a.S) + ", Cin " + std::to_string(a.Cin) + ")");
+  }
   const dim3 grid(8 * p.k * p.gper), block(64 * (NWV + NE));
   auto go = [&](auto kern) {
     static const hipError_t e =
@@ -311,13 +494,13 @@ static void launch_ws_t(const ConvFwdArgs& a, int mode, const WsParams& p, hipSt
     hipLaunchKernelGGL(kern, grid, block, smem, st, a, p);
   };
   if constexpr (PROBE != 0) {
-    if (mode != MODE_BIAS_RELU) throw std::invalid_argument("conv_fwd tiles 41..47: mode 0 only");
-    go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_BIAS_RELU, PROBE>);
+    if (mode != MODE_BIAS_RELU) throw std::invalid_argument("conv_fwd tiles 1000+: mode 0 only");
+    go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_BIAS_RELU, RING, PROBE>);
     return;
   }
-  if (mode == MODE_BIAS_RELU) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_BIAS_RELU>);
-  else if (mode == MODE_MASKBITS) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_MASKBITS>);
-  else if (mode == MODE_NONE) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_NONE>);
+  if (mode == MODE_BIAS_RELU) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_BIAS_RELU, RING>);
+  else if (mode == MODE_MASKBITS) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_MASKBITS, RING>);
+  else if (mode == MODE_NONE) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_NONE, RING>);
   else throw std::invalid_argument("conv_fwd tile 40: modes 0 (bias + ReLU), 2 (none) and 3 (bitmask dgrad)");
 }
 
@@ -363,25 +546,24 @@ void launch_conv_ws(const ConvFwdArgs& a, int mode, int target_wgs, hipStream_t 
   // 128-wide 3x3 (36) and 64-wide 3x3 (18); NE epilogue waves (NWV + NE <= 16)
 #ifdef AGK_KERNEL_LAB
   if (probe) {
-    if (!(nblk == 3 && kw == 6 && nwv == 9)) throw std::invalid_argument("conv_fwd tiles 41..47: 192 x 192 3x3 only");
+    if (!(nblk == 3 && kw == 6 && nwv == 9)) throw std::invalid_argument("conv_fwd tiles 1000+: 192 x 192 3x3 only");
     switch (probe) {
-      case 1: launch_ws_t<3, 6, 9, 3, 1>(a, mode, p, st); return;
-      case 2: launch_ws_t<3, 6, 9, 3, 2>(a, mode, p, st); return;
-      case 3: launch_ws_t<3, 6, 9, 3, 3>(a, mode, p, st); return;
-      case 4: launch_ws_t<3, 6, 9, 3, 4>(a, mode, p, st); return;
-      case 5: launch_ws_t<3, 6, 9, 3, 5>(a, mode, p, st); return;
-      case 6: launch_ws_t<3, 6, 9, 3, 6>(a, mode, p, st); return;
-      default: launch_ws_t<3, 6, 9, 3, 7>(a, mode, p, st); return;
+      case 2: launch_ws_t<3, 6, 9, 3, true, 2>(a, mode, p, st); return;
+      case 4: launch_ws_t<3, 6, 9, 3, true, 4>(a, mode, p, st); return;
+      case 6: launch_ws_t<3, 6, 9, 3, true, 6>(a, mode, p, st); return;
+      case 8: launch_ws_t<3, 6, 9, 3, true, 8>(a, mode, p, st); return;
+      case 14: launch_ws_t<3, 6, 9, 3, true, 14>(a, mode, p, st); return;
+      default: throw std::invalid_argument("conv_fwd tiles 1000 + probe: probes 2, 4, 6, 8, 14");
     }
   }
 #else
-  if (probe) throw std::invalid_argument("conv_fwd tiles 41..47: kernel-lab build only");
+  if (probe) throw std::invalid_argument("conv_fwd tiles 1000+: kernel-lab build only");
 #endif
-  if (nblk == 3 && kw == 6 && nwv == 9) launch_ws_t<3, 6, 9, 3>(a, mode, p, st);
-  else if (nblk == 3 && kw == 5 && nwv == 10) launch_ws_t<3, 5, 10, 2>(a, mode, p, st);
-  else if (nblk == 5 && kw == 3 && nwv == 15) launch_ws_t<5, 3, 15, 1>(a, mode, p, st);
-  else if (nblk == 1 && kw == 6 && nwv == 6) launch_ws_t<1, 6, 6, 1>(a, mode, p, st);
-  else if (nblk == 1 && kw == 6 && nwv == 3) launch_ws_t<1, 6, 3, 1>(a, mode, p, st);
+  if (nblk == 3 && kw == 6 && nwv == 9) launch_ws_t<3, 6, 9, 3, true>(a, mode, p, st);
+  else if (nblk == 3 && kw == 5 && nwv == 10) launch_ws_t<3, 5, 10, 2, true>(a, mode, p, st);
+  else if (nblk == 5 && kw == 3 && nwv == 15) launch_ws_t<5, 3, 15, 1, false>(a, mode, p, st);
+  else if (nblk == 1 && kw == 6 && nwv == 6) launch_ws_t<1, 6, 6, 1, true>(a, mode, p, st);
+  else if (nblk == 1 && kw == 6 && nwv == 3) launch_ws_t<1, 6, 3, 1, true>(a, mode, p, st);
   else throw std::invalid_argument("conv_fwd tile 40: no instantiation for this shape");
 }
 

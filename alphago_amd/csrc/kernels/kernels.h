@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "common.h"
 
 namespace agk {
@@ -199,6 +201,19 @@ void launch_conv_fwd_pk(const ConvFwdArgs& a, int cpt, hipStream_t st);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 // weight-stationary small-batch conv (conv_ws.hip, tile code 40): modes 0 / 2 / 3; target_wgs <= 0: 256
 void launch_conv_ws(const ConvFwdArgs& a, int mode, int target_wgs, hipStream_t st, int probe = 0);
+// weight-stationary order of standard (tap, Cout, Cin) bf16 packs (conv_ws.hip; tile 40 reads it)
+struct WsPackJob {
+  const __bf16* src;
+  __bf16* dst;
+  int Cout, Cin, K;
+  int nblk, kw, bn, nwv, ws, slices;  // filled by launch_ws_pack
+};
+constexpr int kMaxWsPackJobs = 32;
+struct WsPackArgs {
+  WsPackJob job[kMaxWsPackJobs];
+  int n;
+};
+void launch_ws_pack(const std::vector<WsPackJob>& jobs, hipStream_t st);
 bool conv_ws_supported(int Cout, int Cin, int K);
 int wgrad_stage_pixels();  // pixels per wgrad pipeline stage (units of ksteps_per_split)
 int wgrad_tap_group(int Cout, int Cin, int K, int variant);  // taps per wgrad workgroup (tap-merged 64-wide c tiles)

@@ -541,6 +541,31 @@ int64_t wgrad_tap_group(int64_t cout, int64_t cin, int64_t K) {
 
 // {taps per workgroup, workgroups per split, resident workgroups per CU, threads per workgroup} of the
 // production wgrad
+// src: standard (T, Cout, Cin) bf16 packs; dst: same-shape tensors receiving the weight-stationary order
+// (conv_fwd tile 40 reads it; T = K*K or K*K + 1)
+void ws_pack(at::TensorList src, at::TensorList dst) {
+  check_dev("ws_pack", src, dst);
+  TORCH_CHECK(src.size() == dst.size(), "ws_pack: list sizes");
+  std::vector<agk::WsPackJob> jobs;
+  for (size_t i = 0; i < src.size(); ++i) {
+    CHECK_BF16(src[i]); CHECK_BF16(dst[i]); CHECK_CONTIG(src[i]); CHECK_CONTIG(dst[i]);
+    TORCH_CHECK(src[i].dim() == 3 && src[i].sizes() == dst[i].sizes(), "ws_pack: (T, Cout, Cin) pairs of one shape");
+    const int T = (int)src[i].size(0);
+    int K = 1;
+    while ((K + 1) * (K + 1) <= T) ++K;
+    agk::WsPackJob j{};
+    j.src = reinterpret_cast<const __bf16*>(src[i].data_ptr());
+    j.dst = reinterpret_cast<__bf16*>(dst[i].data_ptr());
+    j.Cout = (int)src[i].size(1);
+    j.Cin = (int)src[i].size(2);
+    j.K = K;
+    jobs.push_back(j);
+  }
+  if (jobs.empty()) return;
+  agk::launch_ws_pack(jobs, cur_stream());
+  launch_check("ws_pack");
+}
+
 bool conv_ws_supported(int64_t cout, int64_t cin, int64_t K) {
   return agk::conv_ws_supported((int)cout, (int)cin, (int)K);
 }
@@ -774,6 +799,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("wgrad_tap_group(int cout, int cin, int K) -> int", &wgrad_tap_group);
   m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant=0) -> int[]", &wgrad_plan);
   m.def("conv_ws_supported(int cout, int cin, int K) -> bool", &conv_ws_supported);
+  m.def("ws_pack(Tensor[] src, Tensor(a!)[] dst) -> ()");
   m.def("selftest_bad_launch() -> ()", &selftest_bad_launch);
   m.def("is_debug_build() -> bool", []() -> bool {
 #ifdef AGK_DEBUG
@@ -802,6 +828,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("head_backward", &head_backward);
   m.impl("value_out", &value_out);
   m.impl("pack_weights", &pack_weights);
+  m.impl("ws_pack", &ws_pack);
   m.impl("sgd_update", &sgd_update);
   m.impl("comm_proxy", &comm_proxy);
   m.impl("sgd_update_sched", &sgd_update_sched);

@@ -63,6 +63,10 @@ class HipTrunkInference:
         # packed on the engine's device whatever device the module's parameters are on
         self.wf = [ops.packed_weight_like(tr.weights[l], self.C0p if l == 0 else self.Fp, self.Fp, device=dev)
                    for l in range(self.L)]
+        # weight-stationary copies (tile 40, small buckets) of the layers that kernel covers
+        self.wf_ws = [ops.ws_packed_like(self.wf[l]) if ops.conv_ws_supported(self.Fp, self.C0p if l == 0 else self.Fp,
+                                                                              self.K[l]) else None
+                      for l in range(self.L)]
         self.bias_p = [torch.zeros(self.Fp, device=dev) for _ in range(self.L)]
         self.head_w = torch.zeros(self.F, device=dev)
         self.head_b = torch.zeros(1, device=dev)
@@ -104,6 +108,8 @@ class HipTrunkInference:
         tr = self.net.trunk
         ws = [w.detach().to(self.device, torch.float32).contiguous() for w in tr.weights]
         ops.pack_weights(ws, self.wf)
+        ops.ws_pack([self.wf[l] for l in range(self.L) if self.wf_ws[l] is not None],
+                    [w for w in self.wf_ws if w is not None])
         for l in range(self.L):
             self.bias_p[l][:self.F].copy_(tr.biases[l].detach())
         self.head_w.copy_(self.net.head_w.detach().view(-1))
@@ -138,8 +144,8 @@ class HipTrunkInference:
                  ops.splitk_nsplit(M, self.Fp, self.C0p if l == 0 else self.Fp, self.K[l]) for l in range(self.L)]
         # ... or the weight-stationary kernel (tile 40) where it applies (it replaces split-K there)
         bk.wst = [self.precision != "fp8" or B < self.fp8_min_batch for _ in range(self.L)]
-        bk.wst = [bk.wst[l] and ops.ws_applies(M, self.Fp, self.C0p if l == 0 else self.Fp, self.K[l])
-                  for l in range(self.L)]
+        bk.wst = [bk.wst[l] and self.wf_ws[l] is not None and
+                  ops.ws_applies(M, self.Fp, self.C0p if l == 0 else self.Fp, self.K[l]) for l in range(self.L)]
         bk.sk = [1 if bk.wst[l] else bk.sk[l] for l in range(self.L)]
         bk.ws = torch.empty(max(bk.sk) * M * self.Fp, device=dev) if max(bk.sk) > 1 else None
         if self.precision == "fp8":
@@ -187,7 +193,7 @@ class HipTrunkInference:
         for l in range(self.L):
             y = bk.Y[l % 2]
             if bk.wst[l]:
-                ops.conv_fwd(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1, tile=40)
+                ops.conv_fwd(x, self.wf_ws[l], self.bias_p[l], y, self.K[l], self.S, pin, 1, tile=40)
             elif bk.sk[l] > 1:
                 ops.conv_fwd_splitk(x, self.wf[l], self.bias_p[l], y, self.K[l], self.S, pin, 1, ops.MODE_BIAS_RELU,
                                     None, bk.ws, bk.sk[l])

@@ -153,12 +153,30 @@ def splitk_nsplit(M: int, cout_p: int, cin_p: int, K: int, target_wgs: int = SPL
 
 
 # Weight-stationary small-batch conv (tile 40, conv_ws.hip): the output-channel slice's weights stay in
-# the workgroup's VGPRs while 16-pixel chunks stream past.  Automatic up to these output-pixel counts
-# (graph-timed chains of 11 layers with distinct weights, scripts/r5/ws_bench.py, profiles/r5/README.md):
-# 192-wide layers up to B = 8 (10.7 / 11.5 / 15.4 us per layer at B = 1 / 4 / 8 vs 20.3 / 19.5 / 19.4 on
-# the automatic tile; equal at B = 16), 160-wide up to B = 32 (9.4 .. 18.5 us vs 20.2 .. 20.6).
-# ALPHAGO_AMD_WS=0: off.
-WS_MAX_M = {192: 8 * 361, 160: 32 * 361}
+# the workgroup's VGPRs (read once, in the weight-stationary order of ws_pack) while 16-pixel chunks stream
+# past through an LDS ring of input rows.  Automatic up to these output-pixel counts (graph-timed chains of
+# 11 layers with distinct weights, scripts/r5/ws_bench.py, profiles/r5/README.md): 192-wide layers
+# 6.7 / 9.8 / 12.6 / 18.7 us at B = 1 / 8 / 16 / 32 vs 20.3 / 19.4 / 19.9 / 22.6 on the automatic tile
+# (30.1 vs 25.5 at B = 64), 160-wide 7.2 .. 16.7 us vs 20.1 .. 20.5.  ALPHAGO_AMD_WS=0: off.
+WS_MAX_M = {192: 32 * 361, 160: 32 * 361}
+
+
+def ws_pack(srcs, dsts) -> None:
+    """Weight-stationary order (what conv_fwd tile 40 reads) of standard (T, Cout, Cin) bf16 packs into
+    same-shape tensors, all pairs in one launch."""
+    srcs, dsts = list(srcs), list(dsts)
+    if srcs:
+        _ops().ws_pack(srcs, dsts)
+
+
+def ws_packed_like(w_packed: torch.Tensor) -> torch.Tensor:
+    """A tensor for the weight-stationary copy of a standard bf16 pack (``ws_pack``)."""
+    return torch.empty_like(w_packed)
+
+
+def conv_ws_supported(cout_p: int, cin_p: int, K: int) -> bool:
+    """Whether the weight-stationary kernel (tile 40) has an instantiation for this layer shape."""
+    return bool(_ops().conv_ws_supported(cout_p, cin_p, K))
 
 
 def ws_applies(M: int, cout_p: int, cin_p: int, K: int) -> bool:

@@ -303,6 +303,9 @@ class HipConvTrainer:
                     self.ws_fwd[l], self.sk_fwd[l] = True, 1
                 if l > 0 and ops.ws_applies(M, self.Fp, self.Fp, self.K[l]):
                     self.ws_dg[l], self.sk_dg[l] = True, 1
+        # their weights in the weight-stationary order (ops.ws_pack after every update, repack())
+        self.wf_ws = [ops.ws_packed_like(self.wf[l]) if self.ws_fwd[l] else None for l in range(self.L)]
+        self.wd_ws = [ops.ws_packed_like(self.wd[l]) if self.ws_dg[l] else None for l in range(self.L)]
         sk_max = max(self.sk_fwd + self.sk_dg)
         self._sk_ws = torch.empty(sk_max * M * self.Fp, device=dev) if sk_max > 1 else None
         # Split-K reduce on a side stream (serial backward only): the memory-bound reduce of
@@ -466,6 +469,10 @@ class HipConvTrainer:
         ws = [self.fp.views["w%d" % l] for l in range(self.L)]
         if bf16:
             ops.pack_weights(ws, self.wf, self.wd)
+        # the weight-stationary copies of the small-batch layers (from the bf16 packs, however written)
+        src = [self.wf[l] for l in range(self.L) if self.wf_ws[l] is not None]
+        src += [self.wd[l] for l in range(self.L) if self.wd_ws[l] is not None]
+        ops.ws_pack(src, [w for w in self.wf_ws + self.wd_ws if w is not None])
         if self.precision == "fp8":
             ops.fp8_weight_scales(ws, self.wscale8, self.scales8)
             # every e4m3 pack of the step (forward, and the transposed dgrad packs) in ONE launch
@@ -497,7 +504,8 @@ class HipConvTrainer:
             ops.lab().conv_fwd(x, self.wf[l], self.bias_p[l], None, self.Y[l], 3, self.S, pin, 1, 0, mbits,
                                self.lab_tile)
         elif self.ws_fwd[l]:
-            ops.conv_fwd(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1, mbits=mbits, tile=40)
+            ops.conv_fwd(x, self.wf_ws[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1, mbits=mbits,
+                         tile=40)
         elif self.sk_fwd[l] > 1:
             ops.conv_fwd_splitk(x, self.wf[l], self.bias_p[l], self.Y[l], self.K[l], self.S, pin, 1,
                                 ops.MODE_BIAS_RELU, mbits, self._sk_ws, self.sk_fwd[l])
@@ -638,7 +646,7 @@ class HipConvTrainer:
                     ops.lab().conv_fwd(self.DZ[l], self.wd[l], None, None, self.DZ[l - 1], 3, self.S, 1, 1,
                                        ops.MODE_MASKBITS, self.MBITS[l - 1], self.lab_tile)
                 elif self.ws_dg[l]:  # small batches: weight-stationary bitmask dgrad
-                    ops.conv_fwd(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
+                    ops.conv_fwd(self.DZ[l], self.wd_ws[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,
                                  mode=ops.MODE_MASKBITS, mbits=self.MBITS[l - 1], tile=40)
                 elif self.sk_dg[l] > 1:  # small batches: split-K bitmask dgrad
                     ops.conv_fwd_splitk(self.DZ[l], self.wd[l], None, self.DZ[l - 1], self.K[l], self.S, 1, 1,

@@ -168,6 +168,9 @@ def main():
     ev = getattr(trainer, "comm_events", None)
     if ev:  # exposed all-reduce per step, max over ranks
         comm = agdist.all_reduce_max(sum(a.elapsed_time(b) for a, b in ev) / len(ev))
+    # per-rank device memory (the PyTorch caching allocator's peak reservation: weights, optimizer state,
+    # activations, teacher pool, graph pools; RCCL's own buffers are outside it), max over ranks
+    hbm_gib = agdist.all_reduce_max(torch.cuda.max_memory_reserved(dev) / 2 ** 30) if dev.type == "cuda" else 0.0
     n = env.world_size
     stats = torch.stack([loss_sum, corr_sum]).double()
     agdist.all_reduce_sum_(stats)
@@ -199,6 +202,7 @@ def main():
             "rank_ms_per_step": rank_ms,
             "allreduce_exposed_ms_per_step": None if comm is None else round(comm, 3),
             "pool_build_s": round(pool_s, 1),
+            "hbm_peak_gib_per_rank": round(hbm_gib, 2),
             "config": {
                 "model": "SL policy net (%d-layer, %d filters, %d planes)" % (args.layers, args.filters, args.planes),
                 "global_batch": args.batch * n,

@@ -19,22 +19,27 @@ for C, K, Cin in [(c, 3, c) for c in (int(v) for v in os.environ.get("WS_WIDTHS"
         wfs = [ops.packed_weight_like(w, Cin, C) for w in ws]
         wds = [ops.packed_weight_like(w, Cin, C, True) for w in ws]
         ops.pack_weights(ws, wfs, wds)
+        wfs_ws = [ops.ws_packed_like(w) for w in wfs]
+        wds_ws = [ops.ws_packed_like(w) for w in wds]
+        ops.ws_pack(wfs + wds, wfs_ws + wds_ws)
         b = torch.randn(C, device=dev) * 0.1
         xs = [ops.padded_empty(B, S, 1, C, dev) for _ in range(2)]
         xs[0].normal_()
         mb = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(C), dtype=torch.int32, device=dev)
         res = {"C": C, "B": B}
         for tile in [int(v) for v in os.environ.get("WS_TILES", "0,40").split(",")]:
-            for mode in (("fwd",) if tile > 40 else ("fwd", "dgrad")):
+            for mode in (("fwd",) if tile > 1000 else ("fwd", "dgrad")):
                 def chain():
                     for i in range(11):
-                        if tile > 40:  # kernel-lab probes of tile 40 (forward only)
-                            ops.lab().conv_fwd(xs[i % 2], wfs[i], b, None, xs[(i + 1) % 2], K, S, 1, 1, 0, mb, tile)
+                        if tile > 1000:  # kernel-lab probes of tile 40 (forward only)
+                            ops.lab().conv_fwd(xs[i % 2], wfs_ws[i], b, None, xs[(i + 1) % 2], K, S, 1, 1, 0, mb,
+                                               tile)
                         elif mode == "fwd":
-                            ops.conv_fwd(xs[i % 2], wfs[i], b, xs[(i + 1) % 2], K, S, 1, 1, mbits=mb, tile=tile)
+                            ops.conv_fwd(xs[i % 2], wfs_ws[i] if tile == 40 else wfs[i], b, xs[(i + 1) % 2], K, S, 1,
+                                         1, mbits=mb, tile=tile)
                         else:
-                            ops.conv_fwd(xs[i % 2], wds[i], None, xs[(i + 1) % 2], K, S, 1, 1, mode=ops.MODE_MASKBITS,
-                                         mbits=mb, tile=tile)
+                            ops.conv_fwd(xs[i % 2], wds_ws[i] if tile == 40 else wds[i], None, xs[(i + 1) % 2], K, S,
+                                         1, 1, mode=ops.MODE_MASKBITS, mbits=mb, tile=tile)
                 chain()
                 torch.cuda.synchronize()
                 g = torch.cuda.CUDAGraph()

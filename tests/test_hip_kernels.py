@@ -763,7 +763,8 @@ def test_sample_moves_distribution(ops, cuda_device, beta):
 @pytest.mark.parametrize("B,S,Cin,Cout,K", [(1, 19, 192, 192, 3), (4, 19, 192, 192, 3), (16, 19, 192, 192, 3),
                                             (33, 19, 192, 192, 3), (16, 19, 64, 192, 5), (3, 19, 64, 192, 5),
                                             (16, 19, 160, 160, 3), (2, 19, 160, 160, 3), (5, 9, 128, 128, 3),
-                                            (7, 13, 64, 64, 3)])
+                                            (7, 13, 64, 64, 3), (64, 19, 192, 192, 3), (4, 9, 192, 192, 3),
+                                            (16, 13, 192, 192, 3), (64, 13, 160, 160, 3), (1, 9, 64, 192, 5)])
 def test_conv_weight_stationary(ops, cuda_device, B, S, Cin, Cout, K):
     """Weight-stationary small-batch conv (tile 40, conv_ws.hip: a workgroup's output-channel slice held
     in VGPRs across its waves' K ranges, 16-pixel chunks streamed past): bias + ReLU forward vs fp32
@@ -787,7 +788,9 @@ def test_conv_weight_stationary(ops, cuda_device, B, S, Cin, Cout, K):
     mb_ref = mb.clone()
     y = ops.padded_empty(B, S, 1, Cout, cuda_device)
     yr = ops.padded_empty(B, S, 1, Cout, cuda_device)
-    ops.conv_fwd(xp, wf, bp, y, K, S, P, 1, mbits=mb, tile=40)
+    wws = ops.ws_packed_like(wf)
+    ops.ws_pack([wf], [wws])  # tile 40 reads the weight-stationary order
+    ops.conv_fwd(xp, wws, bp, y, K, S, P, 1, mbits=mb, tile=40)
     ops.conv_fwd(xp, wf, bp, yr, K, S, P, 1, mbits=mb_ref, tile=64 if Cout == 160 else 36)
     torch.cuda.synchronize()
     out = ops.from_padded(y, 1)
@@ -800,9 +803,12 @@ def test_conv_weight_stationary(ops, cuda_device, B, S, Cin, Cout, K):
     # bitmask dgrad (mode 3) with the transposed pack
     wd = ops.packed_weight_like(w, Cin, Cout, True)
     ops.pack_weights([w.contiguous()], [wf], [wd])
+    wdws = ops.ws_packed_like(wd)
+    ops.ws_pack([wd], [wdws])
     g = _bf(torch.randn(B, oreal, S, S, device=cuda_device))
     dx = ops.padded_empty(B, S, 1, Cin, cuda_device)
-    ops.conv_fwd(ops.to_padded(g, 1, Cout), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb_ref, tile=40)
+    ops.conv_fwd(ops.to_padded(g, 1, Cout), wdws, None, dx, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb_ref,
+                 tile=40)
     torch.cuda.synchronize()
     yrf = ops.from_padded(yr, 1)[:, :real]
     ref_dx = torch.nn.grad.conv2d_input((B, real, S, S), w, g, padding=1) * (yrf > 0)
