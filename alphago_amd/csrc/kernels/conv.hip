@@ -254,9 +254,9 @@ static void launch_wgrad_taps(const ConvWgradArgs& a, hipStream_t st) {
 }
 
 int wgrad_tap_group(int Cout, int Cin, int K, int variant) {
-  const bool c64 = Cin != 160 && Cin % 192 != 0 && Cin % 128 != 0;
+  const bool c64 = (Cin != 160 && Cin % 192 != 0 && Cin % 128 != 0) || variant == kWgradSmall;
   (void)Cout;
-  return (c64 && variant == 0 && (K == 3 || K == 5)) ? K : 1;
+  return (c64 && (variant == 0 || variant == kWgradSmall) && (K == 3 || K == 5)) ? K : 1;
 }
 
 #ifdef AGK_KERNEL_LAB
@@ -364,6 +364,13 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[4])
     return;
   }
 #endif
+  if (variant == kWgradSmall) {  // small batches: 64 x 64 tiles, tap-merged kernel rows (launch_conv_wgrad)
+    out[0] = wgrad_tap_group(Cout, Cin, K, variant);
+    out[1] = (K * K / out[0]) * (Cout / 64) * (Cin / 64);
+    out[2] = 2;
+    out[3] = 512;
+    return;
+  }
   // per-tap kernel: tap-merged rows for 64-wide c tiles, else one tap; two workgroups per CU
   const int taps = wgrad_tap_group(Cout, Cin, K, (variant >= 5 && variant <= 13) ? 0 : variant);
   const bool c48 = cin_real <= 48 && Cin == 64;
@@ -413,6 +420,15 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
     a.variant = 0;
   }
 #endif
+  if (a.variant == kWgradSmall) {
+    // small batches (ops.wgrad_config): 64 x 64 output tiles with the kernel row's taps merged -- three
+    // times the workgroups per pixel split of a 192 -> 192 layer
+    if (a.Cout % 64 || a.Cin % 64 || a.cin_real != a.Cin || (a.K != 3 && a.K != 5))
+      throw std::invalid_argument("conv_wgrad: the small-batch tiles need 64-multiple widths and a 3x3 / 5x5 kernel");
+    a.variant = 0;
+    launch_wgrad_t<64, 64>(a, st);
+    return;
+  }
   const bool n192 = a.Cout % 192 == 0, c192 = a.Cin % 192 == 0;
   const bool n128 = a.Cout % 128 == 0, c128 = a.Cin % 128 == 0;
   if (a.Cout == 160) {  // value net (152 filters padded to 160)

@@ -201,6 +201,8 @@ void launch_conv_fwd_pk(const ConvFwdArgs& a, int cpt, hipStream_t st);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
 // weight-stationary small-batch conv (conv_ws.hip, tile code 40): modes 0 / 2 / 3; target_wgs <= 0: 256
 void launch_conv_ws(const ConvFwdArgs& a, int mode, int target_wgs, hipStream_t st, int probe = 0);
+// conv_wgrad's small-batch plan (64 x 64 tap-merged tiles; ops.wgrad_config picks it)
+constexpr int kWgradSmall = 14;
 // weight-stationary order of standard (tap, Cout, Cin) bf16 packs (conv_ws.hip; tile 40 reads it)
 struct WsPackJob {
   const __bf16* src;

@@ -157,8 +157,12 @@ def splitk_nsplit(M: int, cout_p: int, cin_p: int, K: int, target_wgs: int = SPL
 # past through an LDS ring of input rows.  Automatic up to these output-pixel counts (graph-timed chains of
 # 11 layers with distinct weights, scripts/r5/ws_bench.py, profiles/r5/README.md): 192-wide layers
 # 6.7 / 9.8 / 12.6 / 18.7 us at B = 1 / 8 / 16 / 32 vs 20.3 / 19.4 / 19.9 / 22.6 on the automatic tile
-# (30.1 vs 25.5 at B = 64), 160-wide 7.2 .. 16.7 us vs 20.1 .. 20.5.  ALPHAGO_AMD_WS=0: off.
+# (30.1 vs 25.5 at B = 64), 160-wide 7.2 .. 16.7 us vs 20.1 .. 20.5.  Training steps stop at B = 16: there
+# the forward and dgrad share the GPU with the side-stream wgrad, and the one-workgroup-per-CU kernel
+# (122 KB of LDS) lost at B = 32 (SL 34.4k vs 36.2k positions/s; B = 16: 22.8k vs 22.0k, same box).
+# ALPHAGO_AMD_WS=0: off.
 WS_MAX_M = {192: 32 * 361, 160: 32 * 361}
+WS_MAX_M_TRAIN = {192: 16 * 361, 160: 16 * 361}
 
 
 def ws_pack(srcs, dsts) -> None:
@@ -179,9 +183,11 @@ def conv_ws_supported(cout_p: int, cin_p: int, K: int) -> bool:
     return bool(_ops().conv_ws_supported(cout_p, cin_p, K))
 
 
-def ws_applies(M: int, cout_p: int, cin_p: int, K: int) -> bool:
-    """Whether a conv of M output pixels runs on the weight-stationary kernel (tile 40)."""
-    if os.environ.get("ALPHAGO_AMD_WS", "1") == "0" or M > WS_MAX_M.get(conv_n_tile(cout_p), 0):
+def ws_applies(M: int, cout_p: int, cin_p: int, K: int, training: bool = False) -> bool:
+    """Whether a conv of M output pixels runs on the weight-stationary kernel (tile 40); ``training``:
+    inside a training step (lower limit, see WS_MAX_M_TRAIN)."""
+    limit = (WS_MAX_M_TRAIN if training else WS_MAX_M).get(conv_n_tile(cout_p), 0)
+    if os.environ.get("ALPHAGO_AMD_WS", "1") == "0" or M > limit:
         return False
     return bool(_ops().conv_ws_supported(cout_p, cin_p, K))
 
@@ -242,7 +248,8 @@ def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1, cin_r
     the kernel skip zero-padded input channels (only slab columns < cin_real are written).
     ``variant`` 0 = the production per-tap kernel; any other variant is a kernel-lab kernel
     (torch.ops.alphago_amd_lab: 9 = LDS ring, 10-13 = first-layer re-cuts, ...)."""
-    (_ops() if variant == 0 else lab()).conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, variant)
+    (_ops() if variant in (0, WGRAD_SMALL) else lab()).conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real,
+                                                                  variant)
 
 
 def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, beta: float = 0.0):
@@ -369,11 +376,27 @@ def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
     return max(1, min(target // per_split, nks // WGRAD_MIN_STAGES if target_wgs <= 0 else nks))
 
 
+# conv_wgrad's small-batch plan (C++ kWgradSmall): 64 x 64 output tiles with the kernel row's three taps
+# merged -- 27 workgroups per pixel split of a 192 -> 192 layer instead of 9 -- on one resident round
+# (two per CU).  SL positions/s, same box, per-tap plan -> small plan (profiles/r5/README.md): B = 24
+# 30.5k -> 32.1k, B = 32 35.7k -> 39.9k, B = 48 45.0k -> 46.7k, B = 64 54.2k -> 58.3k; B <= 16 equal or
+# mixed (22.0-22.8k either way), so it starts above 16 boards.
+WGRAD_SMALL = 14
+WGRAD_SMALL_M = (16 * 361, 64 * 361)  # (exclusive, inclusive) output-pixel range
+
+
 def wgrad_config(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, target_wgs: int = 0, cus: int = 256,
                  variant: int = 0):
-    """(variant, nsplit) of a layer's wgrad: the requested variant and wgrad_nsplit.  (Round 4's
+    """(variant, nsplit) of a layer's wgrad: the requested variant and wgrad_nsplit, or in the small-batch
+    range (WGRAD_SMALL_M) the small-batch plan for the 3x3 layers of 64-multiple widths.  (Round 4's
     small-batch LDS-ring variant 9 and the first-layer variants 10-12 are kernel-lab kernels since
     round 5: measured slower or equal.)"""
+    if (variant == 0 and WGRAD_SMALL_M[0] < M <= WGRAD_SMALL_M[1] and K == 3 and cout_p % 64 == 0 and
+            cin_p % 64 == 0 and cout_p != 160 and (cin_real == 0 or cin_real == cin_p)):
+        _, per_split, per_cu, _ = wgrad_plan(cout_p, cin_p, K, cin_real, WGRAD_SMALL)
+        target = target_wgs if target_wgs > 0 else cus * per_cu
+        nks = (M + 31) // 32
+        return WGRAD_SMALL, max(1, min(target // per_split, nks // WGRAD_MIN_STAGES))
     return variant, wgrad_nsplit(M, cout_p, cin_p, K, cin_real, target_wgs, cus, variant)
 
 

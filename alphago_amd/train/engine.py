@@ -299,9 +299,9 @@ class HipConvTrainer:
         if conv_tile == 0 and self.precision == "bf16" and not self.lab_tile:
             for l in range(self.L):
                 cin_p = self.C0p if l == 0 else self.Fp
-                if ops.ws_applies(M, self.Fp, cin_p, self.K[l]):
+                if ops.ws_applies(M, self.Fp, cin_p, self.K[l], training=True):
                     self.ws_fwd[l], self.sk_fwd[l] = True, 1
-                if l > 0 and ops.ws_applies(M, self.Fp, self.Fp, self.K[l]):
+                if l > 0 and ops.ws_applies(M, self.Fp, self.Fp, self.K[l], training=True):
                     self.ws_dg[l], self.sk_dg[l] = True, 1
         # their weights in the weight-stationary order (ops.ws_pack after every update, repack())
         self.wf_ws = [ops.ws_packed_like(self.wf[l]) if self.ws_fwd[l] else None for l in range(self.L)]

@@ -48,12 +48,17 @@ def _worker(rank, world, port, q, F=64, L=3, NB=16):
 
 
 @pytest.mark.parametrize("F,L,NB", [(64, 3, 16), (192, 12, 32)])
-def test_hip_dp_matches_single(cuda_device, F, L, NB):
+def test_hip_dp_matches_single(cuda_device, monkeypatch, F, L, NB):
     """2-rank DP (bucketed async all-reduce launched from the wgrad stream) ==
     one process on the union batch: gradients and the weights after the SGD
-    step, on a small net and on the full 12-layer 192-filter benchmark net."""
+    step, on a small net and on the full 12-layer 192-filter benchmark net.  The weight-stationary
+    forward / dgrad (B <= 16 per rank, not at the union batch) is off on both sides: its fp32 partial
+    sums round to bf16 differently from the 32-pixel tile, which moves a 12-layer gradient to a cosine of
+    ~0.99 -- a kernel difference, not a DP one (its own equality test: test_hip_trainer.py)."""
     from alphago_amd.models.nets import PolicyNet
     from alphago_amd.train.engine import HipPolicyTrainer
+
+    monkeypatch.setenv("ALPHAGO_AMD_WS", "0")  # (inherited by the spawned ranks)
 
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")

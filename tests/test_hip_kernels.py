@@ -94,13 +94,14 @@ def test_conv_dgrad_with_relu_mask(ops, cuda_device, B, C, K):
     assert _rel_err(out, ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", lab_params([0, 9, 5, 6, 7, 8, 1, 2, 3, 4], (0, 9)))
+@pytest.mark.parametrize("variant", lab_params([0, 14, 9, 5, 6, 7, 8, 1, 2, 3, 4], (0, 14)))
 @pytest.mark.parametrize("B,Cin,Cout,K,Pin,nsplit", [(6, 192, 192, 3, 1, None), (5, 64, 192, 5, 2, None),
                                                     (3, 64, 64, 3, 1, None), (9, 128, 128, 3, 1, None),
                                                     (7, 192, 192, 3, 1, 1), (4, 192, 192, 3, 1, 3),
                                                     (11, 192, 192, 3, 1, 40), (2, 128, 128, 3, 1, 5)])
 def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
-    """variant 0: production per-tap kernel; 5: the one-kernel-row wgrad (conv_wgrad_row.hip) for
+    """variant 0: production per-tap kernel; 14: its small-batch plan (64 x 64 tap-merged tiles on any
+    64-multiple 3x3 layer, ops.wgrad_config); 5: the one-kernel-row wgrad (conv_wgrad_row.hip) for
     192x192 and 128x128 3x3 layers; kernel-lab variants: 1-4, 6 tap-pair kernel for 192x192 3x3 (odd
     tap over split pairs; the slab starts as NaN, so every split's every tap must be written), 7
     per-tap kernel with whole-line staging, 8 tap pairs with the DMA spread through the MFMAs."""
@@ -116,7 +117,9 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     ns = nsplit or ops.wgrad_splits(M, K * K)
     slab = torch.full((ns, K * K, Cout, Cin), float("nan"), device=cuda_device)
     dbs = torch.zeros(ns, Cout, device=cuda_device)
-    if variant in (0, 9):  # production: per-tap kernel, 9 = its small-batch LDS ring
+    if variant == 14 and (K != 3 or Pin != 1):
+        pytest.skip("the small-batch plan covers 3x3 layers")
+    if variant in (0, 14):  # production: per-tap kernel, 14 = its small-batch plan
         ops.conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, variant=variant)
     else:  # kernel-lab variants
         ops.lab().conv_wgrad(xp, dzp, slab, dbs, K, S, Pin, 1, 0, variant)
@@ -598,13 +601,14 @@ def test_winograd_lab_forward(ops, cuda_device, B, S):
     assert y[:, 0].abs().sum() == 0 and y[:, :, -1].abs().sum() == 0
 
 
-@pytest.mark.parametrize("B", [1, 4, 16])
+@pytest.mark.parametrize("B", [1, 4, 16, 32, 64])
 @pytest.mark.parametrize("tile,ring", [(0, "0"), (36, "0"), (37, "0"),
                                        pytest.param(0, "1", marks=LAB), pytest.param(65, "1", marks=LAB),
                                        pytest.param(130, "0", marks=LAB)])
 def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, B, tile, ring):
     """Small batches (the reference's -B 16 training and batch-1 search calls): forward with the
-    bitmask, bitmask dgrad and the wgrad the trainer picks (ops.wgrad_config: per-tap splits) vs fp32
+    bitmask, bitmask dgrad and the wgrad the trainer picks (ops.wgrad_config: per-tap splits, the
+    small-batch 64 x 64 plan at B = 32 / 64) vs fp32
     conv2d / conv2d_input / conv2d_weight.  Lab cases: the LDS-ring tiles 65 / 130 and the ring wgrad
     (variant 9 with 16-stage splits), retired from the production library in round 5."""
     torch.manual_seed(12)
@@ -624,6 +628,7 @@ def test_small_batch_conv_fwd_dgrad_wgrad(ops, cuda_device, B, tile, ring):
     dx = ops.padded_empty(B, S, 1, C, cuda_device)
     _conv_fwd(ops, tile, ops.to_padded(g, 1), wd, None, dx, 3, S, 1, 1, mode=ops.MODE_MASKBITS, mbits=mb)
     var, ns = ops.wgrad_config(B * S * S, C, C, 3)
+    assert (var == ops.WGRAD_SMALL) == (ops.WGRAD_SMALL_M[0] < B * S * S <= ops.WGRAD_SMALL_M[1])
     if ring == "1":  # the lab's ring wgrad: one workgroup per CU, 16 32-pixel stages per split
         taps, per_split, _, _ = ops.wgrad_plan(C, C, 3)
         var, ns = 9, max(1, min(256 // per_split, (B * S * S + 31) // 32 // 16))
