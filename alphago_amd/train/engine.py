@@ -172,8 +172,11 @@ def optimizer_update_(p: torch.Tensor, g: torch.Tensor, state: List[torch.Tensor
             p.sub_(step * m / (v.sqrt() + sched.epsilon))
 
 
-# automatic wgrad / dgrad stream overlap between these pixel counts per step (B = 8 .. 256 at 19 x 19)
-OVERLAP_AUTO_MIN_PIXELS, OVERLAP_AUTO_MAX_PIXELS = 8 * 361, 256 * 361
+# automatic wgrad / dgrad stream overlap between these pixel counts per step (B = 17 .. 256 at 19 x 19;
+# round 5: with the weight-stationary forward / dgrad at B <= 16 -- one 12-wave workgroup per CU -- the
+# side-stream wgrad no longer finds idle CUs there: B = 8 12.1k overlapped vs 14.1k serial, B = 16 23.0k
+# vs 23.4k; B = 32 40.0k vs 35.8k, profiles/r5/README.md)
+OVERLAP_AUTO_MIN_PIXELS, OVERLAP_AUTO_MAX_PIXELS = 17 * 361, 256 * 361
 
 
 class HipConvTrainer:
