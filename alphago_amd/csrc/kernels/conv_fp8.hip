@@ -261,9 +261,26 @@ __device__ __forceinline__ int cvt4_bf16_bf8(unsigned lo2, unsigned hi2, float s
 // 64-channel chunks.  32 (the 160-channel value width, round 4): a step is four 32-channel chunks
 // and every MFMA K-block is one (tap, 32 channels) pair, so 160 channels are 5 chunks per tap instead
 // of 3 x 64 with a 32-channel zero half -- 45 chunks (12 steps) per 3x3 layer instead of 14 steps.
+// LDS of conv_fwd_fp8_ga_kernel: two weight slots (BN rows rounded up to whole 512-thread pieces),
+// or with the staged epilogue 8 waves x 16*MB pixels x (BN + 16) bytes if larger, then the amax
+// reduction's 8 floats
+constexpr int fp8_ga_wrows(int BN, int NT) { return (BN * 8) % NT == 0 ? BN : ((BN * 8 + NT - 1) / NT * NT) / 8; }
+constexpr int fp8_ga_red_off(int BN, int MB, bool stg, int NW) {
+  return stg && NW * 16 * MB * (BN + 16) > 2 * fp8_ga_wrows(BN, 64 * NW) * 128
+             ? NW * 16 * MB * (BN + 16)
+             : 2 * fp8_ga_wrows(BN, 64 * NW) * 128;
+}
+
 template <int BN, int MB, int NPART, bool OUT_BF16, bool OUT_FP8, bool DG = false, bool DGB = false,
-          bool DGBITS = false, int CW = 64>
-__global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) {
+          bool DGBITS = false, int CW = 64, int NW = 8, bool STGE = false, int PROBE = 0>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) {
+  // PROBE (kernel-lab timing probes, wrong values): bit 1 no MFMA, 2 no pixel loads, 4 no weight
+  // staging (load + ds_write), 8 no LDS fragment reads, 16 no epilogue stores;
+  // NW: waves per workgroup -- 8 (one workgroup per CU) or 4 (two per CU: one workgroup's
+  // prologue, barriers and epilogue overlap the other's MFMA steps).  STGE: byte outputs staged
+  // through LDS and stored as 16-B row segments (instead of one 4-B store per lane and block)
+  static_assert(NW == 8 || NW == 4, "waves per workgroup");
+  constexpr bool STG = STGE && OUT_FP8;
   static_assert(CW == 64 || CW == 32, "chunk width");
   constexpr int CPS = 128 / CW;  // chunks per K-step
   static_assert(!(DG && DGB), "one dgrad form");
@@ -273,12 +290,15 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   constexpr int NB = BN / 16;   // 16-channel blocks per wave
   constexpr int NH = NB / NPART;
   static_assert(NB % NPART == 0, "channel blocks must split evenly into parts");
-  constexpr int BM = 8 * 16 * MB;
+  constexpr int NT = 64 * NW;
+  constexpr int BM = NW * 16 * MB;
   // weight slot rows: BN rounded up so that every thread stages the same number
   // of 16-B pieces (BN 160 -> 192 rows; rows >= BN hold copies, never read)
-  constexpr int WROWS = (BN * 8) % 512 == 0 ? BN : ((BN * 8 + 511) / 512 * 512) / 8;
+  constexpr int WROWS = fp8_ga_wrows(BN, NT);
   constexpr int W_BYTES = WROWS * 128;
-  constexpr int WP = W_BYTES / 16 / 512;  // 16-B weight pieces per thread and step
+  constexpr int WP = W_BYTES / 16 / NT;  // 16-B weight pieces per thread and step
+  constexpr int SROW = BN + 16;           // STG: LDS bytes per staged pixel (16-B aligned, skewed banks)
+  constexpr int RED_OFF = fp8_ga_red_off(BN, MB, STG, NW);
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -319,11 +339,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
     const int jj = rem - ii * a.S;
     xbase[j] = ((b * a.HPi + ii + a.offi) * a.HPi + jj + a.offi) * a.Cin + (CW == 64 ? (g & 1) * 32 : 0);
   }
-  // A operand (weights) staging: piece p = tid + 512 i -> LDS row p/8, physical 16-B chunk p%8
+  // A operand (weights) staging: piece p = tid + NT i -> LDS row p/8, physical 16-B chunk p%8
   int wsrc[WP], wdst[WP];
 #pragma unroll
   for (int i = 0; i < WP; ++i) {
-    const int p = threadIdx.x + 512 * i;
+    const int p = threadIdx.x + NT * i;
     const int r = p >> 3, pc = p & 7;
     const int lc = pc ^ fp8_swz(r);
     // logical 16-B chunk lc of the 128-B row: chunk lc / (CW / 16) of the step, bytes (lc % (CW / 16)) * 16
@@ -351,15 +371,22 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   };
   u32x4 wreg[WP];
   auto load_w = [&](int ks) {
+    if constexpr (PROBE & 4) return;
     const int k0 = ks < nK ? ks : nK - 1;  // one step ahead of the last: any in-range step (unused)
 #pragma unroll
     for (int i = 0; i < WP; ++i) wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, wsrc[i], k0 * a.Cout * 128, 0);
   };
   auto store_w = [&](int slot) {
+    if constexpr (PROBE & 4) return;
 #pragma unroll
     for (int i = 0; i < WP; ++i) *(u32x4*)(smem + slot * W_BYTES + wdst[i]) = wreg[i];
   };
   auto load_x = [&](i32x8 (&xf)[MB], int ks) {
+    if constexpr (PROBE & 2) {
+#pragma unroll
+      for (int j = 0; j < MB; ++j) xf[j] = i32x8{ks, j, lane, 0, ks, j, lane, 0};
+      return;
+    }
     const int off = lane_off(ks);
 #pragma unroll
     for (int j = 0; j < MB; ++j) {
@@ -422,6 +449,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 #pragma unroll
       for (int i = 0; i < NH; ++i) {
         const char* p = wb + wrow + (h * NH + i) * 16 * 128;
+        if constexpr (PROBE & 8) {
+          wf[i] = i32x8{h, i, ks, lane, h, i, ks, lane};
+          continue;
+        }
         const int4 lo = *(const int4*)(p + c0);
         const int4 hi = *(const int4*)(p + c1);
         wf[i] = i32x8{lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
@@ -431,7 +462,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
       for (int i = 0; i < NH; ++i)
 #pragma unroll
         for (int j = 0; j < MB; ++j)
-          acc[h * NH + i][j] = (DG || DGB) ? mfma_fp8_bf8(wf[i], xc[j], acc[h * NH + i][j], sw, sx)
+          if constexpr (PROBE & 1) acc[h * NH + i][j][0] += (float)(wf[i][0] ^ xc[j][1]);
+          else acc[h * NH + i][j] = (DG || DGB) ? mfma_fp8_bf8(wf[i], xc[j], acc[h * NH + i][j], sw, sx)
                                            : mfma_fp8(wf[i], xc[j], acc[h * NH + i][j], sw, sx);
       __builtin_amdgcn_s_setprio(0);
     }
@@ -447,6 +479,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
   wait_vmcnt0();
 
   // --- epilogue: bias + ReLU, amax, bf16 and/or e4m3 stores (lane: 4 channels of one pixel per block)
+  // STG: the wave's byte outputs go to its own LDS rows (SROW bytes per pixel) and leave as 16-B
+  // row segments after the block loop (the weight slots are free: the loop ended on a barrier)
+  char* stg = smem + wave * (16 * MB * SROW);
   const int nbase = n0 + ((lane >> 4) << 2);
   const float osc = a.out_scale[0];
   const bool sr = a.sr_seed != nullptr;  // uniform
@@ -518,6 +553,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
         v[3] = fmaxf(v[3] + bb[3], 0.f);
       }
       if (!ok) continue;
+      if constexpr ((PROBE & 16) != 0) {
+        vmax = fmaxf(vmax, v[0] + v[1] + v[2] + v[3]);
+        continue;
+      }
       if constexpr (DG || DGB)
         vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
       else
@@ -546,11 +585,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
           for (int r = 0; r < 4; ++r) sv[r] = fminf(fmaxf(v[r] * osc, -57344.f), 57344.f);
           int pk = __builtin_amdgcn_cvt_pk_bf8_f32(sv[0], sv[1], 0, false);
           pk = __builtin_amdgcn_cvt_pk_bf8_f32(sv[2], sv[3], pk, true);
-          *(int*)(a.y_fp8 + ooff + n) = pk;
+          if constexpr (STG) *(int*)(stg + (j * 16 + (lane & 15)) * SROW + (n - n0)) = pk;
+          else *(int*)(a.y_fp8 + ooff + n) = pk;
         } else {
           const float s0 = fminf(v[0] * osc, 448.f), s1 = fminf(v[1] * osc, 448.f);
           const float s2 = fminf(v[2] * osc, 448.f), s3 = fminf(v[3] * osc, 448.f);
-          *(int*)(a.y_fp8 + ooff + n) = fp8_pack4(s0, s1, s2, s3, sr, (uint32_t)(ooff + n), seed);
+          const int pk = fp8_pack4(s0, s1, s2, s3, sr, (uint32_t)(ooff + n), seed);
+          if constexpr (STG) *(int*)(stg + (j * 16 + (lane & 15)) * SROW + (n - n0)) = pk;
+          else *(int*)(a.y_fp8 + ooff + n) = pk;
         }
       }
     }
@@ -562,15 +604,34 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
       }
     }
   }
+  if constexpr (STG) {
+    __syncthreads();  // the block loop's LDS writes before the row reads (any lane's rows)
+    constexpr int SEG = BN / 16;  // 16-B segments per pixel
+    constexpr int TOT = 16 * MB * SEG;
+#pragma unroll
+    for (int it = 0; it < (TOT + 63) / 64; ++it) {
+      const int idx = it * 64 + lane;
+      const int p = idx / SEG, sg = idx - p * SEG;
+      const int m = m0 + wave * 16 * MB + p;
+      if (idx < TOT && m < a.M) {
+        const int b = fdiv(m, a.divSS);
+        const int rem = m - b * SS;
+        const int ii = fdiv(rem, a.divS);
+        const int jj = rem - ii * a.S;
+        const size_t po = (size_t)((b * a.HPo + ii + a.Po) * a.HPo + jj + a.Po);
+        *(u32x4*)(a.y_fp8 + po * a.Cout + n0 + sg * 16) = *(const u32x4*)(stg + p * SROW + sg * 16);
+      }
+    }
+  }
   if (a.amax) {
     vmax = wave_max(vmax);
-    float* red = reinterpret_cast<float*>(smem + 2 * W_BYTES);
+    float* red = reinterpret_cast<float*>(smem + RED_OFF);
     if (lane == 0) red[wave] = vmax;
     __syncthreads();
     if (threadIdx.x == 0) {
       float m = red[0];
 #pragma unroll
-      for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w]);
+      for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
       atomicMax(a.amax + (blockIdx.x & (kFp8AmaxSlots - 1)), __float_as_uint(m));
     }
   }
@@ -580,26 +641,33 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_fp8_ga_kernel(ConvFp8Args a) 
 // weights in 4 parts); kernel-lab build only: 1 / 3 / 4 = other L2-operand
 // tilings, 5 = LDS-staged conv_fwd_fp8_kernel
 
-template <int BN, int MB, int NPART, bool OB, bool OF, bool DG, bool DGB, bool DGBITS, int CW>
+template <int BN, int MB, int NPART, bool OB, bool OF, bool DG, bool DGB, bool DGBITS, int CW, int NW, bool STGE,
+          int PROBE = 0>
 static void launch_fp8_ga_cw(const ConvFp8Args& a, hipStream_t st) {
-  constexpr int WROWS = (BN * 8) % 512 == 0 ? BN : ((BN * 8 + 511) / 512 * 512) / 8;  // as in the kernel
-  constexpr int smem = 2 * WROWS * 128 + 64;
+  constexpr int smem = fp8_ga_red_off(BN, MB, STGE && OF, NW) + 64;  // as in the kernel
   static const hipError_t attr = hipFuncSetAttribute(
-      (const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, CW>,
+      (const void*)conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, CW, NW, STGE, PROBE>,
       hipFuncAttributeMaxDynamicSharedMemorySize, smem);  // once per instantiation (thread-safe static)
   hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
-  constexpr int BM = 128 * MB;
+  constexpr int BM = NW * 16 * MB;
   dim3 grid((a.M + BM - 1) / BM, a.Cout / BN);
-  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, CW>), grid, dim3(512), smem, st,
+  hipLaunchKernelGGL((conv_fwd_fp8_ga_kernel<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, CW, NW, STGE, PROBE>), grid, dim3(64 * NW), smem, st,
                      a);
 }
 
 // a.cw: the packed weights' chunk width (32 for the 160-channel value layers packed in 32-channel
-// chunks, else 64)
-template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false, bool DGB = false, bool DGBITS = false>
+// chunks, else 64).  The 160-wide value tile runs 4-wave workgroups, two per CU, with the byte
+// outputs staged through LDS: value layer at B = 1024, e4m3 output + ReLU' bitmask (the fp8
+// training forward), same-box lab A/B (scripts/r5/fp8_probe2.py): 120.3 us (8 waves, direct
+// 4-B stores) -> 116.3 (staged) / 109.4 (4 waves) -> 101.4 (both); bf16 + e4m3 outputs 138.6 -> 115.2
+// (4-wave workgroups only with 32-channel chunks: the 64-channel packing's extra weight pieces spill).
+// NW = 0 / STGE = -1: this policy; lab variants pass explicit values
+template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false, bool DGB = false, bool DGBITS = false,
+          int NW = 0, int STGE = -1>
 static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
-  if (a.cw == 32) launch_fp8_ga_cw<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, 32>(a, st);
-  else launch_fp8_ga_cw<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, 64>(a, st);
+  constexpr bool stg = STGE >= 0 ? STGE != 0 : BN == 160;
+  if (a.cw == 32) launch_fp8_ga_cw<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, 32, NW ? NW : (BN == 160 ? 4 : 8), stg>(a, st);
+  else launch_fp8_ga_cw<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, 64, NW ? NW : 8, stg>(a, st);
 }
 
 // fp8 dgrad of the fp8-wgrad value step: e5m2 operand (the previous dgrad's copy), bitmask ReLU',
@@ -637,7 +705,7 @@ static void launch_fp8_dgrad_bn(const ConvFp8Args& a, hipStream_t st) {
 
 template <int BN, bool OB, bool OF>
 static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
-  if (a.cw != 64 && a.variant != 0) throw std::invalid_argument("conv_fwd_fp8: 32-channel chunks: production kernel only");
+  if (a.cw != 64 && a.variant != 0 && a.variant != 6 && a.variant <= 100) throw std::invalid_argument("conv_fwd_fp8: 32-channel chunks: production kernel only");
 #ifndef AGK_KERNEL_LAB
   if (a.variant != 0) throw std::invalid_argument("conv_fwd_fp8: variant " + std::to_string(a.variant) +
                                                   " is a kernel-lab variant");
@@ -652,6 +720,17 @@ static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
     else if (a.variant == 1) launch_fp8_ga<160, 3, 2, OB, OF>(a, st);
     else if (a.variant == 3) launch_fp8_ga<160, 2, 5, OB, OF>(a, st);
     else if (a.variant == 4) launch_fp8_ga<160, 2, 2, OB, OF>(a, st);
+    else if (a.variant == 6) launch_fp8_ga<160, 3, 5, OB, OF, false, false, false, 8, 0>(a, st);  // round 4
+    else if (a.variant > 100 && a.variant < 132 && a.cw == 32) {  // timing probes (PROBE = variant - 100)
+      switch (a.variant - 100) {
+#define AGK_FP8_PROBE(P) \
+  case P: launch_fp8_ga_cw<160, 3, 5, OB, OF, false, false, false, 32, 4, true, P>(a, st); break;
+        AGK_FP8_PROBE(1) AGK_FP8_PROBE(2) AGK_FP8_PROBE(4) AGK_FP8_PROBE(8) AGK_FP8_PROBE(16)
+        AGK_FP8_PROBE(6) AGK_FP8_PROBE(14) AGK_FP8_PROBE(30) AGK_FP8_PROBE(31) AGK_FP8_PROBE(17)
+#undef AGK_FP8_PROBE
+        default: throw std::invalid_argument("conv_fwd_fp8: probe " + std::to_string(a.variant));
+      }
+    }
 #endif
     else throw std::invalid_argument("conv_fwd_fp8: 160-wide tile variant " + std::to_string(a.variant));
   } else {
@@ -663,6 +742,7 @@ static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
 #ifdef AGK_KERNEL_LAB
         else if (a.variant == 3) launch_fp8_ga<BN, 2, 3, OB, OF>(a, st);
         else if (a.variant == 4) launch_fp8_ga<BN, 3, 6, OB, OF>(a, st);
+        else if (a.variant == 6) launch_fp8_ga<BN, 3, 4, OB, OF, false, false, false, 4, 1>(a, st);
         else launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
 #endif
       } else {

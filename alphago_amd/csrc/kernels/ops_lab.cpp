@@ -45,9 +45,10 @@ void conv_fwd_pk_lab(const Tensor& x, const Tensor& w, const Tensor& bias, const
 void conv_fwd_fp8_lab(const Tensor& x, const Tensor& w, const Tensor& bias, const Tensor& scales,
                       const Tensor& out_scale, const c10::optional<Tensor>& amax,
                       const c10::optional<Tensor>& y_bf16, const c10::optional<Tensor>& y_fp8, int64_t K, int64_t S,
-                      int64_t Pin, int64_t Po, int64_t variant) {
-  check_dev("conv_fwd_fp8_lab", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8);
-  conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, (int)variant);
+                      int64_t Pin, int64_t Po, int64_t variant, const c10::optional<Tensor>& mbits) {
+  check_dev("conv_fwd_fp8_lab", x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, mbits);
+  conv_fwd_fp8_impl(x, w, bias, scales, out_scale, amax, y_bf16, y_fp8, K, S, Pin, Po, (int)variant, c10::nullopt,
+                    mbits);
 }
 
 int64_t wgrad_tap_group_lab(int64_t cout, int64_t cin, int64_t K, int64_t variant) {
@@ -160,7 +161,7 @@ TORCH_LIBRARY(alphago_amd_lab, m) {
         "int cin_real, int variant) -> ()");
   m.def(
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
-      "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, int variant) -> ()");
+      "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, int variant, Tensor(d!)? mbits=None) -> ()");
   m.def(
       "conv_fwd_pk(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int K, int S, int Pin, int Po, int cin_real, "
       "Tensor(b!)? mbits=None) -> ()");

@@ -165,6 +165,7 @@ def test_conv_fwd_fp8_160(ops, cuda_device, monkeypatch, cw, B, Cin, Cin_p, K):
     assert _rel_err(out[:, :Cout], ref) < 1e-2
     assert out[:, Cout:].abs().sum() == 0
     assert _rel_err(ops.fp8_to_float(y8, ey)[:, 1:S + 1, 1:S + 1, :Cout].permute(0, 3, 1, 2), ref) < 0.07
+    assert y8[:, 0].sum() == 0 and y8[:, :, 0].sum() == 0 and y8[:, S + 1].sum() == 0  # borders untouched
     assert abs(amax.view(torch.float32).max().item() - ref.max().item()) <= 1e-2 * ref.max().item()
     # the ReLU' bitmask written by the fp8 epilogue == masking by y_bf16 > 0 in the bf16 dgrad
     w2 = _bf(torch.randn(Cout, Cout, 3, 3, device=cuda_device) * 0.05)
@@ -177,6 +178,70 @@ def test_conv_fwd_fp8_160(ops, cuda_device, monkeypatch, cw, B, Cin, Cin_p, K):
     ops.conv_fwd(dz, wd2, None, d_mask, 3, S, 1, 1, mode=ops.MODE_MASK, mask=yb)
     torch.cuda.synchronize()
     assert torch.equal(d_bits, d_mask)
+
+
+def _fwd_fp8_160_case(ops, dev, B, seed=11):
+    torch.manual_seed(seed)
+    S, K, C, Cp = 19, 3, 152, 160
+    x = F.relu(torch.randn(B, C, S, S, device=dev))
+    xp = ops.to_padded(x, 1, Cp)
+    ex = ops.fp8_exponent(float(x.abs().max()), margin=0)
+    x8 = torch.empty(xp.shape, dtype=torch.uint8, device=dev)
+    ops.quantize_fp8(xp, x8, ex)
+    w8, ew = ops.pack_weights_fp8(torch.randn(C, C, K, K, device=dev) * 0.05, Cp, Cp)
+    bp = F.pad(torch.randn(C, device=dev) * 0.1, (0, Cp - C))
+    scales = torch.tensor([127 - ex, 127 - ew], dtype=torch.int32, device=dev)
+    return x8, w8, bp, scales, torch.tensor([4.0], device=dev)
+
+
+def _fwd_fp8_160_outputs(ops, dev, B, outs):
+    S, Cp = 19, 160
+    y8 = torch.zeros((B, S + 2, S + 2, Cp), dtype=torch.uint8, device=dev)
+    yb = ops.padded_empty(B, S, 1, Cp, dev) if outs == "both" else None
+    mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=dev)
+    return y8, yb, mbits, ops.fp8_amax_buffer(1, dev)[0]
+
+
+@pytest.mark.parametrize("B", [1, 37])
+def test_conv_fwd_fp8_160_byte_outputs(ops, cuda_device, monkeypatch, B):
+    """The fp8 training forward's e4m3-only output (staged through LDS, 16-B row stores, ragged
+    last tile at B = 37) equals the e4m3 copy written next to a bf16 output, with the same ReLU'
+    bitmask and amax, and leaves the zero border untouched."""
+    monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1")
+    S = 19
+    x8, w8, bp, scales, osc = _fwd_fp8_160_case(ops, cuda_device, B)
+    res = {}
+    for outs in ("fp8", "both"):
+        y8, yb, mbits, amax = _fwd_fp8_160_outputs(ops, cuda_device, B, outs)
+        ops.conv_fwd_fp8(x8, w8, bp, scales, osc, 3, S, 1, 1, y_bf16=yb, y_fp8=y8, amax=amax, mbits=mbits)
+        res[outs] = (y8, yb, mbits, amax)
+    torch.cuda.synchronize()
+    (y8a, _, mba, ama), (y8b, yb, mbb, amb) = res["fp8"], res["both"]
+    assert torch.equal(y8a, y8b) and torch.equal(mba, mbb) and torch.equal(ama, amb)
+    assert y8a[:, 0].sum() == 0 and y8a[:, :, 0].sum() == 0 and y8a[:, S + 1].sum() == 0
+    assert y8a[:, :, S + 1].sum() == 0
+    # the e4m3 bytes are the bf16 result's values at 4x (round-to-nearest of the fp32 value: within
+    # one e4m3 step of the bf16-rounded copy)
+    ref = ops.from_padded(yb, 1).float() * 4.0
+    got = ops.fp8_to_float(y8a, 0)[:, 1:S + 1, 1:S + 1, :].permute(0, 3, 1, 2)
+    assert ((got - ref).abs() <= ref.abs() * 0.07 + 1e-3).all()
+
+
+@pytest.mark.parametrize("B", lab_params([1, 5, 37], []))
+def test_conv_fwd_fp8_160_matches_round4_tiling(ops, cuda_device, monkeypatch, B):
+    """Production 160-wide forward (4-wave workgroups, staged byte outputs) == the round-4 tiling
+    (lab variant 6: 8-wave workgroups, 4-B stores) byte for byte."""
+    monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1")
+    S = 19
+    x8, w8, bp, scales, osc = _fwd_fp8_160_case(ops, cuda_device, B)
+    y8, yb, mbits, amax = _fwd_fp8_160_outputs(ops, cuda_device, B, "both")
+    ops.conv_fwd_fp8(x8, w8, bp, scales, osc, 3, S, 1, 1, y_bf16=yb, y_fp8=y8, amax=amax, mbits=mbits)
+    y8l, ybl, mbl, aml = _fwd_fp8_160_outputs(ops, cuda_device, B, "both")
+    ops.lab().conv_fwd_fp8(x8, w8, bp, scales, osc, aml, ybl, y8l, 3, S, 1, 1, 6, mbl)
+    torch.cuda.synchronize()
+    assert torch.equal(y8, y8l) and torch.equal(yb, ybl) and torch.equal(mbits, mbl)
+    # amax slots follow the workgroup index (different grids): the maximum over the slots agrees
+    assert amax.view(torch.float32).max().item() == aml.view(torch.float32).max().item()
 
 
 @pytest.mark.parametrize("C,Cp", [(152, 160), (192, 192)])
