@@ -55,7 +55,7 @@ def hip_path(flavor: str = "prod") -> str:
 def _hip_sources(flavor: str):
     kd = os.path.join(CSRC, "kernels")
     if flavor == "lab":
-        return [os.path.join(kd, f) for f in LAB_SOURCES + ("conv.hip", "conv_ws.hip", "conv_fp8.hip", "ops_lab.cpp")]
+        return [os.path.join(kd, f) for f in LAB_SOURCES + ("conv.hip", "conv_ws.hip", "conv_fp8.hip", "conv_wgrad_fp8.hip", "ops_lab.cpp")]
     srcs = sorted(glob.glob(os.path.join(kd, "*.hip")) + glob.glob(os.path.join(kd, "*.cpp")))
     return [f for f in srcs if os.path.basename(f) not in LAB_SOURCES + ("ops_lab.cpp",)]
 

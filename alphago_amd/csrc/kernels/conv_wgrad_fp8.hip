@@ -19,14 +19,16 @@
 //
 // Scales: the MFMA's E8M0 block scales dequantise both operands (127 - e, from the device-resident
 // delayed scales), so the fp32 partials go to the same per-split slab as the bf16 wgrad and the same
-// deterministic conv_wgrad_reduce sums them.  Bias gradient: the tap-0 workgroups sum the e5m2
-// gradient bytes of their A fragments (e5m2 = the high byte of an fp16) and divide by the multiplier;
-// they also fold max |dZ| into the delayed-scale amax slots (a saturated e5m2 value reads 57344 / 2^eg,
-// so a scale that overflows shrinks by the margin every step until it fits).
+// deterministic conv_wgrad_reduce sums them.  Bias gradient: the tap-0 workgroups multiply their A
+// fragments by an all-ones e4m3 operand (one more MFMA per fragment, dequantised by the same block
+// scale); they also fold max |dZ| into the delayed-scale amax slots from the e5m2 magnitude bytes (a
+// saturated e5m2 value reads 57344 / 2^eg, so a scale that overflows shrinks by the margin every step
+// until it fits).
 // Borders: pixels past the batch read padded-pixel 0 of dZ (always zero).
 #include <hip/hip_runtime.h>
 
 #include <stdexcept>
+#include <string>
 #include <utility>
 
 #include "common.h"
@@ -69,7 +71,9 @@ constexpr int kImgBytes = kStepPx * 160;  // one operand image of a step: 128 pi
 
 // WN x WC tile of one tap per workgroup, 4 waves as 2 (n) x 2 (c); each lane stages the same rows
 // of both operands, so one pixel decomposition serves a dz piece and an x piece.
-template <int WN, int WC>
+// PROBE (kernel-lab timing probes, wrong values): bit 1 no MFMA, 2 no staging loads, 4 no LDS
+// fragment reads, 8 no partial-tile stores
+template <int WN, int WC, int PROBE = 0>
 __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args a) {
   static_assert(WN == 160 && WC == 160, "line staging: whole 160-channel pixel rows");
   constexpr int NBn = WN / 32;  // 16-blocks per wave (a wave covers WN/2 x WC/2)
@@ -96,25 +100,56 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
   const int sa = *a.gscale, sb = *a.xscale;  // E8M0 exponents (dZ, X)
 
   constexpr int NPAIR = kStepPx * WC / 4096;  // 1-KB pieces per operand image per wave
-  auto stage = [&](int ks, int buf) {
+  // Each lane's pixel of piece i advances by exactly 128 pixels per stage() call (consecutive steps),
+  // so the (row, column) decomposition and both padded pixel indices are carried from step to step
+  // with adds and selects: the per-step divisions and 32-bit multiplies of a fresh decomposition
+  // (quarter-rate on CDNA: ~1300 of the SIMD's cycles per wave and step, more than the step's 25
+  // MFMAs) are paid once here.  Past the batch: dz pixel 0 (a zero border) and x pixel 0.
+  int spx[NPAIR], sii[NPAIR], sjx[NPAIR], spo[NPAIR], spi[NPAIR], sc16[NPAIR];
+  const int DB = kStepPx / SS, DI = (kStepPx % SS) / a.S, DJ = kStepPx % a.S;
+  const int stepo = (DB * a.HPo + DI) * a.HPo + DJ, stepi = (DB * a.HPi + DI) * a.HPi + DJ;
+  const int wjo = a.HPo - a.S, wjo_i = (a.HPo - a.S) * a.HPo;
+  const int wji = a.HPi - a.S, wji_i = (a.HPi - a.S) * a.HPi;
+#pragma unroll
+  for (int i = 0; i < NPAIR; ++i) {
+    const int idx = (wave * NPAIR + i) * 64 + lane;  // 16-byte unit of the image
+    const int R = idx / 10, pos = idx - R * 10;
+    int c = pos - ((R >> 3) & 1);
+    c = c < 0 ? c + 10 : c;  // source chunk (16 channels) of this LDS unit
+    const int k = 32 * ((R >> 3) & 3) + 8 * (R >> 5) + (R & 7);
+    const int px = ks_begin * kStepPx + k;
+    const int b = fdiv(px, a.divSS);
+    const int rem = px - b * SS;
+    const int ii = fdiv(rem, a.divS);
+    const int jx = rem - ii * a.S;
+    spx[i] = px;
+    sii[i] = ii;
+    sjx[i] = jx;
+    spo[i] = (b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po;
+    spi[i] = (b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi;
+    sc16[i] = c * 16;
+  }
+  auto stage = [&](int buf) {
+    if constexpr ((PROBE & 2) != 0) return;
     char* base = smem + buf * STAGE;
     int dzo[NPAIR], xo[NPAIR];
 #pragma unroll
     for (int i = 0; i < NPAIR; ++i) {
-      const int P = wave * NPAIR + i;  // piece of the operand image
-      const int idx = P * 64 + lane;   // 16-byte unit of the image
-      const int R = idx / 10, pos = idx - R * 10;
-      int c = pos - ((R >> 3) & 1);
-      c = c < 0 ? c + 10 : c;  // source chunk (16 channels) of this LDS unit
-      const int k = 32 * ((R >> 3) & 3) + 8 * (R >> 5) + (R & 7);
-      const int px = ks * kStepPx + k;
-      const int pm = px < a.M ? px : a.M - 1;
-      const int b = fdiv(pm, a.divSS);
-      const int rem = pm - b * SS;
-      const int ii = fdiv(rem, a.divS);
-      const int jx = rem - ii * a.S;
-      dzo[i] = (px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po) * a.Cout : 0) + c * 16;  // pixel 0: zero border
-      xo[i] = ((b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi) * a.Cin + toff + c * 16;
+      const bool in = spx[i] < a.M;
+      dzo[i] = (in ? (int)__umul24((unsigned)spo[i], (unsigned)a.Cout) : 0) + sc16[i];
+      xo[i] = (in ? (int)__umul24((unsigned)spi[i], (unsigned)a.Cin) : 0) + toff + sc16[i];
+      // advance to the next step's pixel
+      spx[i] += kStepPx;
+      int jx = sjx[i] + DJ;
+      const bool w1 = jx >= a.S;
+      jx = w1 ? jx - a.S : jx;
+      int ii = sii[i] + DI + (w1 ? 1 : 0);
+      const bool w2 = ii >= a.S;
+      ii = w2 ? ii - a.S : ii;
+      sjx[i] = jx;
+      sii[i] = ii;
+      spo[i] += stepo + (w1 ? wjo : 0) + (w2 ? wjo_i : 0);
+      spi[i] += stepi + (w1 ? wji : 0) + (w2 ? wji_i : 0);
     }
 #pragma unroll
     for (int i = 0; i < NPAIR; ++i) glds16(a.dz8 + dzo[i], base + (wave * NPAIR + i) * 1024);
@@ -127,11 +162,18 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
   for (int i = 0; i < NBn; ++i)
 #pragma unroll
     for (int j = 0; j < NBc; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dbs[NBn];
+  // tap-0 workgroups (wc == 0 waves): the bias gradient as one more MFMA per A fragment against an
+  // all-ones e4m3 operand (every column of the 16 x 16 result is the row sum, dequantised by the
+  // block scale), and max |e5m2 dZ| as a packed 16-bit max of the magnitude bytes (e5m2 orders by
+  // byte & 0x7f) -- 4 VALU per dword instead of a float conversion per byte (the conversions made
+  // the tap-0 workgroups, and with one resident round the whole kernel, ~530 VALU per step longer)
+  f32x4 accb[NBn];
 #pragma unroll
-  for (int i = 0; i < NBn; ++i) dbs[i] = 0.f;
-  float vmax = 0.f;  // tap-0 workgroups: max |e5m2 dZ| (scaled)
+  for (int i = 0; i < NBn; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
+  u16x2 mlo = {0, 0}, mhi = {0, 0};
   const bool do_bias = (t == 0) && (c0 == 0) && (wc == 0);
+  const i32x8 ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838, 0x38383838};
 
   // transposed reads: lane (g = lane >> 4, li = lane & 15) reads row 32 j + lrow, byte 8 (li & 1) of
   // the rotated 16-byte chunk of its block
@@ -139,13 +181,13 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
   const int lrow = 8 * g + (li >> 1);
 
   if (ks_begin < ks_end) {
-    stage(ks_begin, 0);
+    stage(0);
     wait_vmcnt0();
     __syncthreads();
   }
   for (int ks = ks_begin; ks < ks_end; ++ks) {
     const int cur = (ks - ks_begin) & 1;
-    if (ks + 1 < ks_end) stage(ks + 1, cur ^ 1);
+    if (ks + 1 < ks_end) stage(cur ^ 1);
     const char* base = smem + cur * STAGE;
     i32x8 af[NBn];
     {
@@ -157,10 +199,18 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
       const uint32_t bn = b0 + wn * NBn * 16, bc = b0 + kImgBytes + wc * NBc * 16;
       const uint32_t bn4 = bn - ((wn == 1 && (g & 1)) ? 160 : 0), bc4 = bc - ((wc == 1 && (g & 1)) ? 160 : 0);
       u32x2 ra[NBn][4], rb[2][4];
-      static_for<4>([&](auto J) {
-        static_for<NBn>([&](auto I) { ra[I][J] = ds_read_tr8_off<J * 32 * 160 + I * 16>(I == NBn - 1 ? bn4 : bn); });
-      });
-      static_for<4>([&](auto J) { rb[0][J] = ds_read_tr8_off<J * 32 * 160>(bc); });
+      if constexpr ((PROBE & 4) != 0) {
+        static_for<4>([&](auto J) {
+          static_for<NBn>([&](auto I) { ra[I][J] = u32x2{bn + I * 7u + J, bn4 ^ (unsigned)ks}; });
+          rb[0][J] = u32x2{bc + J, bc4 ^ (unsigned)ks};
+          rb[1][J] = rb[0][J];
+        });
+      } else {
+        static_for<4>([&](auto J) {
+          static_for<NBn>([&](auto I) { ra[I][J] = ds_read_tr8_off<J * 32 * 160 + I * 16>(I == NBn - 1 ? bn4 : bn); });
+        });
+        static_for<4>([&](auto J) { rb[0][J] = ds_read_tr8_off<J * 32 * 160>(bc); });
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -169,7 +219,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
                       (int)ra[i][2].x, (int)ra[i][2].y, (int)ra[i][3].x, (int)ra[i][3].y};
       static_for<NBc>([&](auto C) {
         constexpr int cb = C & 1, nb = (C + 1) & 1;
-        if constexpr (C + 1 < NBc)
+        if constexpr (C + 1 < NBc && (PROBE & 4) == 0)
           static_for<4>([&](auto J) {
             rb[nb][J] = ds_read_tr8_off<J * 32 * 160 + (C + 1) * 16>(C + 1 == NBc - 1 ? bc4 : bc);
           });
@@ -178,8 +228,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int i = 0; i < NBn; ++i)
-          acc[i][C] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bm, acc[i][C], 1, 0, 0, sa, 0, sb);
+        for (int i = 0; i < NBn; ++i) {
+          if constexpr ((PROBE & 1) != 0) acc[i][C][0] += (float)(af[i][0] ^ bm[1]);
+          else acc[i][C] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bm, acc[i][C], 1, 0, 0, sa, 0, sb);
+        }
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (C + 1 < NBc)
@@ -195,16 +247,13 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
     if (do_bias) {
 #pragma unroll
       for (int i = 0; i < NBn; ++i) {
-        float s = 0.f;
+        accb[i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], ones, accb[i], 1, 0, 0, sa, 0, 127);
 #pragma unroll
         for (int d = 0; d < 8; ++d) {
           const unsigned w = (unsigned)af[i][d];
-          const float v0 = bf8_to_f32(w & 0xffu), v1 = bf8_to_f32((w >> 8) & 0xffu);
-          const float v2 = bf8_to_f32((w >> 16) & 0xffu), v3 = bf8_to_f32(w >> 24);
-          s += (v0 + v1) + (v2 + v3);
-          vmax = fmaxf(vmax, fmaxf(fmaxf(fabsf(v0), fabsf(v1)), fmaxf(fabsf(v2), fabsf(v3))));
+          mlo = __builtin_elementwise_max(mlo, __builtin_bit_cast(u16x2, w & 0x007f007fu));
+          mhi = __builtin_elementwise_max(mhi, __builtin_bit_cast(u16x2, w & 0x7f007f00u));
         }
-        dbs[i] += s;
       }
     }
     wait_vmcnt0();
@@ -222,21 +271,27 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
       const int n = nb0 + i * 16;
       const int cc = cbase + c * 16;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) out[(size_t)(n + r) * a.Cin + cc] = acc[i][c][r];
+      for (int r = 0; r < 4; ++r) {
+        if constexpr ((PROBE & 8) != 0) {
+          if (acc[i][c][r] == 12345.f) out[(size_t)(n + r) * a.Cin + cc] = 0.f;  // keeps the sums live
+        } else {
+          out[(size_t)(n + r) * a.Cin + cc] = acc[i][c][r];
+        }
+      }
     }
   if (do_bias) {
-    // a lane's A fragment is channel row li of block i, 32 of the step's pixels; the 4 lane groups
-    // hold the 4 pixel quarters
-    const float inv = 1.f / *a.gmul;
+    // column 0 of the ones-product: lanes 0, 16, 32, 48 hold rows 4 (lane / 16) + r of block i
+    if ((lane & 15) == 0) {
 #pragma unroll
-    for (int i = 0; i < NBn; ++i) {
-      float s = dbs[i];
-      s += __shfl_xor(s, 16, 64);
-      s += __shfl_xor(s, 32, 64);
-      if (lane < 16) a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / 2) + i * 16 + lane] = s * inv;
+      for (int i = 0; i < NBn; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          a.dbias_slab[(size_t)split * a.Cout + n0 + wn * (WN / 2) + i * 16 + (lane >> 4) * 4 + r] = accb[i][r];
     }
     if (a.amax) {  // the delayed scale of the next step: max |dZ| = max |e5m2| / 2^eg
-      vmax = wave_max(vmax) * inv;
+      const unsigned mb = max(max((unsigned)mlo.x, (unsigned)mlo.y), max((unsigned)mhi.x, (unsigned)mhi.y) >> 8);
+      float vmax = bf8_to_f32(mb);
+      vmax = wave_max(vmax) / *a.gmul;
       if (lane == 0 && vmax > 0.f) atomicMax(a.amax + (split & (kFp8AmaxSlots - 1)), __float_as_uint(vmax));
     }
   }
@@ -246,6 +301,16 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_fp8_kernel(ConvWgradFp8Args
 
 int wgrad_fp8_supported(int Cout, int Cin, int K) { return Cout == 160 && Cin == 160 && K == 3 ? 1 : 0; }
 
+template <int WN, int WC, int PROBE>
+static void launch_wgrad_fp8_t(const ConvWgradFp8Args& a, hipStream_t st) {
+  constexpr int smem = 2 * 2 * kImgBytes;  // two stages of two images
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_fp8_kernel<WN, WC, PROBE>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+  dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
+  hipLaunchKernelGGL((conv_wgrad_fp8_kernel<WN, WC, PROBE>), grid, dim3(256), smem, st, a);
+}
+
 void launch_conv_wgrad_fp8(const ConvWgradFp8Args& a_in, hipStream_t st) {
   ConvWgradFp8Args a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
@@ -253,12 +318,20 @@ void launch_conv_wgrad_fp8(const ConvWgradFp8Args& a_in, hipStream_t st) {
   if (!wgrad_fp8_supported(a.Cout, a.Cin, a.K))
     throw std::invalid_argument("conv_wgrad_fp8: 160 -> 160 3x3 layers only");
   constexpr int WN = 160, WC = 160;
-  constexpr int smem = 2 * 2 * kImgBytes;  // two stages of two images
-  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_fp8_kernel<WN, WC>,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
-  dim3 grid(a.nsplit, a.T, (a.Cout / WN) * (a.Cin / WC));
-  hipLaunchKernelGGL((conv_wgrad_fp8_kernel<WN, WC>), grid, dim3(256), smem, st, a);
+#ifdef AGK_KERNEL_LAB
+  switch (a.probe) {
+    case 0: launch_wgrad_fp8_t<WN, WC, 0>(a, st); break;
+#define AGK_WG8_PROBE(P) \
+  case P: launch_wgrad_fp8_t<WN, WC, P>(a, st); break;
+    AGK_WG8_PROBE(1) AGK_WG8_PROBE(2) AGK_WG8_PROBE(4) AGK_WG8_PROBE(8) AGK_WG8_PROBE(3) AGK_WG8_PROBE(5)
+    AGK_WG8_PROBE(6) AGK_WG8_PROBE(7) AGK_WG8_PROBE(14) AGK_WG8_PROBE(15)
+#undef AGK_WG8_PROBE
+    default: throw std::invalid_argument("conv_wgrad_fp8: probe " + std::to_string(a.probe));
+  }
+#else
+  if (a.probe != 0) throw std::invalid_argument("conv_wgrad_fp8: timing probes are kernel-lab code");
+  launch_wgrad_fp8_t<WN, WC, 0>(a, st);
+#endif
 }
 
 int wgrad_fp8_stage_pixels() { return kStepPx; }

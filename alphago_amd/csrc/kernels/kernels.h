@@ -67,6 +67,7 @@ struct ConvWgradFp8Args {
   int HPi, offi, HPo, Po;
   int ksteps_per_split, nsplit;  // in 128-pixel steps
   FastDiv divSS, divS;           // filled by the launcher
+  int probe;                     // kernel-lab timing probe (0 = production)
 };
 int wgrad_fp8_supported(int Cout, int Cin, int K);
 int wgrad_fp8_stage_pixels();

@@ -198,7 +198,8 @@ inline void conv_wgrad_impl(const Tensor& x, const Tensor& dz, const Tensor& sla
 // fp8 wgrad: x8 e4m3 (B, HPi, HPi, Cin) uint8, dz8 e5m2 (B, HPo, HPo, Cout) uint8, slabs as conv_wgrad_impl
 inline void conv_wgrad_fp8_impl(const Tensor& x8, const Tensor& dz8, const Tensor& slab, const Tensor& dbslab,
                                 const Tensor& xscale, const Tensor& gscale, const Tensor& gmul, int64_t K, int64_t S,
-                                int64_t Pin, int64_t Po, const c10::optional<Tensor>& amax = c10::nullopt) {
+                                int64_t Pin, int64_t Po, const c10::optional<Tensor>& amax = c10::nullopt,
+                                int probe = 0) {
   check_dev("conv_wgrad_fp8", x8, dz8, slab, dbslab, xscale, gscale, gmul, amax);
   TORCH_CHECK(x8.scalar_type() == at::kByte && dz8.scalar_type() == at::kByte, "x8 / dz8: uint8 (e4m3 / e5m2)");
   CHECK_F32(slab); CHECK_F32(dbslab);
@@ -234,6 +235,7 @@ inline void conv_wgrad_fp8_impl(const Tensor& x8, const Tensor& dz8, const Tenso
   const int nks = (a.M + sp - 1) / sp;
   a.nsplit = (int)nsplit;
   a.ksteps_per_split = (nks + a.nsplit - 1) / a.nsplit;
+  a.probe = probe;
   if (a.M == 0) return;
   agk::launch_conv_wgrad_fp8(a, cur_stream());
   launch_check("conv_wgrad_fp8");

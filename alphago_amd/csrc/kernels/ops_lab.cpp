@@ -51,6 +51,12 @@ void conv_fwd_fp8_lab(const Tensor& x, const Tensor& w, const Tensor& bias, cons
                     mbits);
 }
 
+void conv_wgrad_fp8_lab(const Tensor& x8, const Tensor& dz8, const Tensor& slab, const Tensor& dbslab,
+                        const Tensor& xscale, const Tensor& gscale, const Tensor& gmul, int64_t K, int64_t S,
+                        int64_t Pin, int64_t Po, const c10::optional<Tensor>& amax, int64_t probe) {
+  conv_wgrad_fp8_impl(x8, dz8, slab, dbslab, xscale, gscale, gmul, K, S, Pin, Po, amax, (int)probe);
+}
+
 int64_t wgrad_tap_group_lab(int64_t cout, int64_t cin, int64_t K, int64_t variant) {
   return agk::wgrad_tap_group((int)cout, (int)cin, (int)K, (int)variant);
 }
@@ -163,6 +169,9 @@ TORCH_LIBRARY(alphago_amd_lab, m) {
       "conv_fwd_fp8(Tensor x, Tensor w, Tensor bias, Tensor scales, Tensor out_scale, Tensor(a!)? amax, "
       "Tensor(b!)? y_bf16, Tensor(c!)? y_fp8, int K, int S, int Pin, int Po, int variant, Tensor(d!)? mbits=None) -> ()");
   m.def(
+      "conv_wgrad_fp8(Tensor x8, Tensor dz8, Tensor(a!) slab, Tensor(b!) dbslab, Tensor xscale, Tensor gscale, "
+      "Tensor gmul, int K, int S, int Pin, int Po, Tensor(c!)? amax, int probe) -> ()");
+  m.def(
       "conv_fwd_pk(Tensor x, Tensor w, Tensor bias, Tensor(a!) y, int K, int S, int Pin, int Po, int cin_real, "
       "Tensor(b!)? mbits=None) -> ()");
   m.def("wgrad_tap_group(int cout, int cin, int K, int variant) -> int", &wgrad_tap_group_lab);
@@ -180,6 +189,7 @@ TORCH_LIBRARY_IMPL(alphago_amd_lab, CUDA, m) {
   m.impl("conv_fwd", &conv_fwd_lab);
   m.impl("conv_wgrad", &conv_wgrad_lab);
   m.impl("conv_fwd_fp8", &conv_fwd_fp8_lab);
+  m.impl("conv_wgrad_fp8", &conv_wgrad_fp8_lab);
   m.impl("conv_fwd_pk", &conv_fwd_pk_lab);
   m.impl("ladder_planes", &ladder_planes);
 }
