@@ -661,11 +661,14 @@ static void launch_fp8_ga_cw(const ConvFp8Args& a, hipStream_t st) {
 // training forward), same-box lab A/B (scripts/r5/fp8_probe2.py): 120.3 us (8 waves, direct
 // 4-B stores) -> 116.3 (staged) / 109.4 (4 waves) -> 101.4 (both); bf16 + e4m3 outputs 138.6 -> 115.2
 // (4-wave workgroups only with 32-channel chunks: the 64-channel packing's extra weight pieces spill).
+// The 192-wide policy tile stages its byte outputs too, with 8-wave workgroups (4 waves spill 23-81
+// VGPRs there): B = 1024, same-box lab A/B (lab 7 = the staged tile, scripts/r5/gpu49.sh): e4m3
+// output 151.6 -> 146.8 us, e4m3 + bitmask 156.3 -> 148.2, bf16 + e4m3 185.5 -> 161.9; B = 64 34.5 -> 33.2.
 // NW = 0 / STGE = -1: this policy; lab variants pass explicit values
 template <int BN, int MB, int NPART, bool OB, bool OF, bool DG = false, bool DGB = false, bool DGBITS = false,
           int NW = 0, int STGE = -1>
 static void launch_fp8_ga(const ConvFp8Args& a, hipStream_t st) {
-  constexpr bool stg = STGE >= 0 ? STGE != 0 : BN == 160;
+  constexpr bool stg = STGE >= 0 ? STGE != 0 : (BN == 160 || BN == 192);
   if (a.cw == 32) launch_fp8_ga_cw<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, 32, NW ? NW : (BN == 160 ? 4 : 8), stg>(a, st);
   else launch_fp8_ga_cw<BN, MB, NPART, OB, OF, DG, DGB, DGBITS, 64, NW ? NW : 8, stg>(a, st);
 }
@@ -743,6 +746,7 @@ static void launch_fp8_t(const ConvFp8Args& a, hipStream_t st) {
         else if (a.variant == 3) launch_fp8_ga<BN, 2, 3, OB, OF>(a, st);
         else if (a.variant == 4) launch_fp8_ga<BN, 3, 6, OB, OF>(a, st);
         else if (a.variant == 6) launch_fp8_ga<BN, 3, 4, OB, OF, false, false, false, 4, 1>(a, st);
+        else if (a.variant == 7) launch_fp8_ga<BN, 3, 4, OB, OF, false, false, false, 8, 0>(a, st);  // round 4
         else launch_fp8_ga<BN, 2, 2, OB, OF>(a, st);
 #endif
       } else {

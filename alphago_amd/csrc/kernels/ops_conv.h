@@ -307,8 +307,8 @@ inline void conv_fwd_fp8_impl(const Tensor& x, const Tensor& w, const Tensor& bi
     a.sr_seed = sr_seed->data_ptr<int>();
   }
   if (mbits.has_value()) {
-    TORCH_CHECK(!dgrad_mask.has_value() && (variant == 0 || variant == 6 || variant > 100),
-                "mbits: the production forward, its round-4 tiling (lab 6) or a lab probe");
+    TORCH_CHECK(!dgrad_mask.has_value() && (variant == 0 || variant == 6 || variant == 7 || variant > 100),
+                "mbits: the production forward, its lab tilings 6 / 7 or a lab probe");
     CHECK_DEV(*mbits);
     TORCH_CHECK(mbits->scalar_type() == at::kInt && mbits->is_contiguous(), "mbits int32");
     const int64_t words = (Cout == 160 ? 1 : Cout % 192 == 0 ? Cout / 192 : Cout % 128 == 0 ? Cout / 128 : Cout / 64) * 8;

@@ -13,9 +13,11 @@ from alphago_amd import ops  # noqa: E402
 dev = torch.device("cuda:0")
 ops.load()
 B = int(os.environ.get("P_B", "1024"))
-S, K, C = 19, 3, 160
+S, K = 19, 3
+C = int(os.environ.get("P_C", "160"))  # 160 (value) or 192 (policy)
 x8 = torch.randint(0, 0x38, (B, S + 2, S + 2, C), dtype=torch.uint8, device=dev)
-w = torch.randn(152, 152, K, K, device=dev) * 0.05
+CR = 152 if C == 160 else C
+w = torch.randn(CR, CR, K, K, device=dev) * 0.05
 w8, ew = ops.pack_weights_fp8(w, C, C)
 bias = torch.zeros(C, device=dev)
 scales = torch.tensor([127, 127 - ew], dtype=torch.int32, device=dev)
@@ -26,7 +28,7 @@ y8 = torch.zeros((B, S + 2, S + 2, C), dtype=torch.uint8, device=dev)
 # P_OUT: "both" = bf16 + e4m3 outputs; "fp8mb" = the fp8 value-training forward (e4m3 + ReLU' bitmask)
 OUT = os.environ.get("P_OUT", "both")
 mb = torch.zeros(B * (S + 2) * (S + 2) * ops.mbits_words(C), dtype=torch.int32, device=dev) if OUT == "fp8mb" else None
-if OUT == "fp8mb":
+if OUT in ("fp8mb", "fp8"):  # "fp8": the inference chain's e4m3-only output
     yb = None
 variants = [int(v) for v in os.environ.get("P_VARIANTS", "0,101,102,104,108,116,106,114,130,131,117").split(",")]
 res = {v: [] for v in variants}
@@ -53,4 +55,4 @@ for _ in range(4):
         e1.record()
         torch.cuda.synchronize()
         res[v].append(e0.elapsed_time(e1) / 50 * 1e3)
-print(json.dumps({"B": B, "out": OUT, "cw": int(w8.shape[-1]), "us_per_call_min": {v: round(min(t), 1) for v, t in res.items()}}))
+print(json.dumps({"B": B, "C": C, "out": OUT, "cw": int(w8.shape[-1]), "us_per_call_min": {v: round(min(t), 1) for v, t in res.items()}}))

@@ -180,9 +180,10 @@ def test_conv_fwd_fp8_160(ops, cuda_device, monkeypatch, cw, B, Cin, Cin_p, K):
     assert torch.equal(d_bits, d_mask)
 
 
-def _fwd_fp8_160_case(ops, dev, B, seed=11):
+def _fwd_fp8_160_case(ops, dev, B, seed=11, Cp=160):
     torch.manual_seed(seed)
-    S, K, C, Cp = 19, 3, 152, 160
+    S, K = 19, 3
+    C = 152 if Cp == 160 else Cp
     x = F.relu(torch.randn(B, C, S, S, device=dev))
     xp = ops.to_padded(x, 1, Cp)
     ex = ops.fp8_exponent(float(x.abs().max()), margin=0)
@@ -194,25 +195,26 @@ def _fwd_fp8_160_case(ops, dev, B, seed=11):
     return x8, w8, bp, scales, torch.tensor([4.0], device=dev)
 
 
-def _fwd_fp8_160_outputs(ops, dev, B, outs):
-    S, Cp = 19, 160
+def _fwd_fp8_160_outputs(ops, dev, B, outs, Cp=160):
+    S = 19
     y8 = torch.zeros((B, S + 2, S + 2, Cp), dtype=torch.uint8, device=dev)
     yb = ops.padded_empty(B, S, 1, Cp, dev) if outs == "both" else None
     mbits = torch.zeros(B * (S + 2) ** 2 * ops.mbits_words(Cp), dtype=torch.int32, device=dev)
     return y8, yb, mbits, ops.fp8_amax_buffer(1, dev)[0]
 
 
+@pytest.mark.parametrize("Cp", [160, 192])
 @pytest.mark.parametrize("B", [1, 37])
-def test_conv_fwd_fp8_160_byte_outputs(ops, cuda_device, monkeypatch, B):
+def test_conv_fwd_fp8_160_byte_outputs(ops, cuda_device, monkeypatch, B, Cp):
     """The fp8 training forward's e4m3-only output (staged through LDS, 16-B row stores, ragged
     last tile at B = 37) equals the e4m3 copy written next to a bf16 output, with the same ReLU'
     bitmask and amax, and leaves the zero border untouched."""
     monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1")
     S = 19
-    x8, w8, bp, scales, osc = _fwd_fp8_160_case(ops, cuda_device, B)
+    x8, w8, bp, scales, osc = _fwd_fp8_160_case(ops, cuda_device, B, Cp=Cp)
     res = {}
     for outs in ("fp8", "both"):
-        y8, yb, mbits, amax = _fwd_fp8_160_outputs(ops, cuda_device, B, outs)
+        y8, yb, mbits, amax = _fwd_fp8_160_outputs(ops, cuda_device, B, outs, Cp=Cp)
         ops.conv_fwd_fp8(x8, w8, bp, scales, osc, 3, S, 1, 1, y_bf16=yb, y_fp8=y8, amax=amax, mbits=mbits)
         res[outs] = (y8, yb, mbits, amax)
     torch.cuda.synchronize()
@@ -227,17 +229,18 @@ def test_conv_fwd_fp8_160_byte_outputs(ops, cuda_device, monkeypatch, B):
     assert ((got - ref).abs() <= ref.abs() * 0.07 + 1e-3).all()
 
 
+@pytest.mark.parametrize("Cp,lab", [(160, 6), (192, 7)])
 @pytest.mark.parametrize("B", lab_params([1, 5, 37], []))
-def test_conv_fwd_fp8_160_matches_round4_tiling(ops, cuda_device, monkeypatch, B):
-    """Production 160-wide forward (4-wave workgroups, staged byte outputs) == the round-4 tiling
-    (lab variant 6: 8-wave workgroups, 4-B stores) byte for byte."""
+def test_conv_fwd_fp8_160_matches_round4_tiling(ops, cuda_device, monkeypatch, B, Cp, lab):
+    """Production fp8 forward with staged byte outputs (160: 4-wave workgroups too) == the
+    round-4 tiling (lab 6 / 7: 8-wave workgroups, 4-B stores) byte for byte."""
     monkeypatch.setenv("ALPHAGO_AMD_FP8_CW32", "1")
     S = 19
-    x8, w8, bp, scales, osc = _fwd_fp8_160_case(ops, cuda_device, B)
-    y8, yb, mbits, amax = _fwd_fp8_160_outputs(ops, cuda_device, B, "both")
+    x8, w8, bp, scales, osc = _fwd_fp8_160_case(ops, cuda_device, B, Cp=Cp)
+    y8, yb, mbits, amax = _fwd_fp8_160_outputs(ops, cuda_device, B, "both", Cp=Cp)
     ops.conv_fwd_fp8(x8, w8, bp, scales, osc, 3, S, 1, 1, y_bf16=yb, y_fp8=y8, amax=amax, mbits=mbits)
-    y8l, ybl, mbl, aml = _fwd_fp8_160_outputs(ops, cuda_device, B, "both")
-    ops.lab().conv_fwd_fp8(x8, w8, bp, scales, osc, aml, ybl, y8l, 3, S, 1, 1, 6, mbl)
+    y8l, ybl, mbl, aml = _fwd_fp8_160_outputs(ops, cuda_device, B, "both", Cp=Cp)
+    ops.lab().conv_fwd_fp8(x8, w8, bp, scales, osc, aml, ybl, y8l, 3, S, 1, 1, lab, mbl)
     torch.cuda.synchronize()
     assert torch.equal(y8, y8l) and torch.equal(yb, ybl) and torch.equal(mbits, mbl)
     # amax slots follow the workgroup index (different grids): the maximum over the slots agrees
