@@ -895,19 +895,25 @@ __global__ __launch_bounds__(1024) void fp8_weight_scales_kernel(Fp8WeightScales
   const int l = blockIdx.x;
   const float* w = a.w[l];
   const int n = a.n[l];
-  // eight independent loads in flight per thread (a one-load loop was latency-bound: 39.6 us per
-  // value-net repack, profiles/r4/raw/timeline_value_fp8_b1024.txt)
+  // eight independent 16-B loads in flight per thread: a layer is a few round trips of one
+  // workgroup (a one-load loop was latency-bound at 39.6 us per value-net repack, round 4; eight
+  // 4-B loads still took 25 round trips per 208k-weight layer, 56 us per repack in round 5's step)
   float m = 0.f;
-  for (int i0 = threadIdx.x; i0 < n; i0 += 8 * 1024) {
-    float v[8];
+  const int n4 = (((uintptr_t)w) & 15) == 0 ? n >> 2 : 0;  // 16-B aligned prefix (the flat
+                                                           // parameter buffer's views are)
+  const float4* w4 = reinterpret_cast<const float4*>(w);
+  for (int i0 = threadIdx.x; i0 < n4; i0 += 8 * 1024) {
+    float4 v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int i = i0 + k * 1024;
-      v[k] = i < n ? fabsf(w[i]) : 0.f;
+      v[k] = i < n4 ? w4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) m = fmaxf(m, v[k]);
+    for (int k = 0; k < 8; ++k)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
   }
+  for (int i = 4 * n4 + threadIdx.x; i < n; i += 1024) m = fmaxf(m, fabsf(w[i]));
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();

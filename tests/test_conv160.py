@@ -1,6 +1,8 @@
 """160-wide conv tiles (value net: 152 filters padded to 160, AlphaGo/models/value.py:7)
 vs plain PyTorch fp32: forward with straddled K-steps (Cin % 64 == 32), the
 ReLU'-bitmask dgrad, and the 160x160 / tap-merged 160x64 wgrad tiles."""
+import math
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -467,3 +469,22 @@ def test_dgrad_bits_bf8_copy(ops, cuda_device):
     deq = dx8.view(torch.float8_e5m2).float() * 2.0 ** -20
     assert _rel_err(deq, dx.float()) < 0.13
     assert abs(amax.view(torch.float32).max().item() - dx.float().abs().max().item()) <= 1e-2 * dx.float().abs().max().item()
+
+
+def test_fp8_weight_scales_matches_torch(ops, cuda_device):
+    """Per-layer e4m3 weight exponents (16-B vector loads over the aligned prefix, scalar tail and
+    misaligned views) == floor(log2(448 / max |w|)) from torch."""
+    torch.manual_seed(21)
+    flat = torch.randn(300000, device=cuda_device)
+    ws = [flat[0:207936].view(152, 152, 3, 3), flat[1:186201],  # a misaligned view
+          flat[200000:200000 + 1003] * 7.0, torch.randn(152, 49, 5, 5, device=cuda_device) * 1e-3]
+    L = len(ws)
+    wscale = torch.zeros(L, device=cuda_device)
+    scales8 = torch.full((L, 2), 127, dtype=torch.int32, device=cuda_device)
+    ops.fp8_weight_scales(ws, wscale, scales8)
+    torch.cuda.synchronize()
+    for l, w in enumerate(ws):
+        m = w.abs().max().item()
+        e = max(-60, min(60, math.floor(math.log2(448.0 / m))))
+        assert wscale[l].item() == 2.0 ** e, (l, wscale[l].item(), e)
+        assert scales8[l, 1].item() == 127 - e and scales8[l, 0].item() == 127
