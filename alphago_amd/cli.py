@@ -107,9 +107,7 @@ def _match(argv):
     return res
 
 
-class _Exit(int):
-    """An explicit process exit code (commands' own return values, e.g. a
-    position count, are results, not exit codes)."""
+from .parallel.launch import ExitCode as _Exit  # noqa: E402  (explicit process exit codes)
 
 
 def main(argv: Optional[List[str]] = None) -> int:
@@ -158,7 +156,7 @@ def _dispatch(argv: List[str]):
         sys.path.insert(0, root)
         import bench
         sys.argv = ["bench.py"] + rest
-        return bench.main()
+        return _Exit(bench.main() or 0)
     print("unknown command %r\n%s" % (cmd, __doc__))
     return _Exit(2)
 

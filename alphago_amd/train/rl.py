@@ -31,6 +31,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 from typing import List, Optional
 
@@ -40,6 +41,7 @@ import torch
 from .. import go
 from ..models.policy import CNNPolicy
 from ..parallel import dist as agdist
+from ..parallel.launch import add_gpus_arg, cli_ranks, exit_status
 from ..search.selfplay import BatchedSampler, play_games
 from ..utils import faults
 from ..utils.metrics import MetricsLogger
@@ -172,11 +174,16 @@ def _parser():
     p.add_argument("--resume", action="store_true", help="continue from rl_checkpoint.pt if it exists")
     p.add_argument("--watchdog-timeout", type=float, default=0.0,
                    help="exit a rank that makes no progress for this many seconds (0: off)")
+    add_gpus_arg(p)
     return p
 
 
 def run(cmd_line_args: Optional[List[str]] = None) -> dict:
-    args = _parser().parse_args(cmd_line_args)
+    argv = list(sys.argv[1:] if cmd_line_args is None else cmd_line_args)
+    args = _parser().parse_args(argv)
+    code = cli_ranks("train-rl", args, argv)
+    if code is not None:
+        return code
     env = agdist.init_from_env()
     dev = env.device
     rng = np.random.default_rng(args.seed * 7919 + env.rank)
@@ -267,4 +274,4 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
 
 
 if __name__ == "__main__":
-    run()
+    sys.exit(exit_status(run()))

@@ -34,6 +34,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 from typing import List, Optional
 
@@ -44,6 +45,7 @@ from ..data.dataset import PositionDataset, block_shuffle, shard_rows
 from ..io.h5lite import H5File
 from ..models.policy import CNNPolicy
 from ..parallel import dist as agdist
+from ..parallel.launch import add_gpus_arg, cli_ranks, exit_status
 from ..utils import faults
 from ..utils.config import RunConfig
 from ..utils.metrics import MetricsLogger, StepMetrics
@@ -110,11 +112,16 @@ def _parser():
     p.add_argument("--profile", default=None, help="write torch.profiler traces + summary to this directory")
     p.add_argument("--graph", action="store_true",
                    help="HIP backend: run each step as a HIP-graph replay (launch-bound small minibatches)")
+    add_gpus_arg(p)
     return p
 
 
 def run_training(cmd_line_args: Optional[List[str]] = None):
-    args = _parser().parse_args(cmd_line_args)
+    argv = list(sys.argv[1:] if cmd_line_args is None else cmd_line_args)
+    args = _parser().parse_args(argv)
+    code = cli_ranks("train-sl", args, argv)
+    if code is not None:
+        return code
     env = agdist.init_from_env()
     dev = env.device
     resume = args.weights is not None
@@ -305,4 +312,4 @@ def _validate(trainer, dataset, mine, B, dev):
 
 
 if __name__ == "__main__":
-    run_training()
+    sys.exit(exit_status(run_training()))

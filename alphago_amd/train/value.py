@@ -24,6 +24,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import sys
 import time
 from typing import List, Optional
 
@@ -36,6 +37,7 @@ from ..features import VALUE_FEATURES, Preprocess
 from ..io.h5lite import H5File, H5Writer
 from ..models.policy import CNNPolicy, CNNValue
 from ..parallel import dist as agdist
+from ..parallel.launch import add_gpus_arg, cli_ranks, exit_status
 from ..search.selfplay import BatchedSampler
 from ..utils import faults
 from ..utils.metrics import MetricsLogger, StepMetrics
@@ -109,7 +111,12 @@ def generate_cli(argv=None):
     p.add_argument("--max-u", type=int, default=450)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--keep-shards", action="store_true", help="keep the per-rank files after merging")
+    add_gpus_arg(p)
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = p.parse_args(argv)
+    code = cli_ranks("value-generate", a, argv)
+    if code is not None:
+        return code
     env = agdist.init_from_env()
     sl = CNNPolicy.load_model(a.sl_json, device=env.device)
     rl = CNNPolicy.load_model(a.rl_json, device=env.device)
@@ -230,7 +237,12 @@ def train_cli(argv=None):
                    help="continue from out_directory/checkpoint.pt if it exists (exact step, RNG, cursor)")
     p.add_argument("--watchdog-timeout", type=float, default=0.0,
                    help="exit a rank that makes no progress for this many seconds (0: off)")
+    add_gpus_arg(p)
+    argv = list(sys.argv[1:] if argv is None else argv)
     a = p.parse_args(argv)
+    code = cli_ranks("train-value", a, argv)
+    if code is not None:
+        return code
     env = agdist.init_from_env()
     dev = env.device
     world, rank = env.world_size, env.rank
@@ -352,9 +364,6 @@ def train_cli(argv=None):
 
 
 if __name__ == "__main__":
-    import sys
-
     if len(sys.argv) > 1 and sys.argv[1] == "generate":
-        generate_cli(sys.argv[2:])
-    else:
-        train_cli(sys.argv[2:] if len(sys.argv) > 1 and sys.argv[1] == "train" else sys.argv[1:])
+        sys.exit(exit_status(generate_cli(sys.argv[2:])))
+    sys.exit(exit_status(train_cli(sys.argv[2:] if len(sys.argv) > 1 and sys.argv[1] == "train" else sys.argv[1:])))

@@ -74,4 +74,7 @@ def train_batch(player, X_list, y_list, winners, lr, trainer=None):
 __all__ = ["make_training_pairs", "train_batch", "run"]
 
 if __name__ == "__main__":
-    run()
+    import sys
+
+    from ..parallel.launch import exit_status
+    sys.exit(exit_status(run()))

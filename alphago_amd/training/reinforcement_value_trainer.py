@@ -9,4 +9,7 @@ from ..train.value import train_cli as run_training
 __all__ = ["generate", "run_training"]
 
 if __name__ == "__main__":
-    run_training()
+    import sys
+
+    from ..parallel.launch import exit_status
+    sys.exit(exit_status(run_training()))

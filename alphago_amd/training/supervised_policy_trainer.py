@@ -70,4 +70,7 @@ __all__ = ["run_training", "MetadataWriterCallback", "BOARD_TRANSFORMATIONS", "o
            "shuffled_hdf5_batch_generator"]
 
 if __name__ == "__main__":
-    run_training()
+    import sys
+
+    from ..parallel.launch import exit_status
+    sys.exit(exit_status(run_training()))

@@ -11,6 +11,7 @@ checkpoints are reachable offline).
 Single GPU:   python bench.py --steps 20 --warmup 5
 N GPUs:       python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
                   --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+          or    python bench.py --gpus N   (starts the N ranks itself, parallel/launch.py)
 Weak scaling: the per-GPU batch is fixed; the global batch is N x per-GPU batch.
 Rank 0 prints ONE JSON line.
 """
@@ -20,18 +21,13 @@ import os
 import sys
 import time
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-
-from alphago_amd.models.nets import PolicyNet  # noqa: E402
-from alphago_amd.parallel import dist as agdist  # noqa: E402
-from alphago_amd.train.engine import make_policy_trainer  # noqa: E402
 
 PAPER_SL_POS_PER_S = 3000.0  # paper SL throughput, 50 GPUs aggregate (derived)
 
 
 def teacher_pool_on_device(args, dev, rank):
+    import torch
     """Teacher-labelled pool (alphago_amd/data/synthetic.py): the same fixed teacher on every rank,
     a different position stream per rank; the teacher is freed before the student trains."""
     from alphago_amd.data.synthetic import teacher_pool
@@ -86,7 +82,22 @@ def main():
                     help="after the timed run, profile 6 more steps (torch.profiler + roctx ranges) into DIR")
     args = ap.parse_args()
 
+    # `python bench.py --gpus N` without torchrun: this process only supervises N ranks started by
+    # torch.distributed.run (it never touches the GPU); a torchrun world that differs from --gpus, or
+    # fewer visible GPUs than --gpus, is refused (alphago_amd/parallel/launch.py).
+    from alphago_amd.parallel.launch import ensure_ranks
+    code = ensure_ranks(args.gpus, [os.path.abspath(__file__)], sys.argv[1:], require_gpu=args.backend == "hip")
+    if code is not None:
+        return code
+
+    import torch
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.parallel import dist as agdist
+    from alphago_amd.train.engine import make_policy_trainer
+
     env = agdist.init_from_env()
+    if env.world_size != args.gpus:  # belt and braces: the JSON line must describe the world that ran
+        raise SystemExit("bench.py: --gpus %d but the process group has %d ranks" % (args.gpus, env.world_size))
     dev = env.device
     torch.manual_seed(1234 + env.rank)
     net = PolicyNet(args.planes, board=19, filters_per_layer=args.filters, layers=args.layers)
@@ -224,7 +235,8 @@ def main():
         if dev.type == "cuda":
             torch.cuda.synchronize()
     agdist.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -54,3 +54,47 @@ def test_bench_json_line_under_torchrun(nproc):
     assert out["warmup_steps_run"] >= 1 and (out["warmup_steps_run"] - 1) % 10 == 0 and out["warmup_s"] >= 0.5
     # value is the whole-job rate: global positions over the (max-over-ranks) timed span
     assert abs(out["value"] - 2 * nproc * 2 / (out["ms_per_step"] * 2 / 1e3)) / out["value"] < 0.01
+
+
+def _plain_bench(extra, env_extra=None, timeout=600):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--batch", "2",
+           "--filters", "8", "--layers", "3", "--pool", "16", "--min-warmup-s", "0.5"] + extra
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_plain_launch_starts_the_ranks():
+    """`python bench.py --gpus 4` with no torchrun: bench.py supervises 4 ranks itself and the one JSON
+    line describes the 4-rank world (before round 6 it silently measured one rank)."""
+    p = _plain_bench(["--gpus", "4", "--backend", "torch"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["world_size"] == 4 and out["dist_backend"] == "gloo"
+    assert out["config"]["global_batch"] == 8 and out["config"]["parallelism"] == "dp4"
+    assert len(out["rank_ms_per_step"]) == 4
+
+
+def test_bench_refuses_world_mismatch():
+    """--gpus 2 inside a 4-rank torchrun world is refused (non-zero exit, no JSON line)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--backend", "torch", "--batch", "2", "--filters", "8", "--layers", "3", "--pool", "16"]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert "WORLD_SIZE=4" in p.stderr
+
+
+def test_bench_refuses_missing_gpus():
+    """The HIP backend with --gpus 2 and no visible GPU exits 2 with a message instead of running."""
+    p = _plain_bench(["--gpus", "2", "--backend", "hip"], timeout=300)
+    assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
+    assert "GPU(s) are visible" in p.stderr
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

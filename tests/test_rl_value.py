@@ -365,3 +365,42 @@ def test_rl_two_ranks_cli(tmp_path):
     its = [x for x in recs if "games" in x]
     assert len(its) == 2 and all(x["games"] == 4 for x in its)  # both ranks' games counted
 
+
+
+def test_value_pipeline_gpus_flag_without_torchrun(tmp_path):
+    """`python -m alphago_amd value-generate/train-value --gpus 2` with no torchrun starts the two
+    ranks itself (parallel/launch.py): the same merged dataset and per-rank shards as the torchrun form."""
+    import json
+    import subprocess
+    import sys
+
+    from alphago_amd.io.h5lite import H5File
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", PYTHONPATH=root)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ALPHAGO_AMD_FAULT"):
+        env.pop(k, None)
+
+    def cli(argv):
+        return subprocess.run([sys.executable, "-m", "alphago_amd"] + argv, env=env, timeout=400,
+                              capture_output=True, text=True)
+
+    j, w = _save_policy(tmp_path, "cpu")
+    data = str(tmp_path / "v.h5")
+    r = cli(["value-generate", j, j, data, "--games", "6", "--batch-games", "6", "--max-u", "15", "--gpus", "2"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    with H5File(data) as f:
+        n = f["states"].shape[0]
+        assert 6 < n <= 12  # both ranks' games
+    v = CNNValue(VALUE_FEATURES, board=9, filters_per_layer=8, layers=2, dense=16, device=torch.device("cpu"))
+    vj = str(tmp_path / "v.json")
+    v.save_model(vj)
+    out = str(tmp_path / "vout")
+    r = cli(["train-value", vj, data, out, "-B", "2", "-E", "1", "--backend", "torch", "--gpus", "2",
+             "--train-val-test", "0.8", "0.2", "0.0"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    meta = json.load(open(os.path.join(out, "metadata.json")))
+    assert len(meta["data"]["rows_per_rank"]) == 2
+    # a --backend hip request for more GPUs than are visible is refused, not run on fewer
+    r = cli(["train-value", vj, data, out + "2", "--backend", "hip", "--gpus", "2"])
+    assert r.returncode == 2 and "GPU(s) are visible" in r.stderr
