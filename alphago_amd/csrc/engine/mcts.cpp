@@ -69,8 +69,10 @@ void Forest::set_root(int t, const GameState& s) {
   tr.nodes.push_back(make_node(-1, PASS, 1.f));
   tr.sims = 0;
   lad_records_ -= (int64_t)tr.lad.size();
+  lad_bytes_ -= tr.lad_bytes;
   tr.lad.clear();
   tr.lad_rep.clear();
+  tr.lad_bytes = 0;
 }
 
 int Forest::select_child(const SearchTree& tr, int u) const {
@@ -242,6 +244,11 @@ void Forest::leaf_features(uint8_t* out, int threads) const {
   });
 }
 
+// host bytes one cached record holds: the record, its entries (each with its read set) and the map node
+static inline int64_t ladder_record_bytes(const LadderRecord& r) {
+  return (int64_t)sizeof(LadderRecord) + (int64_t)r.e.capacity() * (int64_t)sizeof(LadderEntry) + 64;
+}
+
 void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* ladder, int threads) {
   int L = (int)pending_.size();
   if (L == 0) return;
@@ -310,10 +317,28 @@ void Forest::leaf_encode(int8_t* board, uint8_t* ages, int32_t* meta, uint8_t* l
     const int u = pending_[i].node;
     lad_reused_ += lad_fresh_[i].reused;
     lad_read_ += lad_fresh_[i].read;
-    if (lad_records_ >= kLadderRecordCap) continue;
+    const int64_t share = std::max<int64_t>(lad_budget_bytes_ / (int64_t)trees_.size(), 1 << 16);
+    const int64_t rb = ladder_record_bytes(lad_fresh_[i]);
+    if (tr.lad_bytes + rb > share && !tr.lad.empty()) {  // this tree's share is full: drop its records
+      lad_records_ -= (int64_t)tr.lad.size();
+      lad_bytes_ -= tr.lad_bytes;
+      tr.lad.clear();
+      tr.lad_rep.clear();
+      tr.lad_bytes = 0;
+      ++lad_evictions_;
+    }
     auto ins = tr.lad.emplace(u, LadderRecord());
-    if (ins.second) ++lad_records_;
+    if (ins.second) {
+      ++lad_records_;
+    } else {
+      const int64_t old = ladder_record_bytes(ins.first->second);
+      tr.lad_bytes -= old;
+      lad_bytes_ -= old;
+    }
     std::swap(ins.first->second, lad_fresh_[i]);  // (the fresh slot keeps a vector for the next batch)
+    const int64_t nb = ladder_record_bytes(ins.first->second);
+    tr.lad_bytes += nb;
+    lad_bytes_ += nb;
     const int pu = tr.nodes[u].parent;
     if (pu >= 0) tr.lad_rep.emplace(pu, u);
   }
@@ -516,8 +541,10 @@ void Forest::advance(int t, int move) {
     tr.nodes.clear();
     tr.nodes.push_back(make_node(-1, PASS, 1.f));
     lad_records_ -= (int64_t)tr.lad.size();
+    lad_bytes_ -= tr.lad_bytes;
     tr.lad.clear();
     tr.lad_rep.clear();
+    tr.lad_bytes = 0;
     return;
   }
   // BFS copy of the reused subtree (children stay contiguous)
@@ -553,10 +580,16 @@ void Forest::advance(int t, int move) {
       new_of[old_of[k]] = k;
     }
     auto nw = [&](int o) { return o >= 0 && o < (int)new_of.size() ? new_of[o] : -1; };
+    int64_t kept = 0;
     for (auto& kv : tr.lad) {
       const int k = nw(kv.first);
-      if (k >= 0) lad.emplace(k, std::move(kv.second));
+      if (k >= 0) {
+        kept += ladder_record_bytes(kv.second);
+        lad.emplace(k, std::move(kv.second));
+      }
     }
+    lad_bytes_ += kept - tr.lad_bytes;
+    tr.lad_bytes = kept;
     for (auto& kv : tr.lad_rep) {
       const int a = nw(kv.first), b = nw(kv.second);
       if (a >= 0 && b >= 0) rep.emplace(a, b);

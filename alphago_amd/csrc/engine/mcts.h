@@ -90,6 +90,7 @@ struct SearchTree {
   // children that was encoded (the reference of its siblings)
   std::unordered_map<int, LadderRecord> lad;
   std::unordered_map<int, int> lad_rep;
+  int64_t lad_bytes = 0;  // host bytes of lad (ladder_record_bytes)
   SearchTree() : root_state(19) {}
 };
 
@@ -133,6 +134,12 @@ class Forest {
     for (const Leaf& lf : held_) n += lf.tree == t;
     return n;
   }
+  // held leaves of every tree in one pass over the held batch (n_held_tree per tree is O(trees x held))
+  std::vector<int> held_counts() const {
+    std::vector<int> n(trees_.size(), 0);
+    for (const Leaf& lf : held_) ++n[lf.tree];
+    return n;
+  }
   // Unwind an interrupted search: the pending and the held batch lose their virtual losses and
   // queued status (their leaves become unexpanded again) and both lists are cleared, so set_root /
   // advance work afterwards.
@@ -156,14 +163,23 @@ class Forest {
     for (SearchTree& tr : trees_) {
       tr.lad.clear();
       tr.lad_rep.clear();
+      tr.lad_bytes = 0;
     }
     lad_records_ = 0;
+    lad_bytes_ = 0;
   }
-  // records held, reads taken from a reference, reads run
-  void ladder_cache_stats(int64_t& records, int64_t& reused, int64_t& read) const {
+  // host-memory budget of the ladder cache, forest-wide: each tree may hold budget / n_trees bytes of
+  // records; a tree that would exceed its share drops its own records (they are rebuilt as the search
+  // goes on) instead of the cache freezing.  advance() already drops the records outside the kept subtree.
+  void set_ladder_cache_bytes(int64_t bytes) { lad_budget_bytes_ = bytes < (1 << 20) ? (1 << 20) : bytes; }
+  int64_t ladder_cache_bytes() const { return lad_budget_bytes_; }
+  // records held, reads taken from a reference, reads run, bytes held, tree evictions
+  void ladder_cache_stats(int64_t& records, int64_t& reused, int64_t& read, int64_t& bytes, int64_t& evictions) const {
     records = lad_records_;
     reused = lad_reused_;
     read = lad_read_;
+    bytes = lad_bytes_;
+    evictions = lad_evictions_;
   }
   // priors (L, n*n) float32 (any non-negative scores; renormalised over sensible moves), values (L,);
   // mask (L, n*n) optional sensible-move mask (e.g. from the GPU featurizer) — skips the legality/eye scan
@@ -220,8 +236,8 @@ class Forest {
   int nplanes_ = 0;
   int64_t total_evals_ = 0;
   bool ladder_cache_ = true;
-  int64_t lad_records_ = 0, lad_reused_ = 0, lad_read_ = 0;
-  static constexpr int64_t kLadderRecordCap = 1 << 18;  // forest-wide (~0.3-1 KB each)
+  int64_t lad_records_ = 0, lad_reused_ = 0, lad_read_ = 0, lad_bytes_ = 0, lad_evictions_ = 0;
+  int64_t lad_budget_bytes_ = int64_t(256) << 20;  // forest-wide default (set_ladder_cache_bytes)
   std::vector<LadderRecord> lad_fresh_;
   int threads_ = 1;
   mutable std::unique_ptr<WorkPool> pool_;  // threads_ - 1 persistent workers (set_threads)

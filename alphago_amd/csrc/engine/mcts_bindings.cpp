@@ -84,6 +84,7 @@ void bind_mcts(py::module_& m) {
       .def("swap_held", &Forest::swap_held)
       .def("discard", &Forest::discard)
       .def("n_held_tree", &Forest::n_held_tree)
+      .def("held_counts", &Forest::held_counts)
       .def_property_readonly("n_held", &Forest::n_held)
       .def(
           "leaf_encode_into",
@@ -141,14 +142,18 @@ void bind_mcts(py::module_& m) {
       .def("clear_ladder_cache", &Forest::clear_ladder_cache)
       .def("ladder_cache_stats",
            [](const Forest& f) {
-             int64_t n, reused, read;
-             f.ladder_cache_stats(n, reused, read);
+             int64_t n, reused, read, bytes, ev;
+             f.ladder_cache_stats(n, reused, read, bytes, ev);
              py::dict d;
              d["records"] = n;
              d["reused"] = reused;
              d["read"] = read;
+             d["bytes"] = bytes;
+             d["evictions"] = ev;
+             d["budget_bytes"] = f.ladder_cache_bytes();
              return d;
            })
+      .def("set_ladder_cache_bytes", &Forest::set_ladder_cache_bytes, py::arg("bytes"))
       .def_property("rollout_policy", &Forest::rollout_policy, &Forest::set_rollout_policy)
       .def("add_root_noise", &Forest::add_root_noise, py::arg("tree"), py::arg("alpha") = 0.03,
            py::arg("eps") = 0.25)

@@ -329,6 +329,57 @@ static void launch_wgrad_160x160(const ConvWgradArgs& a, hipStream_t st) {
 
 int wgrad_stage_pixels() { return 32 * kWgradKsub; }
 
+// Split-free small-batch wgrad (kWgradDirect).  At B <= 16 the split-K plan spends ~10 us per layer on
+// its reduce launch beside a ~15 us wgrad (profiles/r5/README.md, B = 16 trace), and its one-round grid
+// gives each split only a few hundred pixels.  Here every workgroup owns one 32 (n) x WC (c) tile of
+// one tap over ALL B*S*S pixels: 6 x 4 x 9 = 216 workgroups for a 192 -> 192 3x3 layer (150 for the
+// 5x5 first layer's 48 real input planes), at most one per CU.  Each streams (32 + WC) channels x M
+// pixels through an LDS double buffer of KS 32-pixel sub-steps (one barrier per 32 KS pixels) and
+// writes its fp32 sums straight into the OIHW gradient (wgrad_store, grad_w != nullptr): deterministic
+// (one workgroup per output element, fixed pixel order), no slab and no reduce launch.
+template <int WC, int NWC, int KS>
+static void launch_wgrad_direct_t(const ConvWgradArgs& a, hipStream_t st) {
+  constexpr int WN = 32;
+  constexpr int smem = 2 * (WN + WC) * 64 * KS;
+  static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_kernel<WN, WC, KS, NWC>,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
+  dim3 grid(1, a.T, (a.Cout / WN) * (a.Cin / WC));
+  hipLaunchKernelGGL((conv_wgrad_kernel<WN, WC, KS, NWC>), grid, dim3(64 * 2 * NWC), smem, st, a);
+}
+
+// c tile of the split-free plan: 48 (192-multiple widths; the first layer's 48 real planes of 64), else 32
+int wgrad_direct_wc(int Cin, int cin_real) {
+  if (Cin == 64 && cin_real <= 48) return 48;
+  if (Cin % 48 == 0 && cin_real == Cin) return 48;
+  if (Cin % 32 == 0) return 32;
+  return 0;
+}
+
+bool wgrad_direct_supported(int Cout, int Cin, int cin_real, int K) {
+  return Cout % 32 == 0 && wgrad_direct_wc(Cin, cin_real) > 0 && (K == 1 || K == 3 || K == 5);
+}
+
+void launch_conv_wgrad_direct(const ConvWgradArgs& a_in, int ksub, hipStream_t st) {
+  ConvWgradArgs a = a_in;
+  a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
+  a.divS = make_fastdiv((uint32_t)a.S);
+  a.xcd_group = 0;
+  a.nsplit = 1;
+  if (!a.grad_w || !wgrad_direct_supported(a.Cout, a.Cin, a.cin_real, a.K))
+    throw std::invalid_argument("conv_wgrad_direct: needs grad_w, Cout % 32 == 0 and a 48 / 32 c tile");
+  const int wc = wgrad_direct_wc(a.Cin, a.cin_real);
+  if (wc == 48) {
+    if (ksub == 4) launch_wgrad_direct_t<48, 3, 4>(a, st);
+    else if (ksub == 12) launch_wgrad_direct_t<48, 3, 12>(a, st);
+    else launch_wgrad_direct_t<48, 3, 8>(a, st);
+  } else {
+    if (ksub == 4) launch_wgrad_direct_t<32, 2, 4>(a, st);
+    else if (ksub == 12) launch_wgrad_direct_t<32, 2, 12>(a, st);
+    else launch_wgrad_direct_t<32, 2, 8>(a, st);
+  }
+}
+
 // tap-pair / line-staged wgrads (variants 6-8): kernel lab (conv_lab.hip, profiles/r3_wgrad_pair.md)
 static bool wgrad_pair_applies(int Cout, int Cin, int cin_real, int K) {
   return K == 3 && Cout == 192 && Cin == 192 && cin_real == Cin;
@@ -388,19 +439,11 @@ void wgrad_plan(int Cout, int Cin, int cin_real, int K, int variant, int out[4])
   out[3] = c48 ? 384 : (wn == 160 && wc == 160) ? 256 : 512;
 }
 
-static int wgrad_xcd_group() {
-  static const int on = [] {
-    const char* e = getenv("AGK_WGRAD_XCD");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return on;
-}
-
 void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
   ConvWgradArgs a = a_in;
   a.divSS = make_fastdiv((uint32_t)(a.S * a.S));
   a.divS = make_fastdiv((uint32_t)a.S);
-  a.xcd_group = wgrad_xcd_group();
+  a.xcd_group = 1;  // kernel-row workgroups of a split on one XCD (conv_wgrad_kernel)
 #ifdef AGK_KERNEL_LAB
   if (a.variant == 5) {
     // one-kernel-row wgrad (conv_wgrad_row.hip), kernel lab: in the power-limited steady state it ran

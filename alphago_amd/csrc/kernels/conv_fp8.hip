@@ -934,13 +934,23 @@ void launch_fp8_weight_scales(const Fp8WeightScalesArgs& a, int L, hipStream_t s
 // Delayed activation scaling: from this step's per-layer output amax set the
 // next step's e4m3 exponents (input of layer l+1 = output of layer l) with
 // `margin` bits of headroom, then clear the amax accumulators.
-__global__ void fp8_act_scales_kernel(unsigned* amax, int* scales8, float* osc, int L, int margin) {
+// Underflow guard (max_drop > 0): the exponent falls by at most max_drop binades per step.  After a
+// loss spike the amax of a layer can grow 2^8 within a few steps; following it at once pushed the bulk
+// of the e4m3 activations below the format's smallest subnormal, round-to-nearest flushed them to zero
+// and the trunk died (SL at lr 0.05, 1 seed of 3, profiles/r5/README.md).  Under the guard the outliers
+// saturate at +-448 (a clip) while the scale follows at max_drop binades per step; a falling amax
+// (growing exponent) is followed at once.  max_drop 0: the plain one-step delayed scale.
+__global__ void fp8_act_scales_kernel(unsigned* amax, int* scales8, float* osc, int L, int margin, int max_drop) {
   const int l = threadIdx.x;
   if (l >= L) return;
   unsigned mu = 0u;
   for (int k = 0; k < kFp8AmaxSlots; ++k) mu = max(mu, amax[l * kFp8AmaxSlots + k]);
   const float m = __uint_as_float(mu);
   int e = (m > 0.f) ? (int)floorf(log2f(448.f / m)) - margin : 0;
+  if (max_drop > 0 && l + 1 < L) {
+    const int e_prev = 127 - scales8[2 * (l + 1)];
+    if (e < e_prev - max_drop) e = e_prev - max_drop;
+  }
   e = e < -60 ? -60 : (e > 60 ? 60 : e);
   if (l + 1 < L) {
     osc[l] = exp2f((float)e);
@@ -949,8 +959,8 @@ __global__ void fp8_act_scales_kernel(unsigned* amax, int* scales8, float* osc, 
   for (int k = 0; k < kFp8AmaxSlots; ++k) amax[l * kFp8AmaxSlots + k] = 0u;
 }
 
-void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st) {
-  hipLaunchKernelGGL(fp8_act_scales_kernel, dim3(1), dim3(64), 0, st, amax, scales8, osc, L, margin);
+void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, int max_drop, hipStream_t st) {
+  hipLaunchKernelGGL(fp8_act_scales_kernel, dim3(1), dim3(64), 0, st, amax, scales8, osc, L, margin, max_drop);
 }
 
 // Delayed gradient scaling for the fp8 dgrad chain: from this step's amax of dZ_l set the next

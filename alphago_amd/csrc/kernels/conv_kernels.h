@@ -697,6 +697,36 @@ __device__ __forceinline__ void wgrad_store(const ConvWgradArgs& a,
   constexpr int NBn = WN / (16 * NWN), NBc = WC / (16 * NWC);
   const int nb0 = n0 + wn * (WN / NWN) + ((lane >> 4) << 2);
   const int cbase = c0 + wc * (WC / NWC) + (lane & 15);
+  if (a.grad_w) {  // split-free plan: this workgroup holds the whole pixel sum -> the OIHW gradient
+    const float sc = a.scale, be = a.beta;
+#pragma unroll
+    for (int tp = 0; tp < TAPS; ++tp)
+#pragma unroll
+      for (int i = 0; i < NBn; ++i)
+#pragma unroll
+        for (int j = 0; j < NBc; ++j) {
+          const int c = cbase + j * 16;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int n = nb0 + i * 16 + r;
+            if (n < a.cout_real && c < a.cin_real) {
+              float* g = a.grad_w + ((size_t)n * a.cin_real + c) * a.T + t + tp;
+              *g = (be != 0.f ? be * *g : 0.f) + sc * acc[tp][i][j][r];  // beta 0: no read of g
+            }
+          }
+        }
+    if (do_bias && a.grad_b) {
+#pragma unroll
+      for (int i = 0; i < NBn; ++i) {
+        float s = dbs[i];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        const int n = n0 + wn * (WN / NWN) + i * 16 + lane;
+        if (lane < 16 && n < a.cout_real) a.grad_b[n] = (be != 0.f ? be * a.grad_b[n] : 0.f) + sc * s;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int tp = 0; tp < TAPS; ++tp) {
     float* out = a.slab + ((size_t)split * a.T + t + tp) * (size_t)a.Cout * a.Cin;

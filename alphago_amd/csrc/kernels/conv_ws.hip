@@ -467,6 +467,14 @@ static RingGeo ring_geometry(int S, int HPi, int offi, int K) {
   return r;
 }
 
+template <auto KERN>
+static void ws_go(dim3 grid, dim3 block, int smem, hipStream_t st, const ConvFwdArgs& a, const WsParams& p) {
+  static const hipError_t e =
+      hipFuncSetAttribute((const void*)KERN, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hip_check(e, "hipFuncSetAttribute(max dynamic LDS)");
+  hipLaunchKernelGGL(KERN, grid, block, smem, st, a, p);
+}
+
 template <int NBLK, int KW, int NWV, int NE, bool RING, int PROBE = 0>
 static void launch_ws_t(const ConvFwdArgs& a, int mode, WsParams p, hipStream_t st) {
   // partials of two chunks + the bitmask words being assembled (+ the input-row ring)
@@ -487,20 +495,17 @@ static void launch_ws_t(const ConvFwdArgs& a, int mode, WsParams p, hipStream_t 
                                   std::to_string(a.S) + ", Cin " + std::to_string(a.Cin) + ")");
   }
   const dim3 grid(8 * p.k * p.gper), block(64 * (NWV + NE));
-  auto go = [&](auto kern) {
-    static const hipError_t e =
-        hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    hip_check(e, "hipFuncSetAttribute(max dynamic LDS)");
-    hipLaunchKernelGGL(kern, grid, block, smem, st, a, p);
-  };
+  // one attribute call per kernel instantiation: the kernel is a template argument of ws_go, so every
+  // mode has its own static (a generic lambda over the kernel pointer shares ONE instantiation -- and
+  // one static -- between all modes, because their pointers have the same type)
   if constexpr (PROBE != 0) {
     if (mode != MODE_BIAS_RELU) throw std::invalid_argument("conv_fwd tiles 1000+: mode 0 only");
-    go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_BIAS_RELU, RING, PROBE>);
+    ws_go<conv_ws_kernel<NBLK, KW, NWV, NE, MODE_BIAS_RELU, RING, PROBE>>(grid, block, smem, st, a, p);
     return;
   }
-  if (mode == MODE_BIAS_RELU) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_BIAS_RELU, RING>);
-  else if (mode == MODE_MASKBITS) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_MASKBITS, RING>);
-  else if (mode == MODE_NONE) go(conv_ws_kernel<NBLK, KW, NWV, NE, MODE_NONE, RING>);
+  if (mode == MODE_BIAS_RELU) ws_go<conv_ws_kernel<NBLK, KW, NWV, NE, MODE_BIAS_RELU, RING>>(grid, block, smem, st, a, p);
+  else if (mode == MODE_MASKBITS) ws_go<conv_ws_kernel<NBLK, KW, NWV, NE, MODE_MASKBITS, RING>>(grid, block, smem, st, a, p);
+  else if (mode == MODE_NONE) ws_go<conv_ws_kernel<NBLK, KW, NWV, NE, MODE_NONE, RING>>(grid, block, smem, st, a, p);
   else throw std::invalid_argument("conv_fwd tile 40: modes 0 (bias + ReLU), 2 (none) and 3 (bitmask dgrad)");
 }
 

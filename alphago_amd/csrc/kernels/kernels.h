@@ -51,6 +51,13 @@ struct ConvWgradArgs {
                        // 1-4 kernel-lab build only
   long long x_elems, dz_elems;  // tensor extents (debug-build bounds checks)
   int xcd_group;       // filled by the launcher: 1 = the kernel-row workgroups of a split share an XCD
+  // split-free plan (kWgradDirect, nsplit 1): the tile is written straight into the OIHW fp32 gradient
+  // grad_w[n][c][t] = beta * grad_w + scale * sum (n < cout_real, c < cin_real) and the bias into
+  // grad_b -- no slab, no reduce launch.  grad_w == nullptr: the split slab as above.
+  float* grad_w;
+  float* grad_b;
+  float scale, beta;
+  int cout_real;
 };
 
 // fp8 wgrad (conv_wgrad_fp8.hip): e5m2 dZ x e4m3 X on the block-scaled MFMA, same slab as the bf16 wgrad
@@ -200,10 +207,16 @@ void launch_conv_fwd(const ConvFwdArgs& a, int mode, hipStream_t st);
 // packed-tap first-layer forward (bias + ReLU, optional bitmask): cpt 8-channel chunks per tap
 void launch_conv_fwd_pk(const ConvFwdArgs& a, int cpt, hipStream_t st);
 void launch_conv_wgrad(const ConvWgradArgs& a, hipStream_t st);
+// split-free wgrad (kWgradDirect): a.grad_w / grad_b / scale / beta / cout_real set; ksub 4 / 8 / 12
+void launch_conv_wgrad_direct(const ConvWgradArgs& a, int ksub, hipStream_t st);
+bool wgrad_direct_supported(int Cout, int Cin, int cin_real, int K);
 // weight-stationary small-batch conv (conv_ws.hip, tile code 40): modes 0 / 2 / 3; target_wgs <= 0: 256
 void launch_conv_ws(const ConvFwdArgs& a, int mode, int target_wgs, hipStream_t st, int probe = 0);
 // conv_wgrad's small-batch plan (64 x 64 tap-merged tiles; ops.wgrad_config picks it)
 constexpr int kWgradSmall = 14;
+// split-free small-batch plan: 32 x 48 (or 32 x 32) per-tap tiles, each workgroup owns the whole pixel
+// range and writes the OIHW gradient itself (ConvWgradArgs::grad_w; conv_wgrad_direct)
+constexpr int kWgradDirect = 15;
 // weight-stationary order of standard (tap, Cout, Cin) bf16 packs (conv_ws.hip; tile 40 reads it)
 struct WsPackJob {
   const __bf16* src;
@@ -280,7 +293,7 @@ struct Fp8PackArgs {
   int n;
 };
 void launch_pack_weights_fp8_multi(const Fp8PackArgs& a, hipStream_t st);
-void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, hipStream_t st);
+void launch_fp8_act_scales(unsigned* amax, int* scales8, float* osc, int L, int margin, int max_drop, hipStream_t st);
 void launch_fp8_grad_scales(unsigned* amax, int* gscales8, float* gosc, int L, int margin, hipStream_t st);
 void launch_quantize_bf8_dev(const __bf16* x, uint8_t* y, long n, const float* scale, unsigned* amax, hipStream_t st,
                              bool e4m3 = false);

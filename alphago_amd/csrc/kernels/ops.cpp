@@ -83,6 +83,47 @@ void conv_wgrad_fp8(const Tensor& x8, const Tensor& dz8, const Tensor& slab, con
 
 int64_t wgrad_fp8_stage_px() { return agk::wgrad_fp8_stage_pixels(); }
 
+bool wgrad_direct_supported_op(int64_t cout, int64_t cin, int64_t cin_real, int64_t K) {
+  return agk::wgrad_direct_supported((int)cout, (int)cin, (int)cin_real, (int)K);
+}
+
+// split-free wgrad (kWgradDirect): grad_w (Cout_real, Cin_real, K, K) f32 = beta * grad_w + scale * dW,
+// grad_b likewise; no slab, no reduce
+void conv_wgrad_direct(const Tensor& x, const Tensor& dz, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
+                       int64_t K, int64_t S, int64_t Pin, int64_t Po, double scale, double beta, int64_t ksub) {
+  check_dev("conv_wgrad_direct", x, dz, grad_w, grad_b);
+  CHECK_BF16(x); CHECK_BF16(dz); CHECK_F32(grad_w); CHECK_CONTIG(x); CHECK_CONTIG(dz); CHECK_CONTIG(grad_w);
+  TORCH_CHECK(x.dim() == 4 && dz.dim() == 4 && dz.size(0) == x.size(0), "x, dz: (B, HP, HP, C) with the same B");
+  TORCH_CHECK(x.size(2) == x.size(1) && dz.size(2) == dz.size(1), "x, dz: square padded boards");
+  TORCH_CHECK(x.numel() < (1ll << 31) && dz.numel() < (1ll << 31), "tensor too large for int32 offsets");
+  const int64_t B = x.size(0), HPi = x.size(1), Cin = x.size(3), HPo = dz.size(1), Cout = dz.size(3);
+  TORCH_CHECK(HPi == S + 2 * Pin && HPo == S + 2 * Po && Po >= 1 && Pin >= K / 2, "geometry mismatch");
+  TORCH_CHECK(grad_w.dim() == 4 && grad_w.size(2) == K && grad_w.size(3) == K && grad_w.size(0) <= Cout &&
+                  grad_w.size(1) <= Cin, "grad_w: OIHW (Cout_real <= Cout, Cin_real <= Cin, K, K)");
+  TORCH_CHECK(agk::wgrad_direct_supported((int)Cout, (int)Cin, (int)grad_w.size(1), (int)K),
+              "conv_wgrad_direct: Cout % 32 == 0 and Cin a multiple of 48 / 32 (or 64 with <= 48 real planes)");
+  TORCH_CHECK(ksub == 4 || ksub == 8 || ksub == 12, "conv_wgrad_direct: ksub 4 / 8 / 12");
+  if (grad_b.has_value()) {
+    CHECK_F32(*grad_b);
+    TORCH_CHECK(grad_b->numel() == grad_w.size(0), "grad_b: (Cout_real,)");
+  }
+  agk::ConvWgradArgs a{};
+  a.x_elems = x.numel();
+  a.dz_elems = dz.numel();
+  a.x = bfp(x); a.dz = bfp(dz);
+  a.M = (int)(B * S * S); a.S = (int)S; a.Cin = (int)Cin; a.Cout = (int)Cout; a.K = (int)K; a.T = (int)(K * K);
+  a.HPi = (int)HPi; a.offi = (int)(Pin - K / 2); a.HPo = (int)HPo; a.Po = (int)Po;
+  a.cin_real = (int)grad_w.size(1);
+  a.cout_real = (int)grad_w.size(0);
+  a.nsplit = 1;
+  a.ksteps_per_split = (a.M + 31) / 32;  // >= the stage count at any ksub: the whole pixel range
+  a.grad_w = grad_w.data_ptr<float>();
+  a.grad_b = grad_b.has_value() ? grad_b->data_ptr<float>() : nullptr;
+  a.scale = (float)scale; a.beta = (float)beta;
+  agk::launch_conv_wgrad_direct(a, (int)ksub, cur_stream());
+  launch_check("conv_wgrad_direct");
+}
+
 void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
                        double scale, double beta) {
   check_dev("conv_wgrad_reduce", slab, dbslab, grad_w, grad_b);
@@ -515,14 +556,14 @@ void fp8_weight_scales(at::TensorList ws, const Tensor& wscale, const Tensor& sc
   launch_check("fp8_weight_scales");
 }
 
-void fp8_act_scales(const Tensor& amax, const Tensor& scales8, const Tensor& osc, int64_t margin) {
+void fp8_act_scales(const Tensor& amax, const Tensor& scales8, const Tensor& osc, int64_t margin, int64_t max_drop) {
   check_dev("fp8_act_scales", amax, scales8, osc);
   TORCH_CHECK(amax.scalar_type() == at::kInt && scales8.scalar_type() == at::kInt && osc.scalar_type() == at::kFloat, "dtypes");
   const int L = (int)(amax.numel() / agk::kFp8AmaxSlots);
   TORCH_CHECK(amax.numel() % agk::kFp8AmaxSlots == 0 && L <= 64 && scales8.numel() >= 2 * L && osc.numel() >= L,
               "sizes (amax is (L, 64))");
   agk::launch_fp8_act_scales(reinterpret_cast<unsigned*>(amax.data_ptr<int>()), scales8.data_ptr<int>(),
-                             osc.data_ptr<float>(), L, (int)margin, cur_stream());
+                             osc.data_ptr<float>(), L, (int)margin, (int)max_drop, cur_stream());
   launch_check("fp8_act_scales");
 }
 
@@ -751,6 +792,9 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("sample_moves(Tensor probs, Tensor has, Tensor(a!) out, float beta, int seed) -> ()");
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0, int variant=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
+  m.def("conv_wgrad_direct(Tensor x, Tensor dz, Tensor(a!) grad_w, Tensor(b!)? grad_b, int K, int S, int Pin, int Po, "
+        "float scale=1.0, float beta=0.0, int ksub=8) -> ()");
+  m.def("wgrad_direct_supported(int cout, int cin, int cin_real, int K) -> bool", &wgrad_direct_supported_op);
   m.def("conv_dgrad_bits_bf8(Tensor dz, Tensor wd, Tensor(a!) dx, Tensor mbits, Tensor(b!) dx8, Tensor scale, "
         "Tensor(c!)? amax, int K, int S, int tile=0) -> ()");
   m.def("conv_wgrad_fp8(Tensor x8, Tensor dz8, Tensor(a!) slab, Tensor(b!) dbslab, Tensor xscale, Tensor gscale, "
@@ -795,7 +839,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("quantize_bf8(Tensor x, Tensor(a!) y, Tensor scale, Tensor(b!) amax) -> ()");
   m.def("quantize_fp8_dev(Tensor x, Tensor(a!) y, Tensor scale, Tensor(b!) amax) -> ()");
   m.def("fp8_weight_scales(Tensor[] ws, Tensor(a!) wscale, Tensor(b!) scales8) -> ()");
-  m.def("fp8_act_scales(Tensor(a!) amax, Tensor(b!) scales8, Tensor(c!) osc, int margin) -> ()");
+  m.def("fp8_act_scales(Tensor(a!) amax, Tensor(b!) scales8, Tensor(c!) osc, int margin, int max_drop=0) -> ()");
   m.def("quantize_fp8(Tensor x, Tensor(a!) y, float scale) -> ()");
   m.def("wgrad_tap_group(int cout, int cin, int K) -> int", &wgrad_tap_group);
   m.def("wgrad_plan(int cout, int cin, int cin_real, int K, int variant=0) -> int[]", &wgrad_plan);
@@ -821,6 +865,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("sample_moves", &sample_moves);
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);
+  m.impl("conv_wgrad_direct", &conv_wgrad_direct);
   m.impl("conv_dgrad_bits_bf8", &conv_dgrad_bits_bf8);
   m.impl("conv_wgrad_fp8", &conv_wgrad_fp8);
   m.impl("policy_head", &policy_head);

@@ -6,7 +6,7 @@ The reference builds the Keras model (value.py:12-31) and leaves
 ``ValueNet`` of ``models/nets.py`` (49 planes, 5x5 + 11 x 3x3 convs of K
 filters, 1x1 head, Dense(256), Dense(1, tanh)), ``get_samples`` draws
 minibatches uniformly at random from self-play positions, and ``train`` runs
-the HIP training engine (MSE, Keras SGD decay) -- the same path as
+the HIP training engine (MSE; the CLI's Adam 3e-4 defaults) -- the same path as
 ``python -m alphago_amd.cli train-value`` (``train/value.py``).
 """
 from __future__ import annotations
@@ -52,15 +52,26 @@ class value_trainer:  # noqa: N801 - reference class name
             z = torch.from_numpy(np.asarray(self.outcomes[idx], dtype=np.float32)).to(self.device)
             yield x, z
 
-    def train(self, steps: int = 100, learning_rate: float = LEARNING_RATE, decay: float = DECAY,
-              backend: str = "auto") -> float:
-        """Run ``steps`` SGD steps (value.py:37-39 TODO); returns the mean MSE of the last step."""
-        from ..train.engine import make_value_trainer
+    def train(self, steps: int = 100, learning_rate: Optional[float] = None, decay: Optional[float] = None,
+              backend: str = "auto", optimizer: Optional[str] = None) -> float:
+        """Run ``steps`` optimizer steps (value.py:37-39 TODO); returns the mean MSE of the last step.
 
+        Defaults are the ``train-value`` CLI's (train/value.py DEFAULT_OPTIMIZER / DEFAULT_LR): Keras 1.0
+        Adam at 3e-4 with no decay on the reference's uniform init.  The paper's SGD(0.003, DECAY) on that
+        init leaves a 12-layer trunk at the constant predictor (profiles/r4, profiles/r5); it stays
+        available as ``optimizer="sgd"`` (then learning_rate / decay default to LEARNING_RATE / DECAY)."""
+        from ..train.engine import make_value_trainer
+        from ..train.value import DEFAULT_LR, DEFAULT_OPTIMIZER
+
+        optimizer = optimizer or DEFAULT_OPTIMIZER
+        if learning_rate is None:
+            learning_rate = DEFAULT_LR[optimizer]
+        if decay is None:
+            decay = 0.0 if optimizer == "adam" else DECAY
         if self._trainer is None:
             self.model.to(self.device)
             self._trainer = make_value_trainer(self.model, self.minibatch, learning_rate, decay, backend=backend,
-                                               device=self.device)
+                                               device=self.device, optimizer=optimizer)
         gen = self.get_samples()
         loss = 0.0
         for _ in range(steps):

@@ -256,6 +256,19 @@ def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, bet
     _ops().conv_wgrad_reduce(slab, dbslab, grad_w, grad_b, scale, beta)
 
 
+def conv_wgrad_direct(x, dz, grad_w, grad_b, K: int, S: int, Pin: int, Po: int = 1, scale: float = 1.0,
+                      beta: float = 0.0, ksub: int = 8):
+    """Split-free weight gradient (C++ kWgradDirect): every workgroup owns one 32 x 48 (or 32 x 32) tile of
+    one tap over all B*S*S pixels and writes ``grad_w`` (OIHW fp32, real channel counts: grad_w.shape[1] <
+    the padded Cin skips the zero planes) = beta * grad_w + scale * dW, and ``grad_b`` likewise -- no split
+    slab, no reduce launch, deterministic.  ``ksub``: 32-pixel sub-steps per pipeline stage (4 / 8 / 12)."""
+    _ops().conv_wgrad_direct(x, dz, grad_w, grad_b, K, S, Pin, Po, float(scale), float(beta), int(ksub))
+
+
+def wgrad_direct_supported(cout_p: int, cin_p: int, cin_real: int, K: int) -> bool:
+    return bool(_ops().wgrad_direct_supported(cout_p, cin_p, cin_real or cin_p, K))
+
+
 def policy_head_train(y, w, b, target, dz, loss, correct, dhead, S: int, grad_scale: float, weight=None,
                       bce: bool = False):
     """Fused policy head training step; ``bce`` selects the reference RL loss
@@ -595,9 +608,11 @@ def fp8_weight_scales(ws, wscale, scales8):
     _ops().fp8_weight_scales(list(ws), wscale, scales8)
 
 
-def fp8_act_scales(amax, scales8, osc, margin: int = 1):
-    """Delayed activation scaling from the per-layer output amax (also clears amax)."""
-    _ops().fp8_act_scales(amax, scales8, osc, margin)
+def fp8_act_scales(amax, scales8, osc, margin: int = 1, max_drop: int = 0):
+    """Delayed activation scaling from the per-layer output amax (also clears amax).  ``max_drop`` > 0:
+    underflow guard -- each layer's exponent falls by at most that many binades per step (outliers of a
+    sudden amax rise saturate instead of flushing the bulk of the activations to zero)."""
+    _ops().fp8_act_scales(amax, scales8, osc, margin, max_drop)
 
 
 def quantize_fp8(x_bf16: torch.Tensor, out: torch.Tensor, exponent: int):

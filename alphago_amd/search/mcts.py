@@ -323,7 +323,8 @@ class BatchedMCTS(object):
             queued leaf (a held batch's) or a terminal.  The held batch's leaves count toward the
             playout budget, so the pipelined search does the serial search's number of playouts."""
             f = self._forests[k]
-            todo = [j for j in range(f.n_trees) if f.sims(j) + f.n_held_tree(j) < targets[k][j]]
+            held = f.held_counts()  # one native pass over the held batch
+            todo = [j for j in range(f.n_trees) if f.sims(j) + held[j] < targets[k][j]]
             return bool(todo) and f.gather(leaves_per_tree, todo) > 0
 
         enc = self._encoded_engines()

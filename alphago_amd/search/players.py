@@ -7,6 +7,7 @@ a list of states in ONE batched forward.
 """
 from __future__ import annotations
 
+import time
 from typing import List, Optional
 
 import numpy as np
@@ -73,10 +74,32 @@ class MCTSPlayer(object):
         self.leaves_per_batch = leaves_per_batch
         self.temperature = temperature
 
-    def get_move(self, state):
+    supports_time_budget = True
+
+    def get_move(self, state, time_budget: Optional[float] = None):
+        """``time_budget`` (seconds, GTP time control): search in growing chunks of playouts on the same
+        tree (each ``search`` call adds to the root's visits) until the next chunk would overrun the
+        budget or ``n_playout`` is reached; None = the fixed ``n_playout``."""
         if not sensible_moves(state):
             return go.PASS_MOVE
-        return self.search.search([state], self.n_playout, self.leaves_per_batch, self.temperature)[0]
+        if time_budget is None:
+            return self.search.search([state], self.n_playout, self.leaves_per_batch, self.temperature)[0]
+        t0 = time.perf_counter()
+        done, chunk, move = 0, max(1, self.leaves_per_batch), None
+        while True:
+            t1 = time.perf_counter()
+            move = self.search.search([state], chunk, self.leaves_per_batch, self.temperature)[0]
+            done += chunk
+            now = time.perf_counter()
+            per = (now - t1) / chunk  # seconds per playout of the last chunk
+            left = time_budget - (now - t0)
+            if done >= self.n_playout or left <= 0:
+                return move
+            # next chunk: double the last, capped by the playout budget and by the time left (with a
+            # 25 % margin for the per-call overhead)
+            chunk = int(min(2 * chunk, self.n_playout - done, 0.75 * left / max(per, 1e-6)))
+            if chunk < 1:
+                return move
 
     def get_moves(self, states):
         self.search.resize(len(states))

@@ -30,11 +30,19 @@ def trainer_state(trainer) -> Dict[str, Any]:
     st = {"flat": trainer.fp.flat.detach().to("cpu", copy=True),
           "names": list(trainer.fp.names),
           "iterations": int(trainer.sched.iterations)}
+    sched = trainer.sched
+    st["optimizer"] = sched.optimizer
+    st["hyper"] = optimizer_hyper(sched)
     opt = getattr(trainer, "opt_state", None)
     if opt:  # momentum velocity / Adam moments
-        st["optimizer"] = trainer.sched.optimizer
         st["opt_state"] = [t.detach().to("cpu", copy=True) for t in opt]
     return st
+
+
+def optimizer_hyper(sched) -> Dict[str, float]:
+    """The optimizer hyperparameters a resume must keep (the moments are only meaningful under them)."""
+    return {"momentum": float(sched.momentum), "nesterov": float(bool(sched.nesterov)),
+            "beta_1": float(sched.beta_1), "beta_2": float(sched.beta_2), "epsilon": float(sched.epsilon)}
 
 
 def load_trainer_state(trainer, st: Dict[str, Any]) -> None:
@@ -44,10 +52,19 @@ def load_trainer_state(trainer, st: Dict[str, Any]) -> None:
     with torch.no_grad():
         trainer.fp.flat.copy_(flat.to(trainer.fp.flat.device))
     trainer.sched.iterations = int(st["iterations"])
-    opt = getattr(trainer, "opt_state", None)
+    opt = getattr(trainer, "opt_state", None) or []
+    saved = st.get("opt_state", [])
+    if "optimizer" in st and st["optimizer"] != trainer.sched.optimizer:
+        # e.g. an Adam checkpoint resumed by an SGD trainer would silently drop its moments
+        raise ValueError("checkpoint optimizer %r != this trainer's %r" % (st["optimizer"], trainer.sched.optimizer))
+    if len(saved) != len(opt):
+        raise ValueError("checkpoint holds %d optimizer state buffers, this trainer keeps %d" % (len(saved), len(opt)))
+    if "hyper" in st:
+        mine = optimizer_hyper(trainer.sched)
+        diff = {k: (v, mine[k]) for k, v in st["hyper"].items() if k in mine and abs(v - mine[k]) > 1e-12}
+        if diff:
+            raise ValueError("resume with different optimizer hyperparameters (saved, now): %s" % diff)
     if opt:
-        if st.get("optimizer") != trainer.sched.optimizer or len(st.get("opt_state", [])) != len(opt):
-            raise ValueError("checkpoint optimizer state does not match this trainer's optimizer")
         with torch.no_grad():
             for dst, src in zip(opt, st["opt_state"]):
                 dst.copy_(src.to(dst.device))

@@ -177,6 +177,8 @@ def optimizer_update_(p: torch.Tensor, g: torch.Tensor, state: List[torch.Tensor
 # side-stream wgrad no longer finds idle CUs there: B = 8 12.1k overlapped vs 14.1k serial, B = 16 23.0k
 # vs 23.4k; B = 32 40.0k vs 35.8k, profiles/r5/README.md)
 OVERLAP_AUTO_MIN_PIXELS, OVERLAP_AUTO_MAX_PIXELS = 17 * 361, 256 * 361
+# split-free wgrad (ops.conv_wgrad_direct) up to this many output pixels per step (B = 16 at 19 x 19)
+WGRAD_DIRECT_MAX_PIXELS = 16 * 361
 
 
 class HipConvTrainer:
@@ -187,8 +189,12 @@ class HipConvTrainer:
                  wgrad_priority: Optional[int] = None, conv_tile: int = 0, fp8_dgrad: Optional[bool] = None,
                  reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None,
                  fp8_wgrad: Optional[bool] = None, optimizer: str = "sgd", momentum: float = 0.0,
-                 nesterov: bool = False, fp8_bf16_layers: Optional[Sequence[int]] = None):
+                 nesterov: bool = False, fp8_bf16_layers: Optional[Sequence[int]] = None,
+                 wgrad_direct: Optional[bool] = None, wgrad_ksub: int = 8, fp8_scale_guard: int = 1):
         ops.load()
+        # fp8 underflow guard: activation scale exponents fall by at most this many binades per step
+        # (ops.fp8_act_scales max_drop; 0 = the plain one-step delayed scale)
+        self.fp8_scale_guard = int(fp8_scale_guard)
         # wgrad kernel: 0 = per-tap kernel (default), 5 = one-kernel-row wgrad (opt-in, slower so far)
         self.wgrad_variant = int(os.environ.get("ALPHAGO_AMD_WGRAD_VARIANT", "0")) if wgrad_variant is None \
             else int(wgrad_variant)
@@ -285,6 +291,16 @@ class HipConvTrainer:
             self.wgrad_var.append(var)
             slab_max = max(slab_max, ns * T * self.Fp * cin_p)
             db_max = max(db_max, ns * self.Fp)
+        # split-free wgrad (ops.conv_wgrad_direct: whole pixel range per workgroup, OIHW gradient written
+        # in the kernel, no slab and no reduce launch); automatic up to WGRAD_DIRECT_MAX_PIXELS, off with
+        # the reduce stream (its slabs are the point) and for kernel-lab wgrad variants
+        if wgrad_direct is None:
+            wgrad_direct = M <= WGRAD_DIRECT_MAX_PIXELS
+        self.wgrad_ksub = int(wgrad_ksub)
+        self.wgrad_direct = [bool(wgrad_direct) and not reduce_stream and self.wgrad_variant in (0, ops.WGRAD_SMALL)
+                             and ops.wgrad_direct_supported(self.Fp, self.C0p if l == 0 else self.Fp,
+                                                            self.C0 if l == 0 else self.Fp, self.K[l])
+                             for l in range(self.L)]
         # small batches (B <= 8, ops.SPLITK_MAX_M): forward and bitmask dgrad on the split-K 32-pixel tile
         # (ops.conv_fwd_splitk: the K loop of a tile over several workgroups, one finishing pass);
         # bf16 path with the automatic tiling only
@@ -543,7 +559,7 @@ class HipConvTrainer:
             self._sr_seed.add_(1)
         if self.fp8_wgrad:
             self.xscale8.copy_(self.scales8[:, 0:1])
-        ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1)  # next step's activation scales
+        ops.fp8_act_scales(self.amax8, self.scales8, self.osc8, 1, self.fp8_scale_guard)  # next step's scales
 
     @torch.no_grad()
     def _fp8_calibrate(self) -> None:
@@ -578,6 +594,12 @@ class HipConvTrainer:
         sr = self.s_r
         if sr is not None and self._slab_free[i] is not None:
             torch.cuda.current_stream(self.device).wait_event(self._slab_free[i])
+        if self.wgrad_direct[l] and not f8:  # split-free: the OIHW gradient straight from the kernel
+            ops.conv_wgrad_direct(x, self.DZ[l], self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l],
+                                  self.K[l], self.S, pin, 1, 1.0, 0.0, self.wgrad_ksub)
+            if red and not self.defer_allreduce and l in self._bucket_after_layer:
+                self.reducer.launch(self._bucket_after_layer[l])
+            return
         if f8:  # e5m2 dZ x e4m3 X, dequantised by the MFMA's block scales
             # (its tap-0 workgroups also fold max |dZ| into the delayed-scale slots of layer l)
             ops.conv_wgrad_fp8(self.X8[l], self.DZ8[l], slab, dbs, self.xscale8[l], self.gscales8[l, 0:1],

@@ -96,6 +96,8 @@ def _parser():
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                    help="HIP backend conv forward precision (fp8: e4m3 block-scaled MFMA forward, bf16 backward)")
+    p.add_argument("--fp8-scale-guard", type=int, default=1,
+                   help="fp8: activation scale exponents fall at most this many binades per step (0: unguarded)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-symmetries", action="store_true", help="disable random D4 augmentation")
     p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
@@ -190,7 +192,7 @@ def run_training(cmd_line_args: Optional[List[str]] = None):
         iterations, cursor = int(state["trainer"]["iterations"]), int(state["cursor"])
 
     B = args.minibatch
-    pkw = {"precision": args.precision} if args.precision != "bf16" else {}
+    pkw = {"precision": args.precision, "fp8_scale_guard": args.fp8_scale_guard} if args.precision != "bf16" else {}
     trainer = make_policy_trainer(net, B, args.learning_rate, args.decay, backend=args.backend, device=dev,
                                   iterations=iterations, **pkw)
     if args.graph and hasattr(trainer, "enable_graphs"):

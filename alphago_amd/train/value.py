@@ -225,6 +225,8 @@ def train_cli(argv=None):
     p.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
+    p.add_argument("--fp8-scale-guard", type=int, default=1,
+                   help="fp8: activation scale exponents fall at most this many binades per step (0: unguarded)")
     p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--metrics", default=None, help="JSONL metrics file (per-epoch and per-step records)")
@@ -272,10 +274,12 @@ def train_cli(argv=None):
     if a.precision != "bf16":
         kw["precision"] = a.precision
         kw["fp8_bf16_layers"] = [int(x) for x in a.fp8_bf16_layers.split(",") if x.strip() != ""]
+        kw["fp8_scale_guard"] = a.fp8_scale_guard
     backend = a.backend if a.backend != "auto" else ("hip" if dev.type == "cuda" else "torch")
     if backend == "torch":
         kw.pop("precision", None)
         kw.pop("fp8_bf16_layers", None)
+        kw.pop("fp8_scale_guard", None)
     trainer = make_value_trainer(val.model, B, lr, decay, backend=backend, device=dev, **kw)
     gen = torch.Generator(device=dev)
     gen.manual_seed(a.seed + rank)
@@ -284,6 +288,14 @@ def train_cli(argv=None):
     agdist.barrier()
     meta = {"epochs": [], "best_epoch": 0, "training_data": a.train_data, "model_file": a.model,
             "data": {"rows_per_rank": agdist.all_gather_object(len(data)) if env.distributed else [len(data)]}}
+    if kw.get("fp8_bf16_layers"):
+        # the weights file carries no per-layer precision: fp8 inference (HipTrunkInference precision="fp8")
+        # runs every layer in fp8, so a net trained with bf16 layers should be evaluated in bf16
+        meta["fp8_bf16_layers"] = sorted(kw["fp8_bf16_layers"])
+        if env.is_main:
+            import warnings
+            warnings.warn("--fp8-bf16-layers %s: fp8 inference ignores per-layer precision (it runs every layer in "
+                          "fp8); evaluate this net with precision bf16 to match its training" % meta["fp8_bf16_layers"])
     log = MetricsLogger(a.metrics if env.is_main else None)
     # per-step records: "acc" is the sign agreement of v and z (the trainer's metric sum)
     step_log = StepMetrics(log, a.log_every if a.metrics else 0, B * world, val.model.flops_per_position(), dev,

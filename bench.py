@@ -78,6 +78,11 @@ def main():
                     help="target workgroups per wgrad launch (sets the split-K factor; 0 = one resident round)")
     ap.add_argument("--reduce-stream", type=int, default=None, choices=[0, 1],
                     help="1: split-K wgrad reduce on a side stream beside the dgrad (default: engine default)")
+    ap.add_argument("--wgrad-direct", type=int, default=None, choices=[0, 1],
+                    help="1: split-free wgrad (no split-K slab / reduce) on every layer; 0: never (default: engine "
+                         "default, automatic at small batches)")
+    ap.add_argument("--wgrad-ksub", type=int, default=8, choices=[4, 8, 12],
+                    help="split-free wgrad: 32-pixel sub-steps per pipeline stage")
     ap.add_argument("--profile", default=None,
                     help="after the timed run, profile 6 more steps (torch.profiler + roctx ranges) into DIR")
     args = ap.parse_args()
@@ -104,7 +109,9 @@ def main():
     kw = {} if args.backend == "torch" else {"overlap": True if args.overlap else None, "precision": args.precision,
                                              "wgrad_target_wgs": args.wgrad_wgs, "conv_tile": args.conv_tile,
                                              "reduce_stream": None if args.reduce_stream is None
-                                             else bool(args.reduce_stream)}
+                                             else bool(args.reduce_stream),
+                                             "wgrad_direct": None if args.wgrad_direct is None
+                                             else bool(args.wgrad_direct), "wgrad_ksub": args.wgrad_ksub}
     trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
     if args.graph:
         trainer.enable_graphs()

@@ -131,6 +131,40 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     assert _rel_err(gb, ref_b) < 2e-3
 
 
+@pytest.mark.parametrize("S,B,Cin,Cin_real,Cout,K,Pin,ksub", [
+    (19, 16, 192, 192, 192, 3, 1, 8), (19, 1, 192, 192, 192, 3, 1, 4), (19, 5, 192, 192, 192, 3, 1, 12),
+    (19, 16, 64, 48, 192, 5, 2, 8), (13, 3, 64, 48, 128, 5, 2, 4), (9, 7, 128, 128, 128, 3, 1, 8),
+    (19, 2, 64, 64, 64, 3, 1, 12), (19, 32, 192, 192, 192, 3, 1, 8), (9, 9, 160, 160, 160, 3, 1, 8)])
+def test_conv_wgrad_direct(ops, cuda_device, S, B, Cin, Cin_real, Cout, K, Pin, ksub):
+    """Split-free wgrad (kWgradDirect) straight into the OIHW gradient: fp32 reference, scale / beta
+    accumulation, the first layer's 48 real planes of 64, other board sizes, and bitwise-equal repeats
+    (one workgroup per output element, fixed pixel order)."""
+    torch.manual_seed(11)
+    assert ops.wgrad_direct_supported(Cout, Cin, Cin_real, K)
+    x = _bf(torch.randn(B, Cin_real, S, S, device=cuda_device))
+    dz = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
+    ref_w = torch.nn.grad.conv2d_weight(x, (Cout, Cin_real, K, K), dz, padding=K // 2)
+    ref_b = dz.sum(dim=(0, 2, 3))
+    xp = ops.to_padded(x, Pin, Cin)
+    dzp = ops.to_padded(dz, 1)
+    gw = torch.full((Cout, Cin_real, K, K), float("nan"), device=cuda_device)
+    gb = torch.full((Cout,), float("nan"), device=cuda_device)
+    ops.conv_wgrad_direct(xp, dzp, gw, gb, K, S, Pin, 1, ksub=ksub)  # beta 0: NaN never read
+    torch.cuda.synchronize()
+    assert _rel_err(gw, ref_w) < 2e-3
+    assert _rel_err(gb, ref_b) < 2e-3
+    gw2 = gw.clone()
+    gb2 = gb.clone()
+    ops.conv_wgrad_direct(xp, dzp, gw2, gb2, K, S, Pin, 1, scale=0.5, beta=2.0, ksub=ksub)
+    torch.cuda.synchronize()
+    assert _rel_err(gw2, 2.5 * gw) < 1e-5 and _rel_err(gb2, 2.5 * gb) < 1e-5
+    gw3 = torch.zeros_like(gw)
+    gb3 = torch.zeros_like(gb)
+    ops.conv_wgrad_direct(xp, dzp, gw3, gb3, K, S, Pin, 1, ksub=ksub)
+    torch.cuda.synchronize()
+    assert torch.equal(gw3, gw) and torch.equal(gb3, gb)
+
+
 @pytest.mark.parametrize("S,B,Cin,Cin_real,Cout,K,Pin", [(9, 13, 192, 192, 192, 3, 1), (13, 6, 192, 192, 192, 3, 1),
                                                          (9, 7, 64, 48, 192, 5, 2), (13, 3, 64, 48, 128, 5, 2),
                                                          (19, 1, 128, 128, 128, 3, 1)])

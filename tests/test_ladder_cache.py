@@ -94,3 +94,27 @@ def test_ladder_cache_pipelined_and_budget_change():
     f.ladder_cache = False
     assert f.ladder_cache_stats()["records"] == 0
     _search(E, f, 4, 16, rng, check=True)
+
+
+def test_ladder_cache_byte_budget_evicts_instead_of_freezing():
+    """The cache holds at most its byte budget (per tree: budget / trees); a full tree drops its own
+    records and keeps caching (counted in 'evictions'); 'bytes' reports the host memory held."""
+    E = engine()
+    rng = np.random.default_rng(3)
+    s = _ladder_positions()[0]
+    f = E.Forest(1, 5.0, 0.0, 0, 1000, 3, 5, [])
+    f.set_root(0, s)
+    _search(E, f, 12, 16, rng, check=True)
+    st = f.ladder_cache_stats()
+    assert st["records"] > 0 and st["bytes"] > 0 and st["evictions"] == 0
+    assert st["budget_bytes"] == 256 << 20
+    per = st["bytes"] / st["records"]
+    f.set_ladder_cache_bytes(1 << 20)  # the floor: 1 MiB
+    budget = f.ladder_cache_stats()["budget_bytes"]
+    assert budget == 1 << 20
+    f.set_root(0, s)
+    assert f.ladder_cache_stats()["bytes"] == 0
+    _search(E, f, 100, 16, rng, check=True)  # planes stay exact across evictions
+    st = f.ladder_cache_stats()
+    assert st["bytes"] <= budget + 16 * per and st["records"] > 0
+    assert st["evictions"] >= 1  # ~2 KB records: 1 MiB fills within 100 rounds of 16 leaves
