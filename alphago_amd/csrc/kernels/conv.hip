@@ -370,13 +370,15 @@ void launch_conv_wgrad_direct(const ConvWgradArgs& a_in, int ksub, hipStream_t s
     throw std::invalid_argument("conv_wgrad_direct: needs grad_w, Cout % 32 == 0 and a 48 / 32 c tile");
   const int wc = wgrad_direct_wc(a.Cin, a.cin_real);
   if (wc == 48) {
-    if (ksub == 4) launch_wgrad_direct_t<48, 3, 4>(a, st);
-    else if (ksub == 12) launch_wgrad_direct_t<48, 3, 12>(a, st);
-    else launch_wgrad_direct_t<48, 3, 8>(a, st);
+    if (ksub == 1) launch_wgrad_direct_t<48, 3, 1>(a, st);
+    else if (ksub == 2) launch_wgrad_direct_t<48, 3, 2>(a, st);
+    else if (ksub == 8) launch_wgrad_direct_t<48, 3, 8>(a, st);
+    else launch_wgrad_direct_t<48, 3, 4>(a, st);
   } else {
-    if (ksub == 4) launch_wgrad_direct_t<32, 2, 4>(a, st);
-    else if (ksub == 12) launch_wgrad_direct_t<32, 2, 12>(a, st);
-    else launch_wgrad_direct_t<32, 2, 8>(a, st);
+    if (ksub == 1) launch_wgrad_direct_t<32, 2, 1>(a, st);
+    else if (ksub == 2) launch_wgrad_direct_t<32, 2, 2>(a, st);
+    else if (ksub == 8) launch_wgrad_direct_t<32, 2, 8>(a, st);
+    else launch_wgrad_direct_t<32, 2, 4>(a, st);
   }
 }
 

@@ -102,7 +102,7 @@ void conv_wgrad_direct(const Tensor& x, const Tensor& dz, const Tensor& grad_w, 
                   grad_w.size(1) <= Cin, "grad_w: OIHW (Cout_real <= Cout, Cin_real <= Cin, K, K)");
   TORCH_CHECK(agk::wgrad_direct_supported((int)Cout, (int)Cin, (int)grad_w.size(1), (int)K),
               "conv_wgrad_direct: Cout % 32 == 0 and Cin a multiple of 48 / 32 (or 64 with <= 48 real planes)");
-  TORCH_CHECK(ksub == 4 || ksub == 8 || ksub == 12, "conv_wgrad_direct: ksub 4 / 8 / 12");
+  TORCH_CHECK(ksub == 1 || ksub == 2 || ksub == 4 || ksub == 8, "conv_wgrad_direct: ksub 1 / 2 / 4 / 8");
   if (grad_b.has_value()) {
     CHECK_F32(*grad_b);
     TORCH_CHECK(grad_b->numel() == grad_w.size(0), "grad_b: (Cout_real,)");
@@ -793,7 +793,7 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0, int variant=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
   m.def("conv_wgrad_direct(Tensor x, Tensor dz, Tensor(a!) grad_w, Tensor(b!)? grad_b, int K, int S, int Pin, int Po, "
-        "float scale=1.0, float beta=0.0, int ksub=8) -> ()");
+        "float scale=1.0, float beta=0.0, int ksub=4) -> ()");
   m.def("wgrad_direct_supported(int cout, int cin, int cin_real, int K) -> bool", &wgrad_direct_supported_op);
   m.def("conv_dgrad_bits_bf8(Tensor dz, Tensor wd, Tensor(a!) dx, Tensor mbits, Tensor(b!) dx8, Tensor scale, "
         "Tensor(c!)? amax, int K, int S, int tile=0) -> ()");

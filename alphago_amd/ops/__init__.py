@@ -257,11 +257,11 @@ def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, bet
 
 
 def conv_wgrad_direct(x, dz, grad_w, grad_b, K: int, S: int, Pin: int, Po: int = 1, scale: float = 1.0,
-                      beta: float = 0.0, ksub: int = 8):
+                      beta: float = 0.0, ksub: int = 4):
     """Split-free weight gradient (C++ kWgradDirect): every workgroup owns one 32 x 48 (or 32 x 32) tile of
     one tap over all B*S*S pixels and writes ``grad_w`` (OIHW fp32, real channel counts: grad_w.shape[1] <
     the padded Cin skips the zero planes) = beta * grad_w + scale * dW, and ``grad_b`` likewise -- no split
-    slab, no reduce launch, deterministic.  ``ksub``: 32-pixel sub-steps per pipeline stage (4 / 8 / 12)."""
+    slab, no reduce launch, deterministic.  ``ksub``: 32-pixel sub-steps per pipeline stage (1 / 2 / 4 / 8)."""
     _ops().conv_wgrad_direct(x, dz, grad_w, grad_b, K, S, Pin, Po, float(scale), float(beta), int(ksub))
 
 

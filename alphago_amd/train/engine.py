@@ -177,8 +177,10 @@ def optimizer_update_(p: torch.Tensor, g: torch.Tensor, state: List[torch.Tensor
 # side-stream wgrad no longer finds idle CUs there: B = 8 12.1k overlapped vs 14.1k serial, B = 16 23.0k
 # vs 23.4k; B = 32 40.0k vs 35.8k, profiles/r5/README.md)
 OVERLAP_AUTO_MIN_PIXELS, OVERLAP_AUTO_MAX_PIXELS = 17 * 361, 256 * 361
-# split-free wgrad (ops.conv_wgrad_direct) up to this many output pixels per step (B = 16 at 19 x 19)
-WGRAD_DIRECT_MAX_PIXELS = 16 * 361
+# split-free wgrad (ops.conv_wgrad_direct) up to this many output pixels per step: per 192 -> 192 layer
+# B = 1 7.8 vs 19.3 us (split-K + reduce), B = 4 16.9 vs 21.2, B = 8 27.1 vs 24.8, B = 16 48.6 vs 26.2
+# (ksub 4; profiles/r6/raw/wgrad_direct_bench_v1.jsonl)
+WGRAD_DIRECT_MAX_PIXELS = 4 * 361
 
 
 class HipConvTrainer:
@@ -190,7 +192,7 @@ class HipConvTrainer:
                  reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None,
                  fp8_wgrad: Optional[bool] = None, optimizer: str = "sgd", momentum: float = 0.0,
                  nesterov: bool = False, fp8_bf16_layers: Optional[Sequence[int]] = None,
-                 wgrad_direct: Optional[bool] = None, wgrad_ksub: int = 8, fp8_scale_guard: int = 1):
+                 wgrad_direct: Optional[bool] = None, wgrad_ksub: int = 4, fp8_scale_guard: int = 1):
         ops.load()
         # fp8 underflow guard: activation scale exponents fall by at most this many binades per step
         # (ops.fp8_act_scales max_drop; 0 = the plain one-step delayed scale)

@@ -81,7 +81,7 @@ def main():
     ap.add_argument("--wgrad-direct", type=int, default=None, choices=[0, 1],
                     help="1: split-free wgrad (no split-K slab / reduce) on every layer; 0: never (default: engine "
                          "default, automatic at small batches)")
-    ap.add_argument("--wgrad-ksub", type=int, default=8, choices=[4, 8, 12],
+    ap.add_argument("--wgrad-ksub", type=int, default=4, choices=[1, 2, 4, 8],
                     help="split-free wgrad: 32-pixel sub-steps per pipeline stage")
     ap.add_argument("--profile", default=None,
                     help="after the timed run, profile 6 more steps (torch.profiler + roctx ranges) into DIR")
@@ -229,6 +229,7 @@ def main():
                 "parallelism": "dp%d" % n,
                 "backend": args.backend,
                 "graph": bool(args.graph),
+                "wgrad_direct": None if args.backend != "hip" else any(getattr(trainer, "wgrad_direct", [])),
                 "baseline": "paper SL throughput ~3.0k pos/s (50 GPUs), BASELINE.md (A)",
             },
         }

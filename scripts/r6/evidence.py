@@ -109,7 +109,7 @@ def stage_sl(a):
     meta = json.load(open(os.path.join(run_dir, "metadata.json")))
     ep = meta["epochs"]
     last = sorted(f for f in os.listdir(run_dir) if f.startswith("weights.") and f.endswith(".hdf5"))[-1]
-    nets = os.path.join(a.out, "nets")
+    nets = a.nets
     os.makedirs(nets, exist_ok=True)
     pol = CNNPolicy.load_model(mj, device=dev, weights_file=os.path.join(run_dir, last))
     pol.save_model(os.path.join(nets, "sl.json"), os.path.join(nets, "sl.hdf5"))
@@ -122,17 +122,17 @@ def stage_sl(a):
 
 def _load_policy(a, name, dev):
     from alphago_amd.models.policy import CNNPolicy
-    nets = os.path.join(a.out, "nets")
+    nets = a.nets
     return CNNPolicy.load_model(os.path.join(nets, name + ".json"), device=dev,
                                 weights_file=os.path.join(nets, name + ".hdf5"))
 
 
 def stage_rl(a):
     from alphago_amd.train.rl import run
-    nets = os.path.join(a.out, "nets")
+    nets = a.nets
     folder = os.path.join(a.work, "rl_pool")
     shutil.rmtree(folder, ignore_errors=True)
-    metrics = os.path.join(a.out, "rl_winrate.jsonl")
+    metrics = os.path.join(a.out, "rl_winrate%s.jsonl" % a.tag)
     if os.path.exists(metrics):
         os.remove(metrics)
     t0 = time.perf_counter()
@@ -143,12 +143,14 @@ def stage_rl(a):
                str(a.iterations), "--seed", str(a.seed), "--verbose"])
     last = res["pool"][-1]
     assert last is not None
-    shutil.copy(last, os.path.join(nets, "rl.hdf5"))
-    shutil.copy(os.path.join(nets, "sl.json"), os.path.join(nets, "rl.json"))
-    relativize(os.path.join(nets, "rl.json"), "rl.hdf5")
+    shutil.copy(last, os.path.join(nets, "rl%s.hdf5" % a.tag))
+    shutil.copy(os.path.join(nets, "sl.json"), os.path.join(nets, "rl%s.json" % a.tag))
+    relativize(os.path.join(nets, "rl%s.json" % a.tag), "rl%s.hdf5" % a.tag)
     h = res["history"]
-    dump(os.path.join(a.out, "rl_summary.json"),
+    dump(os.path.join(a.out, "rl_summary%s.json" % a.tag),
          {"iterations": a.iterations, "games_per_iteration": a.games, "lr": a.lr, "save_every": a.save_every,
+          "opponent_pool": "the SL net only" if a.save_every >= a.iterations else
+          "the SL net + a snapshot every %d iterations, one drawn uniformly per iteration" % a.save_every,
           "seconds": round(time.perf_counter() - t0, 1), "final_weights": os.path.basename(last),
           "win_rate_first10": round(float(np.mean([r["win_rate"] for r in h[:10]])), 4),
           "win_rate_last10": round(float(np.mean([r["win_rate"] for r in h[-10:]])), 4),
@@ -159,8 +161,8 @@ def stage_match(a):
     from alphago_amd.search.arena import batched_match
     from alphago_amd.search.selfplay import BatchedSampler
     dev = DEV
-    sl, rl = _load_policy(a, "sl", dev), _load_policy(a, "rl", dev)
-    out = {}
+    sl, rl = _load_policy(a, "sl", dev), _load_policy(a, "rl" + a.tag, dev)
+    out = {"rl_run": "rl_summary%s.json" % a.tag}
     for label, t in (("T1", 1.0),):
         t0 = time.perf_counter()
         res = batched_match(BatchedSampler(rl, t, seed=a.seed * 2 + 1), BatchedSampler(sl, t, seed=a.seed * 2 + 2),
@@ -172,7 +174,7 @@ def stage_match(a):
         log(label, res)
     out["note"] = ("RL = train-rl from the SL net (REINFORCE, opponent pool); both players sample their "
                    "policy (p^(1/T)) over sensible moves; colours alternate by game")
-    dump(os.path.join(a.out, "match_rl_vs_sl.json"), out)
+    dump(os.path.join(a.out, "match_rl%s_vs_sl.json" % a.tag), out)
 
 
 def stage_value(a):
@@ -183,7 +185,7 @@ def stage_value(a):
     dev = DEV
     os.makedirs(a.work, exist_ok=True)
     data = os.path.join(a.work, "value_selfplay.h5")
-    sl, rl = _load_policy(a, "sl", dev), _load_policy(a, "rl", dev)
+    sl, rl = _load_policy(a, "sl", dev), _load_policy(a, "rl" + a.tag, dev)
     t0 = time.perf_counter()
     n = 0
     zs = []
@@ -207,6 +209,14 @@ def stage_value(a):
     os.replace(data + ".tmp", data)
     gen_s = time.perf_counter() - t0
     z = np.concatenate(zs).astype(np.float64)
+    import hashlib
+    with H5File(data) as f:  # identifies the dataset across GPU calls (generation is seeded)
+        h = hashlib.sha1(np.asarray(f["outcomes"].read()).tobytes())
+        st_ds = f["states"]
+        for r0 in range(0, st_ds.shape[0], 8192):
+            h.update(np.ascontiguousarray(st_ds.read_rows(r0, r0 + 8192)).tobytes())
+    digest = h.hexdigest()[:16]
+    log("dataset sha1", digest)
     torch.manual_seed(3)
     val = CNNValue(VALUE_FEATURES, filters_per_layer=VNET[0], layers=VNET[1], device="cpu")
     vj = os.path.join(a.work, "value_init.json")
@@ -238,7 +248,7 @@ def stage_value(a):
                                                 "train_s": round(time.perf_counter() - t1, 1)})
             log(arm, seed, results[arm][-1])
             if arm == "hip-bf16" and seed == 0:
-                nets = os.path.join(a.out, "nets")
+                nets = a.nets
                 v = CNNValue.load_model(vj, device=dev, weights_file=os.path.join(od, "weights.%05d.hdf5" % best))
                 v.save_model(os.path.join(nets, "value.json"), os.path.join(nets, "value.hdf5"))
                 relativize(os.path.join(nets, "value.json"), "value.hdf5")
@@ -249,7 +259,8 @@ def stage_value(a):
         for arm in summ:
             summ[arm]["vs_fp32"] = round(summ[arm]["best_val_mse_mean"] / summ["torch-fp32"]["best_val_mse_mean"] - 1, 4)
     dump(os.path.join(a.out, "value_selfplay_%s.json" % "_".join(only)),
-         {"positions": int(len(z)), "generate_s": round(gen_s, 1), "z_mean": round(float(z.mean()), 4),
+         {"positions": int(len(z)), "dataset_sha1_16": digest, "rl_net": "rl%s" % a.tag,
+          "generate_s": round(gen_s, 1), "z_mean": round(float(z.mean()), 4),
           "z_var": round(float(z.var()), 4), "batch": a.batch, "epochs": a.epochs,
           "config": "train-value defaults (Adam 3e-4, Keras uniform init, decay 0), 12x152 value net, 49 planes; "
                     "90/10 split by position; self-play positions from value-generate (SL to U-1, random move at U, "
@@ -265,7 +276,7 @@ def stage_search(a):
     from alphago_amd.search.selfplay import BatchedSampler
     dev = DEV
     sl = _load_policy(a, "sl", dev)
-    nets = os.path.join(a.out, "nets")
+    nets = a.nets
     val = CNNValue.load_model(os.path.join(nets, "value.json"), device=dev,
                               weights_file=os.path.join(nets, "value.hdf5"))
     # single-tree genmove latency on positions from greedy SL self-play
@@ -350,11 +361,15 @@ def main():
     ap.add_argument("--latency-moves", type=int, default=40)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--small", action="store_true", help="tiny nets (CPU rehearsal of the pipeline)")
+    ap.add_argument("--nets", default=None, help="where the nets are read / written (default OUT/nets)")
+    ap.add_argument("--tag", default="", help="rl / match: suffix of the RL run's files (lr sweeps)")
     a = ap.parse_args()
     if a.small:
         global PNET, VNET
         PNET, VNET = (16, 2), (16, 2)
     os.makedirs(a.out, exist_ok=True)
+    a.nets = a.nets or os.path.join(a.out, "nets")
+    os.makedirs(a.nets, exist_ok=True)
     {"sl": stage_sl, "rl": stage_rl, "match": stage_match, "value": stage_value, "search": stage_search}[a.stage](a)
 
 

@@ -132,9 +132,9 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
 
 
 @pytest.mark.parametrize("S,B,Cin,Cin_real,Cout,K,Pin,ksub", [
-    (19, 16, 192, 192, 192, 3, 1, 8), (19, 1, 192, 192, 192, 3, 1, 4), (19, 5, 192, 192, 192, 3, 1, 12),
-    (19, 16, 64, 48, 192, 5, 2, 8), (13, 3, 64, 48, 128, 5, 2, 4), (9, 7, 128, 128, 128, 3, 1, 8),
-    (19, 2, 64, 64, 64, 3, 1, 12), (19, 32, 192, 192, 192, 3, 1, 8), (9, 9, 160, 160, 160, 3, 1, 8)])
+    (19, 16, 192, 192, 192, 3, 1, 8), (19, 1, 192, 192, 192, 3, 1, 4), (19, 5, 192, 192, 192, 3, 1, 1),
+    (19, 16, 64, 48, 192, 5, 2, 2), (13, 3, 64, 48, 128, 5, 2, 4), (9, 7, 128, 128, 128, 3, 1, 8),
+    (19, 2, 64, 64, 64, 3, 1, 1), (19, 32, 192, 192, 192, 3, 1, 2), (9, 9, 160, 160, 160, 3, 1, 4)])
 def test_conv_wgrad_direct(ops, cuda_device, S, B, Cin, Cin_real, Cout, K, Pin, ksub):
     """Split-free wgrad (kWgradDirect) straight into the OIHW gradient: fp32 reference, scale / beta
     accumulation, the first layer's 48 real planes of 64, other board sizes, and bitwise-equal repeats
