@@ -96,8 +96,9 @@ def _parser():
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                    help="HIP backend conv forward precision (fp8: e4m3 block-scaled MFMA forward, bf16 backward)")
-    p.add_argument("--fp8-scale-guard", type=int, default=1,
-                   help="fp8: activation scale exponents fall at most this many binades per step (0: unguarded)")
+    p.add_argument("--fp8-scale-guard", type=int, default=0,
+                   help="fp8: activation scale exponents fall at most this many binades per step (0: unguarded, "
+                        "the default; a 1-binade guard collapsed more SL runs, profiles/r6/README.md)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--no-symmetries", action="store_true", help="disable random D4 augmentation")
     p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])

@@ -225,8 +225,9 @@ def train_cli(argv=None):
     p.add_argument("--train-val-test", nargs=3, type=float, default=[0.93, .05, .02])
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
-    p.add_argument("--fp8-scale-guard", type=int, default=1,
-                   help="fp8: activation scale exponents fall at most this many binades per step (0: unguarded)")
+    p.add_argument("--fp8-scale-guard", type=int, default=0,
+                   help="fp8: activation scale exponents fall at most this many binades per step (0: unguarded, "
+                        "the default; a 1-binade guard collapsed more SL runs, profiles/r6/README.md)")
     p.add_argument("--resident", default="auto", choices=["auto", "yes", "no"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--metrics", default=None, help="JSONL metrics file (per-epoch and per-step records)")

@@ -77,7 +77,7 @@ def _uniform_baseline(h5):
 
 
 ARMS = {"hip-bf16": ["--backend", "hip"], "hip-fp8fwd": ["--backend", "hip", "--precision", "fp8"],
-        "hip-fp8fwd-noguard": ["--backend", "hip", "--precision", "fp8", "--fp8-scale-guard", "0"],
+        "hip-fp8fwd-guard1": ["--backend", "hip", "--precision", "fp8", "--fp8-scale-guard", "1"],
         "torch-fp32": ["--backend", "torch"]}
 
 
