@@ -172,8 +172,10 @@ def stage_match(a):
                     "temperature": t})
         out[label] = res
         log(label, res)
-    out["note"] = ("RL = train-rl from the SL net (REINFORCE, opponent pool); both players sample their "
-                   "policy (p^(1/T)) over sensible moves; colours alternate by game")
+    with open(os.path.join(a.out, "rl_summary%s.json" % a.tag)) as f:
+        out["rl_opponent_pool"] = json.load(f).get("opponent_pool")
+    out["note"] = ("RL = train-rl from the SL net (REINFORCE); both players sample their policy (p^(1/T)) over "
+                   "sensible moves; colours alternate by game")
     dump(os.path.join(a.out, "match_rl%s_vs_sl.json" % a.tag), out)
 
 
