@@ -153,7 +153,10 @@ def _parser():
     p.add_argument("initial_weights", help="Path to file with weights to start from.")
     p.add_argument("initial_json", help="Path to file with initial network params.")
     p.add_argument("--model_folder", default=None, help="where snapshots / the opponent pool are saved")
-    p.add_argument("--learning_rate", type=float, default=.03)
+    p.add_argument("--learning_rate", type=float, default=.03,
+                   help="reference default; on a 12x192 teacher-pool SL net with 512-game iterations 0.01 climbs to "
+                        "a 74%% win rate against the SL start in 40 iterations while 0.03 degrades it "
+                        "(profiles/r6/README.md)")
     p.add_argument("--save_every", type=int, default=500, help="save policy every n mini-batches")
     p.add_argument("--game_batch_size", type=int, default=20, help="games per mini-batch (per rank)")
     p.add_argument("--iterations", type=int, default=20, help="number of mini-batches")
