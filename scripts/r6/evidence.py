@@ -306,8 +306,9 @@ def stage_search(a):
         live = [i for i in range(a.games) if not states[i].is_end_of_game and len(states[i].history) < 722]
         if not live:
             break
+        # every round: one search over all games where MCTS is to move, then the greedy replies of every
+        # game where the policy is to move -- after the first round all games search together
         mine = [i for i in live if (states[i].current_player == go.BLACK) == m_black[i]]
-        theirs = [i for i in live if (states[i].current_player == go.BLACK) != m_black[i]]
         if mine:
             t1 = time.perf_counter()
             mvs = search.search(states, a.playouts, a.leaves, temperature=0.0, active=mine)
@@ -317,6 +318,8 @@ def stage_search(a):
                     states[i].do_move(mvs[i])
                 except go.IllegalMove:
                     states[i].do_move(go.PASS_MOVE)
+        theirs = [i for i in range(a.games) if not states[i].is_end_of_game and len(states[i].history) < 722
+                  and (states[i].current_player == go.BLACK) != m_black[i]]
         if theirs:
             mvs2 = greedy.get_moves([states[i] for i in theirs])
             for k, i in enumerate(theirs):
@@ -324,7 +327,7 @@ def stage_search(a):
                     states[i].do_move(mvs2[k])
                 except go.IllegalMove:
                     states[i].do_move(go.PASS_MOVE)
-        if len(rounds) % 20 == 0:
+        if len(rounds) % 10 == 0:
             log("search round %d: %d live, %.1f s" % (len(rounds), len(live), time.perf_counter() - t0))
     wins = draws = 0
     for g, s in enumerate(states):
@@ -337,6 +340,8 @@ def stage_search(a):
           "playouts": a.playouts, "leaves_per_tree": a.leaves, "opponent": "greedy raw SL policy (argmax over sensible moves)",
           "mean_length": float(np.mean([len(s.history) for s in states])), "seconds": round(time.perf_counter() - t0, 1),
           "batched_round_s_p50": round(float(np.median([r["s"] for r in rounds])), 3),
+          "search_rounds": len(rounds), "leaf_evals_per_s": round(search.forest.total_evals /
+                                                                   max(1e-9, sum(r["s"] for r in rounds)), 1),
           "genmove_single_tree_ms_p50": round(float(np.percentile(lat, 50)), 2),
           "genmove_single_tree_ms_p95": round(float(np.percentile(lat, 95)), 2), "genmove_samples": len(lat),
           "note": "MCTS = SL policy priors + value net (lambda 0, c_puct 5), argmax of visits; batched: one tree per "

@@ -6,19 +6,20 @@ mkdir -p $O
 export PYTHONUNBUFFERED=1
 source scripts/r6/lib.sh
 B="--steps 200 --warmup 50 --data random --pool 8192 --min-warmup-s 2"
-for rep in 1 2; do
+for rep in 1; do
   for d in 0 1; do
     step b16_d${d}_r$rep 120 python bench.py --batch 16 --wgrad-direct $d $B
     step b16g_d${d}_r$rep 120 python bench.py --batch 16 --wgrad-direct $d --graph $B
   done
+  step b16_rs_r$rep 120 python bench.py --batch 16 --reduce-stream 1 $B
 done
-for b in 1 4 8 32 64; do
+for b in 1 4 8 32; do
   for d in 0 1; do
     step b${b}_d$d 120 python bench.py --batch $b --wgrad-direct $d $B
   done
 done
-prof prof16_direct 180 20 --batch 16 --wgrad-direct 1 --steps 40 --warmup 20 --data random --pool 8192
-prof prof16_splitk 180 20 --batch 16 --wgrad-direct 0 --steps 40 --warmup 20 --data random --pool 8192
+prof prof4_direct 180 20 --batch 4 --wgrad-direct 1 --steps 40 --warmup 20 --data random --pool 8192
+prof prof4_splitk 180 20 --batch 4 --wgrad-direct 0 --steps 40 --warmup 20 --data random --pool 8192
 python3 - $O <<'PY'
 import glob, json, os, sys
 for f in sorted(glob.glob(os.path.join(sys.argv[1], "b*.log"))):
@@ -30,7 +31,7 @@ for f in sorted(glob.glob(os.path.join(sys.argv[1], "b*.log"))):
 PY
 # headline: fewer wgrad splits (smaller split-K slab, fewer resident waves), same box, alternating
 for rep in 1 2; do
-  for w in 0 256 384; do
+  for w in 0 256; do
     step head_w${w}_r$rep 150 python bench.py --wgrad-wgs $w --steps 30 --warmup 10
   done
 done
