@@ -95,9 +95,9 @@ class MCTSPlayer(object):
             left = time_budget - (now - t0)
             if done >= self.n_playout or left <= 0:
                 return move
-            # next chunk: double the last, capped by the playout budget and by the time left (with a
-            # 25 % margin for the per-call overhead)
-            chunk = int(min(2 * chunk, self.n_playout - done, 0.75 * left / max(per, 1e-6)))
+            # next chunk: double the last, capped by the playout budget and by half the time left (the
+            # per-playout time of a loaded host varies from chunk to chunk)
+            chunk = int(min(2 * chunk, self.n_playout - done, 0.5 * left / max(per, 1e-6)))
             if chunk < 1:
                 return move
 
