@@ -300,6 +300,19 @@ def stage_search(a):
     search = BatchedMCTS(sl, val, n_trees=a.games, lmbda=0.0, seed=a.seed)
     states = [go.GameState(19) for _ in range(a.games)]
     m_black = [g % 2 == 0 for g in range(a.games)]
+    # both players are deterministic (argmax of visits, argmax of the policy): every game pair (2p, 2p+1)
+    # starts from its own random opening of --opening sensible moves, played identically in both games
+    # of the pair (colours swapped between them)
+    for g in range(0, a.games, 2):
+        rng = np.random.default_rng(1000 + g)
+        for _ in range(a.opening):
+            legal = states[g].get_legal_moves(include_eyes=False)
+            if not legal:
+                break
+            mv = legal[int(rng.integers(len(legal)))]
+            for h in (g, g + 1):
+                if h < a.games:
+                    states[h].do_move(mv)
     rounds = []
     t0 = time.perf_counter()
     while True:
@@ -338,6 +351,7 @@ def stage_search(a):
          {"games": a.games, "mcts_wins": int(wins), "policy_wins": int(a.games - wins - draws), "draws": int(draws),
           "mcts_win_rate": round(wins / a.games, 4), "ci95": wilson(wins, a.games),
           "playouts": a.playouts, "leaves_per_tree": a.leaves, "opponent": "greedy raw SL policy (argmax over sensible moves)",
+          "opening": "%d random sensible moves per game pair, the same in both games of a pair (colours swapped)" % a.opening,
           "mean_length": float(np.mean([len(s.history) for s in states])), "seconds": round(time.perf_counter() - t0, 1),
           "batched_round_s_p50": round(float(np.median([r["s"] for r in rounds])), 3),
           "search_rounds": len(rounds), "leaf_evals_per_s": round(search.forest.total_evals /
@@ -366,6 +380,7 @@ def main():
     ap.add_argument("--playouts", type=int, default=1600)
     ap.add_argument("--leaves", type=int, default=32)
     ap.add_argument("--latency-moves", type=int, default=40)
+    ap.add_argument("--opening", type=int, default=8, help="search: random opening moves per game pair")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--small", action="store_true", help="tiny nets (CPU rehearsal of the pipeline)")
     ap.add_argument("--nets", default=None, help="where the nets are read / written (default OUT/nets)")

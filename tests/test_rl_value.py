@@ -118,6 +118,34 @@ def test_reinforce_sign():
     assert p1[40] > p0[40] and p1[0] < p0[0]
 
 
+def test_reinforce_mean_baseline():
+    """baseline="mean": an iteration the learner loses entirely leaves the weights where they are (the
+    runaway that collapsed the lr 0.01 pool run, profiles/r6); baseline="none" pushes its moves down."""
+    from alphago_amd.search.selfplay import GameRecords
+    from alphago_amd.train.engine import TorchPolicyTrainer
+
+    torch.manual_seed(0)
+    pol = _policy(torch.device("cpu"))
+    gs = go.GameState(9)
+    planes = pol.preprocessor.states_to_uint8([gs])
+    lost = GameRecords(planes=[planes, planes], moves=[np.array([40]), np.array([0])], winners=[-1, 1],
+                       learner_colors=[1, -1])
+    w0 = [p.detach().clone() for p in pol.model.parameters()]
+    tr = TorchPolicyTrainer(pol.model, 16, lr=1.0, device="cpu")
+    info = rl.rl_update(tr, lost, 16, torch.device("cpu"))
+    assert info["baseline"] == -1.0 and info["grad_norm"] == 0.0
+    assert all(torch.equal(a, b) for a, b in zip(w0, pol.model.parameters()))
+    p0 = torch.softmax(pol.model.logits_torch(torch.from_numpy(planes).float()), 1)[0]
+    rl.rl_update(tr, lost, 16, torch.device("cpu"), baseline="none")
+    p1 = torch.softmax(pol.model.logits_torch(torch.from_numpy(planes).float()), 1)[0]
+    assert (p1[40].log() + p1[0].log()) < (p0[40].log() + p0[0].log())  # the played moves, pushed down
+    # mixed outcomes: won-game moves up, lost-game moves down around the mean
+    mixed = GameRecords(planes=[planes, planes, planes], moves=[np.array([40]), np.array([0]), np.array([5])],
+                        winners=[1, 1, 1], learner_colors=[1, 1, -1])
+    info = rl.rl_update(tr, mixed, 16, torch.device("cpu"))
+    assert abs(info["baseline"] - 1.0 / 3.0) < 1e-9
+
+
 def test_value_generate_and_train_cpu(tmp_path):
     cpu = torch.device("cpu")
     sl, rlp = _policy(cpu), _policy(cpu)
