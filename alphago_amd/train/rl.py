@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -50,7 +51,8 @@ from . import checkpoint as ckpt
 from .engine import make_policy_trainer
 
 
-def rl_update(trainer, records, B: int, device, loss: str = "reinforce", baseline: str = "mean") -> dict:
+def rl_update(trainer, records, B: int, device, loss: str = "reinforce", baseline: str = "mean",
+              clip_grad_norm: float = 0.0) -> dict:
     """One policy-gradient step over all learner positions of a batch of games
     (``loss="reference"``: the reference's per-game binary-CE steps instead).
 
@@ -58,7 +60,12 @@ def rl_update(trainer, records, B: int, device, loss: str = "reinforce", baselin
     learner positions of the iteration (all ranks).  Without it (``"none"``, the paper's form) an iteration
     the learner loses entirely pushes down every move it played and nothing up; at lr 0.01 from a 12 x 192
     SL net that feedback collapsed the policy within one iteration after 34 iterations of gains
-    (profiles/r6/README.md).  With the baseline such an iteration does not move the weights."""
+    (profiles/r6/README.md).  With the baseline such an iteration does not move the weights.
+
+    ``clip_grad_norm`` > 0: the update's gradient is scaled down to at most this L2 norm, and an update
+    with a non-finite gradient is skipped (the weights stay finite).  With the baseline at lr 0.01 the
+    gradient norm stayed at 2-6 for 22 iterations, then grew to 65, 373 and 1.6e5 and the weights
+    diverged (profiles/r6/README.md)."""
     if loss == "reference":
         return _reference_bce_update(trainer, records, B, device)
     X, T, Z = [], [], []
@@ -91,8 +98,14 @@ def rl_update(trainer, records, B: int, device, loss: str = "reinforce", baselin
     scale = float(B) / max(1, n)
     _accumulate_grads(trainer, X, T, (Z - b) * scale, B, device, n_chunks)
     gnorm = float(trainer.fp.grad.norm())
-    trainer.apply_update()
-    return {"positions": n, "mean_reward": mean_reward, "baseline": b, "grad_norm": gnorm}
+    skipped = not math.isfinite(gnorm)
+    if skipped:  # every rank sees the same all-reduced gradient, so every rank skips
+        trainer.fp.grad.zero_()
+    elif clip_grad_norm > 0 and gnorm > clip_grad_norm:
+        trainer.fp.grad.mul_(clip_grad_norm / gnorm)
+    if not skipped:
+        trainer.apply_update()
+    return {"positions": n, "mean_reward": mean_reward, "baseline": b, "grad_norm": gnorm, "skipped": skipped}
 
 
 def _accumulate_grads(trainer, X, T, W, B, device, n_chunks) -> None:
@@ -185,6 +198,9 @@ def _parser():
     p.add_argument("--loss", default="reinforce", choices=["reinforce", "reference"])
     p.add_argument("--baseline", default="mean", choices=["mean", "none"],
                    help="reinforce: subtract the iteration's mean outcome from z (none: the paper's plain z)")
+    p.add_argument("--clip-grad-norm", type=float, default=0.0,
+                   help="reinforce: scale each update's gradient to at most this L2 norm and skip non-finite "
+                        "updates (0: off)")
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--metrics", default=None)
@@ -267,7 +283,7 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
         learner_pol.refresh()
         rec = play_games(learner, opponent, args.game_batch_size, size=size, max_moves=args.max_moves, rng=rng,
                          standard_two_pass=args.standard_two_pass)
-        info = rl_update(trainer, rec, args.minibatch, dev, args.loss, args.baseline)
+        info = rl_update(trainer, rec, args.minibatch, dev, args.loss, args.baseline, args.clip_grad_norm)
         learner_pol.refresh()
         wins = sum(1 for w, c in zip(rec.winners, rec.learner_colors) if w == c)
         tot = torch.tensor([float(wins), float(len(rec.winners)), float(sum(rec.lengths))], dtype=torch.float64,

@@ -140,7 +140,8 @@ def stage_rl(a):
                "--learning_rate", str(a.lr), "--save_every", str(a.save_every), "--game_batch_size", str(a.games),
                "--iterations", str(a.iterations), "--minibatch", str(a.batch), "--backend", HIP,
                "--metrics", metrics, "--checkpoint-dir", os.path.join(a.work, "rl_ck"), "--checkpoint-every",
-               str(a.iterations), "--seed", str(a.seed), "--verbose"])
+               str(a.iterations), "--seed", str(a.seed), "--verbose", "--baseline", a.baseline,
+               "--clip-grad-norm", str(a.clip)])
     last = res["pool"][-1]
     assert last is not None
     shutil.copy(last, os.path.join(nets, "rl%s.hdf5" % a.tag))
@@ -149,6 +150,8 @@ def stage_rl(a):
     h = res["history"]
     dump(os.path.join(a.out, "rl_summary%s.json" % a.tag),
          {"iterations": a.iterations, "games_per_iteration": a.games, "lr": a.lr, "save_every": a.save_every,
+          "baseline": a.baseline, "clip_grad_norm": a.clip,
+          "skipped_updates": int(sum(1 for r in res["history"] if r.get("skipped"))),
           "opponent_pool": "the SL net only" if a.save_every >= a.iterations else
           "the SL net + a snapshot every %d iterations, one drawn uniformly per iteration" % a.save_every,
           "seconds": round(time.perf_counter() - t0, 1), "final_weights": os.path.basename(last),
@@ -381,6 +384,8 @@ def main():
     ap.add_argument("--leaves", type=int, default=32)
     ap.add_argument("--latency-moves", type=int, default=40)
     ap.add_argument("--opening", type=int, default=8, help="search: random opening moves per game pair")
+    ap.add_argument("--baseline", default="mean", choices=["mean", "none"], help="rl: REINFORCE baseline")
+    ap.add_argument("--clip", type=float, default=0.0, help="rl: gradient-norm clip (0: off)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--small", action="store_true", help="tiny nets (CPU rehearsal of the pipeline)")
     ap.add_argument("--nets", default=None, help="where the nets are read / written (default OUT/nets)")

@@ -144,6 +144,12 @@ def test_reinforce_mean_baseline():
                         winners=[1, 1, 1], learner_colors=[1, 1, -1])
     info = rl.rl_update(tr, mixed, 16, torch.device("cpu"))
     assert abs(info["baseline"] - 1.0 / 3.0) < 1e-9
+    # gradient clipping: the applied step is the clipped gradient's
+    w1 = [p.detach().clone() for p in pol.model.parameters()]
+    info = rl.rl_update(tr, mixed, 16, torch.device("cpu"), clip_grad_norm=1e-3)
+    assert info["grad_norm"] > 1e-3 and not info["skipped"]
+    step = torch.sqrt(sum(((a - b) ** 2).sum() for a, b in zip(pol.model.parameters(), w1)))
+    assert abs(float(step) - 1e-3 * tr.sched.lr) / (1e-3 * tr.sched.lr) < 1e-3
 
 
 def test_value_generate_and_train_cpu(tmp_path):
