@@ -501,7 +501,7 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
 // float4 elements (4 consecutive input channels of one tap and output
 // channel), up to 8 16-B loads in flight; the four partials meet in LDS.  The OIHW
 // write is strided but touches the (small) gradient once.
-__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(WgradReduceArgs a) {
+__device__ __forceinline__ void wgrad_reduce_body(const WgradReduceArgs& a, int bid, int nblk) {
   __shared__ f32x4 part[4][64];
   const int C4 = a.Cin >> 2;
   const int total = a.T * a.Cout_real * C4;
@@ -509,7 +509,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(WgradReduceArgs 
   const size_t sstride = (size_t)a.T * tile;
   const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n4 = a.nsplit & ~3;
-  for (int base = blockIdx.x * 64; base < total; base += gridDim.x * 64) {  // block-uniform trip count
+  for (int base = bid * 64; base < total; base += nblk * 64) {  // block-uniform trip count
     const int idx = base + lane;
     const int e = idx < total ? idx : total - 1;
     const int c = (e % C4) << 2;
@@ -548,7 +548,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(WgradReduceArgs 
     }
     __syncthreads();
   }
-  if (blockIdx.x == gridDim.x - 1 && a.grad_b) {
+  if (bid == nblk - 1 && a.grad_b) {
     // bias: one sequential sum per channel (fixed order) with 8 loads in flight --
     // a load-add chain of nsplit dependent steps set this kernel's duration
     for (int n = threadIdx.x; n < a.Cout_real; n += blockDim.x) {
@@ -568,11 +568,42 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(WgradReduceArgs 
   }
 }
 
-void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st) {
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(WgradReduceArgs a) {
+  wgrad_reduce_body(a, blockIdx.x, gridDim.x);
+}
+
+// Every layer's split-K reduce in ONE launch (the deferred small-batch backward, ops.conv_wgrad_reduce_multi):
+// block b runs job j's reduce body as block b - first[j] of nblk[j], the same fixed summation order as
+// the per-layer kernel, so the gradients are bitwise equal to twelve separate launches.
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_multi_kernel(WgradReduceMultiArgs m) {
+  int j = 0;
+  while (j + 1 < m.n && (int)blockIdx.x >= m.first[j + 1]) ++j;  // block-uniform
+  wgrad_reduce_body(m.job[j], (int)blockIdx.x - m.first[j], m.nblk[j]);
+}
+
+static int wgrad_reduce_blocks(const WgradReduceArgs& a) {
   const int total = a.T * a.Cout_real * (a.Cin >> 2);
   int blocks = (total + 63) / 64;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a);
+  return blocks > 8192 ? 8192 : blocks;
+}
+
+void launch_wgrad_reduce_multi(const std::vector<WgradReduceArgs>& jobs, hipStream_t st) {
+  if (jobs.empty()) return;
+  if ((int)jobs.size() > kMaxReduceJobs) throw std::invalid_argument("conv_wgrad_reduce_multi: too many layers");
+  WgradReduceMultiArgs m{};
+  m.n = (int)jobs.size();
+  int blocks = 0;
+  for (int j = 0; j < m.n; ++j) {
+    m.job[j] = jobs[j];
+    m.first[j] = blocks;
+    m.nblk[j] = wgrad_reduce_blocks(jobs[j]);
+    blocks += m.nblk[j];
+  }
+  hipLaunchKernelGGL(conv_wgrad_reduce_multi_kernel, dim3(blocks), dim3(256), 0, st, m);
+}
+
+void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(wgrad_reduce_blocks(a)), dim3(256), 0, st, a);
 }
 
 }  // namespace agk

@@ -88,6 +88,12 @@ struct WgradReduceArgs {
   int T, Cout, Cin, Cout_real, Cin_real, nsplit;
   float scale, beta;  // grad = beta*grad + scale*sum
 };
+constexpr int kMaxReduceJobs = 16;
+struct WgradReduceMultiArgs {
+  WgradReduceArgs job[kMaxReduceJobs];
+  int first[kMaxReduceJobs], nblk[kMaxReduceJobs];
+  int n;
+};
 
 struct PolicyHeadArgs {
   const __bf16* y;     // padded NHWC (HP = S+2, P = 1, C)
@@ -248,6 +254,7 @@ void launch_invalid_config_probe(hipStream_t st);
 unsigned debug_error_fetch_and_clear(hipStream_t st);
 #endif
 void launch_wgrad_reduce(const WgradReduceArgs& a, hipStream_t st);
+void launch_wgrad_reduce_multi(const std::vector<WgradReduceArgs>& jobs, hipStream_t st);
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st);
 void launch_head_logits(const PolicyHeadArgs& a, hipStream_t st);
 void launch_head_backward(const PolicyHeadArgs& a, const float* dlogits, hipStream_t st);

@@ -124,13 +124,19 @@ void conv_wgrad_direct(const Tensor& x, const Tensor& dz, const Tensor& grad_w, 
   launch_check("conv_wgrad_direct");
 }
 
-void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
-                       double scale, double beta) {
+static agk::WgradReduceArgs reduce_args(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w,
+                                        const c10::optional<Tensor>& grad_b, double scale, double beta) {
   check_dev("conv_wgrad_reduce", slab, dbslab, grad_w, grad_b);
-  CHECK_F32(slab); CHECK_F32(grad_w); CHECK_CONTIG(grad_w);
+  CHECK_F32(slab); CHECK_F32(grad_w); CHECK_CONTIG(grad_w); CHECK_CONTIG(slab); CHECK_CONTIG(dbslab);
+  TORCH_CHECK(slab.dim() == 4 && dbslab.dim() == 2 && dbslab.size(0) == slab.size(0) && dbslab.size(1) == slab.size(2),
+              "slab (nsplit, T, Cout, Cin), dbslab (nsplit, Cout)");
   const int64_t nsplit = slab.size(0), T = slab.size(1), Cout = slab.size(2), Cin = slab.size(3);
   TORCH_CHECK(grad_w.dim() == 4 && grad_w.size(2) * grad_w.size(3) == T, "grad_w must be OIHW");
   TORCH_CHECK(Cin % 4 == 0, "slab channels must be a multiple of 4 (16-byte split reads)");
+  if (grad_b.has_value()) {
+    CHECK_F32(*grad_b);
+    TORCH_CHECK(grad_b->numel() == grad_w.size(0), "grad_b: (Cout_real,)");
+  }
   agk::WgradReduceArgs a{};
   a.slab = slab.data_ptr<float>();
   a.dbias_slab = dbslab.data_ptr<float>();
@@ -141,8 +147,28 @@ void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& g
   TORCH_CHECK(a.Cout_real <= Cout && a.Cin_real <= Cin, "grad_w larger than padded slab");
   a.nsplit = (int)nsplit;
   a.scale = (float)scale; a.beta = (float)beta;
-  agk::launch_wgrad_reduce(a, cur_stream());
+  return a;
+}
+
+void conv_wgrad_reduce(const Tensor& slab, const Tensor& dbslab, const Tensor& grad_w, const c10::optional<Tensor>& grad_b,
+                       double scale, double beta) {
+  agk::launch_wgrad_reduce(reduce_args(slab, dbslab, grad_w, grad_b, scale, beta), cur_stream());
   launch_check("conv_wgrad_reduce");
+}
+
+// every listed layer's split-K reduce in one launch (same summation order as conv_wgrad_reduce)
+void conv_wgrad_reduce_multi(const std::vector<Tensor>& slabs, const std::vector<Tensor>& dbslabs,
+                             const std::vector<Tensor>& grad_ws, const std::vector<Tensor>& grad_bs, double scale,
+                             double beta) {
+  TORCH_CHECK(slabs.size() == dbslabs.size() && slabs.size() == grad_ws.size() && slabs.size() == grad_bs.size(),
+              "conv_wgrad_reduce_multi: one slab, dbias slab, grad_w and grad_b per layer");
+  TORCH_CHECK((int)slabs.size() <= agk::kMaxReduceJobs, "conv_wgrad_reduce_multi: at most ", agk::kMaxReduceJobs,
+              " layers");
+  std::vector<agk::WgradReduceArgs> jobs;
+  for (size_t i = 0; i < slabs.size(); ++i)
+    jobs.push_back(reduce_args(slabs[i], dbslabs[i], grad_ws[i], grad_bs[i], scale, beta));
+  agk::launch_wgrad_reduce_multi(jobs, cur_stream());
+  launch_check("conv_wgrad_reduce_multi");
 }
 
 void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::optional<Tensor>& target,
@@ -792,6 +818,8 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def("sample_moves(Tensor probs, Tensor has, Tensor(a!) out, float beta, int seed) -> ()");
   m.def("conv_wgrad(Tensor x, Tensor dz, Tensor(a!) slab, Tensor(b!) dbslab, int K, int S, int Pin, int Po, int cin_real=0, int variant=0) -> ()");
   m.def("conv_wgrad_reduce(Tensor slab, Tensor dbslab, Tensor(a!) grad_w, Tensor(b!)? grad_b, float scale, float beta) -> ()");
+  m.def("conv_wgrad_reduce_multi(Tensor[] slabs, Tensor[] dbslabs, Tensor(a!)[] grad_ws, Tensor(b!)[] grad_bs, "
+        "float scale, float beta) -> ()");
   m.def("conv_wgrad_direct(Tensor x, Tensor dz, Tensor(a!) grad_w, Tensor(b!)? grad_b, int K, int S, int Pin, int Po, "
         "float scale=1.0, float beta=0.0, int ksub=4) -> ()");
   m.def("wgrad_direct_supported(int cout, int cin, int cin_real, int K) -> bool", &wgrad_direct_supported_op);
@@ -866,6 +894,7 @@ TORCH_LIBRARY_IMPL(alphago_amd, CUDA, m) {
   m.impl("conv_wgrad", &conv_wgrad);
   m.impl("conv_wgrad_reduce", &conv_wgrad_reduce);
   m.impl("conv_wgrad_direct", &conv_wgrad_direct);
+  m.impl("conv_wgrad_reduce_multi", &conv_wgrad_reduce_multi);
   m.impl("conv_dgrad_bits_bf8", &conv_dgrad_bits_bf8);
   m.impl("conv_wgrad_fp8", &conv_wgrad_fp8);
   m.impl("policy_head", &policy_head);

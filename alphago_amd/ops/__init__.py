@@ -256,6 +256,13 @@ def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, bet
     _ops().conv_wgrad_reduce(slab, dbslab, grad_w, grad_b, scale, beta)
 
 
+def conv_wgrad_reduce_multi(slabs, dbslabs, grad_ws, grad_bs, scale: float = 1.0, beta: float = 0.0):
+    """Every listed layer's split-K reduce in ONE launch (<= 16 layers); bitwise equal to one
+    ``conv_wgrad_reduce`` per layer (same fixed summation order)."""
+    _ops().conv_wgrad_reduce_multi(list(slabs), list(dbslabs), list(grad_ws), list(grad_bs), float(scale),
+                                   float(beta))
+
+
 def conv_wgrad_direct(x, dz, grad_w, grad_b, K: int, S: int, Pin: int, Po: int = 1, scale: float = 1.0,
                       beta: float = 0.0, ksub: int = 4):
     """Split-free weight gradient (C++ kWgradDirect): every workgroup owns one 32 x 48 (or 32 x 32) tile of

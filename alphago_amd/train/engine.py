@@ -181,6 +181,8 @@ OVERLAP_AUTO_MIN_PIXELS, OVERLAP_AUTO_MAX_PIXELS = 17 * 361, 256 * 361
 # B = 1 7.8 vs 19.3 us (split-K + reduce), B = 4 16.9 vs 21.2, B = 8 27.1 vs 24.8, B = 16 48.6 vs 26.2
 # (ksub 4; profiles/r6/raw/wgrad_direct_bench_v1.jsonl)
 WGRAD_DIRECT_MAX_PIXELS = 4 * 361
+# one merged split-K reduce launch per backward (HipConvTrainer merged_reduce) up to this many pixels
+MERGED_REDUCE_MAX_PIXELS = 0  # off until measured (profiles/r6/README.md)
 
 
 class HipConvTrainer:
@@ -192,7 +194,8 @@ class HipConvTrainer:
                  reduce_stream: Optional[bool] = None, wgrad_variant: Optional[int] = None,
                  fp8_wgrad: Optional[bool] = None, optimizer: str = "sgd", momentum: float = 0.0,
                  nesterov: bool = False, fp8_bf16_layers: Optional[Sequence[int]] = None,
-                 wgrad_direct: Optional[bool] = None, wgrad_ksub: int = 4, fp8_scale_guard: int = 0):
+                 wgrad_direct: Optional[bool] = None, wgrad_ksub: int = 4, fp8_scale_guard: int = 0,
+                 merged_reduce: Optional[bool] = None):
         ops.load()
         # fp8 underflow guard: activation scale exponents fall by at most this many binades per step
         # (ops.fp8_act_scales max_drop; 0 = the plain one-step delayed scale, the default: SL at lr 0.05
@@ -367,6 +370,16 @@ class HipConvTrainer:
         self._proxy = agdist.CommProxy.from_env(self.fp.grad, self.buckets) if not self.env.distributed else None
         if self._proxy is not None:
             self.reducer = self._proxy
+        # merged reduce (one process, small batches): every layer's wgrad keeps its own split slab and ONE
+        # ops.conv_wgrad_reduce_multi launch after the backward sums them all (the same fixed order per
+        # element as the per-layer reduce, so bitwise equal) instead of a reduce launch per layer.  Without
+        # a gradient all-reduce to overlap nothing waits for an early reduce.
+        if merged_reduce is None:
+            merged_reduce = M <= MERGED_REDUCE_MAX_PIXELS
+        self.merged_reduce = (bool(merged_reduce) and not self.env.distributed and self._proxy is None
+                              and self.s_r is None and self.L <= 16)
+        self._mslabs = [None] * self.L  # per-layer (slab, dbias slab), allocated at first use
+        self._pending_reduce = []
         # ALPHAGO_AMD_DEFER_ALLREDUCE=1: launch every bucket after the backward instead of at its bucket
         # point (no overlap, no CU contention with the dgrad / wgrad kernels)
         self.defer_allreduce = os.environ.get("ALPHAGO_AMD_DEFER_ALLREDUCE", "0") == "1"
@@ -598,6 +611,23 @@ class HipConvTrainer:
         sr = self.s_r
         if sr is not None and self._slab_free[i] is not None:
             torch.cuda.current_stream(self.device).wait_event(self._slab_free[i])
+        if self.merged_reduce and not (self.wgrad_direct[l] and not f8):
+            # this layer's own slab; the reduce waits for the merged launch after the backward
+            if self._mslabs[l] is None or self._mslabs[l][0].numel() < ns * T * self.Fp * cin_p:
+                self._mslabs[l] = (torch.empty(ns * T * self.Fp * cin_p, device=self.device),
+                                   torch.zeros(ns * self.Fp, device=self.device))
+            sl, db = self._mslabs[l]
+            slab = sl[:ns * T * self.Fp * cin_p].view(ns, T, self.Fp, cin_p)
+            dbs = db[:ns * self.Fp].view(ns, self.Fp)
+            if f8:
+                ops.conv_wgrad_fp8(self.X8[l], self.DZ8[l], slab, dbs, self.xscale8[l], self.gscales8[l, 0:1],
+                                   self.gosc8[l:l + 1], self.K[l], self.S, pin, 1,
+                                   amax=self.gamax8[l] if l < self.L - 1 else None)
+            else:
+                ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1,
+                               cin_real=self.C0 if l == 0 else 0, variant=self.wgrad_var[l])
+            self._pending_reduce.append((slab, dbs, l))
+            return
         if self.wgrad_direct[l] and not f8:  # split-free: the OIHW gradient straight from the kernel
             ops.conv_wgrad_direct(x, self.DZ[l], self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l],
                                   self.K[l], self.S, pin, 1, 1.0, 0.0, self.wgrad_ksub)
@@ -689,6 +719,12 @@ class HipConvTrainer:
             main.wait_stream(self.s_w)
         if self.s_r is not None:
             main.wait_stream(self.s_r)
+        if self._pending_reduce:  # merged reduce: every deferred layer's split slab in one launch
+            pr = self._pending_reduce
+            ops.conv_wgrad_reduce_multi([p[0] for p in pr], [p[1] for p in pr],
+                                        [self.fp.grad_views["w%d" % p[2]] for p in pr],
+                                        [self.fp.grad_views["b%d" % p[2]] for p in pr], 1.0, 0.0)
+            self._pending_reduce = []
         if self.precision == "fp8" and (self.fp8_dgrad or self.fp8_wgrad):
             if self._g8_calibrated:
                 ops.fp8_grad_scales(self.gamax8, self.gscales8, self.gosc8, 1)  # next step's gradient scales

@@ -52,7 +52,7 @@ from .engine import make_policy_trainer
 
 
 def rl_update(trainer, records, B: int, device, loss: str = "reinforce", baseline: str = "mean",
-              clip_grad_norm: float = 0.0) -> dict:
+              clip_grad_norm: float = 0.0, weight_decay: float = 0.0) -> dict:
     """One policy-gradient step over all learner positions of a batch of games
     (``loss="reference"``: the reference's per-game binary-CE steps instead).
 
@@ -65,7 +65,9 @@ def rl_update(trainer, records, B: int, device, loss: str = "reinforce", baselin
     ``clip_grad_norm`` > 0: the update's gradient is scaled down to at most this L2 norm, and an update
     with a non-finite gradient is skipped (the weights stay finite).  With the baseline at lr 0.01 the
     gradient norm stayed at 2-6 for 22 iterations, then grew to 65, 373 and 1.6e5 and the weights
-    diverged (profiles/r6/README.md)."""
+    diverged (profiles/r6/README.md).  ``weight_decay``: L2 term wd * w added to the gradient (before the
+    clip): the ReLU trunk has no normalisation, and a sharpening policy grows its weights and with them
+    the gradient norm (2 -> 100 over 60 iterations at lr 0.003, profiles/r6/README.md)."""
     if loss == "reference":
         return _reference_bce_update(trainer, records, B, device)
     X, T, Z = [], [], []
@@ -97,6 +99,8 @@ def rl_update(trainer, records, B: int, device, loss: str = "reinforce", baselin
         raise ValueError("baseline must be 'mean' or 'none'")
     scale = float(B) / max(1, n)
     _accumulate_grads(trainer, X, T, (Z - b) * scale, B, device, n_chunks)
+    if weight_decay > 0:
+        trainer.fp.grad.add_(trainer.fp.flat, alpha=weight_decay)
     gnorm = float(trainer.fp.grad.norm())
     skipped = not math.isfinite(gnorm)
     if skipped:  # every rank sees the same all-reduced gradient, so every rank skips
@@ -201,6 +205,11 @@ def _parser():
     p.add_argument("--clip-grad-norm", type=float, default=0.0,
                    help="reinforce: scale each update's gradient to at most this L2 norm and skip non-finite "
                         "updates (0: off)")
+    p.add_argument("--weight-decay", type=float, default=0.0, help="reinforce: L2 weight decay added to the gradient")
+    p.add_argument("--eval-every", type=int, default=0,
+                   help="every N iterations play --eval-games games against the initial weights (recorded as "
+                        "eval_win_rate); the best snapshot is kept as model_folder/best.hdf5 (0: off)")
+    p.add_argument("--eval-games", type=int, default=200)
     p.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--metrics", default=None)
@@ -231,6 +240,12 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
                                   device=dev)
     learner = BatchedSampler(learner_pol, args.temperature, seed=args.seed * 31 + env.rank)
     opponent = BatchedSampler(opp_pol, args.temperature, seed=args.seed * 37 + env.rank + 1)
+    ref_pol = ev_learner = ev_ref = None
+    best = {"eval_win_rate": -1.0, "iteration": -1, "path": None}
+    if args.eval_every > 0:  # the fixed reference: the initial weights, with evaluation samplers of their own
+        ref_pol = CNNPolicy.load_model(args.initial_json, device=dev, weights_file=args.initial_weights)
+        ev_learner = BatchedSampler(learner_pol, args.temperature, seed=args.seed * 41 + env.rank + 7)
+        ev_ref = BatchedSampler(ref_pol, args.temperature, seed=args.seed * 43 + env.rank + 9)
     pool: List[Optional[str]] = [None]  # None = the initial weights
     folder = args.model_folder
     if folder:
@@ -283,7 +298,8 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
         learner_pol.refresh()
         rec = play_games(learner, opponent, args.game_batch_size, size=size, max_moves=args.max_moves, rng=rng,
                          standard_two_pass=args.standard_two_pass)
-        info = rl_update(trainer, rec, args.minibatch, dev, args.loss, args.baseline, args.clip_grad_norm)
+        info = rl_update(trainer, rec, args.minibatch, dev, args.loss, args.baseline, args.clip_grad_norm,
+                         args.weight_decay)
         learner_pol.refresh()
         wins = sum(1 for w, c in zip(rec.winners, rec.learner_colors) if w == c)
         tot = torch.tensor([float(wins), float(len(rec.winners)), float(sum(rec.lengths))], dtype=torch.float64,
@@ -292,6 +308,21 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
         dt = time.perf_counter() - t0
         row = {"iteration": it, "wins": int(tot[0]), "games": int(tot[1]), "win_rate": float(tot[0] / tot[1]),
                "games_per_s": float(tot[1]) / dt, "moves_per_s": float(tot[2]) / dt, **info}
+        if args.eval_every > 0 and (it + 1) % args.eval_every == 0:
+            g = args.eval_games
+            er = play_games(ev_learner, ev_ref, g, size=size, max_moves=args.max_moves, rng=rng, record=False,
+                            learner_colors=[go.BLACK if i % 2 == 0 else go.WHITE for i in range(g)],
+                            standard_two_pass=args.standard_two_pass)
+            ew = torch.tensor([float(sum(1 for w, c in zip(er.winners, er.learner_colors) if w == c)), float(g)],
+                              dtype=torch.float64, device=dev if env.backend == "nccl" else "cpu")
+            agdist.all_reduce_sum_(ew)
+            row["eval_win_rate"] = float(ew[0] / ew[1])
+            if folder and row["eval_win_rate"] > best["eval_win_rate"]:
+                best.update(eval_win_rate=row["eval_win_rate"], iteration=it + 1,
+                            path=os.path.join(folder, "best.hdf5"))
+                if env.is_main:
+                    learner_pol.save_weights(best["path"])
+                agdist.barrier()
         history.append(row)
         log.log(**row)
         if args.verbose and env.is_main:
@@ -307,7 +338,7 @@ def run(cmd_line_args: Optional[List[str]] = None) -> dict:
         if ck_path and ((it + 1) % args.checkpoint_every == 0 or it + 1 == args.iterations):
             save_checkpoint(it + 1)
     wd.stop()
-    return {"history": history, "pool": pool}
+    return {"history": history, "pool": pool, "best": best}
 
 
 if __name__ == "__main__":

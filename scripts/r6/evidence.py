@@ -141,8 +141,9 @@ def stage_rl(a):
                "--iterations", str(a.iterations), "--minibatch", str(a.batch), "--backend", HIP,
                "--metrics", metrics, "--checkpoint-dir", os.path.join(a.work, "rl_ck"), "--checkpoint-every",
                str(a.iterations), "--seed", str(a.seed), "--verbose", "--baseline", a.baseline,
-               "--clip-grad-norm", str(a.clip)])
-    last = res["pool"][-1]
+               "--clip-grad-norm", str(a.clip), "--weight-decay", str(a.wd), "--eval-every", str(a.eval_every),
+               "--eval-games", "200"])
+    last = res["best"]["path"] if a.eval_every > 0 and res["best"]["path"] else res["pool"][-1]
     assert last is not None
     shutil.copy(last, os.path.join(nets, "rl%s.hdf5" % a.tag))
     shutil.copy(os.path.join(nets, "sl.json"), os.path.join(nets, "rl%s.json" % a.tag))
@@ -150,7 +151,10 @@ def stage_rl(a):
     h = res["history"]
     dump(os.path.join(a.out, "rl_summary%s.json" % a.tag),
          {"iterations": a.iterations, "games_per_iteration": a.games, "lr": a.lr, "save_every": a.save_every,
-          "baseline": a.baseline, "clip_grad_norm": a.clip,
+          "baseline": a.baseline, "clip_grad_norm": a.clip, "weight_decay": a.wd, "eval_every": a.eval_every,
+          "selected": ("best eval snapshot (iteration %d, eval win rate %.3f over 200 games vs SL)" %
+                       (res["best"]["iteration"], res["best"]["eval_win_rate"])) if a.eval_every > 0 else "last",
+          "eval_curve": [(r["iteration"] + 1, round(r["eval_win_rate"], 3)) for r in h if "eval_win_rate" in r],
           "skipped_updates": int(sum(1 for r in res["history"] if r.get("skipped"))),
           "opponent_pool": "the SL net only" if a.save_every >= a.iterations else
           "the SL net + a snapshot every %d iterations, one drawn uniformly per iteration" % a.save_every,
@@ -386,6 +390,8 @@ def main():
     ap.add_argument("--opening", type=int, default=8, help="search: random opening moves per game pair")
     ap.add_argument("--baseline", default="mean", choices=["mean", "none"], help="rl: REINFORCE baseline")
     ap.add_argument("--clip", type=float, default=0.0, help="rl: gradient-norm clip (0: off)")
+    ap.add_argument("--wd", type=float, default=0.0, help="rl: weight decay")
+    ap.add_argument("--eval-every", type=int, default=0, help="rl: evaluate vs SL every N iterations, keep the best")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--small", action="store_true", help="tiny nets (CPU rehearsal of the pipeline)")
     ap.add_argument("--nets", default=None, help="where the nets are read / written (default OUT/nets)")

@@ -390,3 +390,38 @@ def test_weight_stationary_trainer_matches(cuda_device, monkeypatch, B, kind):
         t.apply_update()
     torch.cuda.synchronize()
     assert (a.fp.flat - b.fp.flat).abs().max().item() < 5e-3
+
+
+@pytest.mark.parametrize("B,kind,overlap", [(16, "policy", False), (48, "policy", True), (24, "value", False),
+                                            (3, "policy", False)])
+def test_merged_reduce_bitwise_equal(cuda_device, B, kind, overlap):
+    """merged_reduce: every layer's split slab kept and summed by ONE conv_wgrad_reduce_multi launch
+    after the backward -- bitwise the gradients of a reduce launch per layer (same summation order),
+    with the wgrads on the side stream too, and with the split-free layers (B <= 4) left as they are."""
+    import copy
+
+    from alphago_amd.models.nets import PolicyNet, ValueNet
+    from alphago_amd.train.engine import HipPolicyTrainer, HipValueTrainer
+
+    torch.manual_seed(9)
+    if kind == "policy":
+        net, C, cls = PolicyNet(48, filters_per_layer=192, layers=4), 48, HipPolicyTrainer
+    else:
+        net, C, cls = ValueNet(49, filters_per_layer=152, layers=4), 49, HipValueTrainer
+    trs = [cls(copy.deepcopy(net), B, lr=0.05, device=cuda_device, overlap=overlap, merged_reduce=m)
+           for m in (True, False)]
+    assert trs[0].merged_reduce and not trs[1].merged_reduce
+    planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    if kind == "policy":
+        tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
+    else:
+        tgt = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
+    for _ in range(2):
+        for t in trs:
+            t.compute_grads(planes, tgt)
+        torch.cuda.synchronize()
+        assert torch.equal(trs[0].fp.grad, trs[1].fp.grad)
+        for t in trs:
+            t.apply_update()
+    torch.cuda.synchronize()
+    assert torch.equal(trs[0].fp.flat, trs[1].fp.flat)

@@ -64,6 +64,16 @@ def test_rl_cli_cpu(tmp_path):
     out2 = rl.run([w, j, "--game_batch_size", "2", "--iterations", "1", "--minibatch", "64", "--max-moves", "60",
                    "--loss", "reference"])
     assert out2["history"][0]["games"] == 2
+    # stabilisers and model selection: weight decay, gradient clip, evaluation against the initial weights
+    # every 2 iterations with the best snapshot kept
+    folder3 = str(tmp_path / "pool3")
+    out3 = rl.run([w, j, "--model_folder", folder3, "--game_batch_size", "4", "--iterations", "4",
+                   "--save_every", "10", "--minibatch", "64", "--max-moves", "60", "--backend", "torch",
+                   "--weight-decay", "1e-4", "--clip-grad-norm", "1.0", "--eval-every", "2", "--eval-games", "4"])
+    evs = [r.get("eval_win_rate") for r in out3["history"]]
+    assert evs[0] is None and evs[2] is None and evs[1] is not None and evs[3] is not None
+    assert out3["best"]["iteration"] in (2, 4) and out3["best"]["eval_win_rate"] == max(evs[1], evs[3])
+    assert os.path.exists(os.path.join(folder3, "best.hdf5"))
 
 
 def test_reference_bce_update_matches_keras_semantics():
