@@ -66,10 +66,10 @@ class MCTSPlayer(object):
     """Plays the most visited move of a batched PUCT search (see search.mcts)."""
 
     def __init__(self, policy, value=None, n_playout: int = 1600, c_puct: float = 5.0, lmbda: float = 0.0,
-                 leaves_per_batch: int = 16, temperature: float = 0.0, seed: int = 0):
+                 leaves_per_batch: int = 16, temperature: float = 0.0, seed: int = 0, threads: Optional[int] = None):
         from .mcts import BatchedMCTS
 
-        self.search = BatchedMCTS(policy, value, n_trees=1, c_puct=c_puct, lmbda=lmbda, seed=seed)
+        self.search = BatchedMCTS(policy, value, n_trees=1, c_puct=c_puct, lmbda=lmbda, seed=seed, threads=threads)
         self.n_playout = n_playout
         self.leaves_per_batch = leaves_per_batch
         self.temperature = temperature
@@ -95,9 +95,9 @@ class MCTSPlayer(object):
             left = time_budget - (now - t0)
             if done >= self.n_playout or left <= 0:
                 return move
-            # next chunk: double the last, capped by the playout budget and by half the time left (the
-            # per-playout time of a loaded host varies from chunk to chunk)
-            chunk = int(min(2 * chunk, self.n_playout - done, 0.5 * left / max(per, 1e-6)))
+            # next chunk: double the last, capped by the playout budget and by a third of the time left
+            # (the per-playout time of a loaded host varies from chunk to chunk)
+            chunk = int(min(2 * chunk, self.n_playout - done, left / 3.0 / max(per, 1e-6)))
             if chunk < 1:
                 return move
 

@@ -18,22 +18,23 @@ def _player():
     p = CNNPolicy(FEATS, board=19, filters_per_layer=8, layers=2, device=CPU)
     v = CNNValue(FEATS, board=19, filters_per_layer=8, layers=2, dense=16, device=CPU)
     # a playout budget no clock allows: only the time budget can end the search
-    return MCTSPlayer(p, v, n_playout=10 ** 7, leaves_per_batch=8)
+    return MCTSPlayer(p, v, n_playout=10 ** 7, leaves_per_batch=8, threads=2)
 
 
 def test_genmove_within_byoyomi_period():
-    """time_settings 0 1 1 (1 s per move): every genmove returns inside its second, after a real search."""
+    """time_settings 0 2 1 (2 s per move): every genmove returns inside its period, after a real search.
+    (2 s rather than 1: the CPU suite runs this beside multi-process tests on a loaded host.)"""
     pl = _player()
     eng = GTPEngine(pl, size=19)
-    assert eng.send("time_settings 0 1 1") == "=\n\n"
+    assert eng.send("time_settings 0 2 1") == "=\n\n"
     pl.get_move(go.GameState(19), time_budget=0.05)  # warm the engines (first forwards)
     for colour in ("b", "w", "b"):
         t0 = time.perf_counter()
         reply = eng.send("genmove %s" % colour)
         dt = time.perf_counter() - t0
         assert reply.startswith("= ") and reply.strip() != "= pass", reply
-        assert dt < 1.0, dt
-        assert 0.5 < eng.last_budget < 1.0
+        assert dt < 2.0, dt
+        assert 1.5 < eng.last_budget < 2.0
     assert pl.search.forest.sims(0) > 8  # it searched, not a bare prior move
 
 
