@@ -182,7 +182,9 @@ OVERLAP_AUTO_MIN_PIXELS, OVERLAP_AUTO_MAX_PIXELS = 17 * 361, 256 * 361
 # (ksub 4; profiles/r6/raw/wgrad_direct_bench_v1.jsonl)
 WGRAD_DIRECT_MAX_PIXELS = 4 * 361
 # one merged split-K reduce launch per backward (HipConvTrainer merged_reduce) up to this many pixels
-MERGED_REDUCE_MAX_PIXELS = 0  # off until measured (profiles/r6/README.md)
+# off: slower at every batch measured (B = 16 / 32 / 64 / 128 / 2176: -4 / -10 / -4 / -7 / -0.6 %; the merged
+# launch reads twelve cold slabs, profiles/r6/README.md); merged_reduce=True opts in
+MERGED_REDUCE_MAX_PIXELS = 0
 
 
 class HipConvTrainer:
