@@ -23,6 +23,7 @@ for rep in 1 2; do
   for w in 0 256; do
     step head_w${w}_r$rep 150 python bench.py --wgrad-wgs $w --steps 30 --warmup 10
   done
+  step head_m1_r$rep 150 python bench.py --merged-reduce 1 --steps 30 --warmup 10
 done
 python3 - $O <<'PY'
 import glob, json, os, sys
