@@ -465,17 +465,6 @@ void launch_conv_wgrad(const ConvWgradArgs& a_in, hipStream_t st) {
     a.variant = 0;
   }
 #endif
-  if (a.variant == kWgradDual) {
-    if (a.Cout % 192 || a.Cin % 192 || a.cin_real != a.Cin)
-      throw std::invalid_argument("conv_wgrad: the dual-split tile needs 192-multiple widths");
-    constexpr int smem = 8 * (192 / 32 * (192 / 64) * 4 + 192 / 32) * 64 * 4;  // the half-1 hand-off
-    static const hipError_t attr = hipFuncSetAttribute((const void*)conv_wgrad_dual_kernel<192, 192, 4>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    hip_check(attr, "hipFuncSetAttribute(max dynamic LDS)");
-    dim3 grid((a.nsplit + 1) / 2, a.T, (a.Cout / 192) * (a.Cin / 192));
-    hipLaunchKernelGGL((conv_wgrad_dual_kernel<192, 192, 4>), grid, dim3(1024), smem, st, a);
-    return;
-  }
   if (a.variant == kWgradSmall) {
     // small batches (ops.wgrad_config): 64 x 64 output tiles with the kernel row's taps merged -- three
     // times the workgroups per pixel split of a 192 -> 192 layer

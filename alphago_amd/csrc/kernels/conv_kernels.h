@@ -1017,165 +1017,6 @@ __device__ __forceinline__ void wgrad_tile(const ConvWgradArgs& a, int split, in
   wgrad_store<WN, WC, NWC, TAPS, NWN>(a, acc, dbs, do_bias, split, t, n0, c0, wn, wc, lane, zero_split);
 }
 
-// DUAL (kWgradDual, the per-tap 192 x 192 tile of the large-batch step): one 1024-thread workgroup is two
-// 8-wave halves, each running the production tile above over its own pixel split (2 pair, 2 pair + 1).
-// After the K loop half 1's accumulators and bias partials meet half 0's in LDS, and half 0 writes ONE
-// partial for the pair: the split-K slab the wgrad writes and the reduce reads is halved, at the same
-// 16 waves per CU as two 512-thread workgroups (a 1-workgroup-per-CU grid with half the splits instead
-// ran the B = 2176 step 20 % slower: profiles/r6/README.md).  Both halves run half 0's trip count
-// (the longer); half 1 idles through steps past its own end, so every barrier is reached by all waves.
-template <int WN, int WC, int NWC>
-__device__ __forceinline__ void wgrad_tile_dual(const ConvWgradArgs& a, int pair, int t, int n0, int c0) {
-  constexpr int NWN = 2;
-  constexpr int NWAVES = NWN * NWC;
-  constexpr int NBn = WN / (16 * NWN);
-  constexpr int NBc = WC / (16 * NWC);
-  constexpr int DZ_BYTES = WN * 64;
-  constexpr int STAGE = DZ_BYTES + WC * 64;
-  constexpr int XP = WC / 16;
-  constexpr int NINSTR = WN / 16 + XP;
-  constexpr int IPW = NINSTR / NWAVES;
-  static_assert(NINSTR == NWAVES * IPW && (WN / 16) % IPW == 0, "dual: every wave stages IPW pieces of one tensor");
-  constexpr int PER = NBn * NBc * 4 + NBn;  // floats per lane handed from half 1 to half 0
-  static_assert(NWAVES * PER * 64 * 4 <= 160 * 1024 && 4 * STAGE <= NWAVES * PER * 64 * 4, "dual: LDS plan");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int lane = threadIdx.x & 63;
-  const int wave_all = wave_id();
-  const int half = wave_all >= NWAVES ? 1 : 0;
-  const int wave = wave_all - half * NWAVES;
-  const int wn = wave / NWC, wc = wave % NWC;
-  const int kh = t / a.K, kw = t - (t / a.K) * a.K;
-  const int toff = (kh * a.HPi + kw) * a.Cin + c0;
-  const int SS = a.S * a.S;
-  char* const mine = smem + half * 2 * STAGE;
-  const int nks_total = (a.M + 31) / 32;
-  const int kb0 = 2 * pair * a.ksteps_per_split;
-  const int ke0 = kb0 + a.ksteps_per_split < nks_total ? kb0 + a.ksteps_per_split : nks_total;
-  const int len0 = ke0 > kb0 ? ke0 - kb0 : 0;
-  const int kb = kb0 + half * a.ksteps_per_split;
-  const int ke = kb + a.ksteps_per_split < nks_total ? kb + a.ksteps_per_split : nks_total;
-  const int len = ke > kb ? ke - kb : 0;  // <= len0
-
-  auto stage = [&](int ks, int buf) {
-    const int half8 = (lane & 1) * 8;
-    char* base = mine + buf * STAGE;
-    const int px = ks * 32 + (lane >> 1);
-    const int pm = px < a.M ? px : a.M - 1;
-    const int b = fdiv(pm, a.divSS);
-    const int rem = pm - b * SS;
-    const int ii = fdiv(rem, a.divS);
-    const int jx = rem - ii * a.S;
-    const int dzr = px < a.M ? ((b * a.HPo + ii + a.Po) * a.HPo + jx + a.Po) * a.Cout : 0;  // 0 = zero border
-    const int xr = ((b * a.HPi + ii + a.offi) * a.HPi + jx + a.offi) * a.Cin + toff;
-    if (wave < (WN / 16) / IPW) {
-#pragma unroll
-      for (int i = 0; i < IPW; ++i)
-        glds16(a.dz + dzr + n0 + half8 + (wave * IPW + i) * 16, base + (wave * IPW + i) * 1024);
-    } else {
-#pragma unroll
-      for (int i = 0; i < IPW; ++i) {
-        const int xj = wave * IPW + i - WN / 16;
-        glds16(a.x + xr + half8 + xj * 16, base + (WN / 16 + xj) * 1024);
-      }
-    }
-  };
-
-  f32x4 acc[1][NBn][NBc];
-#pragma unroll
-  for (int i = 0; i < NBn; ++i)
-#pragma unroll
-    for (int j = 0; j < NBc; ++j) acc[0][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dbs[NBn];
-#pragma unroll
-  for (int i = 0; i < NBn; ++i) dbs[i] = 0.f;
-  const bool do_bias = (t == 0) && (c0 == 0) && (wc == 0);
-  const int g = lane >> 4;
-  const int q = (lane & 15) >> 2;
-  const int p = lane & 3;
-  const int tr0 = (4 * g + q) * 32 + p * 8;
-  const int tr1 = (16 + 4 * g + q) * 32 + p * 8;
-  constexpr int NF = NBn + NBc;
-
-  if (len > 0) stage(kb, 0);
-  wait_vmcnt0();
-  __syncthreads();
-  for (int it = 0; it < len0; ++it) {
-    const int cur = it & 1;
-    if (it + 1 < len) stage(kb + it + 1, cur ^ 1);
-    if (it < len) {
-      const char* base = mine + cur * STAGE;
-      bf16x4 tl[NF], th[NF];
-#pragma unroll
-      for (int i = 0; i < NBn; ++i) {
-        const char* cb = base + (wn * NBn + i) * 1024;
-        tl[i] = ds_read_tr16_asm(cb + tr0);
-        th[i] = ds_read_tr16_asm(cb + tr1);
-      }
-#pragma unroll
-      for (int j = 0; j < NBc; ++j) {
-        const char* cb = base + DZ_BYTES + (wc * NBc + j) * 1024;
-        tl[NBn + j] = ds_read_tr16_asm(cb + tr0);
-        th[NBn + j] = ds_read_tr16_asm(cb + tr1);
-      }
-      lgkm_fence<NF>(tl, th);
-      bf16x8 af[NBn], bfm[NBc];
-#pragma unroll
-      for (int i = 0; i < NBn; ++i)
-        af[i] = bf16x8{tl[i][0], tl[i][1], tl[i][2], tl[i][3], th[i][0], th[i][1], th[i][2], th[i][3]};
-#pragma unroll
-      for (int j = 0; j < NBc; ++j)
-        bfm[j] = bf16x8{tl[NBn + j][0], tl[NBn + j][1], tl[NBn + j][2], tl[NBn + j][3],
-                        th[NBn + j][0], th[NBn + j][1], th[NBn + j][2], th[NBn + j][3]};
-#pragma unroll
-      for (int i = 0; i < NBn; ++i)
-#pragma unroll
-        for (int j = 0; j < NBc; ++j) acc[0][i][j] = mfma16x16x32(af[i], bfm[j], acc[0][i][j]);
-      if (do_bias) {
-#pragma unroll
-        for (int i = 0; i < NBn; ++i) {
-          float s = 0.f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) s += (float)af[i][e];
-          dbs[i] += s;
-        }
-      }
-    }
-    wait_vmcnt0();
-    __syncthreads();
-  }
-  // the K loop's last barrier follows every LDS read: the staging area becomes the hand-off buffer
-  float* hand = reinterpret_cast<float*>(smem);
-  if (half == 1) {
-#pragma unroll
-    for (int i = 0; i < NBn; ++i)
-#pragma unroll
-      for (int j = 0; j < NBc; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) hand[(wave * PER + (i * NBc + j) * 4 + r) * 64 + lane] = acc[0][i][j][r];
-#pragma unroll
-    for (int i = 0; i < NBn; ++i) hand[(wave * PER + NBn * NBc * 4 + i) * 64 + lane] = dbs[i];
-  }
-  __syncthreads();
-  if (half == 0) {
-#pragma unroll
-    for (int i = 0; i < NBn; ++i)
-#pragma unroll
-      for (int j = 0; j < NBc; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[0][i][j][r] += hand[(wave * PER + (i * NBc + j) * 4 + r) * 64 + lane];
-#pragma unroll
-    for (int i = 0; i < NBn; ++i) dbs[i] += hand[(wave * PER + NBn * NBc * 4 + i) * 64 + lane];
-    wgrad_store<WN, WC, NWC, 1, NWN>(a, acc, dbs, do_bias, pair, t, n0, c0, wn, wc, lane, -1);
-  }
-}
-
-template <int WN, int WC, int NWC>
-__global__ __launch_bounds__(64 * 2 * NWC * 2, 1) void conv_wgrad_dual_kernel(ConvWgradArgs a) {
-  const int ncb = a.Cin / WC;
-  wgrad_tile_dual<WN, WC, NWC>(a, blockIdx.x, blockIdx.y, (blockIdx.z / ncb) * WN, (blockIdx.z % ncb) * WC);
-}
-
 // LINE staging (wgrad variants 6 and 7): every DMA piece moves 8 whole 128-byte pixel lines (one
 // 64-channel chunk of 8 pixels; lanes 8r..8r+7 fill line r, their 16-byte chunks XOR-swizzled by
 // ((r >> 1) & 3) << 1) -- 8 cache lines per instruction instead of the 32 partial (32-byte) lines

@@ -223,9 +223,6 @@ constexpr int kWgradSmall = 14;
 // split-free small-batch plan: 32 x 48 (or 32 x 32) per-tap tiles, each workgroup owns the whole pixel
 // range and writes the OIHW gradient itself (ConvWgradArgs::grad_w; conv_wgrad_direct)
 constexpr int kWgradDirect = 15;
-// two splits per 1024-thread workgroup, summed in LDS: the 192 x 192 per-tap tile writes ceil(nsplit / 2)
-// slab partials (reduce them as that many splits)
-constexpr int kWgradDual = 16;
 // weight-stationary order of standard (tap, Cout, Cin) bf16 packs (conv_ws.hip; tile 40 reads it)
 struct WsPackJob {
   const __bf16* src;

@@ -60,7 +60,7 @@ void conv_wgrad(const Tensor& x, const Tensor& dz, const Tensor& slab, const Ten
   check_dev("conv_wgrad", x, dz, slab, dbslab);
   // the per-tap / tap-merged kernel only; the round-4 variants (9 LDS ring, 10-13 first-layer re-cuts) and
   // the older lab variants run from torch.ops.alphago_amd_lab
-  TORCH_CHECK(variant == 0 || variant == agk::kWgradSmall || variant == agk::kWgradDual, "conv_wgrad variant ", variant,
+  TORCH_CHECK(variant == 0 || variant == agk::kWgradSmall, "conv_wgrad variant ", variant,
               " is a kernel-lab variant (alphago_amd.ops.lab())");
   conv_wgrad_impl(x, dz, slab, dbslab, K, S, Pin, Po, cin_real, (int)variant);
 }

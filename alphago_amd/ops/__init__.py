@@ -248,8 +248,8 @@ def conv_wgrad(x, dz, slab, dbslab, K: int, S: int, Pin: int, Po: int = 1, cin_r
     the kernel skip zero-padded input channels (only slab columns < cin_real are written).
     ``variant`` 0 = the production per-tap kernel; any other variant is a kernel-lab kernel
     (torch.ops.alphago_amd_lab: 9 = LDS ring, 10-13 = first-layer re-cuts, ...)."""
-    (_ops() if variant in (0, WGRAD_SMALL, WGRAD_DUAL) else lab()).conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po,
-                                                                              cin_real, variant)
+    (_ops() if variant in (0, WGRAD_SMALL) else lab()).conv_wgrad(x, dz, slab, dbslab, K, S, Pin, Po, cin_real,
+                                                                  variant)
 
 
 def conv_wgrad_reduce(slab, dbslab, grad_w, grad_b=None, scale: float = 1.0, beta: float = 0.0):
@@ -402,9 +402,6 @@ def wgrad_nsplit(M: int, cout_p: int, cin_p: int, K: int, cin_real: int = 0, tar
 # 30.5k -> 32.1k, B = 32 35.7k -> 39.9k, B = 48 45.0k -> 46.7k, B = 64 54.2k -> 58.3k; B <= 16 equal or
 # mixed (22.0-22.8k either way), so it starts above 16 boards.
 WGRAD_SMALL = 14
-# C++ kWgradDual: the 192 x 192 per-tap tile with two pixel splits per 1024-thread workgroup summed in LDS;
-# it writes ceil(nsplit / 2) slab partials
-WGRAD_DUAL = 16
 WGRAD_SMALL_M = (16 * 361, 64 * 361)  # (exclusive, inclusive) output-pixel range
 
 

@@ -185,9 +185,6 @@ WGRAD_DIRECT_MAX_PIXELS = 4 * 361
 # off: slower at every batch measured (B = 16 / 32 / 64 / 128 / 2176: -4 / -10 / -4 / -7 / -0.6 %; the merged
 # launch reads twelve cold slabs, profiles/r6/README.md); merged_reduce=True opts in
 MERGED_REDUCE_MAX_PIXELS = 0
-# the dual-split wgrad (HipConvTrainer wgrad_dual) by default above the small-batch plan's range
-WGRAD_DUAL_AUTO = False
-WGRAD_SMALL_M_MAX = 64 * 361
 
 
 class HipConvTrainer:
@@ -200,7 +197,7 @@ class HipConvTrainer:
                  fp8_wgrad: Optional[bool] = None, optimizer: str = "sgd", momentum: float = 0.0,
                  nesterov: bool = False, fp8_bf16_layers: Optional[Sequence[int]] = None,
                  wgrad_direct: Optional[bool] = None, wgrad_ksub: int = 4, fp8_scale_guard: int = 0,
-                 merged_reduce: Optional[bool] = None, wgrad_dual: Optional[bool] = None):
+                 merged_reduce: Optional[bool] = None):
         ops.load()
         # fp8 underflow guard: activation scale exponents fall by at most this many binades per step
         # (ops.fp8_act_scales max_drop; 0 = the plain one-step delayed scale, the default: SL at lr 0.05
@@ -309,12 +306,6 @@ class HipConvTrainer:
         if wgrad_direct is None:
             wgrad_direct = M <= WGRAD_DIRECT_MAX_PIXELS
         self.wgrad_ksub = int(wgrad_ksub)
-        # two pixel splits per 1024-thread wgrad workgroup, summed in LDS (ops.WGRAD_DUAL): half the split
-        # slab on the 192-multiple 3x3 layers of the per-tap plan
-        if wgrad_dual is None:
-            wgrad_dual = WGRAD_DUAL_AUTO and M > WGRAD_SMALL_M_MAX
-        self.wgrad_dual = [bool(wgrad_dual) and l > 0 and self.K[l] == 3 and self.Fp % 192 == 0
-                           and self.wgrad_var[l] == 0 and self.nsplit[l] > 1 for l in range(self.L)]
         self.wgrad_direct = [bool(wgrad_direct) and not reduce_stream and self.wgrad_variant in (0, ops.WGRAD_SMALL)
                              and ops.wgrad_direct_supported(self.Fp, self.C0p if l == 0 else self.Fp,
                                                             self.C0 if l == 0 else self.Fp, self.K[l])
@@ -635,11 +626,8 @@ class HipConvTrainer:
                                    self.gosc8[l:l + 1], self.K[l], self.S, pin, 1,
                                    amax=self.gamax8[l] if l < self.L - 1 else None)
             else:
-                dual = self.wgrad_dual[l]
                 ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1,
-                               cin_real=self.C0 if l == 0 else 0, variant=ops.WGRAD_DUAL if dual else self.wgrad_var[l])
-                if dual:  # ceil(ns / 2) partials
-                    slab, dbs = slab[:(ns + 1) // 2], dbs[:(ns + 1) // 2]
+                               cin_real=self.C0 if l == 0 else 0, variant=self.wgrad_var[l])
             self._pending_reduce.append((slab, dbs, l))
             return
         if self.wgrad_direct[l] and not f8:  # split-free: the OIHW gradient straight from the kernel
@@ -654,11 +642,8 @@ class HipConvTrainer:
                                self.gosc8[l:l + 1], self.K[l], self.S, pin, 1,
                                amax=self.gamax8[l] if l < self.L - 1 else None)
         else:
-            dual = self.wgrad_dual[l]
             ops.conv_wgrad(x, self.DZ[l], slab, dbs, self.K[l], self.S, pin, 1, cin_real=self.C0 if l == 0 else 0,
-                           variant=ops.WGRAD_DUAL if dual else self.wgrad_var[l])
-            if dual:  # ceil(ns / 2) partials
-                slab, dbs = slab[:(ns + 1) // 2], dbs[:(ns + 1) // 2]
+                           variant=self.wgrad_var[l])
 
         def reduce():
             ops.conv_wgrad_reduce(slab, dbs, self.fp.grad_views["w%d" % l], self.fp.grad_views["b%d" % l], 1.0, 0.0)

@@ -83,9 +83,6 @@ def main():
                          "default, automatic at small batches)")
     ap.add_argument("--wgrad-ksub", type=int, default=4, choices=[1, 2, 4, 8],
                     help="split-free wgrad: 32-pixel sub-steps per pipeline stage")
-    ap.add_argument("--wgrad-dual", type=int, default=None, choices=[0, 1],
-                    help="1: two pixel splits per 1024-thread wgrad workgroup summed in LDS (half the split-K slab) "
-                         "on the 192-wide 3x3 layers; 0: off (default: engine default)")
     ap.add_argument("--merged-reduce", type=int, default=None, choices=[0, 1],
                     help="1: one split-K reduce launch for all layers after the backward (one process); 0: one "
                          "per layer (default: engine default)")
@@ -119,8 +116,7 @@ def main():
                                              "wgrad_direct": None if args.wgrad_direct is None
                                              else bool(args.wgrad_direct), "wgrad_ksub": args.wgrad_ksub,
                                              "merged_reduce": None if args.merged_reduce is None
-                                             else bool(args.merged_reduce),
-                                             "wgrad_dual": None if args.wgrad_dual is None else bool(args.wgrad_dual)}
+                                             else bool(args.merged_reduce)}
     trainer = make_policy_trainer(net, args.batch, args.lr, 0.0, backend=args.backend, device=dev, **kw)
     if args.graph:
         trainer.enable_graphs()
@@ -240,7 +236,6 @@ def main():
                 "graph": bool(args.graph),
                 "wgrad_direct": None if args.backend != "hip" else any(getattr(trainer, "wgrad_direct", [])),
                 "merged_reduce": None if args.backend != "hip" else bool(getattr(trainer, "merged_reduce", False)),
-                "wgrad_dual": None if args.backend != "hip" else any(getattr(trainer, "wgrad_dual", [])),
                 "baseline": "paper SL throughput ~3.0k pos/s (50 GPUs), BASELINE.md (A)",
             },
         }

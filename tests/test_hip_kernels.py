@@ -131,33 +131,6 @@ def test_conv_wgrad(ops, cuda_device, B, Cin, Cout, K, Pin, nsplit, variant):
     assert _rel_err(gb, ref_b) < 2e-3
 
 
-@pytest.mark.parametrize("B,S,nsplit", [(5, 19, 2), (8, 19, 3), (64, 19, 7), (96, 19, 56), (40, 13, 9)])
-def test_conv_wgrad_dual(ops, cuda_device, B, S, nsplit):
-    """Dual-split wgrad (kWgradDual): two pixel splits per 1024-thread workgroup summed in LDS, half the
-    slab; the reduce of its ceil(nsplit / 2) partials matches conv2d_weight (odd split counts leave
-    the last pair's second half idle) and repeats bitwise."""
-    torch.manual_seed(13)
-    Cin = Cout = 192
-    x = _bf(torch.randn(B, Cin, S, S, device=cuda_device))
-    dz = _bf(torch.randn(B, Cout, S, S, device=cuda_device))
-    ref_w = torch.nn.grad.conv2d_weight(x, (Cout, Cin, 3, 3), dz, padding=1)
-    ref_b = dz.sum(dim=(0, 2, 3))
-    xp, dzp = ops.to_padded(x, 1), ops.to_padded(dz, 1)
-    outs = []
-    for _ in range(2):
-        slab = torch.full((nsplit, 9, Cout, Cin), float("nan"), device=cuda_device)
-        dbs = torch.full((nsplit, Cout), float("nan"), device=cuda_device)
-        ops.conv_wgrad(xp, dzp, slab, dbs, 3, S, 1, 1, variant=ops.WGRAD_DUAL)
-        np_ = (nsplit + 1) // 2
-        gw = torch.zeros(Cout, Cin, 3, 3, device=cuda_device)
-        gb = torch.zeros(Cout, device=cuda_device)
-        ops.conv_wgrad_reduce(slab[:np_], dbs[:np_], gw, gb, 1.0, 0.0)
-        torch.cuda.synchronize()
-        assert _rel_err(gw, ref_w) < 2e-3 and _rel_err(gb, ref_b) < 2e-3
-        outs.append((gw, gb))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-
-
 @pytest.mark.parametrize("S,B,Cin,Cin_real,Cout,K,Pin,ksub", [
     (19, 16, 192, 192, 192, 3, 1, 8), (19, 1, 192, 192, 192, 3, 1, 4), (19, 5, 192, 192, 192, 3, 1, 1),
     (19, 16, 64, 48, 192, 5, 2, 2), (13, 3, 64, 48, 128, 5, 2, 4), (9, 7, 128, 128, 128, 3, 1, 8),
