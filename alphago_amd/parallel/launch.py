@@ -19,6 +19,7 @@ one rank and labelled the result ``n_gpus: 1``.  ``ensure_ranks`` closes that ho
 from __future__ import annotations
 
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -85,8 +86,19 @@ def ensure_ranks(gpus: int, target: Sequence[str], argv: Sequence[str], require_
     env["PYTHONPATH"] = os.pathsep.join([root] + [x for x in [env.get("PYTHONPATH")] if x])
     sys.stdout.flush()
     sys.stderr.flush()
-    p = subprocess.run(cmd, env=env)
-    return int(p.returncode) if p.returncode >= 0 else 128 - int(p.returncode)
+    p = subprocess.Popen(cmd, env=env)
+
+    def forward(signum, frame):  # a supervisor stopped by its caller stops the launcher (which stops the ranks)
+        if p.poll() is None:
+            p.send_signal(signum)
+
+    old = {sig: signal.signal(sig, forward) for sig in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        rc = p.wait()
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
+    return int(rc) if rc >= 0 else 128 - int(rc)
 
 
 class ExitCode(int):

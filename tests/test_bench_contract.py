@@ -98,3 +98,37 @@ def test_bench_refuses_missing_gpus():
     assert p.returncode == 2, (p.returncode, p.stderr[-2000:])
     assert "GPU(s) are visible" in p.stderr
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_supervisor_forwards_sigterm(tmp_path):
+    """A plain `bench.py --gpus 2` stopped with SIGTERM stops its ranks too (no orphaned rank processes)."""
+    import signal
+    import time
+
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "torch", "--steps", "100000",
+           "--warmup", "1", "--batch", "2", "--filters", "8", "--layers", "3", "--pool", "16", "--min-warmup-s", "0.5"]
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", PYTHONPATH=ROOT)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         start_new_session=True)
+    time.sleep(25)  # ranks started and training
+    pgid = os.getpgid(p.pid)
+    p.send_signal(signal.SIGTERM)
+    try:
+        p.wait(timeout=60)
+    finally:
+        if p.poll() is None:
+            os.killpg(pgid, signal.SIGKILL)
+    assert p.returncode != 0
+    time.sleep(2)
+    # every process of the session (launcher + ranks) is gone
+    alive = []
+    for d in os.listdir("/proc"):
+        if d.isdigit():
+            try:
+                if os.getpgid(int(d)) == pgid:
+                    alive.append(int(d))
+            except OSError:
+                pass
+    assert not alive, alive
