@@ -2,8 +2,9 @@
 // S*S + clipped categorical cross-entropy + top-1 accuracy + the whole backward
 // of the head (dlogits, the ReLU-masked gradient into the last trunk layer, and
 // per-board partials of the head weight/bias gradients).  One workgroup per
-// board: the board's 361 x F activations are read from L2 twice and nothing of
-// the head ever round-trips through HBM as a separate tensor.
+// board: the board's 361 x F activations are read from HBM once into registers
+// (BoardRows / BoardRegs), and nothing of the head round-trips through HBM as a
+// separate tensor.
 //
 // Reference ops replaced: policy.py:145-154 (Conv 1x1 / Flatten / Softmax),
 // Keras categorical_crossentropy with output clipping (supervised_policy_trainer
@@ -147,14 +148,194 @@ __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int
   }
 }
 
+// One board's interior activations held in registers between the policy head's forward and
+// backward passes, so the board is read from HBM once (head_dots + head_input_backward read it
+// twice).  Half-wave `slot` owns positions slot, slot + R, ... (R = NT / 32); lane l32 < C / 8 owns
+// the 16-byte channel group l32 of each.  P = ceil(361 / R) covers every board up to 19 x 19.
+template <int NT>
+struct BoardRegs {
+  static constexpr int R = NT / 32;
+  static constexpr int P = (361 + R - 1) / R;
+  bf16x8 v[P];
+
+  __device__ __forceinline__ static size_t offset(int p, int S, int C, int c8) {
+    const int i = p / S, j = p - i * S;
+    return (size_t)((i + 1) * (S + 2) + j + 1) * C + c8;
+  }
+
+  // every load issued before any is used: P outstanding 16-B loads per lane
+  __device__ __forceinline__ void load(const __bf16* base, int S, int C) {
+    const int l32 = threadIdx.x & 31, slot = threadIdx.x >> 5;
+    const int SS = S * S;
+    const bool lane = l32 < (C >> 3);
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      const int p = u * R + slot;
+      v[u] = (p < SS && lane) ? *(const bf16x8*)(base + offset(p, S, C, l32 << 3)) : bf16x8{};
+    }
+  }
+
+  // z_s[p] = y[p, :] . w with head_dots' xor-shuffle order (same bits)
+  __device__ __forceinline__ void dots(const float* w_s, float* z_s, int S, int C) const {
+    const int l32 = threadIdx.x & 31, slot = threadIdx.x >> 5;
+    const int SS = S * S;
+    const int c8 = l32 << 3;
+    const bool lane = l32 < (C >> 3);
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      const int p = u * R + slot;
+      float d = 0.f;
+      if (lane) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)v[u][e] * w_s[c8 + e];
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+      if (l32 == 0 && p < SS) z_s[p] = d;
+    }
+    __syncthreads();
+  }
+
+  // ReLU'-masked dY = g[p] w into the trunk's last activation gradient and per-board partials of
+  // dW_head (sum_p g[p] y[p, c], slot partials summed through LDS in slot order)
+  __device__ __forceinline__ void backward(const PolicyHeadArgs& a, int b, const float* w_s,
+                                           const float* g_s) const {
+    __shared__ float part[NT * 8];
+    const int tid = threadIdx.x;
+    // laundered so the store addresses are recomputed here instead of kept live from load()
+    // (23 x 64-bit addresses would push the 512-thread kernel past 128 VGPRs)
+    int lane_id = tid;
+    asm volatile("" : "+v"(lane_id));
+    const int l32 = lane_id & 31, slot = lane_id >> 5;
+    const int SS = a.S * a.S;
+    const int c8 = l32 << 3;
+    const bool lane = l32 < (a.C >> 3);
+    __bf16* dzb = a.dz + (size_t)b * (a.S + 2) * (a.S + 2) * a.C;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float wl[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wl[e] = lane ? w_s[c8 + e] : 0.f;
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      const int p = u * R + slot;
+      if (p < SS && lane) {
+        const float g = g_s[p];
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float y = (float)v[u][e];
+          o[e] = (__bf16)(y > 0.f ? g * wl[e] : 0.f);
+          acc[e] += g * y;
+        }
+        *(bf16x8*)(dzb + offset(p, a.S, a.C, c8)) = o;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[tid * 8 + e] = acc[e];
+    __syncthreads();
+    float* dh = a.dhead + (size_t)b * (a.C_real + 1);
+    for (int c = tid; c < a.C_real; c += NT) {
+      const int g8 = c >> 3, e = c & 7;
+      float s = 0.f;
+      for (int r = 0; r < R; ++r) s += part[(r * 32 + g8) * 8 + e];
+      dh[c] = s;
+    }
+  }
+};
+
+// The same for large batches with fewer registers: thread t < S * C / 8 owns 16-byte chunk t of
+// every board row (a row's interior is contiguous in the padded layout), so the 19 loads of a lane
+// differ by one uniform row stride and no per-load address stays live.  A position's dot product
+// is the fixed-order sum of its C / 8 lanes' partials through LDS.  Needs S * C / 8 <= NT.
+template <int NT>
+struct BoardRows {
+  static constexpr int P = 19;
+  bf16x8 v[P];
+
+  __device__ __forceinline__ static size_t offset(int u, int S, int C, int t) {
+    return (size_t)((u + 1) * (S + 2) + 1) * C + t * 8;
+  }
+
+  __device__ __forceinline__ void load(const __bf16* base, int S, int C) {
+    const int t = threadIdx.x;
+    const bool lane = t < S * (C >> 3);
+#pragma unroll
+    for (int u = 0; u < P; ++u) v[u] = (u < S && lane) ? *(const bf16x8*)(base + offset(u, S, C, t)) : bf16x8{};
+  }
+
+  __device__ __forceinline__ void dots(const float* w_s, float* z_s, int S, int C) const {
+    __shared__ float dpart[P * NT];
+    const int t = threadIdx.x;
+    const int C8 = C >> 3;
+    const int cg = t % C8;
+    const bool lane = t < S * C8;
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      float d = 0.f;
+      if (lane) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)v[u][e] * w_s[cg * 8 + e];
+      }
+      dpart[u * NT + t] = d;
+    }
+    __syncthreads();
+    for (int p = t; p < S * S; p += NT) {
+      const int u = p / S, j = p - u * S;
+      const float* q = dpart + u * NT + j * C8;
+      float d = 0.f;
+      for (int k = 0; k < C8; ++k) d += q[k];
+      z_s[p] = d;
+    }
+    __syncthreads();
+  }
+
+  __device__ __forceinline__ void backward(const PolicyHeadArgs& a, int b, const float* w_s,
+                                           const float* g_s) const {
+    __shared__ float part[NT * 8];
+    const int t = threadIdx.x;
+    const int S = a.S, C8 = a.C >> 3;
+    const int j = t / C8, cg = t - j * C8;
+    const bool lane = t < S * C8;
+    __bf16* dzb = a.dz + (size_t)b * (S + 2) * (S + 2) * a.C;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float wl[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) wl[e] = lane ? w_s[cg * 8 + e] : 0.f;
+#pragma unroll
+    for (int u = 0; u < P; ++u) {
+      if (u < S && lane) {
+        const float g = g_s[u * S + j];
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float y = (float)v[u][e];
+          o[e] = (__bf16)(y > 0.f ? g * wl[e] : 0.f);
+          acc[e] += g * y;
+        }
+        *(bf16x8*)(dzb + offset(u, S, a.C, t)) = o;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[t * 8 + e] = acc[e];
+    __syncthreads();
+    float* dh = a.dhead + (size_t)b * (a.C_real + 1);
+    for (int c = t; c < a.C_real; c += NT) {
+      const int g8 = c >> 3, e = c & 7;
+      float s = 0.f;
+      for (int jj = 0; jj < S; ++jj) s += part[(jj * C8 + g8) * 8 + e];
+      dh[c] = s;
+    }
+  }
+};
+
 // Reference RL loss (reinforcement_policy_trainer.py:109, Keras 1.0
 // binary_crossentropy on the softmax output): per board
 //   L = -1/SS * sum_j [y_j log pc_j + (1 - y_j) log(1 - pc_j)],  pc = clip(p, 1e-7, 1 - 1e-7)
 // with y the one-hot move; clip has zero gradient outside its range (Theano
 // clip), and the softmax backward is dz_i = p_i (g_i - sum_j p_j g_j).
-template <int NT>
+template <int NT, class Board>
 __device__ void policy_bce_train(const PolicyHeadArgs& a, int b, int t, float wb, float zmax, float inv, int lidx,
-                                 const __bf16* base, const float* w_s, float* z_s, float* red) {
+                                 const Board& board, const float* w_s, float* z_s, float* red) {
   __shared__ float p_s[368];
   const int tid = threadIdx.x;
   const int SS = a.S * a.S;
@@ -179,16 +360,18 @@ __device__ void policy_bce_train(const PolicyHeadArgs& a, int b, int t, float wb
   const float sc = t >= 0 ? a.grad_scale * wb : 0.f;
   for (int p = tid; p < SS; p += NT) z_s[p] = p_s[p] * (z_s[p] - pg) * sc;
   __syncthreads();
-  head_input_backward<NT>(a, b, base, w_s, z_s);
+  board.backward(a, b, w_s, z_s);
   float gs = 0.f;
   for (int p = tid; p < SS; p += NT) gs += z_s[p];
   gs = block_reduce_sum(gs, red);
   if (tid == 0) a.dhead[(size_t)b * (a.C_real + 1) + a.C_real] = gs;
 }
 
-// NT threads per board: 256 for large batches (occupancy), 1024 below (a board's latency-bound loops
-// get 4x the parallelism: B = 16 has only 16 workgroups)
-template <bool TRAIN, int NT>
+// One workgroup per board, its activations read once into registers (Board).  Large batches: 512
+// threads with BoardRows (126 VGPRs, two boards per CU).  Below kHeadWideBelow boards, or when a
+// row does not fit 512 lanes: 1024 threads with BoardRegs (B = 16 has only 16 workgroups: a board's
+// loads get all the lanes).
+template <bool TRAIN, int NT, class Board>
 __global__ __launch_bounds__(NT) void policy_head_kernel(PolicyHeadArgs a) {
   __shared__ float w_s[256];
   __shared__ float z_s[368];
@@ -199,14 +382,15 @@ __global__ __launch_bounds__(NT) void policy_head_kernel(PolicyHeadArgs a) {
   const int SS = a.S * a.S;
   const int HP = a.S + 2;
   for (int c = tid; c < a.C; c += NT) w_s[c] = c < a.C_real ? a.w[c] : 0.f;
+  Board board;
+  board.load(a.y + (size_t)b * HP * HP * a.C, a.S, a.C);
   __syncthreads();
-  const __bf16* base = a.y + (size_t)b * HP * HP * a.C;
   const float bias = a.b[0];
   const uint8_t* legal = a.legal ? a.legal + (size_t)b * SS : nullptr;
 
   float lmax = -INFINITY;
   int lidx = 0x7fffffff;
-  head_dots(base, w_s, z_s, a.S, a.C);
+  board.dots(w_s, z_s, a.S, a.C);
   for (int p = tid; p < SS; p += NT) {
     float z = (z_s[p] + bias) * a.inv_temp;
     if (legal && !legal[p]) z = -INFINITY;
@@ -253,7 +437,7 @@ __global__ __launch_bounds__(NT) void policy_head_kernel(PolicyHeadArgs a) {
     const int t = a.target[b];
     const float wb = a.weight ? a.weight[b] : 1.f;
     if (a.loss_kind == 1) {
-      policy_bce_train<NT>(a, b, t, wb, zmax, inv, lidx, base, w_s, z_s, red);
+      policy_bce_train<NT, Board>(a, b, t, wb, zmax, inv, lidx, board, w_s, z_s, red);
       return;
     }
     if (tid == 0) {
@@ -274,7 +458,7 @@ __global__ __launch_bounds__(NT) void policy_head_kernel(PolicyHeadArgs a) {
       z_s[p] = g;
     }
     __syncthreads();
-    head_input_backward<NT>(a, b, base, w_s, z_s);
+    board.backward(a, b, w_s, z_s);
     float gs = 0.f;
     for (int p = tid; p < SS; p += NT) gs += z_s[p];
     gs = block_reduce_sum(gs, red);
@@ -388,15 +572,17 @@ void launch_value_out(const ValueOutArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(value_out_kernel, dim3(a.B), dim3(256), 0, st, a);
 }
 
+template <bool TRAIN>
+static void policy_head_go(const PolicyHeadArgs& a, hipStream_t st) {
+  if (a.B >= kHeadWideBelow && a.S * (a.C >> 3) <= 512)
+    hipLaunchKernelGGL((policy_head_kernel<TRAIN, 512, BoardRows<512>>), dim3(a.B), dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((policy_head_kernel<TRAIN, 1024, BoardRegs<1024>>), dim3(a.B), dim3(1024), 0, st, a);
+}
+
 void launch_policy_head(const PolicyHeadArgs& a, bool train, hipStream_t st) {
-  if (a.B < kHeadWideBelow) {
-    if (train) hipLaunchKernelGGL((policy_head_kernel<true, 1024>), dim3(a.B), dim3(1024), 0, st, a);
-    else hipLaunchKernelGGL((policy_head_kernel<false, 1024>), dim3(a.B), dim3(1024), 0, st, a);
-  } else if (train) {
-    hipLaunchKernelGGL((policy_head_kernel<true, 256>), dim3(a.B), dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL((policy_head_kernel<false, 256>), dim3(a.B), dim3(256), 0, st, a);
-  }
+  if (train) policy_head_go<true>(a, st);
+  else policy_head_go<false>(a, st);
 }
 
 }  // namespace agk

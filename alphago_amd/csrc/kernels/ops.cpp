@@ -180,7 +180,7 @@ void policy_head(const Tensor& y, const Tensor& w, const Tensor& b, const c10::o
   const int64_t B = y.size(0), C = y.size(3);
   TORCH_CHECK(y.size(1) == S + 2, "head input must have pad 1");
   TORCH_CHECK(C % 8 == 0 && C <= 256, "head channels must be a multiple of 8 and <= 256");
-  TORCH_CHECK(S * S <= 368, "board too large");
+  TORCH_CHECK(S * S <= 361, "board too large (the head holds at most 19 x 19)");
   agk::PolicyHeadArgs a{};
   a.y = bfp(y);
   a.w = w.data_ptr<float>();

@@ -249,10 +249,12 @@ def test_conv_wgrad_thin_input(ops, cuda_device, K, Pin, variant, S, B, Cout):
     assert _rel_err(gb, ref_b) < 2e-3
 
 
-@pytest.mark.parametrize("C", [192, 64, 128])
-def test_policy_head_train(ops, cuda_device, C):
+# B = 7: 1024-thread BoardRegs; B = 300: 512-thread BoardRows (S * C / 8 <= 512) or, at C = 256,
+# the 1024-thread fallback; S = 9 covers boards smaller than the register tiles
+@pytest.mark.parametrize("C,B,S", [(192, 7, 19), (64, 7, 19), (128, 7, 19), (192, 300, 19), (256, 300, 19),
+                                   (64, 300, 9), (192, 7, 9)])
+def test_policy_head_train(ops, cuda_device, C, B, S):
     torch.manual_seed(3)
-    B, S = 7, 19
     y = _bf(torch.randn(B, C, S, S, device=cuda_device)).clamp_min(0)
     w = torch.randn(C, device=cuda_device) * 0.05
     b = torch.randn(1, device=cuda_device)

@@ -37,17 +37,18 @@ def test_hip_grads_match_torch(cuda_device, F, L, C, B):
     assert torch.allclose(hip.loss, ref._last[0], rtol=2e-2, atol=2e-2)
 
 
-def test_hip_bce_grads_match_torch(cuda_device):
+@pytest.mark.parametrize("B", [6, 264])  # 1024-thread and 512-thread (row-mapped) head kernels
+def test_hip_bce_grads_match_torch(cuda_device, B):
     """Reference RL loss (binary CE on the softmax, per-board signed weights) on
     the fused HIP head (loss_kind=1) vs autograd."""
     torch.manual_seed(5)
-    B, C = 6, 48
+    C = 48
     net = PolicyNet(C, filters_per_layer=64, layers=3)
     net_ref = copy.deepcopy(net)
     planes = torch.randint(0, 2, (B, C, 19, 19), dtype=torch.uint8, device=cuda_device)
     tgt = torch.randint(0, 361, (B,), dtype=torch.int32, device=cuda_device)
     tgt[-1] = -1  # padding board: no loss, no gradient
-    wt = torch.tensor([1.0, -1.0, 2.0, -0.5, 1.0, 3.0], device=cuda_device)
+    wt = torch.tensor([1.0, -1.0, 2.0, -0.5, 1.0, 3.0], device=cuda_device).repeat((B + 5) // 6)[:B].contiguous()
     hip = HipPolicyTrainer(net, B, lr=0.01, device=cuda_device)
     ref = TorchPolicyTrainer(net_ref, B, lr=0.01, device=cuda_device)
     hip.policy_loss = ref.policy_loss = "bce"
