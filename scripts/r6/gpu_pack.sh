@@ -1,0 +1,13 @@
+#!/bin/bash
+# Per-board LDS pack_input: kernel tests, the driver's bench command and the step timeline; then the
+# small-batch split-depth sweep (scripts/r6/gpu_stages.sh).
+O=gpurun_out/r6/pack
+mkdir -p $O
+export PYTHONUNBUFFERED=1
+source scripts/r6/lib.sh
+step tests 400 python -u -m pytest tests/test_hip_kernels.py tests/test_hip_trainer.py -m gpu -x -q --timeout 120 --timeout-method thread
+step bench1 300 python bench.py --gpus 1 --steps 20 --warmup 5
+step bench2 300 python bench.py --gpus 1 --steps 20 --warmup 5
+prof prof_b2176 300 5 --steps 10 --warmup 5
+grep -h '"value"' $O/bench*.log | cut -c1-200
+bash scripts/r6/gpu_stages.sh

@@ -298,18 +298,22 @@ def test_policy_head_probs_legal(ops, cuda_device):
     assert torch.allclose(probs, ref, atol=1e-5)
 
 
-def test_pack_input_symmetries(ops, cuda_device):
+# (48, 19, 64): per-board LDS kernel, 4-byte loads; (3, 9, 8): its byte loads (243 bytes per board);
+# (200, 19, 208): 72 KB per board, the grid-stride kernel
+@pytest.mark.parametrize("C,S,Cp", [(48, 19, 64), (3, 9, 8), (200, 19, 208)])
+def test_pack_input_symmetries(ops, cuda_device, C, S, Cp):
     torch.manual_seed(5)
-    B, C, S = 8, 48, 19
-    planes = torch.randint(0, 2, (B, C, S, S), dtype=torch.uint8)
+    B = 8
+    planes = torch.randint(0, 256, (B, C, S, S), dtype=torch.uint8)
     sym = torch.arange(8, dtype=torch.int32)
     tgt = torch.randint(0, S * S, (B,), dtype=torch.int32)
     tf = [lambda a: a, lambda a: np.rot90(a, 1), lambda a: np.rot90(a, 2), lambda a: np.rot90(a, 3),
           lambda a: np.fliplr(a), lambda a: np.flipud(a), lambda a: np.transpose(a), lambda a: np.fliplr(np.rot90(a, 1))]
-    out = ops.padded_empty(B, S, 2, 64, cuda_device)
+    out = ops.padded_empty(B, S, 2, Cp, cuda_device)
     tout = torch.empty(B, dtype=torch.int32, device=cuda_device)
     ops.pack_input(planes.to(cuda_device), out, 2, sym=sym.to(cuda_device), target=tgt.to(cuda_device), target_out=tout)
-    got = ops.from_padded(out, 2, C).cpu().numpy()
+    assert not ops.from_padded(out, 2)[:, C:].any()  # channels past the real planes are zero
+    got = ops.from_padded(out, 2, C).float().cpu().numpy()
     for b in range(B):
         exp = np.stack([tf[b](planes[b, c].numpy()) for c in range(C)])
         assert np.array_equal(got[b], exp), "symmetry %d" % b
