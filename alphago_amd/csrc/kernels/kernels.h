@@ -129,7 +129,10 @@ struct ValueOutArgs {
 };
 
 struct PackInputArgs {
-  const uint8_t* planes;  // [B][Creal][S][S]
+  const uint8_t* planes;  // [B][Creal][S][S], or [npool][Creal][S][S] with rows
+  const int64_t* rows;    // [B] pool row of each board or null (board b = planes[b]); rows outside
+                          // [0, npool) pack an all-zero board (no out-of-bounds read)
+  int64_t npool;
   const int* sym;         // [B] in 0..7 or null (identity)
   const int* target;      // [B] or null
   int* target_out;        // [B] or null

@@ -299,14 +299,22 @@ void value_out(const Tensor& h, const Tensor& w2, const Tensor& b2, const c10::o
 }
 
 void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c10::optional<Tensor>& target,
-                const c10::optional<Tensor>& target_out, const Tensor& out, int64_t P) {
-  check_dev("pack_input", planes, sym, target, target_out, out);
+                const c10::optional<Tensor>& target_out, const Tensor& out, int64_t P,
+                const c10::optional<Tensor>& rows) {
+  check_dev("pack_input", planes, sym, target, target_out, out, rows);
   TORCH_CHECK(planes.scalar_type() == at::kByte && planes.is_contiguous() && planes.dim() == 4, "planes: uint8 (B,C,S,S)");
   CHECK_BF16(out); CHECK_CONTIG(out);
-  const int64_t B = planes.size(0), C = planes.size(1), S = planes.size(2);
+  const int64_t C = planes.size(1), S = planes.size(2);
+  const int64_t B = rows.has_value() ? rows->numel() : planes.size(0);
+  if (rows.has_value())
+    TORCH_CHECK(rows->scalar_type() == at::kLong && rows->is_contiguous(), "rows: contiguous int64 (B,)");
   TORCH_CHECK(out.size(0) == B && out.size(1) == S + 2 * P && out.size(3) >= C && out.size(3) % 8 == 0, "bad out");
+  if (sym.has_value()) TORCH_CHECK(sym->scalar_type() == at::kInt && sym->numel() == B, "sym: int32 (B,)");
+  if (target.has_value()) TORCH_CHECK(target->scalar_type() == at::kInt && target->numel() == B, "target: int32 (B,)");
   agk::PackInputArgs a{};
   a.planes = planes.data_ptr<uint8_t>();
+  a.rows = rows.has_value() ? rows->data_ptr<int64_t>() : nullptr;
+  a.npool = planes.size(0);
   a.sym = sym.has_value() ? sym->data_ptr<int>() : nullptr;
   a.target = target.has_value() ? target->data_ptr<int>() : nullptr;
   a.target_out = target_out.has_value() ? target_out->data_ptr<int>() : nullptr;
@@ -838,7 +846,8 @@ TORCH_LIBRARY(alphago_amd, m) {
   m.def(
       "value_out(Tensor h, Tensor w2, Tensor b2, Tensor? target, Tensor? weight, Tensor(a!) v, Tensor(b!)? loss, "
       "Tensor(c!)? correct, Tensor(d!)? dh, Tensor(e!)? dout, float grad_scale) -> ()");
-  m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P) -> ()");
+  m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P, "
+        "Tensor? rows=None) -> ()");
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
   m.def("comm_proxy(Tensor src, Tensor(a!) dst, int channels, float wire_us) -> ()");

@@ -54,12 +54,14 @@ __global__ void pack_input_kernel(PackInputArgs a) {
     const int s = a.sym ? a.sym[b] : 0;
     int x, y;
     sym_inv(s, a.S, i, j, x, y);
-    const uint8_t* src = a.planes + (size_t)b * a.Creal * SS + x * a.S + y;
+    const int64_t row = a.rows ? a.rows[b] : b;
+    const bool valid = row >= 0 && row < a.npool;
+    const uint8_t* src = a.planes + (size_t)(valid ? row : 0) * a.Creal * SS + x * a.S + y;
     bf16x8 o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int c = c8 * 8 + e;
-      o[e] = (__bf16)(c < a.Creal ? (float)src[(size_t)c * SS] : 0.f);
+      o[e] = (__bf16)(c < a.Creal && valid ? (float)src[(size_t)c * SS] : 0.f);
     }
     *(bf16x8*)(a.out + ((size_t)(b * HP + i + a.P) * HP + j + a.P) * a.Cp + c8 * 8) = o;
     if (a.target_out && p == 0 && c8 == 0) {
@@ -75,7 +77,8 @@ __global__ void pack_input_kernel(PackInputArgs a) {
   }
 }
 
-// One workgroup per board: the board's Creal x S x S bytes come in with coalesced 4-byte loads into
+// One workgroup per board (pool row rows[b] when given: the minibatch gather fused into the pack):
+// the board's Creal x S x S bytes come in with coalesced 4-byte loads into
 // LDS, then lane (p, c8) gathers its 8 planes at the symmetry's source point from LDS and writes 16
 // contiguous bytes of the padded NHWC row (consecutive lanes: consecutive 16-byte chunks).
 // pack_input_kernel's per-lane strided byte loads from HBM ran at ~3 TB/s (57 us at B = 2176).
@@ -84,8 +87,12 @@ __global__ __launch_bounds__(256) void pack_input_board_kernel(PackInputArgs a) 
   const int b = blockIdx.x;
   const int SS = a.S * a.S;
   const int n = a.Creal * SS;
-  const uint8_t* src = a.planes + (size_t)b * n;
-  if ((n & 3) == 0) {  // the board's bytes start 4-byte aligned: n is a multiple of 4
+  const int64_t row = a.rows ? a.rows[b] : b;
+  const bool valid = row >= 0 && row < a.npool;
+  const uint8_t* src = a.planes + (size_t)(valid ? row : 0) * n;
+  if (!valid) {
+    for (int i = threadIdx.x; i < n; i += 256) pl_s[i] = 0;
+  } else if ((n & 3) == 0) {  // the board's bytes start 4-byte aligned: n is a multiple of 4
     const uint32_t* s4 = (const uint32_t*)src;
     for (int i = threadIdx.x; i < (n >> 2); i += 256) ((uint32_t*)pl_s)[i] = s4[i];
   } else {

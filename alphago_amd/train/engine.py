@@ -199,6 +199,7 @@ class HipConvTrainer:
                  wgrad_direct: Optional[bool] = None, wgrad_ksub: int = 4, fp8_scale_guard: int = 0,
                  merged_reduce: Optional[bool] = None):
         ops.load()
+        self._rows = None  # pool rows of the current training forward (compute_grads(rows=...))
         # fp8 underflow guard: activation scale exponents fall by at most this many binades per step
         # (ops.fp8_act_scales max_drop; 0 = the plain one-step delayed scale, the default: SL at lr 0.05
         # over 5 seeds collapsed 3 times with a 1-binade guard vs once unguarded and once in bf16,
@@ -526,7 +527,8 @@ class HipConvTrainer:
         return (self.X0, self.P0) if l == 0 else (self.Y[l - 1], 1)
 
     def forward_trunk(self, planes: torch.Tensor, sym=None, move_targets=None, target_out=None) -> None:
-        ops.pack_input(planes, self.X0, self.P0, sym=sym, target=move_targets, target_out=target_out)
+        ops.pack_input(planes, self.X0, self.P0, sym=sym, target=move_targets, target_out=target_out,
+                       rows=self._rows)
         if self.precision == "fp8":
             if not self._fp8_calibrated:
                 self._fp8_calibrate()
@@ -755,18 +757,23 @@ class HipConvTrainer:
         self._g8_calibrated = True
 
     def compute_grads(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None,
-                      weight: Optional[torch.Tensor] = None, reduce: bool = True):
+                      weight: Optional[torch.Tensor] = None, reduce: bool = True,
+                      rows: Optional[torch.Tensor] = None):
         """Forward + backward into self.fp.grad (all-reduced when distributed,
-        unless ``reduce=False``)."""
-        B = planes.shape[0]
+        unless ``reduce=False``).  ``rows`` (int64, B): the minibatch is ``planes[rows]`` of a
+        device-resident pool, gathered by the input-pack kernel itself (no separate index_select);
+        ``targets``, ``sym`` and ``weight`` stay per board."""
+        B = planes.shape[0] if rows is None else rows.numel()
         if B != self.batch:
             raise ValueError("batch %d != configured %d" % (B, self.batch))
         with trace_range("forward"):
             self._train_fwd = True
+            self._rows = rows
             try:
                 self._forward_for_head(planes, targets, sym)
             finally:
                 self._train_fwd = False
+                self._rows = None
         with trace_range("head"):
             self._head_train(targets, 1.0 / (B * self.env.world_size), weight)
         with trace_range("backward+allreduce"):
@@ -820,12 +827,15 @@ class HipConvTrainer:
             self.repack()
 
     def step(self, planes: torch.Tensor, targets: torch.Tensor, sym: Optional[torch.Tensor] = None,
-             weight: Optional[torch.Tensor] = None):
+             weight: Optional[torch.Tensor] = None, rows: Optional[torch.Tensor] = None):
         """One SGD step.  Returns (sum of per-board loss, metric sum) as device scalars (local;
-        in graph mode static tensors, valid until the next step)."""
+        in graph mode static tensors, valid until the next step).  ``rows``: see compute_grads
+        (eager steps only)."""
         if self.use_graph and weight is None:
+            if rows is not None:
+                raise ValueError("graph mode: pass the gathered minibatch, not pool rows")
             return self._graph_step(planes, targets, sym)
-        self.compute_grads(planes, targets, sym, weight)
+        self.compute_grads(planes, targets, sym, weight, rows=rows)
         self.apply_update()
         return self._step_metrics()
 
@@ -991,13 +1001,22 @@ class HipValueTrainer(HipConvTrainer):
         ops.value_out(self.h, v["fc2_w"].view(-1), v["fc2_b"], self.val, target=self.tval, weight=weight,
                       loss=self.loss, correct=self.correct, dh=self.dh, dout=self.dout, grad_scale=gscale)
         ops.dense_f32(self.z, self.dh, gv["fc1_w"], trans_a=True)  # dW1 = z^T dh
-        torch.sum(self.dh, dim=0, out=gv["fc1_b"])
+        # column sums of the per-board partials on the fixed-order head_grad_sums kernel (torch's
+        # column reductions were 4 launches, ~50 us of the 4.3 ms fp8 step); every call also writes
+        # the step's (loss, correct) sums into a fresh 2-vector
+        self._metric_sums = torch.empty(2, device=self.device)
+        ops.head_grad_sums(self.dh, self.loss, self.correct, gv["fc1_b"], self._metric_sums)
         o2, n2 = self.fp.segments["fc2_w"]
-        torch.sum(self.dout, dim=0, out=self.fp.grad[o2:o2 + n2 + 1])  # [dw2 | db2]
+        ops.head_grad_sums(self.dout, self.loss, self.correct, self.fp.grad[o2:o2 + n2 + 1],
+                           self._metric_sums)  # [dw2 | db2]
         ops.dense_f32(self.dh, v["fc1_w"], self.dzl, trans_b=True)  # dz = dh W1^T
         ops.head_backward(self.Y[-1], v["head_w"].view(-1), self.dzl, self.DZ[-1], self.dhead, self.S)
         ho, hn = self.fp.segments["head_w"]
-        torch.sum(self.dhead, dim=0, out=self.fp.grad[ho:ho + hn + 1])  # [dW_head | db_head]
+        ops.head_grad_sums(self.dhead, self.loss, self.correct, self.fp.grad[ho:ho + hn + 1],
+                           self._metric_sums)  # [dW_head | db_head]
+
+    def _step_metrics(self):
+        return self._metric_sums[0], self._metric_sums[1]
 
     @torch.no_grad()
     def evaluate(self, planes: torch.Tensor, targets: torch.Tensor):
@@ -1031,7 +1050,9 @@ class _TorchTrainerBase:
         self.opt_state = [torch.zeros_like(self.fp.flat) for _ in range(self.sched.n_moments)]
         self.table = symmetry_tables(net.board, self.device)
 
-    def compute_grads(self, planes, targets, sym=None, weight=None, reduce: bool = True):
+    def compute_grads(self, planes, targets, sym=None, weight=None, reduce: bool = True, rows=None):
+        if rows is not None:  # the HIP trainers gather inside the pack kernel
+            planes = planes.index_select(0, rows)
         for p in self.params:
             p.grad = None
         obj, per, metric = self._loss(planes, targets, sym, weight)
@@ -1053,8 +1074,8 @@ class _TorchTrainerBase:
                 optimizer_update_(self.fp.flat, self.fp.grad, self.opt_state, self.sched, self.sched.current())
         self.sched.advance()
 
-    def step(self, planes, targets, sym=None, weight=None):
-        self.compute_grads(planes, targets, sym, weight)
+    def step(self, planes, targets, sym=None, weight=None, rows=None):
+        self.compute_grads(planes, targets, sym, weight, rows=rows)
         self.apply_update()
         per, metric = self._last
         return per.sum(), metric.sum()

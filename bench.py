@@ -137,9 +137,14 @@ def main():
     pool_s = time.perf_counter() - t_pool
 
     def batch():
+        """(step args, step kwargs) of one random minibatch of the resident pool.  Eager steps pass the
+        pool and the drawn rows: the input-pack kernel gathers the boards itself (no index_select
+        pass over the planes).  Graph replays take the gathered minibatch (static input buffers)."""
         idx = torch.randint(0, args.pool, (args.batch,), device=dev, generator=g)
         sym = torch.randint(0, 8, (args.batch,), device=dev, dtype=torch.int32, generator=g)
-        return pool.index_select(0, idx), pool_tgt.index_select(0, idx), sym
+        if args.graph:
+            return (pool.index_select(0, idx), pool_tgt.index_select(0, idx), sym), {}
+        return (pool, pool_tgt.index_select(0, idx), sym), {"rows": idx}
 
     loss_sum = torch.zeros((), device=dev)
     corr_sum = torch.zeros((), device=dev)
@@ -151,7 +156,8 @@ def main():
         # cache), which landed inside the timed region of the round-1 driver run: 20 x 18.4 ms of
         # GPU work measured as 21.1 ms/step (profiles/r2_fresh_box_diagnosis.md).
         for _ in range(n):
-            l, c = trainer.step(*batch())
+            bargs, bkw = batch()
+            l, c = trainer.step(*bargs, **bkw)
             loss_sum.add_(l)
             corr_sum.add_(c)
 
@@ -244,7 +250,8 @@ def main():
         from alphago_amd.utils.profiling import Profiler
         with Profiler(os.path.join(args.profile, "rank%d" % env.rank), wait=1, warmup=2, active=3) as prof:
             for _ in range(6):
-                trainer.step(*batch())
+                bargs, bkw = batch()
+                trainer.step(*bargs, **bkw)
                 prof.step()
         if dev.type == "cuda":
             torch.cuda.synchronize()

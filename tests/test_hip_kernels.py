@@ -322,6 +322,30 @@ def test_pack_input_symmetries(ops, cuda_device, C, S, Cp):
         assert int(np.argmax(tf[b](onehot))) == int(tout[b])
 
 
+@pytest.mark.parametrize("C,Cp", [(48, 64), (49, 64), (200, 208)])
+def test_pack_input_rows_gather(ops, cuda_device, C, Cp):
+    """rows: the pack kernel gathers pool[rows] itself -- equal to index_select then pack, and a row
+    outside the pool packs an all-zero board instead of reading out of bounds."""
+    torch.manual_seed(6)
+    S, npool, B = 19, 50, 9
+    pool = torch.randint(0, 256, (npool, C, S, S), dtype=torch.uint8, device=cuda_device)
+    rows = torch.randint(0, npool, (B,), device=cuda_device)
+    sym = torch.randint(0, 8, (B,), dtype=torch.int32, device=cuda_device)
+    tgt = torch.randint(0, S * S, (B,), dtype=torch.int32, device=cuda_device)
+    ref, got = (ops.padded_empty(B, S, 2, Cp, cuda_device) for _ in range(2))
+    tref, tgot = (torch.empty(B, dtype=torch.int32, device=cuda_device) for _ in range(2))
+    ops.pack_input(pool.index_select(0, rows), ref, 2, sym=sym, target=tgt, target_out=tref)
+    ops.pack_input(pool, got, 2, sym=sym, target=tgt, target_out=tgot, rows=rows)
+    assert torch.equal(got, ref) and torch.equal(tgot, tref)
+    bad = rows.clone()
+    bad[3], bad[5] = npool, -1
+    ops.pack_input(pool, got, 2, sym=sym, rows=bad)
+    torch.cuda.synchronize()
+    assert not got[3].any() and not got[5].any()
+    keep = [b for b in range(B) if b not in (3, 5)]
+    assert torch.equal(got[keep], ref[keep])
+
+
 def test_sgd_update(ops, cuda_device):
     p = torch.randn(1003, device=cuda_device)
     g = torch.randn(1003, device=cuda_device)

@@ -67,6 +67,42 @@ def test_hip_bce_grads_match_torch(cuda_device, B):
     assert hip.loss[-1].item() == 0.0
 
 
+def test_step_rows_equals_gathered_batch(cuda_device):
+    """step(pool, targets, sym, rows=idx) gathers inside the pack kernel: bitwise the same losses and
+    weights as step(pool[idx], ...), for the policy and the value trainer (which also takes its
+    head-gradient column sums and step metrics from head_grad_sums)."""
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import HipValueTrainer
+
+    torch.manual_seed(4)
+    B, C, npool = 8, 48, 40
+    pool = torch.randint(0, 2, (npool, C, 19, 19), dtype=torch.uint8, device=cuda_device)
+    ptgt = torch.randint(0, 361, (npool,), dtype=torch.int32, device=cuda_device)
+    net = PolicyNet(C, filters_per_layer=64, layers=3)
+    a = HipPolicyTrainer(copy.deepcopy(net), B, lr=0.01, device=cuda_device)
+    b = HipPolicyTrainer(copy.deepcopy(net), B, lr=0.01, device=cuda_device)
+    vnet = ValueNet(C + 1, filters_per_layer=64, layers=3)
+    vpool = torch.randint(0, 2, (npool, C + 1, 19, 19), dtype=torch.uint8, device=cuda_device)
+    pz = (torch.randint(0, 2, (npool,), device=cuda_device) * 2 - 1).float()
+    va = HipValueTrainer(copy.deepcopy(vnet), B, lr=0.01, device=cuda_device)
+    vb = HipValueTrainer(copy.deepcopy(vnet), B, lr=0.01, device=cuda_device)
+    for _ in range(3):
+        idx = torch.randint(0, npool, (B,), device=cuda_device)
+        sym = torch.randint(0, 8, (B,), dtype=torch.int32, device=cuda_device)
+        la = a.step(pool, ptgt.index_select(0, idx), sym, rows=idx)
+        lb = b.step(pool.index_select(0, idx), ptgt.index_select(0, idx), sym)
+        assert all(torch.equal(x, y) for x, y in zip(la, lb))
+        lva = va.step(vpool, pz.index_select(0, idx), sym, rows=idx)
+        lvb = vb.step(vpool.index_select(0, idx), pz.index_select(0, idx), sym)
+        assert all(torch.equal(x, y) for x, y in zip(lva, lvb))
+        # the value metrics are the per-board sums (head_grad_sums' fixed order)
+        torch.testing.assert_close(lva[0], va.loss.sum(), rtol=1e-6, atol=1e-6)
+        torch.testing.assert_close(lva[1], va.correct.sum())
+    assert torch.equal(a.fp.flat, b.fp.flat) and torch.equal(va.fp.flat, vb.fp.flat)
+    with pytest.raises(ValueError):
+        a.step(pool, ptgt[:B], None, rows=torch.zeros(B + 1, dtype=torch.long, device=cuda_device))
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_hip_step_reduces_loss(cuda_device, seed):
     # lr 0.05: at 0.5 this 20-step fit of one batch is chaotic, and a last-bit change in the

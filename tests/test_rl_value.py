@@ -448,3 +448,25 @@ def test_value_pipeline_gpus_flag_without_torchrun(tmp_path):
     # a --backend hip request for more GPUs than are visible is refused, not run on fewer
     r = cli(["train-value", vj, data, out + "2", "--backend", "hip", "--gpus", "2"])
     assert r.returncode == 2 and "GPU(s) are visible" in r.stderr
+
+
+def test_torch_trainer_rows_equals_gathered_batch():
+    """The torch trainers take the same ``rows`` argument as the HIP ones (bench.py passes the pool
+    and the drawn rows): identical to stepping on the gathered minibatch."""
+    import copy
+
+    from alphago_amd.models.nets import PolicyNet
+    from alphago_amd.train.engine import TorchPolicyTrainer
+
+    torch.manual_seed(2)
+    B, C, npool = 4, 48, 10
+    pool = torch.randint(0, 2, (npool, C, 19, 19), dtype=torch.uint8)
+    ptgt = torch.randint(0, 361, (npool,), dtype=torch.int32)
+    net = PolicyNet(C, filters_per_layer=16, layers=2)
+    a = TorchPolicyTrainer(copy.deepcopy(net), B, lr=0.01, device="cpu")
+    b = TorchPolicyTrainer(copy.deepcopy(net), B, lr=0.01, device="cpu")
+    idx = torch.tensor([3, 3, 9, 0])
+    sym = torch.tensor([0, 5, 2, 7], dtype=torch.int32)
+    la = a.step(pool, ptgt.index_select(0, idx), sym, rows=idx)
+    lb = b.step(pool.index_select(0, idx), ptgt.index_select(0, idx), sym)
+    assert torch.equal(la[0], lb[0]) and torch.equal(a.fp.flat, b.fp.flat)
