@@ -509,6 +509,32 @@ __device__ __forceinline__ void wgrad_reduce_body(const WgradReduceArgs& a, int 
   const size_t sstride = (size_t)a.T * tile;
   const int k = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int n4 = a.nsplit & ~3;
+  if (bid == 0 && a.grad_b) {
+    // bias: one sequential sum per channel (fixed order).  The FIRST block issues it before its share
+    // of the slab, so its dependent load-add rounds run under the other blocks; as the last block's
+    // epilogue (up to round 6) they were the launch's tail.  16 loads in flight per round.
+    for (int n = threadIdx.x; n < a.Cout_real; n += blockDim.x) {
+      const float* d = a.dbias_slab + n;
+      float sum = 0.f;
+      int sp = 0;
+      for (; sp + 16 <= a.nsplit; sp += 16) {
+        float v[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = d[(size_t)(sp + i) * a.Cout];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sum += v[i];
+      }
+      for (; sp + 8 <= a.nsplit; sp += 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = d[(size_t)(sp + i) * a.Cout];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum += v[i];
+      }
+      for (; sp < a.nsplit; ++sp) sum += d[(size_t)sp * a.Cout];
+      a.grad_b[n] = (a.beta != 0.f ? a.beta * a.grad_b[n] : 0.f) + a.scale * sum;  // beta 0: no read
+    }
+  }
   for (int base = bid * 64; base < total; base += nblk * 64) {  // block-uniform trip count
     const int idx = base + lane;
     const int e = idx < total ? idx : total - 1;
@@ -547,24 +573,6 @@ __device__ __forceinline__ void wgrad_reduce_body(const WgradReduceArgs& a, int 
       }
     }
     __syncthreads();
-  }
-  if (bid == nblk - 1 && a.grad_b) {
-    // bias: one sequential sum per channel (fixed order) with 8 loads in flight --
-    // a load-add chain of nsplit dependent steps set this kernel's duration
-    for (int n = threadIdx.x; n < a.Cout_real; n += blockDim.x) {
-      const float* d = a.dbias_slab + n;
-      float sum = 0.f;
-      int sp = 0;
-      for (; sp + 8 <= a.nsplit; sp += 8) {
-        float v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = d[(size_t)(sp + k) * a.Cout];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sum += v[k];
-      }
-      for (; sp < a.nsplit; ++sp) sum += d[(size_t)sp * a.Cout];
-      a.grad_b[n] = a.beta * a.grad_b[n] + a.scale * sum;
-    }
   }
 }
 
