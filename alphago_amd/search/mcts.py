@@ -24,6 +24,7 @@ value/policy/rollout *callables*, ``get_move(state)`` and
 from __future__ import annotations
 
 import os
+import time
 from typing import Callable, List, Optional, Sequence
 
 import numpy as np
@@ -282,10 +283,12 @@ class BatchedMCTS(object):
                 self._roots[i] = hist
 
     def search(self, states: Sequence, n_playout: int, leaves_per_tree: int = 16,
-               temperature=0.0, noise: Optional[float] = None, active: Optional[Sequence[int]] = None) -> List:
+               temperature=0.0, noise: Optional[float] = None, active: Optional[Sequence[int]] = None,
+               deadline: Optional[float] = None) -> List:
         """Run ``n_playout`` simulations on every tree (or only the trees in ``active``; the others
         keep their roots and statistics); return the chosen move per tree (None for inactive trees).
-        ``temperature``: one value, or one per tree."""
+        ``temperature``: one value, or one per tree.  ``deadline`` (a ``time.perf_counter()`` value,
+        GTP time control): no new leaf batch is gathered after it; the batches in flight finish."""
         if len(states) != self._n:
             self.resize(len(states))
         act = list(range(self._n)) if active is None else sorted(set(int(i) for i in active))
@@ -307,10 +310,15 @@ class BatchedMCTS(object):
         targets = [[fg.sims(offs[k] + j) + (n_playout if offs[k] + j in on else 0) for j in range(f.n_trees)]
                    for k, f in enumerate(self._forests)]
 
+        def late():
+            return deadline is not None and time.perf_counter() >= deadline
+
         def gather(k):
             """Gather the next leaves of group k; False when its trees are done."""
             f = self._forests[k]
             while True:
+                if late():
+                    return False
                 todo = [j for j in range(f.n_trees) if f.sims(j) < targets[k][j]]
                 if not todo:
                     return False
@@ -323,6 +331,8 @@ class BatchedMCTS(object):
             queued leaf (a held batch's) or a terminal.  The held batch's leaves count toward the
             playout budget, so the pipelined search does the serial search's number of playouts."""
             f = self._forests[k]
+            if late():
+                return False
             held = f.held_counts()  # one native pass over the held batch
             todo = [j for j in range(f.n_trees) if f.sims(j) + held[j] < targets[k][j]]
             return bool(todo) and f.gather(leaves_per_tree, todo) > 0

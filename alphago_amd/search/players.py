@@ -79,16 +79,19 @@ class MCTSPlayer(object):
     def get_move(self, state, time_budget: Optional[float] = None):
         """``time_budget`` (seconds, GTP time control): search in growing chunks of playouts on the same
         tree (each ``search`` call adds to the root's visits) until the next chunk would overrun the
-        budget or ``n_playout`` is reached; None = the fixed ``n_playout``."""
+        budget or ``n_playout`` is reached; None = the fixed ``n_playout``.  The budget's end is also a
+        deadline inside the search, so a chunk slowed by a loaded host stops at its next leaf batch."""
         if not sensible_moves(state):
             return go.PASS_MOVE
         if time_budget is None:
             return self.search.search([state], self.n_playout, self.leaves_per_batch, self.temperature)[0]
         t0 = time.perf_counter()
+        deadline = t0 + time_budget  # a hard stop inside a chunk too: no leaf batch starts after it
         done, chunk, move = 0, max(1, self.leaves_per_batch), None
         while True:
             t1 = time.perf_counter()
-            move = self.search.search([state], chunk, self.leaves_per_batch, self.temperature)[0]
+            move = self.search.search([state], chunk, self.leaves_per_batch, self.temperature,
+                                      deadline=deadline)[0]
             done += chunk
             now = time.perf_counter()
             per = (now - t1) / chunk  # seconds per playout of the last chunk

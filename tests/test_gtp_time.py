@@ -54,3 +54,16 @@ def test_clock_bookkeeping_and_time_left():
     eng.send("time_settings 0 1 1")
     eng._charge(go.BLACK, 0.4)  # one stone of a 1-stone period: a fresh period follows
     assert eng.clock[go.BLACK] == [1.0, 1]
+
+
+def test_search_deadline_stops_inside_a_chunk():
+    """BatchedMCTS.search(deadline=...): a 10^7-playout search stops at its first leaf batch past the
+    deadline (the hard stop behind a loaded host's slow chunk), having searched until then."""
+    pl = _player()
+    st = go.GameState(19)
+    pl.get_move(st, time_budget=0.05)  # warm the engines
+    s0 = pl.search.forest.sims(0)
+    t0 = time.perf_counter()
+    pl.search.search([st], 10 ** 7, 8, 0.0, deadline=t0 + 0.3)
+    assert time.perf_counter() - t0 < 1.5
+    assert pl.search.forest.sims(0) > s0
