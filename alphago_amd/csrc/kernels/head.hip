@@ -103,6 +103,9 @@ __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int
   const int R = blockDim.x / C8;  // positions processed concurrently
   const int r = tid / C8, cg = tid - r * C8;
   __bf16* dzb = a.dz + (size_t)b * HP * HP * a.C;
+  uint8_t* dz8b = a.dz8 ? a.dz8 + (size_t)b * HP * HP * a.C : nullptr;
+  const float sc8 = a.dz8 ? *a.dz8_scale : 0.f;
+  float m8 = 0.f;  // max |bf16 dY| (e5m2 output)
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (r < R) {
     const int c8 = cg << 3;
@@ -131,13 +134,40 @@ __device__ __forceinline__ void head_input_backward(const PolicyHeadArgs& a, int
             o[e] = (__bf16)(y > 0.f ? g * w_s[c8 + e] : 0.f);
             acc[e] += g * y;
           }
-          *(bf16x8*)(dzb + off[u]) = o;
+          if (dz8b) {
+            // quantize_bf8_dev_kernel's conversion of the bf16 value: the same bytes and max, and the
+            // bf16 dz is never written or re-read
+            float f[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              f[e] = (float)o[e];
+              m8 = fmaxf(m8, fabsf(f[e]));
+              f[e] = fminf(fmaxf(f[e] * sc8, -57344.f), 57344.f);
+            }
+            int lo = __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], 0, false);
+            lo = __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], lo, true);
+            int hi = __builtin_amdgcn_cvt_pk_bf8_f32(f[4], f[5], 0, false);
+            hi = __builtin_amdgcn_cvt_pk_bf8_f32(f[6], f[7], hi, true);
+            *(int2*)(dz8b + off[u]) = make_int2(lo, hi);
+          } else {
+            *(bf16x8*)(dzb + off[u]) = o;
+          }
         }
       }
     }
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) part[tid * 8 + e] = acc[e];
+  if (dz8b) {  // one atomic per board into the spread amax slots
+    __shared__ float red8[NT / 64];
+    m8 = wave_max(m8);
+    if ((tid & 63) == 0) red8[tid >> 6] = m8;
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < NT / 64; ++w) m8 = fmaxf(m8, red8[w]);
+      if (m8 > 0.f) atomicMax(a.dz8_amax + (b & (kFp8AmaxSlots - 1)), __float_as_uint(m8));
+    }
+  }
   __syncthreads();
   float* dh = a.dhead + (size_t)b * (a.C_real + 1);
   for (int c = tid; c < a.C_real; c += blockDim.x) {

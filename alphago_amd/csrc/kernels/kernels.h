@@ -107,6 +107,9 @@ struct PolicyHeadArgs {
   float* correct;      // [B]
   float* dhead;        // [B][C_real + 1] per-board partials of dW_head, db_head
   float* probs;        // [B][S*S] or null
+  uint8_t* dz8;        // head_backward only: dY as e5m2 (dz8 = e5m2(bf16(dY) * dz8_scale[0])) instead of
+  const float* dz8_scale;  // the bf16 dz, for an fp8 trunk backward; max |bf16(dY)| into dz8_amax
+  unsigned* dz8_amax;  // [kFp8AmaxSlots] float bits (the quantize_bf8 contract)
   int B, S, C, C_real;
   float grad_scale;    // d(mean loss)/d(logit) scale = 1/global_batch
   float inv_temp;

@@ -253,8 +253,9 @@ void head_grad_sums(const Tensor& dhead, const Tensor& loss, const Tensor& corre
 }
 
 void head_backward(const Tensor& y, const Tensor& w, const Tensor& dlogits, const Tensor& dz, const Tensor& dhead,
-                   int64_t S) {
-  check_dev("head_backward", y, w, dlogits, dz, dhead);
+                   int64_t S, const c10::optional<Tensor>& dz8, const c10::optional<Tensor>& dz8_scale,
+                   const c10::optional<Tensor>& dz8_amax) {
+  check_dev("head_backward", y, w, dlogits, dz, dhead, dz8, dz8_scale, dz8_amax);
   CHECK_BF16(y); CHECK_CONTIG(y); CHECK_F32(w); CHECK_F32(dlogits); CHECK_CONTIG(dlogits);
   CHECK_BF16(dz); CHECK_CONTIG(dz); CHECK_F32(dhead);
   const int64_t B = y.size(0), C = y.size(3);
@@ -263,6 +264,17 @@ void head_backward(const Tensor& y, const Tensor& w, const Tensor& dlogits, cons
   agk::PolicyHeadArgs a{};
   a.y = bfp(y); a.w = w.data_ptr<float>(); a.dz = bfp_mut(dz); a.dhead = dhead.data_ptr<float>();
   a.B = (int)B; a.S = (int)S; a.C = (int)C; a.C_real = (int)w.numel();
+  if (dz8.has_value()) {  // e5m2 dY instead of the bf16 dz (dz is not written)
+    TORCH_CHECK(dz8_scale.has_value() && dz8_amax.has_value(), "head_backward: dz8 needs dz8_scale and dz8_amax");
+    TORCH_CHECK(dz8->scalar_type() == at::kByte && dz8->sizes() == y.sizes() && dz8->is_contiguous(),
+                "head_backward: dz8 uint8 of y's shape");
+    CHECK_F32(*dz8_scale);
+    TORCH_CHECK(dz8_amax->scalar_type() == at::kInt && dz8_amax->numel() >= agk::kFp8AmaxSlots &&
+                    dz8_amax->is_contiguous(), "head_backward: dz8_amax int32[64]");
+    a.dz8 = dz8->data_ptr<uint8_t>();
+    a.dz8_scale = dz8_scale->data_ptr<float>();
+    a.dz8_amax = (unsigned*)dz8_amax->data_ptr<int>();
+  }
   if (B == 0) return;
   agk::launch_head_backward(a, dlogits.data_ptr<float>(), cur_stream());
   launch_check("head_backward");
@@ -841,7 +853,8 @@ TORCH_LIBRARY(alphago_amd, m) {
       "Tensor(c!)? correct, Tensor(d!)? dhead, Tensor(e!)? probs, int S, float grad_scale, float temperature, "
       "int loss_kind=0) -> ()");
   m.def("head_logits(Tensor y, Tensor w, Tensor b, Tensor(a!) z, int S) -> ()");
-  m.def("head_backward(Tensor y, Tensor w, Tensor dlogits, Tensor(a!) dz, Tensor(b!) dhead, int S) -> ()");
+  m.def("head_backward(Tensor y, Tensor w, Tensor dlogits, Tensor(a!) dz, Tensor(b!) dhead, int S, "
+        "Tensor(c!)? dz8=None, Tensor? dz8_scale=None, Tensor(d!)? dz8_amax=None) -> ()");
   m.def("head_grad_sums(Tensor dhead, Tensor loss, Tensor correct, Tensor(a!) grad, Tensor(b!) sums) -> ()");
   m.def(
       "value_out(Tensor h, Tensor w2, Tensor b2, Tensor? target, Tensor? weight, Tensor(a!) v, Tensor(b!)? loss, "

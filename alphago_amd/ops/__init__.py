@@ -442,9 +442,11 @@ def head_logits(y, w, b, z, S: int):
     return z
 
 
-def head_backward(y, w, dlogits, dz, dhead, S: int):
-    """ReLU'-masked dY of a 1x1 head conv from dlogits, plus per-board [dW | db] partials."""
-    _ops().head_backward(y, w, dlogits, dz, dhead, S)
+def head_backward(y, w, dlogits, dz, dhead, S: int, dz8=None, dz8_scale=None, dz8_amax=None):
+    """ReLU'-masked dY of a 1x1 head conv from dlogits, plus per-board [dW | db] partials.  With
+    ``dz8`` (uint8, y's shape) dY goes out as e5m2 of bf16(dY) * dz8_scale[0] with max |bf16(dY)| into
+    ``dz8_amax`` (int32[64]) -- the bytes quantize_bf8 would make -- and ``dz`` is not written."""
+    _ops().head_backward(y, w, dlogits, dz, dhead, S, dz8, dz8_scale, dz8_amax)
 
 
 def value_out(h, w2, b2, v, target=None, weight=None, loss=None, correct=None, dh=None, dout=None,

@@ -166,6 +166,55 @@ def test_fp8_overlap_backward_matches_serial(cuda_device, F):
     assert torch.equal(a.gscales8, b.gscales8) and torch.equal(a.gamax8, b.gamax8)
 
 
+def test_head_backward_e5m2_equals_quantize(cuda_device):
+    """head_backward(dz8=...) writes the bytes and max that head_backward (bf16 dz) + quantize_bf8 make."""
+    from alphago_amd import ops
+
+    torch.manual_seed(5)
+    B, C, S = 6, 160, 19
+    y = ops.to_padded(torch.randn(B, C, S, S, device=cuda_device).clamp_min(0).to(torch.bfloat16), 1, C)
+    w = torch.randn(152, device=cuda_device) * 0.1
+    dl = torch.randn(B, S * S, device=cuda_device) * 0.3
+    sc = torch.tensor([16.0], device=cuda_device)
+    dz = ops.padded_empty(B, S, 1, C, cuda_device)
+    dh1, dh2 = (torch.zeros(B, 153, device=cuda_device) for _ in range(2))
+    ops.head_backward(y, w, dl, dz, dh1, S)
+    ref8 = torch.zeros(dz.shape, dtype=torch.uint8, device=cuda_device)
+    am1, am2 = (ops.fp8_amax_buffer(1, cuda_device)[0] for _ in range(2))
+    ops.quantize_bf8(dz, ref8, sc, am1)
+    got8 = torch.zeros_like(ref8)
+    ops.head_backward(y, w, dl, dz, dh2, S, dz8=got8, dz8_scale=sc, dz8_amax=am2)
+    torch.cuda.synchronize()
+    assert torch.equal(got8, ref8)
+    assert am1.view(torch.float32).max().item() == am2.view(torch.float32).max().item() > 0
+    assert torch.equal(dh1, dh2)
+
+
+def test_value_fp8_head_e5m2_fusion_bitwise(cuda_device):
+    """fp8 value training with the head writing the top dZ as e5m2 (default) equals the trainer that
+    writes bf16 and runs quantize_bf8, bit for bit (weights, gradient scales and maxima)."""
+    import copy
+
+    from alphago_amd.models.nets import ValueNet
+    from alphago_amd.train.engine import HipValueTrainer
+
+    torch.manual_seed(3)
+    B = 64
+    net = ValueNet(49, filters_per_layer=152, layers=4)
+    planes = _planes(B, 49, seed=11).to(cuda_device)
+    z = (torch.randint(0, 2, (B,), device=cuda_device) * 2 - 1).float()
+    a = HipValueTrainer(net, B, lr=0.01, device=cuda_device, precision="fp8")
+    b = HipValueTrainer(copy.deepcopy(net), B, lr=0.01, device=cuda_device, precision="fp8")
+    b._top_e5m2_fusable = lambda: False
+    for _ in range(4):
+        a.step(planes, z)
+        b.step(planes, z)
+    torch.cuda.synchronize()
+    assert a._head_wrote_e5m2 and not b._head_wrote_e5m2
+    assert torch.equal(a.fp.flat, b.fp.flat)
+    assert torch.equal(a.gscales8, b.gscales8) and torch.equal(a.gamax8, b.gamax8)
+
+
 @pytest.mark.gpu
 def test_scalef32_bf8_conversion_semantics(cuda_device):
     """Pins the semantics of v_cvt_scalef32_pk_bf8_bf16 (2 bf16 -> 2 e5m2 with an f32 scale in one
