@@ -140,6 +140,7 @@ struct PackInputArgs {
   const int* target;      // [B] or null
   int* target_out;        // [B] or null
   __bf16* out;            // padded NHWC [B][S+2P][S+2P][Cp]
+  uint8_t* out8;          // the same planes as e4m3 (scale 1: exact for 0/1, saturating at 448) or null
   int B, S, Creal, Cp, P;
 };
 

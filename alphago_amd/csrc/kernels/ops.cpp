@@ -312,8 +312,8 @@ void value_out(const Tensor& h, const Tensor& w2, const Tensor& b2, const c10::o
 
 void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c10::optional<Tensor>& target,
                 const c10::optional<Tensor>& target_out, const Tensor& out, int64_t P,
-                const c10::optional<Tensor>& rows) {
-  check_dev("pack_input", planes, sym, target, target_out, out, rows);
+                const c10::optional<Tensor>& rows, const c10::optional<Tensor>& out8) {
+  check_dev("pack_input", planes, sym, target, target_out, out, rows, out8);
   TORCH_CHECK(planes.scalar_type() == at::kByte && planes.is_contiguous() && planes.dim() == 4, "planes: uint8 (B,C,S,S)");
   CHECK_BF16(out); CHECK_CONTIG(out);
   const int64_t C = planes.size(1), S = planes.size(2);
@@ -326,6 +326,10 @@ void pack_input(const Tensor& planes, const c10::optional<Tensor>& sym, const c1
   agk::PackInputArgs a{};
   a.planes = planes.data_ptr<uint8_t>();
   a.rows = rows.has_value() ? rows->data_ptr<int64_t>() : nullptr;
+  if (out8.has_value())
+    TORCH_CHECK(out8->scalar_type() == at::kByte && out8->sizes() == out.sizes() && out8->is_contiguous(),
+                "pack_input: out8 uint8 of out's shape");
+  a.out8 = out8.has_value() ? out8->data_ptr<uint8_t>() : nullptr;
   a.npool = planes.size(0);
   a.sym = sym.has_value() ? sym->data_ptr<int>() : nullptr;
   a.target = target.has_value() ? target->data_ptr<int>() : nullptr;
@@ -860,7 +864,7 @@ TORCH_LIBRARY(alphago_amd, m) {
       "value_out(Tensor h, Tensor w2, Tensor b2, Tensor? target, Tensor? weight, Tensor(a!) v, Tensor(b!)? loss, "
       "Tensor(c!)? correct, Tensor(d!)? dh, Tensor(e!)? dout, float grad_scale) -> ()");
   m.def("pack_input(Tensor planes, Tensor? sym, Tensor? target, Tensor(a!)? target_out, Tensor(b!) out, int P, "
-        "Tensor? rows=None) -> ()");
+        "Tensor? rows=None, Tensor(c!)? out8=None) -> ()");
   m.def("pack_weights(Tensor[] ws, Tensor(a!)[] wf, Tensor(b!)[] wd) -> ()");
   m.def("sgd_update(Tensor(a!) p, Tensor g, float lr, float gscale) -> ()");
   m.def("comm_proxy(Tensor src, Tensor(a!) dst, int channels, float wire_us) -> ()");

@@ -103,6 +103,7 @@ __global__ __launch_bounds__(256) void pack_input_board_kernel(PackInputArgs a) 
   const int HP = a.S + 2 * a.P;
   const int s = a.sym ? a.sym[b] : 0;
   __bf16* ob = a.out + (size_t)b * HP * HP * a.Cp;
+  uint8_t* ob8 = a.out8 ? a.out8 + (size_t)b * HP * HP * a.Cp : nullptr;
   for (int idx = threadIdx.x; idx < SS * C8; idx += 256) {
     const int c8 = idx % C8;
     const int p = idx / C8;
@@ -116,7 +117,18 @@ __global__ __launch_bounds__(256) void pack_input_board_kernel(PackInputArgs a) 
       const int c = c8 * 8 + e;
       o[e] = (__bf16)(c < a.Creal ? (float)q[c * SS] : 0.f);
     }
-    *(bf16x8*)(ob + ((size_t)(i + a.P) * HP + j + a.P) * a.Cp + c8 * 8) = o;
+    const size_t off = ((size_t)(i + a.P) * HP + j + a.P) * a.Cp + c8 * 8;
+    *(bf16x8*)(ob + off) = o;
+    if (ob8) {  // quantize_fp8_kernel's conversion at scale 1 (the fp8 trunk's input; no second pass)
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fminf(fmaxf((float)o[e], -448.f), 448.f);
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+      *(int2*)(ob8 + off) = make_int2(lo, hi);
+    }
   }
   if (a.target_out && threadIdx.x == 0) {
     const int t = a.target[b];
@@ -132,6 +144,8 @@ __global__ __launch_bounds__(256) void pack_input_board_kernel(PackInputArgs a) 
 
 void launch_pack_input(const PackInputArgs& a, hipStream_t st) {
   const int bytes = a.Creal * a.S * a.S;
+  if (a.out8 && bytes > kPackBoardMaxBytes)
+    throw std::invalid_argument("pack_input: the e4m3 output needs boards of at most 48 KB of planes");
   if (bytes <= kPackBoardMaxBytes) {
     hipLaunchKernelGGL(pack_input_board_kernel, dim3(a.B), dim3(256), bytes, st, a);
     return;

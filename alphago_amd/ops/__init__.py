@@ -294,11 +294,12 @@ def policy_head_probs(y, w, b, probs, S: int, legal=None, temperature: float = 1
     return probs
 
 
-def pack_input(planes_u8, out, P: int, sym=None, target=None, target_out=None, rows=None):
+def pack_input(planes_u8, out, P: int, sym=None, target=None, target_out=None, rows=None, out8=None):
     """uint8 planes -> padded NHWC bf16 with the per-board D4 symmetry ``sym`` (and the target moved
     with it).  ``rows`` (int64, B): board b is ``planes_u8[rows[b]]`` -- the minibatch gather from a
-    resident pool fused into the pack (a row outside the pool packs an all-zero board)."""
-    _ops().pack_input(planes_u8, sym, target, target_out, out, P, rows)
+    resident pool fused into the pack (a row outside the pool packs an all-zero board).  ``out8``
+    (uint8, out's shape): the same values as e4m3 too (``quantize_fp8(out, out8, 0)``'s bytes)."""
+    _ops().pack_input(planes_u8, sym, target, target_out, out, P, rows, out8)
     return out
 
 

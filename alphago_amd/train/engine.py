@@ -535,8 +535,9 @@ class HipConvTrainer:
         return (self.X0, self.P0) if l == 0 else (self.Y[l - 1], 1)
 
     def forward_trunk(self, planes: torch.Tensor, sym=None, move_targets=None, target_out=None) -> None:
+        # fp8 trunk: the pack writes the e4m3 input copy too (was a quantize_fp8 pass over X0)
         ops.pack_input(planes, self.X0, self.P0, sym=sym, target=move_targets, target_out=target_out,
-                       rows=self._rows)
+                       rows=self._rows, out8=self.X08 if self.precision == "fp8" else None)
         if self.precision == "fp8":
             if not self._fp8_calibrated:
                 self._fp8_calibrate()
@@ -562,8 +563,7 @@ class HipConvTrainer:
                          tile=self.conv_tile)
 
     def _forward_fp8(self) -> None:
-        ops.quantize_fp8(self.X0, self.X08, 0)  # binary planes: exact
-        x8, pin = self.X08, self.P0
+        x8, pin = self.X08, self.P0  # e4m3 input written by forward_trunk's pack_input (exact: 0/1 planes)
         # all-fp8 backward (fp8 wgrad + dgrad): below the last layer nothing reads the bf16
         # activations (wgrad reads the e4m3 copies, dgrad the ReLU' bits), so only e4m3 is written
         # (the first, calibrating backward runs bf16 wgrads on these activations)

@@ -346,6 +346,25 @@ def test_pack_input_rows_gather(ops, cuda_device, C, Cp):
     assert torch.equal(got[keep], ref[keep])
 
 
+@pytest.mark.parametrize("C", [48, 49])
+def test_pack_input_e4m3_copy(ops, cuda_device, C):
+    """out8: the pack writes the e4m3 copy the fp8 trunk reads -- quantize_fp8(out, ., 0)'s bytes
+    (plane values 0-255: exact up to 16, saturating at 448), borders untouched."""
+    torch.manual_seed(7)
+    S, B = 19, 5
+    planes = torch.randint(0, 256, (B, C, S, S), dtype=torch.uint8, device=cuda_device)
+    planes[:2] = planes[:2] & 1  # binary boards as in training
+    sym = torch.randint(0, 8, (B,), dtype=torch.int32, device=cuda_device)
+    out = ops.padded_empty(B, S, 2, 64, cuda_device)
+    got8 = torch.zeros(out.shape, dtype=torch.uint8, device=cuda_device)
+    ops.pack_input(planes, out, 2, sym=sym, out8=got8)
+    ref8 = torch.zeros_like(got8)
+    ops.quantize_fp8(out, ref8, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(got8, ref8)
+    assert torch.equal(got8[:2].view(torch.float8_e4m3fn).float(), out[:2].float())  # 0/1 planes: exact
+
+
 def test_sgd_update(ops, cuda_device):
     p = torch.randn(1003, device=cuda_device)
     g = torch.randn(1003, device=cuda_device)
