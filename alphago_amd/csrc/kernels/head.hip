@@ -407,7 +407,9 @@ __global__ __launch_bounds__(NT) void policy_head_kernel(PolicyHeadArgs a) {
   __shared__ float z_s[368];
   __shared__ float red[16];
   __shared__ int redi[16];
-  const int b = blockIdx.x;
+  // boards in reverse: the last-written boards of the final forward are the ones still in the
+  // Infinity Cache, and they are read before this kernel's own dZ writes evict them
+  const int b = (int)gridDim.x - 1 - (int)blockIdx.x;
   const int tid = threadIdx.x;
   const int SS = a.S * a.S;
   const int HP = a.S + 2;
