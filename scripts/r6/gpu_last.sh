@@ -1,6 +1,6 @@
 #!/bin/bash
 # Last check of the shipped tree: GPU suite, smoke(), the driver's bench command.
-O=gpurun_out/r6/last
+O=gpurun_out/r6/last2
 mkdir -p $O
 export PYTHONUNBUFFERED=1
 source scripts/r6/lib.sh
